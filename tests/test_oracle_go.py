@@ -1,0 +1,112 @@
+"""Pin the oracle's graphd restatement against the reference's GoTest expectations
+(src/graph/test/GoTest.cpp; data src/graph/test/TraverseTestBase.h, via tests/golden/nba.json)."""
+from collections import Counter
+
+import pytest
+
+import fixtures as F
+from nebula_amd import expr as X
+
+
+@pytest.fixture(scope="module")
+def nba(oracle):
+    st, vid = F.nba_oracle_store()
+    return st, vid, F.nba()
+
+
+def names(vid, rows):
+    inv = {v: k for k, v in vid.items()}
+    return Counter(tuple(inv.get(c, c) if isinstance(c, int) and c in inv else c for c in r) for r in rows)
+
+
+def expect(data, key):
+    return Counter(tuple(r) for r in data["expect"][key]["rows"])
+
+
+def test_one_step_serve(nba):
+    st, vid, d = nba
+    r = st.go([vid["Tim Duncan"]], 1, F.NBA_SERVE)
+    assert r.code == 0
+    assert names(vid, r.rows()) == expect(d, "one_step_serve_tim")
+
+
+def test_serve_years(nba):
+    st, vid, d = nba
+    ys = [X.AliasProp("serve", "start_year").encode(), X.AliasProp("serve", "end_year").encode(),
+          X.EdgeDst("serve").encode()]
+    r = st.go([vid["Boris Diaw"]], 1, F.NBA_SERVE, yields=ys)
+    assert names(vid, r.rows()) == expect(d, "serve_boris_years")
+
+
+def test_serve_where(nba):
+    st, vid, d = nba
+    w = ((X.AliasProp("serve", "start_year") >= 2013) & (X.AliasProp("serve", "end_year") <= 2018)).encode()
+    ys = [X.AliasProp("serve", "start_year").encode(), X.AliasProp("serve", "end_year").encode(),
+          X.EdgeDst("serve").encode()]
+    r = st.go([vid["Rajon Rondo"]], 1, F.NBA_SERVE, where=w, yields=ys)
+    assert names(vid, r.rows()) == expect(d, "serve_rondo_where")
+
+
+def pipe(st, starts, etypes, distinct_last=False, ylast=()):
+    cur = starts
+    r = None
+    for i, et in enumerate(etypes):
+        last = i == len(etypes) - 1
+        r = st.go(cur, 1, et, yields=ylast if last else (), distinct=distinct_last and last)
+        assert r.code == 0, r.error
+        cur = [row[0] for row in r.rows()]
+    return r
+
+
+def test_pipe_keeps_duplicates(nba):
+    st, vid, d = nba
+    r = pipe(st, [vid["Boris Diaw"]], [F.NBA_LIKE, F.NBA_LIKE, F.NBA_SERVE])
+    assert names(vid, r.rows()) == expect(d, "pipe_boris_like_like_serve")
+
+
+def test_variable_two_hops(nba):
+    st, vid, d = nba
+    r = pipe(st, [vid["Tracy McGrady"]], [F.NBA_LIKE, F.NBA_LIKE])
+    assert names(vid, r.rows()) == expect(d, "var_tracy_like_like")
+    r = pipe(st, [vid["Tracy McGrady"]], [F.NBA_LIKE, F.NBA_LIKE, F.NBA_LIKE])
+    assert names(vid, r.rows()) == expect(d, "var_pipe_tracy")
+
+
+def test_distinct(nba):
+    st, vid, d = nba
+    r = pipe(st, [vid["Boris Diaw"]], [F.NBA_LIKE, F.NBA_LIKE, F.NBA_SERVE], distinct_last=True,
+             ylast=[X.EdgeDst("serve").encode()])
+    assert names(vid, r.rows()) == expect(d, "distinct_boris_serve_dst")
+
+
+def test_vertex_not_exist(nba):
+    st, vid, d = nba
+    nid = d["nonexist_hash"]
+    assert st.go([nid], 1, F.NBA_SERVE).nrows == 0
+    assert pipe(st, [nid], [F.NBA_LIKE, F.NBA_LIKE, F.NBA_SERVE]).nrows == 0
+
+
+def test_go_three_steps_derived(nba):
+    st, vid, d = nba
+    r = st.go([vid["Boris Diaw"]], 3, F.NBA_LIKE)
+    assert names(vid, r.rows()) == expect(d, "derived_go3_boris_like")
+    # the step form dedups the intermediate frontier (P12); the pipe form keeps duplicates (P14)
+    assert pipe(st, [vid["Boris Diaw"]], [F.NBA_LIKE] * 3).nrows == 9
+
+
+def test_relational_type_order(nba):
+    # P8: int vs double compares by variant index -> int < double always; == uses almostEqual
+    st, vid, d = nba
+    w = (X.AliasProp("like", "likeness") > 10.5).encode()
+    assert st.go([vid["Tim Duncan"]], 1, F.NBA_LIKE, where=w).nrows == 0
+    w = (X.AliasProp("like", "likeness") < 10.5).encode()
+    assert st.go([vid["Tim Duncan"]], 1, F.NBA_LIKE, where=w).nrows == 2
+    w = X.AliasProp("like", "likeness").eq(95.0).encode()
+    assert st.go([vid["Tim Duncan"]], 1, F.NBA_LIKE, where=w).nrows == 2
+
+
+def test_where_error_fails_query(nba):
+    st, vid, d = nba
+    w = (X.AliasProp("like", "nope") > 1).encode()
+    r = st.go([vid["Tim Duncan"]], 1, F.NBA_LIKE, where=w)
+    assert r.code != 0

@@ -1,0 +1,134 @@
+"""Pin the oracle's storage restatement against the reference's QueryBoundTest.
+
+Each test restates one TEST in src/storage/test/QueryBoundTest.cpp (line numbers cited) with the
+same fixture and the same expectations, run against oracle/refcpu.cpp.
+"""
+import pytest
+
+import fixtures as F
+import oracle as O
+from nebula_amd import expr as X
+
+E_INVALID_FILTER = -31
+
+
+def check_response(res, vertex_num, edge_fields, dst_from, edge_num, out_bound):
+    """checkResponse (QueryBoundTest.cpp:111-178)."""
+    assert res.failed() == []
+    assert len(res.schema(0)) == edge_fields
+    assert len(res.schema(1)) == 3
+    verts = res.vertices()
+    assert len(verts) == vertex_num
+    rows = res.rows()
+    by_vertex = {}
+    for r, row in enumerate(rows):
+        by_vertex.setdefault(res.row_vertex(r), []).append(row)
+    for vid, tagvals in verts:
+        assert tagvals[0] == vid + 3001
+        assert tagvals[1] == vid + 3003 + 2
+        assert tagvals[2] == "tag_string_col_4"
+        vrows = by_vertex[vid]
+        assert len(vrows) == edge_num
+        for n, row in enumerate(vrows):
+            assert len(row) == edge_fields
+            dst = row[0]
+            assert dst == dst_from + n
+            assert row[1] == 0
+            if out_bound:
+                for i in range(2, 7):
+                    assert row[i] == (i - 2) * 2 + dst
+                for i in range(7, 12):
+                    assert row[i] == f"string_col_{(i - 7 + 5) * 2}_2"
+
+
+@pytest.fixture(scope="module")
+def store(oracle):
+    return F.qb_oracle_store()
+
+
+def test_out_bound_simple(store):  # QueryBoundTest.cpp:181-201
+    parts, vids, cols = F.qb_request()
+    res = store.get_bound(F.EDGE_TYPE, parts, vids, cols, handlers=10, min_per_bucket=3)
+    check_response(res, 30, 12, 10001, 7, True)
+
+
+def test_in_bound_simple(store):  # QueryBoundTest.cpp:204-225
+    parts, vids, cols = F.qb_request(False)
+    res = store.get_bound(-F.EDGE_TYPE, parts, vids, cols, in_bound=True)
+    check_response(res, 30, 2, 20001, 5, False)
+
+
+def test_filter_only_edge(store):  # QueryBoundTest.cpp:227-258
+    parts, vids, cols = F.qb_request()
+    f = X.Relational(X.GE, X.AliasProp("e101", "col_0"), X.Primary(10007)).encode()
+    res = store.get_bound(F.EDGE_TYPE, parts, vids, cols, filt=f)
+    check_response(res, 30, 12, 10007, 1, True)
+
+
+def test_filter_only_tag(store):  # QueryBoundTest.cpp:260-291
+    parts, vids, cols = F.qb_request()
+    f = X.Relational(X.GE, X.SourceProp("3001", "tag_3001_col_0"), X.Primary(20 + 3001)).encode()
+    res = store.get_bound(F.EDGE_TYPE, parts, vids, cols, filt=f)
+    check_response(res, 10, 12, 10001, 7, True)
+
+
+def test_filter_tag_and_edge(store):  # QueryBoundTest.cpp:345-385
+    parts, vids, cols = F.qb_request()
+    left = X.Relational(X.GE, X.SourceProp("3001", "tag_3001_col_0"), X.Primary(20 + 3001))
+    right = X.Relational(X.GE, X.AliasProp("e101", "col_0"), X.Primary(10007))
+    f = X.Logical(X.AND, left, right).encode()
+    res = store.get_bound(F.EDGE_TYPE, parts, vids, cols, filt=f)
+    check_response(res, 10, 12, 10007, 1, True)
+
+
+def test_filter_invalid(store):  # QueryBoundTest.cpp:387-416
+    parts, vids, cols = F.qb_request()
+    f = X.InputProp("tag_3001_col_0").encode()
+    res = store.get_bound(F.EDGE_TYPE, parts, vids, cols, filt=f)
+    failed = res.failed()
+    assert len(failed) == 3
+    assert failed[0][1] == E_INVALID_FILTER
+
+
+@pytest.mark.parametrize("handlers,minper,expect", [
+    (10, 3, [3] * 10),                 # QueryBoundTest.cpp:294-303
+    (9, 3, [4, 4, 4] + [3] * 6),       # :304-316
+    (40, 4, [5, 5] + [4] * 5),         # :317-330
+    (40, 40, [30]),                    # :331-342
+])
+def test_gen_buckets(oracle, handlers, minper, expect):
+    import ctypes as C
+    import numpy as np
+    parts, vids, _ = F.qb_request(False)
+    p = np.asarray(parts, dtype=np.int32)
+    v = np.asarray(vids, dtype=np.int64)
+    out = np.zeros(64, dtype=np.int32)
+    n = O.lib().ora_gen_buckets(p.ctypes.data_as(C.c_void_p), v.ctypes.data_as(C.c_void_p), len(v),
+                                handlers, minper, out.ctypes.data_as(C.c_void_p))
+    assert list(out[:n]) == expect
+
+
+def test_row_writer_offsets_bytes(oracle):
+    # RowWriterTest offsetsCreation (src/dataman/test/RowWriterTest.cpp:128-141): 33 ints give
+    # block offsets 16 and 32; with 1-byte varints the encoded row is header 0x00, the two
+    # 1-byte offsets, then the 33 values.
+    enc = O.encode_row(list(range(33)))
+    assert enc == bytes([0x00, 16, 32]) + bytes(range(33))
+
+
+def test_row_writer_header_and_types(oracle):
+    # RowWriter.cpp:49-75: header low 3 bits = offset bytes - 1, no version for schemaless rows;
+    # INT = LEB128 varint (negative int64 -> 10 bytes), DOUBLE = 8 LE bytes, BOOL = 1 byte,
+    # STRING = varint length + bytes.
+    import struct
+    enc = O.encode_row([True, 10, "Hello World!", 3.1415926])
+    assert enc == b"\x00\x01\x0a\x0cHello World!" + struct.pack("<d", 3.1415926)
+    assert O.encode_row([-1])[1:] == b"\xff" * 9 + b"\x01"
+    assert O.encode_varint(300) == b"\xac\x02"
+
+
+def test_edge_key_layout(oracle):
+    # NebulaKeyUtils.cpp:24-39: part(4) src(8) type(4) rank(8) dst(8) ver(8), native LE
+    import struct
+    k = O.edge_key(7, 123456789, 101, 5, -3, 2**31 - 1)
+    assert k == struct.pack("<iqiqqq", 7, 123456789, 101, 5, -3, 2**31 - 1)
