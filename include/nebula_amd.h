@@ -1,0 +1,201 @@
+/*
+ * nebula_amd.h -- C ABI of the MI355X neighbour-expansion engine.
+ *
+ * This is the drop-in boundary for the reference's getBound / GO hot path (Nebula Graph
+ * v1.0.0-beta).  Every entry point is plain C (pointers + sizes, no C++/torch types), so a
+ * storaged/graphd built from the reference can bind it directly (see INTEGRATION.md for the
+ * C++ operator shapes that wrap it).  Each function names the reference interface it replaces.
+ *
+ * Error convention: functions return 0 on success or a negative code.  Codes -1..-100 are the
+ * reference's storage::cpp2::ErrorCode values (src/interface/storage.thrift:13-35); codes
+ * <= -1000 are engine errors.  nbg_last_error() gives the message for the calling context.
+ * All calls on one context are serialised internally (the reference's processors may call
+ * from many RPC worker threads: QueryBaseProcessor.inl:407-423).
+ */
+#ifndef NEBULA_AMD_H_
+#define NEBULA_AMD_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes (storage.thrift:13-35 + engine range) -------------------------------- */
+#define NBG_OK 0
+#define NBG_E_LEADER_CHANGED (-11)
+#define NBG_E_SPACE_NOT_FOUND (-13)
+#define NBG_E_PART_NOT_FOUND (-14)
+#define NBG_E_EDGE_PROP_NOT_FOUND (-21)
+#define NBG_E_TAG_PROP_NOT_FOUND (-22)
+#define NBG_E_IMPROPER_DATA_TYPE (-23)
+#define NBG_E_INVALID_FILTER (-31)
+#define NBG_E_UNKNOWN (-100)
+#define NBG_E_DEVICE (-1000)      /* HIP runtime / kernel failure                          */
+#define NBG_E_INVALID_ARG (-1001) /* bad argument (null pointer, unknown edge type, ...)   */
+#define NBG_E_STATE (-1002)       /* call out of order (query before snapshot finalize)   */
+#define NBG_E_UNSUPPORTED (-1003) /* expression / column shape the engine does not run    */
+#define NBG_E_EVAL (-1004)        /* expression evaluation error at the final GO step
+                                     (GoExecutor.cpp:754-758 fails the whole query)       */
+#define NBG_E_COMM (-1005)        /* RCCL failure                                          */
+#define NBG_E_NOMEM (-1006)       /* device allocation failed                              */
+
+/* cpp2::SupportedType values (src/interface/common.thrift:30-46) */
+#define NBG_T_BOOL 1
+#define NBG_T_INT 2
+#define NBG_T_VID 3
+#define NBG_T_FLOAT 4
+#define NBG_T_DOUBLE 5
+#define NBG_T_STRING 6
+#define NBG_T_TIMESTAMP 21
+
+/* cpp2::PropOwner (storage.thrift:37-41) */
+#define NBG_OWNER_SOURCE 1
+#define NBG_OWNER_DEST 2
+#define NBG_OWNER_EDGE 3
+
+typedef struct nbg_ctx nbg_ctx;
+
+/* ---- context ------------------------------------------------------------------------------
+ * One context = one space on one GPU (one rank of `world_size`).  Replaces the storaged's
+ * KVStore* + SchemaManager* pair handed to QueryBoundProcessor::instance
+ * (src/storage/QueryBoundProcessor.h:23-28) and graphd's StorageClient for that space.
+ * num_parts: the space's partition count (CreateSpaceProcessor.cpp:10-11); a vid lives in part
+ * (uint64)vid % num_parts + 1 (StorageClient.cpp:10-11) and part p on rank p % world_size
+ * (pickHosts, CreateSpaceProcessor.cpp:77-90).                                              */
+nbg_ctx* nbg_ctx_create(int32_t device, int32_t num_parts, int32_t rank, int32_t world_size);
+void nbg_ctx_destroy(nbg_ctx* ctx);
+const char* nbg_last_error(const nbg_ctx* ctx);
+
+/* Multi-GPU: RCCL communicator over xGMI.  Rank 0 calls nbg_comm_unique_id and the launcher
+ * broadcasts the 128 bytes (e.g. via torch.distributed's store); every rank then calls
+ * nbg_comm_init.  Replaces StorageClient::collectResponse's RPC scatter/gather
+ * (src/storage/client/StorageClient.inl:74-159) with a per-step all-to-all.                 */
+int32_t nbg_comm_unique_id(uint8_t out[128]);
+int32_t nbg_comm_init(nbg_ctx* ctx, const uint8_t unique_id[128]);
+
+/* pure arithmetic helpers (host, no GPU needed) */
+int32_t nbg_part_of(int64_t vid, int32_t num_parts);          /* StorageClient.cpp:238-243 */
+int32_t nbg_rank_of_part(int32_t part, int32_t world_size);   /* CreateSpaceProcessor.cpp:77-90 */
+
+/* ---- schema (meta SchemaManager::getEdgeSchema, src/meta/SchemaManager.h:38) ------------ */
+int32_t nbg_schema_set_edge(nbg_ctx* ctx, int32_t edge_type, int32_t schema_ver,
+                            int32_t nfields, const char* const* names, const int32_t* types);
+
+/* ---- snapshot builder --------------------------------------------------------------------
+ * Consumes a partition's KV pairs in the reference byte layout (NebulaKeyUtils.h:14-21 keys,
+ * dataman RowWriter rows) -- what RocksEngine::prefix iterates (RocksEngine.cpp:191-200) --
+ * and builds the GPU-resident CSR + SoA property columns.  Keys/values are concatenated blobs
+ * with n+1 offsets.  Vertex keys and other edge types are ignored.  Call once per part (any
+ * order), then nbg_snapshot_finalize.                                                       */
+int32_t nbg_snapshot_load_part(nbg_ctx* ctx, int32_t part, const uint8_t* key_bytes,
+                               const uint64_t* key_offsets, const uint8_t* val_bytes,
+                               const uint64_t* val_offsets, size_t n);
+/* Synthetic RMAT graph generated on the device (definition in DESIGN.md): the KV the
+ * reference's INSERT EDGE path would write (out-edge + empty in-edge, rank 0, one version),
+ * produced directly in the decoded-tuple stage of the same builder.                        */
+int32_t nbg_snapshot_gen_rmat(nbg_ctx* ctx, int32_t scale, int32_t edge_factor, uint64_t seed,
+                              int32_t edge_type);
+int32_t nbg_snapshot_finalize(nbg_ctx* ctx);
+
+typedef struct {
+  int64_t num_vertices;     /* global vertex count (vertices appearing in any edge)          */
+  int64_t local_vertices;   /* vertices owned by this rank                                    */
+  int64_t local_out_edges;  /* out-edges (after version / multi-edge collapse) on this rank   */
+  int64_t local_in_edges;
+  int64_t device_bytes;     /* HBM held by the snapshot on this rank                          */
+  double build_seconds;
+} nbg_snapshot_info;
+int32_t nbg_snapshot_info_get(nbg_ctx* ctx, int32_t edge_type, nbg_snapshot_info* out);
+/* CSR export for tests: out-degree of vid (-1 if unknown) */
+int64_t nbg_snapshot_out_degree(nbg_ctx* ctx, int32_t edge_type, int64_t vid);
+
+/* ---- result rows ------------------------------------------------------------------------
+ * Column-major, typed.  col_types: NBG_T_VID (int64; every integer of a GO result is a VID,
+ * GoExecutor.cpp:596-600), NBG_T_INT (int64, storage rows), NBG_T_DOUBLE, NBG_T_BOOL (1 byte),
+ * NBG_T_STRING (int64 offsets n+1 + bytes).  Memory is owned by the engine until
+ * nbg_rows_free.  `on_device` = 1: column pointers are device pointers.                    */
+typedef struct {
+  int64_t n_rows;
+  int32_t n_cols;
+  int32_t on_device;
+  int32_t* col_types;
+  void** cols;            /* per column: int64_t* / double* / uint8_t* / uint8_t* bytes    */
+  int64_t** str_offsets;  /* per column: n_rows+1 offsets for STRING columns, else NULL     */
+  int64_t* row_vertex;    /* get_bound: vid of the vertex a row belongs to (else NULL)      */
+  /* get_bound response parts (QueryResponse, storage.thrift:207-228) */
+  int64_t n_vertices;     /* vertices returned (only those with >= 1 edge row, QBP.cpp:61-67) */
+  int64_t* vertex_ids;
+  int64_t* vertex_row_offsets; /* n_vertices+1 */
+  int32_t n_failed;       /* ResultCode list (BaseProcessor.h:64-71) */
+  int32_t* failed_parts;
+  int32_t* failed_codes;
+  uint64_t edges_scanned; /* adjacency entries read (TEPS numerator)            */
+  void* _impl;
+} nbg_rows;
+void nbg_rows_free(nbg_rows* rows);
+
+/* ---- getBound ------------------------------------------------------------------------------
+ * Replaces QueryBoundProcessor::process(GetNeighborsRequest) for OUT_BOUND / IN_BOUND
+ * (src/storage/QueryBaseProcessor.inl:462-505, QueryBoundProcessor.cpp:16-106).
+ * parts/vids: the request's parts map flattened (pair i = (parts[i], vids[i])).
+ * edge_type < 0: in-bound scan (StorageClient.cpp:118).  filter: Expression::encode bytes or
+ * empty.  Return columns are EDGE-owned props (key props _src/_dst/_rank/_type or schema props);
+ * SOURCE/DEST tag props return NBG_E_UNSUPPORTED in this version.  Request-level errors are
+ * reported per part in failed_codes (QueryBaseProcessor.inl:470-477), not as the return.    */
+typedef struct {
+  const char* name;
+  int32_t owner;
+  int32_t tag_id;
+} nbg_prop_def;
+int32_t nbg_get_bound(nbg_ctx* ctx, int32_t edge_type, const int32_t* parts,
+                      const int64_t* vids, size_t n, const uint8_t* filter, size_t filter_len,
+                      const nbg_prop_def* cols, size_t ncols, nbg_rows* out);
+
+/* ---- GO N STEPS ---------------------------------------------------------------------------
+ * Replaces GoExecutor's stepOut -> getNeighbors -> onStepOutResponse -> getDstIdsFromResp loop
+ * and its final processFinalResult / setupInterimResult (src/graph/GoExecutor.cpp:80-106,
+ * 334-431, 585-782) with one device-resident call.  starts: literal or piped vids (duplicates
+ * kept unless distinct, GoExecutor.cpp:98-104).  where/yields: Expression::encode bytes as the
+ * graphd AST would encode them.  n_yields = 0 means the default YIELD e._dst AS id.
+ * With world_size > 1 every rank passes the same spec; rows come back sharded by owner.     */
+typedef struct {
+  int32_t edge_type;
+  int32_t steps;
+  const int64_t* starts;
+  size_t n_starts;
+  const uint8_t* where;
+  size_t where_len;
+  const uint8_t* const* yields;
+  const size_t* yield_lens;
+  size_t n_yields;
+  int32_t distinct;
+  int32_t keep_on_device; /* 1: leave result columns in HBM (bench / chained queries)        */
+} nbg_go_spec;
+int32_t nbg_go(nbg_ctx* ctx, const nbg_go_spec* spec, nbg_rows* out);
+
+/* ---- FIND SHORTEST PATH (no reference implementation: FindExecutor.cpp:20-22) ------------
+ * Batched bidirectional BFS over edge_type out-edges / -edge_type in-edges.  out rows:
+ * [src, dst, hops] per pair (hops = -1 if unreachable within max_steps) plus the path
+ * (lexicographically smallest vid sequence among shortest paths) in a STRING-free form:
+ * path vids flattened in cols[3] with per-row offsets in vertex_row_offsets.                */
+int32_t nbg_shortest_path(nbg_ctx* ctx, int32_t edge_type, const int64_t* src,
+                          const int64_t* dst, size_t npairs, int32_t max_steps, nbg_rows* out);
+
+/* ---- timing of the last call (HIP events on the engine stream) --------------------------- */
+typedef struct {
+  double total_ms;        /* device time of the last nbg_go / nbg_get_bound                  */
+  double expand_ms;       /* summed time of the expansion kernels                            */
+  int64_t expand_launches;
+  uint64_t edges_scanned;
+  uint64_t expand_bytes;  /* algorithmic bytes of the expansion kernels          */
+  int32_t steps_run;
+} nbg_timing;
+int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out);
+int32_t nbg_set_option(nbg_ctx* ctx, const char* key, int64_t value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NEBULA_AMD_H_ */

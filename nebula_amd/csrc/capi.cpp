@@ -1,0 +1,227 @@
+// capi.cpp -- extern "C" entry points declared in include/nebula_amd.h.
+#include <cstring>
+
+#include "engine.h"
+
+namespace nbg {
+int32_t comm_unique_id(uint8_t out[128]);
+void comm_init(Ctx& c, const uint8_t id[128]);
+void free_rows_impl(void* impl);
+}  // namespace nbg
+
+using nbg::Ctx;
+using nbg::Error;
+
+struct nbg_ctx {
+  Ctx c;
+};
+
+template <typename F>
+static int32_t guarded(nbg_ctx* ctx, F f) {
+  if (!ctx) return NBG_E_INVALID_ARG;
+  std::lock_guard<std::mutex> lg(ctx->c.mu);
+  try {
+    (void)hipSetDevice(ctx->c.device);
+    int32_t rc = f(ctx->c);
+    if (rc == NBG_OK) ctx->c.last_error.clear();
+    return rc;
+  } catch (const Error& e) {
+    ctx->c.last_error = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    ctx->c.last_error = e.what();
+    return NBG_E_UNKNOWN;
+  }
+}
+
+extern "C" {
+
+nbg_ctx* nbg_ctx_create(int32_t device, int32_t num_parts, int32_t rank, int32_t world_size) {
+  if (num_parts <= 0 || world_size <= 0 || rank < 0 || rank >= world_size) return nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  auto* ctx = new nbg_ctx();
+  ctx->c.device = device;
+  ctx->c.num_parts = num_parts;
+  ctx->c.rank = rank;
+  ctx->c.world = world_size;
+  if (hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return nullptr;
+  }
+  for (auto& e : ctx->c.ev) (void)hipEventCreate(&e);
+  return ctx;
+}
+
+void nbg_ctx_destroy(nbg_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->c.device);
+  (void)hipStreamSynchronize(ctx->c.stream);
+  nbg::comm_destroy(ctx->c);
+  for (auto& e : ctx->c.ev) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(ctx->c.stream);
+  delete ctx;
+}
+
+const char* nbg_last_error(const nbg_ctx* ctx) { return ctx ? ctx->c.last_error.c_str() : "null context"; }
+
+int32_t nbg_comm_unique_id(uint8_t out[128]) { return nbg::comm_unique_id(out); }
+
+int32_t nbg_comm_init(nbg_ctx* ctx, const uint8_t unique_id[128]) {
+  return guarded(ctx, [&](Ctx& c) {
+    nbg::comm_init(c, unique_id);
+    return NBG_OK;
+  });
+}
+
+int32_t nbg_part_of(int64_t vid, int32_t num_parts) {
+  return num_parts > 0 ? nbg::part_of_vid(vid, num_parts) : NBG_E_INVALID_ARG;
+}
+int32_t nbg_rank_of_part(int32_t part, int32_t world_size) {
+  return world_size > 0 ? nbg::owner_of_part(part, world_size) : NBG_E_INVALID_ARG;
+}
+
+int32_t nbg_schema_set_edge(nbg_ctx* ctx, int32_t edge_type, int32_t schema_ver, int32_t nfields,
+                            const char* const* names, const int32_t* types) {
+  return guarded(ctx, [&](Ctx& c) {
+    if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
+    if (edge_type <= 0) throw Error(NBG_E_INVALID_ARG, "edge type must be > 0");
+    if (nfields < 0 || (nfields > 0 && (!names || !types))) throw Error(NBG_E_INVALID_ARG, "bad fields");
+    nbg::EdgeSpace& es = c.edges[edge_type];
+    if (es.out_stage.n || es.in_stage.n) throw Error(NBG_E_STATE, "schema changed after data was loaded");
+    es.type = edge_type;
+    es.schema_ver = schema_ver;
+    es.fields.clear();
+    for (int32_t i = 0; i < nfields; i++) {
+      int32_t t = types[i];
+      if (t != NBG_T_BOOL && t != NBG_T_INT && t != NBG_T_VID && t != NBG_T_FLOAT && t != NBG_T_DOUBLE &&
+          t != NBG_T_STRING && t != NBG_T_TIMESTAMP)
+        throw Error(NBG_E_UNSUPPORTED, "unsupported field type");
+      es.fields.push_back(nbg::Field{names[i] ? names[i] : "", t});
+    }
+    return NBG_OK;
+  });
+}
+
+int32_t nbg_snapshot_load_part(nbg_ctx* ctx, int32_t part, const uint8_t* key_bytes, const uint64_t* key_offsets,
+                               const uint8_t* val_bytes, const uint64_t* val_offsets, size_t n) {
+  return guarded(ctx, [&](Ctx& c) {
+    if (n && (!key_bytes || !key_offsets || !val_offsets)) throw Error(NBG_E_INVALID_ARG, "null KV arrays");
+    nbg::snapshot_load_part(c, part, key_bytes, key_offsets, val_bytes, val_offsets, n);
+    return NBG_OK;
+  });
+}
+
+int32_t nbg_snapshot_gen_rmat(nbg_ctx* ctx, int32_t scale, int32_t edge_factor, uint64_t seed, int32_t edge_type) {
+  return guarded(ctx, [&](Ctx& c) {
+    nbg::snapshot_gen_rmat(c, scale, edge_factor, seed, edge_type);
+    return NBG_OK;
+  });
+}
+
+int32_t nbg_snapshot_finalize(nbg_ctx* ctx) {
+  return guarded(ctx, [&](Ctx& c) {
+    nbg::snapshot_finalize(c);
+    return NBG_OK;
+  });
+}
+
+int32_t nbg_snapshot_info_get(nbg_ctx* ctx, int32_t edge_type, nbg_snapshot_info* out) {
+  return guarded(ctx, [&](Ctx& c) {
+    if (!out) throw Error(NBG_E_INVALID_ARG, "null out");
+    auto it = c.edges.find(edge_type);
+    if (it == c.edges.end()) throw Error(NBG_E_INVALID_ARG, "unknown edge type");
+    out->num_vertices = c.n_global;
+    out->local_vertices = c.owned_hi() - c.owned_lo();
+    out->local_out_edges = it->second.out.nnz;
+    out->local_in_edges = it->second.in.nnz;
+    out->device_bytes = int64_t(it->second.out.bytes() + it->second.in.bytes() + c.vid_of.bytes + c.ht_keys.bytes +
+                                c.ht_vals.bytes);
+    out->build_seconds = c.build_seconds;
+    return NBG_OK;
+  });
+}
+
+int64_t nbg_snapshot_out_degree(nbg_ctx* ctx, int32_t edge_type, int64_t vid) {
+  int64_t result = -1;
+  int32_t rc = guarded(ctx, [&](Ctx& c) {
+    if (!c.finalized) throw Error(NBG_E_STATE, "not finalized");
+    auto it = c.edges.find(edge_type < 0 ? -edge_type : edge_type);
+    if (it == c.edges.end()) throw Error(NBG_E_INVALID_ARG, "unknown edge type");
+    const nbg::Csr& csr = edge_type < 0 ? it->second.in : it->second.out;
+    nbg::DevBuf dv, dg;
+    dv.alloc(8);
+    dg.alloc(4);
+    NBG_HIP(hipMemcpyAsync(dv.p, &vid, 8, hipMemcpyHostToDevice, c.stream));
+    nbg::lookup_gidx(c, dv.as<int64_t>(), dg.as<int32_t>(), 1);
+    int32_t g = -1;
+    NBG_HIP(hipMemcpyAsync(&g, dg.p, 4, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    if (g < c.owned_lo() || g >= c.owned_hi()) return NBG_OK;
+    int64_t rp[2];
+    NBG_HIP(hipMemcpy(rp, csr.row_ptr.as<int64_t>() + (g - c.owned_lo()), 16, hipMemcpyDeviceToHost));
+    result = rp[1] - rp[0];
+    return NBG_OK;
+  });
+  return rc == NBG_OK ? result : rc;
+}
+
+void nbg_rows_free(nbg_rows* rows) {
+  if (!rows) return;
+  if (rows->_impl) nbg::free_rows_impl(rows->_impl);
+  memset(rows, 0, sizeof(*rows));
+}
+
+int32_t nbg_get_bound(nbg_ctx* ctx, int32_t edge_type, const int32_t* parts, const int64_t* vids, size_t n,
+                      const uint8_t* filter, size_t filter_len, const nbg_prop_def* cols, size_t ncols,
+                      nbg_rows* out) {
+  return guarded(ctx, [&](Ctx& c) {
+    if (!out || (n && (!parts || !vids)) || (ncols && !cols) || (filter_len && !filter))
+      throw Error(NBG_E_INVALID_ARG, "bad arguments");
+    memset(out, 0, sizeof(*out));
+    return nbg::get_bound_run(c, edge_type, parts, vids, n, filter, filter_len, cols, ncols, out);
+  });
+}
+
+int32_t nbg_go(nbg_ctx* ctx, const nbg_go_spec* spec, nbg_rows* out) {
+  return guarded(ctx, [&](Ctx& c) {
+    if (!spec || !out || (spec->n_starts && !spec->starts) || (spec->where_len && !spec->where) ||
+        (spec->n_yields && (!spec->yields || !spec->yield_lens)))
+      throw Error(NBG_E_INVALID_ARG, "bad arguments");
+    memset(out, 0, sizeof(*out));
+    return nbg::go_run(c, *spec, out);
+  });
+}
+
+int32_t nbg_shortest_path(nbg_ctx* ctx, int32_t edge_type, const int64_t* src, const int64_t* dst, size_t npairs,
+                          int32_t max_steps, nbg_rows* out) {
+  return guarded(ctx, [&](Ctx& c) {
+    if (!out || (npairs && (!src || !dst))) throw Error(NBG_E_INVALID_ARG, "bad arguments");
+    memset(out, 0, sizeof(*out));
+    return nbg::shortest_path_run(c, edge_type, src, dst, npairs, max_steps, out);
+  });
+}
+
+int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out) {
+  return guarded(ctx, [&](Ctx& c) {
+    if (!out) throw Error(NBG_E_INVALID_ARG, "null out");
+    out->total_ms = c.timing.total_ms;
+    out->expand_ms = c.timing.expand_ms;
+    out->expand_launches = c.timing.expand_launches;
+    out->edges_scanned = c.timing.edges_scanned;
+    out->expand_bytes = c.timing.expand_bytes;
+    out->steps_run = c.timing.steps_run;
+    return NBG_OK;
+  });
+}
+
+int32_t nbg_set_option(nbg_ctx* ctx, const char* key, int64_t value) {
+  return guarded(ctx, [&](Ctx& c) {
+    if (!key) throw Error(NBG_E_INVALID_ARG, "null key");
+    c.options[key] = value;
+    return NBG_OK;
+  });
+}
+
+}  // extern "C"

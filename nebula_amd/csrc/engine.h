@@ -1,0 +1,217 @@
+// engine.h -- internal types of the MI355X neighbour-expansion engine.
+//
+// Layout in HBM (per context = one space on one GPU, rank r of G):
+//   vertex map   vid_of[n_global] int64 (replicated), vid->gidx open-addressing hash table,
+//                owner ranges base[G+1]: gidx in [base[r], base[r+1]) are owned by rank r.
+//   per edge type t:
+//     out CSR    row_ptr[n_local+1] int64, col[nnz] int32 (global dst index), rank[nnz] int64
+//                (absent when every rank is 0), SoA prop columns (INT narrowed to 1/2/4/8 B).
+//     in  CSR    same shape for the -t in-edges (no props), used by FIND SHORTEST PATH.
+//   Rows inside a CSR row follow the reference's bytewise key order (rank, dst LE bytes),
+//   i.e. the order RocksEngine::prefix iterates (RocksEngine.cpp:191-200).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/nebula_amd.h"
+
+namespace nbg {
+
+struct Error : std::runtime_error {
+  int32_t code;
+  Error(int32_t c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define NBG_HIP(x)                                                                        \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess)                                                                 \
+      throw ::nbg::Error(NBG_E_DEVICE, std::string(#x) + ": " + hipGetErrorString(e_));   \
+  } while (0)
+
+// Device buffer (RAII).  Never resized inside a launch sequence that a caller may capture.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      p = o.p;
+      bytes = o.bytes;
+      o.p = nullptr;
+      o.bytes = 0;
+    }
+    return *this;
+  }
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  void alloc(size_t b) {
+    release();
+    if (b == 0) return;
+    hipError_t e = hipMalloc(&p, b);
+    if (e != hipSuccess) {
+      p = nullptr;
+      throw Error(NBG_E_NOMEM, "hipMalloc(" + std::to_string(b) + ") failed: " + hipGetErrorString(e));
+    }
+    bytes = b;
+  }
+  void ensure(size_t b) {  // grow-only workspace
+    if (b > bytes) alloc(b + b / 4);
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+struct Field {
+  std::string name;
+  int32_t type;
+};
+
+// One property column of a CSR (SoA).  INT columns are stored at the narrowest width that
+// holds [minv, maxv]; reads sign-extend back to int64, so values are bit-identical.
+struct PropCol {
+  std::string name;
+  int32_t type = 0;    // NBG_T_*
+  int32_t width = 8;   // bytes per element in `data`
+  DevBuf data;
+  DevBuf present;      // uint8 per edge; empty = all present
+  DevBuf str_off;      // int64 [nnz+1] for STRING
+  DevBuf str_bytes;
+  int64_t minv = 0, maxv = 0;
+};
+
+struct Csr {
+  int64_t n_rows = 0;
+  int64_t nnz = 0;
+  DevBuf row_ptr;   // int64 [n_rows+1]
+  DevBuf col;       // int32 [nnz] global vertex index of the other end
+  DevBuf rank;      // int64 [nnz] or empty (all zero)
+  DevBuf row_part;  // int32 [n_rows]: the part holding the row's keys
+  DevBuf row_ok;    // uint8 [n_rows] row_part == hash part; empty when all rows follow the rule
+  std::vector<PropCol> props;
+  size_t bytes() const {
+    size_t b = row_ptr.bytes + col.bytes + rank.bytes + row_part.bytes + row_ok.bytes;
+    for (auto& p : props) b += p.data.bytes + p.present.bytes + p.str_off.bytes + p.str_bytes.bytes;
+    return b;
+  }
+};
+
+// Decoded edge tuples (the KV decode stage output, before CSR build).
+struct Staging {
+  int64_t n = 0;
+  DevBuf src, dst, rank, ver;          // int64 each; rank/ver may stay empty (constant)
+  DevBuf part;                         // int32 part of the key (empty: hash rule)
+  bool rank_const = true, ver_const = true;
+  int64_t rank_value = 0, ver_value = 0;
+  std::vector<DevBuf> props;           // int64 bits per field (double bits for DOUBLE/FLOAT)
+  std::vector<DevBuf> present;         // uint8 per field (empty = all present)
+  std::vector<DevBuf> str_len;         // STRING: int64 length; `props` holds heap offsets
+  size_t cap = 0;
+};
+
+struct EdgeSpace {
+  int32_t type = 0;
+  int32_t schema_ver = 0;
+  std::vector<Field> fields;
+  Staging out_stage, in_stage;
+  Csr out, in;
+};
+
+struct Timing {
+  double total_ms = 0, expand_ms = 0;
+  int64_t expand_launches = 0;
+  uint64_t edges_scanned = 0, expand_bytes = 0;
+  int32_t steps_run = 0;
+};
+
+struct Ctx {
+  int32_t device = 0, num_parts = 1, rank = 0, world = 1;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string last_error;
+  void* comm = nullptr;  // ncclComm_t
+
+  // vertex map
+  bool finalized = false;
+  int64_t n_global = 0;
+  std::vector<int64_t> base;     // G+1
+  DevBuf vid_of;                 // int64 [n_global]
+  DevBuf ht_keys, ht_vals;       // int64 / int32 [ht_cap]
+  int64_t ht_cap = 0;
+  bool ht_has_min = false;       // INT64_MIN vid present (the empty-slot sentinel)
+  int32_t ht_min_gidx = -1;
+  DevBuf heap;                   // device copy of all loaded value blobs (STRING props)
+  size_t heap_used = 0;
+  std::map<int32_t, EdgeSpace> edges;
+  double build_seconds = 0;
+
+  // workspaces for queries
+  DevBuf ws_map;       // uint8 [n_global] visited / next-set bytemap
+  DevBuf ws_map2;
+  DevBuf ws_front[2];  // int32 frontier lists
+  DevBuf ws_off;       // int64 [n+1] degree scan
+  DevBuf ws_tmp;       // scan temp
+  DevBuf ws_rows;      // final rows (int32 src idx, int64 edge)
+  DevBuf ws_counters;  // small device counters
+  DevBuf ws_bits_send, ws_bits_recv;
+  DevBuf ws_starts;
+  Timing timing;
+  hipEvent_t ev[8] = {};
+  std::map<std::string, int64_t> options;
+
+  int64_t owned_lo() const { return base.empty() ? 0 : base[size_t(rank)]; }
+  int64_t owned_hi() const { return base.empty() ? n_global : base[size_t(rank) + 1]; }
+  int64_t opt(const std::string& k, int64_t d) const {
+    auto it = options.find(k);
+    return it == options.end() ? d : it->second;
+  }
+};
+
+// ---- helpers implemented in the .hip files -------------------------------------------------
+// snapshot.hip
+void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t* koff,
+                        const uint8_t* vb, const uint64_t* voff, size_t n);
+void snapshot_gen_rmat(Ctx& c, int32_t scale, int32_t ef, uint64_t seed, int32_t et);
+void snapshot_finalize(Ctx& c);
+void lookup_gidx(Ctx& c, const int64_t* d_vids, int32_t* d_gidx, int64_t n);
+// traverse.hip
+int32_t go_run(Ctx& c, const nbg_go_spec& spec, nbg_rows* out);
+int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* vids, size_t n,
+                      const uint8_t* filter, size_t flen, const nbg_prop_def* cols, size_t ncols,
+                      nbg_rows* out);
+int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t* dst, size_t n,
+                          int32_t max_steps, nbg_rows* out);
+// comm.cpp
+void comm_alltoallv_bytes(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off,
+                          void* recv, const size_t* recv_bytes, const size_t* recv_off);
+void comm_allgather_bytes(Ctx& c, const void* send, size_t bytes_each, void* recv);
+void comm_allreduce_sum_i64(Ctx& c, int64_t* d_vals, size_t n);
+void comm_destroy(Ctx& c);
+
+inline double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+inline int owner_of_part(int32_t part, int32_t world) { return int(part % world); }
+inline int32_t part_of_vid(int64_t vid, int32_t parts) {
+  return int32_t(uint64_t(vid) % uint64_t(parts) + 1);
+}
+
+}  // namespace nbg

@@ -1,0 +1,1044 @@
+// snapshot.hip -- snapshot builder: reference KV bytes (or synthetic RMAT tuples) -> GPU CSR.
+//
+// Stage 1 (decode, per loaded part): one thread per KV pair parses the 40-byte edge key
+//   (NebulaKeyUtils.h:14-21: part i32 | src i64 | type i32 | rank i64 | dst i64 | ver i64, LE)
+//   and, for out-edges, the RowWriter row (RowWriter.cpp:49-75: header byte, schema version,
+//   block offsets every 16 fields, INT = LEB128 varint, VID/TIMESTAMP 8 B, DOUBLE 8 B, FLOAT
+//   4 B, BOOL 1 B, STRING varint length + bytes).  Field offsets follow RowReader::skipToField
+//   (RowReader.cpp:276-368), including the stored block offsets.  Output: SoA tuples.
+// Stage 2 (finalize): vertex set, vid<->gidx map, sort each rank's tuples into the reference's
+//   key order, keep the bytewise-first version of every (src, rank, dst)
+//   (QueryBaseProcessor.inl:349-362, P3), emit CSR + narrowed SoA property columns.
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_reduce.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
+#include <algorithm>
+#include <numeric>
+
+#include "device_common.h"
+#include "engine.h"
+
+namespace nbg {
+
+constexpr int kMaxFields = 64;
+struct SchemaDev {
+  int32_t nfields;
+  int32_t types[kMaxFields];
+};
+
+// ------------------------------------------------------------------------------------------
+// small generic kernels
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void k_fill(T* p, T v, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    p[i] = v;
+}
+__global__ void k_iota_u32(uint32_t* p, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    p[i] = uint32_t(i);
+}
+static int grid_for(int64_t n, int block = 256) {
+  int64_t g = (n + block - 1) / block;
+  return int(std::max<int64_t>(1, std::min<int64_t>(g, 2048 * 8)));
+}
+template <typename T>
+static void fill(Ctx& c, T* p, T v, int64_t n) {
+  if (n <= 0) return;
+  k_fill<T><<<grid_for(n), 256, 0, c.stream>>>(p, v, n);
+}
+
+static void grow_copy(Ctx& c, DevBuf& b, size_t need) {
+  if (need <= b.bytes) return;
+  DevBuf nb;
+  nb.alloc(std::max(need, b.bytes * 2));
+  if (b.bytes) NBG_HIP(hipMemcpyAsync(nb.p, b.p, b.bytes, hipMemcpyDeviceToDevice, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  b = std::move(nb);
+}
+
+static void stage_reserve(Ctx& c, Staging& s, size_t nfields, size_t extra, bool with_props,
+                          const std::vector<Field>& fields) {
+  size_t need = size_t(s.n) + extra;
+  if (need <= s.cap) return;
+  size_t cap = std::max(need, s.cap * 2);
+  grow_copy(c, s.src, cap * 8);
+  grow_copy(c, s.dst, cap * 8);
+  grow_copy(c, s.rank, cap * 8);
+  grow_copy(c, s.ver, cap * 8);
+  grow_copy(c, s.part, cap * 4);
+  if (with_props) {
+    s.props.resize(nfields);
+    s.present.resize(nfields);
+    s.str_len.resize(nfields);
+    for (size_t f = 0; f < nfields; f++) {
+      grow_copy(c, s.props[f], cap * 8);
+      grow_copy(c, s.present[f], cap);
+      if (fields[f].type == NBG_T_STRING) grow_copy(c, s.str_len[f], cap * 8);
+    }
+  }
+  s.cap = cap;
+}
+
+// ------------------------------------------------------------------------------------------
+// Stage 1a: KV decode
+// ------------------------------------------------------------------------------------------
+struct StageOut {
+  int32_t* part;
+  int64_t* src;
+  int64_t* dst;
+  int64_t* rank;
+  int64_t* ver;
+  int64_t* props[kMaxFields];
+  uint8_t* present[kMaxFields];
+  int64_t* str_len[kMaxFields];
+};
+
+template <typename T>
+__device__ inline T ld_unaligned(const uint8_t* p) {
+  T v;
+  __builtin_memcpy(&v, p, sizeof(T));
+  return v;
+}
+
+__device__ inline int dev_varint(const uint8_t* p, int64_t avail, uint64_t& out) {
+  uint64_t v = 0;
+  for (int i = 0; i < 10 && i < avail; i++) {
+    v |= uint64_t(p[i] & 0x7f) << (7 * i);
+    if (!(p[i] & 0x80)) {
+      out = v;
+      return i + 1;
+    }
+  }
+  return -1;
+}
+
+// Decodes one row into field slots.  Mirrors RowReader: header (RowReader.cpp:218-263),
+// sequential skip (skipToNext :276-341), stored block offsets for fields 16k (:239-249).
+__device__ void decode_row(const uint8_t* row, int64_t len, const SchemaDev& sch, int64_t heap_off,
+                           const StageOut& o, int64_t slot, unsigned long long* err) {
+  int nf = sch.nfields;
+  if (len <= 0) {
+    for (int f = 0; f < nf; f++) o.present[f][slot] = 0;
+    return;
+  }
+  uint8_t h = row[0];
+  int offBytes = (h & 7) + 1;
+  int verBytes = h >> 5;
+  int numOffsets = nf >> 4;
+  int64_t hdr = 1 + verBytes + int64_t(offBytes) * numOffsets;
+  if (hdr > len) {  // "Rowe data is too short": reader is invalid, no props
+    for (int f = 0; f < nf; f++) o.present[f][slot] = 0;
+    atomicAdd(err, 1ull);
+    return;
+  }
+  const uint8_t* data = row + hdr;
+  int64_t dlen = len - hdr;
+  int64_t pos = 0;
+  bool broken = false;
+  for (int f = 0; f < nf; f++) {
+    if (f > 0 && (f & 15) == 0) {
+      int64_t bo = 0;
+      const uint8_t* ob = row + 1 + verBytes + int64_t(offBytes) * ((f >> 4) - 1);
+      for (int j = 0; j < offBytes; j++) bo |= int64_t(uint64_t(ob[j]) << (8 * j));
+      pos = bo;
+      broken = false;
+    }
+    int64_t v = 0;
+    int64_t next = -1;
+    if (!broken && pos >= 0 && pos <= dlen) {
+      switch (sch.types[f]) {
+        case NBG_T_BOOL:
+          if (pos + 1 <= dlen) { v = data[pos] != 0; next = pos + 1; }
+          break;
+        case NBG_T_INT: {
+          uint64_t u;
+          int n = dev_varint(data + pos, dlen - pos, u);
+          if (n > 0) { v = int64_t(u); next = pos + n; }
+          break;
+        }
+        case NBG_T_VID:
+        case NBG_T_TIMESTAMP:
+          if (pos + 8 <= dlen) { v = ld_unaligned<int64_t>(data + pos); next = pos + 8; }
+          break;
+        case NBG_T_FLOAT:
+          if (pos + 4 <= dlen) {
+            double d = double(ld_unaligned<float>(data + pos));
+            v = __double_as_longlong(d);
+            next = pos + 4;
+          }
+          break;
+        case NBG_T_DOUBLE:
+          if (pos + 8 <= dlen) { v = ld_unaligned<int64_t>(data + pos); next = pos + 8; }
+          break;
+        case NBG_T_STRING: {
+          uint64_t sl;
+          int n = dev_varint(data + pos, dlen - pos, sl);
+          if (n > 0 && pos + n + int64_t(sl) <= dlen) {
+            v = heap_off + hdr + pos + n;
+            o.str_len[f][slot] = int64_t(sl);
+            next = pos + n + int64_t(sl);
+          }
+          break;
+        }
+        default: break;
+      }
+    }
+    if (next < 0) {
+      broken = true;
+      o.present[f][slot] = 0;
+      o.props[f][slot] = 0;
+    } else {
+      o.present[f][slot] = 1;
+      o.props[f][slot] = v;
+      pos = next;
+    }
+  }
+}
+
+__global__ void k_decode_kv(const uint8_t* __restrict__ kb, const uint64_t* __restrict__ koff,
+                            const uint8_t* __restrict__ vb, const uint64_t* __restrict__ voff,
+                            int64_t n, int32_t etype, int32_t sver, SchemaDev sch, int64_t heap_base,
+                            StageOut outS, unsigned long long* out_cnt, StageOut inS,
+                            unsigned long long* in_cnt, unsigned long long* err) {
+  int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  int64_t n_rounds = (n + stride - 1) / stride;
+  for (int64_t r = 0; r < n_rounds; r++) {
+    int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    bool is_out = false, is_in = false;
+    int64_t src = 0, dst = 0, rank = 0, ver = 0;
+    int32_t kpart = 0;
+    if (i < n) {
+      uint64_t k0 = koff[i], k1 = koff[i + 1];
+      if (k1 - k0 == 40) {
+        const uint8_t* k = kb + k0;
+        int32_t type = ld_unaligned<int32_t>(k + 12);
+        if (type == etype || type == -etype) {
+          kpart = ld_unaligned<int32_t>(k);
+          src = ld_unaligned<int64_t>(k + 4);
+          rank = ld_unaligned<int64_t>(k + 16);
+          dst = ld_unaligned<int64_t>(k + 24);
+          ver = ld_unaligned<int64_t>(k + 32);
+          is_out = type == etype;
+          is_in = !is_out;
+        }
+      }
+    }
+    int64_t so = wave_append(out_cnt, is_out);
+    int64_t si = wave_append(in_cnt, is_in);
+    if (is_out) {
+      outS.part[so] = kpart;
+      outS.src[so] = src;
+      outS.dst[so] = dst;
+      outS.rank[so] = rank;
+      outS.ver[so] = ver;
+      uint64_t v0 = voff[i], v1 = voff[i + 1];
+      const uint8_t* row = vb + v0;
+      int64_t len = int64_t(v1 - v0);
+      if (len > 0) {
+        // schema version from the row header (RowReader.cpp:173-199)
+        int verBytes = row[0] >> 5;
+        int32_t rv = 0;
+        if (verBytes > 0 && verBytes + 1 <= len)
+          for (int b = 0; b < verBytes; b++) rv |= int32_t(uint32_t(row[1 + b]) << (8 * b));
+        if (rv != sver) atomicAdd(err + 1, 1ull);
+      }
+      decode_row(row, len, sch, heap_base + int64_t(v0), outS, so, err);
+    }
+    if (is_in) {
+      inS.part[si] = kpart;
+      inS.src[si] = src;
+      inS.dst[si] = dst;
+      inS.rank[si] = rank;
+      inS.ver[si] = ver;
+    }
+  }
+}
+
+static StageOut stage_ptrs(Staging& s, size_t nf) {
+  StageOut o{};
+  o.part = s.part.as<int32_t>();
+  o.src = s.src.as<int64_t>();
+  o.dst = s.dst.as<int64_t>();
+  o.rank = s.rank.as<int64_t>();
+  o.ver = s.ver.as<int64_t>();
+  for (size_t f = 0; f < nf && f < size_t(kMaxFields); f++) {
+    o.props[f] = f < s.props.size() ? s.props[f].as<int64_t>() : nullptr;
+    o.present[f] = f < s.present.size() ? s.present[f].as<uint8_t>() : nullptr;
+    o.str_len[f] = f < s.str_len.size() ? s.str_len[f].as<int64_t>() : nullptr;
+  }
+  return o;
+}
+
+void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t* koff,
+                        const uint8_t* vb, const uint64_t* voff, size_t n) {
+  if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
+  if (part < 0 || part > c.num_parts) throw Error(NBG_E_PART_NOT_FOUND, "part out of range");
+  if (owner_of_part(part, c.world) != c.rank)
+    throw Error(NBG_E_PART_NOT_FOUND, "part " + std::to_string(part) + " is not owned by this rank");
+  if (c.edges.empty()) throw Error(NBG_E_STATE, "no edge schema registered");
+  if (n == 0) return;
+  double t0 = now_s();
+  size_t kbytes = koff[n], vbytes = voff[n];
+  DevBuf dk, dko, dvo;
+  dk.alloc(kbytes + 8);
+  dko.alloc((n + 1) * 8);
+  dvo.alloc((n + 1) * 8);
+  NBG_HIP(hipMemcpyAsync(dk.p, kb, kbytes, hipMemcpyHostToDevice, c.stream));
+  NBG_HIP(hipMemcpyAsync(dko.p, koff, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  NBG_HIP(hipMemcpyAsync(dvo.p, voff, (n + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  // value bytes go to the string heap (kept until finalize for STRING props)
+  int64_t heap_base = int64_t(c.heap_used);
+  grow_copy(c, c.heap, c.heap_used + vbytes + 8);
+  if (vbytes) NBG_HIP(hipMemcpyAsync(c.heap.as<uint8_t>() + heap_base, vb, vbytes, hipMemcpyHostToDevice, c.stream));
+  c.heap_used += vbytes;
+  DevBuf cnt;
+  cnt.alloc(64);
+  for (auto& kvp : c.edges) {
+    EdgeSpace& es = kvp.second;
+    size_t nf = es.fields.size();
+    if (nf > size_t(kMaxFields)) throw Error(NBG_E_UNSUPPORTED, "more than 64 edge fields");
+    SchemaDev sch{};
+    sch.nfields = int32_t(nf);
+    for (size_t f = 0; f < nf; f++) sch.types[f] = es.fields[f].type;
+    stage_reserve(c, es.out_stage, nf, n, true, es.fields);
+    stage_reserve(c, es.in_stage, 0, n, false, es.fields);
+    NBG_HIP(hipMemsetAsync(cnt.p, 0, 64, c.stream));
+    unsigned long long* d = cnt.as<unsigned long long>();
+    NBG_HIP(hipMemcpyAsync(d, &es.out_stage.n, 8, hipMemcpyHostToDevice, c.stream));
+    NBG_HIP(hipMemcpyAsync(d + 1, &es.in_stage.n, 8, hipMemcpyHostToDevice, c.stream));
+    StageOut so = stage_ptrs(es.out_stage, nf);
+    StageOut si = stage_ptrs(es.in_stage, 0);
+    k_decode_kv<<<grid_for(int64_t(n)), 256, 0, c.stream>>>(
+        dk.as<uint8_t>(), dko.as<uint64_t>(), c.heap.as<uint8_t>() + heap_base, dvo.as<uint64_t>(),
+        int64_t(n), es.type, es.schema_ver, sch, heap_base, so, d, si, d + 1, d + 2);
+    NBG_HIP(hipGetLastError());
+    unsigned long long h[4];
+    NBG_HIP(hipMemcpyAsync(h, d, 32, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    if (h[3] != 0)
+      throw Error(NBG_E_UNSUPPORTED, "row schema version differs from the registered version");
+    es.out_stage.n = int64_t(h[0]);
+    es.in_stage.n = int64_t(h[1]);
+    es.out_stage.rank_const = es.out_stage.ver_const = false;
+    es.in_stage.rank_const = es.in_stage.ver_const = false;
+  }
+  c.build_seconds += now_s() - t0;
+}
+
+// ------------------------------------------------------------------------------------------
+// Stage 1b: synthetic RMAT (definition shared with oracle/refcpu.cpp)
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kTA = 2448131358u;    // floor(0.57 * 2^32)
+constexpr uint32_t kTAB = 3264175144u;   // floor(0.76 * 2^32)
+constexpr uint32_t kTABC = 4080218931u;  // floor(0.95 * 2^32)
+
+__device__ inline void rmat_pick(uint32_t r, uint64_t& u, uint64_t& v) {
+  uint64_t bu = (r >= kTAB) ? 1 : 0;
+  uint64_t bv = ((r >= kTA && r < kTAB) || r >= kTABC) ? 1 : 0;
+  u = (u << 1) | bu;
+  v = (v << 1) | bv;
+}
+__device__ inline int64_t rmat_vid(uint64_t idx, uint64_t smix) {
+  const uint64_t M = (1ull << 63) - 1;
+  uint64_t x = (idx + smix) & M;
+  x ^= x >> 29;
+  x = (x * 0xBF58476D1CE4E5B9ull) & M;
+  x ^= x >> 32;
+  x = (x * 0x94D049BB133111EBull) & M;
+  x ^= x >> 29;
+  return int64_t(x);
+}
+
+__global__ void k_gen_rmat(int64_t lo, int64_t hi, int32_t scale, uint64_t seed, uint64_t smix,
+                           int32_t parts, int32_t world, int32_t rank, int64_t* osrc, int64_t* odst,
+                           int64_t* oweight, unsigned long long* ocnt, int64_t* isrc, int64_t* idst,
+                           unsigned long long* icnt) {
+  int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  int64_t n = hi - lo;
+  int64_t rounds = (n + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    int64_t j = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    bool valid = j < n;
+    int64_t s = 0, d = 0;
+    if (valid) {
+      uint64_t i = uint64_t(lo + j);
+      uint64_t u = 0, v = 0;
+      for (int32_t l = 0; l < scale; l += 2) {
+        uint64_t h = splitmix64(seed ^ (0xD6E8FEB86659FD93ull * (i + 1)) ^ (0xA0761D6478BD642Full * uint64_t(l + 1)));
+        rmat_pick(uint32_t(h >> 32), u, v);
+        if (l + 1 < scale) rmat_pick(uint32_t(h), u, v);
+      }
+      s = rmat_vid(u, smix);
+      d = rmat_vid(v, smix);
+    }
+    bool is_out = valid && (world == 1 || dev_owner(s, parts, world) == rank);
+    bool is_in = valid && (world == 1 || dev_owner(d, parts, world) == rank);
+    int64_t so = wave_append(ocnt, is_out);
+    int64_t si = wave_append(icnt, is_in);
+    if (is_out) {
+      osrc[so] = s;
+      odst[so] = d;
+      uint64_t du = uint64_t(d);
+      oweight[so] = int64_t(splitmix64(uint64_t(s) ^ ((du << 32) | (du >> 32)) ^ seed) % 1000);
+    }
+    if (is_in) {  // in-edge key (dst, -type, rank, src): key src = d, key dst = s
+      isrc[si] = d;
+      idst[si] = s;
+    }
+  }
+}
+
+void snapshot_gen_rmat(Ctx& c, int32_t scale, int32_t ef, uint64_t seed, int32_t et) {
+  if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
+  auto it = c.edges.find(et);
+  if (it == c.edges.end()) throw Error(NBG_E_INVALID_ARG, "edge type not registered");
+  EdgeSpace& es = it->second;
+  if (es.fields.size() != 1 || es.fields[0].type != NBG_T_INT)
+    throw Error(NBG_E_INVALID_ARG, "RMAT edge schema must be (weight int)");
+  if (scale < 1 || scale > 31 || ef < 1) throw Error(NBG_E_INVALID_ARG, "bad RMAT scale");
+  double t0 = now_s();
+  int64_t E = int64_t(ef) << scale;
+  int64_t expect = c.world == 1 ? E : E / c.world + E / (4 * c.world) + (1 << 20);
+  Staging& so = es.out_stage;
+  Staging& si = es.in_stage;
+  if (so.n != 0 || si.n != 0) throw Error(NBG_E_STATE, "RMAT must be the only source of this edge type");
+  auto alloc_stage = [&](Staging& s, int64_t cap, bool props) {
+    s.src.alloc(size_t(cap) * 8);
+    s.dst.alloc(size_t(cap) * 8);
+    s.rank.release();
+    s.ver.release();
+    s.part.release();
+    s.rank_const = s.ver_const = true;
+    s.rank_value = 0;
+    s.ver_value = INT64_MAX - 1;
+    if (props) {
+      s.props.resize(1);
+      s.present.resize(1);
+      s.str_len.resize(1);
+      s.props[0].alloc(size_t(cap) * 8);
+      s.present[0].release();  // all present
+    }
+    s.cap = size_t(cap);
+  };
+  alloc_stage(so, expect, true);
+  alloc_stage(si, expect, false);
+  DevBuf cnt;
+  cnt.alloc(16);
+  NBG_HIP(hipMemsetAsync(cnt.p, 0, 16, c.stream));
+  unsigned long long* d = cnt.as<unsigned long long>();
+  uint64_t smix = splitmix64(seed) & ((1ull << 63) - 1);
+  const int64_t chunk = int64_t(1) << 26;
+  for (int64_t lo = 0; lo < E; lo += chunk) {
+    int64_t hi = std::min(E, lo + chunk);
+    k_gen_rmat<<<grid_for(hi - lo), 256, 0, c.stream>>>(lo, hi, scale, seed, smix, c.num_parts, c.world,
+                                                      c.rank, so.src.as<int64_t>(), so.dst.as<int64_t>(),
+                                                      so.props[0].as<int64_t>(), d, si.src.as<int64_t>(),
+                                                      si.dst.as<int64_t>(), d + 1);
+    NBG_HIP(hipGetLastError());
+    if (c.world > 1) {  // guard against staging overflow on skewed ownership
+      unsigned long long h[2];
+      NBG_HIP(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      if (int64_t(std::max(h[0], h[1])) + chunk > expect)
+        throw Error(NBG_E_NOMEM, "RMAT staging capacity exceeded");
+    }
+  }
+  unsigned long long h[2];
+  NBG_HIP(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  so.n = int64_t(h[0]);
+  si.n = int64_t(h[1]);
+  c.build_seconds += now_s() - t0;
+}
+
+// ------------------------------------------------------------------------------------------
+// Stage 2: finalize
+// ------------------------------------------------------------------------------------------
+template <typename K, typename V>
+static void radix_pairs(Ctx& c, K* kin, K* kout, V* vin, V* vout, int64_t n, int bits) {
+  size_t tb = 0;
+  NBG_HIP(rocprim::radix_sort_pairs(nullptr, tb, kin, kout, vin, vout, size_t(n), 0, bits, c.stream));
+  c.ws_tmp.ensure(tb);
+  NBG_HIP(rocprim::radix_sort_pairs(c.ws_tmp.p, tb, kin, kout, vin, vout, size_t(n), 0, bits, c.stream));
+}
+template <typename K>
+static void radix_keys(Ctx& c, K* kin, K* kout, int64_t n, int bits) {
+  size_t tb = 0;
+  NBG_HIP(rocprim::radix_sort_keys(nullptr, tb, kin, kout, size_t(n), 0, bits, c.stream));
+  c.ws_tmp.ensure(tb);
+  NBG_HIP(rocprim::radix_sort_keys(c.ws_tmp.p, tb, kin, kout, size_t(n), 0, bits, c.stream));
+}
+// unique of a sorted array; returns count
+template <typename T>
+static int64_t unique_sorted(Ctx& c, T* in, T* out, int64_t n) {
+  DevBuf cnt;
+  cnt.alloc(8);
+  size_t tb = 0;
+  NBG_HIP(rocprim::unique(nullptr, tb, in, out, cnt.as<uint64_t>(), size_t(n), rocprim::equal_to<T>(), c.stream));
+  c.ws_tmp.ensure(tb);
+  NBG_HIP(rocprim::unique(c.ws_tmp.p, tb, in, out, cnt.as<uint64_t>(), size_t(n), rocprim::equal_to<T>(), c.stream));
+  uint64_t h = 0;
+  NBG_HIP(hipMemcpyAsync(&h, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  return int64_t(h);
+}
+template <typename T>
+static void exclusive_scan(Ctx& c, const T* in, T* out, int64_t n) {
+  size_t tb = 0;
+  NBG_HIP(rocprim::exclusive_scan(nullptr, tb, in, out, T(0), size_t(n), rocprim::plus<T>(), c.stream));
+  c.ws_tmp.ensure(tb);
+  NBG_HIP(rocprim::exclusive_scan(c.ws_tmp.p, tb, in, out, T(0), size_t(n), rocprim::plus<T>(), c.stream));
+}
+
+// key transform for signed int64 sort order: flip the sign bit
+__global__ void k_flip_copy(const int64_t* in, uint64_t* out, int64_t n, int world, int parts, int rank,
+                            int filter_owner) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    int64_t v = in[i];
+    out[i] = uint64_t(v) ^ (1ull << 63);
+  }
+}
+__global__ void k_unflip(const uint64_t* in, int64_t* out, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = int64_t(in[i] ^ (1ull << 63));
+}
+
+__global__ void k_ht_insert(int64_t* keys, int32_t* vals, uint64_t mask, const int64_t* vids, int64_t n,
+                            int32_t* min_gidx) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    int64_t v = vids[i];
+    if (v == INT64_MIN) {
+      *min_gidx = int32_t(i);
+      continue;
+    }
+    uint64_t h = ht_hash(v) & mask;
+    while (true) {
+      unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(keys + h),
+                                          (unsigned long long)INT64_MIN, (unsigned long long)v);
+      if (prev == (unsigned long long)INT64_MIN || int64_t(prev) == v) {
+        vals[h] = int32_t(i);
+        break;
+      }
+      h = (h + 1) & mask;
+    }
+  }
+}
+__global__ void k_ht_lookup(const int64_t* keys, const int32_t* vals, uint64_t mask, bool has_min,
+                            int32_t min_gidx, const int64_t* vids, int32_t* out, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = ht_lookup(keys, vals, mask, vids[i], has_min, min_gidx);
+}
+
+void lookup_gidx(Ctx& c, const int64_t* d_vids, int32_t* d_gidx, int64_t n) {
+  if (n <= 0) return;
+  k_ht_lookup<<<grid_for(n), 256, 0, c.stream>>>(c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
+                                                uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx,
+                                                d_vids, d_gidx, n);
+  NBG_HIP(hipGetLastError());
+}
+
+// bytewise order rank of every vertex: position of gidx in the order of bswap(vid)
+__global__ void k_bswap_keys(const int64_t* vid_of, uint64_t* keys, uint32_t* idx, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    keys[i] = bswap64(uint64_t(vid_of[i]));
+    idx[i] = uint32_t(i);
+  }
+}
+__global__ void k_scatter_rank(const uint32_t* sorted_idx, uint32_t* byterank, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    byterank[sorted_idx[i]] = uint32_t(i);
+}
+
+// edge sort key (single-pass case): (src_local << 32) | byterank(dst)
+__global__ void k_edge_keys(const int64_t* src, const int64_t* dst, int64_t n, const int64_t* keys_ht,
+                            const int32_t* vals_ht, uint64_t mask, bool has_min, int32_t min_gidx,
+                            int64_t lo, int64_t hi, const uint32_t* byterank, uint64_t* keys,
+                            uint32_t* perm, int32_t* dst_g, unsigned long long* err) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    int32_t sg = ht_lookup(keys_ht, vals_ht, mask, src[i], has_min, min_gidx);
+    int32_t dg = ht_lookup(keys_ht, vals_ht, mask, dst[i], has_min, min_gidx);
+    if (sg < lo || sg >= hi || dg < 0) {
+      atomicAdd(err, 1ull);
+      sg = int32_t(lo);
+      dg = 0;
+    }
+    keys[i] = (uint64_t(uint32_t(sg - lo)) << 32) | uint64_t(byterank[dg]);
+    perm[i] = uint32_t(i);
+    dst_g[i] = dg;
+  }
+}
+// multi-pass LSD helpers: gather a 64-bit key through the current permutation
+__global__ void k_gather_key_bswap(const int64_t* vals, const uint32_t* perm, uint64_t* keys, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    keys[i] = bswap64(uint64_t(vals[perm[i]]));
+}
+__global__ void k_gather_key_src(const uint64_t* srckey, const uint32_t* perm, uint64_t* keys, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    keys[i] = srckey[perm[i]] >> 32;
+}
+
+// keep-first flags in sorted order: (src, rank, dst) differs from predecessor
+__global__ void k_dedup_flags(const uint64_t* skey, const uint32_t* perm, const int64_t* rank,
+                              const int32_t* dst_g, int64_t n, uint8_t* keep) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    bool k = true;
+    if (i > 0) {
+      uint32_t a = perm[i - 1], b = perm[i];
+      bool same = (skey[a] >> 32) == (skey[b] >> 32) && dst_g[a] == dst_g[b] &&
+                  (rank == nullptr || rank[a] == rank[b]);
+      k = !same;
+    }
+    keep[i] = k;
+  }
+}
+
+__global__ void k_row_part_default(const int64_t* vid_of_lo, int64_t n, int32_t parts, int32_t* row_part) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    row_part[i] = dev_part_of(vid_of_lo[i], parts);
+}
+__global__ void k_row_part_scatter(const uint64_t* skey, const uint32_t* kept_perm, int64_t m, const int32_t* part,
+                                   int32_t* row_part) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    uint32_t t = kept_perm[i];
+    row_part[skey[t] >> 32] = part[t];
+  }
+}
+__global__ void k_row_ok(const int64_t* vid_of_lo, int64_t n, int32_t parts, const int32_t* row_part, uint8_t* ok,
+                         unsigned long long* bad) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    bool g = row_part[i] == dev_part_of(vid_of_lo[i], parts);
+    ok[i] = g;
+    if (!g) atomicAdd(bad, 1ull);
+  }
+}
+__global__ void k_row_counts(const uint64_t* skey, const uint32_t* kept_perm, int64_t m, int64_t* counts) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    atomicAdd(reinterpret_cast<unsigned long long*>(counts + (skey[kept_perm[i]] >> 32)), 1ull);
+}
+__global__ void k_gather_i32(const int32_t* in, const uint32_t* perm, int32_t* out, int64_t m) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = in[perm[i]];
+}
+__global__ void k_gather_i64(const int64_t* in, const uint32_t* perm, int64_t* out, int64_t m) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = in[perm[i]];
+}
+__global__ void k_gather_u8(const uint8_t* in, const uint32_t* perm, uint8_t* out, int64_t m) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = in[perm[i]];
+}
+template <typename T>
+__global__ void k_narrow(const int64_t* in, T* out, int64_t m) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = T(in[i]);
+}
+__global__ void k_str_lengths(const int64_t* lens, const uint8_t* present, int64_t m, int64_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = (present == nullptr || present[i]) ? lens[i] : 0;
+}
+__global__ void k_str_copy(const uint8_t* heap, const int64_t* offs_src, const int64_t* dst_off, int64_t m,
+                           uint8_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    int64_t len = dst_off[i + 1] - dst_off[i];
+    const uint8_t* s = heap + offs_src[i];
+    uint8_t* d = out + dst_off[i];
+    for (int64_t j = 0; j < len; j++) d[j] = s[j];
+  }
+}
+
+static void minmax_i64(Ctx& c, const int64_t* d, int64_t n, int64_t& mn, int64_t& mx) {
+  DevBuf r;
+  r.alloc(16);
+  size_t tb = 0;
+  NBG_HIP(rocprim::reduce(nullptr, tb, d, r.as<int64_t>(), INT64_MAX, size_t(n), rocprim::minimum<int64_t>(), c.stream));
+  c.ws_tmp.ensure(tb);
+  NBG_HIP(rocprim::reduce(c.ws_tmp.p, tb, d, r.as<int64_t>(), INT64_MAX, size_t(n), rocprim::minimum<int64_t>(), c.stream));
+  tb = 0;
+  NBG_HIP(rocprim::reduce(nullptr, tb, d, r.as<int64_t>() + 1, INT64_MIN, size_t(n), rocprim::maximum<int64_t>(), c.stream));
+  c.ws_tmp.ensure(tb);
+  NBG_HIP(rocprim::reduce(c.ws_tmp.p, tb, d, r.as<int64_t>() + 1, INT64_MIN, size_t(n), rocprim::maximum<int64_t>(), c.stream));
+  int64_t h[2];
+  NBG_HIP(hipMemcpyAsync(h, r.p, 16, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  mn = h[0];
+  mx = h[1];
+}
+
+// Builds one CSR from a staging area.  Returns after freeing the staging buffers.
+static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool with_props, Csr& out,
+                      const uint32_t* byterank) {
+  int64_t n = s.n;
+  int64_t lo = c.owned_lo(), hi = c.owned_hi();
+  out.n_rows = hi - lo;
+  out.row_ptr.alloc(size_t(out.n_rows + 1) * 8);
+  if (n == 0) {
+    NBG_HIP(hipMemsetAsync(out.row_ptr.p, 0, size_t(out.n_rows + 1) * 8, c.stream));
+    out.nnz = 0;
+    for (auto& f : fields)
+      if (with_props) {
+        PropCol pc;
+        pc.name = f.name;
+        pc.type = f.type;
+        out.props.push_back(std::move(pc));
+      }
+    return;
+  }
+  if (n >= (int64_t(1) << 32)) throw Error(NBG_E_UNSUPPORTED, "more than 2^32 edges on one rank");
+  // keys
+  DevBuf keyA, keyB, permA, permB, dstg, err;
+  keyA.alloc(size_t(n) * 8);
+  keyB.alloc(size_t(n) * 8);
+  permA.alloc(size_t(n) * 4);
+  permB.alloc(size_t(n) * 4);
+  dstg.alloc(size_t(n) * 4);
+  err.alloc(8);
+  NBG_HIP(hipMemsetAsync(err.p, 0, 8, c.stream));
+  k_edge_keys<<<grid_for(n), 256, 0, c.stream>>>(s.src.as<int64_t>(), s.dst.as<int64_t>(), n, c.ht_keys.as<int64_t>(),
+                                               c.ht_vals.as<int32_t>(), uint64_t(c.ht_cap - 1), c.ht_has_min,
+                                               c.ht_min_gidx, lo, hi, byterank, keyA.as<uint64_t>(),
+                                               permA.as<uint32_t>(), dstg.as<int32_t>(), err.as<unsigned long long>());
+  NBG_HIP(hipGetLastError());
+  uint64_t herr = 0;
+  NBG_HIP(hipMemcpyAsync(&herr, err.p, 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  if (herr) throw Error(NBG_E_PART_NOT_FOUND, "edge source not owned by this rank / unknown vertex");
+  int srcbits = 1;
+  while ((int64_t(1) << srcbits) < std::max<int64_t>(out.n_rows, 2)) srcbits++;
+  uint32_t* perm = nullptr;
+  DevBuf& skey_keep = keyA;  // (src_local << 32 | byterank(dst)) by tuple index
+  if (s.rank_const && s.ver_const) {
+    // single pass on (src_local, byterank(dst)) == the reference key order
+    radix_pairs<uint64_t, uint32_t>(c, skey_keep.as<uint64_t>(), keyB.as<uint64_t>(), permA.as<uint32_t>(),
+                                   permB.as<uint32_t>(), n, 32 + srcbits);
+    perm = permB.as<uint32_t>();
+  } else {
+    // LSD passes: version bytes, dst bytes, rank bytes, then src (most significant)
+    DevBuf keyC;
+    keyC.alloc(size_t(n) * 8);
+    uint32_t* pin = permA.as<uint32_t>();
+    uint32_t* pout = permB.as<uint32_t>();
+    auto pass_bswap = [&](const DevBuf& vals) {
+      k_gather_key_bswap<<<grid_for(n), 256, 0, c.stream>>>(vals.as<int64_t>(), pin, keyC.as<uint64_t>(), n);
+      radix_pairs<uint64_t, uint32_t>(c, keyC.as<uint64_t>(), keyB.as<uint64_t>(), pin, pout, n, 64);
+      std::swap(pin, pout);
+    };
+    if (!s.ver_const) pass_bswap(s.ver);
+    pass_bswap(s.dst);
+    if (!s.rank_const) pass_bswap(s.rank);
+    k_gather_key_src<<<grid_for(n), 256, 0, c.stream>>>(skey_keep.as<uint64_t>(), pin, keyC.as<uint64_t>(), n);
+    radix_pairs<uint64_t, uint32_t>(c, keyC.as<uint64_t>(), keyB.as<uint64_t>(), pin, pout, n, srcbits);
+    perm = pout;
+  }
+  // dedup (keep the first = bytewise-smallest version)
+  DevBuf keep;
+  keep.alloc(size_t(n));
+  const int64_t* rank_ptr = s.rank_const ? nullptr : s.rank.as<int64_t>();
+  k_dedup_flags<<<grid_for(n), 256, 0, c.stream>>>(skey_keep.as<uint64_t>(), perm, rank_ptr, dstg.as<int32_t>(), n,
+                                                 keep.as<uint8_t>());
+  DevBuf kept, cnt;
+  kept.alloc(size_t(n) * 4);
+  cnt.alloc(8);
+  size_t tb = 0;
+  NBG_HIP(rocprim::select(nullptr, tb, perm, keep.as<uint8_t>(), kept.as<uint32_t>(), cnt.as<uint64_t>(), size_t(n), c.stream));
+  c.ws_tmp.ensure(tb);
+  NBG_HIP(rocprim::select(c.ws_tmp.p, tb, perm, keep.as<uint8_t>(), kept.as<uint32_t>(), cnt.as<uint64_t>(), size_t(n), c.stream));
+  uint64_t m = 0;
+  NBG_HIP(hipMemcpyAsync(&m, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  keyB.release();
+  permA.release();
+  permB.release();
+  keep.release();
+  out.nnz = int64_t(m);
+  const uint32_t* kp = kept.as<uint32_t>();
+  // row_ptr
+  DevBuf counts;
+  counts.alloc(size_t(out.n_rows + 1) * 8);
+  NBG_HIP(hipMemsetAsync(counts.p, 0, size_t(out.n_rows + 1) * 8, c.stream));
+  k_row_counts<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(skey_keep.as<uint64_t>(), kp, int64_t(m), counts.as<int64_t>());
+  exclusive_scan<int64_t>(c, counts.as<int64_t>(), out.row_ptr.as<int64_t>(), out.n_rows + 1);
+  // row_part: hash rule by default, the key's part where the staging recorded it
+  out.row_part.alloc(size_t(out.n_rows + 1) * 4);
+  k_row_part_default<<<grid_for(out.n_rows), 256, 0, c.stream>>>(c.vid_of.as<int64_t>() + lo, out.n_rows,
+                                                               c.num_parts, out.row_part.as<int32_t>());
+  if (s.part.p) {
+    DevBuf bad;
+    bad.alloc(8);
+    NBG_HIP(hipMemsetAsync(bad.p, 0, 8, c.stream));
+    k_row_part_scatter<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(skey_keep.as<uint64_t>(), kp, int64_t(m),
+                                                                   s.part.as<int32_t>(), out.row_part.as<int32_t>());
+    out.row_ok.alloc(size_t(out.n_rows + 1));
+    k_row_ok<<<grid_for(out.n_rows), 256, 0, c.stream>>>(c.vid_of.as<int64_t>() + lo, out.n_rows, c.num_parts,
+                                                         out.row_part.as<int32_t>(), out.row_ok.as<uint8_t>(),
+                                                         bad.as<unsigned long long>());
+    uint64_t hb = 0;
+    NBG_HIP(hipMemcpyAsync(&hb, bad.p, 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    if (hb == 0) out.row_ok.release();
+  }
+  // col
+  out.col.alloc(size_t(m) * 4 + 4);
+  k_gather_i32<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(dstg.as<int32_t>(), kp, out.col.as<int32_t>(), int64_t(m));
+  // rank
+  if (!s.rank_const) {
+    out.rank.alloc(size_t(m) * 8 + 8);
+    k_gather_i64<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(s.rank.as<int64_t>(), kp, out.rank.as<int64_t>(), int64_t(m));
+    int64_t mn, mx;
+    minmax_i64(c, out.rank.as<int64_t>(), int64_t(m), mn, mx);
+    if (mn == 0 && mx == 0) out.rank.release();
+  } else if (s.rank_value != 0) {
+    out.rank.alloc(size_t(m) * 8 + 8);
+    fill<int64_t>(c, out.rank.as<int64_t>(), s.rank_value, int64_t(m));
+  }
+  // props
+  if (with_props) {
+    DevBuf tmp;
+    tmp.alloc(size_t(m) * 8 + 8);
+    for (size_t f = 0; f < fields.size(); f++) {
+      PropCol pc;
+      pc.name = fields[f].name;
+      pc.type = fields[f].type;
+      k_gather_i64<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(s.props[f].as<int64_t>(), kp, tmp.as<int64_t>(), int64_t(m));
+      bool has_present = f < s.present.size() && s.present[f].p != nullptr;
+      if (has_present) {
+        pc.present.alloc(size_t(m) + 1);
+        k_gather_u8<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(s.present[f].as<uint8_t>(), kp, pc.present.as<uint8_t>(), int64_t(m));
+      }
+      if (pc.type == NBG_T_STRING) {
+        DevBuf lens, offs_src;
+        lens.alloc(size_t(m) * 8 + 8);
+        offs_src.alloc(size_t(m) * 8 + 8);
+        k_gather_i64<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(s.str_len[f].as<int64_t>(), kp, lens.as<int64_t>(), int64_t(m));
+        NBG_HIP(hipMemcpyAsync(offs_src.p, tmp.p, size_t(m) * 8, hipMemcpyDeviceToDevice, c.stream));
+        DevBuf l2;
+        l2.alloc(size_t(m + 1) * 8);
+        k_str_lengths<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(lens.as<int64_t>(),
+                                                               has_present ? pc.present.as<uint8_t>() : nullptr,
+                                                               int64_t(m), l2.as<int64_t>());
+        NBG_HIP(hipMemsetAsync(l2.as<int64_t>() + m, 0, 8, c.stream));
+        pc.str_off.alloc(size_t(m + 1) * 8);
+        exclusive_scan<int64_t>(c, l2.as<int64_t>(), pc.str_off.as<int64_t>(), int64_t(m) + 1);
+        int64_t total = 0;
+        NBG_HIP(hipMemcpyAsync(&total, pc.str_off.as<int64_t>() + m, 8, hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipStreamSynchronize(c.stream));
+        pc.str_bytes.alloc(size_t(total) + 8);
+        k_str_copy<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(c.heap.as<uint8_t>(), offs_src.as<int64_t>(),
+                                                             pc.str_off.as<int64_t>(), int64_t(m), pc.str_bytes.as<uint8_t>());
+        pc.width = 0;
+      } else if (pc.type == NBG_T_DOUBLE || pc.type == NBG_T_FLOAT) {
+        pc.width = 8;
+        pc.data.alloc(size_t(m) * 8 + 8);
+        NBG_HIP(hipMemcpyAsync(pc.data.p, tmp.p, size_t(m) * 8, hipMemcpyDeviceToDevice, c.stream));
+      } else {
+        // INT / VID / TIMESTAMP / BOOL: narrow to the smallest width holding [min, max]
+        int64_t mn = 0, mx = 0;
+        if (m) minmax_i64(c, tmp.as<int64_t>(), int64_t(m), mn, mx);
+        pc.minv = mn;
+        pc.maxv = mx;
+        int w = 8;
+        if (mn >= INT8_MIN && mx <= INT8_MAX) w = 1;
+        else if (mn >= INT16_MIN && mx <= INT16_MAX) w = 2;
+        else if (mn >= INT32_MIN && mx <= INT32_MAX) w = 4;
+        if (c.opt("narrow_props", 1) == 0) w = 8;
+        pc.width = w;
+        pc.data.alloc(size_t(m) * size_t(w) + 16);
+        int g = grid_for(int64_t(m));
+        switch (w) {
+          case 1: k_narrow<int8_t><<<g, 256, 0, c.stream>>>(tmp.as<int64_t>(), pc.data.as<int8_t>(), int64_t(m)); break;
+          case 2: k_narrow<int16_t><<<g, 256, 0, c.stream>>>(tmp.as<int64_t>(), pc.data.as<int16_t>(), int64_t(m)); break;
+          case 4: k_narrow<int32_t><<<g, 256, 0, c.stream>>>(tmp.as<int64_t>(), pc.data.as<int32_t>(), int64_t(m)); break;
+          default: NBG_HIP(hipMemcpyAsync(pc.data.p, tmp.p, size_t(m) * 8, hipMemcpyDeviceToDevice, c.stream));
+        }
+      }
+      out.props.push_back(std::move(pc));
+    }
+  }
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  NBG_HIP(hipGetLastError());
+  // free staging
+  s.src.release();
+  s.dst.release();
+  s.rank.release();
+  s.ver.release();
+  s.part.release();
+  s.props.clear();
+  s.present.clear();
+  s.str_len.clear();
+  s.n = 0;
+  s.cap = 0;
+}
+
+__global__ void k_owned_only(const uint64_t* in, int64_t n, int parts, int world, int rank, uint8_t* flag) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    int64_t v = int64_t(in[i] ^ (1ull << 63));
+    flag[i] = dev_owner(v, parts, world) == rank;
+  }
+}
+
+void snapshot_finalize(Ctx& c) {
+  if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
+  double t0 = now_s();
+  // 1. referenced vids (src/dst of every staged tuple), sign-flipped for unsigned sort
+  int64_t total = 0;
+  for (auto& kv : c.edges) total += 2 * (kv.second.out_stage.n + kv.second.in_stage.n);
+  DevBuf vA, vB;
+  vA.alloc(size_t(std::max<int64_t>(total, 1)) * 8);
+  vB.alloc(size_t(std::max<int64_t>(total, 1)) * 8);
+  int64_t pos = 0;
+  for (auto& kv : c.edges) {
+    for (Staging* s : {&kv.second.out_stage, &kv.second.in_stage}) {
+      if (s->n == 0) continue;
+      k_flip_copy<<<grid_for(s->n), 256, 0, c.stream>>>(s->src.as<int64_t>(), vA.as<uint64_t>() + pos, s->n, 0, 0, 0, 0);
+      pos += s->n;
+      k_flip_copy<<<grid_for(s->n), 256, 0, c.stream>>>(s->dst.as<int64_t>(), vA.as<uint64_t>() + pos, s->n, 0, 0, 0, 0);
+      pos += s->n;
+    }
+  }
+  int64_t nuniq = 0;
+  if (total > 0) {
+    radix_keys<uint64_t>(c, vA.as<uint64_t>(), vB.as<uint64_t>(), total, 64);
+    nuniq = unique_sorted<uint64_t>(c, vB.as<uint64_t>(), vA.as<uint64_t>(), total);
+  }
+  vB.release();
+  // 2. owned set and global table
+  std::vector<int64_t> counts(size_t(c.world), 0);
+  DevBuf owned;
+  int64_t n_owned = nuniq;
+  if (c.world == 1) {
+    owned = std::move(vA);
+  } else {
+    // every rank sends the vids it references to their owners; owners union.  (Simple form:
+    // allgather the unique referenced sets, filter by owner; fine for build-time volumes.)
+    int64_t mine = nuniq;
+    std::vector<int64_t> sizes(size_t(c.world));
+    DevBuf dsz, dall;
+    dsz.alloc(8 * size_t(c.world));
+    DevBuf dmine;
+    dmine.alloc(8);
+    NBG_HIP(hipMemcpyAsync(dmine.p, &mine, 8, hipMemcpyHostToDevice, c.stream));
+    comm_allgather_bytes(c, dmine.p, 8, dsz.p);
+    NBG_HIP(hipMemcpyAsync(sizes.data(), dsz.p, 8 * size_t(c.world), hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    int64_t mx = *std::max_element(sizes.begin(), sizes.end());
+    DevBuf sendb, recvb;
+    sendb.alloc(size_t(std::max<int64_t>(mx, 1)) * 8);
+    recvb.alloc(size_t(std::max<int64_t>(mx, 1)) * 8 * size_t(c.world));
+    if (nuniq) NBG_HIP(hipMemcpyAsync(sendb.p, vA.p, size_t(nuniq) * 8, hipMemcpyDeviceToDevice, c.stream));
+    comm_allgather_bytes(c, sendb.p, size_t(mx) * 8, recvb.p);
+    // compact all received sets, keep owned, sort + unique
+    DevBuf all;
+    int64_t tot = 0;
+    for (auto s : sizes) tot += s;
+    all.alloc(size_t(std::max<int64_t>(tot, 1)) * 8);
+    int64_t p2 = 0;
+    for (int r = 0; r < c.world; r++) {
+      if (sizes[size_t(r)])
+        NBG_HIP(hipMemcpyAsync(all.as<uint64_t>() + p2, recvb.as<uint64_t>() + size_t(r) * size_t(mx),
+                               size_t(sizes[size_t(r)]) * 8, hipMemcpyDeviceToDevice, c.stream));
+      p2 += sizes[size_t(r)];
+    }
+    DevBuf flag, sel, cnt;
+    flag.alloc(size_t(std::max<int64_t>(tot, 1)));
+    sel.alloc(size_t(std::max<int64_t>(tot, 1)) * 8);
+    cnt.alloc(8);
+    k_owned_only<<<grid_for(tot), 256, 0, c.stream>>>(all.as<uint64_t>(), tot, c.num_parts, c.world, c.rank, flag.as<uint8_t>());
+    size_t tb = 0;
+    NBG_HIP(rocprim::select(nullptr, tb, all.as<uint64_t>(), flag.as<uint8_t>(), sel.as<uint64_t>(), cnt.as<uint64_t>(), size_t(tot), c.stream));
+    c.ws_tmp.ensure(tb);
+    NBG_HIP(rocprim::select(c.ws_tmp.p, tb, all.as<uint64_t>(), flag.as<uint8_t>(), sel.as<uint64_t>(), cnt.as<uint64_t>(), size_t(tot), c.stream));
+    uint64_t ns = 0;
+    NBG_HIP(hipMemcpyAsync(&ns, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    DevBuf s2;
+    s2.alloc(size_t(std::max<uint64_t>(ns, 1)) * 8);
+    radix_keys<uint64_t>(c, sel.as<uint64_t>(), s2.as<uint64_t>(), int64_t(ns), 64);
+    owned.alloc(size_t(std::max<uint64_t>(ns, 1)) * 8);
+    n_owned = ns ? unique_sorted<uint64_t>(c, s2.as<uint64_t>(), owned.as<uint64_t>(), int64_t(ns)) : 0;
+    vA.release();
+  }
+  // 3. counts -> base; allgather owned tables into vid_of (rank-major, sorted within rank)
+  if (c.world == 1) {
+    counts[0] = n_owned;
+  } else {
+    DevBuf dsz, dmine;
+    dsz.alloc(8 * size_t(c.world));
+    dmine.alloc(8);
+    NBG_HIP(hipMemcpyAsync(dmine.p, &n_owned, 8, hipMemcpyHostToDevice, c.stream));
+    comm_allgather_bytes(c, dmine.p, 8, dsz.p);
+    NBG_HIP(hipMemcpyAsync(counts.data(), dsz.p, 8 * size_t(c.world), hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+  }
+  c.base.assign(size_t(c.world) + 1, 0);
+  for (int r = 0; r < c.world; r++) c.base[size_t(r) + 1] = c.base[size_t(r)] + counts[size_t(r)];
+  c.n_global = c.base[size_t(c.world)];
+  if (c.n_global >= (int64_t(1) << 31)) throw Error(NBG_E_UNSUPPORTED, "more than 2^31 vertices");
+  c.vid_of.alloc(size_t(std::max<int64_t>(c.n_global, 1)) * 8);
+  if (c.world == 1) {
+    if (n_owned) k_unflip<<<grid_for(n_owned), 256, 0, c.stream>>>(owned.as<uint64_t>(), c.vid_of.as<int64_t>(), n_owned);
+  } else {
+    int64_t mx = *std::max_element(counts.begin(), counts.end());
+    DevBuf sendb, recvb;
+    sendb.alloc(size_t(std::max<int64_t>(mx, 1)) * 8);
+    recvb.alloc(size_t(std::max<int64_t>(mx, 1)) * 8 * size_t(c.world));
+    if (n_owned) NBG_HIP(hipMemcpyAsync(sendb.p, owned.p, size_t(n_owned) * 8, hipMemcpyDeviceToDevice, c.stream));
+    comm_allgather_bytes(c, sendb.p, size_t(mx) * 8, recvb.p);
+    for (int r = 0; r < c.world; r++)
+      if (counts[size_t(r)])
+        k_unflip<<<grid_for(counts[size_t(r)]), 256, 0, c.stream>>>(recvb.as<uint64_t>() + size_t(r) * size_t(mx),
+                                                                     c.vid_of.as<int64_t>() + c.base[size_t(r)],
+                                                                     counts[size_t(r)]);
+  }
+  owned.release();
+  // 4. hash table vid -> gidx
+  int64_t cap = 1024;
+  while (cap < 2 * std::max<int64_t>(c.n_global, 1)) cap <<= 1;
+  c.ht_cap = cap;
+  c.ht_keys.alloc(size_t(cap) * 8);
+  c.ht_vals.alloc(size_t(cap) * 4);
+  fill<int64_t>(c, c.ht_keys.as<int64_t>(), INT64_MIN, cap);
+  DevBuf dmin;
+  dmin.alloc(4);
+  int32_t neg = -1;
+  NBG_HIP(hipMemcpyAsync(dmin.p, &neg, 4, hipMemcpyHostToDevice, c.stream));
+  if (c.n_global)
+    k_ht_insert<<<grid_for(c.n_global), 256, 0, c.stream>>>(c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
+                                                           uint64_t(cap - 1), c.vid_of.as<int64_t>(), c.n_global,
+                                                           dmin.as<int32_t>());
+  NBG_HIP(hipMemcpyAsync(&c.ht_min_gidx, dmin.p, 4, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  c.ht_has_min = c.ht_min_gidx >= 0;
+  // 5. bytewise order rank of every vertex (for CSR row order = RocksDB key order)
+  DevBuf brank;
+  {
+    int64_t ng = std::max<int64_t>(c.n_global, 1);
+    DevBuf k1, k2, i1, i2;
+    k1.alloc(size_t(ng) * 8);
+    k2.alloc(size_t(ng) * 8);
+    i1.alloc(size_t(ng) * 4);
+    i2.alloc(size_t(ng) * 4);
+    brank.alloc(size_t(ng) * 4);
+    if (c.n_global) {
+      k_bswap_keys<<<grid_for(c.n_global), 256, 0, c.stream>>>(c.vid_of.as<int64_t>(), k1.as<uint64_t>(), i1.as<uint32_t>(), c.n_global);
+      radix_pairs<uint64_t, uint32_t>(c, k1.as<uint64_t>(), k2.as<uint64_t>(), i1.as<uint32_t>(), i2.as<uint32_t>(), c.n_global, 64);
+      k_scatter_rank<<<grid_for(c.n_global), 256, 0, c.stream>>>(i2.as<uint32_t>(), brank.as<uint32_t>(), c.n_global);
+    }
+  }
+  // 6. CSRs
+  for (auto& kv : c.edges) {
+    EdgeSpace& es = kv.second;
+    build_csr(c, es.out_stage, es.fields, true, es.out, brank.as<uint32_t>());
+    build_csr(c, es.in_stage, es.fields, false, es.in, brank.as<uint32_t>());
+  }
+  c.heap.release();
+  c.heap_used = 0;
+  c.ws_tmp.release();
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  c.finalized = true;
+  c.build_seconds += now_s() - t0;
+}
+
+}  // namespace nbg

@@ -1,0 +1,1341 @@
+// traverse.hip -- the neighbour-expansion hot path on MI355X (gfx950).
+//
+// Replaces, for a whole frontier at once:
+//   * QueryBaseProcessor::collectEdgeProps prefix scan + filter (QueryBaseProcessor.inl:335-405)
+//     -> k_expand: edge-balanced tiles over the frontier's CSR rows;
+//   * GoExecutor::getDstIdsFromResp unordered_set (GoExecutor.cpp:407-431)
+//     -> byte-map marks (plain stores, no atomics) + k_compact (ballot/prefix compaction);
+//   * processFinalResult WHERE / YIELD / DISTINCT (GoExecutor.cpp:585-782)
+//     -> predicate fused into k_expand, k_materialize for YIELD, byte-map or hash DISTINCT.
+//
+// Load balance (power-law degrees): the frontier's degrees are prefix-summed; each 256-thread
+// workgroup takes a fixed tile of 2048 consecutive edges of that flattened space, stages the
+// (<= 2048) frontier entries covering it in LDS, and each lane finds its edge's owner by a
+// binary search in LDS.  Consecutive lanes read consecutive adjacency entries, so the col /
+// prop loads of a tile are coalesced whatever the degree distribution (a supernode simply
+// spans many tiles).
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_reduce.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
+#include <algorithm>
+#include <cmath>
+
+#include "device_common.h"
+#include "engine.h"
+#include "program.h"
+
+namespace nbg {
+
+int32_t compile_expr(const uint8_t* buf, size_t len, const std::vector<Field>& fields, bool graphd,
+                     bool out_bound, Program* out, std::string* msg);
+Program program_dst();
+FastPred classify_pred(const Program& p, const std::vector<Field>& fields);
+
+constexpr int kThreads = 256;
+constexpr int kItems = 8;
+constexpr int kTile = kThreads * kItems;
+
+static int grid_cap(int64_t n, int block = 256, int cap = 256 * 16) {
+  int64_t g = (n + block - 1) / block;
+  return int(std::max<int64_t>(1, std::min<int64_t>(g, cap)));
+}
+
+// ------------------------------------------------------------------------------------------
+// device value model (boost::variant<int64,double,bool,string> + error)
+// ------------------------------------------------------------------------------------------
+struct Val {
+  int64_t b;
+  int32_t t;
+  int32_t len;
+};
+
+struct PropDev {
+  int32_t type;
+  int32_t width;
+  const void* data;
+  const uint8_t* present;
+  const int64_t* str_off;
+  const uint8_t* str_bytes;
+};
+constexpr int kMaxProps = 16;
+struct EvalEnv {
+  PropDev props[kMaxProps];
+  int32_t nprops;
+  int32_t etype;
+  const int64_t* vid_of;
+  const int32_t* col;
+  const int64_t* rank;
+};
+
+__device__ inline int64_t load_int(const void* data, int width, int64_t i) {
+  switch (width) {
+    case 1: return int64_t(static_cast<const int8_t*>(data)[i]);
+    case 2: return int64_t(static_cast<const int16_t*>(data)[i]);
+    case 4: return int64_t(static_cast<const int32_t*>(data)[i]);
+    default: return static_cast<const int64_t*>(data)[i];
+  }
+}
+
+__device__ inline Val load_prop(const PropDev& p, int64_t ge) {
+  Val v;
+  v.len = 0;
+  if (p.present && !p.present[ge]) {
+    v.t = VT_ERR;
+    v.b = 0;
+    return v;
+  }
+  switch (p.type) {
+    case NBG_T_DOUBLE:
+    case NBG_T_FLOAT:
+      v.t = VT_DOUBLE;
+      v.b = static_cast<const int64_t*>(p.data)[ge];
+      break;
+    case NBG_T_BOOL:
+      v.t = VT_BOOL;
+      v.b = load_int(p.data, p.width, ge) != 0;
+      break;
+    case NBG_T_STRING: {
+      int64_t o = p.str_off[ge];
+      v.t = VT_STR;
+      v.b = int64_t(reinterpret_cast<uintptr_t>(p.str_bytes + o));
+      v.len = int32_t(p.str_off[ge + 1] - o);
+      break;
+    }
+    default:
+      v.t = VT_INT;
+      v.b = load_int(p.data, p.width, ge);
+  }
+  return v;
+}
+
+__device__ inline double as_d(const Val& v) { return v.t == VT_INT ? double(v.b) : __longlong_as_double(v.b); }
+__device__ inline bool as_bool(const Val& v) {
+  switch (v.t) {
+    case VT_INT: return v.b != 0;
+    case VT_DOUBLE: return __longlong_as_double(v.b) != 0.0;
+    case VT_BOOL: return v.b != 0;
+    default: return v.len == 0;  // string -> empty() (Expressions.h:172-173)
+  }
+}
+__device__ inline int str_cmp(const Val& a, const Val& b) {
+  const uint8_t* x = reinterpret_cast<const uint8_t*>(uintptr_t(a.b));
+  const uint8_t* y = reinterpret_cast<const uint8_t*>(uintptr_t(b.b));
+  int n = a.len < b.len ? a.len : b.len;
+  for (int i = 0; i < n; i++)
+    if (x[i] != y[i]) return x[i] < y[i] ? -1 : 1;
+  return a.len == b.len ? 0 : (a.len < b.len ? -1 : 1);
+}
+// boost::variant operator< : index first, then value
+__device__ inline bool v_lt(const Val& a, const Val& b) {
+  if (a.t != b.t) return a.t < b.t;
+  switch (a.t) {
+    case VT_INT: return a.b < b.b;
+    case VT_DOUBLE: return __longlong_as_double(a.b) < __longlong_as_double(b.b);
+    case VT_BOOL: return a.b < b.b;
+    default: return str_cmp(a, b) < 0;
+  }
+}
+__device__ inline bool v_eq(const Val& a, const Val& b) {
+  if (a.t != b.t) return false;
+  switch (a.t) {
+    case VT_INT:
+    case VT_BOOL: return a.b == b.b;
+    case VT_DOUBLE: return __longlong_as_double(a.b) == __longlong_as_double(b.b);
+    default: return str_cmp(a, b) == 0;
+  }
+}
+__device__ inline Val mk(int32_t t, int64_t b) {
+  Val v;
+  v.t = t;
+  v.b = b;
+  v.len = 0;
+  return v;
+}
+__device__ inline Val mkd(double d) { return mk(VT_DOUBLE, __double_as_longlong(d)); }
+
+__device__ Val eval_program(const Program* __restrict__ P, const EvalEnv& env, int64_t ge, int32_t src_g,
+                            int32_t dst_g) {
+  Val st[kMaxStack];
+  int sp = 0;
+  const int n = P->n;
+  for (int pc = 0; pc < n; pc++) {
+    Ins in = P->ins[pc];
+    switch (in.op) {
+      case P_CONST: {
+        Val v;
+        v.t = P->ctype[in.arg];
+        v.b = P->cbits[in.arg];
+        v.len = P->clen[in.arg];
+        if (v.t == VT_STR) v.b = int64_t(reinterpret_cast<uintptr_t>(P->cstr + P->cbits[in.arg]));
+        st[sp++] = v;
+        break;
+      }
+      case P_PROP: st[sp++] = load_prop(env.props[in.arg], ge); break;
+      case P_DST: st[sp++] = mk(VT_INT, env.vid_of[dst_g]); break;
+      case P_SRC: st[sp++] = mk(VT_INT, env.vid_of[src_g]); break;
+      case P_RANK: st[sp++] = mk(VT_INT, env.rank ? env.rank[ge] : 0); break;
+      case P_TYPE: st[sp++] = mk(VT_INT, env.etype); break;
+      case P_UNARY: {
+        Val& a = st[sp - 1];
+        if (a.t == VT_ERR) break;
+        if (in.sub == 0) break;  // PLUS
+        if (in.sub == 1) {       // NEGATE
+          if (a.t == VT_INT) a.b = int64_t(0ull - uint64_t(a.b));
+          else if (a.t == VT_DOUBLE) a.b = __double_as_longlong(-__longlong_as_double(a.b));
+          else a.t = VT_ERR;
+        } else {
+          a = mk(VT_BOOL, !as_bool(a));
+        }
+        break;
+      }
+      case P_ARITH: {
+        Val r = st[--sp];
+        Val l = st[sp - 1];
+        Val o;
+        if (l.t == VT_ERR) o = l;
+        else if (r.t == VT_ERR) o = r;
+        else {
+          bool ar = (l.t == VT_INT || l.t == VT_DOUBLE) && (r.t == VT_INT || r.t == VT_DOUBLE);
+          bool dbl = l.t == VT_DOUBLE || r.t == VT_DOUBLE;
+          o = mk(VT_ERR, 0);
+          switch (in.sub) {
+            case 0:
+              if (ar) o = dbl ? mkd(as_d(l) + as_d(r)) : mk(VT_INT, int64_t(uint64_t(l.b) + uint64_t(r.b)));
+              break;
+            case 1:
+              if (ar) o = dbl ? mkd(as_d(l) - as_d(r)) : mk(VT_INT, int64_t(uint64_t(l.b) - uint64_t(r.b)));
+              break;
+            case 2:
+              if (ar) o = dbl ? mkd(as_d(l) * as_d(r)) : mk(VT_INT, int64_t(uint64_t(l.b) * uint64_t(r.b)));
+              break;
+            case 3:
+              if (ar) {
+                if (dbl) o = mkd(as_d(l) / as_d(r));
+                else if (r.b == 0) o = mk(VT_ERR, 0);
+                else if (r.b == -1) o = mk(VT_INT, int64_t(0ull - uint64_t(l.b)));
+                else o = mk(VT_INT, l.b / r.b);
+              }
+              break;
+            default:
+              if (l.t == VT_INT && r.t == VT_INT) {
+                if (r.b == 0) o = mk(VT_ERR, 0);
+                else if (r.b == -1) o = mk(VT_INT, 0);
+                else o = mk(VT_INT, l.b % r.b);
+              }
+          }
+        }
+        st[sp - 1] = o;
+        break;
+      }
+      case P_REL: {
+        Val r = st[--sp];
+        Val l = st[sp - 1];
+        Val o;
+        if (l.t == VT_ERR) o = l;
+        else if (r.t == VT_ERR) o = r;
+        else {
+          bool res;
+          bool mixed = (l.t == VT_INT || l.t == VT_DOUBLE) && (r.t == VT_INT || r.t == VT_DOUBLE) &&
+                       (l.t == VT_DOUBLE || r.t == VT_DOUBLE);
+          switch (in.sub) {
+            case 0: res = v_lt(l, r); break;
+            case 1: res = !v_lt(r, l); break;
+            case 2: res = v_lt(r, l); break;
+            case 3: res = !v_lt(l, r); break;
+            case 4: res = mixed ? fabs(as_d(l) - as_d(r)) < 1e-8 : v_eq(l, r); break;
+            default: res = mixed ? !(fabs(as_d(l) - as_d(r)) < 1e-8) : !v_eq(l, r); break;
+          }
+          o = mk(VT_BOOL, res);
+        }
+        st[sp - 1] = o;
+        break;
+      }
+      case P_LOGIC: {
+        Val r = st[--sp];
+        Val l = st[sp - 1];
+        Val o;
+        if (l.t == VT_ERR) o = l;
+        else if (r.t == VT_ERR) o = r;
+        else if (in.sub == 0) o = mk(VT_BOOL, as_bool(l) ? as_bool(r) : false);
+        else o = mk(VT_BOOL, as_bool(l) ? true : as_bool(r));
+        st[sp - 1] = o;
+        break;
+      }
+    }
+  }
+  return st[0];
+}
+
+// ------------------------------------------------------------------------------------------
+// expansion
+// ------------------------------------------------------------------------------------------
+enum ExpMode : int { EXP_MARK = 0, EXP_ROWS = 1, EXP_FLAGS = 2 };
+enum PredKind : int { PK_NONE = 0, PK_FAST = 1, PK_VM = 2 };
+
+struct ExpandArgs {
+  const int32_t* F;
+  int64_t nF;
+  const int64_t* off;      // exclusive degree scan, off[nF] = total edges
+  const int64_t* row_ptr;
+  const int32_t* col;
+  int64_t lo;              // gidx of local row 0
+  uint8_t* map;            // EXP_MARK
+  int32_t* rows_src;       // EXP_ROWS: local row index
+  int64_t* rows_edge;      //           global edge index into the CSR
+  unsigned long long* rows_cnt;
+  uint8_t* flags;          // EXP_FLAGS: one byte per flattened edge slot
+  unsigned long long* err; // eval errors (GO semantics)
+  int32_t storage;         // 1: eval error keeps the edge (QueryBaseProcessor.inl:391-396)
+  int32_t mark_check;      // read the byte before storing it
+};
+struct FastArgs {
+  const void* data;
+  const uint8_t* present;
+  int32_t width;
+  int32_t op;
+  int64_t k;
+};
+
+__device__ inline bool fast_cmp(int op, int64_t a, int64_t k) {
+  switch (op) {
+    case 0: return a < k;
+    case 1: return a <= k;
+    case 2: return a > k;
+    case 3: return a >= k;
+    case 4: return a == k;
+    default: return a != k;
+  }
+}
+
+template <int MODE, int PK>
+__global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, const Program* __restrict__ prog,
+                                                     EvalEnv env) {
+  __shared__ int32_t s_off[kTile + 1];  // off[k] - e0 (fits: tile-relative)
+  __shared__ int64_t s_rs[kTile];       // row_ptr[F[k]] - off[k]
+  __shared__ int32_t s_src[kTile];      // F[k]
+  __shared__ int64_t s_hdr[2];
+  const int64_t nF = a.nF;
+  const int64_t E = a.off[nF];
+  const int64_t ntiles = (E + kTile - 1) / kTile;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t e0 = t * kTile;
+    const int64_t e1 = min(e0 + int64_t(kTile), E);
+    if (threadIdx.x == 0) {
+      // i0 = last k with off[k] <= e0 ; i1 = last k with off[k] <= e1 - 1
+      int64_t lo = 0, hi = nF;  // off[lo] <= e0 < off[hi] invariant (off[0] = 0, off[nF] = E)
+      while (hi - lo > 1) {
+        int64_t mid = (lo + hi) >> 1;
+        if (a.off[mid] <= e0) lo = mid; else hi = mid;
+      }
+      int64_t i0 = lo;
+      lo = i0;
+      hi = nF;
+      while (hi - lo > 1) {
+        int64_t mid = (lo + hi) >> 1;
+        if (a.off[mid] <= e1 - 1) lo = mid; else hi = mid;
+      }
+      s_hdr[0] = i0;
+      s_hdr[1] = lo - i0 + 1;
+    }
+    __syncthreads();
+    const int64_t i0 = s_hdr[0];
+    const int cnt = int(s_hdr[1]);
+    for (int k = threadIdx.x; k <= cnt; k += kThreads) {
+      int64_t o = a.off[i0 + k];
+      s_off[k] = int32_t(min(o - e0, int64_t(kTile + 1)));
+      if (k < cnt) {
+        int32_t f = a.F[i0 + k];
+        s_src[k] = f;
+        s_rs[k] = a.row_ptr[f] - o;
+      }
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int r = 0; r < kItems; r++) {
+      const int j = threadIdx.x + r * kThreads;
+      const int64_t e = e0 + j;
+      const bool valid = e < e1;
+      int k = 0;
+      if (valid) {
+        int lo = 0, hi = cnt;  // s_off[lo] <= j < s_off[hi]
+        while (hi - lo > 1) {
+          int mid = (lo + hi) >> 1;
+          if (s_off[mid] <= j) lo = mid; else hi = mid;
+        }
+        k = lo;
+      }
+      const int64_t ge = valid ? s_rs[k] + e : 0;
+      bool pass = valid;
+      int32_t d = 0;
+      if (valid && (MODE != EXP_FLAGS || PK == PK_VM)) d = a.col[ge];
+      if (PK == PK_FAST && valid) {
+        if (fp.present && !fp.present[ge]) {
+          if (a.storage) pass = true;
+          else {
+            atomicAdd(a.err, 1ull);
+            pass = false;
+          }
+        } else {
+          pass = fast_cmp(fp.op, load_int(fp.data, fp.width, ge), fp.k);
+        }
+      } else if (PK == PK_VM && valid) {
+        Val v = eval_program(prog, env, ge, int32_t(a.lo) + s_src[k], d);
+        if (v.t == VT_ERR) {
+          if (a.storage) pass = true;
+          else {
+            atomicAdd(a.err, 1ull);
+            pass = false;
+          }
+        } else {
+          pass = as_bool(v);
+        }
+      }
+      if (MODE == EXP_MARK) {
+        if (pass) {
+          if (a.mark_check) {
+            if (a.map[d] == 0) a.map[d] = 1;
+          } else {
+            a.map[d] = 1;
+          }
+        }
+      } else if (MODE == EXP_ROWS) {
+        int64_t slot = wave_append(a.rows_cnt, pass);
+        if (pass) {
+          a.rows_src[slot] = s_src[k];
+          a.rows_edge[slot] = ge;
+        }
+      } else {
+        if (valid) a.flags[e] = pass;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// deg[i] = outdeg(F[i]); deg[nF] = 0
+__global__ void k_degrees(const int32_t* F, int64_t nF, const int64_t* row_ptr, int64_t* deg) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= nF; i += int64_t(gridDim.x) * blockDim.x) {
+    if (i == nF) {
+      deg[i] = 0;
+    } else {
+      int32_t f = F[i];
+      deg[i] = row_ptr[f + 1] - row_ptr[f];
+    }
+  }
+}
+
+// wave-wide exclusive prefix sum of a per-lane count
+__device__ inline uint32_t wave_excl_scan(uint32_t x, uint32_t& total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t v = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(v, o);
+    if (lane >= o) v += y;
+  }
+  total = __shfl(v, 63);
+  return v - x;
+}
+
+// Compact the owned slice [lo, lo+n) of the byte-map into a frontier list of local indices,
+// clearing it.  require_deg: drop vertices without out-edges (they cannot produce rows).
+// n_set counts every set byte (the reference's "starts_ non-empty" test, GoExecutor.cpp:392).
+__global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64_t n, const int64_t* row_ptr,
+                                                 const uint8_t* row_ok, int require_deg, int32_t* out,
+                                                 unsigned long long* n_out, unsigned long long* n_set) {
+  const int64_t nchunks = (n + 15) / 16;
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int64_t rounds = (nchunks + stride - 1) / stride;
+  const int lane = threadIdx.x & 63;
+  for (int64_t rr = 0; rr < rounds; rr++) {
+    const int64_t ch = rr * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    uint4 w = make_uint4(0, 0, 0, 0);
+    if (ch < nchunks) w = reinterpret_cast<const uint4*>(map + lo)[ch];
+    uint32_t words[4] = {w.x, w.y, w.z, w.w};
+    uint32_t setmask = 0;  // bit j = byte j set
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        if ((words[q] >> (8 * b)) & 0xff) setmask |= 1u << (q * 4 + b);
+    uint32_t keepmask = setmask;
+    if (require_deg && setmask) {
+      for (uint32_t m = setmask; m; m &= m - 1) {
+        int j = __ffs(m) - 1;
+        int64_t v = ch * 16 + j;
+        if (row_ptr[v + 1] == row_ptr[v] || (row_ok && !row_ok[v])) keepmask &= ~(1u << j);
+      }
+    }
+    uint32_t tot_set, tot_keep;
+    wave_excl_scan(__popc(setmask), tot_set);
+    uint32_t pre = wave_excl_scan(__popc(keepmask), tot_keep);
+    unsigned long long base = 0;
+    if (lane == 0) {
+      if (tot_set) atomicAdd(n_set, (unsigned long long)tot_set);
+      if (tot_keep) base = atomicAdd(n_out, (unsigned long long)tot_keep);
+    }
+    base = __shfl(base, 0);
+    uint32_t p = uint32_t(base) + pre;
+    for (uint32_t m = keepmask; m; m &= m - 1) {
+      int j = __ffs(m) - 1;
+      out[p++] = int32_t(ch * 16 + j);
+    }
+    if (setmask) reinterpret_cast<uint4*>(map + lo)[ch] = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// starts (gidx) -> mark owned in the byte-map (dedup path) or list them (steps == 1 path)
+__global__ void k_mark_gidx(const int32_t* g, int64_t n, int64_t lo, int64_t hi, uint8_t* map) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    int32_t x = g[i];
+    if (x >= lo && x < hi) map[x] = 1;
+  }
+}
+__global__ void k_list_starts(const int32_t* g, int64_t n, int64_t lo, int64_t hi, const int64_t* row_ptr,
+                              const uint8_t* row_ok, int32_t* out, unsigned long long* n_out) {
+  // order-preserving is not required (multiset results); wave-aggregated append
+  int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  int64_t rounds = (n + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    bool keep = false;
+    int32_t loc = 0;
+    if (i < n) {
+      int32_t x = g[i];
+      if (x >= lo && x < hi) {
+        loc = int32_t(x - lo);
+        keep = row_ptr[loc + 1] > row_ptr[loc] && (row_ok == nullptr || row_ok[loc]);
+      }
+    }
+    int64_t s = wave_append(n_out, keep);
+    if (keep) out[s] = loc;
+  }
+}
+
+// gidx list (local indices + lo) -> vids
+__global__ void k_local_to_vid(const int32_t* loc, int64_t n, int64_t lo, const int64_t* vid_of, int64_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = vid_of[lo + loc[i]];
+}
+
+// YIELD materialisation: one program per output column
+struct ColOut {
+  void* data;
+  int32_t type;  // VT_*
+};
+constexpr int kMaxYields = 16;
+struct YieldArgs {
+  int32_t ncols;
+  ColOut cols[kMaxYields];
+};
+__global__ void k_materialize(const int32_t* rows_src, const int64_t* rows_edge, int64_t n, const Program* progs,
+                              YieldArgs ya, EvalEnv env, int64_t lo, unsigned long long* err) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t ge = rows_edge[i];
+    const int32_t sg = int32_t(lo) + rows_src[i];
+    const int32_t dg = env.col[ge];
+    for (int c = 0; c < ya.ncols; c++) {
+      Val v = eval_program(progs + c, env, ge, sg, dg);
+      if (v.t == VT_ERR || v.t != ya.cols[c].type) {
+        atomicAdd(err, 1ull);
+        continue;
+      }
+      if (v.t == VT_BOOL) static_cast<uint8_t*>(ya.cols[c].data)[i] = uint8_t(v.b != 0);
+      else static_cast<int64_t*>(ya.cols[c].data)[i] = v.b;
+    }
+  }
+}
+// fast path for YIELD e._dst (the default YIELD)
+__global__ void k_yield_dst(const int64_t* rows_edge, int64_t n, const int32_t* col, const int64_t* vid_of,
+                            int64_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = vid_of[col[rows_edge[i]]];
+}
+
+// DISTINCT over materialised rows (GoExecutor.cpp:638-646 dedups by encoded row bytes; for the
+// fixed-width VID/DOUBLE/BOOL columns the engine emits, equal bytes == equal 64-bit words).
+__device__ inline uint64_t row_hash(const YieldArgs& ya, int64_t i) {
+  uint64_t h = 0x12345678ull;
+  for (int c = 0; c < ya.ncols; c++) {
+    uint64_t w = ya.cols[c].type == VT_BOOL ? static_cast<const uint8_t*>(ya.cols[c].data)[i]
+                                            : uint64_t(static_cast<const int64_t*>(ya.cols[c].data)[i]);
+    h = splitmix64(h ^ w);
+  }
+  return h;
+}
+__device__ inline bool row_eq(const YieldArgs& ya, int64_t i, int64_t j) {
+  for (int c = 0; c < ya.ncols; c++) {
+    if (ya.cols[c].type == VT_BOOL) {
+      if (static_cast<const uint8_t*>(ya.cols[c].data)[i] != static_cast<const uint8_t*>(ya.cols[c].data)[j]) return false;
+    } else if (static_cast<const int64_t*>(ya.cols[c].data)[i] != static_cast<const int64_t*>(ya.cols[c].data)[j]) {
+      return false;
+    }
+  }
+  return true;
+}
+__global__ void k_row_dedup(YieldArgs ya, int64_t n, long long* table, uint64_t mask, uint8_t* keep) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    uint64_t h = row_hash(ya, i) & mask;
+    bool k = true;
+    while (true) {
+      long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(table + h), ~0ull, (unsigned long long)i);
+      if (prev == -1) break;
+      if (row_eq(ya, prev, i)) {
+        k = false;
+        break;
+      }
+      h = (h + 1) & mask;
+    }
+    keep[i] = k;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host drivers
+// ------------------------------------------------------------------------------------------
+namespace {
+
+struct HostRows {
+  std::vector<int32_t> types;
+  std::vector<void*> cols;
+  std::vector<int64_t*> str_off;
+  std::vector<DevBuf> dev;       // device column storage when on_device
+  std::vector<std::vector<uint8_t>> host;
+  std::vector<std::vector<int64_t>> host_off;
+  std::vector<int64_t> row_vertex, vertex_ids, vertex_row_offsets;
+  std::vector<int32_t> failed_parts, failed_codes;
+};
+
+void fill_rows(nbg_rows* out, HostRows* h, int64_t nrows, bool on_device) {
+  memset(out, 0, sizeof(*out));
+  out->n_rows = nrows;
+  out->n_cols = int32_t(h->types.size());
+  out->on_device = on_device ? 1 : 0;
+  out->col_types = h->types.data();
+  out->cols = h->cols.data();
+  out->str_offsets = h->str_off.data();
+  out->row_vertex = h->row_vertex.empty() ? nullptr : h->row_vertex.data();
+  out->n_vertices = int64_t(h->vertex_ids.size());
+  out->vertex_ids = h->vertex_ids.empty() ? nullptr : h->vertex_ids.data();
+  out->vertex_row_offsets = h->vertex_row_offsets.empty() ? nullptr : h->vertex_row_offsets.data();
+  out->n_failed = int32_t(h->failed_parts.size());
+  out->failed_parts = h->failed_parts.empty() ? nullptr : h->failed_parts.data();
+  out->failed_codes = h->failed_codes.empty() ? nullptr : h->failed_codes.data();
+  out->_impl = h;
+}
+
+EvalEnv make_env(Ctx& c, EdgeSpace& es, const Csr& csr, int32_t etype) {
+  EvalEnv env{};
+  env.nprops = int32_t(std::min<size_t>(csr.props.size(), kMaxProps));
+  for (int i = 0; i < env.nprops; i++) {
+    const PropCol& p = csr.props[size_t(i)];
+    env.props[i] = PropDev{p.type, p.width, p.data.p, p.present.as<uint8_t>(), p.str_off.as<int64_t>(),
+                           p.str_bytes.as<uint8_t>()};
+  }
+  env.etype = etype;
+  env.vid_of = c.vid_of.as<int64_t>();
+  env.col = csr.col.as<int32_t>();
+  env.rank = csr.rank.as<int64_t>();
+  return env;
+}
+
+template <typename T>
+void exclusive_scan_dev(Ctx& c, const T* in, T* out, int64_t n) {
+  size_t tb = 0;
+  NBG_HIP(rocprim::exclusive_scan(nullptr, tb, in, out, T(0), size_t(n), rocprim::plus<T>(), c.stream));
+  c.ws_tmp.ensure(tb);
+  NBG_HIP(rocprim::exclusive_scan(c.ws_tmp.p, tb, in, out, T(0), size_t(n), rocprim::plus<T>(), c.stream));
+}
+
+struct Counters {
+  unsigned long long* d;
+  unsigned long long h[8];
+};
+
+int64_t map_bytes(const Ctx& c) { return ((c.n_global + 63) / 64) * 64 + 64; }
+
+void ensure_workspaces(Ctx& c, int64_t nF_cap) {
+  int64_t mb = map_bytes(c);
+  if (c.ws_map.bytes < size_t(mb)) {
+    c.ws_map.alloc(size_t(mb));
+    NBG_HIP(hipMemsetAsync(c.ws_map.p, 0, size_t(mb), c.stream));
+  }
+  c.ws_front[0].ensure(size_t(nF_cap + 64) * 4);
+  c.ws_front[1].ensure(size_t(nF_cap + 64) * 4);
+  c.ws_off.ensure(size_t(nF_cap + 2) * 8);
+  c.ws_counters.ensure(256);
+}
+
+// frontier degree scan: fills c.ws_off[0..nF] and returns total edges (synchronises)
+int64_t degree_scan(Ctx& c, const int32_t* F, int64_t nF, const Csr& csr, DevBuf& degbuf) {
+  degbuf.ensure(size_t(nF + 1) * 8);
+  k_degrees<<<grid_cap(nF + 1), 256, 0, c.stream>>>(F, nF, csr.row_ptr.as<int64_t>(), degbuf.as<int64_t>());
+  exclusive_scan_dev<int64_t>(c, degbuf.as<int64_t>(), c.ws_off.as<int64_t>(), nF + 1);
+  int64_t E = 0;
+  NBG_HIP(hipMemcpyAsync(&E, c.ws_off.as<int64_t>() + nF, 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  return E;
+}
+
+template <int MODE>
+void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Program* dprog, const EvalEnv& env,
+                   int64_t E) {
+  int64_t ntiles = (E + kTile - 1) / kTile;
+  int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, int64_t(c.opt("expand_grid", 256 * 8)))));
+  hipEventRecord(c.ev[2], c.stream);
+  switch (pk) {
+    case PK_NONE: k_expand<MODE, PK_NONE><<<grid, kThreads, 0, c.stream>>>(a, fp, dprog, env); break;
+    case PK_FAST: k_expand<MODE, PK_FAST><<<grid, kThreads, 0, c.stream>>>(a, fp, dprog, env); break;
+    default: k_expand<MODE, PK_VM><<<grid, kThreads, 0, c.stream>>>(a, fp, dprog, env); break;
+  }
+  NBG_HIP(hipGetLastError());
+  hipEventRecord(c.ev[3], c.stream);
+  NBG_HIP(hipEventSynchronize(c.ev[3]));
+  float ms = 0;
+  hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
+  c.timing.expand_ms += ms;
+  c.timing.expand_launches++;
+}
+
+// algorithmic bytes of one expansion (DESIGN.md "byte model"): frontier id 4 B + row_ptr pair
+// 16 B + off 8 B per frontier entry; per edge: col 4 B (+ predicate column width) + the
+// output it makes (1 B map mark, or 12 B row, or 1 B flag).
+uint64_t expand_bytes(int64_t nF, int64_t E, int pred_width, int mode) {
+  uint64_t b = uint64_t(nF) * 28 + uint64_t(E) * (4 + uint64_t(pred_width));
+  b += uint64_t(E) * (mode == EXP_ROWS ? 0 : 1);
+  return b;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// GO N STEPS
+// ------------------------------------------------------------------------------------------
+int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
+  if (!c.finalized) throw Error(NBG_E_STATE, "snapshot not finalized");
+  if (s.steps < 1) throw Error(NBG_E_INVALID_ARG, "steps must be >= 1");
+  if (s.edge_type <= 0) throw Error(NBG_E_INVALID_ARG, "GO ... REVERSELY is not supported (GoExecutor.cpp:203-205)");
+  auto it = c.edges.find(s.edge_type);
+  if (it == c.edges.end()) throw Error(NBG_E_INVALID_ARG, "edge type not in snapshot");
+  EdgeSpace& es = it->second;
+  Csr& csr = es.out;
+  c.timing = Timing{};
+  hipEventRecord(c.ev[0], c.stream);
+
+  // compile WHERE / YIELD (errors are deferred to the final step, as the reference only
+  // reports them when the final getNeighbors request is actually sent)
+  Program where{};
+  bool has_where = s.where_len > 0;
+  std::string msg;
+  int32_t deferred = NBG_OK;
+  std::string deferred_msg;
+  if (has_where) {
+    int32_t rc = compile_expr(s.where, s.where_len, es.fields, true, true, &where, &msg);
+    if (rc == NBG_E_UNSUPPORTED || rc == NBG_E_INVALID_ARG) throw Error(rc, "WHERE: " + msg);
+    if (rc != NBG_OK) {
+      deferred = rc;
+      deferred_msg = "WHERE: " + msg;
+    }
+  }
+  std::vector<Program> yields;
+  bool default_yield = s.n_yields == 0;
+  if (default_yield) {
+    yields.push_back(program_dst());
+  } else {
+    if (s.n_yields > size_t(kMaxYields)) throw Error(NBG_E_UNSUPPORTED, "too many YIELD columns");
+    for (size_t i = 0; i < s.n_yields; i++) {
+      Program p{};
+      int32_t rc = compile_expr(s.yields[i], s.yield_lens[i], es.fields, true, true, &p, &msg);
+      if (rc == NBG_E_UNSUPPORTED || rc == NBG_E_INVALID_ARG) throw Error(rc, "YIELD: " + msg);
+      if (rc != NBG_OK && deferred == NBG_OK) {
+        deferred = rc;
+        deferred_msg = "YIELD: " + msg;
+      }
+      if (rc == NBG_OK && p.result_type == VT_STR) throw Error(NBG_E_UNSUPPORTED, "STRING YIELD columns");
+      yields.push_back(p);
+    }
+  }
+  const int64_t lo = c.owned_lo(), hi = c.owned_hi();
+  const int64_t n_own = hi - lo;
+  ensure_workspaces(c, std::max<int64_t>({n_own, int64_t(s.n_starts), 1}));
+  Counters K{c.ws_counters.as<unsigned long long>(), {}};
+  DevBuf degbuf;
+  uint8_t* map = c.ws_map.as<uint8_t>();
+  const int64_t* row_ptr = csr.row_ptr.as<int64_t>();
+  const uint8_t* row_ok = csr.row_ok.as<uint8_t>();  // rows whose keys sit outside hash(vid)'s part
+
+  // starts -> gidx
+  int64_t ns = int64_t(s.n_starts);
+  c.ws_starts.ensure(size_t(std::max<int64_t>(ns, 1)) * 12 + 64);
+  int64_t* d_starts = c.ws_starts.as<int64_t>();
+  int32_t* d_sg = reinterpret_cast<int32_t*>(d_starts + std::max<int64_t>(ns, 1));
+  if (ns) {
+    NBG_HIP(hipMemcpyAsync(d_starts, s.starts, size_t(ns) * 8, hipMemcpyHostToDevice, c.stream));
+    lookup_gidx(c, d_starts, d_sg, ns);
+  }
+  int cur = 0;
+  int32_t* F = c.ws_front[0].as<int32_t>();
+  int64_t nF = 0;
+  int64_t nset_global = ns;  // "starts_ non-empty" (GoExecutor.cpp:93-97)
+  NBG_HIP(hipMemsetAsync(K.d, 0, 64, c.stream));
+  if (ns) {
+    if (s.steps == 1 && !s.distinct) {
+      k_list_starts<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, F, K.d);
+    } else {
+      k_mark_gidx<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, map);
+      k_compact<<<grid_cap((n_own + 15) / 16), 256, 0, c.stream>>>(map, lo, n_own, row_ptr, row_ok, 1, F, K.d, K.d + 1);
+    }
+    NBG_HIP(hipGetLastError());
+    NBG_HIP(hipMemcpyAsync(K.h, K.d, 16, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    nF = int64_t(K.h[0]);
+  }
+  if (c.world > 1) {
+    // frontier emptiness is global
+    throw Error(NBG_E_UNSUPPORTED, "multi-GPU GO is built in the comm path (see go_run_dist)");
+  }
+  auto finish_empty = [&]() -> int32_t {
+    auto* h = new HostRows();
+    for (auto& p : yields) {
+      h->types.push_back(p.result_type == VT_DOUBLE ? NBG_T_DOUBLE : p.result_type == VT_BOOL ? NBG_T_BOOL : NBG_T_VID);
+      h->cols.push_back(nullptr);
+      h->str_off.push_back(nullptr);
+    }
+    fill_rows(out, h, 0, s.keep_on_device != 0);
+    hipEventRecord(c.ev[1], c.stream);
+    hipEventSynchronize(c.ev[1]);
+    float ms = 0;
+    hipEventElapsedTime(&ms, c.ev[0], c.ev[1]);
+    c.timing.total_ms = ms;
+    out->edges_scanned = c.timing.edges_scanned;
+    return NBG_OK;
+  };
+  if (nset_global == 0) return finish_empty();
+
+  ExpandArgs a{};
+  a.row_ptr = row_ptr;
+  a.col = csr.col.as<int32_t>();
+  a.lo = lo;
+  a.map = map;
+  a.err = K.d + 4;
+  a.storage = 0;
+  a.mark_check = int32_t(c.opt("mark_check", 0));
+  FastArgs fp{};
+  EvalEnv env = make_env(c, es, csr, s.edge_type);
+
+  for (int32_t step = 1; step < s.steps; step++) {
+    c.timing.steps_run++;
+    int64_t E = nF ? degree_scan(c, F, nF, csr, degbuf) : 0;
+    c.timing.edges_scanned += uint64_t(E);
+    if (E > 0) {
+      a.F = F;
+      a.nF = nF;
+      a.off = c.ws_off.as<int64_t>();
+      launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, E);
+      c.timing.expand_bytes += expand_bytes(nF, E, 0, EXP_MARK);
+    }
+    // next frontier = set of dsts (P12), compacted and deg-0 vertices dropped
+    cur ^= 1;
+    F = c.ws_front[cur].as<int32_t>();
+    NBG_HIP(hipMemsetAsync(K.d, 0, 16, c.stream));
+    k_compact<<<grid_cap((n_own + 15) / 16), 256, 0, c.stream>>>(map, lo, n_own, row_ptr, row_ok, 1, F, K.d, K.d + 1);
+    NBG_HIP(hipGetLastError());
+    NBG_HIP(hipMemcpyAsync(K.h, K.d, 16, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    nF = int64_t(K.h[0]);
+    nset_global = int64_t(K.h[1]);
+    if (nset_global == 0) return finish_empty();  // onEmptyInputs (GoExecutor.cpp:392-395)
+  }
+  // ---- final step ----
+  c.timing.steps_run++;
+  if (deferred != NBG_OK) throw Error(deferred, deferred_msg);
+  FastPred fpk = has_where ? classify_pred(where, es.fields) : FastPred{};
+  int pk = fpk.kind;
+  if (pk == PK_FAST) {
+    const PropCol& pc = csr.props[size_t(fpk.col)];
+    fp = FastArgs{pc.data.p, pc.present.as<uint8_t>(), pc.width, fpk.op, fpk.k};
+  }
+  DevBuf dprog;
+  if (pk == PK_VM || !default_yield) {
+    dprog.alloc(sizeof(Program) * (yields.size() + 1));
+    NBG_HIP(hipMemcpyAsync(dprog.p, &where, sizeof(Program), hipMemcpyHostToDevice, c.stream));
+    NBG_HIP(hipMemcpyAsync(dprog.as<Program>() + 1, yields.data(), sizeof(Program) * yields.size(),
+                           hipMemcpyHostToDevice, c.stream));
+  }
+  int pred_w = pk == PK_FAST ? fp.width : 0;
+  int64_t E = nF ? degree_scan(c, F, nF, csr, degbuf) : 0;
+  c.timing.edges_scanned += uint64_t(E);
+  a.F = F;
+  a.nF = nF;
+  a.off = c.ws_off.as<int64_t>();
+  bool distinct_dst = s.distinct && yields.size() == 1 && yields[0].n == 1 && yields[0].ins[0].op == P_DST;
+  auto* h = new HostRows();
+  int64_t nrows = 0;
+  try {
+    if (distinct_dst) {
+      // DISTINCT e._dst: mark surviving dsts, compact the whole vertex space (no deg filter)
+      if (E > 0) {
+        launch_expand<EXP_MARK>(c, a, pk, fp, dprog.as<Program>(), env, E);
+        c.timing.expand_bytes += expand_bytes(nF, E, pred_w, EXP_MARK);
+      }
+      DevBuf lst;
+      lst.alloc(size_t(c.n_global + 64) * 4);
+      NBG_HIP(hipMemsetAsync(K.d, 0, 48, c.stream));
+      k_compact<<<grid_cap((c.n_global + 15) / 16), 256, 0, c.stream>>>(map, 0, c.n_global, row_ptr, nullptr, 0,
+                                                                       lst.as<int32_t>(), K.d, K.d + 1);
+      NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      if (K.h[4]) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
+      nrows = int64_t(K.h[0]);
+      DevBuf vids;
+      vids.alloc(size_t(nrows + 1) * 8);
+      if (nrows)
+        k_local_to_vid<<<grid_cap(nrows), 256, 0, c.stream>>>(lst.as<int32_t>(), nrows, 0, c.vid_of.as<int64_t>(),
+                                                             vids.as<int64_t>());
+      h->types.push_back(NBG_T_VID);
+      h->dev.push_back(std::move(vids));
+    } else {
+      // rows (src, edge) passing WHERE
+      c.ws_rows.ensure(size_t(E + 64) * 12);
+      int64_t* rows_edge = c.ws_rows.as<int64_t>();
+      int32_t* rows_src = reinterpret_cast<int32_t*>(rows_edge + E + 32);
+      a.rows_edge = rows_edge;
+      a.rows_src = rows_src;
+      a.rows_cnt = K.d + 2;
+      NBG_HIP(hipMemsetAsync(K.d, 0, 48, c.stream));
+      if (E > 0) {
+        launch_expand<EXP_ROWS>(c, a, pk, fp, dprog.as<Program>(), env, E);
+        c.timing.expand_bytes += expand_bytes(nF, E, pred_w, EXP_ROWS);
+      }
+      NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      if (K.h[4]) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
+      nrows = int64_t(K.h[2]);
+      c.timing.expand_bytes += uint64_t(nrows) * 12;
+      YieldArgs ya{};
+      ya.ncols = int32_t(yields.size());
+      for (auto& p : yields) {
+        int32_t t = p.result_type;
+        DevBuf b;
+        b.alloc(size_t(nrows + 1) * (t == VT_BOOL ? 1 : 8));
+        ya.cols[h->types.size()] = ColOut{b.p, t};
+        h->types.push_back(t == VT_DOUBLE ? NBG_T_DOUBLE : t == VT_BOOL ? NBG_T_BOOL : NBG_T_VID);
+        h->dev.push_back(std::move(b));
+      }
+      if (nrows) {
+        if (default_yield) {
+          k_yield_dst<<<grid_cap(nrows), 256, 0, c.stream>>>(rows_edge, nrows, csr.col.as<int32_t>(),
+                                                             c.vid_of.as<int64_t>(), h->dev[0].as<int64_t>());
+        } else {
+          k_materialize<<<grid_cap(nrows), 256, 0, c.stream>>>(rows_src, rows_edge, nrows, dprog.as<Program>() + 1, ya,
+                                                               env, lo, K.d + 5);
+        }
+        NBG_HIP(hipGetLastError());
+        NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipStreamSynchronize(c.stream));
+        if (K.h[5]) throw Error(NBG_E_EVAL, "YIELD evaluation failed");
+      }
+      if (s.distinct && nrows) {
+        uint64_t cap = 1024;
+        while (cap < uint64_t(2 * nrows)) cap <<= 1;
+        DevBuf table, keep, idx, cnt;
+        table.alloc(cap * 8);
+        NBG_HIP(hipMemsetAsync(table.p, 0xff, cap * 8, c.stream));
+        keep.alloc(size_t(nrows));
+        k_row_dedup<<<grid_cap(nrows), 256, 0, c.stream>>>(ya, nrows, table.as<long long>(), cap - 1, keep.as<uint8_t>());
+        cnt.alloc(8);
+        int64_t kept = 0;
+        for (size_t cc = 0; cc < h->dev.size(); cc++) {
+          DevBuf nb;
+          bool is_bool = ya.cols[cc].type == VT_BOOL;
+          nb.alloc(size_t(nrows + 1) * (is_bool ? 1 : 8));
+          size_t tb = 0;
+          if (is_bool) {
+            NBG_HIP(rocprim::select(nullptr, tb, h->dev[cc].as<uint8_t>(), keep.as<uint8_t>(), nb.as<uint8_t>(),
+                                    cnt.as<uint64_t>(), size_t(nrows), c.stream));
+            c.ws_tmp.ensure(tb);
+            NBG_HIP(rocprim::select(c.ws_tmp.p, tb, h->dev[cc].as<uint8_t>(), keep.as<uint8_t>(), nb.as<uint8_t>(),
+                                    cnt.as<uint64_t>(), size_t(nrows), c.stream));
+          } else {
+            NBG_HIP(rocprim::select(nullptr, tb, h->dev[cc].as<int64_t>(), keep.as<uint8_t>(), nb.as<int64_t>(),
+                                    cnt.as<uint64_t>(), size_t(nrows), c.stream));
+            c.ws_tmp.ensure(tb);
+            NBG_HIP(rocprim::select(c.ws_tmp.p, tb, h->dev[cc].as<int64_t>(), keep.as<uint8_t>(), nb.as<int64_t>(),
+                                    cnt.as<uint64_t>(), size_t(nrows), c.stream));
+          }
+          uint64_t kc = 0;
+          NBG_HIP(hipMemcpyAsync(&kc, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
+          NBG_HIP(hipStreamSynchronize(c.stream));
+          kept = int64_t(kc);
+          h->dev[cc] = std::move(nb);
+        }
+        nrows = kept;
+      }
+    }
+  } catch (...) {
+    delete h;
+    throw;
+  }
+  hipEventRecord(c.ev[1], c.stream);
+  NBG_HIP(hipEventSynchronize(c.ev[1]));
+  float ms = 0;
+  hipEventElapsedTime(&ms, c.ev[0], c.ev[1]);
+  c.timing.total_ms = ms;
+  // hand the columns out
+  bool on_dev = s.keep_on_device != 0;
+  for (size_t cc = 0; cc < h->types.size(); cc++) {
+    h->str_off.push_back(nullptr);
+    if (on_dev) {
+      h->cols.push_back(h->dev[cc].p);
+    } else {
+      size_t w = h->types[cc] == NBG_T_BOOL ? 1 : 8;
+      h->host.emplace_back(size_t(nrows) * w + 8);
+      if (nrows) NBG_HIP(hipMemcpy(h->host.back().data(), h->dev[cc].p, size_t(nrows) * w, hipMemcpyDeviceToHost));
+      h->cols.push_back(h->host.back().data());
+    }
+  }
+  if (!on_dev) h->dev.clear();
+  fill_rows(out, h, nrows, on_dev);
+  out->edges_scanned = c.timing.edges_scanned;
+  return NBG_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// getBound (QueryBoundProcessor)
+// ------------------------------------------------------------------------------------------
+// request entry -> local row; a (part, vid) pair whose part does not hold the vertex's keys scans
+// an empty prefix in the reference, so it gets a zero-degree stand-in (-1)
+__global__ void k_bound_frontier(const int32_t* parts, const int32_t* g, int64_t n, int64_t lo, int64_t hi,
+                                 const int32_t* row_part, int32_t* F) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    int32_t x = g[i];
+    bool ok = x >= lo && x < hi && row_part[x - lo] == parts[i];
+    F[i] = ok ? int32_t(x - lo) : -1;
+  }
+}
+__global__ void k_degrees_masked(const int32_t* F, int64_t n, const int64_t* row_ptr, int64_t* deg) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= n; i += int64_t(gridDim.x) * blockDim.x) {
+    if (i == n) deg[i] = 0;
+    else deg[i] = F[i] < 0 ? 0 : row_ptr[F[i] + 1] - row_ptr[F[i]];
+  }
+}
+// request entries with deg 0 are removed so every frontier entry covers >= 1 edge slot
+__global__ void k_slot_owner(const int64_t* kept_slots, int64_t m, const int64_t* off, int64_t nF, int64_t* owner) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    int64_t e = kept_slots[i];
+    int64_t lo = 0, hi = nF;
+    while (hi - lo > 1) {
+      int64_t mid = (lo + hi) >> 1;
+      if (off[mid] <= e) lo = mid; else hi = mid;
+    }
+    owner[i] = lo;
+  }
+}
+struct BoundCol {
+  int32_t kind;  // 0 prop, 1 _dst, 2 _src, 3 _rank, 4 _type
+  int32_t prop;
+  int32_t type;  // NBG_T_*
+  void* out;
+  int64_t* str_len;  // STRING pass 1
+};
+constexpr int kMaxBoundCols = 32;
+struct BoundCols {
+  int32_t n;
+  BoundCol c[kMaxBoundCols];
+};
+__global__ void k_bound_rows(const int64_t* kept_slots, const int64_t* owner, int64_t m, const int64_t* off,
+                             const int32_t* F, const int64_t* row_ptr, int64_t lo, EvalEnv env, BoundCols bc,
+                             int64_t* ge_out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    int64_t k = owner[i];
+    int32_t f = F[k];
+    int64_t ge = row_ptr[f] + (kept_slots[i] - off[k]);
+    ge_out[i] = ge;
+    for (int c = 0; c < bc.n; c++) {
+      const BoundCol& b = bc.c[c];
+      int64_t v = 0;
+      switch (b.kind) {
+        case 1: v = env.vid_of[env.col[ge]]; break;
+        case 2: v = env.vid_of[lo + f]; break;
+        case 3: v = env.rank ? env.rank[ge] : 0; break;
+        case 4: v = env.etype; break;
+        default: {
+          const PropDev& p = env.props[b.prop];
+          if (p.type == NBG_T_STRING) {
+            b.str_len[i] = (p.present && !p.present[ge]) ? -1 : p.str_off[ge + 1] - p.str_off[ge];
+            continue;
+          }
+          if (p.present && !p.present[ge]) {
+            v = INT64_MIN;
+          } else if (p.type == NBG_T_DOUBLE || p.type == NBG_T_FLOAT) {
+            v = static_cast<const int64_t*>(p.data)[ge];
+          } else {
+            v = load_int(p.data, p.width, ge);
+          }
+        }
+      }
+      if (b.type == NBG_T_BOOL) static_cast<uint8_t*>(b.out)[i] = uint8_t(v != 0);
+      else static_cast<int64_t*>(b.out)[i] = v;
+    }
+  }
+}
+__global__ void k_str_gather(const int64_t* ge, int64_t m, const int64_t* src_off, const uint8_t* src_bytes,
+                             const int64_t* dst_off, uint8_t* dst) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    int64_t len = dst_off[i + 1] - dst_off[i];
+    const uint8_t* s = src_bytes + src_off[ge[i]];
+    for (int64_t j = 0; j < len; j++) dst[dst_off[i] + j] = s[j];
+  }
+}
+__global__ void k_clamp_len(int64_t* l, int64_t m) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    if (l[i] < 0) l[i] = 0;
+}
+
+int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* vids, size_t n, const uint8_t* filter,
+                      size_t flen, const nbg_prop_def* cols, size_t ncols, nbg_rows* out) {
+  if (!c.finalized) throw Error(NBG_E_STATE, "snapshot not finalized");
+  auto* h = new HostRows();
+  auto finish = [&](int64_t nrows) {
+    fill_rows(out, h, nrows, false);
+    return NBG_OK;
+  };
+  // request-level validation -> every part of the request fails (QueryBaseProcessor.inl:470-477)
+  std::vector<int32_t> req_parts;
+  for (size_t i = 0; i < n; i++)
+    if (std::find(req_parts.begin(), req_parts.end(), parts[i]) == req_parts.end()) req_parts.push_back(parts[i]);
+  auto fail_all = [&](int32_t code) {
+    for (auto p : req_parts) {
+      h->failed_parts.push_back(p);
+      h->failed_codes.push_back(code);
+    }
+    return finish(0);
+  };
+  bool in_bound = et < 0;
+  auto it = c.edges.find(in_bound ? -et : et);
+  if (it == c.edges.end()) return fail_all(NBG_E_EDGE_PROP_NOT_FOUND);
+  EdgeSpace& es = it->second;
+  Csr& csr = in_bound ? es.in : es.out;
+  BoundCols bc{};
+  for (size_t i = 0; i < ncols; i++) {
+    if (cols[i].owner != NBG_OWNER_EDGE) {
+      delete h;
+      throw Error(NBG_E_UNSUPPORTED, "SOURCE/DEST tag props are not supported yet");
+    }
+    std::string name = cols[i].name ? cols[i].name : "";
+    BoundCol b{};
+    if (name == "_dst") b.kind = 1;
+    else if (name == "_src") b.kind = 2;
+    else if (name == "_rank") b.kind = 3;
+    else if (name == "_type") b.kind = 4;
+    if (b.kind) {
+      b.type = NBG_T_INT;
+    } else if (!in_bound) {
+      int idx = -1;
+      for (size_t f = 0; f < es.fields.size(); f++)
+        if (es.fields[f].name == name) idx = int(f);
+      if (idx < 0) return fail_all(NBG_E_IMPROPER_DATA_TYPE);
+      b.kind = 0;
+      b.prop = idx;
+      int32_t t = es.fields[size_t(idx)].type;
+      b.type = (t == NBG_T_FLOAT) ? NBG_T_DOUBLE : (t == NBG_T_VID || t == NBG_T_TIMESTAMP) ? NBG_T_INT : t;
+    } else {
+      continue;  // "InBound has none props, skip it!"
+    }
+    if (bc.n >= kMaxBoundCols) {
+      delete h;
+      throw Error(NBG_E_UNSUPPORTED, "too many return columns");
+    }
+    bc.c[bc.n++] = b;
+  }
+  Program fprog{};
+  int pk = PK_NONE;
+  FastArgs fp{};
+  if (flen) {
+    std::string msg;
+    int32_t rc = compile_expr(filter, flen, es.fields, false, !in_bound, &fprog, &msg);
+    if (rc == NBG_E_UNSUPPORTED) {
+      delete h;
+      throw Error(rc, "filter: " + msg);
+    }
+    if (rc != NBG_OK) return fail_all(NBG_E_INVALID_FILTER);
+    FastPred f = classify_pred(fprog, es.fields);
+    pk = f.kind;
+    if (pk == PK_FAST) {
+      const PropCol& pc = csr.props[size_t(f.col)];
+      fp = FastArgs{pc.data.p, pc.present.as<uint8_t>(), pc.width, f.op, f.k};
+    }
+  }
+  int64_t N = int64_t(n);
+  const int64_t lo = c.owned_lo(), hi = c.owned_hi();
+  // parts not held by this rank -> E_PART_NOT_FOUND (NebulaStore::engine, BaseProcessor.inl:14-27)
+  for (auto p : req_parts)
+    if (p < 0 || p > c.num_parts || owner_of_part(p, c.world) != c.rank) {
+      h->failed_parts.push_back(p);
+      h->failed_codes.push_back(NBG_E_PART_NOT_FOUND);
+    }
+  DevBuf dv, dp, dg, dF, ddeg, doff;
+  dv.alloc(size_t(N + 1) * 8);
+  dp.alloc(size_t(N + 1) * 4);
+  dg.alloc(size_t(N + 1) * 4);
+  dF.alloc(size_t(N + 1) * 4);
+  ddeg.alloc(size_t(N + 1) * 8);
+  doff.alloc(size_t(N + 1) * 8);
+  if (N) {
+    NBG_HIP(hipMemcpyAsync(dv.p, vids, size_t(N) * 8, hipMemcpyHostToDevice, c.stream));
+    NBG_HIP(hipMemcpyAsync(dp.p, parts, size_t(N) * 4, hipMemcpyHostToDevice, c.stream));
+    lookup_gidx(c, dv.as<int64_t>(), dg.as<int32_t>(), N);
+    k_bound_frontier<<<grid_cap(N), 256, 0, c.stream>>>(dp.as<int32_t>(), dg.as<int32_t>(), N, lo, hi,
+                                                      csr.row_part.as<int32_t>(), dF.as<int32_t>());
+  }
+  k_degrees_masked<<<grid_cap(N + 1), 256, 0, c.stream>>>(dF.as<int32_t>(), N, csr.row_ptr.as<int64_t>(), ddeg.as<int64_t>());
+  exclusive_scan_dev<int64_t>(c, ddeg.as<int64_t>(), doff.as<int64_t>(), N + 1);
+  std::vector<int64_t> hoff(size_t(N + 1));
+  NBG_HIP(hipMemcpyAsync(hoff.data(), doff.p, size_t(N + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  int64_t E = hoff[size_t(N)];
+  c.timing = Timing{};
+  c.timing.edges_scanned = uint64_t(E);
+  // compress away zero-degree request entries for the expansion (tile owner search needs deg>=1)
+  std::vector<int32_t> hF(static_cast<size_t>(N));
+  if (N) NBG_HIP(hipMemcpy(hF.data(), dF.p, size_t(N) * 4, hipMemcpyDeviceToHost));
+  std::vector<int32_t> cF;
+  std::vector<int64_t> coff, centry;
+  for (int64_t i = 0; i < N; i++)
+    if (hoff[size_t(i + 1)] > hoff[size_t(i)]) {
+      cF.push_back(hF[size_t(i)]);
+      coff.push_back(hoff[size_t(i)]);
+      centry.push_back(i);
+    }
+  coff.push_back(E);
+  int64_t nF = int64_t(cF.size());
+  DevBuf dcF, dcoff, flags, slots, cnt, owner, geb;
+  dcF.alloc(size_t(nF + 1) * 4);
+  dcoff.alloc(size_t(nF + 1) * 8);
+  if (nF) NBG_HIP(hipMemcpyAsync(dcF.p, cF.data(), size_t(nF) * 4, hipMemcpyHostToDevice, c.stream));
+  NBG_HIP(hipMemcpyAsync(dcoff.p, coff.data(), size_t(nF + 1) * 8, hipMemcpyHostToDevice, c.stream));
+  flags.alloc(size_t(E + 1));
+  EvalEnv env = make_env(c, es, csr, in_bound ? -es.type : es.type);
+  DevBuf dprog;
+  dprog.alloc(sizeof(Program));
+  NBG_HIP(hipMemcpyAsync(dprog.p, &fprog, sizeof(Program), hipMemcpyHostToDevice, c.stream));
+  DevBuf cnts;
+  cnts.alloc(64);
+  NBG_HIP(hipMemsetAsync(cnts.p, 0, 64, c.stream));
+  hipEventRecord(c.ev[0], c.stream);
+  int64_t m = 0;
+  if (E > 0) {
+    ExpandArgs a{};
+    a.F = dcF.as<int32_t>();
+    a.nF = nF;
+    a.off = dcoff.as<int64_t>();
+    a.row_ptr = csr.row_ptr.as<int64_t>();
+    a.col = csr.col.as<int32_t>();
+    a.lo = lo;
+    a.flags = flags.as<uint8_t>();
+    a.err = cnts.as<unsigned long long>();
+    a.storage = 1;
+    launch_expand<EXP_FLAGS>(c, a, pk, fp, dprog.as<Program>(), env, E);
+    c.timing.expand_bytes += expand_bytes(nF, E, pk == PK_FAST ? fp.width : 0, EXP_FLAGS);
+    slots.alloc(size_t(E + 1) * 8);
+    cnt.alloc(8);
+    size_t tb = 0;
+    auto first = rocprim::counting_iterator<int64_t>(0);
+    NBG_HIP(rocprim::select(nullptr, tb, first, flags.as<uint8_t>(), slots.as<int64_t>(), cnt.as<uint64_t>(), size_t(E), c.stream));
+    c.ws_tmp.ensure(tb);
+    NBG_HIP(rocprim::select(c.ws_tmp.p, tb, first, flags.as<uint8_t>(), slots.as<int64_t>(), cnt.as<uint64_t>(), size_t(E), c.stream));
+    uint64_t hm = 0;
+    NBG_HIP(hipMemcpyAsync(&hm, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    m = int64_t(hm);
+  }
+  owner.alloc(size_t(m + 1) * 8);
+  geb.alloc(size_t(m + 1) * 8);
+  std::vector<DevBuf> dcols(size_t(bc.n));
+  std::vector<DevBuf> slen(size_t(bc.n));
+  for (int i = 0; i < bc.n; i++) {
+    BoundCol& b = bc.c[i];
+    if (b.type == NBG_T_STRING) {
+      slen[size_t(i)].alloc(size_t(m + 1) * 8);
+      b.str_len = slen[size_t(i)].as<int64_t>();
+    } else {
+      dcols[size_t(i)].alloc(size_t(m + 1) * (b.type == NBG_T_BOOL ? 1 : 8));
+      b.out = dcols[size_t(i)].p;
+    }
+  }
+  std::vector<int64_t> howner(static_cast<size_t>(m));
+  if (m) {
+    k_slot_owner<<<grid_cap(m), 256, 0, c.stream>>>(slots.as<int64_t>(), m, dcoff.as<int64_t>(), nF, owner.as<int64_t>());
+    k_bound_rows<<<grid_cap(m), 256, 0, c.stream>>>(slots.as<int64_t>(), owner.as<int64_t>(), m, dcoff.as<int64_t>(),
+                                                  dcF.as<int32_t>(), csr.row_ptr.as<int64_t>(), lo, env, bc,
+                                                  geb.as<int64_t>());
+    NBG_HIP(hipGetLastError());
+    NBG_HIP(hipMemcpyAsync(howner.data(), owner.p, size_t(m) * 8, hipMemcpyDeviceToHost, c.stream));
+  }
+  hipEventRecord(c.ev[1], c.stream);
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  float ms = 0;
+  hipEventElapsedTime(&ms, c.ev[0], c.ev[1]);
+  c.timing.total_ms = ms;
+  // assemble: typed columns to host; absent values (INT64_MIN marker / -1 length) stay absent
+  for (int i = 0; i < bc.n; i++) {
+    const BoundCol& b = bc.c[i];
+    h->types.push_back(b.type);
+    if (b.type == NBG_T_STRING) {
+      std::vector<int64_t> lens(static_cast<size_t>(m));
+      if (m) NBG_HIP(hipMemcpy(lens.data(), slen[size_t(i)].p, size_t(m) * 8, hipMemcpyDeviceToHost));
+      std::vector<int64_t> offs(size_t(m) + 1, 0);
+      for (int64_t r = 0; r < m; r++) offs[size_t(r + 1)] = offs[size_t(r)] + std::max<int64_t>(lens[size_t(r)], 0);
+      DevBuf doffs, dbytes;
+      doffs.alloc(size_t(m + 1) * 8);
+      dbytes.alloc(size_t(offs[size_t(m)]) + 8);
+      NBG_HIP(hipMemcpy(doffs.p, offs.data(), size_t(m + 1) * 8, hipMemcpyHostToDevice));
+      const PropCol& pc = csr.props[size_t(b.prop)];
+      if (m)
+        k_str_gather<<<grid_cap(m), 256, 0, c.stream>>>(geb.as<int64_t>(), m, pc.str_off.as<int64_t>(),
+                                                        pc.str_bytes.as<uint8_t>(), doffs.as<int64_t>(), dbytes.as<uint8_t>());
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      h->host.emplace_back(size_t(offs[size_t(m)]) + 8);
+      if (offs[size_t(m)]) NBG_HIP(hipMemcpy(h->host.back().data(), dbytes.p, size_t(offs[size_t(m)]), hipMemcpyDeviceToHost));
+      h->host_off.push_back(offs);
+      h->cols.push_back(h->host.back().data());
+      h->str_off.push_back(h->host_off.back().data());
+    } else {
+      size_t w = b.type == NBG_T_BOOL ? 1 : 8;
+      h->host.emplace_back(size_t(m) * w + 8);
+      if (m) NBG_HIP(hipMemcpy(h->host.back().data(), dcols[size_t(i)].p, size_t(m) * w, hipMemcpyDeviceToHost));
+      h->cols.push_back(h->host.back().data());
+      h->str_off.push_back(nullptr);
+    }
+  }
+  // vertices with >= 1 row, in request order (QueryBoundProcessor.cpp:61-67)
+  h->row_vertex.resize(size_t(m));
+  int64_t last = -1;
+  for (int64_t r = 0; r < m; r++) {
+    int64_t k = howner[size_t(r)];
+    int64_t entry = centry[size_t(k)];
+    h->row_vertex[size_t(r)] = vids[entry];
+    if (k != last) {
+      h->vertex_ids.push_back(vids[entry]);
+      h->vertex_row_offsets.push_back(r);
+      last = k;
+    }
+  }
+  h->vertex_row_offsets.push_back(m);
+  fill_rows(out, h, m, false);
+  out->edges_scanned = uint64_t(E);
+  return NBG_OK;
+}
+
+int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t* dst, size_t n, int32_t max_steps,
+                          nbg_rows* out) {
+  (void)c; (void)et; (void)src; (void)dst; (void)n; (void)max_steps; (void)out;
+  throw Error(NBG_E_UNSUPPORTED, "FIND SHORTEST PATH lands in the next milestone");
+}
+
+void free_rows_impl(void* impl) { delete static_cast<HostRows*>(impl); }
+
+}  // namespace nbg

@@ -1,0 +1,287 @@
+"""Host-side mirror of the reference's operator interfaces over the C ABI.
+
+* ``GraphSpace``        -- one space on one GPU rank (the storaged's KVStore + schemas, and
+                           graphd's StorageClient for that space).
+* ``QueryBoundProcessor`` -- ``instance(space, bound_type)`` + ``process(GetNeighborsRequest)``
+                           -> ``QueryResponse``, the shape of
+                           src/storage/QueryBoundProcessor.h:23-28 / QueryBaseProcessor.h:47.
+* ``GoExecutor``        -- GO N STEPS FROM ... OVER ... [WHERE] [YIELD [DISTINCT]], the
+                           device-resident replacement of src/graph/GoExecutor.cpp:80-782.
+
+Everything executes in libnebula_amd.so on the GPU; there is no Python or CPU compute path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _lib
+from . import expr as X
+from ._lib import NbgError
+
+OUT_BOUND, IN_BOUND = 0, 1
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def pack_kv(pairs):
+    """[(key bytes, value bytes)] -> the C-ABI blob layout (bytes + n+1 offsets)."""
+    ks = [bytes(k) for k, _ in pairs]
+    vs = [bytes(v) for _, v in pairs]
+    koff = np.zeros(len(ks) + 1, dtype=np.uint64)
+    voff = np.zeros(len(vs) + 1, dtype=np.uint64)
+    if ks:
+        koff[1:] = np.cumsum([len(k) for k in ks])
+        voff[1:] = np.cumsum([len(v) for v in vs])
+    kb = np.frombuffer(b"".join(ks) + b"\0" * 8, dtype=np.uint8)
+    vb = np.frombuffer(b"".join(vs) + b"\0" * 8, dtype=np.uint8)
+    return kb, koff, vb, voff
+
+
+class RowSet:
+    """Typed columnar result (copied to host unless ``on_device``)."""
+
+    def __init__(self, rows: _lib.Rows, keep_device: bool = False):
+        self.n_rows = int(rows.n_rows)
+        self.types = [rows.col_types[i] for i in range(rows.n_cols)]
+        self.edges_scanned = int(rows.edges_scanned)
+        self.on_device = bool(rows.on_device)
+        self.columns = []
+        self.device_ptrs = []
+        for c, t in enumerate(self.types):
+            ptr = rows.cols[c]
+            if self.on_device:
+                self.device_ptrs.append(ptr)
+                self.columns.append(None)
+                continue
+            if t == _lib.T_STRING:
+                offs = np.ctypeslib.as_array(rows.str_offsets[c], shape=(self.n_rows + 1,)).copy()
+                raw = C.string_at(ptr, int(offs[-1])) if self.n_rows else b""
+                self.columns.append([raw[offs[i]:offs[i + 1]].decode() for i in range(self.n_rows)])
+            elif self.n_rows == 0:
+                self.columns.append(np.zeros(0, dtype=np.uint8 if t == _lib.T_BOOL else
+                                             (np.float64 if t == _lib.T_DOUBLE else np.int64)))
+            elif t == _lib.T_BOOL:
+                self.columns.append(np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(self.n_rows,)).astype(bool))
+            elif t == _lib.T_DOUBLE:
+                self.columns.append(np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_double)), shape=(self.n_rows,)).copy())
+            else:
+                self.columns.append(np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_int64)), shape=(self.n_rows,)).copy())
+        self.row_vertex = (np.ctypeslib.as_array(rows.row_vertex, shape=(self.n_rows,)).copy()
+                           if rows.row_vertex and self.n_rows else np.zeros(0, dtype=np.int64))
+        nv = int(rows.n_vertices)
+        self.vertex_ids = (np.ctypeslib.as_array(rows.vertex_ids, shape=(nv,)).copy() if nv else np.zeros(0, np.int64))
+        self.vertex_row_offsets = (np.ctypeslib.as_array(rows.vertex_row_offsets, shape=(nv + 1,)).copy()
+                                   if nv else np.zeros(1, np.int64))
+        self.failed = [(rows.failed_parts[i], rows.failed_codes[i]) for i in range(rows.n_failed)]
+
+    def rows(self):
+        out = []
+        for r in range(self.n_rows):
+            row = []
+            for c, t in enumerate(self.types):
+                v = self.columns[c][r]
+                if t == _lib.T_BOOL:
+                    row.append(bool(v))
+                elif t == _lib.T_DOUBLE:
+                    row.append(float(v))
+                elif t == _lib.T_STRING:
+                    row.append(v)
+                else:
+                    row.append(int(v))
+            out.append(tuple(row))
+        return out
+
+
+class GraphSpace:
+    def __init__(self, num_parts: int, device: int = 0, rank: int = 0, world_size: int = 1):
+        self.L = _lib.load()
+        self.num_parts, self.rank, self.world_size = num_parts, rank, world_size
+        self.h = self.L.nbg_ctx_create(device, num_parts, rank, world_size)
+        if not self.h:
+            raise RuntimeError("nbg_ctx_create failed: no MI355X visible or bad arguments "
+                               "(the engine has no CPU path)")
+
+    # ---- lifecycle -------------------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.nbg_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int):
+        if rc != _lib.NBG_OK:
+            raise NbgError(rc, self.L.nbg_last_error(self.h).decode())
+
+    def comm_init(self, unique_id: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._check(self.L.nbg_comm_init(self.h, buf))
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        L = _lib.load()
+        buf = (C.c_uint8 * 128)()
+        rc = L.nbg_comm_unique_id(buf)
+        if rc != 0:
+            raise NbgError(rc, "ncclGetUniqueId failed")
+        return bytes(buf)
+
+    def set_option(self, key: str, value: int):
+        self._check(self.L.nbg_set_option(self.h, key.encode(), int(value)))
+
+    # ---- schema + snapshot -----------------------------------------------------------
+    def set_edge_schema(self, edge_type: int, fields: Sequence[tuple[str, int]], ver: int = 0):
+        names = (C.c_char_p * max(len(fields), 1))(*[f.encode() for f, _ in fields])
+        types = (C.c_int32 * max(len(fields), 1))(*[t for _, t in fields])
+        self._check(self.L.nbg_schema_set_edge(self.h, edge_type, ver, len(fields), names, types))
+
+    def load_part(self, part: int, pairs):
+        kb, koff, vb, voff = pairs if isinstance(pairs, tuple) else pack_kv(pairs)
+        n = len(koff) - 1
+        self._check(self.L.nbg_snapshot_load_part(self.h, part, _p(kb), _p(koff), _p(vb), _p(voff), n))
+
+    def gen_rmat(self, scale: int, edge_factor: int, seed: int, edge_type: int):
+        self._check(self.L.nbg_snapshot_gen_rmat(self.h, scale, edge_factor, seed, edge_type))
+
+    def finalize(self):
+        self._check(self.L.nbg_snapshot_finalize(self.h))
+
+    def info(self, edge_type: int) -> dict:
+        si = _lib.SnapshotInfo()
+        self._check(self.L.nbg_snapshot_info_get(self.h, edge_type, C.byref(si)))
+        return {k: getattr(si, k) for k, _ in si._fields_}
+
+    def out_degree(self, edge_type: int, vid: int) -> int:
+        return int(self.L.nbg_snapshot_out_degree(self.h, edge_type, vid))
+
+    def last_timing(self) -> dict:
+        t = _lib.Timing()
+        self._check(self.L.nbg_last_timing(self.h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in t._fields_}
+
+    # ---- queries ---------------------------------------------------------------------
+    def get_bound(self, edge_type: int, parts, vids, return_columns, filter: bytes | X.Expr | None = b"") -> RowSet:
+        parts = np.ascontiguousarray(parts, dtype=np.int32)
+        vids = np.ascontiguousarray(vids, dtype=np.int64)
+        f = X.encode(filter)
+        fb = np.frombuffer(f + b"\0", dtype=np.uint8)
+        arr = (_lib.PropDef * max(len(return_columns), 1))()
+        keep = []
+        for i, col in enumerate(return_columns):
+            name, owner, tag = (col if isinstance(col, tuple) else (col, _lib.OWNER_EDGE, 0))
+            b = name.encode()
+            keep.append(b)
+            arr[i] = _lib.PropDef(b, owner, tag)
+        rows = _lib.Rows()
+        self._check(self.L.nbg_get_bound(self.h, edge_type, _p(parts), _p(vids), len(vids), _p(fb), len(f),
+                                         arr, len(return_columns), C.byref(rows)))
+        try:
+            return RowSet(rows)
+        finally:
+            self.L.nbg_rows_free(C.byref(rows))
+
+    def go(self, starts, steps: int, edge_type: int, where=None, yields: Iterable = (), distinct: bool = False,
+           keep_on_device: bool = False) -> RowSet:
+        starts = np.ascontiguousarray(starts, dtype=np.int64)
+        w = X.encode(where)
+        wb = np.frombuffer(w + b"\0", dtype=np.uint8)
+        ys = [X.encode(y) for y in yields]
+        ybufs = [C.create_string_buffer(y, len(y) + 1) for y in ys]
+        yp = (C.c_void_p * max(len(ys), 1))(*[C.cast(b, C.c_void_p) for b in ybufs])
+        yl = (C.c_size_t * max(len(ys), 1))(*[len(y) for y in ys])
+        spec = _lib.GoSpec(edge_type, steps, _p(starts), len(starts), _p(wb), len(w), yp, yl, len(ys),
+                           int(distinct), int(keep_on_device))
+        rows = _lib.Rows()
+        self._check(self.L.nbg_go(self.h, C.byref(spec), C.byref(rows)))
+        try:
+            return RowSet(rows)
+        finally:
+            self.L.nbg_rows_free(C.byref(rows))
+
+
+# ---- reference-shaped operator wrappers ---------------------------------------------------
+@dataclass
+class PropDef:
+    """storage::cpp2::PropDef (src/interface/storage.thrift:43-49)."""
+    owner: int
+    name: str
+    tag_id: int = 0
+
+
+@dataclass
+class GetNeighborsRequest:
+    """storage::cpp2::GetNeighborsRequest (storage.thrift:125-133)."""
+    space_id: int
+    parts: dict
+    edge_type: int
+    filter: bytes = b""
+    return_columns: list = field(default_factory=list)
+
+
+@dataclass
+class VertexData:
+    vertex_id: int
+    edge_rows: list
+
+
+@dataclass
+class QueryResponse:
+    failed_codes: list
+    edge_schema: list
+    vertices: list
+
+
+class QueryBoundProcessor:
+    """QueryBoundProcessor::instance(...) / process(req) (QueryBoundProcessor.h:23-28)."""
+
+    def __init__(self, space: GraphSpace, bound_type: int = OUT_BOUND):
+        self.space, self.bound_type = space, bound_type
+
+    @classmethod
+    def instance(cls, space: GraphSpace, bound_type: int = OUT_BOUND):
+        return cls(space, bound_type)
+
+    def process(self, req: GetNeighborsRequest) -> QueryResponse:
+        parts, vids = [], []
+        for p, vs in req.parts.items():
+            parts += [p] * len(vs)
+            vids += list(vs)
+        cols = [(c.name, c.owner, c.tag_id) for c in req.return_columns]
+        et = req.edge_type
+        rs = self.space.get_bound(et, parts, vids, cols, req.filter)
+        rows = rs.rows()
+        verts = []
+        for i, vid in enumerate(rs.vertex_ids):
+            a, b = rs.vertex_row_offsets[i], rs.vertex_row_offsets[i + 1]
+            verts.append(VertexData(int(vid), rows[a:b]))
+        names = [c.name for c in req.return_columns if c.owner == _lib.OWNER_EDGE]
+        return QueryResponse([{"part_id": p, "code": c} for p, c in rs.failed], list(zip(names, rs.types)), verts)
+
+
+class GoExecutor:
+    """GO [N STEPS] FROM starts OVER edge [WHERE f] [YIELD [DISTINCT] cols]."""
+
+    def __init__(self, space: GraphSpace, starts, edge_type: int, steps: int = 1, where=None, yields=(),
+                 distinct: bool = False):
+        self.space, self.starts, self.edge_type = space, starts, edge_type
+        self.steps, self.where, self.yields, self.distinct = steps, where, list(yields), distinct
+
+    def execute(self, keep_on_device: bool = False) -> RowSet:
+        return self.space.go(self.starts, self.steps, self.edge_type, self.where, self.yields, self.distinct,
+                             keep_on_device)

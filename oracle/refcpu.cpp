@@ -1235,6 +1235,34 @@ size_t ora_store_num_keys(const ora_store* st) {
   return n;
 }
 
+size_t ora_store_part_size(const ora_store* st, int32_t part, size_t* kbytes, size_t* vbytes) {
+  *kbytes = *vbytes = 0;
+  if (part < 0 || size_t(part) >= st->parts.size()) return 0;
+  const Part& p = st->parts[size_t(part)];
+  for (auto& r : p.kvs) {
+    *kbytes += r.klen;
+    *vbytes += r.vlen;
+  }
+  return p.kvs.size();
+}
+void ora_store_dump_part(const ora_store* st, int32_t part, uint8_t* kb, uint64_t* koff, uint8_t* vb,
+                         uint64_t* voff) {
+  const Part& p = st->parts[size_t(part)];
+  uint64_t ko = 0, vo = 0;
+  size_t i = 0;
+  for (auto& r : p.kvs) {
+    koff[i] = ko;
+    voff[i] = vo;
+    memcpy(kb + ko, p.key(r), r.klen);
+    memcpy(vb + vo, p.val(r), r.vlen);
+    ko += r.klen;
+    vo += r.vlen;
+    i++;
+  }
+  koff[i] = ko;
+  voff[i] = vo;
+}
+
 void ora_schema_set_edge(ora_store* st, int32_t et, int32_t ver, int32_t nf,
                          const char* const* names, const int32_t* types) {
   auto s = std::make_shared<Schema>();

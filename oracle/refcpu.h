@@ -30,6 +30,10 @@ void ora_store_put_batch(ora_store* st, int32_t part, const uint8_t* kbytes, con
                          const uint8_t* vbytes, const uint64_t* voff, size_t n);
 void ora_store_finalize(ora_store* st);  // sort each part bytewise (RocksEngine prefix order)
 size_t ora_store_num_keys(const ora_store* st);
+// dump one part's sorted KV (after finalize): sizes first, then the blobs (n+1 offsets)
+size_t ora_store_part_size(const ora_store* st, int32_t part, size_t* kbytes, size_t* vbytes);
+void ora_store_dump_part(const ora_store* st, int32_t part, uint8_t* kb, uint64_t* koff,
+                         uint8_t* vb, uint64_t* voff);
 // schema registry (meta SchemaManager stand-in).  types = cpp2::SupportedType values.
 void ora_schema_set_edge(ora_store* st, int32_t edge_type, int32_t ver, int32_t nfields,
                          const char* const* names, const int32_t* types);

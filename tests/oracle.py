@@ -44,6 +44,8 @@ def lib():
             "ora_store_put_batch": (None, [vp, i32, vp, vp, vp, vp, sz]),
             "ora_store_finalize": (None, [vp]),
             "ora_store_num_keys": (sz, [vp]),
+            "ora_store_part_size": (sz, [vp, i32, P(sz), P(sz)]),
+            "ora_store_dump_part": (None, [vp, i32, vp, vp, vp, vp]),
             "ora_schema_set_edge": (None, [vp, i32, i32, i32, P(C.c_char_p), P(i32)]),
             "ora_schema_set_tag": (None, [vp, i32, C.c_char_p, i32, i32, P(C.c_char_p), P(i32)]),
             "ora_schema_set_edge_name": (None, [vp, i32, C.c_char_p]),
@@ -255,6 +257,17 @@ class Store:
 
     def num_keys(self):
         return lib().ora_store_num_keys(self.h)
+
+    def dump_part(self, part):
+        """(kbytes, koff, vbytes, voff) numpy blobs of one finalized part (the C-ABI layout)."""
+        kbn, vbn = C.c_size_t(), C.c_size_t()
+        n = lib().ora_store_part_size(self.h, part, C.byref(kbn), C.byref(vbn))
+        kb = np.zeros(kbn.value + 8, dtype=np.uint8)
+        vb = np.zeros(vbn.value + 8, dtype=np.uint8)
+        koff = np.zeros(n + 1, dtype=np.uint64)
+        voff = np.zeros(n + 1, dtype=np.uint64)
+        lib().ora_store_dump_part(self.h, part, _ptr(kb), _ptr(koff), _ptr(vb), _ptr(voff))
+        return kb, koff, vb, voff
 
     def set_edge_schema(self, etype, fields, ver=0, name=None):
         names = _cstrs([f for f, _ in fields])

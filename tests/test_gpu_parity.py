@@ -1,0 +1,339 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the reference fixtures.
+
+Every comparison is bit-exact on integer/byte results; rows are compared as multisets after
+sorting (the reference's own result check, src/graph/test/TestBase.h:182-222).
+"""
+from collections import Counter
+
+import numpy as np
+import pytest
+
+import fixtures as F
+import oracle as O
+from nebula_amd import GraphSpace, NbgError
+from nebula_amd import expr as X
+
+pytestmark = pytest.mark.gpu
+
+FOLLOW = 1
+SEED = 1
+
+
+def ms(rows):
+    return Counter(tuple(r) for r in rows)
+
+
+# ------------------------------------------------------------------------------------------
+# NBA dataset (GoTest)
+# ------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def nba():
+    sp = GraphSpace(1)
+    for et, (name, fields) in F.NBA_EDGE_SCHEMAS.items():
+        sp.set_edge_schema(et, fields)
+    parts, vid = F.nba_kv()
+    for p, kv in parts.items():
+        sp.load_part(p, kv)
+    sp.finalize()
+    st, _ = F.nba_oracle_store()
+    yield sp, st, vid, F.nba()
+    sp.close()
+
+
+def names(vid, rows):
+    inv = {v: k for k, v in vid.items()}
+    return Counter(tuple(inv.get(c, c) if isinstance(c, int) and c in inv else c for c in r) for r in rows)
+
+
+def golden(d, key):
+    return Counter(tuple(r) for r in d["expect"][key]["rows"])
+
+
+def gpu_pipe(sp, starts, etypes, distinct_last=False, ylast=()):
+    cur = list(starts)
+    rs = None
+    for i, et in enumerate(etypes):
+        last = i == len(etypes) - 1
+        rs = sp.go(cur, 1, et, yields=ylast if last else (), distinct=distinct_last and last)
+        cur = [r[0] for r in rs.rows()]
+    return rs
+
+
+def test_nba_one_step(nba):
+    sp, st, vid, d = nba
+    rs = sp.go([vid["Tim Duncan"]], 1, F.NBA_SERVE)
+    assert names(vid, rs.rows()) == golden(d, "one_step_serve_tim")
+
+
+def test_nba_yield_props_and_where(nba):
+    sp, st, vid, d = nba
+    ys = [X.AliasProp("serve", "start_year"), X.AliasProp("serve", "end_year"), X.EdgeDst("serve")]
+    rs = sp.go([vid["Boris Diaw"]], 1, F.NBA_SERVE, yields=ys)
+    assert names(vid, rs.rows()) == golden(d, "serve_boris_years")
+    w = (X.AliasProp("serve", "start_year") >= 2013) & (X.AliasProp("serve", "end_year") <= 2018)
+    rs = sp.go([vid["Rajon Rondo"]], 1, F.NBA_SERVE, where=w, yields=ys)
+    assert names(vid, rs.rows()) == golden(d, "serve_rondo_where")
+    ref = st.go([vid["Rajon Rondo"]], 1, F.NBA_SERVE, where=w.encode(), yields=[y.encode() for y in ys])
+    assert ms(rs.rows()) == ms(ref.rows())
+
+
+def test_nba_pipes(nba):
+    sp, st, vid, d = nba
+    rs = gpu_pipe(sp, [vid["Boris Diaw"]], [F.NBA_LIKE, F.NBA_LIKE, F.NBA_SERVE])
+    assert names(vid, rs.rows()) == golden(d, "pipe_boris_like_like_serve")
+    rs = gpu_pipe(sp, [vid["Tracy McGrady"]], [F.NBA_LIKE, F.NBA_LIKE])
+    assert names(vid, rs.rows()) == golden(d, "var_tracy_like_like")
+    rs = gpu_pipe(sp, [vid["Tracy McGrady"]], [F.NBA_LIKE] * 3)
+    assert names(vid, rs.rows()) == golden(d, "var_pipe_tracy")
+    rs = gpu_pipe(sp, [vid["Boris Diaw"]], [F.NBA_LIKE, F.NBA_LIKE, F.NBA_SERVE], distinct_last=True,
+                  ylast=[X.EdgeDst("serve")])
+    assert names(vid, rs.rows()) == golden(d, "distinct_boris_serve_dst")
+
+
+def test_nba_steps_and_empty(nba):
+    sp, st, vid, d = nba
+    rs = sp.go([vid["Boris Diaw"]], 3, F.NBA_LIKE)
+    assert names(vid, rs.rows()) == golden(d, "derived_go3_boris_like")
+    assert sp.go([d["nonexist_hash"]], 1, F.NBA_SERVE).n_rows == 0
+    assert sp.go([d["nonexist_hash"]], 3, F.NBA_LIKE).n_rows == 0
+    assert sp.go([], 2, F.NBA_LIKE).n_rows == 0
+
+
+def test_nba_expression_semantics(nba):
+    sp, st, vid, d = nba
+    tim = [vid["Tim Duncan"], vid["Tony Parker"], vid["Dejounte Murray"]]
+    cases = [
+        X.AliasProp("like", "likeness") > 10.5,        # int vs double: variant index order
+        X.AliasProp("like", "likeness") < 10.5,
+        X.AliasProp("like", "likeness").eq(95.0),      # almostEqual
+        X.AliasProp("like", "likeness").ne(95),
+        (X.AliasProp("like", "likeness") % 7) > 2,
+        ~(X.AliasProp("like", "likeness") >= 95) | X.Primary(False),
+        X.Primary("x") > X.AliasProp("like", "likeness"),   # string vs int
+        X.Unary(X.NOT, X.Primary("")),                       # asBool(string) is empty()
+        (X.AliasProp("like", "likeness") * 2 - 100) / 3 > 20,
+        X.EdgeDst("like") > 0,
+        X.EdgeRank("like").eq(0),
+    ]
+    for w in cases:
+        g = sp.go(tim, 1, F.NBA_LIKE, where=w, yields=[X.EdgeDst("like"), X.AliasProp("like", "likeness")])
+        r = st.go(tim, 1, F.NBA_LIKE, where=w.encode(),
+                  yields=[X.EdgeDst("like").encode(), X.AliasProp("like", "likeness").encode()])
+        assert r.code == 0
+        assert ms(g.rows()) == ms(r.rows()), w.encode()
+
+
+def test_nba_eval_error_fails_query(nba):
+    sp, st, vid, d = nba
+    with pytest.raises(NbgError) as e:
+        sp.go([vid["Tim Duncan"]], 1, F.NBA_LIKE, where=X.AliasProp("like", "nope") > 1)
+    assert e.value.code == -23  # E_IMPROPER_DATA_TYPE
+    with pytest.raises(NbgError):
+        sp.go([vid["Tim Duncan"]], 1, F.NBA_LIKE, where=(X.AliasProp("like", "likeness") / 0) > 1)
+    # the deferred error is not raised when the frontier empties first (onEmptyInputs)
+    assert sp.go([d["nonexist_hash"]], 2, F.NBA_LIKE, where=X.AliasProp("like", "nope") > 1).n_rows == 0
+
+
+def test_nba_yield_distinct_multicol(nba):
+    sp, st, vid, d = nba
+    starts = [p["vid"] for p in d["players"]]
+    ys = [X.AliasProp("serve", "end_year"), X.AliasProp("serve", "end_year") > 2015]
+    g = sp.go(starts, 1, F.NBA_SERVE, yields=ys, distinct=True)
+    r = st.go(starts, 1, F.NBA_SERVE, yields=[y.encode() for y in ys], distinct=True)
+    assert ms(g.rows()) == ms(r.rows())
+    g = sp.go(starts, 2, F.NBA_LIKE, distinct=False)
+    r = st.go(starts, 2, F.NBA_LIKE)
+    assert ms(g.rows()) == ms(r.rows())
+
+
+# ------------------------------------------------------------------------------------------
+# QueryBoundTest fixture (storage getBound)
+# ------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def qb():
+    sp = GraphSpace(6)
+    sp.set_edge_schema(F.EDGE_TYPE, F.qb_edge_schema())
+    for part, data in F.qb_kv_parts().items():
+        sp.load_part(part, data)
+    sp.finalize()
+    st = F.qb_oracle_store()
+    yield sp, st
+    sp.close()
+
+
+def edge_cols():
+    return [("_dst", O.EDGE, 0), ("_rank", O.EDGE, 0)] + [(f"col_{i * 2}", O.EDGE, 0) for i in range(10)]
+
+
+def by_vertex(rs):
+    out = {}
+    rows = rs.rows()
+    for i, v in enumerate(rs.vertex_ids):
+        out[int(v)] = rows[rs.vertex_row_offsets[i]:rs.vertex_row_offsets[i + 1]]
+    return out
+
+
+def oracle_by_vertex(res):
+    out = {}
+    for r, row in enumerate(res.rows()):
+        out.setdefault(res.row_vertex(r), []).append(row)
+    return out
+
+
+@pytest.mark.parametrize("filt", [
+    None,
+    X.Relational(X.GE, X.AliasProp("e101", "col_0"), X.Primary(10007)),
+    X.Relational(X.LT, X.AliasProp("e101", "col_2"), X.Primary(10005)) | (X.AliasProp("e101", "col_14").eq("string_col_14_2")),
+    X.AliasProp("e101", "col_11") > X.Primary("string_col_11_1"),
+])
+def test_get_bound_matches_reference(qb, filt):
+    sp, st = qb
+    parts, vids, _ = F.qb_request()
+    cols = edge_cols()
+    f = X.encode(filt)
+    g = sp.get_bound(F.EDGE_TYPE, parts, vids, cols, f)
+    r = st.get_bound(F.EDGE_TYPE, parts, vids, cols, filt=f)
+    assert g.failed == r.failed() == []
+    gv, rv = by_vertex(g), oracle_by_vertex(r)
+    assert gv == rv  # same vertices, same rows, same per-vertex order (bytewise key order)
+    if filt is None:  # checkResponse expectations (QueryBoundTest.cpp:111-178), edge part
+        assert len(gv) == 30
+        for vid, rows in gv.items():
+            assert [row[0] for row in rows] == list(range(10001, 10008))
+            for row in rows:
+                assert row[1] == 0
+                assert list(row[2:7]) == [row[0] + 2 * i for i in range(5)]
+                assert list(row[7:]) == [f"string_col_{(i + 5) * 2}_2" for i in range(5)]
+
+
+def test_get_bound_in_bound(qb):
+    sp, st = qb
+    parts, vids, _ = F.qb_request(False)
+    cols = edge_cols()
+    g = sp.get_bound(-F.EDGE_TYPE, parts, vids, cols)
+    r = st.get_bound(-F.EDGE_TYPE, parts, vids, cols, in_bound=True)
+    gv = by_vertex(g)
+    assert gv == oracle_by_vertex(r)
+    assert len(gv) == 30 and all([row[0] for row in rows] == list(range(20001, 20006)) for rows in gv.values())
+
+
+def test_get_bound_invalid_filter(qb):
+    sp, st = qb
+    parts, vids, _ = F.qb_request()
+    g = sp.get_bound(F.EDGE_TYPE, parts, vids, edge_cols(), X.InputProp("tag_3001_col_0"))
+    assert sorted(g.failed) == [(0, -31), (1, -31), (2, -31)]
+    g = sp.get_bound(F.EDGE_TYPE, parts, vids, edge_cols() + [("nope", O.EDGE, 0)])
+    assert sorted(g.failed) == [(0, -23), (1, -23), (2, -23)]
+
+
+def test_get_bound_wrong_part_and_dups(qb):
+    sp, st = qb
+    # vertex 5 lives in part 0; asking part 1 scans an empty prefix. Duplicates repeat rows.
+    parts, vids = [1, 0, 0], [5, 5, 5]
+    cols = edge_cols()
+    g = sp.get_bound(F.EDGE_TYPE, parts, vids, cols)
+    r = st.get_bound(F.EDGE_TYPE, parts, vids, cols)
+    assert g.n_rows == r.nrows == 14
+    assert ms(g.rows()) == ms(r.rows())
+
+
+# ------------------------------------------------------------------------------------------
+# synthetic RMAT: device generator + KV ingest vs the oracle
+# ------------------------------------------------------------------------------------------
+def oracle_rmat(scale, versions=1, parts=64):
+    st = O.Store(parts)
+    st.set_edge_schema(FOLLOW, [("weight", O.INT)], name="follow")
+    st.load_rmat(scale, 16, SEED, FOLLOW, versions=versions)
+    return st
+
+
+def seeds_from(scale, n, seed=7):
+    s, d, w = O.rmat_edges(scale, 16, SEED)
+    rng = np.random.default_rng(seed)
+    return [int(x) for x in s[rng.integers(0, len(s), n)]]
+
+
+@pytest.fixture(scope="module")
+def rmat12():
+    sp = GraphSpace(64)
+    sp.set_edge_schema(FOLLOW, [("weight", O.INT)])
+    sp.gen_rmat(12, 16, SEED, FOLLOW)
+    sp.finalize()
+    st = oracle_rmat(12)
+    yield sp, st
+    sp.close()
+
+
+@pytest.mark.parametrize("steps", [1, 2, 3])
+def test_rmat_go_steps(rmat12, steps):
+    sp, st = rmat12
+    starts = seeds_from(12, 16)
+    g = sp.go(starts, steps, FOLLOW)
+    r = st.go(starts, steps, FOLLOW)
+    assert g.n_rows == r.nrows
+    assert np.array_equal(np.sort(g.columns[0]), np.sort(r.int_col(0)))
+    assert g.edges_scanned == r.edges_scanned
+
+
+def test_rmat_go_where_distinct(rmat12):
+    sp, st = rmat12
+    starts = seeds_from(12, 64)
+    w = X.AliasProp("follow", "weight") > 499
+    y = [X.EdgeDst("follow")]
+    g = sp.go(starts, 3, FOLLOW, where=w, yields=y, distinct=True)
+    r = st.go(starts, 3, FOLLOW, where=w.encode(), yields=[y[0].encode()], distinct=True)
+    assert np.array_equal(np.sort(g.columns[0]), np.sort(r.int_col(0)))
+    assert len(set(g.columns[0].tolist())) == g.n_rows
+    # non-distinct with a VM predicate and computed yields
+    w2 = (X.AliasProp("follow", "weight") % 3).eq(1) & (X.EdgeSrc("follow") > 0)
+    y2 = [X.EdgeSrc("follow"), X.EdgeDst("follow"), X.AliasProp("follow", "weight") * 2]
+    g = sp.go(starts, 2, FOLLOW, where=w2, yields=y2)
+    r = st.go(starts, 2, FOLLOW, where=w2.encode(), yields=[y.encode() for y in y2])
+    assert ms(g.rows()) == ms(r.rows())
+
+
+def test_rmat_kv_ingest_equals_generator(rmat12):
+    sp, st = rmat12
+    kv = GraphSpace(64)
+    kv.set_edge_schema(FOLLOW, [("weight", O.INT)])
+    for p in range(1, 65):
+        kv.load_part(p, st.dump_part(p))
+    kv.finalize()
+    a, b = sp.info(FOLLOW), kv.info(FOLLOW)
+    assert a["num_vertices"] == b["num_vertices"] and a["local_out_edges"] == b["local_out_edges"]
+    assert a["local_in_edges"] == b["local_in_edges"]
+    starts = seeds_from(12, 32, seed=3)
+    for steps in (1, 3):
+        ga = sp.go(starts, steps, FOLLOW, yields=[X.EdgeDst("f"), X.AliasProp("f", "weight")])
+        gb = kv.go(starts, steps, FOLLOW, yields=[X.EdgeDst("f"), X.AliasProp("f", "weight")])
+        assert ms(ga.rows()) == ms(gb.rows())
+    kv.close()
+
+
+def test_rmat_multiversion_first_version_wins():
+    st = oracle_rmat(10, versions=3)
+    sp = GraphSpace(64)
+    sp.set_edge_schema(FOLLOW, [("weight", O.INT)])
+    for p in range(1, 65):
+        sp.load_part(p, st.dump_part(p))
+    sp.finalize()
+    starts = seeds_from(10, 32)
+    for steps in (1, 2, 3):
+        w = X.AliasProp("follow", "weight") > 499
+        y = [X.EdgeDst("follow"), X.AliasProp("follow", "weight")]
+        g = sp.go(starts, steps, FOLLOW, where=w, yields=y)
+        r = st.go(starts, steps, FOLLOW, where=w.encode(), yields=[x.encode() for x in y])
+        assert ms(g.rows()) == ms(r.rows())
+    sp.close()
+
+
+def test_rmat_get_bound_matches_oracle(rmat12):
+    sp, st = rmat12
+    starts = seeds_from(12, 40, seed=5)
+    parts = [O.part_of(v, 64) for v in starts]
+    cols = [("_dst", O.EDGE, 0), ("weight", O.EDGE, 0), ("_rank", O.EDGE, 0), ("_src", O.EDGE, 0)]
+    f = X.AliasProp("follow", "weight") >= 300
+    g = sp.get_bound(FOLLOW, parts, starts, cols, f)
+    r = st.get_bound(FOLLOW, parts, starts, cols, filt=f.encode())
+    gv, rv = by_vertex(g), oracle_by_vertex(r)
+    assert gv == rv
