@@ -125,6 +125,7 @@ def main():
     exp_ms = 0.0
     exp_bytes = 0
     tot_ms = 0.0
+    bu_steps = 0
     for _ in range(args.steps):
         r = one()
         t = sp.last_timing()
@@ -133,6 +134,7 @@ def main():
         exp_ms += t["expand_ms"]
         exp_bytes += t["expand_bytes"]
         tot_ms += t["total_ms"]
+        bu_steps = t["bu_steps"]
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -180,6 +182,7 @@ def main():
                 "algorithmic_bytes_per_query": exp_bytes // max(args.steps, 1),
                 "expand_ms_per_query": exp_ms / max(args.steps, 1),
                 "device_ms_per_query": tot_ms / max(args.steps, 1),
+                "bottom_up_hops": bu_steps,
             },
             "cpu_baseline": None,
         }

@@ -191,6 +191,7 @@ typedef struct {
   uint64_t edges_scanned;
   uint64_t expand_bytes;  /* algorithmic bytes of the expansion kernels          */
   int32_t steps_run;
+  int32_t bu_steps;       /* steps that ran bottom-up over the transposed CSR               */
 } nbg_timing;
 int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out);
 int32_t nbg_set_option(nbg_ctx* ctx, const char* key, int64_t value);

@@ -68,7 +68,8 @@ class GoSpec(C.Structure):
 
 class Timing(C.Structure):
     _fields_ = [("total_ms", C.c_double), ("expand_ms", C.c_double), ("expand_launches", C.c_int64),
-                ("edges_scanned", C.c_uint64), ("expand_bytes", C.c_uint64), ("steps_run", C.c_int32)]
+                ("edges_scanned", C.c_uint64), ("expand_bytes", C.c_uint64), ("steps_run", C.c_int32),
+                ("bu_steps", C.c_int32)]
 
 
 _lib = None

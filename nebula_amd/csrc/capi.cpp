@@ -212,6 +212,7 @@ int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out) {
     out->edges_scanned = c.timing.edges_scanned;
     out->expand_bytes = c.timing.expand_bytes;
     out->steps_run = c.timing.steps_run;
+    out->bu_steps = c.timing.bu_steps;
     return NBG_OK;
   });
 }

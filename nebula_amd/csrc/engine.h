@@ -107,6 +107,7 @@ struct Csr {
   DevBuf row_part;  // int32 [n_rows]: the part holding the row's keys
   DevBuf row_ok;    // uint8 [n_rows] row_part == hash part; empty when all rows follow the rule
   std::vector<PropCol> props;
+  DevBuf prop_table;  // device copy of the column descriptors (built on first query)
   size_t bytes() const {
     size_t b = row_ptr.bytes + col.bytes + rank.bytes + row_part.bytes + row_ok.bytes;
     for (auto& p : props) b += p.data.bytes + p.present.bytes + p.str_off.bytes + p.str_bytes.bytes;
@@ -133,6 +134,11 @@ struct EdgeSpace {
   std::vector<Field> fields;
   Staging out_stage, in_stage;
   Csr out, in;
+  // Transpose of the out CSR for bottom-up steps: row = owned dst, col = global src index,
+  // props = copies of the INT-like out props in transpose order, t_eid = out-edge index.
+  Csr tr;
+  DevBuf t_eid;   // uint32 [nnz]
+  bool has_tr = false;
 };
 
 struct Timing {
@@ -140,6 +146,7 @@ struct Timing {
   int64_t expand_launches = 0;
   uint64_t edges_scanned = 0, expand_bytes = 0;
   int32_t steps_run = 0;
+  int32_t bu_steps = 0;
 };
 
 struct Ctx {

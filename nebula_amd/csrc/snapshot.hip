@@ -37,6 +37,10 @@ __global__ void k_fill(T* p, T v, int64_t n) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
     p[i] = v;
 }
+__global__ void k_iota_rev_u32(uint32_t* p, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    p[i] = uint32_t(n - 1 - i);
+}
 __global__ void k_iota_u32(uint32_t* p, int64_t n) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
     p[i] = uint32_t(i);
@@ -596,6 +600,18 @@ __global__ void k_dedup_flags(const uint64_t* skey, const uint32_t* perm, const 
   }
 }
 
+// row_ptr from row keys sorted ascending (no atomics): row_ptr[v] = first i with key[i] >= v
+__global__ void k_rowptr_sorted(const uint32_t* keys, int64_t m, int64_t n, int64_t* row_ptr) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= m; i += int64_t(gridDim.x) * blockDim.x) {
+    int64_t prev = i == 0 ? -1 : int64_t(keys[i - 1]);
+    int64_t cur = i == m ? n : int64_t(keys[i]);
+    for (int64_t v = prev + 1; v <= cur; v++) row_ptr[v] = i;
+  }
+}
+__global__ void k_kept_src(const uint64_t* skey, const uint32_t* kept, int64_t m, uint32_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = uint32_t(skey[kept[i]] >> 32);
+}
 __global__ void k_row_part_default(const int64_t* vid_of_lo, int64_t n, int32_t parts, int32_t* row_part) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
     row_part[i] = dev_part_of(vid_of_lo[i], parts);
@@ -721,6 +737,9 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
     keyC.alloc(size_t(n) * 8);
     uint32_t* pin = permA.as<uint32_t>();
     uint32_t* pout = permB.as<uint32_t>();
+    // start from reverse load order: stable passes then put the LAST write of identical keys
+    // first, so keep-first implements WriteBatch last-write-wins (RocksEngine.cpp:216-230)
+    k_iota_rev_u32<<<grid_for(n), 256, 0, c.stream>>>(pin, n);
     auto pass_bswap = [&](const DevBuf& vals) {
       k_gather_key_bswap<<<grid_for(n), 256, 0, c.stream>>>(vals.as<int64_t>(), pin, keyC.as<uint64_t>(), n);
       radix_pairs<uint64_t, uint32_t>(c, keyC.as<uint64_t>(), keyB.as<uint64_t>(), pin, pout, n, 64);
@@ -755,12 +774,15 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
   keep.release();
   out.nnz = int64_t(m);
   const uint32_t* kp = kept.as<uint32_t>();
-  // row_ptr
-  DevBuf counts;
-  counts.alloc(size_t(out.n_rows + 1) * 8);
-  NBG_HIP(hipMemsetAsync(counts.p, 0, size_t(out.n_rows + 1) * 8, c.stream));
-  k_row_counts<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(skey_keep.as<uint64_t>(), kp, int64_t(m), counts.as<int64_t>());
-  exclusive_scan<int64_t>(c, counts.as<int64_t>(), out.row_ptr.as<int64_t>(), out.n_rows + 1);
+  // row_ptr (kept edges are sorted by src)
+  {
+    DevBuf ks;
+    ks.alloc(size_t(m + 1) * 4);
+    k_kept_src<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(skey_keep.as<uint64_t>(), kp, int64_t(m), ks.as<uint32_t>());
+    k_rowptr_sorted<<<grid_for(int64_t(m) + 1), 256, 0, c.stream>>>(ks.as<uint32_t>(), int64_t(m), out.n_rows,
+                                                                   out.row_ptr.as<int64_t>());
+    NBG_HIP(hipStreamSynchronize(c.stream));
+  }
   // row_part: hash rule by default, the key's part where the staging recorded it
   out.row_part.alloc(size_t(out.n_rows + 1) * 4);
   k_row_part_default<<<grid_for(out.n_rows), 256, 0, c.stream>>>(c.vid_of.as<int64_t>() + lo, out.n_rows,
@@ -870,6 +892,72 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
   s.str_len.clear();
   s.n = 0;
   s.cap = 0;
+}
+
+__global__ void k_edge_src(const int64_t* row_ptr, int64_t n_rows, int32_t* esrc) {
+  for (int64_t r = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; r < n_rows; r += int64_t(gridDim.x) * blockDim.x)
+    for (int64_t e = row_ptr[r]; e < row_ptr[r + 1]; e++) esrc[e] = int32_t(r);
+}
+__global__ void k_tr_col(const uint32_t* t_eid, const int32_t* esrc, int64_t m, int64_t lo, int32_t* tcol) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    tcol[i] = int32_t(lo) + esrc[t_eid[i]];
+}
+template <typename T>
+__global__ void k_gather_w(const T* in, const uint32_t* perm, T* out, int64_t m) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = in[perm[i]];
+}
+
+// Transpose of the out CSR (single rank): rows = dst, entries = src, plus INT-like prop copies.
+static void build_transpose(Ctx& c, EdgeSpace& es) {
+  Csr& o = es.out;
+  Csr& t = es.tr;
+  int64_t m = o.nnz;
+  int64_t n = c.n_global;
+  t.n_rows = n;
+  t.nnz = m;
+  t.row_ptr.alloc(size_t(n + 1) * 8);
+  t.col.alloc(size_t(m + 1) * 4);
+  es.t_eid.alloc(size_t(m + 1) * 4);
+  if (m == 0) {
+    NBG_HIP(hipMemsetAsync(t.row_ptr.p, 0, size_t(n + 1) * 8, c.stream));
+  } else {
+    DevBuf esrc, keysB, iota;
+    esrc.alloc(size_t(m) * 4);
+    keysB.alloc(size_t(m) * 4);
+    iota.alloc(size_t(m) * 4);
+    k_edge_src<<<grid_for(o.n_rows), 256, 0, c.stream>>>(o.row_ptr.as<int64_t>(), o.n_rows, esrc.as<int32_t>());
+    k_iota_u32<<<grid_for(m), 256, 0, c.stream>>>(iota.as<uint32_t>(), m);
+    int bits = 1;
+    while ((int64_t(1) << bits) < std::max<int64_t>(n, 2)) bits++;
+    radix_pairs<uint32_t, uint32_t>(c, o.col.as<uint32_t>(), keysB.as<uint32_t>(), iota.as<uint32_t>(),
+                                   es.t_eid.as<uint32_t>(), m, bits);
+    k_tr_col<<<grid_for(m), 256, 0, c.stream>>>(es.t_eid.as<uint32_t>(), esrc.as<int32_t>(), m, c.owned_lo(),
+                                              t.col.as<int32_t>());
+    k_rowptr_sorted<<<grid_for(m + 1), 256, 0, c.stream>>>(keysB.as<uint32_t>(), m, n, t.row_ptr.as<int64_t>());
+  }
+  for (const PropCol& p : o.props) {
+    PropCol q;
+    q.name = p.name;
+    q.type = p.type;
+    q.width = p.width;
+    bool intlike = p.type == NBG_T_INT || p.type == NBG_T_VID || p.type == NBG_T_TIMESTAMP || p.type == NBG_T_BOOL;
+    if (intlike && !p.present.p && m) {
+      q.data.alloc(size_t(m) * size_t(p.width) + 16);
+      int g = grid_for(m);
+      const uint32_t* pe = es.t_eid.as<uint32_t>();
+      switch (p.width) {
+        case 1: k_gather_w<int8_t><<<g, 256, 0, c.stream>>>(p.data.as<int8_t>(), pe, q.data.as<int8_t>(), m); break;
+        case 2: k_gather_w<int16_t><<<g, 256, 0, c.stream>>>(p.data.as<int16_t>(), pe, q.data.as<int16_t>(), m); break;
+        case 4: k_gather_w<int32_t><<<g, 256, 0, c.stream>>>(p.data.as<int32_t>(), pe, q.data.as<int32_t>(), m); break;
+        default: k_gather_w<int64_t><<<g, 256, 0, c.stream>>>(p.data.as<int64_t>(), pe, q.data.as<int64_t>(), m);
+      }
+    }
+    t.props.push_back(std::move(q));
+  }
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  NBG_HIP(hipGetLastError());
+  es.has_tr = true;
 }
 
 __global__ void k_owned_only(const uint64_t* in, int64_t n, int parts, int world, int rank, uint8_t* flag) {
@@ -1032,6 +1120,7 @@ void snapshot_finalize(Ctx& c) {
     EdgeSpace& es = kv.second;
     build_csr(c, es.out_stage, es.fields, true, es.out, brank.as<uint32_t>());
     build_csr(c, es.in_stage, es.fields, false, es.in, brank.as<uint32_t>());
+    if (c.world == 1 && c.opt("bottom_up", 1)) build_transpose(c, es);
   }
   c.heap.release();
   c.heap_used = 0;

@@ -60,9 +60,8 @@ struct PropDev {
   const int64_t* str_off;
   const uint8_t* str_bytes;
 };
-constexpr int kMaxProps = 16;
 struct EvalEnv {
-  PropDev props[kMaxProps];
+  const PropDev* props;  // device table, one entry per schema field (Csr::prop_table)
   int32_t nprops;
   int32_t etype;
   const int64_t* vid_of;
@@ -415,18 +414,6 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
   }
 }
 
-// deg[i] = outdeg(F[i]); deg[nF] = 0
-__global__ void k_degrees(const int32_t* F, int64_t nF, const int64_t* row_ptr, int64_t* deg) {
-  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= nF; i += int64_t(gridDim.x) * blockDim.x) {
-    if (i == nF) {
-      deg[i] = 0;
-    } else {
-      int32_t f = F[i];
-      deg[i] = row_ptr[f + 1] - row_ptr[f];
-    }
-  }
-}
-
 // wave-wide exclusive prefix sum of a per-lane count
 __device__ inline uint32_t wave_excl_scan(uint32_t x, uint32_t& total) {
   const int lane = threadIdx.x & 63;
@@ -440,12 +427,54 @@ __device__ inline uint32_t wave_excl_scan(uint32_t x, uint32_t& total) {
   return v - x;
 }
 
+// Bottom-up step (direction-optimising BFS, Beamer et al.): every owned vertex d scans its
+// in-neighbours (transpose CSR) until one is in the frontier bitmap (and passes the predicate),
+// then marks itself.  No random writes: the frontier bitmap is read-only (L2/MALL resident) and
+// each thread writes only its own byte.  Same set as the top-down step: next = {d : exists s in F,
+// s -> d [, pred]}, i.e. getDstIdsFromResp's set (GoExecutor.cpp:407-431).
+template <int PK>
+__global__ __launch_bounds__(256) void k_bottom_up(const int64_t* __restrict__ trp, const int32_t* __restrict__ tcol,
+                                                   int64_t n, int64_t lo, const uint32_t* __restrict__ fbits,
+                                                   uint8_t* __restrict__ map, FastArgs fp,
+                                                   unsigned long long* examined) {
+  uint32_t ex = 0;
+  for (int64_t d = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; d < n; d += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t b = trp[d], end = trp[d + 1];
+    bool found = false;
+    for (int64_t e = b; e < end; e++) {
+      const int32_t s = tcol[e];
+      ex++;
+      if (!((fbits[s >> 5] >> (s & 31)) & 1u)) continue;
+      if (PK == PK_FAST && !fast_cmp(fp.op, load_int(fp.data, fp.width, e), fp.k)) continue;
+      found = true;
+      break;
+    }
+    if (found) map[lo + d] = 1;
+  }
+  uint32_t tot;
+  wave_excl_scan(ex, tot);
+  if ((threadIdx.x & 63) == 0 && tot) atomicAdd(examined, (unsigned long long)tot);
+}
+
+// deg[i] = outdeg(F[i]); deg[nF] = 0
+__global__ void k_degrees(const int32_t* F, int64_t nF, const int64_t* row_ptr, int64_t* deg) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= nF; i += int64_t(gridDim.x) * blockDim.x) {
+    if (i == nF) {
+      deg[i] = 0;
+    } else {
+      int32_t f = F[i];
+      deg[i] = row_ptr[f + 1] - row_ptr[f];
+    }
+  }
+}
+
 // Compact the owned slice [lo, lo+n) of the byte-map into a frontier list of local indices,
 // clearing it.  require_deg: drop vertices without out-edges (they cannot produce rows).
 // n_set counts every set byte (the reference's "starts_ non-empty" test, GoExecutor.cpp:392).
 __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64_t n, const int64_t* row_ptr,
                                                  const uint8_t* row_ok, int require_deg, int32_t* out,
-                                                 unsigned long long* n_out, unsigned long long* n_set) {
+                                                 unsigned long long* n_out, unsigned long long* n_set,
+                                                 uint16_t* bits) {
   const int64_t nchunks = (n + 15) / 16;
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   const int64_t rounds = (nchunks + stride - 1) / stride;
@@ -469,6 +498,7 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
         if (row_ptr[v + 1] == row_ptr[v] || (row_ok && !row_ok[v])) keepmask &= ~(1u << j);
       }
     }
+    if (bits && ch < nchunks) bits[ch] = uint16_t(keepmask);  // frontier bitmap for bottom-up
     uint32_t tot_set, tot_keep;
     wave_excl_scan(__popc(setmask), tot_set);
     uint32_t pre = wave_excl_scan(__popc(keepmask), tot_keep);
@@ -627,14 +657,18 @@ void fill_rows(nbg_rows* out, HostRows* h, int64_t nrows, bool on_device) {
   out->_impl = h;
 }
 
-EvalEnv make_env(Ctx& c, EdgeSpace& es, const Csr& csr, int32_t etype) {
+EvalEnv make_env(Ctx& c, EdgeSpace& es, Csr& csr, int32_t etype) {
   EvalEnv env{};
-  env.nprops = int32_t(std::min<size_t>(csr.props.size(), kMaxProps));
-  for (int i = 0; i < env.nprops; i++) {
-    const PropCol& p = csr.props[size_t(i)];
-    env.props[i] = PropDev{p.type, p.width, p.data.p, p.present.as<uint8_t>(), p.str_off.as<int64_t>(),
-                           p.str_bytes.as<uint8_t>()};
+  env.nprops = int32_t(csr.props.size());
+  if (env.nprops && !csr.prop_table.p) {
+    std::vector<PropDev> tab;
+    for (const PropCol& p : csr.props)
+      tab.push_back(PropDev{p.type, p.width, p.data.p, p.present.as<uint8_t>(), p.str_off.as<int64_t>(),
+                            p.str_bytes.as<uint8_t>()});
+    csr.prop_table.alloc(sizeof(PropDev) * tab.size());
+    NBG_HIP(hipMemcpy(csr.prop_table.p, tab.data(), sizeof(PropDev) * tab.size(), hipMemcpyHostToDevice));
   }
+  env.props = csr.prop_table.as<PropDev>();
   env.etype = etype;
   env.vid_of = c.vid_of.as<int64_t>();
   env.col = csr.col.as<int32_t>();
@@ -667,6 +701,7 @@ void ensure_workspaces(Ctx& c, int64_t nF_cap) {
   c.ws_front[1].ensure(size_t(nF_cap + 64) * 4);
   c.ws_off.ensure(size_t(nF_cap + 2) * 8);
   c.ws_counters.ensure(256);
+  c.ws_bits_send.ensure(size_t(mb / 8 + 64));
 }
 
 // frontier degree scan: fills c.ws_off[0..nF] and returns total edges (synchronises)
@@ -698,6 +733,35 @@ void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Progr
   hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
   c.timing.expand_ms += ms;
   c.timing.expand_launches++;
+}
+
+// bottom-up launch (timed like the expansion); returns adjacency entries examined
+uint64_t launch_bottom_up(Ctx& c, EdgeSpace& es, const uint32_t* fbits, uint8_t* map, int pk, const FastArgs& fp,
+                          unsigned long long* d_examined) {
+  const Csr& tr = es.tr;
+  NBG_HIP(hipMemsetAsync(d_examined, 0, 8, c.stream));
+  int grid = grid_cap(tr.n_rows, 256, int(c.opt("bu_grid", 256 * 16)));
+  hipEventRecord(c.ev[2], c.stream);
+  if (pk == PK_FAST)
+    k_bottom_up<PK_FAST><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows,
+                                                     c.owned_lo(), fbits, map, fp, d_examined);
+  else
+    k_bottom_up<PK_NONE><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows,
+                                                     c.owned_lo(), fbits, map, fp, d_examined);
+  NBG_HIP(hipGetLastError());
+  hipEventRecord(c.ev[3], c.stream);
+  uint64_t ex = 0;
+  NBG_HIP(hipMemcpyAsync(&ex, d_examined, 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipEventSynchronize(c.ev[3]));
+  float ms = 0;
+  hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
+  c.timing.expand_ms += ms;
+  c.timing.expand_launches++;
+  c.timing.bu_steps++;
+  // byte model: row_ptr 8 B/row, frontier bitmap once, examined entries (col + predicate), mark
+  c.timing.expand_bytes += uint64_t(tr.n_rows) * 9 + uint64_t(tr.n_rows) / 8 +
+                           ex * (4 + uint64_t(pk == PK_FAST ? fp.width : 0));
+  return ex;
 }
 
 // algorithmic bytes of one expansion (DESIGN.md "byte model"): frontier id 4 B + row_ptr pair
@@ -764,7 +828,12 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   Counters K{c.ws_counters.as<unsigned long long>(), {}};
   DevBuf degbuf;
   uint8_t* map = c.ws_map.as<uint8_t>();
+  uint16_t* bits16 = c.ws_bits_send.as<uint16_t>();  // frontier bitmap written by k_compact
+  const uint32_t* fbits = c.ws_bits_send.as<uint32_t>();
   const int64_t* row_ptr = csr.row_ptr.as<int64_t>();
+  const bool bu_ok = es.has_tr && c.opt("bottom_up", 1) != 0;
+  const int64_t bu_div = std::max<int64_t>(1, c.opt("bu_div", 4));  // bottom-up when E >= nnz / bu_div
+  const int64_t bu_force = c.opt("bu_force", 0);                     // 1: always, -1: never
   const uint8_t* row_ok = csr.row_ok.as<uint8_t>();  // rows whose keys sit outside hash(vid)'s part
 
   // starts -> gidx
@@ -786,7 +855,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       k_list_starts<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, F, K.d);
     } else {
       k_mark_gidx<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, map);
-      k_compact<<<grid_cap((n_own + 15) / 16), 256, 0, c.stream>>>(map, lo, n_own, row_ptr, row_ok, 1, F, K.d, K.d + 1);
+      k_compact<<<grid_cap((n_own + 15) / 16), 256, 0, c.stream>>>(map, lo, n_own, row_ptr, row_ok, 1, F, K.d, K.d + 1,
+                                                                    bits16);
     }
     NBG_HIP(hipGetLastError());
     NBG_HIP(hipMemcpyAsync(K.h, K.d, 16, hipMemcpyDeviceToHost, c.stream));
@@ -831,17 +901,23 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     int64_t E = nF ? degree_scan(c, F, nF, csr, degbuf) : 0;
     c.timing.edges_scanned += uint64_t(E);
     if (E > 0) {
-      a.F = F;
-      a.nF = nF;
-      a.off = c.ws_off.as<int64_t>();
-      launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, E);
-      c.timing.expand_bytes += expand_bytes(nF, E, 0, EXP_MARK);
+      bool bu = bu_ok && bu_force >= 0 && (bu_force > 0 || E >= csr.nnz / bu_div);
+      if (bu) {
+        launch_bottom_up(c, es, fbits, map, PK_NONE, fp, K.d + 6);
+      } else {
+        a.F = F;
+        a.nF = nF;
+        a.off = c.ws_off.as<int64_t>();
+        launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, E);
+        c.timing.expand_bytes += expand_bytes(nF, E, 0, EXP_MARK);
+      }
     }
     // next frontier = set of dsts (P12), compacted and deg-0 vertices dropped
     cur ^= 1;
     F = c.ws_front[cur].as<int32_t>();
     NBG_HIP(hipMemsetAsync(K.d, 0, 16, c.stream));
-    k_compact<<<grid_cap((n_own + 15) / 16), 256, 0, c.stream>>>(map, lo, n_own, row_ptr, row_ok, 1, F, K.d, K.d + 1);
+    k_compact<<<grid_cap((n_own + 15) / 16), 256, 0, c.stream>>>(map, lo, n_own, row_ptr, row_ok, 1, F, K.d, K.d + 1,
+                                                                    bits16);
     NBG_HIP(hipGetLastError());
     NBG_HIP(hipMemcpyAsync(K.h, K.d, 16, hipMemcpyDeviceToHost, c.stream));
     NBG_HIP(hipStreamSynchronize(c.stream));
@@ -876,16 +952,25 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   int64_t nrows = 0;
   try {
     if (distinct_dst) {
-      // DISTINCT e._dst: mark surviving dsts, compact the whole vertex space (no deg filter)
-      if (E > 0) {
+      // DISTINCT e._dst: mark surviving dsts, compact the whole vertex space (no deg filter).
+      // Bottom-up only when the predicate cannot error (the reference fails the query on any
+      // row's eval error, so every row must be evaluated when errors are possible).
+      bool pred_bu = pk == PK_NONE || (pk == PK_FAST && fp.present == nullptr &&
+                                       es.tr.props.size() > size_t(fpk.col) && es.tr.props[size_t(fpk.col)].data.p);
+      bool bu = E > 0 && bu_ok && pred_bu && bu_force >= 0 && (bu_force > 0 || E >= csr.nnz / bu_div);
+      if (bu) {
+        FastArgs tfp = fp;
+        if (pk == PK_FAST) tfp.data = es.tr.props[size_t(fpk.col)].data.p;
+        launch_bottom_up(c, es, fbits, map, pk, tfp, K.d + 6);
+      } else if (E > 0) {
         launch_expand<EXP_MARK>(c, a, pk, fp, dprog.as<Program>(), env, E);
         c.timing.expand_bytes += expand_bytes(nF, E, pred_w, EXP_MARK);
       }
       DevBuf lst;
       lst.alloc(size_t(c.n_global + 64) * 4);
-      NBG_HIP(hipMemsetAsync(K.d, 0, 48, c.stream));
+      NBG_HIP(hipMemsetAsync(K.d, 0, 16, c.stream));  // keep the eval-error counter (K.d[4])
       k_compact<<<grid_cap((c.n_global + 15) / 16), 256, 0, c.stream>>>(map, 0, c.n_global, row_ptr, nullptr, 0,
-                                                                       lst.as<int32_t>(), K.d, K.d + 1);
+                                                                       lst.as<int32_t>(), K.d, K.d + 1, nullptr);
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
       if (K.h[4]) throw Error(NBG_E_EVAL, "WHERE evaluation failed");

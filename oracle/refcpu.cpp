@@ -745,6 +745,7 @@ struct ora_result {
     std::string vertexData, edgeData;
     std::vector<refcpu::Val> tagVals;
     std::vector<bool> tagPresent;
+    size_t nrows = 0;
   };
   std::vector<V> vertices;
   std::vector<refcpu::Field> edgeSchema, vertexSchema;
@@ -1487,6 +1488,7 @@ ora_result* ora_get_bound(ora_store* st, int32_t et, int32_t inBound, const int3
       out->rows.push_back(std::move(row));
       out->present.push_back(std::move(pres));
       out->rowVertex.push_back(v.vid);
+      v.nrows++;
     });
   }
   return out;
@@ -1767,6 +1769,7 @@ void ora_res_failed(const ora_result* r, size_t i, int32_t* part, int32_t* code)
 int64_t ora_res_row_vertex(const ora_result* r, size_t row) { return r->rowVertex[row]; }
 size_t ora_res_nvertices(const ora_result* r) { return r->vertices.size(); }
 int64_t ora_res_vertex_id(const ora_result* r, size_t i) { return r->vertices[i].vid; }
+size_t ora_res_vertex_nrows(const ora_result* r, size_t i) { return r->vertices[i].nrows; }
 int32_t ora_res_vertex_ncols(const ora_result* r) { return int32_t(r->vertexSchema.size()); }
 int32_t ora_res_vertex_type(const ora_result* r, size_t i, int32_t col) {
   auto& v = r->vertices[i];

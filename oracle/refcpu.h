@@ -101,6 +101,7 @@ void ora_res_failed(const ora_result* r, size_t i, int32_t* part, int32_t* code)
 int64_t ora_res_row_vertex(const ora_result* r, size_t row);
 size_t ora_res_nvertices(const ora_result* r);
 int64_t ora_res_vertex_id(const ora_result* r, size_t i);
+size_t ora_res_vertex_nrows(const ora_result* r, size_t i);
 int32_t ora_res_vertex_ncols(const ora_result* r);
 int32_t ora_res_vertex_type(const ora_result* r, size_t i, int32_t col);
 int64_t ora_res_vertex_int(const ora_result* r, size_t i, int32_t col);

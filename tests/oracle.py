@@ -73,6 +73,7 @@ def lib():
             "ora_res_row_vertex": (i64, [vp, sz]),
             "ora_res_nvertices": (sz, [vp]),
             "ora_res_vertex_id": (i64, [vp, sz]),
+            "ora_res_vertex_nrows": (sz, [vp, sz]),
             "ora_res_vertex_ncols": (i32, [vp]),
             "ora_res_vertex_type": (i32, [vp, sz, i32]),
             "ora_res_vertex_int": (i64, [vp, sz, i32]),
@@ -226,6 +227,9 @@ class Result:
                     vals.append(None)
             out.append((L.ora_res_vertex_id(self.h, i), vals))
         return out
+
+    def vertex_nrows(self, i) -> int:
+        return lib().ora_res_vertex_nrows(self.h, i)
 
     def edge_bytes(self, i) -> bytes:
         n = C.c_size_t()
