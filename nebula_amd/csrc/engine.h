@@ -180,6 +180,7 @@ struct Ctx {
   DevBuf ws_counters;  // small device counters
   DevBuf ws_bits_send, ws_bits_recv;
   DevBuf ws_starts;
+  DevBuf ws_partials;  // per-block partial sums of the aggregated kernels
   Timing timing;
   hipEvent_t ev[8] = {};
   std::map<std::string, int64_t> options;
