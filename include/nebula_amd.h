@@ -74,6 +74,10 @@ const char* nbg_last_error(const nbg_ctx* ctx);
  * (src/storage/client/StorageClient.inl:74-159) with a per-step all-to-all.                 */
 int32_t nbg_comm_unique_id(uint8_t out[128]);
 int32_t nbg_comm_init(nbg_ctx* ctx, const uint8_t unique_id[128]);
+/* Test transport: contexts of ONE process (one per rank, any device) with the same group_key
+ * form a group whose collectives are device-to-device copies; the sharded algorithm then runs
+ * unchanged with world_size ranks on a single GPU.  Each rank must call from its own thread. */
+int32_t nbg_comm_init_local(nbg_ctx* ctx, int64_t group_key);
 
 /* pure arithmetic helpers (host, no GPU needed) */
 int32_t nbg_part_of(int64_t vid, int32_t num_parts);          /* StorageClient.cpp:238-243 */
@@ -192,6 +196,8 @@ typedef struct {
   uint64_t expand_bytes;  /* algorithmic bytes of the expansion kernels          */
   int32_t steps_run;
   int32_t bu_steps;       /* steps that ran bottom-up over the transposed CSR               */
+  double comm_ms;         /* time in frontier exchanges / reductions between ranks          */
+  uint64_t comm_bytes;    /* bytes this rank sent to other ranks                            */
 } nbg_timing;
 int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out);
 int32_t nbg_set_option(nbg_ctx* ctx, const char* key, int64_t value);

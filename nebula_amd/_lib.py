@@ -26,6 +26,7 @@ OWNER_SOURCE, OWNER_DEST, OWNER_EDGE = 1, 2, 3
 # every symbol the header declares (tests/test_capi.py checks the .so exports them all)
 EXPORTS = [
     "nbg_ctx_create", "nbg_ctx_destroy", "nbg_last_error", "nbg_comm_unique_id", "nbg_comm_init",
+    "nbg_comm_init_local",
     "nbg_part_of", "nbg_rank_of_part", "nbg_schema_set_edge", "nbg_snapshot_load_part",
     "nbg_snapshot_gen_rmat", "nbg_snapshot_finalize", "nbg_snapshot_info_get",
     "nbg_snapshot_out_degree", "nbg_rows_free", "nbg_get_bound", "nbg_go", "nbg_shortest_path",
@@ -69,7 +70,7 @@ class GoSpec(C.Structure):
 class Timing(C.Structure):
     _fields_ = [("total_ms", C.c_double), ("expand_ms", C.c_double), ("expand_launches", C.c_int64),
                 ("edges_scanned", C.c_uint64), ("expand_bytes", C.c_uint64), ("steps_run", C.c_int32),
-                ("bu_steps", C.c_int32)]
+                ("bu_steps", C.c_int32), ("comm_ms", C.c_double), ("comm_bytes", C.c_uint64)]
 
 
 _lib = None
@@ -91,6 +92,7 @@ def load(path: str | os.PathLike | None = None):
         "nbg_last_error": (C.c_char_p, [vp]),
         "nbg_comm_unique_id": (i32, [vp]),
         "nbg_comm_init": (i32, [vp, vp]),
+        "nbg_comm_init_local": (i32, [vp, i64]),
         "nbg_part_of": (i32, [i64, i32]),
         "nbg_rank_of_part": (i32, [i32, i32]),
         "nbg_schema_set_edge": (i32, [vp, i32, i32, i32, C.POINTER(C.c_char_p), C.POINTER(i32)]),

@@ -75,6 +75,13 @@ int32_t nbg_comm_init(nbg_ctx* ctx, const uint8_t unique_id[128]) {
   });
 }
 
+int32_t nbg_comm_init_local(nbg_ctx* ctx, int64_t group_key) {
+  return guarded(ctx, [&](Ctx& c) {
+    nbg::comm_init_local(c, group_key);
+    return NBG_OK;
+  });
+}
+
 int32_t nbg_part_of(int64_t vid, int32_t num_parts) {
   return num_parts > 0 ? nbg::part_of_vid(vid, num_parts) : NBG_E_INVALID_ARG;
 }
@@ -132,8 +139,8 @@ int32_t nbg_snapshot_info_get(nbg_ctx* ctx, int32_t edge_type, nbg_snapshot_info
     if (!out) throw Error(NBG_E_INVALID_ARG, "null out");
     auto it = c.edges.find(edge_type);
     if (it == c.edges.end()) throw Error(NBG_E_INVALID_ARG, "unknown edge type");
-    out->num_vertices = c.n_global;
-    out->local_vertices = c.owned_hi() - c.owned_lo();
+    out->num_vertices = c.n_vertices;
+    out->local_vertices = c.counts.empty() ? 0 : c.counts[size_t(c.rank)];
     out->local_out_edges = it->second.out.nnz;
     out->local_in_edges = it->second.in.nnz;
     out->device_bytes = int64_t(it->second.out.bytes() + it->second.in.bytes() + c.vid_of.bytes + c.ht_keys.bytes +
@@ -213,6 +220,8 @@ int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out) {
     out->expand_bytes = c.timing.expand_bytes;
     out->steps_run = c.timing.steps_run;
     out->bu_steps = c.timing.bu_steps;
+    out->comm_ms = c.timing.comm_ms;
+    out->comm_bytes = c.timing.comm_bytes;
     return NBG_OK;
   });
 }

@@ -1,26 +1,162 @@
-// comm.cpp -- RCCL over xGMI: the multi-GPU replacement of StorageClient's per-host RPC
-// scatter/gather (src/storage/client/StorageClient.inl:74-159).  One process per GPU; every
-// collective runs on the context's stream so it orders with the expansion kernels.
+// comm.cpp -- frontier exchange between ranks: the multi-GPU replacement of StorageClient's
+// per-host RPC scatter/gather (src/storage/client/StorageClient.inl:74-159).
+//
+// Two transports behind one interface:
+//   * RCCL over xGMI (production): one process per GPU; collectives are issued on the
+//     context's stream so they order with the expansion kernels.  Variable-size exchanges use
+//     grouped ncclSend/ncclRecv: on MI355X every peer pair has its own xGMI link, so the 7
+//     transfers of an 8-GPU exchange run concurrently (all-to-all, not ring).
+//   * LocalGroup (tests): several contexts of one process on one device form a group; the same
+//     collective calls become device-to-device copies between the ranks' buffers, so the
+//     sharded algorithm runs unchanged with N ranks on a single GPU.
 #include <rccl/rccl.h>
 
+#include <condition_variable>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "engine.h"
 
 namespace nbg {
 
-#define NBG_NCCL(x)                                                                        \
-  do {                                                                                     \
-    ncclResult_t r_ = (x);                                                                 \
+#define NBG_NCCL(x)                                                                                \
+  do {                                                                                             \
+    ncclResult_t r_ = (x);                                                                         \
     if (r_ != ncclSuccess) throw Error(NBG_E_COMM, std::string(#x) + ": " + ncclGetErrorString(r_)); \
   } while (0)
 
-static ncclComm_t comm_of(Ctx& c) {
-  if (c.world == 1) return nullptr;
-  if (!c.comm) throw Error(NBG_E_STATE, "nbg_comm_init was not called");
-  return static_cast<ncclComm_t>(c.comm);
+struct CommImpl {
+  virtual ~CommImpl() = default;
+  // every rank contributes `send` (send_bytes) into recv + recv_off[r] of every rank
+  virtual void allgatherv(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
+                          const size_t* recv_off) = 0;
+  virtual void alltoallv(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
+                         const size_t* recv_bytes, const size_t* recv_off) = 0;
+  virtual void allreduce_sum_i64(Ctx& c, int64_t* d, size_t n) = 0;
+};
+
+// ------------------------------------------------------------------------------------------
+struct RcclComm : CommImpl {
+  ncclComm_t comm = nullptr;
+  ~RcclComm() override {
+    if (comm) ncclCommDestroy(comm);
+  }
+  void allgatherv(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
+                  const size_t* recv_off) override {
+    NBG_NCCL(ncclGroupStart());
+    for (int p = 0; p < c.world; p++) {
+      if (p == c.rank) continue;
+      if (send_bytes) NBG_NCCL(ncclSend(send, send_bytes, ncclUint8, p, comm, c.stream));
+      if (recv_bytes[p])
+        NBG_NCCL(ncclRecv(static_cast<uint8_t*>(recv) + recv_off[p], recv_bytes[p], ncclUint8, p, comm, c.stream));
+    }
+    NBG_NCCL(ncclGroupEnd());
+    if (send_bytes && static_cast<uint8_t*>(recv) + recv_off[c.rank] != send)
+      NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[c.rank], send, send_bytes,
+                             hipMemcpyDeviceToDevice, c.stream));
+  }
+  void alltoallv(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
+                 const size_t* recv_bytes, const size_t* recv_off) override {
+    NBG_NCCL(ncclGroupStart());
+    for (int p = 0; p < c.world; p++) {
+      if (p == c.rank) continue;
+      if (send_bytes[p])
+        NBG_NCCL(ncclSend(static_cast<const uint8_t*>(send) + send_off[p], send_bytes[p], ncclUint8, p, comm, c.stream));
+      if (recv_bytes[p])
+        NBG_NCCL(ncclRecv(static_cast<uint8_t*>(recv) + recv_off[p], recv_bytes[p], ncclUint8, p, comm, c.stream));
+    }
+    NBG_NCCL(ncclGroupEnd());
+    if (send_bytes[c.rank])
+      NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[c.rank],
+                             static_cast<const uint8_t*>(send) + send_off[c.rank], send_bytes[c.rank],
+                             hipMemcpyDeviceToDevice, c.stream));
+  }
+  void allreduce_sum_i64(Ctx& c, int64_t* d, size_t n) override {
+    NBG_NCCL(ncclAllReduce(d, d, n, ncclInt64, ncclSum, comm, c.stream));
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+struct LocalGroup {
+  int world = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  std::vector<const void*> ptr;
+  std::vector<const size_t*> sizes, offs;
+  std::vector<size_t> scalar;
+  std::vector<std::vector<int64_t>> vals;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    uint64_t g = gen;
+    if (++arrived == world) {
+      arrived = 0;
+      gen++;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+static std::mutex g_groups_mu;
+static std::map<int64_t, std::shared_ptr<LocalGroup>> g_groups;
+
+struct LocalComm : CommImpl {
+  std::shared_ptr<LocalGroup> g;
+  void allgatherv(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
+                  const size_t* recv_off) override {
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    g->ptr[size_t(c.rank)] = send;
+    g->scalar[size_t(c.rank)] = send_bytes;
+    g->barrier();
+    for (int p = 0; p < c.world; p++) {
+      size_t b = std::min(g->scalar[size_t(p)], recv_bytes[p]);
+      if (b) NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[p], g->ptr[size_t(p)], b,
+                                    hipMemcpyDeviceToDevice, c.stream));
+    }
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    g->barrier();
+  }
+  void alltoallv(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
+                 const size_t* recv_bytes, const size_t* recv_off) override {
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    g->ptr[size_t(c.rank)] = send;
+    g->sizes[size_t(c.rank)] = send_bytes;
+    g->offs[size_t(c.rank)] = send_off;
+    g->barrier();
+    for (int p = 0; p < c.world; p++) {
+      size_t b = std::min(g->sizes[size_t(p)][c.rank], recv_bytes[p]);
+      if (b)
+        NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[p],
+                               static_cast<const uint8_t*>(g->ptr[size_t(p)]) + g->offs[size_t(p)][c.rank], b,
+                               hipMemcpyDeviceToDevice, c.stream));
+    }
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    g->barrier();
+  }
+  void allreduce_sum_i64(Ctx& c, int64_t* d, size_t n) override {
+    std::vector<int64_t> h(n);
+    NBG_HIP(hipMemcpyAsync(h.data(), d, n * 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    g->vals[size_t(c.rank)] = h;
+    g->barrier();
+    std::vector<int64_t> s(n, 0);
+    for (int p = 0; p < c.world; p++)
+      for (size_t i = 0; i < n; i++) s[i] += g->vals[size_t(p)][i];
+    g->barrier();
+    NBG_HIP(hipMemcpyAsync(d, s.data(), n * 8, hipMemcpyHostToDevice, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+  }
+};
+
+static CommImpl* impl(Ctx& c) {
+  if (!c.comm) throw Error(NBG_E_STATE, "multi-rank context without a communicator (nbg_comm_init)");
+  return static_cast<CommImpl*>(c.comm);
 }
 
+// ------------------------------------------------------------------------------------------
 int32_t comm_unique_id(uint8_t out[128]) {
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
   ncclUniqueId id;
@@ -31,16 +167,46 @@ int32_t comm_unique_id(uint8_t out[128]) {
 
 void comm_init(Ctx& c, const uint8_t id_bytes[128]) {
   if (c.world == 1) return;
+  if (c.comm) throw Error(NBG_E_STATE, "communicator already initialised");
   ncclUniqueId id;
   memcpy(&id, id_bytes, 128);
   NBG_HIP(hipSetDevice(c.device));
-  ncclComm_t comm;
-  NBG_NCCL(ncclCommInitRank(&comm, c.world, id, c.rank));
-  c.comm = comm;
+  auto* r = new RcclComm();
+  ncclResult_t rc = ncclCommInitRank(&r->comm, c.world, id, c.rank);
+  if (rc != ncclSuccess) {
+    r->comm = nullptr;
+    delete r;
+    throw Error(NBG_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(rc));
+  }
+  c.comm = r;
+}
+
+void comm_init_local(Ctx& c, int64_t key) {
+  if (c.world == 1) return;
+  if (c.comm) throw Error(NBG_E_STATE, "communicator already initialised");
+  std::shared_ptr<LocalGroup> g;
+  {
+    std::lock_guard<std::mutex> lk(g_groups_mu);
+    auto& slot = g_groups[key];
+    if (!slot) {
+      slot = std::make_shared<LocalGroup>();
+      slot->world = c.world;
+      slot->ptr.resize(size_t(c.world));
+      slot->sizes.resize(size_t(c.world));
+      slot->offs.resize(size_t(c.world));
+      slot->scalar.resize(size_t(c.world));
+      slot->vals.resize(size_t(c.world));
+    }
+    g = slot;
+  }
+  if (g->world != c.world) throw Error(NBG_E_INVALID_ARG, "local group world size mismatch");
+  auto* l = new LocalComm();
+  l->g = g;
+  c.comm = l;
 }
 
 void comm_destroy(Ctx& c) {
-  if (c.comm) ncclCommDestroy(static_cast<ncclComm_t>(c.comm));
+  delete static_cast<CommImpl*>(c.comm);
   c.comm = nullptr;
 }
 
@@ -49,11 +215,22 @@ void comm_allgather_bytes(Ctx& c, const void* send, size_t bytes_each, void* rec
     NBG_HIP(hipMemcpyAsync(recv, send, bytes_each, hipMemcpyDeviceToDevice, c.stream));
     return;
   }
-  NBG_NCCL(ncclAllGather(send, recv, bytes_each, ncclUint8, comm_of(c), c.stream));
+  std::vector<size_t> rb(size_t(c.world), bytes_each), ro(size_t(c.world));
+  for (int p = 0; p < c.world; p++) ro[size_t(p)] = size_t(p) * bytes_each;
+  impl(c)->allgatherv(c, send, bytes_each, recv, rb.data(), ro.data());
 }
 
-// all-to-all with per-peer byte counts (grouped point-to-point: on xGMI every peer pair has
-// its own link, so the 7 transfers of an 8-GPU exchange run concurrently)
+void comm_allgatherv_bytes(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
+                           const size_t* recv_off) {
+  if (c.world == 1) {
+    if (send_bytes && static_cast<uint8_t*>(recv) + recv_off[0] != send)
+      NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[0], send, send_bytes, hipMemcpyDeviceToDevice,
+                             c.stream));
+    return;
+  }
+  impl(c)->allgatherv(c, send, send_bytes, recv, recv_bytes, recv_off);
+}
+
 void comm_alltoallv_bytes(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
                           const size_t* recv_bytes, const size_t* recv_off) {
   if (c.world == 1) {
@@ -63,20 +240,12 @@ void comm_alltoallv_bytes(Ctx& c, const void* send, const size_t* send_bytes, co
                              hipMemcpyDeviceToDevice, c.stream));
     return;
   }
-  ncclComm_t comm = comm_of(c);
-  NBG_NCCL(ncclGroupStart());
-  for (int p = 0; p < c.world; p++) {
-    if (send_bytes[p])
-      NBG_NCCL(ncclSend(static_cast<const uint8_t*>(send) + send_off[p], send_bytes[p], ncclUint8, p, comm, c.stream));
-    if (recv_bytes[p])
-      NBG_NCCL(ncclRecv(static_cast<uint8_t*>(recv) + recv_off[p], recv_bytes[p], ncclUint8, p, comm, c.stream));
-  }
-  NBG_NCCL(ncclGroupEnd());
+  impl(c)->alltoallv(c, send, send_bytes, send_off, recv, recv_bytes, recv_off);
 }
 
 void comm_allreduce_sum_i64(Ctx& c, int64_t* d_vals, size_t n) {
   if (c.world == 1) return;
-  NBG_NCCL(ncclAllReduce(d_vals, d_vals, n, ncclInt64, ncclSum, comm_of(c), c.stream));
+  impl(c)->allreduce_sum_i64(c, d_vals, n);
 }
 
 }  // namespace nbg

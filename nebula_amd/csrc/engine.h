@@ -137,8 +137,10 @@ struct EdgeSpace {
   // Transpose of the out CSR for bottom-up steps: row = owned dst, col = global src index,
   // props = copies of the INT-like out props in transpose order, t_eid = out-edge index.
   Csr tr;
-  DevBuf t_eid;   // uint32 [nnz]
+  DevBuf t_eid;   // uint32 [nnz] (single rank only)
   bool has_tr = false;
+  bool has_t_eid = false;
+  int64_t out_nnz_global = -1;  // sum of out.nnz over ranks (direction heuristic)
 };
 
 struct Timing {
@@ -147,6 +149,8 @@ struct Timing {
   uint64_t edges_scanned = 0, expand_bytes = 0;
   int32_t steps_run = 0;
   int32_t bu_steps = 0;
+  double comm_ms = 0;
+  uint64_t comm_bytes = 0;
 };
 
 struct Ctx {
@@ -158,8 +162,10 @@ struct Ctx {
 
   // vertex map
   bool finalized = false;
-  int64_t n_global = 0;
+  int64_t n_global = 0;          // size of the gidx space (owner ranges padded to 64)
+  int64_t n_vertices = 0;        // vertices in the snapshot
   std::vector<int64_t> base;     // G+1
+  std::vector<int64_t> counts;   // vertices per rank
   DevBuf vid_of;                 // int64 [n_global]
   DevBuf ht_keys, ht_vals;       // int64 / int32 [ht_cap]
   int64_t ht_cap = 0;
@@ -179,6 +185,8 @@ struct Ctx {
   DevBuf ws_rows;      // final rows (int32 src idx, int64 edge)
   DevBuf ws_counters;  // small device counters
   DevBuf ws_bits_send, ws_bits_recv;
+  DevBuf ws_bits_glob;  // world > 1: allgathered frontier bitmap / per-owner mark bitmap
+  DevBuf ws_bits_xchg;  // world > 1: received mark segments [world][owned/32]
   DevBuf ws_starts;
   DevBuf ws_partials;  // per-block partial sums of the aggregated kernels
   Timing timing;
@@ -212,6 +220,9 @@ void comm_alltoallv_bytes(Ctx& c, const void* send, const size_t* send_bytes, co
                           void* recv, const size_t* recv_bytes, const size_t* recv_off);
 void comm_allgather_bytes(Ctx& c, const void* send, size_t bytes_each, void* recv);
 void comm_allreduce_sum_i64(Ctx& c, int64_t* d_vals, size_t n);
+void comm_allgatherv_bytes(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
+                           const size_t* recv_off);
+void comm_init_local(Ctx& c, int64_t key);
 void comm_destroy(Ctx& c);
 
 inline double now_s() {

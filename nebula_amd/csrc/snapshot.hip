@@ -512,11 +512,11 @@ __global__ void k_unflip(const uint64_t* in, int64_t* out, int64_t n) {
 }
 
 __global__ void k_ht_insert(int64_t* keys, int32_t* vals, uint64_t mask, const int64_t* vids, int64_t n,
-                            int32_t* min_gidx) {
+                            int64_t gbase, int32_t* min_gidx) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
     int64_t v = vids[i];
     if (v == INT64_MIN) {
-      *min_gidx = int32_t(i);
+      *min_gidx = int32_t(gbase + i);
       continue;
     }
     uint64_t h = ht_hash(v) & mask;
@@ -524,7 +524,7 @@ __global__ void k_ht_insert(int64_t* keys, int32_t* vals, uint64_t mask, const i
       unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(keys + h),
                                           (unsigned long long)INT64_MIN, (unsigned long long)v);
       if (prev == (unsigned long long)INT64_MIN || int64_t(prev) == v) {
-        vals[h] = int32_t(i);
+        vals[h] = int32_t(gbase + i);
         break;
       }
       h = (h + 1) & mask;
@@ -908,52 +908,173 @@ __global__ void k_gather_w(const T* in, const uint32_t* perm, T* out, int64_t m)
     out[i] = in[perm[i]];
 }
 
-// Transpose of the out CSR (single rank): rows = dst, entries = src, plus INT-like prop copies.
+__global__ void k_sorted_bounds(const uint32_t* keys, int64_t m, const int64_t* bounds, int nb, int64_t* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb) return;
+  int64_t lo = 0, hi = m, x = bounds[i];  // first index with key >= x
+  while (lo < hi) {
+    int64_t mid = (lo + hi) >> 1;
+    if (int64_t(keys[mid]) < x) lo = mid + 1; else hi = mid;
+  }
+  out[i] = lo;
+}
+__global__ void k_src_global(const uint32_t* perm, const int32_t* esrc, int64_t m, int64_t lo, int32_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = int32_t(lo) + esrc[perm[i]];
+}
+__global__ void k_sub_lo(const int32_t* in, int64_t m, int64_t lo, uint32_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = uint32_t(in[i] - lo);
+}
+static void gather_width(Ctx& c, const void* in, const uint32_t* perm, void* out, int64_t m, int w) {
+  int g = grid_for(m);
+  switch (w) {
+    case 1: k_gather_w<int8_t><<<g, 256, 0, c.stream>>>(static_cast<const int8_t*>(in), perm, static_cast<int8_t*>(out), m); break;
+    case 2: k_gather_w<int16_t><<<g, 256, 0, c.stream>>>(static_cast<const int16_t*>(in), perm, static_cast<int16_t*>(out), m); break;
+    case 4: k_gather_w<int32_t><<<g, 256, 0, c.stream>>>(static_cast<const int32_t*>(in), perm, static_cast<int32_t*>(out), m); break;
+    default: k_gather_w<int64_t><<<g, 256, 0, c.stream>>>(static_cast<const int64_t*>(in), perm, static_cast<int64_t*>(out), m);
+  }
+}
+static bool copy_prop(const PropCol& p) {
+  bool intlike = p.type == NBG_T_INT || p.type == NBG_T_VID || p.type == NBG_T_TIMESTAMP || p.type == NBG_T_BOOL;
+  return intlike && !p.present.p;
+}
+
+// Transpose of the out CSR for bottom-up hops: rows = owned dst, entries = global src index,
+// plus copies of the INT-like props in transpose order.  With several ranks every out-edge is
+// shipped to the owner of its dst (one build-time all-to-all), so each rank can run bottom-up
+// hops over its own vertices against the allgathered frontier bitmap.
 static void build_transpose(Ctx& c, EdgeSpace& es) {
   Csr& o = es.out;
   Csr& t = es.tr;
-  int64_t m = o.nnz;
-  int64_t n = c.n_global;
-  t.n_rows = n;
-  t.nnz = m;
-  t.row_ptr.alloc(size_t(n + 1) * 8);
-  t.col.alloc(size_t(m + 1) * 4);
-  es.t_eid.alloc(size_t(m + 1) * 4);
-  if (m == 0) {
-    NBG_HIP(hipMemsetAsync(t.row_ptr.p, 0, size_t(n + 1) * 8, c.stream));
-  } else {
-    DevBuf esrc, keysB, iota;
-    esrc.alloc(size_t(m) * 4);
-    keysB.alloc(size_t(m) * 4);
-    iota.alloc(size_t(m) * 4);
+  const int64_t m = o.nnz;
+  const int64_t lo = c.owned_lo(), hi = c.owned_hi();
+  const int G = c.world;
+  int bits = 1;
+  while ((int64_t(1) << bits) < std::max<int64_t>(c.n_global, 2)) bits++;
+  // local out-edges sorted by dst gidx
+  DevBuf esrc, keysB, iota, perm;
+  esrc.alloc(size_t(m + 1) * 4);
+  keysB.alloc(size_t(m + 1) * 4);
+  iota.alloc(size_t(m + 1) * 4);
+  perm.alloc(size_t(m + 1) * 4);
+  if (m) {
     k_edge_src<<<grid_for(o.n_rows), 256, 0, c.stream>>>(o.row_ptr.as<int64_t>(), o.n_rows, esrc.as<int32_t>());
     k_iota_u32<<<grid_for(m), 256, 0, c.stream>>>(iota.as<uint32_t>(), m);
-    int bits = 1;
-    while ((int64_t(1) << bits) < std::max<int64_t>(n, 2)) bits++;
     radix_pairs<uint32_t, uint32_t>(c, o.col.as<uint32_t>(), keysB.as<uint32_t>(), iota.as<uint32_t>(),
-                                   es.t_eid.as<uint32_t>(), m, bits);
-    k_tr_col<<<grid_for(m), 256, 0, c.stream>>>(es.t_eid.as<uint32_t>(), esrc.as<int32_t>(), m, c.owned_lo(),
-                                              t.col.as<int32_t>());
-    k_rowptr_sorted<<<grid_for(m + 1), 256, 0, c.stream>>>(keysB.as<uint32_t>(), m, n, t.row_ptr.as<int64_t>());
+                                   perm.as<uint32_t>(), m, bits);
   }
+  iota.release();
+  std::vector<const PropCol*> cp;
+  for (const PropCol& p : o.props) cp.push_back(copy_prop(p) ? &p : nullptr);
+  t.n_rows = hi - lo;
+  t.props.clear();
   for (const PropCol& p : o.props) {
     PropCol q;
     q.name = p.name;
     q.type = p.type;
     q.width = p.width;
-    bool intlike = p.type == NBG_T_INT || p.type == NBG_T_VID || p.type == NBG_T_TIMESTAMP || p.type == NBG_T_BOOL;
-    if (intlike && !p.present.p && m) {
-      q.data.alloc(size_t(m) * size_t(p.width) + 16);
-      int g = grid_for(m);
-      const uint32_t* pe = es.t_eid.as<uint32_t>();
-      switch (p.width) {
-        case 1: k_gather_w<int8_t><<<g, 256, 0, c.stream>>>(p.data.as<int8_t>(), pe, q.data.as<int8_t>(), m); break;
-        case 2: k_gather_w<int16_t><<<g, 256, 0, c.stream>>>(p.data.as<int16_t>(), pe, q.data.as<int16_t>(), m); break;
-        case 4: k_gather_w<int32_t><<<g, 256, 0, c.stream>>>(p.data.as<int32_t>(), pe, q.data.as<int32_t>(), m); break;
-        default: k_gather_w<int64_t><<<g, 256, 0, c.stream>>>(p.data.as<int64_t>(), pe, q.data.as<int64_t>(), m);
-      }
-    }
     t.props.push_back(std::move(q));
+  }
+  t.row_ptr.alloc(size_t(t.n_rows + 1) * 8);
+  if (G == 1) {
+    t.nnz = m;
+    t.col.alloc(size_t(m + 1) * 4);
+    es.t_eid = std::move(perm);
+    if (m) {
+      k_tr_col<<<grid_for(m), 256, 0, c.stream>>>(es.t_eid.as<uint32_t>(), esrc.as<int32_t>(), m, lo, t.col.as<int32_t>());
+      k_rowptr_sorted<<<grid_for(m + 1), 256, 0, c.stream>>>(keysB.as<uint32_t>(), m, t.n_rows, t.row_ptr.as<int64_t>());
+    } else {
+      NBG_HIP(hipMemsetAsync(t.row_ptr.p, 0, size_t(t.n_rows + 1) * 8, c.stream));
+    }
+    for (size_t f = 0; f < o.props.size(); f++)
+      if (cp[f] && m) {
+        t.props[f].data.alloc(size_t(m) * size_t(cp[f]->width) + 16);
+        gather_width(c, cp[f]->data.p, es.t_eid.as<uint32_t>(), t.props[f].data.p, m, cp[f]->width);
+      }
+    es.has_t_eid = true;
+  } else {
+    // per-owner ranges of the dst-sorted edges
+    DevBuf dbase, dcut;
+    dbase.alloc(size_t(G + 1) * 8);
+    dcut.alloc(size_t(G + 1) * 8);
+    NBG_HIP(hipMemcpyAsync(dbase.p, c.base.data(), size_t(G + 1) * 8, hipMemcpyHostToDevice, c.stream));
+    k_sorted_bounds<<<1, 64, 0, c.stream>>>(keysB.as<uint32_t>(), m, dbase.as<int64_t>(), G + 1, dcut.as<int64_t>());
+    std::vector<int64_t> cut(size_t(G + 1));
+    NBG_HIP(hipMemcpyAsync(cut.data(), dcut.p, size_t(G + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    cut[size_t(G)] = m;
+    // send buffers in dst-sorted order
+    DevBuf ssrc, sprops;
+    ssrc.alloc(size_t(m + 1) * 4);
+    if (m) k_src_global<<<grid_for(m), 256, 0, c.stream>>>(perm.as<uint32_t>(), esrc.as<int32_t>(), m, lo, ssrc.as<int32_t>());
+    // count matrix
+    std::vector<int64_t> mine(static_cast<size_t>(G)), all(static_cast<size_t>(G) * static_cast<size_t>(G));
+    for (int h = 0; h < G; h++) mine[size_t(h)] = cut[size_t(h + 1)] - cut[size_t(h)];
+    {
+      DevBuf dm, da;
+      dm.alloc(size_t(G) * 8);
+      da.alloc(size_t(G) * size_t(G) * 8);
+      NBG_HIP(hipMemcpyAsync(dm.p, mine.data(), size_t(G) * 8, hipMemcpyHostToDevice, c.stream));
+      comm_allgather_bytes(c, dm.p, size_t(G) * 8, da.p);
+      NBG_HIP(hipMemcpyAsync(all.data(), da.p, size_t(G) * size_t(G) * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+    }
+    int64_t R = 0;
+    std::vector<int64_t> roff(size_t(G) + 1, 0);
+    for (int p = 0; p < G; p++) {
+      int64_t from_p = all[size_t(p) * size_t(G) + size_t(c.rank)];
+      roff[size_t(p) + 1] = roff[size_t(p)] + from_p;
+    }
+    R = roff[size_t(G)];
+    auto exchange = [&](const void* send, void* recv, int w) {
+      const size_t ng = static_cast<size_t>(G);
+      std::vector<size_t> sb(ng), so(ng), rb(ng), ro(ng);
+      for (int p = 0; p < G; p++) {
+        sb[size_t(p)] = size_t(mine[size_t(p)]) * size_t(w);
+        so[size_t(p)] = size_t(cut[size_t(p)]) * size_t(w);
+        rb[size_t(p)] = size_t(roff[size_t(p) + 1] - roff[size_t(p)]) * size_t(w);
+        ro[size_t(p)] = size_t(roff[size_t(p)]) * size_t(w);
+      }
+      comm_alltoallv_bytes(c, send, sb.data(), so.data(), recv, rb.data(), ro.data());
+    };
+    DevBuf rsrc, rdst, rkey, rperm, riota;
+    rsrc.alloc(size_t(R + 1) * 4);
+    rdst.alloc(size_t(R + 1) * 4);
+    exchange(ssrc.p, rsrc.p, 4);
+    exchange(keysB.p, rdst.p, 4);
+    // received edges sorted by local dst
+    rkey.alloc(size_t(R + 1) * 4);
+    DevBuf rkeyS;
+    rkeyS.alloc(size_t(R + 1) * 4);
+    rperm.alloc(size_t(R + 1) * 4);
+    riota.alloc(size_t(R + 1) * 4);
+    t.nnz = R;
+    t.col.alloc(size_t(R + 1) * 4);
+    if (R) {
+      k_sub_lo<<<grid_for(R), 256, 0, c.stream>>>(rdst.as<int32_t>(), R, lo, rkey.as<uint32_t>());
+      k_iota_u32<<<grid_for(R), 256, 0, c.stream>>>(riota.as<uint32_t>(), R);
+      int lbits = 1;
+      while ((int64_t(1) << lbits) < std::max<int64_t>(t.n_rows, 2)) lbits++;
+      radix_pairs<uint32_t, uint32_t>(c, rkey.as<uint32_t>(), rkeyS.as<uint32_t>(), riota.as<uint32_t>(),
+                                     rperm.as<uint32_t>(), R, lbits);
+      k_gather_w<int32_t><<<grid_for(R), 256, 0, c.stream>>>(rsrc.as<int32_t>(), rperm.as<uint32_t>(), t.col.as<int32_t>(), R);
+      k_rowptr_sorted<<<grid_for(R + 1), 256, 0, c.stream>>>(rkeyS.as<uint32_t>(), R, t.n_rows, t.row_ptr.as<int64_t>());
+    } else {
+      NBG_HIP(hipMemsetAsync(t.row_ptr.p, 0, size_t(t.n_rows + 1) * 8, c.stream));
+    }
+    for (size_t f = 0; f < o.props.size(); f++) {
+      if (!cp[f]) continue;
+      int w = cp[f]->width;
+      DevBuf sp, rp;
+      sp.alloc(size_t(m + 1) * size_t(w));
+      rp.alloc(size_t(R + 1) * size_t(w));
+      if (m) gather_width(c, cp[f]->data.p, perm.as<uint32_t>(), sp.p, m, w);
+      exchange(sp.p, rp.p, w);
+      t.props[f].data.alloc(size_t(R) * size_t(w) + 16);
+      if (R) gather_width(c, rp.p, rperm.as<uint32_t>(), t.props[f].data.p, R, w);
+    }
+    es.has_t_eid = false;
   }
   NBG_HIP(hipStreamSynchronize(c.stream));
   NBG_HIP(hipGetLastError());
@@ -1060,11 +1181,17 @@ void snapshot_finalize(Ctx& c) {
     NBG_HIP(hipMemcpyAsync(counts.data(), dsz.p, 8 * size_t(c.world), hipMemcpyDeviceToHost, c.stream));
     NBG_HIP(hipStreamSynchronize(c.stream));
   }
+  // owner ranges padded to 64 vertices: every rank's slice of a frontier bitmap starts on a
+  // 64-bit word, so bitmap slices are exchanged without shifting (holes have no edges)
   c.base.assign(size_t(c.world) + 1, 0);
-  for (int r = 0; r < c.world; r++) c.base[size_t(r) + 1] = c.base[size_t(r)] + counts[size_t(r)];
+  c.counts = counts;
+  for (int r = 0; r < c.world; r++) c.base[size_t(r) + 1] = c.base[size_t(r)] + ((counts[size_t(r)] + 63) / 64) * 64;
   c.n_global = c.base[size_t(c.world)];
+  c.n_vertices = 0;
+  for (auto x : counts) c.n_vertices += x;
   if (c.n_global >= (int64_t(1) << 31)) throw Error(NBG_E_UNSUPPORTED, "more than 2^31 vertices");
   c.vid_of.alloc(size_t(std::max<int64_t>(c.n_global, 1)) * 8);
+  fill<int64_t>(c, c.vid_of.as<int64_t>(), INT64_MIN, c.n_global);
   if (c.world == 1) {
     if (n_owned) k_unflip<<<grid_for(n_owned), 256, 0, c.stream>>>(owned.as<uint64_t>(), c.vid_of.as<int64_t>(), n_owned);
   } else {
@@ -1092,10 +1219,11 @@ void snapshot_finalize(Ctx& c) {
   dmin.alloc(4);
   int32_t neg = -1;
   NBG_HIP(hipMemcpyAsync(dmin.p, &neg, 4, hipMemcpyHostToDevice, c.stream));
-  if (c.n_global)
-    k_ht_insert<<<grid_for(c.n_global), 256, 0, c.stream>>>(c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
-                                                           uint64_t(cap - 1), c.vid_of.as<int64_t>(), c.n_global,
-                                                           dmin.as<int32_t>());
+  for (int r = 0; r < c.world; r++)
+    if (counts[size_t(r)])
+      k_ht_insert<<<grid_for(counts[size_t(r)]), 256, 0, c.stream>>>(
+          c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(), uint64_t(cap - 1), c.vid_of.as<int64_t>() + c.base[size_t(r)],
+          counts[size_t(r)], c.base[size_t(r)], dmin.as<int32_t>());
   NBG_HIP(hipMemcpyAsync(&c.ht_min_gidx, dmin.p, 4, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
   c.ht_has_min = c.ht_min_gidx >= 0;
@@ -1120,7 +1248,7 @@ void snapshot_finalize(Ctx& c) {
     EdgeSpace& es = kv.second;
     build_csr(c, es.out_stage, es.fields, true, es.out, brank.as<uint32_t>());
     build_csr(c, es.in_stage, es.fields, false, es.in, brank.as<uint32_t>());
-    if (c.world == 1 && c.opt("bottom_up", 1)) build_transpose(c, es);
+    if (c.opt("bottom_up", 1)) build_transpose(c, es);
   }
   c.heap.release();
   c.heap_used = 0;

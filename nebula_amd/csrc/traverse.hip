@@ -702,6 +702,41 @@ __global__ void k_list_starts(const int32_t* g, int64_t n, int64_t lo, int64_t h
   }
 }
 
+// ---- multi-rank frontier exchange ----------------------------------------------------------
+// global byte-map -> 32-bit mark words (one word per thread), clearing the map
+__global__ void k_map_to_bits(uint8_t* map, int64_t n, uint32_t* bits) {
+  const int64_t nw = (n + 31) / 32;
+  for (int64_t w = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; w < nw; w += int64_t(gridDim.x) * blockDim.x) {
+    uint4* p = reinterpret_cast<uint4*>(map + w * 32);
+    uint4 a = p[0], b = p[1];
+    const uint32_t x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if ((x[i] >> (8 * k)) & 0xff) m |= 1u << (i * 4 + k);
+    bits[w] = m;
+    if (m) {
+      p[0] = make_uint4(0, 0, 0, 0);
+      p[1] = make_uint4(0, 0, 0, 0);
+    }
+  }
+}
+// OR the [G][nw] received mark words and set the owned slice of the byte-map
+__global__ void k_or_segments_to_map(const uint32_t* recv, int G, int64_t nw, uint8_t* map_lo) {
+  for (int64_t w = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; w < nw; w += int64_t(gridDim.x) * blockDim.x) {
+    uint32_t m = 0;
+    for (int p = 0; p < G; p++) m |= recv[size_t(p) * size_t(nw) + size_t(w)];
+    for (; m; m &= m - 1) map_lo[w * 32 + (__ffs(m) - 1)] = 1;
+  }
+}
+// DISTINCT over rows with several ranks: rows are shuffled to rank hash(row) % G first
+__global__ void k_flag_dest(const uint32_t* dest, int64_t n, uint32_t p, uint8_t* flag) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    flag[i] = dest[i] == p;
+}
+
 // gidx list (local indices + lo) -> vids
 __global__ void k_local_to_vid(const int32_t* loc, int64_t n, int64_t lo, const int64_t* vid_of, int64_t* out) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
@@ -778,6 +813,11 @@ __global__ void k_row_dedup(YieldArgs ya, int64_t n, long long* table, uint64_t 
     }
     keep[i] = k;
   }
+}
+
+__global__ void k_row_dest(YieldArgs ya, int64_t n, uint32_t G, uint32_t* dest) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    dest[i] = uint32_t((row_hash(ya, i) >> 17) % G);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -861,6 +901,162 @@ void ensure_workspaces(Ctx& c, int64_t nF_cap) {
   c.ws_partials.ensure(size_t(kAggBlocks) * 4 * 8);
   c.ws_bits_send.ensure(size_t(mb / 8 + 64));
   c.ws_bits_recv.ensure(size_t(mb / 8 + 64));
+  if (c.world > 1) {
+    c.ws_bits_glob.ensure(size_t(mb / 8 + 64));
+    c.ws_bits_xchg.ensure(size_t(c.world) * size_t((c.owned_hi() - c.owned_lo()) / 8) + 64);
+  }
+}
+
+// ---- cross-rank helpers (no-ops with one rank) ---------------------------------------------
+struct CommTimer {
+  Ctx& c;
+  explicit CommTimer(Ctx& cc) : c(cc) { hipEventRecord(c.ev[4], c.stream); }
+  ~CommTimer() {
+    hipEventRecord(c.ev[5], c.stream);
+    if (hipEventSynchronize(c.ev[5]) == hipSuccess) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, c.ev[4], c.ev[5]);
+      c.timing.comm_ms += ms;
+    }
+  }
+};
+
+// element-wise sum of a few host counters over ranks
+void allsum(Ctx& c, int64_t* v, int n, unsigned long long* dscratch) {
+  if (c.world == 1) return;
+  CommTimer t(c);
+  NBG_HIP(hipMemcpyAsync(dscratch, v, size_t(n) * 8, hipMemcpyHostToDevice, c.stream));
+  comm_allreduce_sum_i64(c, reinterpret_cast<int64_t*>(dscratch), size_t(n));
+  NBG_HIP(hipMemcpyAsync(v, dscratch, size_t(n) * 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+}
+
+// owned frontier bitmap -> bitmap over the whole gidx space (bottom-up hops read sources of
+// every rank).  Owner ranges are padded to 64, so every segment is whole 64-bit words.
+const uint32_t* global_bits(Ctx& c, const uint32_t* owned) {
+  if (c.world == 1) return owned;
+  CommTimer t(c);
+  const size_t G = size_t(c.world);
+  std::vector<size_t> rb(G), ro(G);
+  for (size_t p = 0; p < G; p++) {
+    rb[p] = size_t(c.base[p + 1] - c.base[p]) / 8;
+    ro[p] = size_t(c.base[p]) / 8;
+  }
+  comm_allgatherv_bytes(c, owned, rb[size_t(c.rank)], c.ws_bits_glob.p, rb.data(), ro.data());
+  c.timing.comm_bytes += uint64_t(rb[size_t(c.rank)]) * (G - 1);
+  return c.ws_bits_glob.as<uint32_t>();
+}
+
+// top-down hops mark dsts of every rank in the global byte-map: ship each owner its slice as
+// a bitmap and OR the received slices back into the owned range of the map
+void exchange_marks(Ctx& c, uint8_t* map) {
+  if (c.world == 1) return;
+  CommTimer t(c);
+  const size_t G = size_t(c.world);
+  const int64_t lo = c.owned_lo(), n_own = c.owned_hi() - lo;
+  uint32_t* sb = c.ws_bits_glob.as<uint32_t>();
+  uint32_t* rbuf = c.ws_bits_xchg.as<uint32_t>();
+  int64_t nw = c.n_global / 32;
+  k_map_to_bits<<<grid_cap(nw), 256, 0, c.stream>>>(map, c.n_global, sb);
+  NBG_HIP(hipGetLastError());
+  std::vector<size_t> sbytes(G), soff(G), rbytes(G), roff(G);
+  for (size_t p = 0; p < G; p++) {
+    sbytes[p] = size_t(c.base[p + 1] - c.base[p]) / 8;
+    soff[p] = size_t(c.base[p]) / 8;
+    rbytes[p] = size_t(n_own) / 8;
+    roff[p] = p * size_t(n_own) / 8;
+  }
+  comm_alltoallv_bytes(c, sb, sbytes.data(), soff.data(), rbuf, rbytes.data(), roff.data());
+  c.timing.comm_bytes += uint64_t(c.n_global - n_own) / 8;
+  k_or_segments_to_map<<<grid_cap(n_own / 32), 256, 0, c.stream>>>(rbuf, int(G), n_own / 32, map + lo);
+  NBG_HIP(hipGetLastError());
+}
+
+__global__ void k_hist_dest(const uint32_t* dest, int64_t n, int G, unsigned long long* counts) {
+  __shared__ unsigned int h[64];
+  if (threadIdx.x < 64) h[threadIdx.x] = 0;
+  __syncthreads();
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    atomicAdd(&h[dest[i]], 1u);
+  __syncthreads();
+  if (threadIdx.x < unsigned(G) && h[threadIdx.x]) atomicAdd(counts + threadIdx.x, (unsigned long long)h[threadIdx.x]);
+}
+
+// DISTINCT with several ranks: every row goes to rank hash(row) % G (all copies of a row meet
+// on one rank), then the local dedup runs as with one rank.  Returns the received row count.
+int64_t shuffle_rows(Ctx& c, YieldArgs& ya, std::vector<DevBuf>& cols, int64_t n) {
+  CommTimer t(c);
+  const size_t G = size_t(c.world);
+  if (G > 64) throw Error(NBG_E_UNSUPPORTED, "more than 64 ranks");
+  DevBuf dest, flag, cnt, dcounts;
+  dest.alloc(size_t(n + 1) * 4);
+  flag.alloc(size_t(n + 1));
+  cnt.alloc(8);
+  dcounts.alloc(G * G * 8 + 8);
+  NBG_HIP(hipMemsetAsync(dcounts.p, 0, G * 8, c.stream));
+  if (n) {
+    k_row_dest<<<grid_cap(n), 256, 0, c.stream>>>(ya, n, uint32_t(G), dest.as<uint32_t>());
+    k_hist_dest<<<grid_cap(n), 256, 0, c.stream>>>(dest.as<uint32_t>(), n, int(G), dcounts.as<unsigned long long>());
+  }
+  std::vector<int64_t> all(G * G);
+  DevBuf dall;
+  dall.alloc(G * G * 8);
+  comm_allgather_bytes(c, dcounts.p, G * 8, dall.p);
+  NBG_HIP(hipMemcpyAsync(all.data(), dall.p, G * G * 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  const size_t me = size_t(c.rank);
+  std::vector<int64_t> soff(G + 1, 0), roff(G + 1, 0);
+  for (size_t p = 0; p < G; p++) {
+    soff[p + 1] = soff[p] + all[me * G + p];
+    roff[p + 1] = roff[p] + all[p * G + me];
+  }
+  const int64_t R = roff[G];
+  std::vector<DevBuf> send(cols.size()), recv(cols.size());
+  for (size_t cc = 0; cc < cols.size(); cc++) {
+    size_t w = ya.cols[cc].type == VT_BOOL ? 1 : 8;
+    send[cc].alloc(size_t(n + 1) * w);
+    recv[cc].alloc(size_t(R + 1) * w);
+  }
+  for (size_t p = 0; p < G && n; p++) {
+    if (!all[me * G + p]) continue;
+    k_flag_dest<<<grid_cap(n), 256, 0, c.stream>>>(dest.as<uint32_t>(), n, uint32_t(p), flag.as<uint8_t>());
+    for (size_t cc = 0; cc < cols.size(); cc++) {
+      size_t tb = 0;
+      if (ya.cols[cc].type == VT_BOOL) {
+        uint8_t* o = send[cc].as<uint8_t>() + soff[p];
+        NBG_HIP(rocprim::select(nullptr, tb, cols[cc].as<uint8_t>(), flag.as<uint8_t>(), o, cnt.as<uint64_t>(),
+                                size_t(n), c.stream));
+        c.ws_tmp.ensure(tb);
+        NBG_HIP(rocprim::select(c.ws_tmp.p, tb, cols[cc].as<uint8_t>(), flag.as<uint8_t>(), o, cnt.as<uint64_t>(),
+                                size_t(n), c.stream));
+      } else {
+        int64_t* o = send[cc].as<int64_t>() + soff[p];
+        NBG_HIP(rocprim::select(nullptr, tb, cols[cc].as<int64_t>(), flag.as<uint8_t>(), o, cnt.as<uint64_t>(),
+                                size_t(n), c.stream));
+        c.ws_tmp.ensure(tb);
+        NBG_HIP(rocprim::select(c.ws_tmp.p, tb, cols[cc].as<int64_t>(), flag.as<uint8_t>(), o, cnt.as<uint64_t>(),
+                                size_t(n), c.stream));
+      }
+    }
+  }
+  for (size_t cc = 0; cc < cols.size(); cc++) {
+    size_t w = ya.cols[cc].type == VT_BOOL ? 1 : 8;
+    std::vector<size_t> sb(G), so(G), rb(G), ro(G);
+    for (size_t p = 0; p < G; p++) {
+      sb[p] = size_t(soff[p + 1] - soff[p]) * w;
+      so[p] = size_t(soff[p]) * w;
+      rb[p] = size_t(roff[p + 1] - roff[p]) * w;
+      ro[p] = size_t(roff[p]) * w;
+    }
+    comm_alltoallv_bytes(c, send[cc].p, sb.data(), so.data(), recv[cc].p, rb.data(), ro.data());
+    c.timing.comm_bytes += uint64_t(n - (soff[me + 1] - soff[me])) * w;
+  }
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  for (size_t cc = 0; cc < cols.size(); cc++) {
+    cols[cc] = std::move(recv[cc]);
+    ya.cols[cc].data = cols[cc].p;
+  }
+  return R;
 }
 
 // frontier degree scan: fills c.ws_off[0..nF] and returns total edges (synchronises)
@@ -1032,9 +1228,11 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     NBG_HIP(hipStreamSynchronize(c.stream));
     nF = int64_t(K.h[0]);
   }
-  if (c.world > 1) {
-    // frontier emptiness is global
-    throw Error(NBG_E_UNSUPPORTED, "multi-GPU GO is built in the comm path (see go_run_dist)");
+  unsigned long long* red = K.d + 24;  // scratch of the cross-rank sums
+  if (es.out_nnz_global < 0) {
+    int64_t v = csr.nnz;
+    allsum(c, &v, 1, red);
+    es.out_nnz_global = v;
   }
   auto finish_empty = [&]() -> int32_t {
     auto* h = new HostRows();
@@ -1093,21 +1291,25 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       off_ready = true;
     }
   };
-  auto want_bu = [&](int64_t e) {
-    return e > 0 && bu_ok && bu_force >= 0 && (bu_force > 0 || e >= csr.nnz / bu_div);
+  // direction choice is global (every rank must take the same branch: bottom-up allgathers)
+  auto want_bu = [&](int64_t eg) {
+    return eg > 0 && bu_ok && bu_force >= 0 && (bu_force > 0 || eg >= es.out_nnz_global / bu_div);
   };
   ensure_off();
+  int64_t Eg = E;  // frontier out-degree sum over all ranks
+  allsum(c, &Eg, 1, red);
   for (int32_t step = 1; step < s.steps; step++) {
     c.timing.steps_run++;
     c.timing.edges_scanned += uint64_t(E);
-    if (E == 0) return finish_empty();  // every frontier vertex lacks out-edges
-    if (want_bu(E)) {
+    if (Eg == 0) return finish_empty();  // every frontier vertex lacks out-edges
+    if (want_bu(Eg)) {
       // bottom-up: frontier bitmap in, next frontier bitmap out
       NBG_HIP(hipMemsetAsync(K.d, 0, 24, c.stream));
       const Csr& tr = es.tr;
       int grid = grid_cap(tr.n_rows, 256, int(std::min<int64_t>(c.opt("bu_grid", 4096), kAggBlocks)));
+      const uint32_t* fb = global_bits(c, bitsA);
       hipEventRecord(c.ev[2], c.stream);
-      k_bu_bits<PK_NONE><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows, bitsA,
+      k_bu_bits<PK_NONE><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows, fb,
                                                      reinterpret_cast<unsigned long long*>(bitsB), row_ptr, row_ok, fp,
                                                      partials);
       k_reduce_partials<<<1, 256, 0, c.stream>>>(partials, grid, K.d);
@@ -1124,15 +1326,21 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       std::swap(bitsA, bitsB);
       have_list = false;
       off_ready = false;
-      nset_global = int64_t(K.h[0]);
       E = int64_t(K.h[1]);
+      int64_t g2[2] = {int64_t(K.h[0]), E};
+      allsum(c, g2, 2, red);
+      nset_global = g2[0];
+      Eg = g2[1];
     } else {
       ensure_off();
       a.F = F;
       a.nF = nF;
       a.off = c.ws_off.as<int64_t>();
-      launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, E);
-      c.timing.expand_bytes += expand_bytes(nF, E, 0, EXP_MARK);
+      if (E > 0) {
+        launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, E);
+        c.timing.expand_bytes += expand_bytes(nF, E, 0, EXP_MARK);
+      }
+      exchange_marks(c, map);
       // next frontier = set of dsts (P12): compact, drop rows without out-edges, bitmap too
       cur ^= 1;
       F = c.ws_front[cur].as<int32_t>();
@@ -1141,8 +1349,11 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 128, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
       nF = int64_t(K.h[0]);
-      nset_global = int64_t(K.h[12]);
       E = int64_t(K.h[13]);
+      int64_t g2[2] = {int64_t(K.h[12]), E};
+      allsum(c, g2, 2, red);
+      nset_global = g2[0];
+      Eg = g2[1];
       have_list = true;
       off_ready = false;
     }
@@ -1176,7 +1387,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // row's eval error, so every row must be evaluated when errors are possible).
       bool pred_bu = pk == PK_NONE || (pk == PK_FAST && fp.present == nullptr &&
                                        es.tr.props.size() > size_t(fpk.col) && es.tr.props[size_t(fpk.col)].data.p);
-      bool bu = pred_bu && want_bu(E);
+      bool bu = pred_bu && want_bu(Eg);
       DevBuf vids;
       vids.alloc(size_t(c.n_global + 64) * 8);
       if (bu) {
@@ -1186,12 +1397,13 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         NBG_HIP(hipMemsetAsync(K.d, 0, 8, c.stream));
         int grid = grid_cap(tr.n_rows, 256, int(std::min<int64_t>(c.opt("bu_grid", 4096), kAggBlocks)));
         unsigned long long* ob = reinterpret_cast<unsigned long long*>(bitsB);
+        const uint32_t* fb = global_bits(c, bitsA);
         hipEventRecord(c.ev[2], c.stream);
         if (pk == PK_FAST)
-          k_bu_bits<PK_FAST><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows, bitsA,
+          k_bu_bits<PK_FAST><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows, fb,
                                                          ob, nullptr, nullptr, tfp, partials);
         else
-          k_bu_bits<PK_NONE><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows, bitsA,
+          k_bu_bits<PK_NONE><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows, fb,
                                                          ob, nullptr, nullptr, tfp, partials);
         k_reduce_partials<<<1, 256, 0, c.stream>>>(partials, grid, K.d + 8);
         k_bits_compact<1><<<grid_cap((tr.n_rows + 31) / 32, 1024, 4096), 256, 0, c.stream>>>(
@@ -1218,16 +1430,19 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
           launch_expand<EXP_MARK>(c, a, pk, fp, dprog.as<Program>(), env, E);
           c.timing.expand_bytes += expand_bytes(nF, E, pred_w, EXP_MARK);
         }
+        exchange_marks(c, map);
         DevBuf lst;
-        lst.alloc(size_t(c.n_global + 64) * 4);
+        lst.alloc(size_t(n_own + 64) * 4);
         NBG_HIP(hipMemsetAsync(K.d, 0, 16, c.stream));  // keep the eval-error counter (K.d[4])
-        launch_compact(c, map, 0, c.n_global, row_ptr, nullptr, 0, lst.as<int32_t>(), nullptr, K.d);
+        launch_compact(c, map, lo, n_own, row_ptr, nullptr, 0, lst.as<int32_t>(), nullptr, K.d);
         NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
         NBG_HIP(hipStreamSynchronize(c.stream));
-        if (K.h[4]) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
+        int64_t errs = int64_t(K.h[4]);
+        allsum(c, &errs, 1, red);
+        if (errs) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
         nrows = int64_t(K.h[0]);
         if (nrows)
-          k_local_to_vid<<<grid_cap(nrows), 256, 0, c.stream>>>(lst.as<int32_t>(), nrows, 0, c.vid_of.as<int64_t>(),
+          k_local_to_vid<<<grid_cap(nrows), 256, 0, c.stream>>>(lst.as<int32_t>(), nrows, lo, c.vid_of.as<int64_t>(),
                                                                vids.as<int64_t>());
       }
       h->types.push_back(NBG_T_VID);
@@ -1251,7 +1466,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       }
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
-      if (K.h[4]) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
+      int64_t errs = int64_t(K.h[4]);
+      allsum(c, &errs, 1, red);
+      if (errs) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
       nrows = int64_t(K.h[2]);
       c.timing.expand_bytes += uint64_t(nrows) * 12;
       YieldArgs ya{};
@@ -1273,13 +1490,17 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
                                                                env, lo, K.d + 5);
         }
         NBG_HIP(hipGetLastError());
-        NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
-        NBG_HIP(hipStreamSynchronize(c.stream));
-        if (K.h[5]) throw Error(NBG_E_EVAL, "YIELD evaluation failed");
       }
+      NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      int64_t yerr = int64_t(K.h[5]);
+      allsum(c, &yerr, 1, red);
+      if (yerr) throw Error(NBG_E_EVAL, "YIELD evaluation failed");
+      if (s.distinct && c.world > 1) nrows = shuffle_rows(c, ya, h->dev, nrows);
       if (s.distinct && nrows) {
         uint64_t cap = 1024;
         while (cap < uint64_t(2 * nrows)) cap <<= 1;
+        for (size_t cc = 0; cc < h->dev.size(); cc++) ya.cols[cc].data = h->dev[cc].p;
         DevBuf table, keep, idx, cnt;
         table.alloc(cap * 8);
         NBG_HIP(hipMemsetAsync(table.p, 0xff, cap * 8, c.stream));

@@ -133,6 +133,10 @@ class GraphSpace:
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         self._check(self.L.nbg_comm_init(self.h, buf))
 
+    def comm_init_local(self, group_key: int):
+        """In-process rank group on one device (tests of the sharded path)."""
+        self._check(self.L.nbg_comm_init_local(self.h, int(group_key)))
+
     @staticmethod
     def comm_unique_id() -> bytes:
         L = _lib.load()

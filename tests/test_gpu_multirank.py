@@ -1,0 +1,222 @@
+"""Sharded path (part % world ranks) on one GPU: N contexts of one process form an in-process
+rank group (nbg_comm_init_local), so the exchange steps of the multi-GPU path -- the build-time
+edge shuffle of the transposed CSR, the per-hop frontier mark exchange (top-down), the frontier
+allgather (bottom-up), the global direction/emptiness sums and the DISTINCT row shuffle -- run
+unchanged, with device-to-device copies in place of RCCL.  The union of the ranks' results must
+equal the oracle's result (the reference's graphd merges the per-host responses,
+GoExecutor.cpp:411-470 / StorageClient.inl:74-159).
+"""
+from collections import Counter
+from concurrent.futures import ThreadPoolExecutor
+import itertools
+
+import numpy as np
+import pytest
+
+import oracle as O
+from nebula_amd import GraphSpace, NbgError
+from nebula_amd import expr as X
+
+pytestmark = pytest.mark.gpu
+
+FOLLOW = 1
+SEED = 1
+_keys = itertools.count(1000)
+
+
+def ms(rows):
+    return Counter(tuple(r) for r in rows)
+
+
+class Group:
+    """`world` contexts on device 0, one per rank; every call runs on all ranks in threads."""
+
+    def __init__(self, world, parts=64):
+        key = next(_keys)
+        self.world = world
+        self.sp = [GraphSpace(parts, device=0, rank=r, world_size=world) for r in range(world)]
+        for s in self.sp:
+            s.comm_init_local(key)
+        self.pool = ThreadPoolExecutor(max_workers=world)
+
+    def each(self, fn):
+        futs = [self.pool.submit(fn, r, s) for r, s in enumerate(self.sp)]
+        out, err = [], None
+        for f in futs:
+            try:
+                out.append(f.result(timeout=300))
+            except Exception as e:  # collect, so every rank has finished before raising
+                out.append(None)
+                err = err or e
+        if err:
+            raise err
+        return out
+
+    def go(self, *a, **k):
+        return self.each(lambda r, s: s.go(*a, **k))
+
+    def close(self):
+        for s in self.sp:
+            s.close()
+        self.pool.shutdown()
+
+
+def union_rows(results):
+    c = Counter()
+    for g in results:
+        c.update(tuple(r) for r in g.rows())
+    return c
+
+
+def seeds_from(scale, n, seed=7):
+    s, _, _ = O.rmat_edges(scale, 16, SEED)
+    rng = np.random.default_rng(seed)
+    return [int(x) for x in s[rng.integers(0, len(s), n)]]
+
+
+@pytest.fixture(scope="module")
+def oracle12():
+    st = O.Store(64)
+    st.set_edge_schema(FOLLOW, [("weight", O.INT)], name="follow")
+    st.load_rmat(12, 16, SEED, FOLLOW)
+    return st
+
+
+@pytest.fixture(scope="module", params=[2, 3])
+def rmat_group(request):
+    g = Group(request.param)
+    for s in g.sp:
+        s.set_edge_schema(FOLLOW, [("weight", O.INT)])
+    g.each(lambda r, s: s.gen_rmat(12, 16, SEED, FOLLOW))
+    g.each(lambda r, s: s.finalize())
+    yield g
+    g.close()
+
+
+def test_shard_sizes_cover_graph(rmat_group, oracle12):
+    infos = rmat_group.each(lambda r, s: s.info(FOLLOW))
+    one = GraphSpace(64)
+    one.set_edge_schema(FOLLOW, [("weight", O.INT)])
+    one.gen_rmat(12, 16, SEED, FOLLOW)
+    one.finalize()
+    i1 = one.info(FOLLOW)
+    one.close()
+    assert all(i["num_vertices"] == i1["num_vertices"] for i in infos)
+    assert sum(i["local_vertices"] for i in infos) == i1["num_vertices"]
+    assert sum(i["local_out_edges"] for i in infos) == i1["local_out_edges"]
+    assert sum(i["local_in_edges"] for i in infos) == i1["local_in_edges"]
+
+
+@pytest.mark.parametrize("force", [0, 1, -1])
+def test_sharded_go_distinct_dst(rmat_group, oracle12, force):
+    g = rmat_group
+    g.each(lambda r, s: s.set_option("bu_force", force))
+    try:
+        starts = seeds_from(12, 64)
+        w = X.AliasProp("follow", "weight") > 499
+        y = [X.EdgeDst("follow")]
+        for steps in (1, 2, 3):
+            res = g.go(starts, steps, FOLLOW, where=w, yields=y, distinct=True)
+            ref = oracle12.go(starts, steps, FOLLOW, where=w.encode(), yields=[y[0].encode()], distinct=True)
+            got = np.sort(np.concatenate([x.columns[0] for x in res]))
+            assert np.array_equal(got, np.sort(ref.int_col(0)))
+            assert len(np.unique(got)) == len(got)  # each vertex reported by its owner only
+            assert sum(x.edges_scanned for x in res) == ref.edges_scanned
+        t = g.each(lambda r, s: s.last_timing())
+        if force == 1:
+            assert all(x["bu_steps"] > 0 for x in t)
+        if force == -1:
+            assert all(x["bu_steps"] == 0 for x in t)
+    finally:
+        g.each(lambda r, s: s.set_option("bu_force", 0))
+
+
+@pytest.mark.parametrize("force", [1, -1])
+def test_sharded_go_rows_and_yields(rmat_group, oracle12, force):
+    g = rmat_group
+    g.each(lambda r, s: s.set_option("bu_force", force))
+    try:
+        starts = seeds_from(12, 24, seed=3)
+        for steps in (1, 2, 3):
+            res = g.go(starts, steps, FOLLOW)
+            ref = oracle12.go(starts, steps, FOLLOW)
+            assert union_rows(res) == ms(ref.rows())
+            assert sum(x.edges_scanned for x in res) == ref.edges_scanned
+        w2 = (X.AliasProp("follow", "weight") % 3).eq(1) & (X.EdgeSrc("follow") > 0)
+        y2 = [X.EdgeSrc("follow"), X.EdgeDst("follow"), X.AliasProp("follow", "weight") * 2]
+        res = g.go(starts, 2, FOLLOW, where=w2, yields=y2)
+        ref = oracle12.go(starts, 2, FOLLOW, where=w2.encode(), yields=[y.encode() for y in y2])
+        assert union_rows(res) == ms(ref.rows())
+    finally:
+        g.each(lambda r, s: s.set_option("bu_force", 0))
+
+
+def test_sharded_distinct_rows_shuffle(rmat_group, oracle12):
+    """DISTINCT over computed columns: equal rows made on different ranks meet on one rank"""
+    g = rmat_group
+    starts = seeds_from(12, 32, seed=11)
+    y = [X.AliasProp("follow", "weight") % 7, X.AliasProp("follow", "weight") > 500]
+    for steps in (1, 3):
+        res = g.go(starts, steps, FOLLOW, yields=y, distinct=True)
+        ref = oracle12.go(starts, steps, FOLLOW, yields=[v.encode() for v in y], distinct=True)
+        u = union_rows(res)
+        assert u == ms(ref.rows())
+        assert all(n == 1 for n in u.values())
+
+
+def test_sharded_eval_error_fails_every_rank(rmat_group):
+    g = rmat_group
+    starts = seeds_from(12, 8)
+    bad = X.AliasProp("follow", "weight") / 0 > 1  # division by zero -> E_EVAL on some row
+    errs = []
+
+    def run(r, s):
+        try:
+            s.go(starts, 2, FOLLOW, where=bad)
+        except NbgError as e:
+            errs.append(e.code)
+
+    g.each(run)
+    assert len(errs) == g.world
+    # the group is still consistent afterwards
+    res = g.go(starts, 2, FOLLOW)
+    assert sum(x.n_rows for x in res) > 0
+
+
+def test_sharded_empty_frontier(rmat_group):
+    g = rmat_group
+    res = g.go([123456789123], 3, FOLLOW)  # not a vertex: empty result on every rank
+    assert all(x.n_rows == 0 for x in res)
+    res = g.go([], 2, FOLLOW, distinct=True)
+    assert all(x.n_rows == 0 for x in res)
+
+
+def test_sharded_kv_ingest(oracle12):
+    """KV parts loaded on their owner rank (part % world) give the oracle's results"""
+    g = Group(2)
+    try:
+        for s in g.sp:
+            s.set_edge_schema(FOLLOW, [("weight", O.INT)])
+
+        def load(r, s):
+            for p in range(1, 65):
+                if p % 2 == r:
+                    s.load_part(p, oracle12.dump_part(p))
+
+        g.each(load)
+        g.each(lambda r, s: s.finalize())
+        starts = seeds_from(12, 32, seed=5)
+        w = X.AliasProp("follow", "weight") > 250
+        y = [X.EdgeDst("follow"), X.AliasProp("follow", "weight")]
+        for steps in (1, 3):
+            res = g.go(starts, steps, FOLLOW, where=w, yields=y)
+            ref = oracle12.go(starts, steps, FOLLOW, where=w.encode(), yields=[v.encode() for v in y])
+            assert union_rows(res) == ms(ref.rows())
+        # getBound: each rank serves its own parts, reports the others as failed
+        parts = [O.part_of(v, 64) for v in starts]
+        cols = [("_dst", O.EDGE, 0), ("weight", O.EDGE, 0)]
+        bound = g.each(lambda r, s: s.get_bound(FOLLOW, parts, starts, cols))
+        ref = oracle12.get_bound(FOLLOW, parts, starts, cols)
+        assert union_rows(bound) == ms(ref.rows())
+    finally:
+        g.close()
