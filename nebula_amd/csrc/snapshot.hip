@@ -360,7 +360,7 @@ __device__ inline int64_t rmat_vid(uint64_t idx, uint64_t smix) {
 __global__ void k_gen_rmat(int64_t lo, int64_t hi, int32_t scale, uint64_t seed, uint64_t smix,
                            int32_t parts, int32_t world, int32_t rank, int64_t* osrc, int64_t* odst,
                            int64_t* oweight, unsigned long long* ocnt, int64_t* isrc, int64_t* idst,
-                           unsigned long long* icnt) {
+                           unsigned long long* icnt, int64_t cap) {
   int64_t stride = int64_t(gridDim.x) * blockDim.x;
   int64_t n = hi - lo;
   int64_t rounds = (n + stride - 1) / stride;
@@ -383,13 +383,13 @@ __global__ void k_gen_rmat(int64_t lo, int64_t hi, int32_t scale, uint64_t seed,
     bool is_in = valid && (world == 1 || dev_owner(d, parts, world) == rank);
     int64_t so = wave_append(ocnt, is_out);
     int64_t si = wave_append(icnt, is_in);
-    if (is_out) {
+    if (is_out && so < cap) {  // counts keep growing past cap: the host re-runs with the exact size
       osrc[so] = s;
       odst[so] = d;
       uint64_t du = uint64_t(d);
       oweight[so] = int64_t(splitmix64(uint64_t(s) ^ ((du << 32) | (du >> 32)) ^ seed) % 1000);
     }
-    if (is_in) {  // in-edge key (dst, -type, rank, src): key src = d, key dst = s
+    if (is_in && si < cap) {  // in-edge key (dst, -type, rank, src): key src = d, key dst = s
       isrc[si] = d;
       idst[si] = s;
     }
@@ -428,32 +428,29 @@ void snapshot_gen_rmat(Ctx& c, int32_t scale, int32_t ef, uint64_t seed, int32_t
     }
     s.cap = size_t(cap);
   };
-  alloc_stage(so, expect, true);
-  alloc_stage(si, expect, false);
   DevBuf cnt;
   cnt.alloc(16);
-  NBG_HIP(hipMemsetAsync(cnt.p, 0, 16, c.stream));
   unsigned long long* d = cnt.as<unsigned long long>();
   uint64_t smix = splitmix64(seed) & ((1ull << 63) - 1);
   const int64_t chunk = int64_t(1) << 26;
-  for (int64_t lo = 0; lo < E; lo += chunk) {
-    int64_t hi = std::min(E, lo + chunk);
-    k_gen_rmat<<<grid_for(hi - lo), 256, 0, c.stream>>>(lo, hi, scale, seed, smix, c.num_parts, c.world,
-                                                      c.rank, so.src.as<int64_t>(), so.dst.as<int64_t>(),
-                                                      so.props[0].as<int64_t>(), d, si.src.as<int64_t>(),
-                                                      si.dst.as<int64_t>(), d + 1);
-    NBG_HIP(hipGetLastError());
-    if (c.world > 1) {  // guard against staging overflow on skewed ownership
-      unsigned long long h[2];
-      NBG_HIP(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
-      if (int64_t(std::max(h[0], h[1])) + chunk > expect)
-        throw Error(NBG_E_NOMEM, "RMAT staging capacity exceeded");
-    }
-  }
   unsigned long long h[2];
-  NBG_HIP(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, c.stream));
-  NBG_HIP(hipStreamSynchronize(c.stream));
+  for (int attempt = 0; attempt < 2; attempt++) {
+    alloc_stage(so, expect, true);
+    alloc_stage(si, expect, false);
+    NBG_HIP(hipMemsetAsync(cnt.p, 0, 16, c.stream));
+    for (int64_t lo = 0; lo < E; lo += chunk) {
+      int64_t hi = std::min(E, lo + chunk);
+      k_gen_rmat<<<grid_for(hi - lo), 256, 0, c.stream>>>(lo, hi, scale, seed, smix, c.num_parts, c.world,
+                                                        c.rank, so.src.as<int64_t>(), so.dst.as<int64_t>(),
+                                                        so.props[0].as<int64_t>(), d, si.src.as<int64_t>(),
+                                                        si.dst.as<int64_t>(), d + 1, expect);
+      NBG_HIP(hipGetLastError());
+    }
+    NBG_HIP(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    if (int64_t(std::max(h[0], h[1])) <= expect) break;
+    expect = int64_t(std::max(h[0], h[1]));  // skewed ownership: regenerate with the exact size
+  }
   so.n = int64_t(h[0]);
   si.n = int64_t(h[1]);
   c.build_seconds += now_s() - t0;
