@@ -4,6 +4,7 @@
 #include "engine.h"
 
 namespace nbg {
+thread_local std::shared_ptr<BufPool> tl_pool;
 int32_t comm_unique_id(uint8_t out[128]);
 void comm_init(Ctx& c, const uint8_t id[128]);
 void free_rows_impl(void* impl);
@@ -51,6 +52,12 @@ nbg_ctx* nbg_ctx_create(int32_t device, int32_t num_parts, int32_t rank, int32_t
     return nullptr;
   }
   for (auto& e : ctx->c.ev) (void)hipEventCreate(&e);
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->c.host_counters), 64 * 8, hipHostMallocDefault) != hipSuccess) {
+    (void)hipStreamDestroy(ctx->c.stream);
+    delete ctx;
+    return nullptr;
+  }
+  memset(ctx->c.host_counters, 0, 64 * 8);
   return ctx;
 }
 
@@ -60,6 +67,7 @@ void nbg_ctx_destroy(nbg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->c.stream);
   nbg::comm_destroy(ctx->c);
   for (auto& e : ctx->c.ev) (void)hipEventDestroy(e);
+  if (ctx->c.host_counters) (void)hipHostFree(ctx->c.host_counters);
   (void)hipStreamDestroy(ctx->c.stream);
   delete ctx;
 }

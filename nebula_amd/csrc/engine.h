@@ -40,18 +40,60 @@ struct Error : std::runtime_error {
   } while (0)
 
 // Device buffer (RAII).  Never resized inside a launch sequence that a caller may capture.
+// Per-context cache of device blocks used while a query runs: queries allocate and drop many
+// temporaries, and hipFree synchronises the whole device, so blocks freed during a query go
+// back to the context's pool and are reused by later queries on the same stream (stream order
+// makes the reuse safe).  Blocks allocated outside a query scope (the snapshot) use
+// hipMalloc/hipFree directly.
+struct BufPool {
+  std::mutex mu;
+  std::multimap<size_t, void*> blocks;
+  size_t cached = 0;
+  size_t limit = size_t(16) << 30;
+  ~BufPool() {
+    for (auto& b : blocks) (void)hipFree(b.second);
+  }
+  void* get(size_t want, size_t& got) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = blocks.lower_bound(want);
+    if (it == blocks.end() || it->first > 2 * want + (size_t(1) << 20)) return nullptr;
+    got = it->first;
+    void* p = it->second;
+    blocks.erase(it);
+    cached -= got;
+    return p;
+  }
+  void put(void* p, size_t cap) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (cached + cap <= limit) {
+        blocks.emplace(cap, p);
+        cached += cap;
+        return;
+      }
+    }
+    (void)hipFree(p);
+  }
+};
+extern thread_local std::shared_ptr<BufPool> tl_pool;  // set for the duration of a query
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  std::shared_ptr<BufPool> pool;
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
-  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes), pool(std::move(o.pool)) {
+    o.p = nullptr;
+    o.bytes = 0;
+  }
   DevBuf& operator=(DevBuf&& o) noexcept {
     if (this != &o) {
       release();
       p = o.p;
       bytes = o.bytes;
+      pool = std::move(o.pool);
       o.p = nullptr;
       o.bytes = 0;
     }
@@ -59,25 +101,46 @@ struct DevBuf {
   }
   ~DevBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      if (pool) pool->put(p, bytes);
+      else (void)hipFree(p);
+    }
     p = nullptr;
     bytes = 0;
+    pool.reset();
   }
   void alloc(size_t b) {
     release();
     if (b == 0) return;
+    if (tl_pool) {
+      size_t got = 0;
+      if (void* q = tl_pool->get(b, got)) {
+        p = q;
+        bytes = got;
+        pool = tl_pool;
+        return;
+      }
+    }
     hipError_t e = hipMalloc(&p, b);
     if (e != hipSuccess) {
       p = nullptr;
       throw Error(NBG_E_NOMEM, "hipMalloc(" + std::to_string(b) + ") failed: " + hipGetErrorString(e));
     }
     bytes = b;
+    pool = tl_pool;
   }
   void ensure(size_t b) {  // grow-only workspace
     if (b > bytes) alloc(b + b / 4);
   }
   template <typename T>
   T* as() const { return static_cast<T*>(p); }
+};
+
+// RAII: route DevBuf allocations of the current thread through the context's pool
+struct PoolScope {
+  std::shared_ptr<BufPool> prev;
+  explicit PoolScope(const std::shared_ptr<BufPool>& p) : prev(tl_pool) { tl_pool = p; }
+  ~PoolScope() { tl_pool = prev; }
 };
 
 struct Field {
@@ -141,6 +204,11 @@ struct EdgeSpace {
   bool has_tr = false;
   bool has_t_eid = false;
   int64_t out_nnz_global = -1;  // sum of out.nnz over ranks (direction heuristic)
+  // bottom-up slab: the first slab_k entries of every transposed row, slot-major [k][row]
+  int32_t slab_k = 0;
+  DevBuf slab_col;                 // int32, -1 past the row's end
+  std::vector<DevBuf> slab_props;  // per out prop with a transposed copy, same width
+  DevBuf odeg;                     // uint32 [owned rows]: out-degree, 0 where row_ok == 0
 };
 
 struct Timing {
@@ -191,6 +259,8 @@ struct Ctx {
   DevBuf ws_partials;  // per-block partial sums of the aggregated kernels
   Timing timing;
   hipEvent_t ev[8] = {};
+  std::shared_ptr<BufPool> pool = std::make_shared<BufPool>();
+  unsigned long long* host_counters = nullptr;  // pinned, 64 entries
   std::map<std::string, int64_t> options;
 
   int64_t owned_lo() const { return base.empty() ? 0 : base[size_t(rank)]; }

@@ -937,34 +937,175 @@ static bool copy_prop(const PropCol& p) {
   return intlike && !p.present.p;
 }
 
+__global__ void k_out_deg(const int64_t* row_ptr, const uint8_t* row_ok, int64_t n, uint32_t* deg,
+                          unsigned int* maxd) {
+  unsigned int m = 0;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    uint32_t d = uint32_t(row_ptr[i + 1] - row_ptr[i]);
+    if (row_ok && !row_ok[i]) d = 0;
+    deg[i] = d;
+    m = d > m ? d : m;
+  }
+  if (maxd) atomicMax(maxd, m);
+}
+// hub-first key: sources with larger out-degree sort first inside a transposed row
+__global__ void k_hub_key(const int32_t* tsrc, int64_t m, const uint32_t* gdeg, uint32_t maxd, uint32_t* key) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    key[i] = maxd - gdeg[tsrc[i]];
+}
+__global__ void k_gather_u32(const uint32_t* in, const uint32_t* perm, uint32_t* out, int64_t m) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = in[perm[i]];
+}
+// ELL slab of the first K entries of every transposed row, slot-major ([k][row]) so a wave's
+// lanes (consecutive rows) read consecutive words; -1 past the row's end
+template <typename T>
+__global__ void k_build_slab(const int64_t* trp, const T* src, int64_t n, int K, T* slab, T none) {
+  for (int64_t d = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; d < n; d += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t b = trp[d], e = trp[d + 1];
+    for (int k = 0; k < K; k++) slab[size_t(k) * size_t(n) + size_t(d)] = b + k < e ? src[b + k] : none;
+  }
+}
+static void build_slab_w(Ctx& c, const int64_t* trp, const void* src, int64_t n, int K, void* slab, int w) {
+  int g = grid_for(n);
+  switch (w) {
+    case 1: k_build_slab<int8_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int8_t*>(src), n, K, static_cast<int8_t*>(slab), 0); break;
+    case 2: k_build_slab<int16_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int16_t*>(src), n, K, static_cast<int16_t*>(slab), 0); break;
+    case 4: k_build_slab<int32_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int32_t*>(src), n, K, static_cast<int32_t*>(slab), 0); break;
+    default: k_build_slab<int64_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int64_t*>(src), n, K, static_cast<int64_t*>(slab), 0);
+  }
+}
+
 // Transpose of the out CSR for bottom-up hops: rows = owned dst, entries = global src index,
 // plus copies of the INT-like props in transpose order.  With several ranks every out-edge is
 // shipped to the owner of its dst (one build-time all-to-all), so each rank can run bottom-up
 // hops over its own vertices against the allgathered frontier bitmap.
+//
+// Inside a row the sources are ordered hub-first (descending out-degree): in a dense frontier
+// the first in-neighbour checked is then almost always a frontier member, and the first K
+// entries of every row are copied into a slot-major slab, so the common case of a bottom-up hop
+// reads 4 coalesced bytes per row instead of one scattered cache line per row.
 static void build_transpose(Ctx& c, EdgeSpace& es) {
   Csr& o = es.out;
   Csr& t = es.tr;
   const int64_t m = o.nnz;
   const int64_t lo = c.owned_lo(), hi = c.owned_hi();
+  const int64_t n_own = hi - lo;
   const int G = c.world;
-  int bits = 1;
-  while ((int64_t(1) << bits) < std::max<int64_t>(c.n_global, 2)) bits++;
-  // local out-edges sorted by dst gidx
-  DevBuf esrc, keysB, iota, perm;
-  esrc.alloc(size_t(m + 1) * 4);
-  keysB.alloc(size_t(m + 1) * 4);
-  iota.alloc(size_t(m + 1) * 4);
-  perm.alloc(size_t(m + 1) * 4);
-  if (m) {
-    k_edge_src<<<grid_for(o.n_rows), 256, 0, c.stream>>>(o.row_ptr.as<int64_t>(), o.n_rows, esrc.as<int32_t>());
-    k_iota_u32<<<grid_for(m), 256, 0, c.stream>>>(iota.as<uint32_t>(), m);
-    radix_pairs<uint32_t, uint32_t>(c, o.col.as<uint32_t>(), keysB.as<uint32_t>(), iota.as<uint32_t>(),
-                                   perm.as<uint32_t>(), m, bits);
+  auto nbits = [](int64_t x) {
+    int b = 1;
+    while ((int64_t(1) << b) < std::max<int64_t>(x, 2)) b++;
+    return b;
+  };
+  // out-degrees (0 for rows outside hash(vid)'s part) of every vertex of the gidx space
+  es.odeg.alloc(size_t(n_own + 1) * 4);
+  DevBuf gdeg, dmax;
+  dmax.alloc(8);
+  NBG_HIP(hipMemsetAsync(dmax.p, 0, 8, c.stream));
+  k_out_deg<<<grid_for(n_own), 256, 0, c.stream>>>(o.row_ptr.as<int64_t>(), o.row_ok.as<uint8_t>(), n_own,
+                                                  es.odeg.as<uint32_t>(), dmax.as<unsigned int>());
+  const uint32_t* gdegp = es.odeg.as<uint32_t>();
+  if (G > 1) {
+    gdeg.alloc(size_t(c.n_global + 1) * 4);
+    std::vector<size_t> rb(static_cast<size_t>(G)), ro(static_cast<size_t>(G));
+    for (int p = 0; p < G; p++) {
+      rb[size_t(p)] = size_t(c.base[size_t(p) + 1] - c.base[size_t(p)]) * 4;
+      ro[size_t(p)] = size_t(c.base[size_t(p)]) * 4;
+    }
+    comm_allgatherv_bytes(c, es.odeg.p, size_t(n_own) * 4, gdeg.p, rb.data(), ro.data());
+    gdegp = gdeg.as<uint32_t>();
   }
-  iota.release();
+  uint32_t maxd = 0;
+  NBG_HIP(hipMemcpyAsync(&maxd, dmax.p, 4, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  if (G > 1) maxd = UINT32_MAX;  // other ranks' degrees may exceed the local maximum
+  // the transposed edge list: tdst (local row), tsrc (global), and the order props come in
+  DevBuf tdst, tsrc;
+  int64_t R = 0;
   std::vector<const PropCol*> cp;
   for (const PropCol& p : o.props) cp.push_back(copy_prop(p) ? &p : nullptr);
-  t.n_rows = hi - lo;
+  std::vector<DevBuf> rprops(o.props.size());  // world > 1: received prop columns
+  {
+    DevBuf esrc;
+    esrc.alloc(size_t(m + 1) * 4);
+    if (m) k_edge_src<<<grid_for(o.n_rows), 256, 0, c.stream>>>(o.row_ptr.as<int64_t>(), o.n_rows, esrc.as<int32_t>());
+    if (G == 1) {
+      R = m;
+      tsrc = std::move(esrc);  // lo == 0: local == global
+      tdst.alloc(size_t(m + 1) * 4);
+      if (m) NBG_HIP(hipMemcpyAsync(tdst.p, o.col.p, size_t(m) * 4, hipMemcpyDeviceToDevice, c.stream));
+    } else {
+      // ship every out-edge to its dst's owner: sort by dst gidx, cut at the owner bases
+      DevBuf keysB, iota, perm;
+      keysB.alloc(size_t(m + 1) * 4);
+      iota.alloc(size_t(m + 1) * 4);
+      perm.alloc(size_t(m + 1) * 4);
+      if (m) {
+        k_iota_u32<<<grid_for(m), 256, 0, c.stream>>>(iota.as<uint32_t>(), m);
+        radix_pairs<uint32_t, uint32_t>(c, o.col.as<uint32_t>(), keysB.as<uint32_t>(), iota.as<uint32_t>(),
+                                       perm.as<uint32_t>(), m, nbits(c.n_global));
+      }
+      iota.release();
+      DevBuf dbase, dcut;
+      dbase.alloc(size_t(G + 1) * 8);
+      dcut.alloc(size_t(G + 1) * 8);
+      NBG_HIP(hipMemcpyAsync(dbase.p, c.base.data(), size_t(G + 1) * 8, hipMemcpyHostToDevice, c.stream));
+      k_sorted_bounds<<<1, 64, 0, c.stream>>>(keysB.as<uint32_t>(), m, dbase.as<int64_t>(), G + 1, dcut.as<int64_t>());
+      std::vector<int64_t> cut(static_cast<size_t>(G + 1));
+      NBG_HIP(hipMemcpyAsync(cut.data(), dcut.p, size_t(G + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      cut[size_t(G)] = m;
+      DevBuf ssrc;
+      ssrc.alloc(size_t(m + 1) * 4);
+      if (m) k_src_global<<<grid_for(m), 256, 0, c.stream>>>(perm.as<uint32_t>(), esrc.as<int32_t>(), m, lo, ssrc.as<int32_t>());
+      esrc.release();
+      const size_t ng = static_cast<size_t>(G);
+      std::vector<int64_t> mine(ng), all(ng * ng);
+      for (size_t h = 0; h < ng; h++) mine[h] = cut[h + 1] - cut[h];
+      {
+        DevBuf dm, da;
+        dm.alloc(ng * 8);
+        da.alloc(ng * ng * 8);
+        NBG_HIP(hipMemcpyAsync(dm.p, mine.data(), ng * 8, hipMemcpyHostToDevice, c.stream));
+        comm_allgather_bytes(c, dm.p, ng * 8, da.p);
+        NBG_HIP(hipMemcpyAsync(all.data(), da.p, ng * ng * 8, hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipStreamSynchronize(c.stream));
+      }
+      std::vector<int64_t> roff(ng + 1, 0);
+      for (size_t p = 0; p < ng; p++) roff[p + 1] = roff[p] + all[p * ng + size_t(c.rank)];
+      R = roff[ng];
+      auto exchange = [&](const void* send, void* recv, int w) {
+        std::vector<size_t> sb(ng), so(ng), rb(ng), ro(ng);
+        for (size_t p = 0; p < ng; p++) {
+          sb[p] = size_t(mine[p]) * size_t(w);
+          so[p] = size_t(cut[p]) * size_t(w);
+          rb[p] = size_t(roff[p + 1] - roff[p]) * size_t(w);
+          ro[p] = size_t(roff[p]) * size_t(w);
+        }
+        comm_alltoallv_bytes(c, send, sb.data(), so.data(), recv, rb.data(), ro.data());
+      };
+      DevBuf rdst;
+      tsrc.alloc(size_t(R + 1) * 4);
+      rdst.alloc(size_t(R + 1) * 4);
+      exchange(ssrc.p, tsrc.p, 4);
+      exchange(keysB.p, rdst.p, 4);
+      tdst.alloc(size_t(R + 1) * 4);
+      if (R) k_sub_lo<<<grid_for(R), 256, 0, c.stream>>>(rdst.as<int32_t>(), R, lo, tdst.as<uint32_t>());
+      for (size_t f = 0; f < o.props.size(); f++) {
+        if (!cp[f]) continue;
+        int w = cp[f]->width;
+        DevBuf sp;
+        sp.alloc(size_t(m + 1) * size_t(w));
+        rprops[f].alloc(size_t(R + 1) * size_t(w));
+        if (m) gather_width(c, cp[f]->data.p, perm.as<uint32_t>(), sp.p, m, w);
+        exchange(sp.p, rprops[f].p, w);
+      }
+      NBG_HIP(hipStreamSynchronize(c.stream));
+    }
+  }
+  // order: stable sort by hub key, then stable sort by row -> rows hub-first
+  t.n_rows = n_own;
+  t.nnz = R;
   t.props.clear();
   for (const PropCol& p : o.props) {
     PropCol q;
@@ -974,104 +1115,59 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
     t.props.push_back(std::move(q));
   }
   t.row_ptr.alloc(size_t(t.n_rows + 1) * 8);
+  t.col.alloc(size_t(R + 1) * 4);
+  DevBuf perm;
+  perm.alloc(size_t(R + 1) * 4);
+  if (R) {
+    DevBuf key, keyS, iota, perm1;
+    key.alloc(size_t(R) * 4);
+    keyS.alloc(size_t(R) * 4);
+    iota.alloc(size_t(R) * 4);
+    perm1.alloc(size_t(R) * 4);
+    k_hub_key<<<grid_for(R), 256, 0, c.stream>>>(tsrc.as<int32_t>(), R, gdegp, maxd, key.as<uint32_t>());
+    k_iota_u32<<<grid_for(R), 256, 0, c.stream>>>(iota.as<uint32_t>(), R);
+    radix_pairs<uint32_t, uint32_t>(c, key.as<uint32_t>(), keyS.as<uint32_t>(), iota.as<uint32_t>(),
+                                   perm1.as<uint32_t>(), R, G > 1 ? 32 : nbits(int64_t(maxd) + 1));
+    iota.release();
+    k_gather_u32<<<grid_for(R), 256, 0, c.stream>>>(tdst.as<uint32_t>(), perm1.as<uint32_t>(), key.as<uint32_t>(), R);
+    radix_pairs<uint32_t, uint32_t>(c, key.as<uint32_t>(), keyS.as<uint32_t>(), perm1.as<uint32_t>(),
+                                   perm.as<uint32_t>(), R, nbits(n_own));
+    k_gather_w<int32_t><<<grid_for(R), 256, 0, c.stream>>>(tsrc.as<int32_t>(), perm.as<uint32_t>(), t.col.as<int32_t>(), R);
+    k_rowptr_sorted<<<grid_for(R + 1), 256, 0, c.stream>>>(keyS.as<uint32_t>(), R, t.n_rows, t.row_ptr.as<int64_t>());
+  } else {
+    NBG_HIP(hipMemsetAsync(t.row_ptr.p, 0, size_t(t.n_rows + 1) * 8, c.stream));
+  }
+  tsrc.release();
+  tdst.release();
+  for (size_t f = 0; f < o.props.size(); f++) {
+    if (!cp[f]) continue;
+    int w = cp[f]->width;
+    t.props[f].data.alloc(size_t(R) * size_t(w) + 16);
+    const void* src = G == 1 ? cp[f]->data.p : rprops[f].p;
+    if (R) gather_width(c, src, perm.as<uint32_t>(), t.props[f].data.p, R, w);
+    rprops[f].release();
+  }
   if (G == 1) {
-    t.nnz = m;
-    t.col.alloc(size_t(m + 1) * 4);
     es.t_eid = std::move(perm);
-    if (m) {
-      k_tr_col<<<grid_for(m), 256, 0, c.stream>>>(es.t_eid.as<uint32_t>(), esrc.as<int32_t>(), m, lo, t.col.as<int32_t>());
-      k_rowptr_sorted<<<grid_for(m + 1), 256, 0, c.stream>>>(keysB.as<uint32_t>(), m, t.n_rows, t.row_ptr.as<int64_t>());
-    } else {
-      NBG_HIP(hipMemsetAsync(t.row_ptr.p, 0, size_t(t.n_rows + 1) * 8, c.stream));
-    }
-    for (size_t f = 0; f < o.props.size(); f++)
-      if (cp[f] && m) {
-        t.props[f].data.alloc(size_t(m) * size_t(cp[f]->width) + 16);
-        gather_width(c, cp[f]->data.p, es.t_eid.as<uint32_t>(), t.props[f].data.p, m, cp[f]->width);
-      }
     es.has_t_eid = true;
   } else {
-    // per-owner ranges of the dst-sorted edges
-    DevBuf dbase, dcut;
-    dbase.alloc(size_t(G + 1) * 8);
-    dcut.alloc(size_t(G + 1) * 8);
-    NBG_HIP(hipMemcpyAsync(dbase.p, c.base.data(), size_t(G + 1) * 8, hipMemcpyHostToDevice, c.stream));
-    k_sorted_bounds<<<1, 64, 0, c.stream>>>(keysB.as<uint32_t>(), m, dbase.as<int64_t>(), G + 1, dcut.as<int64_t>());
-    std::vector<int64_t> cut(size_t(G + 1));
-    NBG_HIP(hipMemcpyAsync(cut.data(), dcut.p, size_t(G + 1) * 8, hipMemcpyDeviceToHost, c.stream));
-    NBG_HIP(hipStreamSynchronize(c.stream));
-    cut[size_t(G)] = m;
-    // send buffers in dst-sorted order
-    DevBuf ssrc, sprops;
-    ssrc.alloc(size_t(m + 1) * 4);
-    if (m) k_src_global<<<grid_for(m), 256, 0, c.stream>>>(perm.as<uint32_t>(), esrc.as<int32_t>(), m, lo, ssrc.as<int32_t>());
-    // count matrix
-    std::vector<int64_t> mine(static_cast<size_t>(G)), all(static_cast<size_t>(G) * static_cast<size_t>(G));
-    for (int h = 0; h < G; h++) mine[size_t(h)] = cut[size_t(h + 1)] - cut[size_t(h)];
-    {
-      DevBuf dm, da;
-      dm.alloc(size_t(G) * 8);
-      da.alloc(size_t(G) * size_t(G) * 8);
-      NBG_HIP(hipMemcpyAsync(dm.p, mine.data(), size_t(G) * 8, hipMemcpyHostToDevice, c.stream));
-      comm_allgather_bytes(c, dm.p, size_t(G) * 8, da.p);
-      NBG_HIP(hipMemcpyAsync(all.data(), da.p, size_t(G) * size_t(G) * 8, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
-    }
-    int64_t R = 0;
-    std::vector<int64_t> roff(size_t(G) + 1, 0);
-    for (int p = 0; p < G; p++) {
-      int64_t from_p = all[size_t(p) * size_t(G) + size_t(c.rank)];
-      roff[size_t(p) + 1] = roff[size_t(p)] + from_p;
-    }
-    R = roff[size_t(G)];
-    auto exchange = [&](const void* send, void* recv, int w) {
-      const size_t ng = static_cast<size_t>(G);
-      std::vector<size_t> sb(ng), so(ng), rb(ng), ro(ng);
-      for (int p = 0; p < G; p++) {
-        sb[size_t(p)] = size_t(mine[size_t(p)]) * size_t(w);
-        so[size_t(p)] = size_t(cut[size_t(p)]) * size_t(w);
-        rb[size_t(p)] = size_t(roff[size_t(p) + 1] - roff[size_t(p)]) * size_t(w);
-        ro[size_t(p)] = size_t(roff[size_t(p)]) * size_t(w);
-      }
-      comm_alltoallv_bytes(c, send, sb.data(), so.data(), recv, rb.data(), ro.data());
-    };
-    DevBuf rsrc, rdst, rkey, rperm, riota;
-    rsrc.alloc(size_t(R + 1) * 4);
-    rdst.alloc(size_t(R + 1) * 4);
-    exchange(ssrc.p, rsrc.p, 4);
-    exchange(keysB.p, rdst.p, 4);
-    // received edges sorted by local dst
-    rkey.alloc(size_t(R + 1) * 4);
-    DevBuf rkeyS;
-    rkeyS.alloc(size_t(R + 1) * 4);
-    rperm.alloc(size_t(R + 1) * 4);
-    riota.alloc(size_t(R + 1) * 4);
-    t.nnz = R;
-    t.col.alloc(size_t(R + 1) * 4);
-    if (R) {
-      k_sub_lo<<<grid_for(R), 256, 0, c.stream>>>(rdst.as<int32_t>(), R, lo, rkey.as<uint32_t>());
-      k_iota_u32<<<grid_for(R), 256, 0, c.stream>>>(riota.as<uint32_t>(), R);
-      int lbits = 1;
-      while ((int64_t(1) << lbits) < std::max<int64_t>(t.n_rows, 2)) lbits++;
-      radix_pairs<uint32_t, uint32_t>(c, rkey.as<uint32_t>(), rkeyS.as<uint32_t>(), riota.as<uint32_t>(),
-                                     rperm.as<uint32_t>(), R, lbits);
-      k_gather_w<int32_t><<<grid_for(R), 256, 0, c.stream>>>(rsrc.as<int32_t>(), rperm.as<uint32_t>(), t.col.as<int32_t>(), R);
-      k_rowptr_sorted<<<grid_for(R + 1), 256, 0, c.stream>>>(rkeyS.as<uint32_t>(), R, t.n_rows, t.row_ptr.as<int64_t>());
-    } else {
-      NBG_HIP(hipMemsetAsync(t.row_ptr.p, 0, size_t(t.n_rows + 1) * 8, c.stream));
-    }
-    for (size_t f = 0; f < o.props.size(); f++) {
-      if (!cp[f]) continue;
-      int w = cp[f]->width;
-      DevBuf sp, rp;
-      sp.alloc(size_t(m + 1) * size_t(w));
-      rp.alloc(size_t(R + 1) * size_t(w));
-      if (m) gather_width(c, cp[f]->data.p, perm.as<uint32_t>(), sp.p, m, w);
-      exchange(sp.p, rp.p, w);
-      t.props[f].data.alloc(size_t(R) * size_t(w) + 16);
-      if (R) gather_width(c, rp.p, rperm.as<uint32_t>(), t.props[f].data.p, R, w);
-    }
     es.has_t_eid = false;
+  }
+  // the slab
+  es.slab_k = int32_t(std::max<int64_t>(0, std::min<int64_t>(c.opt("bu_slab", 4), 16)));
+  es.slab_props.clear();
+  es.slab_props.resize(o.props.size());
+  if (es.slab_k > 0) {
+    es.slab_col.alloc(size_t(es.slab_k) * size_t(n_own) * 4 + 16);
+    if (n_own)
+      k_build_slab<int32_t><<<grid_for(n_own), 256, 0, c.stream>>>(t.row_ptr.as<int64_t>(), t.col.as<int32_t>(), n_own,
+                                                                  es.slab_k, es.slab_col.as<int32_t>(), -1);
+    for (size_t f = 0; f < o.props.size(); f++) {
+      if (!t.props[f].data.p) continue;
+      int w = t.props[f].width;
+      es.slab_props[f].alloc(size_t(es.slab_k) * size_t(n_own) * size_t(w) + 16);
+      if (n_own) build_slab_w(c, t.row_ptr.as<int64_t>(), t.props[f].data.p, n_own, es.slab_k, es.slab_props[f].p, w);
+    }
   }
   NBG_HIP(hipStreamSynchronize(c.stream));
   NBG_HIP(hipGetLastError());
@@ -1083,6 +1179,64 @@ __global__ void k_owned_only(const uint64_t* in, int64_t n, int parts, int world
     int64_t v = int64_t(in[i] ^ (1ull << 63));
     flag[i] = dev_owner(v, parts, world) == rank;
   }
+}
+
+// out-degree (pre-collapse multiplicity is fine: it only orders vertices) via a provisional table
+__global__ void k_count_deg(const int64_t* src, int64_t n, const int64_t* keys, const int32_t* vals, uint64_t mask,
+                            bool has_min, int32_t min_idx, unsigned int* deg) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t g = ht_lookup(keys, vals, mask, src[i], has_min, min_idx);
+    if (g >= 0) atomicAdd(deg + g, 1u);
+  }
+}
+__global__ void k_not_u32(const unsigned int* in, int64_t n, uint32_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = ~in[i];
+}
+
+// Degree-ordered vertex numbering: a rank's owned gidx range lists its vertices by descending
+// out-degree (ties by vid).  The hubs -- the sources a bottom-up hop finds first (hub-first
+// transposed rows) -- then share a few cache lines of every frontier bitmap instead of being
+// scattered over all of it.  `owned` holds sign-flipped vids, sorted ascending on entry.
+static void order_by_degree(Ctx& c, DevBuf& owned, int64_t n_owned) {
+  if (n_owned <= 1) return;
+  int64_t cap = 1024;
+  while (cap < 2 * n_owned) cap <<= 1;
+  DevBuf keys, vals, vids, deg, dmin;
+  keys.alloc(size_t(cap) * 8);
+  vals.alloc(size_t(cap) * 4);
+  vids.alloc(size_t(n_owned) * 8);
+  deg.alloc(size_t(n_owned) * 4);
+  dmin.alloc(4);
+  fill<int64_t>(c, keys.as<int64_t>(), INT64_MIN, cap);
+  int32_t neg = -1;
+  NBG_HIP(hipMemcpyAsync(dmin.p, &neg, 4, hipMemcpyHostToDevice, c.stream));
+  NBG_HIP(hipMemsetAsync(deg.p, 0, size_t(n_owned) * 4, c.stream));
+  k_unflip<<<grid_for(n_owned), 256, 0, c.stream>>>(owned.as<uint64_t>(), vids.as<int64_t>(), n_owned);
+  k_ht_insert<<<grid_for(n_owned), 256, 0, c.stream>>>(keys.as<int64_t>(), vals.as<int32_t>(), uint64_t(cap - 1),
+                                                       vids.as<int64_t>(), n_owned, 0, dmin.as<int32_t>());
+  int32_t min_idx = -1;
+  NBG_HIP(hipMemcpyAsync(&min_idx, dmin.p, 4, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  for (auto& kv : c.edges) {
+    const Staging& st = kv.second.out_stage;
+    if (st.n)
+      k_count_deg<<<grid_for(st.n), 256, 0, c.stream>>>(st.src.as<int64_t>(), st.n, keys.as<int64_t>(),
+                                                       vals.as<int32_t>(), uint64_t(cap - 1), min_idx >= 0, min_idx,
+                                                       deg.as<unsigned int>());
+  }
+  keys.release();
+  vals.release();
+  DevBuf key, keyS, sorted;
+  key.alloc(size_t(n_owned) * 4);
+  keyS.alloc(size_t(n_owned) * 4);
+  sorted.alloc(size_t(n_owned) * 8);
+  k_not_u32<<<grid_for(n_owned), 256, 0, c.stream>>>(deg.as<unsigned int>(), n_owned, key.as<uint32_t>());
+  radix_pairs<uint32_t, uint64_t>(c, key.as<uint32_t>(), keyS.as<uint32_t>(), owned.as<uint64_t>(),
+                                 sorted.as<uint64_t>(), n_owned, 32);
+  NBG_HIP(hipMemcpyAsync(owned.p, sorted.p, size_t(n_owned) * 8, hipMemcpyDeviceToDevice, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  NBG_HIP(hipGetLastError());
 }
 
 void snapshot_finalize(Ctx& c) {
@@ -1166,7 +1320,9 @@ void snapshot_finalize(Ctx& c) {
     n_owned = ns ? unique_sorted<uint64_t>(c, s2.as<uint64_t>(), owned.as<uint64_t>(), int64_t(ns)) : 0;
     vA.release();
   }
-  // 3. counts -> base; allgather owned tables into vid_of (rank-major, sorted within rank)
+  if (c.opt("degree_order", 1)) order_by_degree(c, owned, n_owned);
+  // 3. counts -> base; allgather owned tables into vid_of (rank-major; within a rank by
+  // descending out-degree, or by vid with degree_order=0)
   if (c.world == 1) {
     counts[0] = n_owned;
   } else {

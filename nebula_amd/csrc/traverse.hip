@@ -464,7 +464,8 @@ __device__ inline unsigned long long wave_sum_u64(unsigned long long x) {
 
 // ---- block-level aggregation helpers (one atomic per block or none: a single global counter
 // serialises at ~88 returning atomics/us on MI355X, MI355X_MICROARCH "dequeue") ----------------
-constexpr int kAggBlocks = 8192;  // max grid of the aggregated kernels (partials are [block][4])
+constexpr int kAggBlocks = 8192;  // max grid of the aggregated kernels (partials are [block][kSlots])
+constexpr int kSlots = 8;
 
 __device__ inline uint32_t block_excl_scan_u32(uint32_t x, uint32_t& total, uint32_t* lds) {
   uint32_t wt;
@@ -490,27 +491,192 @@ __device__ inline void block_store_partials(const unsigned long long* v, int k, 
     if ((threadIdx.x & 63) == 0) lds[i * 16 + w] = s;
   }
   __syncthreads();
-  if (threadIdx.x < unsigned(k)) {
+  if (threadIdx.x < unsigned(kSlots)) {
     unsigned long long s = 0;
-    for (int j = 0; j < nw; j++) s += lds[threadIdx.x * 16 + j];
-    partials[size_t(blockIdx.x) * 4 + threadIdx.x] = s;
+    if (threadIdx.x < unsigned(k))
+      for (int j = 0; j < nw; j++) s += lds[threadIdx.x * 16 + j];
+    partials[size_t(threadIdx.x) * kAggBlocks + blockIdx.x] = s;  // slot-major: coalesced reduce
   }
 }
-// sums the [kAggBlocks][4] partials into out[0..3] (one block)
+// sums the [kSlots][kAggBlocks] partials into out[0..kSlots) (one block)
 __global__ void k_reduce_partials(const unsigned long long* partials, int nblocks, unsigned long long* out) {
-  __shared__ unsigned long long s[4][256];
-  for (int k = 0; k < 4; k++) {
+  __shared__ unsigned long long s[kSlots][256];
+  for (int k = 0; k < kSlots; k++) {
     unsigned long long a = 0;
-    for (int b = threadIdx.x; b < nblocks; b += blockDim.x) a += partials[size_t(b) * 4 + k];
+    for (int b = threadIdx.x; b < nblocks; b += blockDim.x) a += partials[size_t(k) * kAggBlocks + b];
     s[k][threadIdx.x] = a;
   }
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if (threadIdx.x < unsigned(o))
-      for (int k = 0; k < 4; k++) s[k][threadIdx.x] += s[k][threadIdx.x + o];
+      for (int k = 0; k < kSlots; k++) s[k][threadIdx.x] += s[k][threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x < 4) out[threadIdx.x] = s[threadIdx.x][0];
+  if (threadIdx.x < unsigned(kSlots)) out[threadIdx.x] = s[threadIdx.x][0];
+}
+
+// Bottom-up hop over the slab (first K hub-first entries of each transposed row, slot-major)
+// with a fallback scan of the rows' remaining entries; writes the next frontier as ballot words.
+// The hop is latency bound (each row is a chain slab -> frontier bit), so a wave owns tiles of
+// 64 x R rows and issues the loads of all R rows (and of the first EAGER slots) before using
+// any of them; rows whose slab entries all miss are then scanned by the whole wave, 64
+// consecutive entries per step (coalesced), instead of by one lane.
+// Only existence matters (a vertex is in the next frontier if ANY in-edge qualifies), so the
+// slots need not be evaluated in order.
+// odeg == nullptr: final hop (keep every found vertex); otherwise keep found vertices with
+// out-edges and sum their out-degrees (the next hop's E).  partials: [0] found, [1] out-degree
+// sum, [2] slab words read (+ their predicate values), [3] rows scanned past the slab, [4] entries
+// read past the slab, [5] predicate values read past the slab.
+template <int PK, int EAGER, int R>
+__global__ __launch_bounds__(256) void k_bu_slab(const int32_t* __restrict__ slab, const void* __restrict__ slab_w,
+                                                 int K, const int64_t* __restrict__ trp,
+                                                 const int32_t* __restrict__ tcol, int64_t n,
+                                                 const uint32_t* __restrict__ fbits,
+                                                 unsigned long long* __restrict__ nbits,
+                                                 const uint32_t* __restrict__ odeg, FastArgs fp,
+                                                 unsigned long long* partials) {
+  __shared__ unsigned long long lds[kSlots * 16];
+  unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  const int64_t ntiles = (n + 64 * R - 1) / (64 * R);
+  const int KE = K < EAGER ? K : EAGER;
+  for (int64_t t = wave; t < ntiles; t += nwaves) {
+    int64_t d[R];
+    bool found[R], pend[R];
+    uint32_t od[R];
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      d[j] = t * 64 * R + j * 64 + lane;
+      found[j] = false;
+      pend[j] = d[j] < n;
+      od[j] = 0;
+    }
+    // level 1: eager slots (+ predicate values, + out-degrees): independent loads
+    int32_t sv[R][EAGER];
+    int64_t wv[R][EAGER];
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      if (odeg && pend[j]) od[j] = odeg[d[j]];
+#pragma unroll
+      for (int q = 0; q < EAGER; q++) {
+        sv[j][q] = -1;
+        wv[j][q] = 0;
+        if (pend[j] && q < KE) {
+          const int64_t si = int64_t(q) * n + d[j];
+          sv[j][q] = slab[si];
+          if (PK == PK_FAST) wv[j][q] = load_int(slab_w, fp.width, si);
+        }
+      }
+    }
+    // level 2: frontier bits
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      bool exhausted = false;
+#pragma unroll
+      for (int q = 0; q < EAGER; q++) {
+        if (!pend[j] || q >= KE) continue;
+        const int32_t s = sv[j][q];
+        acc[2]++;
+        if (s < 0) {
+          exhausted = true;
+          continue;
+        }
+        if ((fbits[s >> 5] >> (s & 31)) & 1u) {
+          if (PK != PK_FAST || fast_cmp(fp.op, wv[j][q], fp.k)) found[j] = true;
+        }
+      }
+      pend[j] = pend[j] && !found[j] && !exhausted;
+    }
+    // lazy slots (one level each, only while some row of the wave is still pending)
+    for (int q = KE; q < K; q++) {
+      bool anyp = false;
+#pragma unroll
+      for (int j = 0; j < R; j++) anyp |= pend[j];
+      if (__ballot(anyp) == 0) break;
+      int32_t s1[R];
+      int64_t w1[R];
+#pragma unroll
+      for (int j = 0; j < R; j++) {
+        s1[j] = -1;
+        w1[j] = 0;
+        if (pend[j]) {
+          const int64_t si = int64_t(q) * n + d[j];
+          s1[j] = slab[si];
+          if (PK == PK_FAST) w1[j] = load_int(slab_w, fp.width, si);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < R; j++) {
+        if (!pend[j]) continue;
+        acc[2]++;
+        const int32_t s = s1[j];
+        if (s < 0) {
+          pend[j] = false;
+          continue;
+        }
+        if ((fbits[s >> 5] >> (s & 31)) & 1u) {
+          if (PK != PK_FAST || fast_cmp(fp.op, w1[j], fp.k)) {
+            found[j] = true;
+            pend[j] = false;
+          }
+        }
+      }
+    }
+    // rows with more entries than the slab: wave-cooperative scan of the rest
+    int64_t rb[R], re[R];
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      rb[j] = re[j] = 0;
+      if (pend[j]) {
+        rb[j] = trp[d[j]] + K;
+        re[j] = trp[d[j] + 1];
+        if (rb[j] >= re[j]) pend[j] = false;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      unsigned long long pm = __ballot(pend[j]);
+      while (pm) {
+        const int src = __ffsll((long long)pm) - 1;
+        pm &= pm - 1;
+        const int64_t b = __shfl((long long)rb[j], src), e = __shfl((long long)re[j], src);
+        acc[3] += lane == 0;
+        bool f = false;
+        for (int64_t x = b; x < e && !f; x += 64) {
+          const int64_t ex = x + lane;
+          bool h = false;
+          if (ex < e) {
+            const int32_t s = tcol[ex];
+            acc[4]++;
+            if ((fbits[s >> 5] >> (s & 31)) & 1u) {
+              if (PK == PK_FAST) {
+                acc[5]++;
+                h = fast_cmp(fp.op, load_int(fp.data, fp.width, ex), fp.k);
+              } else {
+                h = true;
+              }
+            }
+          }
+          f = __ballot(h) != 0;
+        }
+        if (lane == src) found[j] = f;
+      }
+    }
+    // next frontier words
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      const uint32_t o = found[j] ? od[j] : 0u;
+      const bool keep = odeg ? o > 0 : found[j];
+      const unsigned long long km = __ballot(keep);
+      const int64_t d0 = t * 64 * R + j * 64;
+      if (lane == 0 && d0 < n) nbits[d0 >> 6] = km;
+      acc[0] += found[j];
+      acc[1] += o;
+    }
+  }
+  block_store_partials(acc, 6, lds, partials);
 }
 
 // Bottom-up hop writing the next frontier straight into a bitmap (one 64-bit ballot word per
@@ -523,7 +689,7 @@ __global__ __launch_bounds__(256) void k_bu_bits(const int64_t* __restrict__ trp
                                                  unsigned long long* __restrict__ nbits,
                                                  const int64_t* __restrict__ row_ptr, const uint8_t* __restrict__ row_ok,
                                                  FastArgs fp, unsigned long long* partials) {
-  __shared__ unsigned long long lds[64];
+  __shared__ unsigned long long lds[kSlots * 16];
   unsigned long long acc[3] = {0, 0, 0};  // found, esum, examined
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   const int64_t rounds = (n + stride - 1) / stride;
@@ -552,48 +718,63 @@ __global__ __launch_bounds__(256) void k_bu_bits(const int64_t* __restrict__ trp
   block_store_partials(acc, 3, lds, partials);
 }
 
-// bitmap -> compacted list.  mode 0: local rows with out-edges (a top-down hop's frontier);
-// mode 1: vids of every set vertex (the DISTINCT _dst output).  One tile of 256 x 4 words
-// (32768 vertices) per block-iteration, one returning atomic per tile.
+// bitmap -> compacted list.  mode 0: local rows (a top-down hop's frontier; the bitmaps this
+// reads already exclude rows without out-edges); mode 1: vids of every set vertex (the DISTINCT
+// _dst output).  A tile of 1024 words (32768 vertices) per block-iteration: the words and their
+// exclusive offsets go to LDS, one returning atomic reserves the tile's output range, then each
+// wave expands two words per step with one lane per bit, so consecutive set bits write
+// consecutive output slots (coalesced stores, coalesced vid_of reads).
 template <int MODE>
 __global__ __launch_bounds__(256) void k_bits_compact(const uint32_t* __restrict__ bits, int64_t n, int64_t lo,
-                                                      const int64_t* __restrict__ row_ptr,
                                                       const int64_t* __restrict__ vid_of, void* out,
                                                       unsigned long long* n_out) {
+  constexpr int kTileWords = 1024;
+  __shared__ uint32_t sw[kTileWords];
+  __shared__ uint32_t so[kTileWords];
   __shared__ uint32_t lds[8];
   __shared__ unsigned long long s_base;
   const int64_t nwords = (n + 31) / 32;
-  const int64_t tile_words = int64_t(blockDim.x) * 4;
-  const int64_t ntiles = (nwords + tile_words - 1) / tile_words;
+  const int64_t ntiles = (nwords + kTileWords - 1) / kTileWords;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    uint32_t m[4];
-    uint32_t cnt = 0;
+    const int64_t w0 = t * kTileWords + int64_t(threadIdx.x) * 4;
+    uint32_t x[4];
+    if (w0 + 4 <= nwords) {
+      const uint4 v = *reinterpret_cast<const uint4*>(bits + w0);
+      x[0] = v.x, x[1] = v.y, x[2] = v.z, x[3] = v.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++) x[q] = w0 + q < nwords ? bits[w0 + q] : 0u;
+    }
+    uint32_t o[4], cnt = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const int64_t w = t * tile_words + q * int64_t(blockDim.x) + threadIdx.x;
-      uint32_t x = w < nwords ? bits[w] : 0u;
-      if (MODE == 0) {
-        for (uint32_t y = x; y; y &= y - 1) {
-          const int j = __ffs(y) - 1;
-          const int64_t v = w * 32 + j;
-          if (v >= n || row_ptr[v + 1] == row_ptr[v]) x &= ~(1u << j);
-        }
-      }
-      m[q] = x;
-      cnt += __popc(x);
+      o[q] = cnt;
+      cnt += __popc(x[q]);
     }
     uint32_t total;
-    uint32_t pre = block_excl_scan_u32(cnt, total, lds);
-    if (threadIdx.x == 0) s_base = total ? atomicAdd(n_out, (unsigned long long)total) : 0ull;
-    __syncthreads();
-    unsigned long long p = s_base + pre;
+    const uint32_t pre = block_excl_scan_u32(cnt, total, lds);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const int64_t w = t * tile_words + q * int64_t(blockDim.x) + threadIdx.x;
-      for (uint32_t y = m[q]; y; y &= y - 1) {
-        const int64_t v = w * 32 + (__ffs(y) - 1);
-        if (MODE == 0) static_cast<int32_t*>(out)[p++] = int32_t(v);
-        else static_cast<int64_t*>(out)[p++] = vid_of[lo + v];
+      sw[threadIdx.x * 4 + q] = x[q];
+      so[threadIdx.x * 4 + q] = pre + o[q];
+    }
+    if (threadIdx.x == 0) s_base = total ? atomicAdd(n_out, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    if (total) {
+      const unsigned long long base = s_base;
+      const int half = lane >> 5, bit = lane & 31;
+      for (int j = wv * (kTileWords / 4); j < (wv + 1) * (kTileWords / 4); j += 2) {
+        const int wi = j + half;
+        const uint32_t xw = sw[wi];
+        if (__ballot(xw != 0) == 0) continue;
+        if ((xw >> bit) & 1u) {
+          const unsigned long long p = base + so[wi] + __popc(xw & ((1u << bit) - 1u));
+          const int64_t v = (t * kTileWords + wi) * 32 + bit;
+          if (MODE == 0) static_cast<int32_t*>(out)[p] = int32_t(v);
+          else static_cast<int64_t*>(out)[p] = vid_of[lo + v];
+        }
       }
     }
     __syncthreads();
@@ -622,7 +803,7 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
   // tile = 256 threads x 4 chunks of 16 bytes = 16384 vertices; one returning atomic per tile;
   // n_set (partials[0]) and the kept out-degree sum (partials[1]) go to per-block partials.
   __shared__ uint32_t lds[8];
-  __shared__ unsigned long long lds64[64];
+  __shared__ unsigned long long lds64[kSlots * 16];
   __shared__ unsigned long long s_base;
   const int64_t nchunks = (n + 15) / 16;
   const int64_t tile = int64_t(blockDim.x) * 4;
@@ -882,8 +1063,8 @@ void exclusive_scan_dev(Ctx& c, const T* in, T* out, int64_t n) {
 }
 
 struct Counters {
-  unsigned long long* d;
-  unsigned long long h[16];
+  unsigned long long* d;  // device counters
+  unsigned long long* h;  // pinned host mirror (64 entries)
 };
 
 int64_t map_bytes(const Ctx& c) { return ((c.n_global + 63) / 64) * 64 + 64; }
@@ -898,7 +1079,7 @@ void ensure_workspaces(Ctx& c, int64_t nF_cap) {
   c.ws_front[1].ensure(size_t(nF_cap + 64) * 4);
   c.ws_off.ensure(size_t(nF_cap + 2) * 8);
   c.ws_counters.ensure(256);
-  c.ws_partials.ensure(size_t(kAggBlocks) * 4 * 8);
+  c.ws_partials.ensure(size_t(kAggBlocks) * kSlots * 8);
   c.ws_bits_send.ensure(size_t(mb / 8 + 64));
   c.ws_bits_recv.ensure(size_t(mb / 8 + 64));
   if (c.world > 1) {
@@ -1060,10 +1241,12 @@ int64_t shuffle_rows(Ctx& c, YieldArgs& ya, std::vector<DevBuf>& cols, int64_t n
 }
 
 // frontier degree scan: fills c.ws_off[0..nF] and returns total edges (synchronises)
-int64_t degree_scan(Ctx& c, const int32_t* F, int64_t nF, const Csr& csr, DevBuf& degbuf) {
+// known >= 0: the caller already has the total (from a compaction's partials): no round trip
+int64_t degree_scan(Ctx& c, const int32_t* F, int64_t nF, const Csr& csr, DevBuf& degbuf, int64_t known) {
   degbuf.ensure(size_t(nF + 1) * 8);
   k_degrees<<<grid_cap(nF + 1), 256, 0, c.stream>>>(F, nF, csr.row_ptr.as<int64_t>(), degbuf.as<int64_t>());
   exclusive_scan_dev<int64_t>(c, degbuf.as<int64_t>(), c.ws_off.as<int64_t>(), nF + 1);
+  if (known >= 0) return known;
   int64_t E = 0;
   NBG_HIP(hipMemcpyAsync(&E, c.ws_off.as<int64_t>() + nF, 8, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
@@ -1099,6 +1282,35 @@ void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Progr
   hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
   c.timing.expand_ms += ms;
   c.timing.expand_launches++;
+}
+
+// bottom-up hop over the slab: launches the kernel and the partials reduction into out[0..8)
+// (no synchronisation); returns the grid used
+int launch_bu_slab(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
+                   const FastArgs& fp, const void* slab_w, unsigned long long* out) {
+  constexpr int R = 2;
+  const Csr& tr = es.tr;
+  unsigned long long* partials = c.ws_partials.as<unsigned long long>();
+  const int64_t tiles = (tr.n_rows + 64 * R - 1) / (64 * R);
+  int grid = int(std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, std::min<int64_t>(c.opt("bu_grid", 4096), kAggBlocks))));
+  auto* nb = reinterpret_cast<unsigned long long*>(nbits);
+  const int32_t* sc = es.slab_col.as<int32_t>();
+  const int64_t* trp = tr.row_ptr.as<int64_t>();
+  const int32_t* tc = tr.col.as<int32_t>();
+  if (pk == PK_FAST)
+    k_bu_slab<PK_FAST, 4, R><<<grid, 256, 0, c.stream>>>(sc, slab_w, es.slab_k, trp, tc, tr.n_rows, fb, nb, odeg, fp,
+                                                         partials);
+  else
+    k_bu_slab<PK_NONE, 1, R><<<grid, 256, 0, c.stream>>>(sc, slab_w, es.slab_k, trp, tc, tr.n_rows, fb, nb, odeg, fp,
+                                                         partials);
+  k_reduce_partials<<<1, 256, 0, c.stream>>>(partials, grid, out);
+  NBG_HIP(hipGetLastError());
+  return grid;
+}
+// byte model of one slab hop from its counters
+uint64_t bu_slab_bytes(const unsigned long long* h, int64_t n_rows, int pred_width, bool with_odeg) {
+  return h[2] * (4 + uint64_t(pred_width)) + h[3] * 16 + h[4] * 4 + h[5] * uint64_t(pred_width) +
+         uint64_t(n_rows) / 8 + (with_odeg ? uint64_t(n_rows) * 4 : 0);
 }
 
 // bottom-up launch (timed like the expansion); returns adjacency entries examined
@@ -1145,6 +1357,7 @@ uint64_t expand_bytes(int64_t nF, int64_t E, int pred_width, int mode) {
 // GO N STEPS
 // ------------------------------------------------------------------------------------------
 int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
+  PoolScope pool_scope(c.pool);
   if (!c.finalized) throw Error(NBG_E_STATE, "snapshot not finalized");
   if (s.steps < 1) throw Error(NBG_E_INVALID_ARG, "steps must be >= 1");
   if (s.edge_type <= 0) throw Error(NBG_E_INVALID_ARG, "GO ... REVERSELY is not supported (GoExecutor.cpp:203-205)");
@@ -1191,7 +1404,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   const int64_t lo = c.owned_lo(), hi = c.owned_hi();
   const int64_t n_own = hi - lo;
   ensure_workspaces(c, std::max<int64_t>({n_own, int64_t(s.n_starts), 1}));
-  Counters K{c.ws_counters.as<unsigned long long>(), {}};
+  Counters K{c.ws_counters.as<unsigned long long>(), c.host_counters};
   DevBuf degbuf;
   uint8_t* map = c.ws_map.as<uint8_t>();
   uint16_t* bits16 = c.ws_bits_send.as<uint16_t>();  // frontier bitmap written by k_compact
@@ -1212,6 +1425,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     lookup_gidx(c, d_starts, d_sg, ns);
   }
   int cur = 0;
+  int64_t E_known = -1;  // frontier out-degree sum when a compaction already produced it
   int32_t* F = c.ws_front[0].as<int32_t>();
   int64_t nF = 0;
   int64_t nset_global = ns;  // "starts_ non-empty" (GoExecutor.cpp:93-97)
@@ -1224,9 +1438,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, F, bits16, K.d);
     }
     NBG_HIP(hipGetLastError());
-    NBG_HIP(hipMemcpyAsync(K.h, K.d, 16, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipMemcpyAsync(K.h, K.d, 128, hipMemcpyDeviceToHost, c.stream));
     NBG_HIP(hipStreamSynchronize(c.stream));
     nF = int64_t(K.h[0]);
+    if (!(s.steps == 1 && !s.distinct)) E_known = int64_t(K.h[13]);
   }
   unsigned long long* red = K.d + 24;  // scratch of the cross-rank sums
   if (es.out_nnz_global < 0) {
@@ -1275,8 +1490,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     cur ^= 1;
     F = c.ws_front[cur].as<int32_t>();
     NBG_HIP(hipMemsetAsync(K.d, 0, 8, c.stream));
-    k_bits_compact<0><<<grid_cap((n_own + 31) / 32, 1024, 4096), 256, 0, c.stream>>>(bitsA, n_own, lo, row_ptr,
-                                                                                     nullptr, F, K.d);
+    k_bits_compact<0><<<grid_cap((n_own + 31) / 32, 1024, 4096), 256, 0, c.stream>>>(bitsA, n_own, lo, nullptr, F,
+                                                                                     K.d);
     NBG_HIP(hipMemcpyAsync(K.h, K.d, 8, hipMemcpyDeviceToHost, c.stream));
     NBG_HIP(hipStreamSynchronize(c.stream));
     nF = int64_t(K.h[0]);
@@ -1286,8 +1501,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   auto ensure_off = [&]() {
     ensure_list();
     if (!off_ready) {
-      int64_t e2 = nF ? degree_scan(c, F, nF, csr, degbuf) : 0;
+      int64_t e2 = nF ? degree_scan(c, F, nF, csr, degbuf, E_known) : 0;
       E = e2;
+      E_known = e2;
       off_ready = true;
     }
   };
@@ -1304,29 +1520,25 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     if (Eg == 0) return finish_empty();  // every frontier vertex lacks out-edges
     if (want_bu(Eg)) {
       // bottom-up: frontier bitmap in, next frontier bitmap out
-      NBG_HIP(hipMemsetAsync(K.d, 0, 24, c.stream));
       const Csr& tr = es.tr;
-      int grid = grid_cap(tr.n_rows, 256, int(std::min<int64_t>(c.opt("bu_grid", 4096), kAggBlocks)));
       const uint32_t* fb = global_bits(c, bitsA);
       hipEventRecord(c.ev[2], c.stream);
-      k_bu_bits<PK_NONE><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows, fb,
-                                                     reinterpret_cast<unsigned long long*>(bitsB), row_ptr, row_ok, fp,
-                                                     partials);
-      k_reduce_partials<<<1, 256, 0, c.stream>>>(partials, grid, K.d);
-      NBG_HIP(hipGetLastError());
+      launch_bu_slab(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, nullptr, K.d);
       hipEventRecord(c.ev[3], c.stream);
-      NBG_HIP(hipMemcpyAsync(K.h, K.d, 24, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipMemcpyAsync(K.h, K.d, 64, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipEventSynchronize(c.ev[3]));
+      NBG_HIP(hipStreamSynchronize(c.stream));
       float ms = 0;
       hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
       c.timing.expand_ms += ms;
       c.timing.expand_launches++;
       c.timing.bu_steps++;
-      c.timing.expand_bytes += uint64_t(tr.n_rows) * 8 + uint64_t(tr.n_rows) / 4 + K.h[2] * 4;
+      c.timing.expand_bytes += bu_slab_bytes(K.h, tr.n_rows, 0, true);
       std::swap(bitsA, bitsB);
       have_list = false;
       off_ready = false;
       E = int64_t(K.h[1]);
+      E_known = E;
       int64_t g2[2] = {int64_t(K.h[0]), E};
       allsum(c, g2, 2, red);
       nset_global = g2[0];
@@ -1350,6 +1562,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       NBG_HIP(hipStreamSynchronize(c.stream));
       nF = int64_t(K.h[0]);
       E = int64_t(K.h[13]);
+      E_known = E;
       int64_t g2[2] = {int64_t(K.h[12]), E};
       allsum(c, g2, 2, red);
       nset_global = g2[0];
@@ -1395,32 +1608,24 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         if (pk == PK_FAST) tfp.data = es.tr.props[size_t(fpk.col)].data.p;
         const Csr& tr = es.tr;
         NBG_HIP(hipMemsetAsync(K.d, 0, 8, c.stream));
-        int grid = grid_cap(tr.n_rows, 256, int(std::min<int64_t>(c.opt("bu_grid", 4096), kAggBlocks)));
-        unsigned long long* ob = reinterpret_cast<unsigned long long*>(bitsB);
         const uint32_t* fb = global_bits(c, bitsA);
+        const void* slab_w = pk == PK_FAST ? es.slab_props[size_t(fpk.col)].p : nullptr;
         hipEventRecord(c.ev[2], c.stream);
-        if (pk == PK_FAST)
-          k_bu_bits<PK_FAST><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows, fb,
-                                                         ob, nullptr, nullptr, tfp, partials);
-        else
-          k_bu_bits<PK_NONE><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows, fb,
-                                                         ob, nullptr, nullptr, tfp, partials);
-        k_reduce_partials<<<1, 256, 0, c.stream>>>(partials, grid, K.d + 8);
+        launch_bu_slab(c, es, fb, bitsB, nullptr, pk, tfp, slab_w, K.d + 8);
         k_bits_compact<1><<<grid_cap((tr.n_rows + 31) / 32, 1024, 4096), 256, 0, c.stream>>>(
-            bitsB, tr.n_rows, lo, nullptr, c.vid_of.as<int64_t>(), vids.p, K.d);
+            bitsB, tr.n_rows, lo, c.vid_of.as<int64_t>(), vids.p, K.d);
         NBG_HIP(hipGetLastError());
         hipEventRecord(c.ev[3], c.stream);
-        NBG_HIP(hipMemcpyAsync(K.h, K.d, 96, hipMemcpyDeviceToHost, c.stream));
-        NBG_HIP(hipEventSynchronize(c.ev[3]));
+        NBG_HIP(hipMemcpyAsync(K.h, K.d, 128, hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipStreamSynchronize(c.stream));  // K.h is pinned: the copy is truly asynchronous
         float ms = 0;
         hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
         c.timing.expand_ms += ms;
         c.timing.expand_launches++;
         c.timing.bu_steps++;
-        K.h[2] = K.h[10];  // examined
         nrows = int64_t(K.h[0]);
-        c.timing.expand_bytes += uint64_t(tr.n_rows) * 8 + uint64_t(tr.n_rows) / 8 +
-                                 K.h[2] * (4 + uint64_t(pk == PK_FAST ? tfp.width : 0)) + uint64_t(nrows) * 16;
+        c.timing.expand_bytes += bu_slab_bytes(K.h + 8, tr.n_rows, pk == PK_FAST ? tfp.width : 0, false) +
+                                 uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
       } else {
         ensure_off();
         a.F = F;
@@ -1657,6 +1862,7 @@ __global__ void k_clamp_len(int64_t* l, int64_t m) {
 
 int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* vids, size_t n, const uint8_t* filter,
                       size_t flen, const nbg_prop_def* cols, size_t ncols, nbg_rows* out) {
+  PoolScope pool_scope(c.pool);
   if (!c.finalized) throw Error(NBG_E_STATE, "snapshot not finalized");
   auto* h = new HostRows();
   auto finish = [&](int64_t nrows) {

@@ -376,3 +376,27 @@ def test_rmat_direction_modes_agree(rmat12, force):
         assert (t["bu_steps"] > 0) == (force > 0)
     finally:
         sp.set_option("bu_force", 0)
+
+
+@pytest.mark.parametrize("slab,order", [(0, 1), (1, 1), (3, 1), (4, 0)])
+def test_rmat_bottom_up_slab_widths(slab, order):
+    """the bottom-up slab (first K hub-first entries per transposed row) with its fallback scan
+    gives the oracle's results for any K, with and without the final-hop predicate"""
+    st = oracle_rmat(10)
+    sp = GraphSpace(64)
+    sp.set_option("bu_slab", slab)
+    sp.set_option("degree_order", order)
+    sp.set_edge_schema(FOLLOW, [("weight", O.INT)])
+    sp.gen_rmat(10, 16, SEED, FOLLOW)
+    sp.finalize()
+    sp.set_option("bu_force", 1)
+    starts = sorted(set(seeds_from(10, 24, seed=4)))
+    for k in (0, 499, 900):
+        w = X.AliasProp("follow", "weight") > k
+        for steps in (1, 2, 3):
+            g = sp.go(starts, steps, FOLLOW, where=w, yields=[X.EdgeDst("follow")], distinct=True)
+            r = st.go(starts, steps, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()], distinct=True)
+            assert np.array_equal(np.sort(g.columns[0]), np.sort(r.int_col(0)))
+            assert g.edges_scanned == r.edges_scanned
+    assert sp.last_timing()["bu_steps"] > 0
+    sp.close()
