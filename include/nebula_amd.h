@@ -136,6 +136,10 @@ typedef struct {
   int32_t* failed_parts;
   int32_t* failed_codes;
   uint64_t edges_scanned; /* adjacency entries read (TEPS numerator)            */
+  /* nbg_shortest_path: path of row i = path_vids[path_offsets[i] .. path_offsets[i+1])
+   * (empty when the pair is unreachable); host memory.  NULL for other calls.              */
+  int64_t* path_offsets;  /* n_rows+1 */
+  int64_t* path_vids;
   void* _impl;
 } nbg_rows;
 void nbg_rows_free(nbg_rows* rows);
@@ -180,10 +184,14 @@ typedef struct {
 int32_t nbg_go(nbg_ctx* ctx, const nbg_go_spec* spec, nbg_rows* out);
 
 /* ---- FIND SHORTEST PATH (no reference implementation: FindExecutor.cpp:20-22) ------------
- * Batched bidirectional BFS over edge_type out-edges / -edge_type in-edges.  out rows:
- * [src, dst, hops] per pair (hops = -1 if unreachable within max_steps) plus the path
- * (lexicographically smallest vid sequence among shortest paths) in a STRING-free form:
- * path vids flattened in cols[3] with per-row offsets in vertex_row_offsets.                */
+ * Definition (owned by this build): the unweighted hop distance from src to
+ * dst over edge_type out-edges, -1 when dst is not reached within max_steps hops; the path is
+ * the lexicographically smallest vid sequence among the shortest paths.  Distances toward dst
+ * follow the -edge_type in-edge keys (P5: INSERT EDGE writes both), so parity with the oracle
+ * assumes the in-edge keys mirror the out-edge keys, as the write path guarantees.
+ * Runs as batched bidirectional BFS (pairs in batches, option "sp_batch").
+ * out: 3 VID columns [src, dst, hops] per pair, in input order; paths in path_offsets /
+ * path_vids (src ... dst, hops+1 vids).  src == dst gives hops 0 and the path [src].        */
 int32_t nbg_shortest_path(nbg_ctx* ctx, int32_t edge_type, const int64_t* src,
                           const int64_t* dst, size_t npairs, int32_t max_steps, nbg_rows* out);
 

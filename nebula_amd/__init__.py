@@ -6,8 +6,9 @@ multi-step frontier loop, as hand-written HIP kernels for gfx950 behind a C ABI
 """
 from . import expr  # noqa: F401
 from ._lib import NbgError, load  # noqa: F401
-from .engine import (GetNeighborsRequest, GoExecutor, GraphSpace, PropDef, QueryBoundProcessor,  # noqa: F401
-                     QueryResponse, RowSet, pack_kv)
+from .engine import (FindPathExecutor, GetNeighborsRequest, GoExecutor, GraphSpace, PathResult,  # noqa: F401
+                     PropDef, QueryBoundProcessor, QueryResponse, RowSet, pack_kv)
 
-__all__ = ["GraphSpace", "QueryBoundProcessor", "GoExecutor", "GetNeighborsRequest", "PropDef",
+__all__ = ["GraphSpace", "QueryBoundProcessor", "GoExecutor", "FindPathExecutor", "PathResult",
+           "GetNeighborsRequest", "PropDef",
            "QueryResponse", "RowSet", "NbgError", "expr", "load", "pack_kv"]

@@ -53,7 +53,8 @@ class Rows(C.Structure):
                 ("n_vertices", C.c_int64), ("vertex_ids", C.POINTER(C.c_int64)),
                 ("vertex_row_offsets", C.POINTER(C.c_int64)), ("n_failed", C.c_int32),
                 ("failed_parts", C.POINTER(C.c_int32)), ("failed_codes", C.POINTER(C.c_int32)),
-                ("edges_scanned", C.c_uint64), ("_impl", C.c_void_p)]
+                ("edges_scanned", C.c_uint64), ("path_offsets", C.POINTER(C.c_int64)),
+                ("path_vids", C.POINTER(C.c_int64)), ("_impl", C.c_void_p)]
 
 
 class PropDef(C.Structure):

@@ -257,6 +257,10 @@ struct Ctx {
   DevBuf ws_bits_xchg;  // world > 1: received mark segments [world][owned/32]
   DevBuf ws_starts;
   DevBuf ws_partials;  // per-block partial sums of the aggregated kernels
+  // FIND SHORTEST PATH distance bytes [side][pair][owned row], kept 0xFF between calls
+  DevBuf sp_dist[2];
+  size_t sp_dist_bytes = 0;
+  bool sp_dirty = false;
   Timing timing;
   hipEvent_t ev[8] = {};
   std::shared_ptr<BufPool> pool = std::make_shared<BufPool>();

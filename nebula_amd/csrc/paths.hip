@@ -1,0 +1,716 @@
+// paths.hip -- FIND SHORTEST PATH as batched bidirectional BFS on the GO snapshot
+// (SURVEY 8a row A10).
+//
+// The reference has no implementation (src/graph/FindExecutor.cpp:20-22 is a stub and the
+// parser has no grammar for it), so the definition is this build's (include/nebula_amd.h):
+// the hop distance over out-edges of one type, and the lexicographically smallest vid sequence
+// among the shortest paths.  The oracle (oracle/refcpu.cpp ora_shortest_path) states it as a
+// backward BFS from dst over the -type in-edge keys followed by a greedy walk from src.
+//
+// Device algorithm, for a batch of B pairs at once (one context = one GPU):
+//  * per side (F = forward from src over the out CSR, B = backward from dst over the in CSR),
+//    pair and owned vertex, a distance byte dist[side][pair * n + row] (0xFF = unseen).  A
+//    claim is a CAS on the 32-bit word holding the byte, so each (side, pair, vertex) enters
+//    exactly one frontier.
+//  * frontiers are lists of 64-bit tuples (side | pair | level | row) of all pairs together.
+//    Every iteration each active pair expands the side whose frontier has the smaller sum of
+//    (degree + 1), and ONE edge-balanced launch (the GO expansion's LDS tile scheme: 2048
+//    adjacency entries per workgroup, owner found by binary search in LDS) expands the chosen
+//    sides of all pairs; hubs spread over many tiles.
+//  * a claim of a vertex the other side has already seen is a meet.  With depths (f, b) after
+//    that expansion the distance is f + b, and the meet set is exactly the set of vertices at
+//    position f of the shortest paths (any seen-by-both vertex has ds <= f, dt <= b and
+//    ds + dt >= f + b, so ds = f and dt = b).
+//  * path: the backward distances are extended from the meet set toward src over in-edges,
+//    restricted to vertices whose forward distance completes a shortest path (the "sweep");
+//    afterwards every shortest-path vertex carries its exact distance to dst, and one wave per
+//    pair walks from src taking the smallest vid w among out-neighbours with
+//    dist_B(w) = L - i - 1, the oracle's greedy rule.
+//  * every claimed byte is recorded in an arena and reset after the batch, so the distance
+//    arrays (2 * B * n bytes, HBM-sized) stay allocated and clean across calls.
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <cmath>
+
+#include "device_common.h"
+#include "engine.h"
+#include "rows.h"
+
+namespace nbg {
+namespace {
+
+constexpr int kT = 256;
+constexpr int kIt = 8;
+constexpr int kTileE = kT * kIt;
+
+enum : int32_t { SP_ACTIVE = 0, SP_MET = 1, SP_DONE = 2 };
+// device counters (one array): live list F / B, arena, meets, X list, active pairs, overflow,
+// sweep list, X edges
+enum : int { C_LIVE0 = 0, C_LIVE1 = 1, C_ARENA = 2, C_MEET = 3, C_X = 4, C_ACTIVE = 5, C_OVF = 6, C_SWEEP = 7,
+             C_XE = 8, C_WALKERR = 9, C_N = 16 };
+
+__host__ __device__ inline uint64_t mk_tup(uint32_t side, uint32_t pair, uint32_t lvl, uint32_t row) {
+  return (uint64_t(side) << 63) | (uint64_t(pair & 0x7FFFFFu) << 40) | (uint64_t(lvl & 0xFFu) << 32) | uint64_t(row);
+}
+__device__ inline uint32_t t_side(uint64_t t) { return uint32_t(t >> 63); }
+__device__ inline uint32_t t_pair(uint64_t t) { return uint32_t(t >> 40) & 0x7FFFFFu; }
+__device__ inline uint32_t t_lvl(uint64_t t) { return uint32_t(t >> 32) & 0xFFu; }
+__device__ inline uint32_t t_row(uint64_t t) { return uint32_t(t); }
+
+struct SpCsr {  // one direction's adjacency over the owned rows
+  const int64_t* row_ptr;
+  const int32_t* col;     // global gidx of the other end
+  const uint8_t* row_ok;  // rows whose keys sit outside hash(vid)'s part are invisible
+};
+
+__device__ inline int64_t sp_deg(const SpCsr& g, uint32_t r) {
+  if (g.row_ok && !g.row_ok[r]) return 0;
+  return g.row_ptr[r + 1] - g.row_ptr[r];
+}
+
+struct SpState {  // per-pair arrays, B entries each
+  int32_t* state;
+  int32_t* res;             // hops (-1 unreachable)
+  int32_t* lvl;             // [2][B] depth of each side
+  int32_t* side;            // side expanded this iteration
+  int32_t* met;
+  unsigned long long* deg;  // [2][B] frontier sum of (degree + 1)
+  int32_t B;
+};
+
+struct SpBufs {
+  uint64_t* live_next[2];
+  uint64_t* arena;
+  uint64_t* meet;
+  uint64_t* sweep_next;
+  int64_t cap_live[2], cap_arena, cap_meet, cap_sweep;
+};
+
+__device__ inline unsigned long long wsum(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// wave-aggregated arr[key] += v over the lanes with act (lanes of one wave mostly share a key:
+// an edge tile covers consecutive frontier entries, usually of one pair).  Wave-uniform call.
+__device__ inline void wave_add_keyed(unsigned long long* arr, uint32_t key, unsigned long long v, bool act) {
+  const int lane = threadIdx.x & 63;
+  uint64_t m = __ballot(act);
+  while (m) {
+    const int leader = __ffsll((long long)m) - 1;
+    const uint32_t k = uint32_t(__shfl(int(key), leader));
+    const bool mine = act && key == k;
+    const unsigned long long s = wsum(mine ? v : 0ull);
+    if (lane == leader) atomicAdd(arr + k, s);
+    m &= ~__ballot(mine);
+    act = act && !mine;
+  }
+}
+
+// append with a capacity guard (an overflow sets C_OVF; the host sizes lists so it never does)
+__device__ inline void put(uint64_t* list, int64_t cap, unsigned long long* cnt, int which, bool pred, uint64_t v) {
+  const int64_t s = wave_append(cnt + which, pred);
+  if (pred) {
+    if (s < cap) list[s] = v;
+    else atomicOr(cnt + C_OVF, 1ull);
+  }
+}
+
+// claim the unseen (0xFF) distance byte idx with val: true for exactly one caller
+__device__ inline bool claim_byte(uint8_t* base, uint64_t idx, uint32_t val) {
+  if (base[idx] != 0xFF) return false;  // already seen (values only leave 0xFF within a batch)
+  uint32_t* w = reinterpret_cast<uint32_t*>(base + (idx & ~uint64_t(3)));
+  const uint32_t sh = uint32_t(idx & 3) * 8;
+  uint32_t old = *reinterpret_cast<volatile uint32_t*>(w);
+  while (((old >> sh) & 0xFFu) == 0xFFu) {
+    const uint32_t nw = (old & ~(0xFFu << sh)) | (val << sh);
+    const uint32_t prev = atomicCAS(w, old, nw);
+    if (prev == old) return true;
+    old = prev;
+  }
+  return false;
+}
+
+// seed both frontiers; trivial pairs (src == dst, unknown vertex, max_steps < 1) finish here
+__global__ void k_sp_init(const int64_t* svid, const int64_t* tvid, const int32_t* gs, const int32_t* gt, int32_t B,
+                          int32_t max_steps, int64_t n, SpState st, SpCsr gout, SpCsr gin, uint8_t* d0, uint8_t* d1,
+                          SpBufs bf, unsigned long long* cnt) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;  // grid covers B rounded up to a block
+  bool go = false;
+  int32_t a = -1, b = -1;
+  if (p < B) {
+    a = gs[p];
+    b = gt[p];
+    st.res[p] = svid[p] == tvid[p] ? 0 : -1;
+    st.lvl[p] = st.lvl[B + p] = 0;
+    st.met[p] = 0;
+    go = svid[p] != tvid[p] && a >= 0 && b >= 0 && max_steps >= 1;
+    st.state[p] = go ? SP_ACTIVE : SP_DONE;
+    st.deg[p] = st.deg[B + p] = 0;
+    if (go) {
+      d0[uint64_t(p) * n + uint32_t(a)] = 0;
+      d1[uint64_t(p) * n + uint32_t(b)] = 0;
+      st.deg[p] = (unsigned long long)sp_deg(gout, uint32_t(a)) + 1;
+      st.deg[B + p] = (unsigned long long)sp_deg(gin, uint32_t(b)) + 1;
+    }
+  }
+  const uint64_t tf = mk_tup(0, uint32_t(p), 0, uint32_t(a)), tb = mk_tup(1, uint32_t(p), 0, uint32_t(b));
+  put(bf.live_next[0], bf.cap_live[0], cnt, C_LIVE0, go, tf);
+  put(bf.live_next[1], bf.cap_live[1], cnt, C_LIVE1, go, tb);
+  put(bf.arena, bf.cap_arena, cnt, C_ARENA, go, tf);
+  put(bf.arena, bf.cap_arena, cnt, C_ARENA, go, tb);
+}
+
+// end of an iteration (first = 0) and the side choice of the next one
+__global__ void k_sp_step(SpState st, int32_t max_steps, int32_t first, unsigned long long* cnt) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  bool active = false;
+  if (p < st.B && st.state[p] == SP_ACTIVE) {
+    const int B = st.B;
+    if (!first) {
+      const int s = st.side[p];
+      st.lvl[s * B + p] += 1;
+      const int32_t L = st.lvl[p] + st.lvl[B + p];
+      if (st.met[p]) {
+        st.res[p] = L;
+        st.state[p] = SP_MET;
+      } else if (st.deg[s * B + p] == 0 || L >= max_steps) {
+        st.state[p] = SP_DONE;  // a side's reachable set is closed, or the step bound is hit
+      }
+    }
+    if (st.state[p] == SP_ACTIVE) {
+      const int s = st.deg[p] <= st.deg[B + p] ? 0 : 1;
+      st.side[p] = s;
+      st.deg[s * B + p] = 0;  // the expansion accumulates the new frontier's sum
+      active = true;
+    }
+  }
+  const int64_t slot = wave_append(cnt + C_ACTIVE, active);
+  (void)slot;
+}
+
+// split a live list: tuples of the side their pair expands now -> X (with degrees), the rest
+// of still-active pairs -> carried into the next live list.  sweep = 1: the list holds sweep
+// tuples; those of MET pairs short of src go to X.
+__global__ void k_sp_select(const uint64_t* __restrict__ live, int64_t nl, int32_t sweep, SpState st, SpCsr gout,
+                            SpCsr gin, uint64_t* X, int64_t* Xdeg, int64_t cap_x, SpBufs bf,
+                            unsigned long long* cnt) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int64_t rounds = (nl + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    bool go = false, stay = false;
+    uint64_t t = 0;
+    uint32_t side = 0;
+    int64_t d = 0;
+    if (i < nl) {
+      t = live[i];
+      const uint32_t p = t_pair(t);
+      side = t_side(t);
+      const int32_t s = st.state[p];
+      if (sweep) {
+        go = s == SP_MET && int32_t(t_lvl(t)) < st.res[p];
+      } else if (s == SP_ACTIVE) {
+        go = uint32_t(st.side[p]) == side;
+        stay = !go;
+      }
+      if (go) d = sp_deg(side ? gin : gout, t_row(t));
+    }
+    const int64_t xs = wave_append(cnt + C_X, go);
+    if (go) {
+      if (xs < cap_x) {
+        X[xs] = t;
+        Xdeg[xs] = d;
+      } else {
+        atomicOr(cnt + C_OVF, 2ull);
+      }
+    }
+    const unsigned long long e = wsum((unsigned long long)d);
+    if ((threadIdx.x & 63) == 0 && e) atomicAdd(cnt + C_XE, e);
+    // carried tuples: every tuple of one launch has the same side (one list per side)
+    put(bf.live_next[side], bf.cap_live[side], cnt, side ? C_LIVE1 : C_LIVE0, stay, t);
+  }
+}
+
+struct SpExpand {
+  const uint64_t* X;
+  int64_t nX;
+  const int64_t* off;  // exclusive scan of X degrees, off[nX] = E
+  SpCsr g[2];          // [0] out CSR (forward), [1] in CSR (backward)
+  uint8_t* dist[2];
+  const int64_t* vid_of;
+  int64_t n;           // owned rows (pair stride of dist)
+  int64_t lo;
+  int32_t sweep;
+};
+
+// One edge-balanced pass over the adjacency of every X tuple (tiles of kTileE entries).
+//  sweep = 0: BFS level of the chosen side; claims append to that side's next live list (and
+//             the arena), add (degree + 1) to the pair's frontier sum, and detect meets.
+//  sweep = 1: backward extension restricted to shortest paths: u (in-neighbour of w, which has
+//             dt = l) is on a shortest path iff ds(u) = L - l - 1; it gets dt = l + 1.
+__global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs bf, unsigned long long* cnt) {
+  __shared__ int32_t s_off[kTileE + 1];
+  __shared__ int64_t s_rs[kTileE];
+  __shared__ uint64_t s_tup[kTileE];
+  __shared__ int64_t s_hdr[2];
+  const int64_t nX = a.nX;
+  const int64_t E = a.off[nX];
+  const int64_t ntiles = (E + kTileE - 1) / kTileE;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t e0 = t * kTileE;
+    const int64_t e1 = min(e0 + int64_t(kTileE), E);
+    if (threadIdx.x == 0) {
+      int64_t lo = 0, hi = nX;  // off[lo] <= e0 < off[hi]
+      while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a.off[mid] <= e0) lo = mid; else hi = mid;
+      }
+      const int64_t i0 = lo;
+      hi = nX;
+      while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a.off[mid] <= e1 - 1) lo = mid; else hi = mid;
+      }
+      s_hdr[0] = i0;
+      s_hdr[1] = lo - i0 + 1;
+    }
+    __syncthreads();
+    const int64_t i0 = s_hdr[0];
+    const int cnt_k = int(s_hdr[1]);
+    for (int k = threadIdx.x; k <= cnt_k; k += kT) {
+      const int64_t o = a.off[i0 + k];
+      s_off[k] = int32_t(min(o - e0, int64_t(kTileE + 1)));
+      if (k < cnt_k) {
+        const uint64_t tu = a.X[i0 + k];
+        s_tup[k] = tu;
+        s_rs[k] = a.g[t_side(tu)].row_ptr[t_row(tu)] - o;
+      }
+    }
+    __syncthreads();
+    for (int r = 0; r < kIt; r++) {
+      const int j = threadIdx.x + r * kT;
+      const int64_t e = e0 + j;
+      const bool valid = e < e1;
+      int k = 0;
+      if (valid) {
+        int lo = 0, hi = cnt_k;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (s_off[mid] <= j) lo = mid; else hi = mid;
+        }
+        k = lo;
+      }
+      const uint64_t tu = s_tup[k];
+      const uint32_t side = t_side(tu), p = t_pair(tu), l = t_lvl(tu);
+      uint32_t w = 0;
+      bool claimed = false;
+      if (valid) {
+        w = uint32_t(int64_t(a.g[side].col[s_rs[k] + e]) - a.lo);
+        const uint64_t idx = uint64_t(p) * uint64_t(a.n) + w;
+        if (!a.sweep) {
+          claimed = claim_byte(a.dist[side], idx, l + 1);
+        } else {
+          const int32_t need = st.res[p] - int32_t(l) - 1;
+          if (need >= 0 && a.dist[0][idx] == uint8_t(need)) claimed = claim_byte(a.dist[1], idx, l + 1);
+        }
+      }
+      const uint64_t nt = mk_tup(side, p, l + 1, w);
+      put(bf.arena, bf.cap_arena, cnt, C_ARENA, claimed, nt);
+      if (a.sweep) {
+        put(bf.sweep_next, bf.cap_sweep, cnt, C_SWEEP, claimed, nt);
+        continue;
+      }
+      put(bf.live_next[0], bf.cap_live[0], cnt, C_LIVE0, claimed && side == 0, nt);
+      put(bf.live_next[1], bf.cap_live[1], cnt, C_LIVE1, claimed && side == 1, nt);
+      const unsigned long long dv = claimed ? (unsigned long long)sp_deg(a.g[side], w) + 1 : 0ull;
+      wave_add_keyed(st.deg, side * uint32_t(st.B) + p, dv, claimed);
+      bool meet = false;
+      uint32_t dt = 0;
+      if (claimed) {
+        const uint8_t o = a.dist[side ^ 1][uint64_t(p) * uint64_t(a.n) + w];
+        if (o != 0xFF) {
+          meet = true;
+          dt = side ? l + 1 : uint32_t(o);
+          st.met[p] = 1;
+        }
+      }
+      put(bf.meet, bf.cap_meet, cnt, C_MEET, meet, mk_tup(1, p, dt, w));
+    }
+    __syncthreads();
+  }
+}
+
+// one wave per pair that met: greedy walk from src (dist_B now exact on every shortest path)
+__global__ void k_sp_walk(SpState st, const int32_t* gs, const int64_t* path_off, int64_t* path, SpCsr gout,
+                          const uint8_t* dist_b, const int64_t* vid_of, int64_t n, int64_t lo,
+                          unsigned long long* cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t p = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  if (p >= st.B || st.state[p] != SP_MET) return;
+  const int32_t L = st.res[p];
+  const int64_t o = path_off[p];
+  uint32_t v = uint32_t(gs[p]);
+  if (lane == 0) path[o] = vid_of[lo + v];
+  const uint8_t* db = dist_b + uint64_t(p) * uint64_t(n);
+  for (int32_t i = 0; i < L; i++) {
+    const uint8_t need = uint8_t(L - i - 1);
+    int64_t best = INT64_MAX;
+    int64_t bw = -1;
+    if (!(gout.row_ok && !gout.row_ok[v])) {
+      const int64_t e1 = gout.row_ptr[v + 1];
+      for (int64_t e = gout.row_ptr[v] + lane; e < e1; e += 64) {
+        const int64_t w = int64_t(gout.col[e]) - lo;
+        if (db[w] == need) {
+          const int64_t vv = vid_of[lo + w];
+          if (vv < best) {
+            best = vv;
+            bw = w;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+      const int64_t ob = __shfl_xor(best, s);
+      const int64_t ow = __shfl_xor(bw, s);
+      if (ow >= 0 && (bw < 0 || ob < best)) {
+        best = ob;
+        bw = ow;
+      }
+    }
+    if (bw < 0) {  // in-edge keys without the mirrored out-edge: the definition does not hold
+      if (lane == 0) atomicAdd(cnt + C_WALKERR, 1ull);
+      return;
+    }
+    v = uint32_t(bw);
+    if (lane == 0) path[o + i + 1] = best;
+  }
+}
+
+// reset every claimed distance byte of the batch
+__global__ void k_sp_clear(const uint64_t* arena, int64_t m, uint8_t* d0, uint8_t* d1, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    const uint64_t t = arena[i];
+    (t_side(t) ? d1 : d0)[uint64_t(t_pair(t)) * uint64_t(n) + t_row(t)] = 0xFF;
+  }
+}
+
+int grid_n(int64_t n, int cap = 4096) {
+  return int(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap)));
+}
+
+// grow a list keeping its first `used` elements (stream-ordered copy)
+void grow_keep(Ctx& c, DevBuf& b, int64_t need, int64_t used, int64_t& cap) {
+  if (need <= cap) return;
+  const int64_t nc = std::max<int64_t>(need + need / 2, 1 << 16);
+  DevBuf nb;
+  nb.alloc(size_t(nc) * 8);
+  if (used > 0) NBG_HIP(hipMemcpyAsync(nb.p, b.p, size_t(used) * 8, hipMemcpyDeviceToDevice, c.stream));
+  b = std::move(nb);
+  cap = nc;
+}
+
+}  // namespace
+
+int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t* dst, size_t npairs, int32_t max_steps,
+                          nbg_rows* out) {
+  if (!c.finalized) throw Error(NBG_E_STATE, "snapshot not finalized");
+  if (et <= 0) throw Error(NBG_E_INVALID_ARG, "edge type must be > 0 (paths follow out-edges)");
+  if (max_steps > 254) throw Error(NBG_E_UNSUPPORTED, "max_steps above 254");
+  if (c.world > 1) throw Error(NBG_E_UNSUPPORTED, "sharded FIND SHORTEST PATH is not built yet (one rank only)");
+  auto it = c.edges.find(et);
+  if (it == c.edges.end()) throw Error(NBG_E_INVALID_ARG, "edge type not in snapshot");
+  EdgeSpace& es = it->second;
+  const int64_t lo = c.owned_lo(), n = std::max<int64_t>(c.owned_hi() - lo, 1);
+  if (!es.out.row_ptr.p || !es.in.row_ptr.p) throw Error(NBG_E_STATE, "missing CSR");
+
+  // batch size: bounded by the distance arrays' HBM budget (2 bytes per pair and vertex)
+  const int64_t budget = c.opt("sp_mem_mb", 96 * 1024) << 20;
+  int64_t B = std::min<int64_t>(c.opt("sp_batch", 1024), std::max<int64_t>(1, budget / (2 * n)));
+  B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(int64_t(npairs), 1)));
+  B = std::min<int64_t>(B, 0x7FFFFF);
+  const size_t dist_bytes = ((size_t(B) * size_t(n) + 3) & ~size_t(3)) + 64;
+  if (c.sp_dist_bytes < dist_bytes || c.sp_dirty) {
+    for (auto& d : c.sp_dist) d.release();
+    PoolScope none(nullptr);  // the distance arrays live outside the query pool
+    for (auto& d : c.sp_dist) {
+      d.alloc(dist_bytes);
+      NBG_HIP(hipMemsetAsync(d.p, 0xFF, dist_bytes, c.stream));
+    }
+    c.sp_dist_bytes = dist_bytes;
+    c.sp_dirty = false;
+  }
+  PoolScope pool_scope(c.pool);
+  c.timing = Timing{};
+  hipEventRecord(c.ev[0], c.stream);
+
+  uint8_t* d0 = c.sp_dist[0].as<uint8_t>();
+  uint8_t* d1 = c.sp_dist[1].as<uint8_t>();
+  SpCsr gout{es.out.row_ptr.as<int64_t>(), es.out.col.as<int32_t>(), es.out.row_ok.as<uint8_t>()};
+  SpCsr gin{es.in.row_ptr.as<int64_t>(), es.in.col.as<int32_t>(), es.in.row_ok.as<uint8_t>()};
+  const int64_t* vid_of = c.vid_of.as<int64_t>();
+
+  DevBuf dstate, dcnt, dvids, dg;
+  dstate.alloc(size_t(B) * 4 * 7 + size_t(B) * 16 + 64);
+  SpState st{};
+  st.B = int32_t(B);
+  st.deg = dstate.as<unsigned long long>();
+  st.state = reinterpret_cast<int32_t*>(st.deg + 2 * B);
+  st.res = st.state + B;
+  st.lvl = st.res + B;
+  st.side = st.lvl + 2 * B;
+  st.met = st.side + B;
+  dcnt.alloc(C_N * 8);
+  unsigned long long* cnt = dcnt.as<unsigned long long>();
+  unsigned long long* hc = c.host_counters;  // pinned
+  dvids.alloc(size_t(B) * 16);
+  dg.alloc(size_t(B) * 8);
+  int64_t* dsv = dvids.as<int64_t>();
+  int64_t* dtv = dsv + B;
+  int32_t* dgs = dg.as<int32_t>();
+  int32_t* dgt = dgs + B;
+
+  DevBuf live[2], live_next[2], arena, meet, sweep[2], X, Xdeg, Xoff;
+  int64_t cap_live[2] = {0, 0}, cap_next[2] = {0, 0}, cap_arena = 0, cap_meet = 0, cap_sweep[2] = {0, 0};
+  int64_t cap_x = 0;
+
+  std::vector<int64_t> hres(npairs), hoff(1, 0), hpath;
+  std::vector<int32_t> hstate(static_cast<size_t>(B)), hres_b(static_cast<size_t>(B));
+  c.sp_dirty = true;  // until the batch's bytes are reset
+  for (size_t b0 = 0; b0 < npairs; b0 += size_t(B)) {
+    const int64_t nb = std::min<int64_t>(B, int64_t(npairs - b0));
+    st.B = int32_t(nb);
+    NBG_HIP(hipMemcpyAsync(dsv, src + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
+    NBG_HIP(hipMemcpyAsync(dtv, dst + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
+    lookup_gidx(c, dsv, dgs, nb);
+    lookup_gidx(c, dtv, dgt, nb);
+    // per-pair state arrays are indexed with stride nb ([2][nb] blocks)
+    st.state = reinterpret_cast<int32_t*>(st.deg + 2 * nb);
+    st.res = st.state + nb;
+    st.lvl = st.res + nb;
+    st.side = st.lvl + 2 * nb;
+    st.met = st.side + nb;
+    NBG_HIP(hipMemsetAsync(cnt, 0, C_N * 8, c.stream));
+    for (int s = 0; s < 2; s++) grow_keep(c, live_next[s], nb + 64, 0, cap_next[s]);
+    grow_keep(c, arena, 2 * nb + 64, 0, cap_arena);
+    grow_keep(c, meet, 1 << 16, 0, cap_meet);
+    SpBufs bf{};
+    auto refresh = [&]() {
+      bf.live_next[0] = live_next[0].as<uint64_t>();
+      bf.live_next[1] = live_next[1].as<uint64_t>();
+      bf.arena = arena.as<uint64_t>();
+      bf.meet = meet.as<uint64_t>();
+      bf.cap_live[0] = cap_next[0];
+      bf.cap_live[1] = cap_next[1];
+      bf.cap_arena = cap_arena;
+      bf.cap_meet = cap_meet;
+      bf.sweep_next = sweep[1].as<uint64_t>();
+      bf.cap_sweep = cap_sweep[1];
+    };
+    refresh();
+    k_sp_init<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(dsv, dtv, dgs, dgt, int32_t(nb), max_steps, n, st, gout, gin,
+                                                         d0, d1, bf, cnt);
+    k_sp_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, max_steps, 1, cnt);
+    NBG_HIP(hipGetLastError());
+    NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    int64_t n_live[2] = {int64_t(hc[C_LIVE0]), int64_t(hc[C_LIVE1])};
+    int64_t n_arena = int64_t(hc[C_ARENA]), n_meet = 0;
+    int64_t active = int64_t(hc[C_ACTIVE]);
+    for (int s = 0; s < 2; s++) {
+      std::swap(live[s], live_next[s]);
+      std::swap(cap_live[s], cap_next[s]);
+    }
+    auto launch_scan = [&](int64_t nX) {
+      size_t tb = 0;
+      NBG_HIP(hipMemsetAsync(Xdeg.as<int64_t>() + nX, 0, 8, c.stream));
+      NBG_HIP(rocprim::exclusive_scan(nullptr, tb, Xdeg.as<int64_t>(), Xoff.as<int64_t>(), int64_t(0), size_t(nX + 1),
+                                      rocprim::plus<int64_t>(), c.stream));
+      c.ws_tmp.ensure(tb);
+      NBG_HIP(rocprim::exclusive_scan(c.ws_tmp.p, tb, Xdeg.as<int64_t>(), Xoff.as<int64_t>(), int64_t(0),
+                                      size_t(nX + 1), rocprim::plus<int64_t>(), c.stream));
+    };
+    auto launch_expand = [&](int64_t nX, int64_t E, int32_t sweep_mode) {
+      SpExpand a{};
+      a.X = X.as<uint64_t>();
+      a.nX = nX;
+      a.off = Xoff.as<int64_t>();
+      a.g[0] = gout;
+      a.g[1] = gin;
+      a.dist[0] = d0;
+      a.dist[1] = d1;
+      a.vid_of = vid_of;
+      a.n = n;
+      a.lo = lo;
+      a.sweep = sweep_mode;
+      const int64_t tiles = (E + kTileE - 1) / kTileE;
+      const int grid = int(std::max<int64_t>(1, std::min<int64_t>(tiles, c.opt("sp_grid", 256 * 8))));
+      hipEventRecord(c.ev[2], c.stream);
+      k_sp_expand<<<grid, kT, 0, c.stream>>>(a, st, bf, cnt);
+      NBG_HIP(hipGetLastError());
+      hipEventRecord(c.ev[3], c.stream);
+    };
+    auto expand_time = [&]() {
+      float ms = 0;
+      hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
+      c.timing.expand_ms += ms;
+      c.timing.expand_launches++;
+    };
+    auto ensure_x = [&](int64_t need) {
+      if (need + 1 > cap_x) {
+        cap_x = std::max<int64_t>(need + need / 2 + 64, 1 << 16);
+        X.alloc(size_t(cap_x) * 8);
+        Xdeg.alloc(size_t(cap_x + 1) * 8);
+        Xoff.alloc(size_t(cap_x + 1) * 8);
+      }
+    };
+
+    while (active > 0) {
+      c.timing.steps_run++;
+      // live lists -> X (expanding side) + carried tuples
+      ensure_x(n_live[0] + n_live[1]);
+      for (int s = 0; s < 2; s++) grow_keep(c, live_next[s], n_live[s] + 64, 0, cap_next[s]);
+      refresh();
+      NBG_HIP(hipMemsetAsync(cnt + C_LIVE0, 0, 16, c.stream));
+      NBG_HIP(hipMemsetAsync(cnt + C_X, 0, 16, c.stream));  // C_X, C_ACTIVE
+      NBG_HIP(hipMemsetAsync(cnt + C_XE, 0, 8, c.stream));
+      for (int s = 0; s < 2; s++)
+        if (n_live[s])
+          k_sp_select<<<grid_n(n_live[s]), 256, 0, c.stream>>>(live[s].as<uint64_t>(), n_live[s], 0, st, gout, gin,
+                                                                 X.as<uint64_t>(), Xdeg.as<int64_t>(), cap_x, bf, cnt);
+      NBG_HIP(hipGetLastError());
+      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      if (hc[C_OVF]) throw Error(NBG_E_UNKNOWN, "shortest path: list overflow");
+      const int64_t nX = int64_t(hc[C_X]), E = int64_t(hc[C_XE]);
+      const int64_t carried[2] = {int64_t(hc[C_LIVE0]), int64_t(hc[C_LIVE1])};
+      c.timing.edges_scanned += uint64_t(E);
+      if (E > 0) {
+        // every edge may claim once: size the lists for the worst case
+        for (int s = 0; s < 2; s++) grow_keep(c, live_next[s], carried[s] + E + 64, carried[s], cap_next[s]);
+        grow_keep(c, arena, n_arena + E + 64, n_arena, cap_arena);
+        grow_keep(c, meet, n_meet + E + 64, n_meet, cap_meet);
+        refresh();
+        launch_scan(nX);
+        launch_expand(nX, E, 0);
+      }
+      k_sp_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, max_steps, 0, cnt);
+      NBG_HIP(hipGetLastError());
+      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      if (E > 0) expand_time();
+      if (hc[C_OVF]) throw Error(NBG_E_UNKNOWN, "shortest path: list overflow");
+      c.timing.expand_bytes += uint64_t(nX) * 32 + uint64_t(E) * 5 + (hc[C_ARENA] - uint64_t(n_arena)) * 26;
+      n_live[0] = int64_t(hc[C_LIVE0]);
+      n_live[1] = int64_t(hc[C_LIVE1]);
+      n_arena = int64_t(hc[C_ARENA]);
+      n_meet = int64_t(hc[C_MEET]);
+      active = int64_t(hc[C_ACTIVE]);
+      for (int s = 0; s < 2; s++) {
+        std::swap(live[s], live_next[s]);
+        std::swap(cap_live[s], cap_next[s]);
+      }
+    }
+
+    // sweep: extend dist_B from the meet sets toward src along shortest paths only
+    int64_t n_sw = n_meet;
+    std::swap(sweep[0], meet);
+    std::swap(cap_sweep[0], cap_meet);
+    while (n_sw > 0) {
+      ensure_x(n_sw);
+      NBG_HIP(hipMemsetAsync(cnt + C_X, 0, 8, c.stream));
+      NBG_HIP(hipMemsetAsync(cnt + C_XE, 0, 8, c.stream));
+      NBG_HIP(hipMemsetAsync(cnt + C_SWEEP, 0, 8, c.stream));
+      refresh();
+      k_sp_select<<<grid_n(n_sw), 256, 0, c.stream>>>(sweep[0].as<uint64_t>(), n_sw, 1, st, gout, gin,
+                                                       X.as<uint64_t>(), Xdeg.as<int64_t>(), cap_x, bf, cnt);
+      NBG_HIP(hipGetLastError());
+      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      const int64_t nX = int64_t(hc[C_X]), E = int64_t(hc[C_XE]);
+      if (nX == 0 || E == 0) break;
+      c.timing.edges_scanned += uint64_t(E);
+      grow_keep(c, arena, n_arena + E + 64, n_arena, cap_arena);
+      grow_keep(c, sweep[1], E + 64, 0, cap_sweep[1]);
+      refresh();
+      launch_scan(nX);
+      launch_expand(nX, E, 1);
+      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      expand_time();
+      if (hc[C_OVF]) throw Error(NBG_E_UNKNOWN, "shortest path: list overflow");
+      c.timing.expand_bytes += uint64_t(nX) * 32 + uint64_t(E) * 6 + (hc[C_ARENA] - uint64_t(n_arena)) * 9;
+      n_arena = int64_t(hc[C_ARENA]);
+      n_sw = int64_t(hc[C_SWEEP]);
+      std::swap(sweep[0], sweep[1]);
+      std::swap(cap_sweep[0], cap_sweep[1]);
+    }
+    std::swap(sweep[0], meet);
+    std::swap(cap_sweep[0], cap_meet);
+
+    // results + paths
+    NBG_HIP(hipMemcpyAsync(hstate.data(), st.state, size_t(nb) * 4, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipMemcpyAsync(hres_b.data(), st.res, size_t(nb) * 4, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    std::vector<int64_t> boff(size_t(nb) + 1, 0);
+    for (int64_t p = 0; p < nb; p++) {
+      const int32_t L = hstate[size_t(p)] == SP_ACTIVE ? -1 : hres_b[size_t(p)];
+      hres[b0 + size_t(p)] = L;
+      boff[size_t(p) + 1] = boff[size_t(p)] + (L >= 0 ? L + 1 : 0);
+    }
+    const int64_t plen = boff[size_t(nb)];
+    const size_t base = hpath.size();
+    hpath.resize(base + size_t(plen));
+    if (plen > 0) {
+      DevBuf doff, dpath;
+      doff.alloc(size_t(nb + 1) * 8);
+      dpath.alloc(size_t(plen) * 8);
+      NBG_HIP(hipMemcpyAsync(doff.p, boff.data(), size_t(nb + 1) * 8, hipMemcpyHostToDevice, c.stream));
+      NBG_HIP(hipMemsetAsync(cnt + C_WALKERR, 0, 8, c.stream));
+      k_sp_walk<<<int((nb + 3) / 4), 256, 0, c.stream>>>(st, dgs, doff.as<int64_t>(), dpath.as<int64_t>(), gout, d1,
+                                                         vid_of, n, lo, cnt);
+      NBG_HIP(hipGetLastError());
+      NBG_HIP(hipMemcpyAsync(hpath.data() + base, dpath.p, size_t(plen) * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      if (hc[C_WALKERR])
+        throw Error(NBG_E_UNKNOWN, "shortest path: in-edge keys without mirrored out-edges on a shortest path");
+      for (int64_t p = 0; p < nb; p++)  // src == dst (vertex possibly unknown): the path is [src]
+        if (hres[b0 + size_t(p)] == 0) hpath[base + size_t(boff[size_t(p)])] = src[b0 + size_t(p)];
+    }
+    for (int64_t p = 0; p < nb; p++) hoff.push_back(hoff.back() + boff[size_t(p) + 1] - boff[size_t(p)]);
+    // reset the batch's distance bytes
+    if (n_arena) k_sp_clear<<<grid_n(n_arena), 256, 0, c.stream>>>(arena.as<uint64_t>(), n_arena, d0, d1, n);
+    NBG_HIP(hipGetLastError());
+  }
+  hipEventRecord(c.ev[1], c.stream);
+  NBG_HIP(hipEventSynchronize(c.ev[1]));
+  c.sp_dirty = false;
+  float ms = 0;
+  hipEventElapsedTime(&ms, c.ev[0], c.ev[1]);
+  c.timing.total_ms = ms;
+
+  auto* h = new HostRows();
+  for (int k = 0; k < 3; k++) {
+    h->types.push_back(NBG_T_VID);
+    h->host.emplace_back(npairs * 8 + 8);
+    h->str_off.push_back(nullptr);
+  }
+  for (size_t i = 0; i < npairs; i++) {
+    memcpy(h->host[0].data() + i * 8, src + i, 8);
+    memcpy(h->host[1].data() + i * 8, dst + i, 8);
+    memcpy(h->host[2].data() + i * 8, &hres[i], 8);
+  }
+  for (int k = 0; k < 3; k++) h->cols.push_back(h->host[size_t(k)].data());
+  h->path_offsets = std::move(hoff);
+  h->path_vids = std::move(hpath);
+  if (h->path_vids.empty()) h->path_vids.push_back(0);  // non-null pointer for an empty result
+  fill_rows(out, h, int64_t(npairs), false);
+  out->edges_scanned = c.timing.edges_scanned;
+  return NBG_OK;
+}
+
+}  // namespace nbg

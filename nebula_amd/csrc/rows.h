@@ -1,0 +1,42 @@
+// rows.h -- host-side owner of a result handed out through nbg_rows (freed by nbg_rows_free).
+#pragma once
+#include <cstring>
+#include <vector>
+
+#include "engine.h"
+
+namespace nbg {
+
+struct HostRows {
+  std::vector<int32_t> types;
+  std::vector<void*> cols;
+  std::vector<int64_t*> str_off;
+  std::vector<DevBuf> dev;       // device column storage when on_device
+  std::vector<std::vector<uint8_t>> host;
+  std::vector<std::vector<int64_t>> host_off;
+  std::vector<int64_t> row_vertex, vertex_ids, vertex_row_offsets;
+  std::vector<int32_t> failed_parts, failed_codes;
+  std::vector<int64_t> path_offsets, path_vids;  // nbg_shortest_path
+};
+
+inline void fill_rows(nbg_rows* out, HostRows* h, int64_t nrows, bool on_device) {
+  memset(out, 0, sizeof(*out));
+  out->n_rows = nrows;
+  out->n_cols = int32_t(h->types.size());
+  out->on_device = on_device ? 1 : 0;
+  out->col_types = h->types.data();
+  out->cols = h->cols.data();
+  out->str_offsets = h->str_off.data();
+  out->row_vertex = h->row_vertex.empty() ? nullptr : h->row_vertex.data();
+  out->n_vertices = int64_t(h->vertex_ids.size());
+  out->vertex_ids = h->vertex_ids.empty() ? nullptr : h->vertex_ids.data();
+  out->vertex_row_offsets = h->vertex_row_offsets.empty() ? nullptr : h->vertex_row_offsets.data();
+  out->n_failed = int32_t(h->failed_parts.size());
+  out->failed_parts = h->failed_parts.empty() ? nullptr : h->failed_parts.data();
+  out->failed_codes = h->failed_codes.empty() ? nullptr : h->failed_codes.data();
+  out->path_offsets = h->path_offsets.empty() ? nullptr : h->path_offsets.data();
+  out->path_vids = h->path_vids.empty() ? nullptr : h->path_vids.data();
+  out->_impl = h;
+}
+
+}  // namespace nbg

@@ -26,6 +26,7 @@
 #include "device_common.h"
 #include "engine.h"
 #include "program.h"
+#include "rows.h"
 
 namespace nbg {
 
@@ -1005,35 +1006,6 @@ __global__ void k_row_dest(YieldArgs ya, int64_t n, uint32_t G, uint32_t* dest) 
 // host drivers
 // ------------------------------------------------------------------------------------------
 namespace {
-
-struct HostRows {
-  std::vector<int32_t> types;
-  std::vector<void*> cols;
-  std::vector<int64_t*> str_off;
-  std::vector<DevBuf> dev;       // device column storage when on_device
-  std::vector<std::vector<uint8_t>> host;
-  std::vector<std::vector<int64_t>> host_off;
-  std::vector<int64_t> row_vertex, vertex_ids, vertex_row_offsets;
-  std::vector<int32_t> failed_parts, failed_codes;
-};
-
-void fill_rows(nbg_rows* out, HostRows* h, int64_t nrows, bool on_device) {
-  memset(out, 0, sizeof(*out));
-  out->n_rows = nrows;
-  out->n_cols = int32_t(h->types.size());
-  out->on_device = on_device ? 1 : 0;
-  out->col_types = h->types.data();
-  out->cols = h->cols.data();
-  out->str_offsets = h->str_off.data();
-  out->row_vertex = h->row_vertex.empty() ? nullptr : h->row_vertex.data();
-  out->n_vertices = int64_t(h->vertex_ids.size());
-  out->vertex_ids = h->vertex_ids.empty() ? nullptr : h->vertex_ids.data();
-  out->vertex_row_offsets = h->vertex_row_offsets.empty() ? nullptr : h->vertex_row_offsets.data();
-  out->n_failed = int32_t(h->failed_parts.size());
-  out->failed_parts = h->failed_parts.empty() ? nullptr : h->failed_parts.data();
-  out->failed_codes = h->failed_codes.empty() ? nullptr : h->failed_codes.data();
-  out->_impl = h;
-}
 
 EvalEnv make_env(Ctx& c, EdgeSpace& es, Csr& csr, int32_t etype) {
   EvalEnv env{};
@@ -2094,12 +2066,6 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
   fill_rows(out, h, m, false);
   out->edges_scanned = uint64_t(E);
   return NBG_OK;
-}
-
-int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t* dst, size_t n, int32_t max_steps,
-                          nbg_rows* out) {
-  (void)c; (void)et; (void)src; (void)dst; (void)n; (void)max_steps; (void)out;
-  throw Error(NBG_E_UNSUPPORTED, "FIND SHORTEST PATH lands in the next milestone");
 }
 
 void free_rows_impl(void* impl) { delete static_cast<HostRows*>(impl); }

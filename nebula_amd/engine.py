@@ -7,6 +7,9 @@
                            src/storage/QueryBoundProcessor.h:23-28 / QueryBaseProcessor.h:47.
 * ``GoExecutor``        -- GO N STEPS FROM ... OVER ... [WHERE] [YIELD [DISTINCT]], the
                            device-resident replacement of src/graph/GoExecutor.cpp:80-782.
+* ``FindPathExecutor``  -- FIND SHORTEST PATH FROM ... TO ... OVER ... UPTO N STEPS (the
+                           reference's FindExecutor is a stub, src/graph/FindExecutor.cpp:20-22;
+                           semantics in include/nebula_amd.h), batched bidirectional BFS.
 
 Everything executes in libnebula_amd.so on the GPU; there is no Python or CPU compute path.
 """
@@ -219,6 +222,42 @@ class GraphSpace:
             self.L.nbg_rows_free(C.byref(rows))
 
 
+    def shortest_path(self, src, dst, edge_type: int, max_steps: int = 5) -> "PathResult":
+        """Pairwise shortest paths (src[i] -> dst[i]) over edge_type out-edges."""
+        src = np.ascontiguousarray(src, dtype=np.int64)
+        dst = np.ascontiguousarray(dst, dtype=np.int64)
+        if src.shape != dst.shape:
+            raise ValueError("src and dst must have the same length")
+        rows = _lib.Rows()
+        self._check(self.L.nbg_shortest_path(self.h, edge_type, _p(src), _p(dst), len(src), max_steps,
+                                             C.byref(rows)))
+        try:
+            n = int(rows.n_rows)
+            hops = (np.ctypeslib.as_array(C.cast(rows.cols[2], C.POINTER(C.c_int64)), shape=(n,)).copy()
+                    if n else np.zeros(0, np.int64))
+            off = np.ctypeslib.as_array(rows.path_offsets, shape=(n + 1,)).copy() if n else np.zeros(1, np.int64)
+            tot = int(off[-1])
+            vids = (np.ctypeslib.as_array(rows.path_vids, shape=(tot,)).copy() if tot else np.zeros(0, np.int64))
+            paths = [vids[off[i]:off[i + 1]] for i in range(n)]
+            return PathResult(src.copy(), dst.copy(), hops, paths, int(rows.edges_scanned))
+        finally:
+            self.L.nbg_rows_free(C.byref(rows))
+
+
+@dataclass
+class PathResult:
+    """FIND SHORTEST PATH result: per pair the hop count (-1 = unreachable) and the path."""
+    src: np.ndarray
+    dst: np.ndarray
+    hops: np.ndarray
+    paths: list
+    edges_scanned: int = 0
+
+    def rows(self):
+        return [(int(s), int(d), int(h), tuple(int(v) for v in p))
+                for s, d, h, p in zip(self.src, self.dst, self.hops, self.paths)]
+
+
 # ---- reference-shaped operator wrappers ---------------------------------------------------
 @dataclass
 class PropDef:
@@ -289,3 +328,17 @@ class GoExecutor:
     def execute(self, keep_on_device: bool = False) -> RowSet:
         return self.space.go(self.starts, self.steps, self.edge_type, self.where, self.yields, self.distinct,
                              keep_on_device)
+
+
+class FindPathExecutor:
+    """FIND SHORTEST PATH FROM froms TO tos OVER edge UPTO n STEPS: every (from, to) combination,
+    in from-major order (the reference only declares the executor, FindExecutor.cpp:20-22)."""
+
+    def __init__(self, space: GraphSpace, froms, tos, edge_type: int, upto: int = 5):
+        self.space, self.froms, self.tos = space, list(froms), list(tos)
+        self.edge_type, self.upto = edge_type, upto
+
+    def execute(self) -> PathResult:
+        src = np.repeat(np.asarray(self.froms, dtype=np.int64), len(self.tos))
+        dst = np.tile(np.asarray(self.tos, dtype=np.int64), len(self.froms))
+        return self.space.shortest_path(src, dst, self.edge_type, self.upto)

@@ -1,0 +1,143 @@
+"""GPU parity of FIND SHORTEST PATH against the oracle.
+
+The reference has no implementation (src/graph/FindExecutor.cpp:20-22), so the oracle
+(oracle/refcpu.cpp ora_shortest_path: backward BFS from dst over the in-edge keys + greedy
+smallest-vid walk from src) is the definition; no reference fixture pins it ("parity unpinned"
+in DESIGN.md).  Hop counts and whole paths must match bit-exactly.
+"""
+import numpy as np
+import pytest
+
+import fixtures as F
+import oracle as O
+from nebula_amd import FindPathExecutor, GraphSpace, NbgError, synth
+
+pytestmark = pytest.mark.gpu
+
+FOLLOW = 1
+
+
+def oracle_paths(st, src, dst, et, max_steps):
+    r = st.shortest_path(np.asarray(src, np.int64), np.asarray(dst, np.int64), et, max_steps)
+    out = []
+    for row in r.rows():
+        row = [x for x in row if x is not None]
+        out.append((row[0], row[1], row[2], tuple(row[3:])))
+    return out
+
+
+@pytest.fixture(scope="module", params=[10, 13])
+def rmat(request):
+    scale = request.param
+    sp = GraphSpace(64)
+    sp.set_edge_schema(FOLLOW, [("weight", 2)])
+    sp.gen_rmat(scale, 16, 1, FOLLOW)
+    sp.finalize()
+    st = O.Store(64)
+    st.set_edge_schema(FOLLOW, [("weight", O.INT)], name="follow")
+    st.load_rmat(scale, 16, 1, FOLLOW)
+    yield scale, sp, st
+    sp.close()
+
+
+def edge_case_pairs(scale):
+    s, t = synth.pairs(scale, 16, 1, 8, pick_seed=3)
+    nb_s, nb_t = synth.edges(scale, 1, np.arange(4, dtype=np.uint64))  # direct edges: 1 hop
+    src = list(s) + list(nb_s) + [s[0], -5, s[1], -7, t[2]]
+    dst = list(t) + list(nb_t) + [s[0], t[0], -9, -7, t[2]]
+    return np.array(src, np.int64), np.array(dst, np.int64)
+
+
+@pytest.mark.parametrize("max_steps", [1, 2, 3, 6])
+def test_rmat_pairs_vs_oracle(rmat, max_steps):
+    scale, sp, st = rmat
+    s, t = synth.pairs(scale, 16, 1, 200)
+    es, et_ = edge_case_pairs(scale)
+    src = np.concatenate([s, es])
+    dst = np.concatenate([t, et_])
+    got = sp.shortest_path(src, dst, FOLLOW, max_steps).rows()
+    want = oracle_paths(st, src, dst, FOLLOW, max_steps)
+    assert got == want
+    if max_steps >= 6:
+        assert sum(1 for r in got if r[2] >= 3) >= 5  # the set exercises multi-level meets
+
+
+def test_rmat_batches_equal_single_launch(rmat):
+    scale, sp, st = rmat
+    s, t = synth.pairs(scale, 16, 1, 150, pick_seed=5)
+    one = sp.shortest_path(s, t, FOLLOW, 8).rows()
+    sp.set_option("sp_batch", 7)  # 22 batches of 7 pairs; distance bytes reset between batches
+    try:
+        many = sp.shortest_path(s, t, FOLLOW, 8).rows()
+    finally:
+        sp.set_option("sp_batch", 1024)
+    assert one == many
+    assert one == oracle_paths(st, s, t, FOLLOW, 8)
+
+
+def test_repeated_calls_are_clean(rmat):
+    # the distance arrays persist across calls: a second identical call must not see stale bytes
+    scale, sp, st = rmat
+    s, t = synth.pairs(scale, 16, 1, 64, pick_seed=9)
+    a = sp.shortest_path(s, t, FOLLOW, 5).rows()
+    b = sp.shortest_path(s, t, FOLLOW, 5).rows()
+    c = sp.shortest_path(t, s, FOLLOW, 5).rows()
+    assert a == b
+    assert c == oracle_paths(st, t, s, FOLLOW, 5)
+
+
+def test_duplicate_pairs_and_empty(rmat):
+    scale, sp, st = rmat
+    s, t = synth.pairs(scale, 16, 1, 4, pick_seed=13)
+    src = np.concatenate([s, s, s])
+    dst = np.concatenate([t, t, t])
+    got = sp.shortest_path(src, dst, FOLLOW, 6).rows()
+    assert got == oracle_paths(st, src, dst, FOLLOW, 6)
+    empty = sp.shortest_path(np.zeros(0, np.int64), np.zeros(0, np.int64), FOLLOW, 4)
+    assert empty.rows() == []
+
+
+def test_paths_are_edges_and_shortest(rmat):
+    # size-independent properties: every path step is an out-edge, length = hops
+    scale, sp, st = rmat
+    s, t = synth.pairs(scale, 16, 1, 64, pick_seed=21)
+    res = sp.shortest_path(s, t, FOLLOW, 8)
+    for (a, b, h, path) in res.rows():
+        if h < 0:
+            assert path == ()
+            continue
+        assert len(path) == h + 1 and path[0] == a and path[-1] == b
+        for u, v in zip(path, path[1:]):
+            nbrs = sp.go([u], 1, FOLLOW).columns[0]
+            assert v in set(int(x) for x in nbrs)
+
+
+def test_bad_arguments(rmat):
+    scale, sp, st = rmat
+    with pytest.raises(NbgError):
+        sp.shortest_path([1], [2], FOLLOW, 300)
+    with pytest.raises(NbgError):
+        sp.shortest_path([1], [2], 99, 3)
+    with pytest.raises(NbgError):
+        sp.shortest_path([1], [2], -FOLLOW, 3)
+
+
+def test_nba_like_paths():
+    sp = GraphSpace(1)
+    for et, (name, fields) in F.NBA_EDGE_SCHEMAS.items():
+        sp.set_edge_schema(et, fields)
+    parts, vid = F.nba_kv()
+    for p, kv in parts.items():
+        sp.load_part(p, kv)
+    sp.finalize()
+    st, _ = F.nba_oracle_store()
+    names = sorted(vid)
+    froms = [vid[n] for n in names[:12]]
+    tos = [vid[n] for n in names[-12:]] + [vid["Tim Duncan"], vid["Tony Parker"]]
+    got = FindPathExecutor(sp, froms, tos, F.NBA_LIKE, upto=5).execute().rows()
+    src = np.repeat(np.array(froms, np.int64), len(tos))
+    dst = np.tile(np.array(tos, np.int64), len(froms))
+    want = oracle_paths(st, src, dst, F.NBA_LIKE, 5)
+    assert got == want
+    assert any(r[2] >= 2 for r in got)
+    sp.close()
