@@ -61,6 +61,86 @@ def cpu_baseline(scale: int, seeds: int, where_k: int):
     }
 
 
+def cpu_baseline_paths(scale: int, npairs: int, max_steps: int):
+    """The oracle's FIND SHORTEST PATH (backward BFS + greedy walk, one thread) on a sample."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle as O
+    from nebula_amd import synth
+
+    st = O.Store(64)
+    st.set_edge_schema(1, [("weight", O.INT)], name="follow")
+    st.load_rmat(scale, 16, 1, 1, versions=1, threads=min(8, os.cpu_count() or 1))
+    s, t = synth.pairs(scale, 16, 1, npairs)
+    t0 = time.time()
+    st.shortest_path(s, t, 1, max_steps)
+    dt = time.time() - t0
+    return {"value": npairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
+            "sample": f"oracle FIND SHORTEST PATH {npairs} pairs on RMAT-{scale} (ef16) UPTO {max_steps} STEPS "
+                      f"in {dt:.2f}s"}
+
+
+def bench_paths(args, sp, info, build_s, rank, world):
+    """BASELINE.json configs[3]: FIND SHORTEST PATH, 1024 (src, dst) pairs on RMAT-26."""
+    from nebula_amd import synth
+    s, t = synth.pairs(args.scale, args.edge_factor, 1, args.pairs)
+    for _ in range(args.warmup):
+        sp.shortest_path(s, t, 1, args.max_steps)
+    t0 = time.perf_counter()
+    edges = 0
+    exp_ms = exp_bytes = dev_ms = 0.0
+    iters = 0
+    for _ in range(args.steps):
+        r = sp.shortest_path(s, t, 1, args.max_steps)
+        tm = sp.last_timing()
+        edges += r.edges_scanned
+        exp_ms += tm["expand_ms"]
+        exp_bytes += tm["expand_bytes"]
+        dev_ms += tm["total_ms"]
+        iters = tm["steps_run"]
+    dt = time.perf_counter() - t0
+    hops = r.hops
+    achieved = exp_bytes / (exp_ms / 1e3) / 1e9 if exp_ms > 0 else 0.0
+    out = {
+        "metric": "FIND SHORTEST PATH pairs/s (batched bidirectional BFS) on RMAT-26",
+        "value": args.pairs * args.steps / dt,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic RMAT (Graph500 a/b/c=0.57/0.19/0.19, seed 1) generated on device",
+        "config": {
+            "workload": f"FIND SHORTEST PATH {args.pairs} pairs UPTO {args.max_steps} STEPS OVER follow; "
+                        f"RMAT-{args.scale} ef{args.edge_factor}",
+            "vertices": info["num_vertices"],
+            "edges_examined_per_query": edges // max(args.steps, 1),
+            "gteps": edges / dt / 1e9,
+            "reachable": int((hops >= 0).sum()),
+            "hops_histogram": {int(h): int((hops == h).sum()) for h in sorted(set(hops.tolist()))},
+            "bfs_iterations": iters,
+            "snapshot_build_s": round(build_s, 2),
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": "k_sp_expand", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "expand_ms_per_query": exp_ms / max(args.steps, 1), "device_ms_per_query": dev_ms / max(args.steps, 1),
+        },
+        "cpu_baseline": None,
+    }
+    if not args.no_cpu:
+        try:
+            out["cpu_baseline"] = cpu_baseline_paths(args.cpu_scale, 64, args.max_steps)
+        except Exception as e:
+            out["cpu_baseline"] = {"error": str(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    sp.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -74,6 +154,10 @@ def main():
     ap.add_argument("--cpu-scale", type=int, default=18)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--option", action="append", default=[], help="engine option key=value")
+    ap.add_argument("--workload", choices=["go", "paths"], default="go",
+                    help="go: BASELINE metric (GO 3 STEPS); paths: configs[3] FIND SHORTEST PATH")
+    ap.add_argument("--pairs", type=int, default=1024)
+    ap.add_argument("--max-steps", type=int, default=8)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -104,6 +188,8 @@ def main():
     sp.finalize()
     build_s = time.time() - t0
     info = sp.info(FOLLOW)
+    if args.workload == "paths":
+        return bench_paths(args, sp, info, build_s, rank, world)
     starts = synth.seeds(args.scale, args.edge_factor, 1, args.seeds)
     where = X.AliasProp("follow", "weight") > args.where
     yields = [X.EdgeDst("follow")]

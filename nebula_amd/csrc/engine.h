@@ -257,10 +257,16 @@ struct Ctx {
   DevBuf ws_bits_xchg;  // world > 1: received mark segments [world][owned/32]
   DevBuf ws_starts;
   DevBuf ws_partials;  // per-block partial sums of the aggregated kernels
-  // FIND SHORTEST PATH distance bytes [side][pair][owned row], kept 0xFF between calls
+  // FIND SHORTEST PATH distance bytes [side][pair][owned row], kept 0xFF between calls, and
+  // its tuple lists (kept across calls; allocated outside the query pool)
   DevBuf sp_dist[2];
   size_t sp_dist_bytes = 0;
   bool sp_dirty = false;
+  struct SpWork {
+    DevBuf live[2], live_next[2], arena, meet, sweep[2], X, Xdeg, Xoff, state, cnt, vids, gidx, plist;
+    int64_t cap_live[2] = {0, 0}, cap_next[2] = {0, 0}, cap_arena = 0, cap_meet = 0, cap_sweep[2] = {0, 0};
+    int64_t cap_x = 0, cap_state = 0, cap_plist = 0;
+  } sp;
   Timing timing;
   hipEvent_t ev[8] = {};
   std::shared_ptr<BufPool> pool = std::make_shared<BufPool>();

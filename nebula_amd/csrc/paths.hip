@@ -74,7 +74,8 @@ struct SpState {  // per-pair arrays, B entries each
   int32_t* res;             // hops (-1 unreachable)
   int32_t* lvl;             // [2][B] depth of each side
   int32_t* side;            // side expanded this iteration
-  int32_t* met;
+  int32_t* pside;           // side expanded by the iteration that just ended
+  int32_t* met;             // 1: a meet this iteration; 2 + i: met in iteration i
   unsigned long long* deg;  // [2][B] frontier sum of (degree + 1)
   int32_t B;
 };
@@ -163,19 +164,21 @@ __global__ void k_sp_init(const int64_t* svid, const int64_t* tvid, const int32_
   put(bf.arena, bf.cap_arena, cnt, C_ARENA, go, tb);
 }
 
-// end of an iteration (first = 0) and the side choice of the next one
-__global__ void k_sp_step(SpState st, int32_t max_steps, int32_t first, unsigned long long* cnt) {
+// end of iteration `iter` (first = 0) and the side choice of the next one
+__global__ void k_sp_step(SpState st, int32_t max_steps, int32_t first, int32_t iter, unsigned long long* cnt) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   bool active = false;
   if (p < st.B && st.state[p] == SP_ACTIVE) {
     const int B = st.B;
     if (!first) {
       const int s = st.side[p];
+      st.pside[p] = s;
       st.lvl[s * B + p] += 1;
       const int32_t L = st.lvl[p] + st.lvl[B + p];
       if (st.met[p]) {
         st.res[p] = L;
         st.state[p] = SP_MET;
+        st.met[p] = 2 + iter;
       } else if (st.deg[s * B + p] == 0 || L >= max_steps) {
         st.state[p] = SP_DONE;  // a side's reachable set is closed, or the step bound is hit
       }
@@ -189,6 +192,43 @@ __global__ void k_sp_step(SpState st, int32_t max_steps, int32_t first, unsigned
   }
   const int64_t slot = wave_append(cnt + C_ACTIVE, active);
   (void)slot;
+}
+
+// Rebuild a list whose appends overflowed from the distance bytes (claims are recorded in the
+// bytes even when their tuple could not be stored).  One y-slice of the grid per listed pair.
+//  RG_LIVE:  side s tuples at the side's new depth (pairs that expanded s)
+//  RG_MEET:  vertices seen at depth f forward and b backward (pairs that met this iteration)
+//  RG_SWEEP: sweep claims of step j (dist_B = b + j)
+enum : int { RG_LIVE = 0, RG_MEET = 1, RG_SWEEP = 2 };
+__global__ void k_sp_regen(int mode, int side, int32_t j, const int32_t* plist, int32_t np, SpState st,
+                           const uint8_t* d0, const uint8_t* d1, int64_t n, uint64_t* out, int64_t cap,
+                           unsigned long long* cnt, int which) {
+  const int32_t B = st.B;
+  for (int32_t q = blockIdx.y; q < np; q += gridDim.y) {
+    const uint32_t p = uint32_t(plist[q]);
+    uint32_t tv, tf = 0;
+    if (mode == RG_LIVE) {
+      tv = uint32_t(st.lvl[side * B + p]);
+    } else if (mode == RG_MEET) {
+      tv = uint32_t(st.lvl[B + p]);
+      tf = uint32_t(st.lvl[p]);
+    } else {
+      tv = uint32_t(st.lvl[B + p] + j);
+    }
+    const uint8_t* rowd = ((mode == RG_LIVE && side == 0) ? d0 : d1) + uint64_t(p) * uint64_t(n);
+    const uint8_t* rowf = d0 + uint64_t(p) * uint64_t(n);
+    const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+    const int64_t rounds = (n + stride - 1) / stride;
+    for (int64_t r = 0; r < rounds; r++) {
+      const int64_t v = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+      bool hit = false;
+      if (v < n) {
+        hit = rowd[v] == tv;
+        if (mode == RG_MEET) hit = hit && rowf[v] == tf;
+      }
+      put(out, cap, cnt, which, hit, mk_tup(mode == RG_LIVE ? uint32_t(side) : 1u, p, tv, uint32_t(v)));
+    }
+  }
 }
 
 // split a live list: tuples of the side their pair expands now -> X (with degrees), the rest
@@ -402,13 +442,18 @@ int grid_n(int64_t n, int cap = 4096) {
   return int(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap)));
 }
 
-// grow a list keeping its first `used` elements (stream-ordered copy)
-void grow_keep(Ctx& c, DevBuf& b, int64_t need, int64_t used, int64_t& cap) {
+// (re)size a persistent list to hold `need` tuples, keeping its first `keep` ones.  Lists
+// persist across calls, so growth (a synchronising hipFree) is rare.
+void reserve(Ctx& c, DevBuf& b, int64_t& cap, int64_t need, int64_t keep) {
   if (need <= cap) return;
-  const int64_t nc = std::max<int64_t>(need + need / 2, 1 << 16);
+  const int64_t nc = std::max<int64_t>(need + need / 4, 1 << 16);
+  PoolScope none(nullptr);
   DevBuf nb;
   nb.alloc(size_t(nc) * 8);
-  if (used > 0) NBG_HIP(hipMemcpyAsync(nb.p, b.p, size_t(used) * 8, hipMemcpyDeviceToDevice, c.stream));
+  if (keep > 0) {
+    NBG_HIP(hipMemcpyAsync(nb.p, b.p, size_t(keep) * 8, hipMemcpyDeviceToDevice, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+  }
   b = std::move(nb);
   cap = nc;
 }
@@ -433,15 +478,28 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t*
   B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(int64_t(npairs), 1)));
   B = std::min<int64_t>(B, 0x7FFFFF);
   const size_t dist_bytes = ((size_t(B) * size_t(n) + 3) & ~size_t(3)) + 64;
-  if (c.sp_dist_bytes < dist_bytes || c.sp_dirty) {
-    for (auto& d : c.sp_dist) d.release();
+  {
     PoolScope none(nullptr);  // the distance arrays live outside the query pool
-    for (auto& d : c.sp_dist) {
-      d.alloc(dist_bytes);
-      NBG_HIP(hipMemsetAsync(d.p, 0xFF, dist_bytes, c.stream));
+    if (c.sp_dist_bytes < dist_bytes) {
+      for (auto& d : c.sp_dist) d.release();
+      c.sp_dist_bytes = 0;
+      for (auto& d : c.sp_dist) d.alloc(dist_bytes);
+      c.sp_dist_bytes = dist_bytes;
+      c.sp_dirty = true;
     }
-    c.sp_dist_bytes = dist_bytes;
+    if (c.sp_dirty)
+      for (auto& d : c.sp_dist) NBG_HIP(hipMemsetAsync(d.p, 0xFF, c.sp_dist_bytes, c.stream));
     c.sp_dirty = false;
+  }
+  Ctx::SpWork& W = c.sp;
+  if (W.cap_state < B) {
+    PoolScope none(nullptr);
+    W.state.alloc(size_t(B) * 48 + 64);
+    W.cnt.alloc(C_N * 8);
+    W.vids.alloc(size_t(B) * 16);
+    W.gidx.alloc(size_t(B) * 8);
+    W.plist.alloc(size_t(B) * 4 + 64);
+    W.cap_state = B;
   }
   PoolScope pool_scope(c.pool);
   c.timing = Timing{};
@@ -452,92 +510,82 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t*
   SpCsr gout{es.out.row_ptr.as<int64_t>(), es.out.col.as<int32_t>(), es.out.row_ok.as<uint8_t>()};
   SpCsr gin{es.in.row_ptr.as<int64_t>(), es.in.col.as<int32_t>(), es.in.row_ok.as<uint8_t>()};
   const int64_t* vid_of = c.vid_of.as<int64_t>();
-
-  DevBuf dstate, dcnt, dvids, dg;
-  dstate.alloc(size_t(B) * 4 * 7 + size_t(B) * 16 + 64);
-  SpState st{};
-  st.B = int32_t(B);
-  st.deg = dstate.as<unsigned long long>();
-  st.state = reinterpret_cast<int32_t*>(st.deg + 2 * B);
-  st.res = st.state + B;
-  st.lvl = st.res + B;
-  st.side = st.lvl + 2 * B;
-  st.met = st.side + B;
-  dcnt.alloc(C_N * 8);
-  unsigned long long* cnt = dcnt.as<unsigned long long>();
+  unsigned long long* cnt = W.cnt.as<unsigned long long>();
   unsigned long long* hc = c.host_counters;  // pinned
-  dvids.alloc(size_t(B) * 16);
-  dg.alloc(size_t(B) * 8);
-  int64_t* dsv = dvids.as<int64_t>();
+  int64_t* dsv = W.vids.as<int64_t>();
   int64_t* dtv = dsv + B;
-  int32_t* dgs = dg.as<int32_t>();
+  int32_t* dgs = W.gidx.as<int32_t>();
   int32_t* dgt = dgs + B;
-
-  DevBuf live[2], live_next[2], arena, meet, sweep[2], X, Xdeg, Xoff;
-  int64_t cap_live[2] = {0, 0}, cap_next[2] = {0, 0}, cap_arena = 0, cap_meet = 0, cap_sweep[2] = {0, 0};
-  int64_t cap_x = 0;
+  const int64_t soft = std::max<int64_t>(c.opt("sp_list_soft", int64_t(16) << 20), 1024);
 
   std::vector<int64_t> hres(npairs), hoff(1, 0), hpath;
-  std::vector<int32_t> hstate(static_cast<size_t>(B)), hres_b(static_cast<size_t>(B));
+  std::vector<int32_t> hstate(static_cast<size_t>(B)), hres_b(static_cast<size_t>(B)),
+      hside(static_cast<size_t>(B)), hmet(static_cast<size_t>(B));
   c.sp_dirty = true;  // until the batch's bytes are reset
   for (size_t b0 = 0; b0 < npairs; b0 += size_t(B)) {
     const int64_t nb = std::min<int64_t>(B, int64_t(npairs - b0));
+    SpState st{};
     st.B = int32_t(nb);
-    NBG_HIP(hipMemcpyAsync(dsv, src + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
-    NBG_HIP(hipMemcpyAsync(dtv, dst + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
-    lookup_gidx(c, dsv, dgs, nb);
-    lookup_gidx(c, dtv, dgt, nb);
-    // per-pair state arrays are indexed with stride nb ([2][nb] blocks)
+    st.deg = W.state.as<unsigned long long>();
     st.state = reinterpret_cast<int32_t*>(st.deg + 2 * nb);
     st.res = st.state + nb;
     st.lvl = st.res + nb;
     st.side = st.lvl + 2 * nb;
-    st.met = st.side + nb;
+    st.pside = st.side + nb;
+    st.met = st.pside + nb;
+    NBG_HIP(hipMemcpyAsync(dsv, src + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
+    NBG_HIP(hipMemcpyAsync(dtv, dst + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
+    lookup_gidx(c, dsv, dgs, nb);
+    lookup_gidx(c, dtv, dgt, nb);
     NBG_HIP(hipMemsetAsync(cnt, 0, C_N * 8, c.stream));
-    for (int s = 0; s < 2; s++) grow_keep(c, live_next[s], nb + 64, 0, cap_next[s]);
-    grow_keep(c, arena, 2 * nb + 64, 0, cap_arena);
-    grow_keep(c, meet, 1 << 16, 0, cap_meet);
+    for (int s = 0; s < 2; s++) reserve(c, W.live_next[s], W.cap_next[s], nb + 64, 0);
+    reserve(c, W.arena, W.cap_arena, 2 * nb + 64, 0);
+    reserve(c, W.meet, W.cap_meet, 4096, 0);
     SpBufs bf{};
-    auto refresh = [&]() {
-      bf.live_next[0] = live_next[0].as<uint64_t>();
-      bf.live_next[1] = live_next[1].as<uint64_t>();
-      bf.arena = arena.as<uint64_t>();
-      bf.meet = meet.as<uint64_t>();
-      bf.cap_live[0] = cap_next[0];
-      bf.cap_live[1] = cap_next[1];
-      bf.cap_arena = cap_arena;
-      bf.cap_meet = cap_meet;
-      bf.sweep_next = sweep[1].as<uint64_t>();
-      bf.cap_sweep = cap_sweep[1];
+    auto refresh = [&](DevBuf* sweep_next, int64_t cap_sweep_next) {
+      bf.live_next[0] = W.live_next[0].as<uint64_t>();
+      bf.live_next[1] = W.live_next[1].as<uint64_t>();
+      bf.arena = W.arena.as<uint64_t>();
+      bf.meet = W.meet.as<uint64_t>();
+      bf.cap_live[0] = W.cap_next[0];
+      bf.cap_live[1] = W.cap_next[1];
+      bf.cap_arena = W.cap_arena;
+      bf.cap_meet = W.cap_meet;
+      bf.sweep_next = sweep_next ? sweep_next->as<uint64_t>() : nullptr;
+      bf.cap_sweep = sweep_next ? cap_sweep_next : 0;
     };
-    refresh();
-    k_sp_init<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(dsv, dtv, dgs, dgt, int32_t(nb), max_steps, n, st, gout, gin,
-                                                         d0, d1, bf, cnt);
-    k_sp_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, max_steps, 1, cnt);
-    NBG_HIP(hipGetLastError());
-    NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
-    NBG_HIP(hipStreamSynchronize(c.stream));
-    int64_t n_live[2] = {int64_t(hc[C_LIVE0]), int64_t(hc[C_LIVE1])};
-    int64_t n_arena = int64_t(hc[C_ARENA]), n_meet = 0;
-    int64_t active = int64_t(hc[C_ACTIVE]);
-    for (int s = 0; s < 2; s++) {
-      std::swap(live[s], live_next[s]);
-      std::swap(cap_live[s], cap_next[s]);
-    }
+    auto sync_counters = [&]() {
+      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+    };
+    auto set_counter = [&](int which, int64_t v) {
+      hc[32] = (unsigned long long)v;
+      NBG_HIP(hipMemcpyAsync(cnt + which, hc + 32, 8, hipMemcpyHostToDevice, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+    };
+    auto ensure_x = [&](int64_t need) {
+      if (need + 1 > W.cap_x) {
+        PoolScope none(nullptr);
+        W.cap_x = std::max<int64_t>(need + need / 4 + 64, 1 << 16);
+        W.X.alloc(size_t(W.cap_x) * 8);
+        W.Xdeg.alloc(size_t(W.cap_x + 1) * 8);
+        W.Xoff.alloc(size_t(W.cap_x + 1) * 8);
+      }
+    };
     auto launch_scan = [&](int64_t nX) {
       size_t tb = 0;
-      NBG_HIP(hipMemsetAsync(Xdeg.as<int64_t>() + nX, 0, 8, c.stream));
-      NBG_HIP(rocprim::exclusive_scan(nullptr, tb, Xdeg.as<int64_t>(), Xoff.as<int64_t>(), int64_t(0), size_t(nX + 1),
-                                      rocprim::plus<int64_t>(), c.stream));
+      NBG_HIP(hipMemsetAsync(W.Xdeg.as<int64_t>() + nX, 0, 8, c.stream));
+      NBG_HIP(rocprim::exclusive_scan(nullptr, tb, W.Xdeg.as<int64_t>(), W.Xoff.as<int64_t>(), int64_t(0),
+                                      size_t(nX + 1), rocprim::plus<int64_t>(), c.stream));
       c.ws_tmp.ensure(tb);
-      NBG_HIP(rocprim::exclusive_scan(c.ws_tmp.p, tb, Xdeg.as<int64_t>(), Xoff.as<int64_t>(), int64_t(0),
+      NBG_HIP(rocprim::exclusive_scan(c.ws_tmp.p, tb, W.Xdeg.as<int64_t>(), W.Xoff.as<int64_t>(), int64_t(0),
                                       size_t(nX + 1), rocprim::plus<int64_t>(), c.stream));
     };
     auto launch_expand = [&](int64_t nX, int64_t E, int32_t sweep_mode) {
       SpExpand a{};
-      a.X = X.as<uint64_t>();
+      a.X = W.X.as<uint64_t>();
       a.nX = nX;
-      a.off = Xoff.as<int64_t>();
+      a.off = W.Xoff.as<int64_t>();
       a.g[0] = gout;
       a.g[1] = gin;
       a.dist[0] = d0;
@@ -559,97 +607,146 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t*
       c.timing.expand_ms += ms;
       c.timing.expand_launches++;
     };
-    auto ensure_x = [&](int64_t need) {
-      if (need + 1 > cap_x) {
-        cap_x = std::max<int64_t>(need + need / 2 + 64, 1 << 16);
-        X.alloc(size_t(cap_x) * 8);
-        Xdeg.alloc(size_t(cap_x + 1) * 8);
-        Xoff.alloc(size_t(cap_x + 1) * 8);
-      }
+    // pairs (of this batch) matching a host predicate over (state, pside, met) -> W.plist
+    auto pair_list = [&](auto pred) -> int32_t {
+      NBG_HIP(hipMemcpyAsync(hstate.data(), st.state, size_t(nb) * 4, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipMemcpyAsync(hside.data(), st.pside, size_t(nb) * 4, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipMemcpyAsync(hmet.data(), st.met, size_t(nb) * 4, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      std::vector<int32_t> pl;
+      for (int32_t p = 0; p < int32_t(nb); p++)
+        if (pred(hstate[size_t(p)], hside[size_t(p)], hmet[size_t(p)])) pl.push_back(p);
+      if (!pl.empty())
+        NBG_HIP(hipMemcpy(W.plist.p, pl.data(), pl.size() * 4, hipMemcpyHostToDevice));
+      return int32_t(pl.size());
+    };
+    auto regen = [&](int mode, int side, int32_t j, int32_t np, uint64_t* outl, int64_t cap, int which) {
+      if (np == 0) return;
+      dim3 grid(unsigned(std::min<int64_t>((n + 255) / 256, 1024)), unsigned(std::min<int32_t>(np, 65535)));
+      k_sp_regen<<<grid, 256, 0, c.stream>>>(mode, side, j, W.plist.as<int32_t>(), np, st, d0, d1, n, outl, cap, cnt,
+                                             which);
+      NBG_HIP(hipGetLastError());
     };
 
+    k_sp_init<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(dsv, dtv, dgs, dgt, int32_t(nb), max_steps, n, st, gout, gin,
+                                                         d0, d1, (refresh(nullptr, 0), bf), cnt);
+    k_sp_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, max_steps, 1, 0, cnt);
+    NBG_HIP(hipGetLastError());
+    sync_counters();
+    int64_t n_live[2] = {int64_t(hc[C_LIVE0]), int64_t(hc[C_LIVE1])};
+    int64_t n_arena = int64_t(hc[C_ARENA]), n_meet = 0;
+    int64_t active = int64_t(hc[C_ACTIVE]);
+    int64_t last_claims = 0;
+    bool arena_lost = false;
+    for (int s = 0; s < 2; s++) {
+      std::swap(W.live[s], W.live_next[s]);
+      std::swap(W.cap_live[s], W.cap_next[s]);
+    }
+    int32_t iter = 0;
     while (active > 0) {
+      iter++;
       c.timing.steps_run++;
       // live lists -> X (expanding side) + carried tuples
       ensure_x(n_live[0] + n_live[1]);
-      for (int s = 0; s < 2; s++) grow_keep(c, live_next[s], n_live[s] + 64, 0, cap_next[s]);
-      refresh();
+      for (int s = 0; s < 2; s++) reserve(c, W.live_next[s], W.cap_next[s], n_live[s] + 64, 0);
+      refresh(nullptr, 0);
       NBG_HIP(hipMemsetAsync(cnt + C_LIVE0, 0, 16, c.stream));
-      NBG_HIP(hipMemsetAsync(cnt + C_X, 0, 16, c.stream));  // C_X, C_ACTIVE
+      NBG_HIP(hipMemsetAsync(cnt + C_X, 0, 24, c.stream));  // C_X, C_ACTIVE, C_OVF
       NBG_HIP(hipMemsetAsync(cnt + C_XE, 0, 8, c.stream));
       for (int s = 0; s < 2; s++)
         if (n_live[s])
-          k_sp_select<<<grid_n(n_live[s]), 256, 0, c.stream>>>(live[s].as<uint64_t>(), n_live[s], 0, st, gout, gin,
-                                                                 X.as<uint64_t>(), Xdeg.as<int64_t>(), cap_x, bf, cnt);
+          k_sp_select<<<grid_n(n_live[s]), 256, 0, c.stream>>>(W.live[s].as<uint64_t>(), n_live[s], 0, st, gout, gin,
+                                                                 W.X.as<uint64_t>(), W.Xdeg.as<int64_t>(), W.cap_x, bf,
+                                                                 cnt);
       NBG_HIP(hipGetLastError());
-      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
-      if (hc[C_OVF]) throw Error(NBG_E_UNKNOWN, "shortest path: list overflow");
+      sync_counters();
+      if (hc[C_OVF] & 2) throw Error(NBG_E_UNKNOWN, "shortest path: frontier list overflow");
       const int64_t nX = int64_t(hc[C_X]), E = int64_t(hc[C_XE]);
       const int64_t carried[2] = {int64_t(hc[C_LIVE0]), int64_t(hc[C_LIVE1])};
       c.timing.edges_scanned += uint64_t(E);
       if (E > 0) {
-        // every edge may claim once: size the lists for the worst case
-        for (int s = 0; s < 2; s++) grow_keep(c, live_next[s], carried[s] + E + 64, carried[s], cap_next[s]);
-        grow_keep(c, arena, n_arena + E + 64, n_arena, cap_arena);
-        grow_keep(c, meet, n_meet + E + 64, n_meet, cap_meet);
-        refresh();
+        // lists sized for min(every edge claims, a soft bound); an overflow is rebuilt below
+        const int64_t want = std::min<int64_t>(E, std::max<int64_t>(soft, 2 * last_claims)) + 64;
+        for (int s = 0; s < 2; s++) reserve(c, W.live_next[s], W.cap_next[s], carried[s] + want, carried[s]);
+        if (!arena_lost) reserve(c, W.arena, W.cap_arena, n_arena + want, n_arena);
+        reserve(c, W.meet, W.cap_meet, n_meet + std::min<int64_t>(E, soft) + 64, n_meet);
+        refresh(nullptr, 0);
         launch_scan(nX);
         launch_expand(nX, E, 0);
       }
-      k_sp_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, max_steps, 0, cnt);
+      k_sp_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, max_steps, 0, iter, cnt);
       NBG_HIP(hipGetLastError());
-      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
+      sync_counters();
       if (E > 0) expand_time();
-      if (hc[C_OVF]) throw Error(NBG_E_UNKNOWN, "shortest path: list overflow");
-      c.timing.expand_bytes += uint64_t(nX) * 32 + uint64_t(E) * 5 + (hc[C_ARENA] - uint64_t(n_arena)) * 26;
+      const int64_t cl = int64_t(hc[C_LIVE0] + hc[C_LIVE1]) - carried[0] - carried[1];
+      last_claims = cl;
+      c.timing.expand_bytes += uint64_t(nX) * 32 + uint64_t(E) * 5 + uint64_t(cl) * 26;
+      if (int64_t(hc[C_ARENA]) > W.cap_arena) arena_lost = true;  // the batch end resets every byte instead
+      n_arena = std::min<int64_t>(int64_t(hc[C_ARENA]), W.cap_arena);
+      for (int s = 0; s < 2; s++) {
+        if (int64_t(hc[C_LIVE0 + s]) <= W.cap_next[s]) continue;
+        const int64_t total = int64_t(hc[C_LIVE0 + s]);
+        reserve(c, W.live_next[s], W.cap_next[s], total + 64, carried[s]);
+        const int32_t np = pair_list([s](int32_t stt, int32_t ps, int32_t) { return stt == SP_ACTIVE && ps == s; });
+        set_counter(C_LIVE0 + s, carried[s]);
+        regen(RG_LIVE, s, 0, np, W.live_next[s].as<uint64_t>(), W.cap_next[s], C_LIVE0 + s);
+      }
+      if (int64_t(hc[C_MEET]) > W.cap_meet) {
+        reserve(c, W.meet, W.cap_meet, int64_t(hc[C_MEET]) + 64, n_meet);
+        const int32_t tag = 2 + iter;
+        const int32_t np = pair_list([tag](int32_t stt, int32_t, int32_t m) { return stt == SP_MET && m == tag; });
+        set_counter(C_MEET, n_meet);
+        regen(RG_MEET, 1, 0, np, W.meet.as<uint64_t>(), W.cap_meet, C_MEET);
+      }
+      sync_counters();
       n_live[0] = int64_t(hc[C_LIVE0]);
       n_live[1] = int64_t(hc[C_LIVE1]);
-      n_arena = int64_t(hc[C_ARENA]);
       n_meet = int64_t(hc[C_MEET]);
       active = int64_t(hc[C_ACTIVE]);
       for (int s = 0; s < 2; s++) {
-        std::swap(live[s], live_next[s]);
-        std::swap(cap_live[s], cap_next[s]);
+        std::swap(W.live[s], W.live_next[s]);
+        std::swap(W.cap_live[s], W.cap_next[s]);
       }
     }
 
     // sweep: extend dist_B from the meet sets toward src along shortest paths only
     int64_t n_sw = n_meet;
-    std::swap(sweep[0], meet);
-    std::swap(cap_sweep[0], cap_meet);
-    while (n_sw > 0) {
+    DevBuf* cur = &W.meet;
+    int nxt = 0;
+    for (int32_t j = 1; n_sw > 0; j++) {
       ensure_x(n_sw);
-      NBG_HIP(hipMemsetAsync(cnt + C_X, 0, 8, c.stream));
-      NBG_HIP(hipMemsetAsync(cnt + C_XE, 0, 8, c.stream));
-      NBG_HIP(hipMemsetAsync(cnt + C_SWEEP, 0, 8, c.stream));
-      refresh();
-      k_sp_select<<<grid_n(n_sw), 256, 0, c.stream>>>(sweep[0].as<uint64_t>(), n_sw, 1, st, gout, gin,
-                                                       X.as<uint64_t>(), Xdeg.as<int64_t>(), cap_x, bf, cnt);
+      NBG_HIP(hipMemsetAsync(cnt + C_X, 0, 24, c.stream));
+      NBG_HIP(hipMemsetAsync(cnt + C_SWEEP, 0, 16, c.stream));  // C_SWEEP, C_XE
+      refresh(nullptr, 0);
+      k_sp_select<<<grid_n(n_sw), 256, 0, c.stream>>>(cur->as<uint64_t>(), n_sw, 1, st, gout, gin, W.X.as<uint64_t>(),
+                                                       W.Xdeg.as<int64_t>(), W.cap_x, bf, cnt);
       NBG_HIP(hipGetLastError());
-      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
+      sync_counters();
       const int64_t nX = int64_t(hc[C_X]), E = int64_t(hc[C_XE]);
       if (nX == 0 || E == 0) break;
       c.timing.edges_scanned += uint64_t(E);
-      grow_keep(c, arena, n_arena + E + 64, n_arena, cap_arena);
-      grow_keep(c, sweep[1], E + 64, 0, cap_sweep[1]);
-      refresh();
+      const int64_t want = std::min<int64_t>(E, soft) + 64;
+      reserve(c, W.sweep[nxt], W.cap_sweep[nxt], want, 0);
+      if (!arena_lost) reserve(c, W.arena, W.cap_arena, n_arena + want, n_arena);
+      refresh(&W.sweep[nxt], W.cap_sweep[nxt]);
       launch_scan(nX);
       launch_expand(nX, E, 1);
-      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
+      sync_counters();
       expand_time();
-      if (hc[C_OVF]) throw Error(NBG_E_UNKNOWN, "shortest path: list overflow");
-      c.timing.expand_bytes += uint64_t(nX) * 32 + uint64_t(E) * 6 + (hc[C_ARENA] - uint64_t(n_arena)) * 9;
-      n_arena = int64_t(hc[C_ARENA]);
+      c.timing.expand_bytes += uint64_t(nX) * 32 + uint64_t(E) * 6 + hc[C_SWEEP] * 18;
+      if (int64_t(hc[C_ARENA]) > W.cap_arena) arena_lost = true;
+      n_arena = std::min<int64_t>(int64_t(hc[C_ARENA]), W.cap_arena);
+      if (int64_t(hc[C_SWEEP]) > W.cap_sweep[nxt]) {
+        reserve(c, W.sweep[nxt], W.cap_sweep[nxt], int64_t(hc[C_SWEEP]) + 64, 0);
+        const int32_t np = pair_list([](int32_t stt, int32_t, int32_t) { return stt == SP_MET; });
+        set_counter(C_SWEEP, 0);
+        regen(RG_SWEEP, 1, j, np, W.sweep[nxt].as<uint64_t>(), W.cap_sweep[nxt], C_SWEEP);
+        sync_counters();
+      }
       n_sw = int64_t(hc[C_SWEEP]);
-      std::swap(sweep[0], sweep[1]);
-      std::swap(cap_sweep[0], cap_sweep[1]);
+      cur = &W.sweep[nxt];
+      nxt ^= 1;
     }
-    std::swap(sweep[0], meet);
-    std::swap(cap_sweep[0], cap_meet);
 
     // results + paths
     NBG_HIP(hipMemcpyAsync(hstate.data(), st.state, size_t(nb) * 4, hipMemcpyDeviceToHost, c.stream));
@@ -674,8 +771,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t*
                                                          vid_of, n, lo, cnt);
       NBG_HIP(hipGetLastError());
       NBG_HIP(hipMemcpyAsync(hpath.data() + base, dpath.p, size_t(plen) * 8, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
+      sync_counters();
       if (hc[C_WALKERR])
         throw Error(NBG_E_UNKNOWN, "shortest path: in-edge keys without mirrored out-edges on a shortest path");
       for (int64_t p = 0; p < nb; p++)  // src == dst (vertex possibly unknown): the path is [src]
@@ -683,8 +779,13 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t*
     }
     for (int64_t p = 0; p < nb; p++) hoff.push_back(hoff.back() + boff[size_t(p) + 1] - boff[size_t(p)]);
     // reset the batch's distance bytes
-    if (n_arena) k_sp_clear<<<grid_n(n_arena), 256, 0, c.stream>>>(arena.as<uint64_t>(), n_arena, d0, d1, n);
-    NBG_HIP(hipGetLastError());
+    if (arena_lost) {
+      const size_t used = ((size_t(nb) * size_t(n) + 3) & ~size_t(3)) + 64;
+      for (auto& d : c.sp_dist) NBG_HIP(hipMemsetAsync(d.p, 0xFF, std::min(used, c.sp_dist_bytes), c.stream));
+    } else if (n_arena) {
+      k_sp_clear<<<grid_n(n_arena), 256, 0, c.stream>>>(W.arena.as<uint64_t>(), n_arena, d0, d1, n);
+      NBG_HIP(hipGetLastError());
+    }
   }
   hipEventRecord(c.ev[1], c.stream);
   NBG_HIP(hipEventSynchronize(c.ev[1]));

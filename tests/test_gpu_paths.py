@@ -141,3 +141,23 @@ def test_nba_like_paths():
     assert got == want
     assert any(r[2] >= 2 for r in got)
     sp.close()
+
+
+def test_list_overflow_recovery():
+    # tiny list bounds force every overflow path: frontier lists and meet lists rebuilt from
+    # the distance bytes, the claim arena replaced by a full reset of the batch's bytes
+    scale = 12
+    sp = GraphSpace(64)
+    sp.set_edge_schema(FOLLOW, [("weight", 2)])
+    sp.gen_rmat(scale, 16, 1, FOLLOW)
+    sp.finalize()
+    st = O.Store(64)
+    st.set_edge_schema(FOLLOW, [("weight", O.INT)], name="follow")
+    st.load_rmat(scale, 16, 1, FOLLOW)
+    sp.set_option("sp_list_soft", 1)
+    s, t = synth.pairs(scale, 16, 1, 300, pick_seed=17)
+    got = sp.shortest_path(s, t, FOLLOW, 7).rows()
+    assert got == oracle_paths(st, s, t, FOLLOW, 7)
+    again = sp.shortest_path(t, s, FOLLOW, 7).rows()  # bytes were reset after the overflowed batch
+    assert again == oracle_paths(st, t, s, FOLLOW, 7)
+    sp.close()
