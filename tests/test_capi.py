@@ -1,0 +1,74 @@
+"""CPU checks of the C-ABI boundary (no compute calls: there is no GPU here).
+
+* every function include/nebula_amd.h declares is exported by libnebula_amd.so and bound in
+  nebula_amd/_lib.py;
+* the pure host helpers (partition / owner arithmetic) agree with the oracle's restatement of
+  StorageClient::partId (StorageClient.cpp:238-243) and pickHosts (CreateSpaceProcessor.cpp:77-90);
+* the product path refuses to run without an MI355X instead of falling back to the CPU.
+"""
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "nebula_amd.h"
+
+
+def _declared():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(nbg_[a-z_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from nebula_amd import _lib
+    if not _lib.LIB_PATH.exists():
+        pytest.skip("libnebula_amd.so not built (run __graft_entry__.build())")
+    return _lib.load()
+
+
+def test_header_declares_the_bound_surface():
+    from nebula_amd._lib import EXPORTS
+    assert _declared() == sorted(EXPORTS)
+
+
+def test_library_exports_every_declared_symbol(lib):
+    missing = [s for s in _declared() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_part_of_matches_oracle(lib, oracle):
+    rng = np.random.default_rng(3)
+    vids = np.concatenate([rng.integers(-2**63, 2**63 - 1, 2000, dtype=np.int64),
+                           np.array([0, 1, -1, 2**63 - 1, -2**63], dtype=np.int64)])
+    for parts in (1, 3, 64, 100):
+        for v in vids:
+            want = (int(v) % 2**64) % parts + 1  # StorageClient.cpp:238-243 (uint64 cast)
+            assert lib.nbg_part_of(int(v), parts) == want
+            assert oracle.part_of(int(v), parts) == want
+
+
+def test_rank_of_part(lib):
+    for world in (1, 2, 4, 8):
+        for p in range(1, 65):
+            assert lib.nbg_rank_of_part(p, world) == p % world
+
+
+def test_no_cpu_fallback(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    assert not lib.nbg_ctx_create(0, 64, 0, 1)
+    from nebula_amd import GraphSpace
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        GraphSpace(64)
+
+
+def test_invalid_context_arguments(lib):
+    assert not lib.nbg_ctx_create(0, 0, 0, 1)      # no parts
+    assert not lib.nbg_ctx_create(0, 64, 2, 2)     # rank out of range
+    assert lib.nbg_go(None, None, None) == -1001   # NBG_E_INVALID_ARG on a null context
