@@ -25,6 +25,39 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 
+def hop_kernels(h):
+    """rocprof names of the kernels one hop stat times"""
+    if h["mode"] == "bottom-up":
+        return ["nbg::k_bu_slab<1," if h["final"] else "nbg::k_bu_slab<0,"] + (["nbg::k_bits_compact<1>"] if h["final"] else [])
+    return ["nbg::k_expand<"]
+
+
+def pmc_traffic(workload: str, prefixes):
+    """HBM bytes per launch of the given kernels from the newest committed rocprof PMC summary of
+    the same workload (profiles/<tag>_summary.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
+    separate --pmc passes, tools/gpu_profile.sh + tools/profile_summary.py).  None if absent."""
+    best = None
+    for f in sorted((ROOT / "profiles").glob("*_summary.json"), key=lambda p: p.stat().st_mtime):
+        try:
+            d = json.loads(f.read_text())
+        except ValueError:
+            continue
+        b = d.get("bench") or {}
+        if (b.get("config") or {}).get("workload") != workload:
+            continue
+        tot, hit = 0.0, 0
+        for pre in prefixes:
+            ks = [k for k in d.get("query_kernels", []) if k["kernel"].startswith(pre)
+                  and k.get("fetch_bytes_x2") is not None]
+            if ks:
+                k = max(ks, key=lambda k: k["total_ms"])
+                tot += k["fetch_bytes_x2"] + (k.get("write_bytes") or 0.0)
+                hit += 1
+        if hit == len(prefixes):
+            best = {"bytes": tot, "source": f"profiles/{f.name}"}
+    return best
+
+
 def cpu_baseline(scale: int, seeds: int, where_k: int):
     """The oracle (CPU restatement of storaged+graphd, faithful mode: 10 bucket handlers,
     single-threaded graphd loop) on a bounded sample of the same query."""
@@ -151,7 +184,7 @@ def main():
     ap.add_argument("--seeds", type=int, default=64)
     ap.add_argument("--where", type=int, default=499)
     ap.add_argument("--hops", type=int, default=3)
-    ap.add_argument("--cpu-scale", type=int, default=18)
+    ap.add_argument("--cpu-scale", type=int, default=20)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--option", action="append", default=[], help="engine option key=value")
     ap.add_argument("--workload", choices=["go", "paths"], default="go",
@@ -212,6 +245,7 @@ def main():
     exp_bytes = 0
     tot_ms = 0.0
     bu_steps = 0
+    hop_ms, hop_bytes = {}, {}
     for _ in range(args.steps):
         r = one()
         t = sp.last_timing()
@@ -221,6 +255,10 @@ def main():
         exp_bytes += t["expand_bytes"]
         tot_ms += t["total_ms"]
         bu_steps = t["bu_steps"]
+        hop_stats = t["hops"]
+        for i, h in enumerate(hop_stats):
+            hop_ms[i] = hop_ms.get(i, 0.0) + h["ms"]
+            hop_bytes[i] = hop_bytes.get(i, 0) + h["bytes"]
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -233,6 +271,15 @@ def main():
         edges, rows = int(te[0].item()), int(te[1].item())
     gteps = edges / dt / 1e9
     achieved = exp_bytes / (exp_ms / 1e3) / 1e9 if exp_ms > 0 else 0.0
+    # dominant kernel: the hop with the largest summed time (the final bottom-up hop here)
+    dom = max(range(len(hop_stats)), key=lambda i: hop_ms[i]) if hop_stats else None
+    workload = (f"GO {args.hops} STEPS FROM {args.seeds} seeds OVER follow WHERE follow.weight > "
+                f"{args.where} YIELD DISTINCT follow._dst; RMAT-{args.scale} ef{args.edge_factor}")
+    if dom is not None:
+        dh = hop_stats[dom]
+        dom_ach = hop_bytes[dom] / (hop_ms[dom] / 1e3) / 1e9 if hop_ms[dom] > 0 else 0.0
+        dom_names = hop_kernels(dh)
+        tr = pmc_traffic(workload, dom_names)
     if rank == 0:
         out = {
             "metric": "GTEPS for GO 3 STEPS on RMAT-26 at 1/2/4/8 GPUs; % of HBM roofline",
@@ -248,8 +295,7 @@ def main():
             "dtype": "int64",
             "data": "synthetic RMAT (Graph500 a/b/c=0.57/0.19/0.19, seed 1) generated on device",
             "config": {
-                "workload": f"GO {args.hops} STEPS FROM {args.seeds} seeds OVER follow WHERE follow.weight > "
-                            f"{args.where} YIELD DISTINCT follow._dst; RMAT-{args.scale} ef{args.edge_factor}",
+                "workload": workload,
                 "vertices": info["num_vertices"],
                 "edges_after_collapse": info["local_out_edges"] if world == 1 else None,
                 "edges_scanned_per_query": edges // max(args.steps, 1),
@@ -259,16 +305,21 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_expand",
-                "achieved": achieved,
+                "kernel": " + ".join(k.rstrip("<,") for k in dom_names) + f" (hop {dom + 1} of {len(hop_stats)})",
+                "achieved": dom_ach,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": None,
+                "frac": dom_ach / HBM_PEAK_GBS,
+                "traffic": tr["bytes"] if tr else None,
+                "traffic_source": tr["source"] + " (FETCH_SIZE x2 + WRITE_SIZE per launch)" if tr else None,
+                "algorithmic_bytes_per_launch": hop_bytes[dom] // max(args.steps, 1),
+                "launch_ms": hop_ms[dom] / max(args.steps, 1),
+                "all_expansion_kernels": {"achieved": achieved, "frac": achieved / HBM_PEAK_GBS},
                 "algorithmic_bytes_per_query": exp_bytes // max(args.steps, 1),
                 "expand_ms_per_query": exp_ms / max(args.steps, 1),
                 "device_ms_per_query": tot_ms / max(args.steps, 1),
                 "bottom_up_hops": bu_steps,
+                "hops": hop_stats,
             },
             "cpu_baseline": None,
         }

@@ -196,6 +196,18 @@ int32_t nbg_shortest_path(nbg_ctx* ctx, int32_t edge_type, const int64_t* src,
                           const int64_t* dst, size_t npairs, int32_t max_steps, nbg_rows* out);
 
 /* ---- timing of the last call (HIP events on the engine stream) --------------------------- */
+/* one hop of the last nbg_go: mode 0 = top-down expansion of a frontier list, 1 = bottom-up
+ * over the transposed CSR.  c[]: top-down {frontier, entries, next frontier, 0, 0, 0};
+ * bottom-up {found, next-hop out-degree sum, slab words read, rows scanned past the slab,
+ * entries read past the slab, predicate values read past the slab}.                        */
+typedef struct {
+  int32_t mode;
+  int32_t final_hop;
+  double ms;         /* HIP-event time of the hop's expansion kernels                      */
+  uint64_t bytes;    /* their algorithmic bytes                       */
+  uint64_t c[6];
+} nbg_hop_stat;
+#define NBG_MAX_HOP_STATS 16
 typedef struct {
   double total_ms;        /* device time of the last nbg_go / nbg_get_bound                  */
   double expand_ms;       /* summed time of the expansion kernels                            */
@@ -206,6 +218,8 @@ typedef struct {
   int32_t bu_steps;       /* steps that ran bottom-up over the transposed CSR               */
   double comm_ms;         /* time in frontier exchanges / reductions between ranks          */
   uint64_t comm_bytes;    /* bytes this rank sent to other ranks                            */
+  int32_t n_hops;         /* entries of hops[] filled (nbg_go only)                          */
+  nbg_hop_stat hops[NBG_MAX_HOP_STATS];
 } nbg_timing;
 int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out);
 int32_t nbg_set_option(nbg_ctx* ctx, const char* key, int64_t value);

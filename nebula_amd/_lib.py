@@ -68,10 +68,19 @@ class GoSpec(C.Structure):
                 ("n_yields", C.c_size_t), ("distinct", C.c_int32), ("keep_on_device", C.c_int32)]
 
 
+class HopStat(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("final_hop", C.c_int32), ("ms", C.c_double), ("bytes", C.c_uint64),
+                ("c", C.c_uint64 * 6)]
+
+
+MAX_HOP_STATS = 16
+
+
 class Timing(C.Structure):
     _fields_ = [("total_ms", C.c_double), ("expand_ms", C.c_double), ("expand_launches", C.c_int64),
                 ("edges_scanned", C.c_uint64), ("expand_bytes", C.c_uint64), ("steps_run", C.c_int32),
-                ("bu_steps", C.c_int32), ("comm_ms", C.c_double), ("comm_bytes", C.c_uint64)]
+                ("bu_steps", C.c_int32), ("comm_ms", C.c_double), ("comm_bytes", C.c_uint64),
+                ("n_hops", C.c_int32), ("hops", HopStat * MAX_HOP_STATS)]
 
 
 _lib = None

@@ -230,6 +230,8 @@ int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out) {
     out->bu_steps = c.timing.bu_steps;
     out->comm_ms = c.timing.comm_ms;
     out->comm_bytes = c.timing.comm_bytes;
+    out->n_hops = c.timing.n_hops;
+    memcpy(out->hops, c.timing.hops, sizeof(out->hops));
     return NBG_OK;
   });
 }

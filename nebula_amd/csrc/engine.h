@@ -219,6 +219,20 @@ struct Timing {
   int32_t bu_steps = 0;
   double comm_ms = 0;
   uint64_t comm_bytes = 0;
+  int32_t n_hops = 0;
+  nbg_hop_stat hops[NBG_MAX_HOP_STATS] = {};
+  uint64_t hop_bytes_mark = 0;  // expand_bytes at the previous hop record
+  void hop(int32_t mode, bool final_hop, double ms, const unsigned long long* c6) {
+    const uint64_t b = expand_bytes - hop_bytes_mark;
+    hop_bytes_mark = expand_bytes;
+    if (n_hops >= NBG_MAX_HOP_STATS) return;
+    nbg_hop_stat& h = hops[n_hops++];
+    h.mode = mode;
+    h.final_hop = final_hop ? 1 : 0;
+    h.ms = ms;
+    h.bytes = b;
+    for (int i = 0; i < 6; i++) h.c[i] = c6 ? c6[i] : 0;
+  }
 };
 
 struct Ctx {

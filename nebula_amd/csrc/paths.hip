@@ -48,7 +48,7 @@ enum : int32_t { SP_ACTIVE = 0, SP_MET = 1, SP_DONE = 2 };
 // device counters (one array): live list F / B, arena, meets, X list, active pairs, overflow,
 // sweep list, X edges
 enum : int { C_LIVE0 = 0, C_LIVE1 = 1, C_ARENA = 2, C_MEET = 3, C_X = 4, C_ACTIVE = 5, C_OVF = 6, C_SWEEP = 7,
-             C_XE = 8, C_WALKERR = 9, C_N = 16 };
+             C_XE = 8, C_WALKERR = 9, C_PE = 10, C_N = 16 };
 
 __host__ __device__ inline uint64_t mk_tup(uint32_t side, uint32_t pair, uint32_t lvl, uint32_t row) {
   return (uint64_t(side) << 63) | (uint64_t(pair & 0x7FFFFFu) << 40) | (uint64_t(lvl & 0xFFu) << 32) | uint64_t(row);
@@ -78,7 +78,15 @@ struct SpState {  // per-pair arrays, B entries each
   int32_t* met;             // 1: a meet this iteration; 2 + i: met in iteration i
   unsigned long long* deg;  // [2][B] frontier sum of (degree + 1)
   int32_t B;
+  int32_t vmajor;           // distance bytes vertex-major [v][pair] (else pair-major [pair][v])
 };
+
+// byte index of (pair p, vertex v) in a distance array.  Vertex-major keeps the bytes of all
+// pairs of one vertex in one cache line run, so hub neighbourhoods expanded by many pairs share
+// lines in L2 / the Infinity cache; pair-major keeps each pair's bytes contiguous.
+__device__ inline uint64_t didx(const SpState& st, uint32_t p, uint64_t v, int64_t n) {
+  return st.vmajor ? v * uint64_t(st.B) + p : uint64_t(p) * uint64_t(n) + v;
+}
 
 struct SpBufs {
   uint64_t* live_next[2];
@@ -151,8 +159,8 @@ __global__ void k_sp_init(const int64_t* svid, const int64_t* tvid, const int32_
     st.state[p] = go ? SP_ACTIVE : SP_DONE;
     st.deg[p] = st.deg[B + p] = 0;
     if (go) {
-      d0[uint64_t(p) * n + uint32_t(a)] = 0;
-      d1[uint64_t(p) * n + uint32_t(b)] = 0;
+      d0[didx(st, uint32_t(p), uint32_t(a), n)] = 0;
+      d1[didx(st, uint32_t(p), uint32_t(b), n)] = 0;
       st.deg[p] = (unsigned long long)sp_deg(gout, uint32_t(a)) + 1;
       st.deg[B + p] = (unsigned long long)sp_deg(gin, uint32_t(b)) + 1;
     }
@@ -215,16 +223,16 @@ __global__ void k_sp_regen(int mode, int side, int32_t j, const int32_t* plist, 
     } else {
       tv = uint32_t(st.lvl[B + p] + j);
     }
-    const uint8_t* rowd = ((mode == RG_LIVE && side == 0) ? d0 : d1) + uint64_t(p) * uint64_t(n);
-    const uint8_t* rowf = d0 + uint64_t(p) * uint64_t(n);
+    const uint8_t* rowd = (mode == RG_LIVE && side == 0) ? d0 : d1;
+    const uint8_t* rowf = d0;
     const int64_t stride = int64_t(gridDim.x) * blockDim.x;
     const int64_t rounds = (n + stride - 1) / stride;
     for (int64_t r = 0; r < rounds; r++) {
       const int64_t v = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
       bool hit = false;
       if (v < n) {
-        hit = rowd[v] == tv;
-        if (mode == RG_MEET) hit = hit && rowf[v] == tf;
+        hit = rowd[didx(st, p, uint64_t(v), n)] == tv;
+        if (mode == RG_MEET) hit = hit && rowf[didx(st, p, uint64_t(v), n)] == tf;
       }
       put(out, cap, cnt, which, hit, mk_tup(mode == RG_LIVE ? uint32_t(side) : 1u, p, tv, uint32_t(v)));
     }
@@ -319,8 +327,12 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
     }
     __syncthreads();
     const int64_t i0 = s_hdr[0];
-    const int cnt_k = int(s_hdr[1]);
-    for (int k = threadIdx.x; k <= cnt_k; k += kT) {
+    const int64_t cnt64 = s_hdr[1];
+    // zero-degree X entries (dropped pairs, vertices without edges) can put more than kTileE
+    // entries under one tile: such a tile searches off[] in global memory instead of LDS
+    const bool big = cnt64 > kTileE;
+    const int cnt_k = big ? 0 : int(cnt64);
+    for (int k = threadIdx.x; k <= cnt_k && !big; k += kT) {
       const int64_t o = a.off[i0 + k];
       s_off[k] = int32_t(min(o - e0, int64_t(kTileE + 1)));
       if (k < cnt_k) {
@@ -335,21 +347,32 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
       const int64_t e = e0 + j;
       const bool valid = e < e1;
       int k = 0;
-      if (valid) {
+      uint64_t tu = 0;
+      int64_t rsk = 0;
+      if (valid && !big) {
         int lo = 0, hi = cnt_k;
         while (hi - lo > 1) {
           const int mid = (lo + hi) >> 1;
           if (s_off[mid] <= j) lo = mid; else hi = mid;
         }
         k = lo;
+        tu = s_tup[k];
+        rsk = s_rs[k];
+      } else if (valid) {
+        int64_t lo = i0, hi = i0 + cnt64;  // off[lo] <= e < off[hi]
+        while (hi - lo > 1) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (a.off[mid] <= e) lo = mid; else hi = mid;
+        }
+        tu = a.X[lo];
+        rsk = a.g[t_side(tu)].row_ptr[t_row(tu)] - a.off[lo];
       }
-      const uint64_t tu = s_tup[k];
       const uint32_t side = t_side(tu), p = t_pair(tu), l = t_lvl(tu);
       uint32_t w = 0;
       bool claimed = false;
       if (valid) {
-        w = uint32_t(int64_t(a.g[side].col[s_rs[k] + e]) - a.lo);
-        const uint64_t idx = uint64_t(p) * uint64_t(a.n) + w;
+        w = uint32_t(int64_t(a.g[side].col[rsk + e]) - a.lo);
+        const uint64_t idx = didx(st, p, w, a.n);
         if (!a.sweep) {
           claimed = claim_byte(a.dist[side], idx, l + 1);
         } else {
@@ -370,7 +393,7 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
       bool meet = false;
       uint32_t dt = 0;
       if (claimed) {
-        const uint8_t o = a.dist[side ^ 1][uint64_t(p) * uint64_t(a.n) + w];
+        const uint8_t o = a.dist[side ^ 1][didx(st, p, w, a.n)];
         if (o != 0xFF) {
           meet = true;
           dt = side ? l + 1 : uint32_t(o);
@@ -383,27 +406,150 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
   }
 }
 
-// one wave per pair that met: greedy walk from src (dist_B now exact on every shortest path)
-__global__ void k_sp_walk(SpState st, const int32_t* gs, const int64_t* path_off, int64_t* path, SpCsr gout,
-                          const uint8_t* dist_b, const int64_t* vid_of, int64_t n, int64_t lo,
-                          unsigned long long* cnt) {
+// ---- meet probe -----------------------------------------------------------------------------
+// Before a pair expands its cheaper side s (frontier at depth l, the other side at depth l_o),
+// probe whether the two frontiers are already one edge apart: a tuple's vertex r is a meet vertex
+// of length f + b + 1 iff some neighbour of r (out-neighbour for s = 0, in-neighbour for s = 1)
+// sits at depth l_o on the other side.  The probe scans each adjacency list only until its first
+// hit, so pairs that meet skip the full expansion (whose cost is the whole frontier's degree sum,
+// hubs included).  A failed probe leaves everything as it was: the expansion then finds no meet
+// either (a meet at f + b + 1 is exactly such an edge), so detection stays complete.
+constexpr int kProbeCh = 1024;  // adjacency entries per probe chunk (one wave each)
+
+// ch[i] = number of probe chunks of X[i]; ch[nX] = 0
+__global__ void k_sp_chunks(const int64_t* Xdeg, int64_t nX, int64_t* ch) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= nX; i += int64_t(gridDim.x) * blockDim.x)
+    ch[i] = i == nX ? 0 : (Xdeg[i] + kProbeCh - 1) / kProbeCh;
+}
+
+// One wave per chunk of kProbeCh entries of an X tuple, 64 entries a step, stopping at the first
+// hit or once another chunk has claimed the vertex.  The winner claims r's byte on the other
+// side (depth l_o + 1: the vertex is then seen by both sides, as after an expansion of the other
+// side) and records that claim in slot[c] (an arena tuple); k_sp_gather_meets turns the slots into
+// the meet list without a global atomic per meet.
+__global__ __launch_bounds__(256) void k_sp_probe(const uint64_t* __restrict__ X, int64_t nX,
+                                                  const int64_t* __restrict__ choff, SpCsr g0, SpCsr g1, uint8_t* d0,
+                                                  uint8_t* d1, int64_t n, int64_t lo, SpState st, uint64_t* slot,
+                                                  unsigned long long* cnt) {
   const int lane = threadIdx.x & 63;
-  const int64_t p = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  if (p >= st.B || st.state[p] != SP_MET) return;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  const int64_t total = choff[nX];
+  unsigned long long examined = 0;
+  for (int64_t c = wave; c < total; c += nwaves) {
+    int64_t a = 0, b = nX;  // last tuple with choff[a] <= c
+    while (b - a > 1) {
+      const int64_t mid = (a + b) >> 1;
+      if (choff[mid] <= c) a = mid; else b = mid;
+    }
+    const uint64_t t = X[a];
+    const uint32_t side = t_side(t), p = t_pair(t), row = t_row(t);
+    const int64_t* rp = side ? g1.row_ptr : g0.row_ptr;
+    const int32_t* col = side ? g1.col : g0.col;
+    const int64_t x0 = rp[row] + (c - choff[a]) * kProbeCh;
+    const int64_t x1 = min(x0 + int64_t(kProbeCh), rp[row + 1]);
+    const uint32_t other = side ^ 1u;
+    const uint32_t need = uint32_t(st.lvl[other * uint32_t(st.B) + p]);
+    uint8_t* od = other ? d1 : d0;
+    const uint64_t ci = didx(st, p, row, n);
+    for (int64_t x = x0; x < x1; x += 64) {
+      if (*reinterpret_cast<volatile const uint8_t*>(od + ci) != 0xFF) break;
+      const int64_t ex = x + lane;
+      bool hit = false;
+      if (ex < x1) {
+        examined++;
+        hit = od[didx(st, p, uint32_t(int64_t(col[ex]) - lo), n)] == uint8_t(need);
+      }
+      if (__ballot(hit)) {
+        if (lane == 0 && claim_byte(od, ci, need + 1)) {
+          st.met[p] = 1;
+          slot[c] = mk_tup(other, p, need + 1, row);
+        }
+        break;
+      }
+    }
+  }
+  const unsigned long long ev = wsum(examined);
+  if (lane == 0 && ev) atomicAdd(cnt + C_PE, ev);
+}
+
+// slots -> meet list (1, p, dt, r) + arena (the claimed byte).  Runs before k_sp_probe_step, so
+// lvl still holds the depths the probe compared against.
+__global__ void k_sp_gather_meets(const uint64_t* slot, int64_t m, SpState st, SpBufs bf, unsigned long long* cnt) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int64_t rounds = (m + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    const uint64_t t = i < m ? slot[i] : ~0ull;
+    const bool ok = t != ~0ull;
+    uint64_t mt = 0;
+    if (ok) {
+      const uint32_t p = t_pair(t);
+      // claimed backward byte: r has dt = its new depth; claimed forward byte: r is on the
+      // backward frontier (dt = the backward depth)
+      mt = t_side(t) ? mk_tup(1, p, t_lvl(t), t_row(t))
+                     : mk_tup(1, p, uint32_t(st.lvl[uint32_t(st.B) + p]), t_row(t));
+    }
+    put(bf.meet, bf.cap_meet, cnt, C_MEET, ok, mt);
+    put(bf.arena, bf.cap_arena, cnt, C_ARENA, ok, t);
+  }
+}
+
+// pairs whose probe met: finish as if the other side had expanded (its depth + 1)
+__global__ void k_sp_probe_step(SpState st, int32_t iter) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= st.B || st.state[p] != SP_ACTIVE || st.met[p] != 1) return;
+  const int B = st.B;
+  const int adv = st.side[p] ^ 1;
+  st.lvl[adv * B + p] += 1;
+  st.res[p] = st.lvl[p] + st.lvl[B + p];
+  st.state[p] = SP_MET;
+  st.met[p] = 2 + iter;
+  st.pside[p] = adv;
+}
+
+// X tuples of pairs that are no longer active: degree 0 (the expansion skips them)
+__global__ void k_sp_drop(const uint64_t* X, int64_t* Xdeg, int64_t nX, SpState st, unsigned long long* cnt) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int64_t rounds = (nX + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    unsigned long long d = 0;
+    if (i < nX && st.state[t_pair(X[i])] != SP_ACTIVE) {
+      d = (unsigned long long)Xdeg[i];
+      Xdeg[i] = 0;
+    }
+    const unsigned long long sd = wsum(d);
+    if ((threadIdx.x & 63) == 0 && sd) atomicAdd(cnt + C_XE, 0ull - sd);
+  }
+}
+
+// one workgroup per pair that met: greedy walk from src (dist_B now exact on every shortest
+// path).  Each step scans the current vertex's out-edges with the whole workgroup (hub rows on a
+// path hold 10^5+ entries) and takes the smallest vid among those one step closer to dst.
+constexpr int kWalkT = 512;
+__global__ __launch_bounds__(kWalkT) void k_sp_walk(SpState st, const int32_t* gs, const int64_t* path_off,
+                                                    int64_t* path, SpCsr gout, const uint8_t* dist_b,
+                                                    const int64_t* vid_of, int64_t n, int64_t lo,
+                                                    unsigned long long* cnt) {
+  __shared__ int64_t s_best[kWalkT / 64], s_w[kWalkT / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t p = blockIdx.x;
+  if (p >= st.B || st.state[p] != SP_MET) return;  // uniform over the workgroup
   const int32_t L = st.res[p];
   const int64_t o = path_off[p];
   uint32_t v = uint32_t(gs[p]);
-  if (lane == 0) path[o] = vid_of[lo + v];
-  const uint8_t* db = dist_b + uint64_t(p) * uint64_t(n);
+  if (threadIdx.x == 0) path[o] = vid_of[lo + v];
+  const uint8_t* db = dist_b;
   for (int32_t i = 0; i < L; i++) {
     const uint8_t need = uint8_t(L - i - 1);
     int64_t best = INT64_MAX;
     int64_t bw = -1;
     if (!(gout.row_ok && !gout.row_ok[v])) {
       const int64_t e1 = gout.row_ptr[v + 1];
-      for (int64_t e = gout.row_ptr[v] + lane; e < e1; e += 64) {
+      for (int64_t e = gout.row_ptr[v] + threadIdx.x; e < e1; e += kWalkT) {
         const int64_t w = int64_t(gout.col[e]) - lo;
-        if (db[w] == need) {
+        if (db[didx(st, uint32_t(p), uint64_t(w), n)] == need) {
           const int64_t vv = vid_of[lo + w];
           if (vv < best) {
             best = vv;
@@ -413,28 +559,41 @@ __global__ void k_sp_walk(SpState st, const int32_t* gs, const int64_t* path_off
       }
     }
 #pragma unroll
-    for (int s = 32; s > 0; s >>= 1) {
-      const int64_t ob = __shfl_xor(best, s);
-      const int64_t ow = __shfl_xor(bw, s);
+    for (int sft = 32; sft > 0; sft >>= 1) {
+      const int64_t ob = __shfl_xor(best, sft);
+      const int64_t ow = __shfl_xor(bw, sft);
       if (ow >= 0 && (bw < 0 || ob < best)) {
         best = ob;
         bw = ow;
       }
     }
+    if (lane == 0) {
+      s_best[wv] = best;
+      s_w[wv] = bw;
+    }
+    __syncthreads();
+    best = INT64_MAX;
+    bw = -1;
+    for (int k = 0; k < kWalkT / 64; k++)
+      if (s_w[k] >= 0 && (bw < 0 || s_best[k] < best)) {
+        best = s_best[k];
+        bw = s_w[k];
+      }
+    __syncthreads();
     if (bw < 0) {  // in-edge keys without the mirrored out-edge: the definition does not hold
-      if (lane == 0) atomicAdd(cnt + C_WALKERR, 1ull);
+      if (threadIdx.x == 0) atomicAdd(cnt + C_WALKERR, 1ull);
       return;
     }
     v = uint32_t(bw);
-    if (lane == 0) path[o + i + 1] = best;
+    if (threadIdx.x == 0) path[o + i + 1] = best;
   }
 }
 
 // reset every claimed distance byte of the batch
-__global__ void k_sp_clear(const uint64_t* arena, int64_t m, uint8_t* d0, uint8_t* d1, int64_t n) {
+__global__ void k_sp_clear(const uint64_t* arena, int64_t m, uint8_t* d0, uint8_t* d1, int64_t n, SpState st) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
     const uint64_t t = arena[i];
-    (t_side(t) ? d1 : d0)[uint64_t(t_pair(t)) * uint64_t(n) + t_row(t)] = 0xFF;
+    (t_side(t) ? d1 : d0)[didx(st, t_pair(t), t_row(t), n)] = 0xFF;
   }
 }
 
@@ -517,6 +676,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t*
   int32_t* dgs = W.gidx.as<int32_t>();
   int32_t* dgt = dgs + B;
   const int64_t soft = std::max<int64_t>(c.opt("sp_list_soft", int64_t(16) << 20), 1024);
+  const bool probe = c.opt("sp_probe", 1) != 0;
 
   std::vector<int64_t> hres(npairs), hoff(1, 0), hpath;
   std::vector<int32_t> hstate(static_cast<size_t>(B)), hres_b(static_cast<size_t>(B)),
@@ -533,6 +693,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t*
     st.side = st.lvl + 2 * nb;
     st.pside = st.side + nb;
     st.met = st.pside + nb;
+    st.vmajor = int32_t(c.opt("sp_vmajor", 0));
     NBG_HIP(hipMemcpyAsync(dsv, src + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
     NBG_HIP(hipMemcpyAsync(dtv, dst + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
     lookup_gidx(c, dsv, dgs, nb);
@@ -661,8 +822,50 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t*
       NBG_HIP(hipGetLastError());
       sync_counters();
       if (hc[C_OVF] & 2) throw Error(NBG_E_UNKNOWN, "shortest path: frontier list overflow");
-      const int64_t nX = int64_t(hc[C_X]), E = int64_t(hc[C_XE]);
+      const int64_t nX = int64_t(hc[C_X]);
+      int64_t E = int64_t(hc[C_XE]);
       const int64_t carried[2] = {int64_t(hc[C_LIVE0]), int64_t(hc[C_LIVE1])};
+      if (E > 0 && probe) {
+        // meet probe: pairs one edge short of meeting skip this iteration's expansion
+        const int64_t max_chunks = nX + E / kProbeCh + 64;
+        reserve(c, W.meet, W.cap_meet, n_meet + max_chunks, n_meet);
+        if (!arena_lost) reserve(c, W.arena, W.cap_arena, n_arena + max_chunks, n_arena);
+        refresh(nullptr, 0);
+        DevBuf ch, choff, slot;
+        ch.alloc(size_t(nX + 1) * 8);
+        choff.alloc(size_t(nX + 1) * 8);
+        slot.alloc(size_t(max_chunks) * 8);
+        NBG_HIP(hipMemsetAsync(slot.p, 0xFF, size_t(max_chunks) * 8, c.stream));
+        NBG_HIP(hipMemsetAsync(cnt + C_PE, 0, 8, c.stream));
+        k_sp_chunks<<<grid_n(nX + 1), 256, 0, c.stream>>>(W.Xdeg.as<int64_t>(), nX, ch.as<int64_t>());
+        size_t tb = 0;
+        NBG_HIP(rocprim::exclusive_scan(nullptr, tb, ch.as<int64_t>(), choff.as<int64_t>(), int64_t(0),
+                                        size_t(nX + 1), rocprim::plus<int64_t>(), c.stream));
+        c.ws_tmp.ensure(tb);
+        NBG_HIP(rocprim::exclusive_scan(c.ws_tmp.p, tb, ch.as<int64_t>(), choff.as<int64_t>(), int64_t(0),
+                                        size_t(nX + 1), rocprim::plus<int64_t>(), c.stream));
+        hipEventRecord(c.ev[4], c.stream);
+        const int pgrid =
+            int(std::max<int64_t>(1, std::min<int64_t>((max_chunks + 3) / 4, c.opt("sp_probe_grid", 4096))));
+        k_sp_probe<<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), gout, gin, d0, d1, n, lo,
+                                                st, slot.as<uint64_t>(), cnt);
+        k_sp_gather_meets<<<grid_n(max_chunks), 256, 0, c.stream>>>(slot.as<uint64_t>(), max_chunks, st, bf, cnt);
+        k_sp_probe_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, iter);
+        k_sp_drop<<<grid_n(nX), 256, 0, c.stream>>>(W.X.as<uint64_t>(), W.Xdeg.as<int64_t>(), nX, st, cnt);
+        NBG_HIP(hipGetLastError());
+        hipEventRecord(c.ev[5], c.stream);
+        sync_counters();
+        float pms = 0;
+        hipEventElapsedTime(&pms, c.ev[4], c.ev[5]);
+        c.timing.expand_ms += pms;
+        c.timing.expand_launches++;
+        c.timing.edges_scanned += hc[C_PE];
+        c.timing.expand_bytes += uint64_t(nX) * 24 + hc[C_PE] * 5;
+        E = int64_t(hc[C_XE]);
+        n_meet = int64_t(hc[C_MEET]);
+        if (int64_t(hc[C_ARENA]) > W.cap_arena) arena_lost = true;
+        n_arena = std::min<int64_t>(int64_t(hc[C_ARENA]), W.cap_arena);
+      }
       c.timing.edges_scanned += uint64_t(E);
       if (E > 0) {
         // lists sized for min(every edge claims, a soft bound); an overflow is rebuilt below
@@ -767,7 +970,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t*
       dpath.alloc(size_t(plen) * 8);
       NBG_HIP(hipMemcpyAsync(doff.p, boff.data(), size_t(nb + 1) * 8, hipMemcpyHostToDevice, c.stream));
       NBG_HIP(hipMemsetAsync(cnt + C_WALKERR, 0, 8, c.stream));
-      k_sp_walk<<<int((nb + 3) / 4), 256, 0, c.stream>>>(st, dgs, doff.as<int64_t>(), dpath.as<int64_t>(), gout, d1,
+      k_sp_walk<<<int(nb), kWalkT, 0, c.stream>>>(st, dgs, doff.as<int64_t>(), dpath.as<int64_t>(), gout, d1,
                                                          vid_of, n, lo, cnt);
       NBG_HIP(hipGetLastError());
       NBG_HIP(hipMemcpyAsync(hpath.data() + base, dpath.p, size_t(plen) * 8, hipMemcpyDeviceToHost, c.stream));
@@ -783,7 +986,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t*
       const size_t used = ((size_t(nb) * size_t(n) + 3) & ~size_t(3)) + 64;
       for (auto& d : c.sp_dist) NBG_HIP(hipMemsetAsync(d.p, 0xFF, std::min(used, c.sp_dist_bytes), c.stream));
     } else if (n_arena) {
-      k_sp_clear<<<grid_n(n_arena), 256, 0, c.stream>>>(W.arena.as<uint64_t>(), n_arena, d0, d1, n);
+      k_sp_clear<<<grid_n(n_arena), 256, 0, c.stream>>>(W.arena.as<uint64_t>(), n_arena, d0, d1, n, st);
       NBG_HIP(hipGetLastError());
     }
   }

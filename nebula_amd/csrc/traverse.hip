@@ -79,6 +79,16 @@ __device__ inline int64_t load_int(const void* data, int width, int64_t i) {
   }
 }
 
+// compile-time width variant (W = 0: runtime width)
+template <int W>
+__device__ inline int64_t load_w(const void* data, int width, int64_t i) {
+  if (W == 1) return int64_t(static_cast<const int8_t*>(data)[i]);
+  if (W == 2) return int64_t(static_cast<const int16_t*>(data)[i]);
+  if (W == 4) return int64_t(static_cast<const int32_t*>(data)[i]);
+  if (W == 8) return static_cast<const int64_t*>(data)[i];
+  return load_int(data, width, i);
+}
+
 __device__ inline Val load_prop(const PropDev& p, int64_t ge) {
   Val v;
   v.len = 0;
@@ -342,8 +352,12 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
     }
     __syncthreads();
     const int64_t i0 = s_hdr[0];
-    const int cnt = int(s_hdr[1]);
-    for (int k = threadIdx.x; k <= cnt; k += kThreads) {
+    const int64_t cnt64 = s_hdr[1];
+    // a run of zero-degree frontier entries can put more than kTile entries under one tile:
+    // such a tile searches off[] in global memory instead of staging it in LDS
+    const bool big = cnt64 > kTile;
+    const int cnt = big ? 0 : int(cnt64);
+    for (int k = threadIdx.x; k <= cnt && !big; k += kThreads) {
       int64_t o = a.off[i0 + k];
       s_off[k] = int32_t(min(o - e0, int64_t(kTile + 1)));
       if (k < cnt) {
@@ -359,15 +373,29 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
       const int64_t e = e0 + j;
       const bool valid = e < e1;
       int k = 0;
+      int32_t srck = 0;
+      int64_t rsk = 0;
       if (valid) {
-        int lo = 0, hi = cnt;  // s_off[lo] <= j < s_off[hi]
-        while (hi - lo > 1) {
-          int mid = (lo + hi) >> 1;
-          if (s_off[mid] <= j) lo = mid; else hi = mid;
+        if (!big) {
+          int lo = 0, hi = cnt;  // s_off[lo] <= j < s_off[hi]
+          while (hi - lo > 1) {
+            int mid = (lo + hi) >> 1;
+            if (s_off[mid] <= j) lo = mid; else hi = mid;
+          }
+          k = lo;
+          srck = s_src[k];
+          rsk = s_rs[k];
+        } else {
+          int64_t lo = i0, hi = i0 + cnt64;  // off[lo] <= e < off[hi]
+          while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (a.off[mid] <= e) lo = mid; else hi = mid;
+          }
+          srck = a.F[lo];
+          rsk = a.row_ptr[srck] - a.off[lo];
         }
-        k = lo;
       }
-      const int64_t ge = valid ? s_rs[k] + e : 0;
+      const int64_t ge = valid ? rsk + e : 0;
       bool pass = valid;
       int32_t d = 0;
       if (valid && (MODE != EXP_FLAGS || PK == PK_VM)) d = a.col[ge];
@@ -382,7 +410,7 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
           pass = fast_cmp(fp.op, load_int(fp.data, fp.width, ge), fp.k);
         }
       } else if (PK == PK_VM && valid) {
-        Val v = eval_program(prog, env, ge, int32_t(a.lo) + s_src[k], d);
+        Val v = eval_program(prog, env, ge, int32_t(a.lo) + srck, d);
         if (v.t == VT_ERR) {
           if (a.storage) pass = true;
           else {
@@ -404,7 +432,7 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
       } else if (MODE == EXP_ROWS) {
         int64_t slot = wave_append(a.rows_cnt, pass);
         if (pass) {
-          a.rows_src[slot] = s_src[k];
+          a.rows_src[slot] = srck;
           a.rows_edge[slot] = ge;
         }
       } else {
@@ -499,21 +527,31 @@ __device__ inline void block_store_partials(const unsigned long long* v, int k, 
     partials[size_t(threadIdx.x) * kAggBlocks + blockIdx.x] = s;  // slot-major: coalesced reduce
   }
 }
-// sums the [kSlots][kAggBlocks] partials into out[0..kSlots) (one block)
-__global__ void k_reduce_partials(const unsigned long long* partials, int nblocks, unsigned long long* out) {
-  __shared__ unsigned long long s[kSlots][256];
+// sums the [kSlots][kAggBlocks] partials into out[0..kSlots) (one block of 1024 threads; all
+// kSlots loads of an iteration are independent, so the block has 8 loads in flight per lane
+// instead of one dependent chain per slot)
+__global__ __launch_bounds__(1024) void k_reduce_partials(const unsigned long long* partials, int nblocks,
+                                                          unsigned long long* out) {
+  __shared__ unsigned long long s[kSlots][16];
+  unsigned long long a[kSlots];
+#pragma unroll
+  for (int k = 0; k < kSlots; k++) a[k] = 0;
+  for (int b = threadIdx.x; b < nblocks; b += blockDim.x) {
+#pragma unroll
+    for (int k = 0; k < kSlots; k++) a[k] += partials[size_t(k) * kAggBlocks + b];
+  }
+  const int w = threadIdx.x >> 6, nw = int(blockDim.x >> 6);
+#pragma unroll
   for (int k = 0; k < kSlots; k++) {
-    unsigned long long a = 0;
-    for (int b = threadIdx.x; b < nblocks; b += blockDim.x) a += partials[size_t(k) * kAggBlocks + b];
-    s[k][threadIdx.x] = a;
+    unsigned long long v = wave_sum_u64(a[k]);
+    if ((threadIdx.x & 63) == 0) s[k][w] = v;
   }
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < unsigned(o))
-      for (int k = 0; k < kSlots; k++) s[k][threadIdx.x] += s[k][threadIdx.x + o];
-    __syncthreads();
+  if (threadIdx.x < unsigned(kSlots)) {
+    unsigned long long v = 0;
+    for (int j = 0; j < nw; j++) v += s[threadIdx.x][j];
+    out[threadIdx.x] = v;
   }
-  if (threadIdx.x < unsigned(kSlots)) out[threadIdx.x] = s[threadIdx.x][0];
 }
 
 // Bottom-up hop over the slab (first K hub-first entries of each transposed row, slot-major)
@@ -528,15 +566,27 @@ __global__ void k_reduce_partials(const unsigned long long* partials, int nblock
 // out-edges and sum their out-degrees (the next hop's E).  partials: [0] found, [1] out-degree
 // sum, [2] slab words read (+ their predicate values), [3] rows scanned past the slab, [4] entries
 // read past the slab, [5] predicate values read past the slab.
-template <int PK, int EAGER, int R>
-__global__ __launch_bounds__(256) void k_bu_slab(const int32_t* __restrict__ slab, const void* __restrict__ slab_w,
+template <int PK, int EAGER, int R, int W>
+__global__ __launch_bounds__(1024) void k_bu_slab(const int32_t* __restrict__ slab, const void* __restrict__ slab_w,
                                                  int K, const int64_t* __restrict__ trp,
                                                  const int32_t* __restrict__ tcol, int64_t n,
                                                  const uint32_t* __restrict__ fbits,
                                                  unsigned long long* __restrict__ nbits,
                                                  const uint32_t* __restrict__ odeg, FastArgs fp,
-                                                 unsigned long long* partials) {
+                                                 unsigned long long* partials, int nt,
+                                                 unsigned long long* __restrict__ pbits, int cw) {
   __shared__ unsigned long long lds[kSlots * 16];
+  // the first cw words of the frontier bitmap (the hubs: vertices are numbered by descending
+  // out-degree and slab rows list hub sources first) are copied into LDS, so most lookups are
+  // LDS reads instead of random L2 / Infinity-cache requests
+  extern __shared__ uint32_t s_fb[];
+  for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
+  if (cw) __syncthreads();
+  auto in_front = [&](int32_t sv) -> bool {
+    const int32_t wi = sv >> 5;
+    const uint32_t w = wi < cw ? s_fb[wi] : fbits[wi];
+    return (w >> (sv & 31)) & 1u;
+  };
   unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
@@ -559,15 +609,15 @@ __global__ __launch_bounds__(256) void k_bu_slab(const int32_t* __restrict__ sla
     int64_t wv[R][EAGER];
 #pragma unroll
     for (int j = 0; j < R; j++) {
-      if (odeg && pend[j]) od[j] = odeg[d[j]];
+      if (odeg && pend[j]) od[j] = nt ? __builtin_nontemporal_load(odeg + d[j]) : odeg[d[j]];
 #pragma unroll
       for (int q = 0; q < EAGER; q++) {
         sv[j][q] = -1;
         wv[j][q] = 0;
         if (pend[j] && q < KE) {
           const int64_t si = int64_t(q) * n + d[j];
-          sv[j][q] = slab[si];
-          if (PK == PK_FAST) wv[j][q] = load_int(slab_w, fp.width, si);
+          sv[j][q] = nt ? __builtin_nontemporal_load(slab + si) : slab[si];
+          if (PK == PK_FAST) wv[j][q] = load_w<W>(slab_w, fp.width, si);
         }
       }
     }
@@ -584,7 +634,7 @@ __global__ __launch_bounds__(256) void k_bu_slab(const int32_t* __restrict__ sla
           exhausted = true;
           continue;
         }
-        if ((fbits[s >> 5] >> (s & 31)) & 1u) {
+        if (in_front(s)) {
           if (PK != PK_FAST || fast_cmp(fp.op, wv[j][q], fp.k)) found[j] = true;
         }
       }
@@ -604,8 +654,8 @@ __global__ __launch_bounds__(256) void k_bu_slab(const int32_t* __restrict__ sla
         w1[j] = 0;
         if (pend[j]) {
           const int64_t si = int64_t(q) * n + d[j];
-          s1[j] = slab[si];
-          if (PK == PK_FAST) w1[j] = load_int(slab_w, fp.width, si);
+          s1[j] = nt ? __builtin_nontemporal_load(slab + si) : slab[si];
+          if (PK == PK_FAST) w1[j] = load_w<W>(slab_w, fp.width, si);
         }
       }
 #pragma unroll
@@ -617,7 +667,7 @@ __global__ __launch_bounds__(256) void k_bu_slab(const int32_t* __restrict__ sla
           pend[j] = false;
           continue;
         }
-        if ((fbits[s >> 5] >> (s & 31)) & 1u) {
+        if (in_front(s)) {
           if (PK != PK_FAST || fast_cmp(fp.op, w1[j], fp.k)) {
             found[j] = true;
             pend[j] = false;
@@ -625,7 +675,23 @@ __global__ __launch_bounds__(256) void k_bu_slab(const int32_t* __restrict__ sla
         }
       }
     }
-    // rows with more entries than the slab: wave-cooperative scan of the rest
+    // rows with more entries than the slab and no hit in it.  Deferred (pbits): one pending
+    // bit per row (a coalesced ballot word, no atomics) for the edge-balanced second pass
+    // k_bu_rest; rows of a non-final hop without out-edges are dropped (they cannot extend
+    // the frontier).  Otherwise the whole wave scans the rest of each such row in turn.
+    if (pbits) {
+#pragma unroll
+      for (int j = 0; j < R; j++) {
+        bool pj = pend[j] && (odeg == nullptr || od[j] > 0);
+        // only rows with entries past the slab (k_bu_rest's tiles assume no empty rows)
+        if (pj) pj = trp[d[j] + 1] - trp[d[j]] > K;
+        const unsigned long long pm = __ballot(pj);
+        const int64_t d0 = t * 64 * R + j * 64;
+        if (lane == 0 && d0 < n) pbits[d0 >> 6] = pm;
+        acc[3] += pj;
+        pend[j] = false;
+      }
+    }
     int64_t rb[R], re[R];
 #pragma unroll
     for (int j = 0; j < R; j++) {
@@ -636,9 +702,20 @@ __global__ __launch_bounds__(256) void k_bu_slab(const int32_t* __restrict__ sla
         if (rb[j] >= re[j]) pend[j] = false;
       }
     }
+    // Long rests (> kLongRest entries) are scanned by the whole wave, 64 entries a step; short
+    // ones by 16-lane groups, four rows at a time, so the tile's latency chain is paid once per
+    // four pending rows instead of once per row.  Both stop at the row's first hit.
+    constexpr int kLongRest = 256, GL = 16, NG = 64 / GL;
+    unsigned long long pml[R], pms[R];
 #pragma unroll
     for (int j = 0; j < R; j++) {
-      unsigned long long pm = __ballot(pend[j]);
+      const bool lng = pend[j] && re[j] - rb[j] > kLongRest;
+      pml[j] = __ballot(lng);
+      pms[j] = __ballot(pend[j] && !lng);
+    }
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      unsigned long long pm = pml[j];
       while (pm) {
         const int src = __ffsll((long long)pm) - 1;
         pm &= pm - 1;
@@ -651,10 +728,10 @@ __global__ __launch_bounds__(256) void k_bu_slab(const int32_t* __restrict__ sla
           if (ex < e) {
             const int32_t s = tcol[ex];
             acc[4]++;
-            if ((fbits[s >> 5] >> (s & 31)) & 1u) {
+            if (in_front(s)) {
               if (PK == PK_FAST) {
                 acc[5]++;
-                h = fast_cmp(fp.op, load_int(fp.data, fp.width, ex), fp.k);
+                h = fast_cmp(fp.op, load_w<W>(fp.data, fp.width, ex), fp.k);
               } else {
                 h = true;
               }
@@ -663,6 +740,66 @@ __global__ __launch_bounds__(256) void k_bu_slab(const int32_t* __restrict__ sla
           f = __ballot(h) != 0;
         }
         if (lane == src) found[j] = f;
+      }
+    }
+    {
+      const int grp = lane / GL, gl = lane % GL;
+      for (;;) {
+        int my_j = -1, my_src = 0, taken = 0;
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+          while (pms[j] && taken < NG) {
+            const int sidx = __ffsll((long long)pms[j]) - 1;
+            if (taken == grp) {
+              my_j = j;
+              my_src = sidx;
+            }
+            pms[j] &= pms[j] - 1;
+            taken++;
+          }
+        }
+        if (taken == 0) break;
+        int64_t b = 0, e = 0;
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+          const int64_t bj = __shfl((long long)rb[j], my_src), ej = __shfl((long long)re[j], my_src);
+          if (my_j == j) {
+            b = bj;
+            e = ej;
+          }
+        }
+        acc[3] += gl == 0 && my_j >= 0;
+        bool f = false;
+        for (int64_t x = b;; x += GL) {
+          const bool act = !f && x < e;
+          if (__ballot(act) == 0) break;
+          bool h = false;
+          if (act) {
+            const int64_t ex = x + gl;
+            if (ex < e) {
+              const int32_t s = tcol[ex];
+              acc[4]++;
+              if (in_front(s)) {
+                if (PK == PK_FAST) {
+                  acc[5]++;
+                  h = fast_cmp(fp.op, load_w<W>(fp.data, fp.width, ex), fp.k);
+                } else {
+                  h = true;
+                }
+              }
+            }
+          }
+          const unsigned long long hb = __ballot(h);
+          if (act && ((hb >> (grp * GL)) & ((1ull << GL) - 1ull))) f = true;
+        }
+#pragma unroll
+        for (int g = 0; g < NG; g++) {
+          const int sj = __shfl(my_j, g * GL), ss = __shfl(my_src, g * GL);
+          const int fg = __shfl(int(f), g * GL);
+#pragma unroll
+          for (int j = 0; j < R; j++)
+            if (sj == j && lane == ss) found[j] = fg != 0;
+        }
       }
     }
     // next frontier words
@@ -678,6 +815,111 @@ __global__ __launch_bounds__(256) void k_bu_slab(const int32_t* __restrict__ sla
     }
   }
   block_store_partials(acc, 6, lds, partials);
+}
+
+// Second pass of a deferred bottom-up hop: the rows k_bu_slab left pending (list F, nF rows),
+// entries past the slab [trp[r] + K, trp[r + 1]) spread edge-balanced over the workgroups exactly
+// like the top-down expansion (tiles of kTile entries, owner row by binary search in LDS), so the
+// long in-edge lists no longer serialise one wave.  A hit sets the row's flag in LDS; after the
+// tile one thread per hit row ORs the row's bit into the next-frontier words (returning atomic:
+// only the first setter counts the row).  partials: [0] rows found, [1] their out-degree sum,
+// [2] entries read, [3] predicate values read.
+template <int PK>
+__global__ __launch_bounds__(kThreads) void k_bu_rest(const int32_t* __restrict__ F, int64_t nF,
+                                                      const int64_t* __restrict__ off, const int64_t* __restrict__ trp,
+                                                      const int32_t* __restrict__ tcol, int K,
+                                                      const uint32_t* __restrict__ fbits, unsigned long long* nbits,
+                                                      const uint32_t* __restrict__ odeg, FastArgs fp,
+                                                      unsigned long long* partials) {
+  __shared__ int32_t s_off[kTile + 1];
+  __shared__ int64_t s_rs[kTile];
+  __shared__ int32_t s_row[kTile];
+  __shared__ uint8_t s_hit[kTile];
+  __shared__ int64_t s_hdr[2];
+  __shared__ unsigned long long lds[kSlots * 16];
+  unsigned long long acc[4] = {0, 0, 0, 0};
+  const int64_t E = off[nF];
+  const int64_t ntiles = (E + kTile - 1) / kTile;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t e0 = t * kTile;
+    const int64_t e1 = min(e0 + int64_t(kTile), E);
+    if (threadIdx.x == 0) {
+      int64_t lo = 0, hi = nF;
+      while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (off[mid] <= e0) lo = mid; else hi = mid;
+      }
+      const int64_t i0 = lo;
+      hi = nF;
+      while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (off[mid] <= e1 - 1) lo = mid; else hi = mid;
+      }
+      s_hdr[0] = i0;
+      s_hdr[1] = lo - i0 + 1;
+    }
+    __syncthreads();
+    const int64_t i0 = s_hdr[0];
+    const int cnt = int(s_hdr[1]);
+    for (int k = threadIdx.x; k <= cnt; k += kThreads) {
+      const int64_t o = off[i0 + k];
+      s_off[k] = int32_t(min(o - e0, int64_t(kTile + 1)));
+      if (k < cnt) {
+        const int32_t r = F[i0 + k];
+        s_row[k] = r;
+        s_rs[k] = trp[r] + K - o;
+        s_hit[k] = 0;
+      }
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (int q = 0; q < kItems; q++) {
+      const int j = threadIdx.x + q * kThreads;
+      const int64_t e = e0 + j;
+      if (e >= e1) continue;
+      int lo = 0, hi = cnt;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (s_off[mid] <= j) lo = mid; else hi = mid;
+      }
+      const int64_t ge = s_rs[lo] + e;
+      const int32_t sv = tcol[ge];
+      acc[2]++;
+      if ((fbits[sv >> 5] >> (sv & 31)) & 1u) {
+        bool h = true;
+        if (PK == PK_FAST) {
+          acc[3]++;
+          h = fast_cmp(fp.op, load_int(fp.data, fp.width, ge), fp.k);
+        }
+        if (h) s_hit[lo] = 1;
+      }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < cnt; k += kThreads) {
+      if (!s_hit[k]) continue;
+      const int32_t r = s_row[k];
+      const unsigned long long bit = 1ull << (r & 63);
+      const unsigned long long old = atomicOr(nbits + (r >> 6), bit);
+      if (!(old & bit)) {
+        acc[0]++;
+        acc[1] += odeg ? odeg[r] : 0u;
+      }
+    }
+    __syncthreads();
+  }
+  block_store_partials(acc, 4, lds, partials);
+}
+
+// remaining in-degree past the slab of each pending row; deg[nF] = 0
+__global__ void k_rest_deg(const int32_t* F, int64_t nF, const int64_t* trp, int K, int64_t* deg) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= nF; i += int64_t(gridDim.x) * blockDim.x) {
+    if (i == nF) {
+      deg[i] = 0;
+    } else {
+      const int32_t r = F[i];
+      deg[i] = max(int64_t(0), trp[r + 1] - trp[r] - K);
+    }
+  }
 }
 
 // Bottom-up hop writing the next frontier straight into a bitmap (one 64-bit ballot word per
@@ -1050,7 +1292,7 @@ void ensure_workspaces(Ctx& c, int64_t nF_cap) {
   c.ws_front[0].ensure(size_t(nF_cap + 64) * 4);
   c.ws_front[1].ensure(size_t(nF_cap + 64) * 4);
   c.ws_off.ensure(size_t(nF_cap + 2) * 8);
-  c.ws_counters.ensure(256);
+  c.ws_counters.ensure(512);
   c.ws_partials.ensure(size_t(kAggBlocks) * kSlots * 8);
   c.ws_bits_send.ensure(size_t(mb / 8 + 64));
   c.ws_bits_recv.ensure(size_t(mb / 8 + 64));
@@ -1232,7 +1474,7 @@ void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* 
   int64_t ntiles = ((n + 15) / 16 + 1023) / 1024;
   int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, kAggBlocks)));
   k_compact<<<grid, 256, 0, c.stream>>>(map, lo, n, row_ptr, row_ok, require_deg, out, Kd, partials, bits);
-  k_reduce_partials<<<1, 256, 0, c.stream>>>(partials, grid, Kd + 12);
+  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, Kd + 12);
   NBG_HIP(hipGetLastError());
 }
 
@@ -1259,26 +1501,99 @@ void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Progr
 // bottom-up hop over the slab: launches the kernel and the partials reduction into out[0..8)
 // (no synchronisation); returns the grid used
 int launch_bu_slab(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
-                   const FastArgs& fp, const void* slab_w, unsigned long long* out) {
-  constexpr int R = 2;
+                   const FastArgs& fp, const void* slab_w, unsigned long long* out,
+                   unsigned long long* pbits = nullptr) {
+  // rows per lane (R) and eagerly loaded slab slots (EAGER) are options (bu_r, bu_eager[_fast])
+  constexpr int R = 2;  // rows per lane
+  const int EG = int(c.opt(pk == PK_FAST ? "bu_eager_fast" : "bu_eager", 1));
   const Csr& tr = es.tr;
   unsigned long long* partials = c.ws_partials.as<unsigned long long>();
   const int64_t tiles = (tr.n_rows + 64 * R - 1) / (64 * R);
-  int grid = int(std::max<int64_t>(1, std::min<int64_t>((tiles + 3) / 4, std::min<int64_t>(c.opt("bu_grid", 4096), kAggBlocks))));
+  const int64_t per_wave = std::max<int64_t>(1, c.opt("bu_tiles_per_wave", 4));
+  int grid = int(std::max<int64_t>(
+      1, std::min<int64_t>((tiles + per_wave - 1) / per_wave, std::min<int64_t>(c.opt("bu_grid", 4096), kAggBlocks))));
+  // LDS copy of the bitmap's hub words (bu_lds_kb KiB, 0 = off): 1024-thread persistent blocks
+  const int64_t fb_words = (c.n_global + 31) / 32;
+  const int cw = int(std::min<int64_t>(c.opt("bu_lds_kb", 0) * 256, std::min<int64_t>(fb_words, 36 * 1024)));
+  int bs = 256;
+  if (cw > 0) {
+    bs = 1024;
+    grid = int(std::max<int64_t>(1, std::min<int64_t>((tiles + 16 * per_wave - 1) / (16 * per_wave),
+                                                      std::min<int64_t>(c.opt("bu_lds_grid", 512), kAggBlocks))));
+  }
   auto* nb = reinterpret_cast<unsigned long long*>(nbits);
   const int32_t* sc = es.slab_col.as<int32_t>();
   const int64_t* trp = tr.row_ptr.as<int64_t>();
   const int32_t* tc = tr.col.as<int32_t>();
-  if (pk == PK_FAST)
-    k_bu_slab<PK_FAST, 4, R><<<grid, 256, 0, c.stream>>>(sc, slab_w, es.slab_k, trp, tc, tr.n_rows, fb, nb, odeg, fp,
-                                                         partials);
-  else
-    k_bu_slab<PK_NONE, 1, R><<<grid, 256, 0, c.stream>>>(sc, slab_w, es.slab_k, trp, tc, tr.n_rows, fb, nb, odeg, fp,
-                                                         partials);
-  k_reduce_partials<<<1, 256, 0, c.stream>>>(partials, grid, out);
+  const int nt = int(c.opt("bu_nt", 0));  // non-temporal slab / out-degree loads (keep L2 for the bitmap)
+#define NBG_BU(PKV, EV, WV)                                                                             \
+  k_bu_slab<PKV, EV, 2, WV><<<grid, bs, size_t(cw) * 4, c.stream>>>(sc, slab_w, es.slab_k, trp, tc, tr.n_rows, fb, nb, \
+                                                                    odeg, fp, partials, nt, pbits, cw)
+#define NBG_BU_W(EV)                      \
+  switch (fp.width) {                     \
+    case 1: NBG_BU(PK_FAST, EV, 1); break; \
+    case 2: NBG_BU(PK_FAST, EV, 2); break; \
+    case 4: NBG_BU(PK_FAST, EV, 4); break; \
+    default: NBG_BU(PK_FAST, EV, 8); break; \
+  }
+  if (pk == PK_FAST) {
+    switch (EG) {
+      case 1: NBG_BU_W(1); break;
+      case 2: NBG_BU_W(2); break;
+      default: NBG_BU_W(4); break;
+    }
+  } else {
+    switch (EG) {
+      case 2: NBG_BU(PK_NONE, 2, 0); break;
+      default: NBG_BU(PK_NONE, 1, 0); break;
+    }
+  }
+#undef NBG_BU_W
+#undef NBG_BU
+  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, out);
   NBG_HIP(hipGetLastError());
   return grid;
 }
+// Second pass of a deferred slab hop (h: the first pass's reduced counters on the host, h[3] =
+// pending rows).  Adds the rows it finds into h[0] / h[1] and its reads into h[4] / h[5], so the
+// counters read as one hop.  Synchronises once.
+void bu_finish(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
+               const FastArgs& fp, const unsigned long long* pbits, unsigned long long* h, unsigned long long* Kd) {
+  const int64_t P = int64_t(h[3]);
+  if (P <= 0) return;
+  const Csr& tr = es.tr;
+  DevBuf lst, deg, off;
+  lst.alloc(size_t(P + 64) * 4);
+  deg.alloc(size_t(P + 1) * 8);
+  off.alloc(size_t(P + 1) * 8);
+  NBG_HIP(hipMemsetAsync(Kd, 0, 8, c.stream));
+  k_bits_compact<0><<<grid_cap((tr.n_rows + 31) / 32, 1024, 4096), 256, 0, c.stream>>>(
+      reinterpret_cast<const uint32_t*>(pbits), tr.n_rows, 0, nullptr, lst.as<int32_t>(), Kd);
+  k_rest_deg<<<grid_cap(P + 1), 256, 0, c.stream>>>(lst.as<int32_t>(), P, tr.row_ptr.as<int64_t>(), es.slab_k,
+                                                    deg.as<int64_t>());
+  exclusive_scan_dev<int64_t>(c, deg.as<int64_t>(), off.as<int64_t>(), P + 1);
+  unsigned long long* partials = c.ws_partials.as<unsigned long long>();
+  const int grid = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("rest_grid", 2048), kAggBlocks)));
+  if (pk == PK_FAST)
+    k_bu_rest<PK_FAST><<<grid, kThreads, 0, c.stream>>>(lst.as<int32_t>(), P, off.as<int64_t>(),
+                                                        tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), es.slab_k, fb,
+                                                        reinterpret_cast<unsigned long long*>(nbits), odeg, fp, partials);
+  else
+    k_bu_rest<PK_NONE><<<grid, kThreads, 0, c.stream>>>(lst.as<int32_t>(), P, off.as<int64_t>(),
+                                                        tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), es.slab_k, fb,
+                                                        reinterpret_cast<unsigned long long*>(nbits), odeg, fp, partials);
+  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, Kd + 1);
+  NBG_HIP(hipGetLastError());
+  NBG_HIP(hipMemcpyAsync(c.host_counters + 40, Kd, 8 * 6, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  if (int64_t(c.host_counters[40]) != P) throw Error(NBG_E_DEVICE, "bottom-up pending-row count mismatch");
+  const unsigned long long* r = c.host_counters + 41;
+  h[0] += r[0];
+  h[1] += r[1];
+  h[4] += r[2];
+  h[5] += r[3];
+}
+
 // byte model of one slab hop from its counters
 uint64_t bu_slab_bytes(const unsigned long long* h, int64_t n_rows, int pred_width, bool with_odeg) {
   return h[2] * (4 + uint64_t(pred_width)) + h[3] * 16 + h[4] * 4 + h[5] * uint64_t(pred_width) +
@@ -1494,18 +1809,25 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // bottom-up: frontier bitmap in, next frontier bitmap out
       const Csr& tr = es.tr;
       const uint32_t* fb = global_bits(c, bitsA);
+      const bool defer = c.opt("bu_defer", 0) != 0;
+      DevBuf pb;
+      if (defer) pb.alloc(size_t((tr.n_rows + 63) / 64 + 1) * 8);
       hipEventRecord(c.ev[2], c.stream);
-      launch_bu_slab(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, nullptr, K.d);
-      hipEventRecord(c.ev[3], c.stream);
+      launch_bu_slab(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, nullptr, K.d,
+                     defer ? pb.as<unsigned long long>() : nullptr);
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 64, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipEventSynchronize(c.ev[3]));
       NBG_HIP(hipStreamSynchronize(c.stream));
+      if (defer) bu_finish(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, pb.as<unsigned long long>(), K.h,
+                           K.d + 40);
+      hipEventRecord(c.ev[3], c.stream);
+      NBG_HIP(hipEventSynchronize(c.ev[3]));
       float ms = 0;
       hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
       c.timing.expand_ms += ms;
       c.timing.expand_launches++;
       c.timing.bu_steps++;
       c.timing.expand_bytes += bu_slab_bytes(K.h, tr.n_rows, 0, true);
+      c.timing.hop(1, false, ms, K.h);
       std::swap(bitsA, bitsB);
       have_list = false;
       off_ready = false;
@@ -1520,10 +1842,13 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       a.F = F;
       a.nF = nF;
       a.off = c.ws_off.as<int64_t>();
+      const double ms0 = c.timing.expand_ms;
       if (E > 0) {
         launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, E);
         c.timing.expand_bytes += expand_bytes(nF, E, 0, EXP_MARK);
       }
+      const unsigned long long hs[6] = {(unsigned long long)nF, (unsigned long long)E, 0, 0, 0, 0};
+      c.timing.hop(0, false, c.timing.expand_ms - ms0, hs);
       exchange_marks(c, map);
       // next frontier = set of dsts (P12): compact, drop rows without out-edges, bitmap too
       cur ^= 1;
@@ -1582,8 +1907,19 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         NBG_HIP(hipMemsetAsync(K.d, 0, 8, c.stream));
         const uint32_t* fb = global_bits(c, bitsA);
         const void* slab_w = pk == PK_FAST ? es.slab_props[size_t(fpk.col)].p : nullptr;
+        const bool defer = c.opt("bu_defer", 0) != 0;
+        DevBuf pb;
+        if (defer) pb.alloc(size_t((tr.n_rows + 63) / 64 + 1) * 8);
         hipEventRecord(c.ev[2], c.stream);
-        launch_bu_slab(c, es, fb, bitsB, nullptr, pk, tfp, slab_w, K.d + 8);
+        launch_bu_slab(c, es, fb, bitsB, nullptr, pk, tfp, slab_w, K.d + 8,
+                       defer ? pb.as<unsigned long long>() : nullptr);
+        unsigned long long h2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (defer) {
+          NBG_HIP(hipMemcpyAsync(K.h + 8, K.d + 8, 64, hipMemcpyDeviceToHost, c.stream));
+          NBG_HIP(hipStreamSynchronize(c.stream));
+          memcpy(h2, K.h + 8, sizeof(h2));
+          bu_finish(c, es, fb, bitsB, nullptr, pk, tfp, pb.as<unsigned long long>(), h2, K.d + 40);
+        }
         k_bits_compact<1><<<grid_cap((tr.n_rows + 31) / 32, 1024, 4096), 256, 0, c.stream>>>(
             bitsB, tr.n_rows, lo, c.vid_of.as<int64_t>(), vids.p, K.d);
         NBG_HIP(hipGetLastError());
@@ -1596,17 +1932,22 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         c.timing.expand_launches++;
         c.timing.bu_steps++;
         nrows = int64_t(K.h[0]);
+        if (defer) memcpy(K.h + 8, h2, sizeof(h2));
         c.timing.expand_bytes += bu_slab_bytes(K.h + 8, tr.n_rows, pk == PK_FAST ? tfp.width : 0, false) +
                                  uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
+        c.timing.hop(1, true, ms, K.h + 8);
       } else {
         ensure_off();
         a.F = F;
         a.nF = nF;
         a.off = c.ws_off.as<int64_t>();
+        const double ms0 = c.timing.expand_ms;
         if (E > 0) {
           launch_expand<EXP_MARK>(c, a, pk, fp, dprog.as<Program>(), env, E);
           c.timing.expand_bytes += expand_bytes(nF, E, pred_w, EXP_MARK);
         }
+        const unsigned long long hs[6] = {(unsigned long long)nF, (unsigned long long)E, 0, 0, 0, 0};
+        c.timing.hop(0, true, c.timing.expand_ms - ms0, hs);
         exchange_marks(c, map);
         DevBuf lst;
         lst.alloc(size_t(n_own + 64) * 4);
@@ -1637,10 +1978,13 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       a.rows_src = rows_src;
       a.rows_cnt = K.d + 2;
       NBG_HIP(hipMemsetAsync(K.d, 0, 48, c.stream));
+      const double ms0 = c.timing.expand_ms;
       if (E > 0) {
         launch_expand<EXP_ROWS>(c, a, pk, fp, dprog.as<Program>(), env, E);
         c.timing.expand_bytes += expand_bytes(nF, E, pred_w, EXP_ROWS);
       }
+      const unsigned long long hs[6] = {(unsigned long long)nF, (unsigned long long)E, 0, 0, 0, 0};
+      c.timing.hop(0, true, c.timing.expand_ms - ms0, hs);
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
       int64_t errs = int64_t(K.h[4]);

@@ -180,7 +180,10 @@ class GraphSpace:
     def last_timing(self) -> dict:
         t = _lib.Timing()
         self._check(self.L.nbg_last_timing(self.h, C.byref(t)))
-        return {k: getattr(t, k) for k, _ in t._fields_}
+        d = {k: getattr(t, k) for k, _ in t._fields_ if k not in ("hops", "n_hops")}
+        d["hops"] = [{"mode": "bottom-up" if h.mode else "top-down", "final": bool(h.final_hop), "ms": h.ms,
+                      "bytes": int(h.bytes), "c": list(h.c)} for h in t.hops[:t.n_hops]]
+        return d
 
     # ---- queries ---------------------------------------------------------------------
     def get_bound(self, edge_type: int, parts, vids, return_columns, filter: bytes | X.Expr | None = b"") -> RowSet:

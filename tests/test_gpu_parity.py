@@ -400,3 +400,30 @@ def test_rmat_bottom_up_slab_widths(slab, order):
             assert g.edges_scanned == r.edges_scanned
     assert sp.last_timing()["bu_steps"] > 0
     sp.close()
+
+
+@pytest.mark.parametrize("defer,r,eager", [(1, 2, 4), (0, 2, 4), (1, 1, 1), (1, 4, 2), (0, 4, 1)])
+def test_rmat_bottom_up_rest_pass(rmat12, defer, r, eager):
+    """rows that outlive the slab: the deferred edge-balanced second pass (k_bu_rest) and the
+    inline wave scan agree with the oracle for every lane/slot shape of k_bu_slab"""
+    sp, st = rmat12
+    opts = {"bu_force": 1, "bu_defer": defer, "bu_r": r, "bu_eager_fast": eager, "bu_eager": min(eager, 2)}
+    for k, v in opts.items():
+        sp.set_option(k, v)
+    try:
+        starts = sorted(set(seeds_from(12, 48, seed=21)))
+        for k in (0, 499, 990):
+            w = X.AliasProp("follow", "weight") > k
+            for steps in (2, 3):
+                g = sp.go(starts, steps, FOLLOW, where=w, yields=[X.EdgeDst("follow")], distinct=True)
+                r_ = st.go(starts, steps, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()],
+                           distinct=True)
+                assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
+                assert g.edges_scanned == r_.edges_scanned
+                hops = sp.last_timing()["hops"]
+                assert any(h["mode"] == "bottom-up" for h in hops)
+        # the high threshold leaves rows pending past the slab, so the rest pass really ran
+        assert any(h["mode"] == "bottom-up" and h["c"][3] > 0 for h in hops)
+    finally:
+        for k, v in {"bu_force": 0, "bu_defer": 0, "bu_r": 2, "bu_eager_fast": 1, "bu_eager": 1}.items():
+            sp.set_option(k, v)

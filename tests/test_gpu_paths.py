@@ -161,3 +161,23 @@ def test_list_overflow_recovery():
     again = sp.shortest_path(t, s, FOLLOW, 7).rows()  # bytes were reset after the overflowed batch
     assert again == oracle_paths(st, t, s, FOLLOW, 7)
     sp.close()
+
+
+@pytest.mark.parametrize("probe,vmajor", [(0, 1), (1, 1), (1, 0), (0, 0)])
+def test_meet_probe_on_and_off_match_oracle(rmat, probe, vmajor):
+    """the early-exit meet probe (pairs one edge short of meeting skip the expansion) and the
+    plain level-by-level expansion, over vertex-major and pair-major distance bytes, give the
+    oracle's hop counts and canonical paths"""
+    scale, sp, st = rmat
+    sp.set_option("sp_probe", probe)
+    sp.set_option("sp_vmajor", vmajor)
+    try:
+        s, t = synth.pairs(scale, 16, 1, 300, pick_seed=17)
+        es, et_ = edge_case_pairs(scale)
+        src, dst = np.concatenate([s, es]), np.concatenate([t, et_])
+        for max_steps in (2, 8):
+            got = sp.shortest_path(src, dst, FOLLOW, max_steps).rows()
+            assert got == oracle_paths(st, src, dst, FOLLOW, max_steps)
+    finally:
+        sp.set_option("sp_probe", 1)
+        sp.set_option("sp_vmajor", 0)
