@@ -19,6 +19,8 @@ import sys
 import time
 from pathlib import Path
 
+import numpy as np
+
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
@@ -112,12 +114,16 @@ def cpu_baseline_paths(scale: int, npairs: int, max_steps: int):
                       f"in {dt:.2f}s"}
 
 
-def bench_paths(args, sp, info, build_s, rank, world):
-    """BASELINE.json configs[3]: FIND SHORTEST PATH, 1024 (src, dst) pairs on RMAT-26."""
+def bench_paths(args, sp, info, build_s, rank, world, dist=None):
+    """BASELINE.json configs[3]: FIND SHORTEST PATH, 1024 (src, dst) pairs on RMAT-26.  With
+    world > 1 the pairs are sharded i % world over the ranks (each answers its own against the
+    replicated CSRs, no collective in the timed region): strong scaling of a fixed pair set."""
     from nebula_amd import synth
     s, t = synth.pairs(args.scale, args.edge_factor, 1, args.pairs)
     for _ in range(args.warmup):
         sp.shortest_path(s, t, 1, args.max_steps)
+    if dist is not None:
+        dist.barrier()
     t0 = time.perf_counter()
     edges = 0
     exp_ms = exp_bytes = dev_ms = 0.0
@@ -130,8 +136,21 @@ def bench_paths(args, sp, info, build_s, rank, world):
         exp_bytes += tm["expand_bytes"]
         dev_ms += tm["total_ms"]
         iters = tm["steps_run"]
+    if dist is not None:
+        dist.barrier()
     dt = time.perf_counter() - t0
     hops = r.hops
+    if dist is not None:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        te = torch.tensor([edges], dtype=torch.int64)
+        dist.all_reduce(te, op=dist.ReduceOp.SUM)
+        edges = int(te.item())
+        hl = [None] * world
+        dist.all_gather_object(hl, hops.tolist())
+        hops = np.array([h for part in hl for h in part], dtype=np.int64)
     achieved = exp_bytes / (exp_ms / 1e3) / 1e9 if exp_ms > 0 else 0.0
     out = {
         "metric": "FIND SHORTEST PATH pairs/s (batched bidirectional BFS) on RMAT-26",
@@ -147,6 +166,7 @@ def bench_paths(args, sp, info, build_s, rank, world):
         "dtype": "int64",
         "data": "synthetic RMAT (Graph500 a/b/c=0.57/0.19/0.19, seed 1) generated on device",
         "config": {
+            "parallelism": f"pairs sharded i % {world} over the ranks, replicated CSRs" if world > 1 else "1 GPU",
             "workload": f"FIND SHORTEST PATH {args.pairs} pairs UPTO {args.max_steps} STEPS OVER follow; "
                         f"RMAT-{args.scale} ef{args.edge_factor}",
             "vertices": info["num_vertices"],
@@ -164,7 +184,7 @@ def bench_paths(args, sp, info, build_s, rank, world):
         },
         "cpu_baseline": None,
     }
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:
         try:
             out["cpu_baseline"] = cpu_baseline_paths(args.cpu_scale, 64, args.max_steps)
         except Exception as e:
@@ -222,7 +242,7 @@ def main():
     build_s = time.time() - t0
     info = sp.info(FOLLOW)
     if args.workload == "paths":
-        return bench_paths(args, sp, info, build_s, rank, world)
+        return bench_paths(args, sp, info, build_s, rank, world, dist)
     starts = synth.seeds(args.scale, args.edge_factor, 1, args.seeds)
     where = X.AliasProp("follow", "weight") > args.where
     yields = [X.EdgeDst("follow")]

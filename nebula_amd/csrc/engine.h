@@ -197,6 +197,10 @@ struct EdgeSpace {
   std::vector<Field> fields;
   Staging out_stage, in_stage;
   Csr out, in;
+  // world > 1: replicas of every rank's out / in CSR over the whole gidx space (built on the
+  // first FIND SHORTEST PATH, which shards its pairs over the ranks)
+  Csr rep_out, rep_in;
+  bool has_rep = false;
   // Transpose of the out CSR for bottom-up steps: row = owned dst, col = global src index,
   // props = copies of the INT-like out props in transpose order, t_eid = out-edge index.
   Csr tr;

@@ -619,17 +619,106 @@ void reserve(Ctx& c, DevBuf& b, int64_t& cap, int64_t need, int64_t keep) {
 
 }  // namespace
 
-int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t* dst, size_t npairs, int32_t max_steps,
-                          nbg_rows* out) {
+// ---- world > 1: the pairs are independent, so they are sharded over the ranks (pair i on rank
+// i % world) and every rank answers its own pairs against a replica of the whole graph's out / in
+// CSRs.  The replicas are assembled once with allgathers of every rank's rows (the rows of rank r
+// are the gidx range [base[r], base[r+1])); the traversal itself exchanges nothing.
+__global__ void k_add_i64(int64_t* a, int64_t n, int64_t v) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    a[i] += v;
+}
+
+static void replicate_csr(Ctx& c, const Csr& loc, Csr& rep) {
+  const int W = c.world;
+  PoolScope none(nullptr);
+  DevBuf dm, dall, ok_loc, flag;
+  dm.alloc(16);
+  dall.alloc(size_t(W) * 16);
+  int64_t mine[2] = {loc.nnz, loc.row_ok.p ? 1 : 0};
+  NBG_HIP(hipMemcpyAsync(dm.p, mine, 16, hipMemcpyHostToDevice, c.stream));
+  comm_allgather_bytes(c, dm.p, 16, dall.p);
+  std::vector<int64_t> all(size_t(W) * 2);
+  NBG_HIP(hipMemcpyAsync(all.data(), dall.p, size_t(W) * 16, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  std::vector<int64_t> nnz_off(size_t(W) + 1, 0);
+  bool any_ok = false;
+  for (int r = 0; r < W; r++) {
+    nnz_off[size_t(r) + 1] = nnz_off[size_t(r)] + all[size_t(r) * 2];
+    any_ok = any_ok || all[size_t(r) * 2 + 1] != 0;
+  }
+  const int64_t N = c.n_global;
+  rep.n_rows = N;
+  rep.nnz = nnz_off[size_t(W)];
+  rep.col.alloc(size_t(rep.nnz + 16) * 4);
+  rep.row_ptr.alloc(size_t(N + 1) * 8);
+  std::vector<size_t> rb(static_cast<size_t>(W)), ro(static_cast<size_t>(W));
+  for (int r = 0; r < W; r++) {
+    rb[size_t(r)] = size_t(all[size_t(r) * 2]) * 4;
+    ro[size_t(r)] = size_t(nnz_off[size_t(r)]) * 4;
+  }
+  comm_allgatherv_bytes(c, loc.col.p, size_t(loc.nnz) * 4, rep.col.p, rb.data(), ro.data());
+  for (int r = 0; r < W; r++) {
+    rb[size_t(r)] = size_t(c.base[size_t(r) + 1] - c.base[size_t(r)]) * 8;
+    ro[size_t(r)] = size_t(c.base[size_t(r)]) * 8;
+  }
+  comm_allgatherv_bytes(c, loc.row_ptr.p, size_t(loc.n_rows) * 8, rep.row_ptr.p, rb.data(), ro.data());
+  for (int r = 0; r < W; r++) {  // local row offsets -> offsets into the concatenated col
+    const int64_t a = c.base[size_t(r)], m = c.base[size_t(r) + 1] - a;
+    if (m > 0 && nnz_off[size_t(r)] > 0)
+      k_add_i64<<<grid_n(m), 256, 0, c.stream>>>(rep.row_ptr.as<int64_t>() + a, m, nnz_off[size_t(r)]);
+  }
+  NBG_HIP(hipMemcpyAsync(rep.row_ptr.as<int64_t>() + N, &nnz_off[size_t(W)], 8, hipMemcpyHostToDevice, c.stream));
+  if (any_ok) {  // rows whose keys sit outside hash(vid)'s part stay invisible on every replica
+    ok_loc.alloc(size_t(loc.n_rows) + 64);
+    if (loc.row_ok.p)
+      NBG_HIP(hipMemcpyAsync(ok_loc.p, loc.row_ok.p, size_t(loc.n_rows), hipMemcpyDeviceToDevice, c.stream));
+    else
+      NBG_HIP(hipMemsetAsync(ok_loc.p, 1, size_t(loc.n_rows), c.stream));
+    rep.row_ok.alloc(size_t(N) + 64);
+    for (int r = 0; r < W; r++) {
+      rb[size_t(r)] = size_t(c.base[size_t(r) + 1] - c.base[size_t(r)]);
+      ro[size_t(r)] = size_t(c.base[size_t(r)]);
+    }
+    comm_allgatherv_bytes(c, ok_loc.p, size_t(loc.n_rows), rep.row_ok.p, rb.data(), ro.data());
+  }
+  NBG_HIP(hipGetLastError());
+  NBG_HIP(hipStreamSynchronize(c.stream));
+}
+
+int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int64_t* dst_all, size_t npairs_all,
+                          int32_t max_steps, nbg_rows* out) {
   if (!c.finalized) throw Error(NBG_E_STATE, "snapshot not finalized");
   if (et <= 0) throw Error(NBG_E_INVALID_ARG, "edge type must be > 0 (paths follow out-edges)");
   if (max_steps > 254) throw Error(NBG_E_UNSUPPORTED, "max_steps above 254");
-  if (c.world > 1) throw Error(NBG_E_UNSUPPORTED, "sharded FIND SHORTEST PATH is not built yet (one rank only)");
   auto it = c.edges.find(et);
   if (it == c.edges.end()) throw Error(NBG_E_INVALID_ARG, "edge type not in snapshot");
   EdgeSpace& es = it->second;
-  const int64_t lo = c.owned_lo(), n = std::max<int64_t>(c.owned_hi() - lo, 1);
   if (!es.out.row_ptr.p || !es.in.row_ptr.p) throw Error(NBG_E_STATE, "missing CSR");
+  const Csr* cout = &es.out;
+  const Csr* cin = &es.in;
+  int64_t lo = c.owned_lo(), n = std::max<int64_t>(c.owned_hi() - lo, 1);
+  const int64_t* src = src_all;
+  const int64_t* dst = dst_all;
+  size_t npairs = npairs_all;
+  std::vector<int64_t> my_src, my_dst;
+  if (c.world > 1) {
+    if (!es.has_rep) {
+      replicate_csr(c, es.out, es.rep_out);
+      replicate_csr(c, es.in, es.rep_in);
+      es.has_rep = true;
+    }
+    cout = &es.rep_out;
+    cin = &es.rep_in;
+    lo = 0;
+    n = std::max<int64_t>(c.n_global, 1);
+    for (size_t i = size_t(c.rank); i < npairs_all; i += size_t(c.world)) {
+      my_src.push_back(src_all[i]);
+      my_dst.push_back(dst_all[i]);
+    }
+    src = my_src.data();
+    dst = my_dst.data();
+    npairs = my_src.size();
+  }
 
   // batch size: bounded by the distance arrays' HBM budget (2 bytes per pair and vertex)
   const int64_t budget = c.opt("sp_mem_mb", 96 * 1024) << 20;
@@ -666,8 +755,8 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t*
 
   uint8_t* d0 = c.sp_dist[0].as<uint8_t>();
   uint8_t* d1 = c.sp_dist[1].as<uint8_t>();
-  SpCsr gout{es.out.row_ptr.as<int64_t>(), es.out.col.as<int32_t>(), es.out.row_ok.as<uint8_t>()};
-  SpCsr gin{es.in.row_ptr.as<int64_t>(), es.in.col.as<int32_t>(), es.in.row_ok.as<uint8_t>()};
+  SpCsr gout{cout->row_ptr.as<int64_t>(), cout->col.as<int32_t>(), cout->row_ok.as<uint8_t>()};
+  SpCsr gin{cin->row_ptr.as<int64_t>(), cin->col.as<int32_t>(), cin->row_ok.as<uint8_t>()};
   const int64_t* vid_of = c.vid_of.as<int64_t>();
   unsigned long long* cnt = W.cnt.as<unsigned long long>();
   unsigned long long* hc = c.host_counters;  // pinned

@@ -242,7 +242,10 @@ class GraphSpace:
             tot = int(off[-1])
             vids = (np.ctypeslib.as_array(rows.path_vids, shape=(tot,)).copy() if tot else np.zeros(0, np.int64))
             paths = [vids[off[i]:off[i + 1]] for i in range(n)]
-            return PathResult(src.copy(), dst.copy(), hops, paths, int(rows.edges_scanned))
+            # with world_size > 1 this rank answers pairs rank, rank + world, ... (columns 0 / 1)
+            rs = np.ctypeslib.as_array(C.cast(rows.cols[0], C.POINTER(C.c_int64)), shape=(n,)).copy() if n else src[:0]
+            rd = np.ctypeslib.as_array(C.cast(rows.cols[1], C.POINTER(C.c_int64)), shape=(n,)).copy() if n else dst[:0]
+            return PathResult(rs, rd, hops, paths, int(rows.edges_scanned))
         finally:
             self.L.nbg_rows_free(C.byref(rows))
 

@@ -220,3 +220,25 @@ def test_sharded_kv_ingest(oracle12):
         assert union_rows(bound) == ms(ref.rows())
     finally:
         g.close()
+
+
+def test_sharded_shortest_path(rmat_group, oracle12):
+    """FIND SHORTEST PATH with world > 1: pairs sharded i % world over the ranks, each answered
+    against the allgathered replica of the out / in CSRs; the union of the ranks' rows (and their
+    canonical paths) equals the oracle's"""
+    from nebula_amd import synth
+    g = rmat_group
+    s, t = synth.pairs(12, 16, SEED, 120, pick_seed=3)
+    src = np.concatenate([s, [s[0], -5]]).astype(np.int64)
+    dst = np.concatenate([t, [s[0], t[0]]]).astype(np.int64)
+    res = g.each(lambda r, sp: sp.shortest_path(src, dst, FOLLOW, 6))
+    got = Counter()
+    for r, pr in enumerate(res):
+        rows = pr.rows()
+        assert len(rows) == len(range(r, len(src), g.world))
+        got.update(rows)
+    want = Counter()
+    for row in oracle12.shortest_path(src, dst, FOLLOW, 6).rows():
+        row = [x for x in row if x is not None]
+        want[(row[0], row[1], row[2], tuple(row[3:]))] += 1
+    assert got == want
