@@ -161,6 +161,20 @@ int32_t nbg_get_bound(nbg_ctx* ctx, int32_t edge_type, const int32_t* parts,
                       const int64_t* vids, size_t n, const uint8_t* filter, size_t filter_len,
                       const nbg_prop_def* cols, size_t ncols, nbg_rows* out);
 
+/* ---- outBoundStats / inBoundStats ---------------------------------------------------------
+ * Replaces QueryStatsProcessor::process (src/storage/QueryStatsProcessor.cpp:16-125,
+ * StorageServiceHandler.cpp:40-53): the getBound scan with the same filter push-down, reduced
+ * on the device to one row.  stat_types[i] = cpp2::StatType of cols[i] (SUM 1, COUNT 2, AVG 3,
+ * storage.thrift:51-55).  Columns in request order: SUM -> INT (int64 sum), COUNT -> INT,
+ * AVG -> DOUBLE (sum / count, NaN without rows); in-bound requests skip edge props.  SUM / AVG
+ * over BOOL / STRING fail every part with E_IMPROPER_DATA_TYPE (validOperation,
+ * QueryBaseProcessor.inl:18-35); SUM / AVG over DOUBLE values return NBG_E_UNSUPPORTED (the
+ * reference's int64-initialised sum throws boost::bad_get).  SOURCE / DEST tag props:
+ * NBG_E_UNSUPPORTED in this version.                                                        */
+int32_t nbg_bound_stats(nbg_ctx* ctx, int32_t edge_type, const int32_t* parts, const int64_t* vids,
+                        size_t n, const uint8_t* filter, size_t filter_len, const nbg_prop_def* cols,
+                        const int32_t* stat_types, size_t ncols, nbg_rows* out);
+
 /* ---- GO N STEPS ---------------------------------------------------------------------------
  * Replaces GoExecutor's stepOut -> getNeighbors -> onStepOutResponse -> getDstIdsFromResp loop
  * and its final processFinalResult / setupInterimResult (src/graph/GoExecutor.cpp:80-106,

@@ -29,7 +29,7 @@ EXPORTS = [
     "nbg_comm_init_local",
     "nbg_part_of", "nbg_rank_of_part", "nbg_schema_set_edge", "nbg_snapshot_load_part",
     "nbg_snapshot_gen_rmat", "nbg_snapshot_finalize", "nbg_snapshot_info_get",
-    "nbg_snapshot_out_degree", "nbg_rows_free", "nbg_get_bound", "nbg_go", "nbg_shortest_path",
+    "nbg_snapshot_out_degree", "nbg_rows_free", "nbg_get_bound", "nbg_bound_stats", "nbg_go", "nbg_shortest_path",
     "nbg_last_timing", "nbg_set_option",
 ]
 
@@ -113,6 +113,7 @@ def load(path: str | os.PathLike | None = None):
         "nbg_snapshot_out_degree": (i64, [vp, i32, i64]),
         "nbg_rows_free": (None, [C.POINTER(Rows)]),
         "nbg_get_bound": (i32, [vp, i32, vp, vp, sz, vp, sz, C.POINTER(PropDef), sz, C.POINTER(Rows)]),
+        "nbg_bound_stats": (i32, [vp, i32, vp, vp, sz, vp, sz, C.POINTER(PropDef), vp, sz, C.POINTER(Rows)]),
         "nbg_go": (i32, [vp, C.POINTER(GoSpec), C.POINTER(Rows)]),
         "nbg_shortest_path": (i32, [vp, i32, vp, vp, sz, i32, C.POINTER(Rows)]),
         "nbg_last_timing": (i32, [vp, C.POINTER(Timing)]),

@@ -199,6 +199,17 @@ int32_t nbg_get_bound(nbg_ctx* ctx, int32_t edge_type, const int32_t* parts, con
   });
 }
 
+int32_t nbg_bound_stats(nbg_ctx* ctx, int32_t edge_type, const int32_t* parts, const int64_t* vids, size_t n,
+                        const uint8_t* filter, size_t filter_len, const nbg_prop_def* cols,
+                        const int32_t* stat_types, size_t ncols, nbg_rows* out) {
+  return guarded(ctx, [&](Ctx& c) {
+    if (!out || (n && (!parts || !vids)) || (ncols && (!cols || !stat_types)) || (filter_len && !filter))
+      throw Error(NBG_E_INVALID_ARG, "bad arguments");
+    memset(out, 0, sizeof(*out));
+    return nbg::get_bound_run(c, edge_type, parts, vids, n, filter, filter_len, cols, ncols, out, stat_types);
+  });
+}
+
 int32_t nbg_go(nbg_ctx* ctx, const nbg_go_spec* spec, nbg_rows* out) {
   return guarded(ctx, [&](Ctx& c) {
     if (!spec || !out || (spec->n_starts && !spec->starts) || (spec->where_len && !spec->where) ||

@@ -310,7 +310,7 @@ void lookup_gidx(Ctx& c, const int64_t* d_vids, int32_t* d_gidx, int64_t n);
 int32_t go_run(Ctx& c, const nbg_go_spec& spec, nbg_rows* out);
 int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* vids, size_t n,
                       const uint8_t* filter, size_t flen, const nbg_prop_def* cols, size_t ncols,
-                      nbg_rows* out);
+                      nbg_rows* out, const int32_t* stats = nullptr);
 int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t* dst, size_t n,
                           int32_t max_steps, nbg_rows* out);
 // comm.cpp

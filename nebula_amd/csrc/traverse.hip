@@ -2119,6 +2119,7 @@ struct BoundCol {
   int32_t kind;  // 0 prop, 1 _dst, 2 _src, 3 _rank, 4 _type
   int32_t prop;
   int32_t type;  // NBG_T_*
+  int32_t stat;  // outBoundStats: cpp2::StatType SUM 1 / COUNT 2 / AVG 3 (0: plain getBound)
   void* out;
   int64_t* str_len;  // STRING pass 1
 };
@@ -2163,6 +2164,46 @@ __global__ void k_bound_rows(const int64_t* kept_slots, const int64_t* owner, in
     }
   }
 }
+// outBoundStats / inBoundStats (QueryStatsProcessor.cpp:69-125, StatsCollector Collector.h:66-94):
+// over the kept edge slots, the int64 sum (wrapping, as the reference's int64 adds) and the count
+// of present values of column c.  acc[2c] = sum, acc[2c+1] = count.  Doubles only count (a double
+// reaching the reference's int64-initialised sum throws, reported by the caller).
+__global__ void k_bound_stats(const int64_t* kept_slots, const int64_t* owner, int64_t m, const int64_t* off,
+                              const int32_t* F, const int64_t* row_ptr, int64_t lo, EvalEnv env, BoundCol b,
+                              unsigned long long* acc) {
+  unsigned long long sum = 0, cnt = 0;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t k = owner[i];
+    const int32_t f = F[k];
+    const int64_t ge = row_ptr[f] + (kept_slots[i] - off[k]);
+    int64_t v = 0;
+    bool present = true;
+    switch (b.kind) {
+      case 1: v = env.vid_of[env.col[ge]]; break;
+      case 2: v = env.vid_of[lo + f]; break;
+      case 3: v = env.rank ? env.rank[ge] : 0; break;
+      case 4: v = env.etype; break;
+      default: {
+        const PropDev& p = env.props[b.prop];
+        present = !(p.present && !p.present[ge]);
+        if (present && p.type != NBG_T_STRING && p.type != NBG_T_DOUBLE && p.type != NBG_T_FLOAT &&
+            p.type != NBG_T_BOOL)
+          v = load_int(p.data, p.width, ge);
+      }
+    }
+    if (present) {
+      sum += (unsigned long long)v;
+      cnt++;
+    }
+  }
+  sum = wave_sum_u64(sum);
+  cnt = wave_sum_u64(cnt);
+  if ((threadIdx.x & 63) == 0 && cnt) {
+    atomicAdd(acc, sum);
+    atomicAdd(acc + 1, cnt);
+  }
+}
+
 __global__ void k_str_gather(const int64_t* ge, int64_t m, const int64_t* src_off, const uint8_t* src_bytes,
                              const int64_t* dst_off, uint8_t* dst) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
@@ -2177,7 +2218,7 @@ __global__ void k_clamp_len(int64_t* l, int64_t m) {
 }
 
 int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* vids, size_t n, const uint8_t* filter,
-                      size_t flen, const nbg_prop_def* cols, size_t ncols, nbg_rows* out) {
+                      size_t flen, const nbg_prop_def* cols, size_t ncols, nbg_rows* out, const int32_t* stats) {
   PoolScope pool_scope(c.pool);
   if (!c.finalized) throw Error(NBG_E_STATE, "snapshot not finalized");
   auto* h = new HostRows();
@@ -2226,6 +2267,14 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
       b.type = (t == NBG_T_FLOAT) ? NBG_T_DOUBLE : (t == NBG_T_VID || t == NBG_T_TIMESTAMP) ? NBG_T_INT : t;
     } else {
       continue;  // "InBound has none props, skip it!"
+    }
+    if (stats) {  // validOperation (QueryBaseProcessor.inl:18-35): SUM / AVG need a numeric column
+      b.stat = stats[i];
+      if (b.stat < 1 || b.stat > 3) {
+        delete h;
+        throw Error(NBG_E_INVALID_ARG, "stat type must be SUM 1, COUNT 2 or AVG 3");
+      }
+      if (b.stat != 2 && (b.type == NBG_T_BOOL || b.type == NBG_T_STRING)) return fail_all(NBG_E_IMPROPER_DATA_TYPE);
     }
     if (bc.n >= kMaxBoundCols) {
       delete h;
@@ -2336,6 +2385,51 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
   }
   owner.alloc(size_t(m + 1) * 8);
   geb.alloc(size_t(m + 1) * 8);
+  if (stats) {
+    // one row: per column SUM (INT) / COUNT (INT) / AVG (DOUBLE), in request order (retIndex)
+    DevBuf acc;
+    acc.alloc(size_t(2 * bc.n + 2) * 8);
+    NBG_HIP(hipMemsetAsync(acc.p, 0, size_t(2 * bc.n + 2) * 8, c.stream));
+    if (m) {
+      k_slot_owner<<<grid_cap(m), 256, 0, c.stream>>>(slots.as<int64_t>(), m, dcoff.as<int64_t>(), nF,
+                                                      owner.as<int64_t>());
+      for (int i = 0; i < bc.n; i++)
+        k_bound_stats<<<grid_cap(m, 256, 1024), 256, 0, c.stream>>>(slots.as<int64_t>(), owner.as<int64_t>(), m,
+                                                                    dcoff.as<int64_t>(), dcF.as<int32_t>(),
+                                                                    csr.row_ptr.as<int64_t>(), lo, env, bc.c[i],
+                                                                    acc.as<unsigned long long>() + 2 * i);
+      NBG_HIP(hipGetLastError());
+    }
+    std::vector<unsigned long long> ha(size_t(2 * bc.n + 2));
+    NBG_HIP(hipMemcpyAsync(ha.data(), acc.p, ha.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    hipEventRecord(c.ev[1], c.stream);
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    float sms = 0;
+    hipEventElapsedTime(&sms, c.ev[0], c.ev[1]);
+    c.timing.total_ms = sms;
+    for (int i = 0; i < bc.n; i++) {
+      const BoundCol& b = bc.c[i];
+      const int64_t sum = int64_t(ha[size_t(2 * i)]);
+      const int64_t cnt = int64_t(ha[size_t(2 * i + 1)]);
+      if (b.stat != 2 && b.type == NBG_T_DOUBLE && cnt > 0) {
+        delete h;
+        throw Error(NBG_E_UNSUPPORTED, "SUM/AVG over a double prop (the reference's int64 sum throws bad_get)");
+      }
+      h->types.push_back(b.stat == 3 ? NBG_T_DOUBLE : NBG_T_INT);
+      h->host.emplace_back(8);
+      if (b.stat == 3) {
+        const double avg = double(sum) / double(int32_t(cnt));  // count_ is int32 (CommonUtils.h:51)
+        memcpy(h->host.back().data(), &avg, 8);
+      } else {
+        const int64_t v = b.stat == 2 ? int64_t(int32_t(cnt)) : sum;
+        memcpy(h->host.back().data(), &v, 8);
+      }
+      h->str_off.push_back(nullptr);
+    }
+    for (auto& hc : h->host) h->cols.push_back(hc.data());
+    out->edges_scanned = uint64_t(E);
+    return finish(1);
+  }
   std::vector<DevBuf> dcols(size_t(bc.n));
   std::vector<DevBuf> slen(size_t(bc.n));
   for (int i = 0; i < bc.n; i++) {

@@ -206,6 +206,31 @@ class GraphSpace:
         finally:
             self.L.nbg_rows_free(C.byref(rows))
 
+    def bound_stats(self, edge_type: int, parts, vids, return_columns, stats,
+                    filter: bytes | X.Expr | None = b"") -> RowSet:
+        """outBoundStats / inBoundStats: one row, stats[i] = SUM 1 / COUNT 2 / AVG 3 of column i."""
+        parts = np.ascontiguousarray(parts, dtype=np.int32)
+        vids = np.ascontiguousarray(vids, dtype=np.int64)
+        f = X.encode(filter)
+        fb = np.frombuffer(f + b"\0", dtype=np.uint8)
+        arr = (_lib.PropDef * max(len(return_columns), 1))()
+        keep = []
+        for i, col in enumerate(return_columns):
+            name, owner, tag = (col if isinstance(col, tuple) else (col, _lib.OWNER_EDGE, 0))
+            b = name.encode()
+            keep.append(b)
+            arr[i] = _lib.PropDef(b, owner, tag)
+        st = np.ascontiguousarray(list(stats) + [0], dtype=np.int32)
+        if len(st) - 1 != len(return_columns):
+            raise ValueError("one stat type per return column")
+        rows = _lib.Rows()
+        self._check(self.L.nbg_bound_stats(self.h, edge_type, _p(parts), _p(vids), len(vids), _p(fb), len(f),
+                                           arr, _p(st), len(return_columns), C.byref(rows)))
+        try:
+            return RowSet(rows)
+        finally:
+            self.L.nbg_rows_free(C.byref(rows))
+
     def go(self, starts, steps: int, edge_type: int, where=None, yields: Iterable = (), distinct: bool = False,
            keep_on_device: bool = False) -> RowSet:
         starts = np.ascontiguousarray(starts, dtype=np.int64)
@@ -321,6 +346,45 @@ class QueryBoundProcessor:
             verts.append(VertexData(int(vid), rows[a:b]))
         names = [c.name for c in req.return_columns if c.owner == _lib.OWNER_EDGE]
         return QueryResponse([{"part_id": p, "code": c} for p, c in rs.failed], list(zip(names, rs.types)), verts)
+
+
+SUM, COUNT, AVG = 1, 2, 3  # storage::cpp2::StatType (storage.thrift:51-55)
+
+
+@dataclass
+class QueryStatsResponse:
+    """storage::cpp2::QueryStatsResponse (storage.thrift:95-99): schema + one row of stats."""
+    failed_codes: list
+    schema: list
+    row: tuple | None
+
+
+class QueryStatsProcessor:
+    """QueryStatsProcessor::instance(...) / process(req) (QueryStatsProcessor.h, StorageServiceHandler.cpp:40-53).
+    The request's PropDefs carry their stat (storage.thrift:43-49): pass them as (PropDef, stat)."""
+
+    def __init__(self, space: GraphSpace, bound_type: int = OUT_BOUND):
+        self.space, self.bound_type = space, bound_type
+
+    @classmethod
+    def instance(cls, space: GraphSpace, bound_type: int = OUT_BOUND):
+        return cls(space, bound_type)
+
+    def process(self, req: GetNeighborsRequest) -> QueryStatsResponse:
+        parts, vids = [], []
+        for p, vs in req.parts.items():
+            parts += [p] * len(vs)
+            vids += list(vs)
+        cols = [(c.name, c.owner, c.tag_id) for c, _ in req.return_columns]
+        stats = [st for _, st in req.return_columns]
+        et = req.edge_type if self.bound_type == OUT_BOUND else -req.edge_type
+        rs = self.space.bound_stats(et, parts, vids, cols, stats, req.filter)
+        kept = [c.name for c, _ in req.return_columns
+                if self.bound_type == OUT_BOUND or c.owner != _lib.OWNER_EDGE or c.name.startswith("_")]
+        failed = [{"part_id": p, "code": c} for p, c in rs.failed]
+        if rs.n_rows == 0:
+            return QueryStatsResponse(failed, [], None)
+        return QueryStatsResponse(failed, list(zip(kept, rs.types)), rs.rows()[0])
 
 
 class GoExecutor:

@@ -806,6 +806,15 @@ struct PropCtx {
   bool returned = false;
   bool filtered = false;
   std::string tagOrEdgeName;
+  // QueryStatsProcessor state (CommonUtils.h:50-53): the request's stat, the column's position
+  // in the request, and the collector's sum / count.  sum_ is boost::variant<int64_t, double>
+  // initialised to int64 0, so collectDouble's boost::get<double>(sum_) throws (bad_get): kept
+  // as a flag.
+  int32_t stat = 0;
+  int retIndex = -1;
+  mutable int64_t sum = 0;
+  mutable int32_t count = 0;
+  mutable bool badGet = false;
 };
 struct TagCtx {
   int32_t tagId = 0;
@@ -819,6 +828,8 @@ struct FilterCtx {
 struct BoundProcessor {
   const ora_store* st;
   bool outBound;
+  bool stats = false;            // QueryStatsProcessor instead of QueryBoundProcessor
+  const int32_t* statTypes = nullptr;
   int32_t edgeType = 0;
   std::vector<TagCtx> tagCtxs;
   std::vector<PropCtx> edgeProps;
@@ -831,16 +842,20 @@ struct BoundProcessor {
                                 const uint8_t* filter, size_t flen) {
     edgeType = et;
     std::unordered_map<int32_t, size_t> tagIndex;
+    int index = 0;
     for (size_t i = 0; i < ncols; i++) {
       PropCtx prop;
       prop.name = cols[i].name;
       prop.owner = cols[i].owner;
+      prop.stat = statTypes ? statTypes[i] : 0;
       if (cols[i].owner == SOURCE || cols[i].owner == DEST) {
         auto schema = latestTagSchema(st, cols[i].tag_id);
         if (!schema) return E_TAG_PROP_NOT_FOUND;
         int fi = schema->fieldIndex(prop.name);
         if (fi < 0) return E_IMPROPER_DATA_TYPE;
         prop.type = schema->fields[size_t(fi)].type;
+        if (prop.stat && !validOperation(prop.type, prop.stat)) return E_IMPROPER_DATA_TYPE;
+        prop.retIndex = index++;
         prop.returned = true;
         auto it = tagIndex.find(cols[i].tag_id);
         if (it == tagIndex.end()) {
@@ -868,6 +883,8 @@ struct BoundProcessor {
         } else {
           continue;  // "InBound has none props, skip it!"
         }
+        if (prop.stat && !validOperation(prop.type, prop.stat)) return E_IMPROPER_DATA_TYPE;
+        prop.retIndex = index++;
         prop.returned = true;
         edgeProps.push_back(prop);
       }
@@ -878,6 +895,24 @@ struct BoundProcessor {
       if (!checkExp(*exp)) return E_INVALID_FILTER;
     }
     return SUCCEEDED;
+  }
+
+  // validOperation (QueryBaseProcessor.inl:18-35): SUM / AVG only over numeric types
+  static bool validOperation(int32_t t, int32_t stat) {
+    if (stat == 1 || stat == 3)
+      return t == T_INT || t == T_VID || t == T_TIMESTAMP || t == T_FLOAT || t == T_DOUBLE;
+    return true;
+  }
+
+  // StatsCollector (Collector.h:66-94), under BaseProcessor::lock_
+  void statCollect(const PropCtx& prop, const Val& v) {
+    std::lock_guard<std::mutex> lg(lock);
+    switch (v.index()) {
+      case 0: prop.sum += std::get<int64_t>(v); break;  // collectInt64
+      case 1: prop.badGet = true; break;                 // collectDouble: boost::get<double> throws
+      default: break;                                    // collectBool / collectString
+    }
+    prop.count++;
   }
 
   // checkExp (QueryBaseProcessor.inl:138-245)
@@ -949,19 +984,28 @@ struct BoundProcessor {
   void collectProps(const RowReader* reader, const char* key, const std::vector<PropCtx>& props,
                     FilterCtx* fctx, RowWriter& w) {
     for (auto& prop : props) {
+      Val kv{int64_t(0)};
       switch (prop.pik) {
-        case PIK_SRC: w << keySrc(key); continue;
-        case PIK_DST: w << keyDst(key); continue;
-        case PIK_TYPE: w << int64_t(keyType(key)); continue;
-        case PIK_RANK: w << keyRank(key); continue;
+        case PIK_SRC: kv = keySrc(key); break;
+        case PIK_DST: kv = keyDst(key); break;
+        case PIK_TYPE: kv = int64_t(keyType(key)); break;
+        case PIK_RANK: kv = keyRank(key); break;
         default: break;
+      }
+      if (prop.pik != PIK_NONE) {
+        if (stats) statCollect(prop, kv);
+        else w << kv;
+        continue;
       }
       if (reader != nullptr) {
         auto res = reader->getByName(prop.name);
         if (!res.ok()) continue;  // "Skip the bad value for prop"
         if ((prop.owner == SOURCE || prop.owner == DEST) && prop.filtered)
           fctx->tagFilters.emplace(std::make_pair(prop.tagOrEdgeName, prop.name), res.v);
-        if (prop.returned) w << res.v;
+        if (prop.returned) {
+          if (stats) statCollect(prop, res.v);
+          else w << res.v;
+        }
       }
     }
   }
@@ -1030,9 +1074,22 @@ struct BoundProcessor {
     });
   }
 
-  // processVertex (QueryBoundProcessor.cpp:16-72)
+  // processVertex (QueryBoundProcessor.cpp:16-72; QueryStatsProcessor.cpp:69-99 for stats)
   KvCode processVertex(int32_t part, int64_t vid) {
     FilterCtx fctx;
+    if (stats) {
+      RowWriter unused;
+      for (auto& tc : tagCtxs) {
+        auto code = collectVertexProps(part, vid, tc.tagId, tc.props, &fctx, unused);
+        if (code != KV_OK) return code;
+      }
+      if (!edgeProps.empty())
+        return collectEdgeProps(part, vid, edgeType, &fctx, [&](const RowReader* reader, const char* key) {
+          RowWriter w;
+          collectProps(reader, key, edgeProps, &fctx, w);
+        });
+      return KV_OK;
+    }
     ora_result::V vresp;
     vresp.vid = vid;
     if (!tagCtxs.empty()) {
@@ -1088,7 +1145,7 @@ static std::vector<std::vector<std::pair<int32_t, int64_t>>> genBuckets(
 
 // QueryBaseProcessor::process (QueryBaseProcessor.inl:462-505) + onProcessFinished
 // (QueryBoundProcessor.cpp:75-106).  Buckets run concurrently, one thread each.
-static void processRequest(BoundProcessor& proc,
+static int32_t processRequest(BoundProcessor& proc,
                            const std::vector<std::pair<int32_t, std::vector<int64_t>>>& parts,
                            const ora_prop_def* cols, size_t ncols, const uint8_t* filter,
                            size_t flen, int32_t maxHandlers, int32_t minPerBucket,
@@ -1096,7 +1153,7 @@ static void processRequest(BoundProcessor& proc,
   int32_t rc = proc.checkAndBuildContexts(proc.edgeType, cols, ncols, filter, flen);
   if (rc != SUCCEEDED) {
     for (auto& p : parts) out->failed.emplace_back(p.first, rc);
-    return;
+    return rc;
   }
   auto buckets = genBuckets(parts, maxHandlers, minPerBucket);
   std::vector<std::vector<std::pair<int32_t, KvCode>>> codes(buckets.size());
@@ -1117,6 +1174,7 @@ static void processRequest(BoundProcessor& proc,
       if (p.returned) out->vertexSchema.push_back(Field{p.name, p.type});
   for (auto& p : proc.edgeProps) out->edgeSchema.push_back(Field{p.name, p.type});
   out->vertices = std::move(proc.vertices);
+  return SUCCEEDED;
 }
 
 static SchemaPtr toSchema(const std::vector<Field>& f) {
@@ -1491,6 +1549,64 @@ ora_result* ora_get_bound(ora_store* st, int32_t et, int32_t inBound, const int3
       v.nrows++;
     });
   }
+  return out;
+}
+
+// QueryStatsProcessor (src/storage/QueryStatsProcessor.cpp:16-125): one row, one column per
+// returned prop in request order (retIndex): SUM -> INT (int64 sum), COUNT -> INT, AVG -> DOUBLE
+// (sum / count, NaN for no rows).  A double value reaching the int64-initialised sum variant
+// throws in the reference (boost::bad_get): reported as code -1003 (E_UNSUPPORTED).
+ora_result* ora_bound_stats(ora_store* st, int32_t et, int32_t inBound, const int32_t* parts,
+                            const int64_t* vids, size_t n, const uint8_t* filter, size_t flen,
+                            const ora_prop_def* cols, const int32_t* statTypes, size_t ncols,
+                            int32_t maxH, int32_t minPer) {
+  auto* out = new ora_result();
+  std::vector<std::pair<int32_t, std::vector<int64_t>>> pv;
+  std::map<int32_t, size_t> idx;
+  for (size_t i = 0; i < n; i++) {
+    auto it = idx.find(parts[i]);
+    if (it == idx.end()) {
+      idx[parts[i]] = pv.size();
+      pv.push_back({parts[i], {}});
+      it = idx.find(parts[i]);
+    }
+    pv[it->second].second.push_back(vids[i]);
+  }
+  BoundProcessor proc;
+  proc.st = st;
+  proc.outBound = !inBound;
+  proc.edgeType = et;
+  proc.stats = true;
+  proc.statTypes = statTypes;
+  if (processRequest(proc, pv, cols, ncols, filter, flen, maxH, minPer, out) != SUCCEEDED)
+    return out;  // request-level validation error: every part failed, no stats row
+  std::vector<const PropCtx*> props;
+  for (auto& tc : proc.tagCtxs)
+    for (auto& p : tc.props)
+      if (p.returned) props.push_back(&p);
+  for (auto& p : proc.edgeProps) props.push_back(&p);
+  std::sort(props.begin(), props.end(), [](const PropCtx* a, const PropCtx* b) { return a->retIndex < b->retIndex; });
+  out->edgeSchema.clear();
+  std::vector<Val> row;
+  std::vector<bool> pres;
+  for (auto* p : props) {
+    if (p->badGet && p->stat != 2) {
+      out->code = -1003;
+      out->error = "SUM/AVG over a double value (boost::bad_get in the reference)";
+      return out;
+    }
+    if (p->stat == 3) {
+      row.push_back(Val{double(p->sum) / double(p->count)});
+      out->edgeSchema.push_back(Field{p->name, T_DOUBLE});
+    } else {
+      row.push_back(Val{p->stat == 2 ? int64_t(p->count) : p->sum});
+      out->edgeSchema.push_back(Field{p->name, T_INT});
+    }
+    pres.push_back(true);
+  }
+  out->rows.push_back(std::move(row));
+  out->present.push_back(std::move(pres));
+  out->rowVertex.push_back(0);
   return out;
 }
 

@@ -68,6 +68,13 @@ ora_result* ora_get_bound(ora_store* st, int32_t edge_type, int32_t in_bound,
                           const uint8_t* filter, size_t filter_len,
                           const ora_prop_def* cols, size_t ncols,
                           int32_t max_handlers, int32_t min_per_bucket);
+// QueryStatsProcessor restatement (outBoundStats / inBoundStats, QueryStatsProcessor.cpp:16-125):
+// stat_types[i] = cpp2::StatType (SUM 1, COUNT 2, AVG 3) of cols[i].  One result row.
+ora_result* ora_bound_stats(ora_store* st, int32_t edge_type, int32_t in_bound,
+                            const int32_t* parts, const int64_t* vids, size_t n,
+                            const uint8_t* filter, size_t filter_len,
+                            const ora_prop_def* cols, const int32_t* stat_types, size_t ncols,
+                            int32_t max_handlers, int32_t min_per_bucket);
 // GenBuckets restatement (QueryBaseProcessor.inl:425-460): writes bucket sizes, returns count.
 int32_t ora_gen_buckets(const int32_t* parts, const int64_t* vids, size_t n,
                         int32_t max_handlers, int32_t min_per_bucket, int32_t* sizes_out);

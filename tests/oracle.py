@@ -56,6 +56,7 @@ def lib():
             "ora_rmat_vid": (i64, [u64, u64]),
             "ora_rmat_load": (None, [vp, i32, i32, u64, i32, i32, i32]),
             "ora_get_bound": (vp, [vp, i32, i32, vp, vp, sz, vp, sz, vp, sz, i32, i32]),
+            "ora_bound_stats": (vp, [vp, i32, i32, vp, vp, sz, vp, sz, vp, vp, sz, i32, i32]),
             "ora_gen_buckets": (i32, [vp, vp, sz, i32, i32, vp]),
             "ora_go": (vp, [vp, vp, sz, i32, i32, vp, sz, vp, vp, sz, i32, i32, i32, i32, P(u64)]),
             "ora_shortest_path": (vp, [vp, vp, vp, sz, i32, i32]),
@@ -300,6 +301,23 @@ class Store:
         fb = np.frombuffer(filt + b"\0", dtype=np.uint8)
         h = lib().ora_get_bound(self.h, etype, int(in_bound), _ptr(parts), _ptr(vids), len(vids),
                                 _ptr(fb), len(filt), arr, len(cols), handlers, min_per_bucket)
+        return Result(h)
+
+    def bound_stats(self, etype, parts, vids, cols, stats, filt=b"", in_bound=False, handlers=10,
+                    min_per_bucket=3):
+        """QueryStatsProcessor (outBoundStats / inBoundStats): stats[i] = SUM 1 / COUNT 2 / AVG 3"""
+        parts = np.ascontiguousarray(parts, dtype=np.int32)
+        vids = np.ascontiguousarray(vids, dtype=np.int64)
+        arr = (PropDef * max(len(cols), 1))()
+        keep = []
+        for i, (name, owner, tag) in enumerate(cols):
+            b = name.encode()
+            keep.append(b)
+            arr[i] = PropDef(b, owner, tag)
+        st = np.ascontiguousarray(list(stats) + [0], dtype=np.int32)
+        fb = np.frombuffer(filt + b"\0", dtype=np.uint8)
+        h = lib().ora_bound_stats(self.h, etype, int(in_bound), _ptr(parts), _ptr(vids), len(vids), _ptr(fb),
+                                  len(filt), arr, _ptr(st), len(cols), handlers, min_per_bucket)
         return Result(h)
 
     def go(self, starts, steps, etype, where=b"", yields=(), distinct=False, hosts=1,

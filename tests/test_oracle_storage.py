@@ -132,3 +132,34 @@ def test_edge_key_layout(oracle):
     import struct
     k = O.edge_key(7, 123456789, 101, 5, -3, 2**31 - 1)
     assert k == struct.pack("<iqiqqq", 7, 123456789, 101, 5, -3, 2**31 - 1)
+
+
+def test_stats_simple(oracle):  # QueryStatsTest.cpp:164-183, checkResponse :88-135
+    st = F.qs_oracle_store()
+    parts, vids, cols, stats = F.qs_request()
+    r = st.bound_stats(F.EDGE_TYPE, parts, vids, cols, stats)
+    assert r.code == 0 and r.failed() == []
+    names = [n for n, _ in r.schema(0)]
+    assert names == ["tag_3001_col_0", "tag_3003_col_2", "col_0", "col_2", "col_4", "col_6", "col_8"]
+    types = [t for _, t in r.schema(0)]
+    assert types == [O.DOUBLE, O.DOUBLE] + [O.INT] * 5
+    row = r.rows()[0]
+    assert row[:2] == (0.0, 2.0)
+    assert list(row[2:]) == [i * 2 * 210 for i in range(5)]
+
+
+def test_stats_validation_and_in_bound(oracle):
+    """SUM over a STRING prop fails every part with E_IMPROPER_DATA_TYPE (validOperation,
+    QueryBaseProcessor.inl:18-35, :100-102); in-bound requests skip edge props (:96-98)"""
+    st = F.qs_oracle_store()
+    parts, vids, _, _ = F.qs_request()
+    r = st.bound_stats(F.EDGE_TYPE, parts, vids, [("col_10", O.EDGE, 0)], [1])
+    assert sorted(r.failed()) == [(0, -23), (1, -23), (2, -23)] and r.nrows == 0
+    r = st.bound_stats(F.EDGE_TYPE, parts, vids, [("col_10", O.EDGE, 0)], [2])  # COUNT of a string is fine
+    assert r.rows() == [(210,)]
+    r = st.bound_stats(-F.EDGE_TYPE, parts, vids, [("col_1", O.EDGE, 0), ("_dst", O.EDGE, 0)], [2, 1],
+                       in_bound=True)
+    assert r.rows() == [(0,)]  # no in-edges in this fixture; col_1 skipped, SUM(_dst) = 0
+    f = (X.AliasProp("e101", "col_3") > 100).encode()
+    r = st.bound_stats(F.EDGE_TYPE, parts, vids, [("_rank", O.EDGE, 0), ("col_9", O.EDGE, 0)], [1, 3], filt=f)
+    assert r.rows()[0][0] == 0 and r.rows()[0][1] != r.rows()[0][1]  # nothing passes: AVG = 0/0 = NaN
