@@ -210,6 +210,8 @@ def main():
     ap.add_argument("--workload", choices=["go", "paths"], default="go",
                     help="go: BASELINE metric (GO 3 STEPS); paths: configs[3] FIND SHORTEST PATH")
     ap.add_argument("--pairs", type=int, default=1024)
+    ap.add_argument("--plain", action="store_true",
+                    help="GO without WHERE / DISTINCT (configs[1]: RMAT-22 3 steps, configs[4]: RMAT-28 2 steps)")
     ap.add_argument("--max-steps", type=int, default=8)
     args = ap.parse_args()
 
@@ -244,11 +246,13 @@ def main():
     if args.workload == "paths":
         return bench_paths(args, sp, info, build_s, rank, world, dist)
     starts = synth.seeds(args.scale, args.edge_factor, 1, args.seeds)
-    where = X.AliasProp("follow", "weight") > args.where
+    # --plain: no WHERE, default YIELD follow._dst rows without DISTINCT (configs[1] / configs[4])
+    where = None if args.plain else X.AliasProp("follow", "weight") > args.where
     yields = [X.EdgeDst("follow")]
 
     def one():
-        return sp.go(starts, args.hops, FOLLOW, where=where, yields=yields, distinct=True, keep_on_device=True)
+        return sp.go(starts, args.hops, FOLLOW, where=where, yields=yields, distinct=not args.plain,
+                     keep_on_device=True)
 
     for _ in range(args.warmup):
         one()
@@ -295,6 +299,9 @@ def main():
     dom = max(range(len(hop_stats)), key=lambda i: hop_ms[i]) if hop_stats else None
     workload = (f"GO {args.hops} STEPS FROM {args.seeds} seeds OVER follow WHERE follow.weight > "
                 f"{args.where} YIELD DISTINCT follow._dst; RMAT-{args.scale} ef{args.edge_factor}")
+    if args.plain:
+        workload = (f"GO {args.hops} STEPS FROM {args.seeds} seeds OVER follow (YIELD follow._dst rows); "
+                    f"RMAT-{args.scale} ef{args.edge_factor}")
     if dom is not None:
         dh = hop_stats[dom]
         dom_ach = hop_bytes[dom] / (hop_ms[dom] / 1e3) / 1e9 if hop_ms[dom] > 0 else 0.0
@@ -343,7 +350,7 @@ def main():
             },
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu:
+        if world == 1 and not args.no_cpu and not args.plain:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.cpu_scale, args.seeds, args.where)
             except Exception as e:  # the baseline must not hide the GPU number

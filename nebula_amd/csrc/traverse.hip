@@ -300,6 +300,8 @@ struct ExpandArgs {
   unsigned long long* err; // eval errors (GO semantics)
   int32_t storage;         // 1: eval error keeps the edge (QueryBaseProcessor.inl:391-396)
   int32_t mark_check;      // read the byte before storing it
+  int64_t* out_vid;        // EXP_ROWS fused YIELD _dst: write vid_of[dst] instead of (src, edge)
+  const int64_t* vid_of;
 };
 struct FastArgs {
   const void* data;
@@ -327,6 +329,8 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
   __shared__ int64_t s_rs[kTile];       // row_ptr[F[k]] - off[k]
   __shared__ int32_t s_src[kTile];      // F[k]
   __shared__ int64_t s_hdr[2];
+  __shared__ uint32_t s_wsum[kThreads / 64];
+  __shared__ unsigned long long s_base;
   const int64_t nF = a.nF;
   const int64_t E = a.off[nF];
   const int64_t ntiles = (E + kTile - 1) / kTile;
@@ -367,34 +371,36 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
       }
     }
     __syncthreads();
+    // owner of tile slot j: its frontier row and (row_ptr - off) so that ge = rsk + e
+    auto locate = [&](int j, int32_t& srck, int64_t& rsk) {
+      const int64_t e = e0 + j;
+      if (!big) {
+        int lo = 0, hi = cnt;  // s_off[lo] <= j < s_off[hi]
+        while (hi - lo > 1) {
+          int mid = (lo + hi) >> 1;
+          if (s_off[mid] <= j) lo = mid; else hi = mid;
+        }
+        srck = s_src[lo];
+        rsk = s_rs[lo];
+      } else {
+        int64_t lo = i0, hi = i0 + cnt64;  // off[lo] <= e < off[hi]
+        while (hi - lo > 1) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (a.off[mid] <= e) lo = mid; else hi = mid;
+        }
+        srck = a.F[lo];
+        rsk = a.row_ptr[srck] - a.off[lo];
+      }
+    };
+    uint32_t pm = 0;  // ROWS: items of this thread that pass
 #pragma unroll 2
     for (int r = 0; r < kItems; r++) {
       const int j = threadIdx.x + r * kThreads;
       const int64_t e = e0 + j;
       const bool valid = e < e1;
-      int k = 0;
       int32_t srck = 0;
       int64_t rsk = 0;
-      if (valid) {
-        if (!big) {
-          int lo = 0, hi = cnt;  // s_off[lo] <= j < s_off[hi]
-          while (hi - lo > 1) {
-            int mid = (lo + hi) >> 1;
-            if (s_off[mid] <= j) lo = mid; else hi = mid;
-          }
-          k = lo;
-          srck = s_src[k];
-          rsk = s_rs[k];
-        } else {
-          int64_t lo = i0, hi = i0 + cnt64;  // off[lo] <= e < off[hi]
-          while (hi - lo > 1) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (a.off[mid] <= e) lo = mid; else hi = mid;
-          }
-          srck = a.F[lo];
-          rsk = a.row_ptr[srck] - a.off[lo];
-        }
-      }
+      if (valid) locate(j, srck, rsk);
       const int64_t ge = valid ? rsk + e : 0;
       bool pass = valid;
       int32_t d = 0;
@@ -430,13 +436,49 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
           }
         }
       } else if (MODE == EXP_ROWS) {
-        int64_t slot = wave_append(a.rows_cnt, pass);
-        if (pass) {
-          a.rows_src[slot] = srck;
-          a.rows_edge[slot] = ge;
-        }
+        if (pass) pm |= 1u << r;
       } else {
         if (valid) a.flags[e] = pass;
+      }
+    }
+    if (MODE == EXP_ROWS) {
+      // block-aggregated append: one returning atomic per tile (a single counter serialises at
+      // ~90 appends / us, so a per-wave append made row output the bottleneck)
+      const uint32_t c0 = __popc(pm);
+      const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+      uint32_t incl = c0;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      if (lane == 63) s_wsum[wv] = incl;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < kThreads / 64; w++) {
+          const uint32_t x = s_wsum[w];
+          s_wsum[w] = tot;
+          tot += x;
+        }
+        s_base = tot ? atomicAdd(a.rows_cnt, (unsigned long long)tot) : 0ull;
+      }
+      __syncthreads();
+      unsigned long long pos = s_base + s_wsum[wv] + (incl - c0);
+      while (pm) {
+        const int r = __ffs(pm) - 1;
+        pm &= pm - 1;
+        const int j = threadIdx.x + r * kThreads;
+        int32_t srck;
+        int64_t rsk;
+        locate(j, srck, rsk);
+        if (a.out_vid) {
+          a.out_vid[pos] = a.vid_of[a.col[rsk + e0 + j]];
+        } else {
+          a.rows_src[pos] = srck;
+          a.rows_edge[pos] = rsk + e0 + j;
+        }
+        pos++;
       }
     }
     __syncthreads();
@@ -1966,14 +2008,26 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       h->types.push_back(NBG_T_VID);
       h->dev.push_back(std::move(vids));
     } else {
-      // rows (src, edge) passing WHERE
+      // rows (src, edge) passing WHERE; a lone YIELD _dst (the default) is written directly as
+      // vids by the expansion (no row list, no materialisation pass)
       ensure_off();
       a.F = F;
       a.nF = nF;
       a.off = c.ws_off.as<int64_t>();
-      c.ws_rows.ensure(size_t(E + 64) * 12);
-      int64_t* rows_edge = c.ws_rows.as<int64_t>();
-      int32_t* rows_src = reinterpret_cast<int32_t*>(rows_edge + E + 32);
+      const bool dst_only = yields.size() == 1 && yields[0].n == 1 && yields[0].ins[0].op == P_DST &&
+                            c.opt("fuse_dst", 1) != 0;
+      DevBuf fused;
+      int64_t* rows_edge = nullptr;
+      int32_t* rows_src = nullptr;
+      if (dst_only) {
+        fused.alloc(size_t(E + 64) * 8);
+        a.out_vid = fused.as<int64_t>();
+        a.vid_of = c.vid_of.as<int64_t>();
+      } else {
+        c.ws_rows.ensure(size_t(E + 64) * 12);
+        rows_edge = c.ws_rows.as<int64_t>();
+        rows_src = reinterpret_cast<int32_t*>(rows_edge + E + 32);
+      }
       a.rows_edge = rows_edge;
       a.rows_src = rows_src;
       a.rows_cnt = K.d + 2;
@@ -1991,18 +2045,19 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       allsum(c, &errs, 1, red);
       if (errs) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
       nrows = int64_t(K.h[2]);
-      c.timing.expand_bytes += uint64_t(nrows) * 12;
+      c.timing.expand_bytes += uint64_t(nrows) * (dst_only ? 12 : 12);  // dst_only: 4 B col re-read + 8 B vid
       YieldArgs ya{};
       ya.ncols = int32_t(yields.size());
       for (auto& p : yields) {
         int32_t t = p.result_type;
         DevBuf b;
-        b.alloc(size_t(nrows + 1) * (t == VT_BOOL ? 1 : 8));
+        if (dst_only) b = std::move(fused);
+        else b.alloc(size_t(nrows + 1) * (t == VT_BOOL ? 1 : 8));
         ya.cols[h->types.size()] = ColOut{b.p, t};
         h->types.push_back(t == VT_DOUBLE ? NBG_T_DOUBLE : t == VT_BOOL ? NBG_T_BOOL : NBG_T_VID);
         h->dev.push_back(std::move(b));
       }
-      if (nrows) {
+      if (nrows && !dst_only) {
         if (default_yield) {
           k_yield_dst<<<grid_cap(nrows), 256, 0, c.stream>>>(rows_edge, nrows, csr.col.as<int32_t>(),
                                                              c.vid_of.as<int64_t>(), h->dev[0].as<int64_t>());
