@@ -537,6 +537,8 @@ __device__ inline unsigned long long wave_sum_u64(unsigned long long x) {
 // serialises at ~88 returning atomics/us on MI355X, MI355X_MICROARCH "dequeue") ----------------
 constexpr int kAggBlocks = 8192;  // max grid of the aggregated kernels (partials are [block][kSlots])
 constexpr int kSlots = 8;
+constexpr int kLazyMax = 3;  // k_bu_slab: max lazy slab slots loaded per round trip
+constexpr int kRestMax = 2;  // k_bu_slab: max 64- / 16-entry chunks of a rest loaded per step
 
 __device__ inline uint32_t block_excl_scan_u32(uint32_t x, uint32_t& total, uint32_t* lds) {
   uint32_t wt;
@@ -608,15 +610,18 @@ __global__ __launch_bounds__(1024) void k_reduce_partials(const unsigned long lo
 // out-edges and sum their out-degrees (the next hop's E).  partials: [0] found, [1] out-degree
 // sum, [2] slab words read (+ their predicate values), [3] rows scanned past the slab, [4] entries
 // read past the slab, [5] predicate values read past the slab.
-template <int PK, int EAGER, int R, int W>
-__global__ __launch_bounds__(1024) void k_bu_slab(const int32_t* __restrict__ slab, const void* __restrict__ slab_w,
+// WPE: minimum resident waves per SIMD the register allocation must allow (6..8; the final-hop
+// variant needs ~74 VGPRs unconstrained, i.e. 6 waves)
+template <int PK, int EAGER, int R, int W, int WPE>
+__global__ __launch_bounds__(256, WPE) void k_bu_slab(const int32_t* __restrict__ slab, const void* __restrict__ slab_w,
                                                  int K, const int64_t* __restrict__ trp,
                                                  const int32_t* __restrict__ tcol, int64_t n,
                                                  const uint32_t* __restrict__ fbits,
                                                  unsigned long long* __restrict__ nbits,
                                                  const uint32_t* __restrict__ odeg, FastArgs fp,
                                                  unsigned long long* partials, int nt,
-                                                 unsigned long long* __restrict__ pbits, int cw) {
+                                                 unsigned long long* __restrict__ pbits, int cw, int lb,
+                                                 int ru) {
   __shared__ unsigned long long lds[kSlots * 16];
   // the first cw words of the frontier bitmap (the hubs: vertices are numbered by descending
   // out-degree and slab rows list hub sources first) are copied into LDS, so most lookups are
@@ -629,7 +634,11 @@ __global__ __launch_bounds__(1024) void k_bu_slab(const int32_t* __restrict__ sl
     const uint32_t w = wi < cw ? s_fb[wi] : fbits[wi];
     return (w >> (sv & 31)) & 1u;
   };
-  unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+  // per-lane counters (32-bit except the out-degree sum; widened for the block partials)
+  // predicate values held in registers at their loaded width (32-bit unless W == 8)
+  using WT = typename std::conditional<W == 8, int64_t, int32_t>::type;
+  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long odsum = 0;
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
@@ -648,7 +657,7 @@ __global__ __launch_bounds__(1024) void k_bu_slab(const int32_t* __restrict__ sl
     }
     // level 1: eager slots (+ predicate values, + out-degrees): independent loads
     int32_t sv[R][EAGER];
-    int64_t wv[R][EAGER];
+    WT wv[R][EAGER];
 #pragma unroll
     for (int j = 0; j < R; j++) {
       if (odeg && pend[j]) od[j] = nt ? __builtin_nontemporal_load(odeg + d[j]) : odeg[d[j]];
@@ -659,7 +668,7 @@ __global__ __launch_bounds__(1024) void k_bu_slab(const int32_t* __restrict__ sl
         if (pend[j] && q < KE) {
           const int64_t si = int64_t(q) * n + d[j];
           sv[j][q] = nt ? __builtin_nontemporal_load(slab + si) : slab[si];
-          if (PK == PK_FAST) wv[j][q] = load_w<W>(slab_w, fp.width, si);
+          if (PK == PK_FAST) wv[j][q] = WT(load_w<W>(slab_w, fp.width, si));
         }
       }
     }
@@ -682,39 +691,42 @@ __global__ __launch_bounds__(1024) void k_bu_slab(const int32_t* __restrict__ sl
       }
       pend[j] = pend[j] && !found[j] && !exhausted;
     }
-    // lazy slots (one level each, only while some row of the wave is still pending)
-    for (int q = KE; q < K; q++) {
+    // lazy slots, lb (<= kLazyMax) levels per round trip, only while some row of the wave is
+    // still pending: the loads of a batch are independent (masked by pend), so a batch costs one
+    // slab -> bitmap chain instead of one per slot
+    for (int q0 = KE; q0 < K; q0 += lb) {
       bool anyp = false;
 #pragma unroll
       for (int j = 0; j < R; j++) anyp |= pend[j];
       if (__ballot(anyp) == 0) break;
-      int32_t s1[R];
-      int64_t w1[R];
+      int32_t s1[R][kLazyMax];
+      WT w1[R][kLazyMax];
 #pragma unroll
       for (int j = 0; j < R; j++) {
-        s1[j] = -1;
-        w1[j] = 0;
-        if (pend[j]) {
-          const int64_t si = int64_t(q) * n + d[j];
-          s1[j] = nt ? __builtin_nontemporal_load(slab + si) : slab[si];
-          if (PK == PK_FAST) w1[j] = load_w<W>(slab_w, fp.width, si);
+#pragma unroll
+        for (int i = 0; i < kLazyMax; i++) {
+          s1[j][i] = -1;
+          w1[j][i] = 0;
+          if (pend[j] && i < lb && q0 + i < K) {
+            const int64_t si = int64_t(q0 + i) * n + d[j];
+            s1[j][i] = nt ? __builtin_nontemporal_load(slab + si) : slab[si];
+            if (PK == PK_FAST) w1[j][i] = WT(load_w<W>(slab_w, fp.width, si));
+          }
         }
       }
 #pragma unroll
       for (int j = 0; j < R; j++) {
-        if (!pend[j]) continue;
-        acc[2]++;
-        const int32_t s = s1[j];
-        if (s < 0) {
-          pend[j] = false;
-          continue;
+        bool h = false, ex = false;
+#pragma unroll
+        for (int i = 0; i < kLazyMax; i++) {
+          if (!pend[j] || i >= lb || q0 + i >= K) continue;
+          const int32_t s = s1[j][i];
+          acc[2]++;
+          if (s < 0) ex = true;  // slots past the row's end are -1 (and so are all later ones)
+          else if (in_front(s) && (PK != PK_FAST || fast_cmp(fp.op, w1[j][i], fp.k))) h = true;
         }
-        if (in_front(s)) {
-          if (PK != PK_FAST || fast_cmp(fp.op, w1[j], fp.k)) {
-            found[j] = true;
-            pend[j] = false;
-          }
-        }
+        if (h) found[j] = true;
+        if (h || ex) pend[j] = false;
       }
     }
     // rows with more entries than the slab and no hit in it.  Deferred (pbits): one pending
@@ -764,16 +776,23 @@ __global__ __launch_bounds__(1024) void k_bu_slab(const int32_t* __restrict__ sl
         const int64_t b = __shfl((long long)rb[j], src), e = __shfl((long long)re[j], src);
         acc[3] += lane == 0;
         bool f = false;
-        for (int64_t x = b; x < e && !f; x += 64) {
-          const int64_t ex = x + lane;
+        for (int64_t x = b; x < e && !f; x += 64 * ru) {
+          int32_t sr[kRestMax];
+#pragma unroll
+          for (int u = 0; u < kRestMax; u++) {
+            const int64_t ex = x + u * 64 + lane;
+            sr[u] = (u < ru && ex < e) ? tcol[ex] : -1;
+          }
           bool h = false;
-          if (ex < e) {
-            const int32_t s = tcol[ex];
+#pragma unroll
+          for (int u = 0; u < kRestMax; u++) {
+            const int64_t ex = x + u * 64 + lane;
+            if (sr[u] < 0) continue;
             acc[4]++;
-            if (in_front(s)) {
+            if (in_front(sr[u])) {
               if (PK == PK_FAST) {
                 acc[5]++;
-                h = fast_cmp(fp.op, load_w<W>(fp.data, fp.width, ex), fp.k);
+                if (fast_cmp(fp.op, load_w<W>(fp.data, fp.width, ex), fp.k)) h = true;
               } else {
                 h = true;
               }
@@ -812,19 +831,26 @@ __global__ __launch_bounds__(1024) void k_bu_slab(const int32_t* __restrict__ sl
         }
         acc[3] += gl == 0 && my_j >= 0;
         bool f = false;
-        for (int64_t x = b;; x += GL) {
+        for (int64_t x = b;; x += GL * ru) {
           const bool act = !f && x < e;
           if (__ballot(act) == 0) break;
           bool h = false;
           if (act) {
-            const int64_t ex = x + gl;
-            if (ex < e) {
-              const int32_t s = tcol[ex];
+            int32_t sr[kRestMax];
+#pragma unroll
+            for (int u = 0; u < kRestMax; u++) {
+              const int64_t ex = x + u * GL + gl;
+              sr[u] = (u < ru && ex < e) ? tcol[ex] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < kRestMax; u++) {
+              const int64_t ex = x + u * GL + gl;
+              if (sr[u] < 0) continue;
               acc[4]++;
-              if (in_front(s)) {
+              if (in_front(sr[u])) {
                 if (PK == PK_FAST) {
                   acc[5]++;
-                  h = fast_cmp(fp.op, load_w<W>(fp.data, fp.width, ex), fp.k);
+                  if (fast_cmp(fp.op, load_w<W>(fp.data, fp.width, ex), fp.k)) h = true;
                 } else {
                   h = true;
                 }
@@ -853,10 +879,11 @@ __global__ __launch_bounds__(1024) void k_bu_slab(const int32_t* __restrict__ sl
       const int64_t d0 = t * 64 * R + j * 64;
       if (lane == 0 && d0 < n) nbits[d0 >> 6] = km;
       acc[0] += found[j];
-      acc[1] += o;
+      odsum += o;
     }
   }
-  block_store_partials(acc, 6, lds, partials);
+  unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
+  block_store_partials(acc64, 6, lds, partials);
 }
 
 // Second pass of a deferred bottom-up hop: the rows k_bu_slab left pending (list F, nF rows),
@@ -1554,13 +1581,12 @@ int launch_bu_slab(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
   const int64_t per_wave = std::max<int64_t>(1, c.opt("bu_tiles_per_wave", 4));
   int grid = int(std::max<int64_t>(
       1, std::min<int64_t>((tiles + per_wave - 1) / per_wave, std::min<int64_t>(c.opt("bu_grid", 4096), kAggBlocks))));
-  // LDS copy of the bitmap's hub words (bu_lds_kb KiB, 0 = off): 1024-thread persistent blocks
+  // LDS copy of the bitmap's hub words (bu_lds_kb KiB, 0 = off): fewer, persistent blocks
   const int64_t fb_words = (c.n_global + 31) / 32;
   const int cw = int(std::min<int64_t>(c.opt("bu_lds_kb", 0) * 256, std::min<int64_t>(fb_words, 36 * 1024)));
-  int bs = 256;
+  const int bs = 256;
   if (cw > 0) {
-    bs = 1024;
-    grid = int(std::max<int64_t>(1, std::min<int64_t>((tiles + 16 * per_wave - 1) / (16 * per_wave),
+    grid = int(std::max<int64_t>(1, std::min<int64_t>((tiles + 4 * per_wave - 1) / (4 * per_wave),
                                                       std::min<int64_t>(c.opt("bu_lds_grid", 512), kAggBlocks))));
   }
   auto* nb = reinterpret_cast<unsigned long long*>(nbits);
@@ -1568,9 +1594,19 @@ int launch_bu_slab(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
   const int64_t* trp = tr.row_ptr.as<int64_t>();
   const int32_t* tc = tr.col.as<int32_t>();
   const int nt = int(c.opt("bu_nt", 0));  // non-temporal slab / out-degree loads (keep L2 for the bitmap)
-#define NBG_BU(PKV, EV, WV)                                                                             \
-  k_bu_slab<PKV, EV, 2, WV><<<grid, bs, size_t(cw) * 4, c.stream>>>(sc, slab_w, es.slab_k, trp, tc, tr.n_rows, fb, nb, \
-                                                                    odeg, fp, partials, nt, pbits, cw)
+  // lazy slab slots per round trip, and 64- / 16-entry chunks per step of a rest scan
+  const int lb = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_lazy", 3), kLazyMax)));
+  const int ru = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_unroll", 1), kRestMax)));
+  const int wpe = int(c.opt("bu_wpe", 8));
+#define NBG_BU_K(PKV, EV, WV, WP)                                                                      \
+  k_bu_slab<PKV, EV, 2, WV, WP><<<grid, bs, size_t(cw) * 4, c.stream>>>(sc, slab_w, es.slab_k, trp, tc, tr.n_rows, fb, \
+                                                                        nb, odeg, fp, partials, nt, pbits, cw, lb, ru)
+#define NBG_BU(PKV, EV, WV)                            \
+  switch (wpe) {                                       \
+    case 8: NBG_BU_K(PKV, EV, WV, 8); break;           \
+    case 7: NBG_BU_K(PKV, EV, WV, 7); break;           \
+    default: NBG_BU_K(PKV, EV, WV, 6); break;          \
+  }
 #define NBG_BU_W(EV)                      \
   switch (fp.width) {                     \
     case 1: NBG_BU(PK_FAST, EV, 1); break; \
@@ -1592,6 +1628,7 @@ int launch_bu_slab(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
   }
 #undef NBG_BU_W
 #undef NBG_BU
+#undef NBG_BU_K
   k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, out);
   NBG_HIP(hipGetLastError());
   return grid;

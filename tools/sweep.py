@@ -15,6 +15,11 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
+# engine defaults of the swept options (traverse.hip / snapshot.hip), restored after each config
+DEFAULTS = {"bu_r": 2, "bu_eager_fast": 1, "bu_eager": 1, "bu_nt": 0, "bu_defer": 0, "bu_grid": 4096,
+            "bu_tiles_per_wave": 4, "bu_lds_kb": 0, "bu_lds_grid": 512, "bu_div": 4, "bu_slab": 4,
+            "bu_lazy": 3, "bu_unroll": 1, "bu_wpe": 8}
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -34,27 +39,33 @@ def main():
     print(json.dumps({"build_s": time.time() - t0}), flush=True)
     starts = synth.seeds(args.scale, 16, 1, 64)
     where = X.AliasProp("follow", "weight") > args.where
-    ref = None
-    for cfg in [""] + args.config:
-        opts = dict(kv.split("=") for kv in cfg.split(",") if kv)
-        for k, v in opts.items():
-            sp.set_option(k, int(v))
-        ms, rows = [], None
-        for _ in range(args.reps):
+    cfgs = [""] + args.config
+    # interleaved: every rep runs each config once, so clock / neighbour drift hits all alike
+    ms = {c: [] for c in cfgs}
+    hop_ms = {c: [] for c in cfgs}
+    res = {}
+    for _ in range(args.reps):
+        for cfg in cfgs:
+            opts = dict(kv.split("=") for kv in cfg.split(",") if kv)
+            saved = {k: DEFAULTS.get(k, 0) for k in opts}
+            for k, v in opts.items():
+                sp.set_option(k, int(v))
             t = time.perf_counter()
             r = sp.go(starts, args.hops, 1, where=where, yields=[X.EdgeDst("follow")], distinct=True,
                       keep_on_device=True)
-            ms.append((time.perf_counter() - t) * 1e3)
-            rows = r.n_rows
-        tm = sp.last_timing()
-        if ref is None:
-            ref = rows
-        print(json.dumps({"config": cfg or "default", "ms_median": statistics.median(ms), "ms_min": min(ms),
-                          "rows": rows, "rows_ok": rows == ref, "edges": r.edges_scanned,
-                          "hops": [(h["mode"], round(h["ms"], 4), h["c"]) for h in tm["hops"]]}), flush=True)
-        for k in opts:  # back to defaults
-            sp.set_option(k, {"bu_r": 2, "bu_eager_fast": 1, "bu_eager": 1, "bu_nt": 0, "bu_defer": 0, "bu_grid": 4096,
-                              "bu_tiles_per_wave": 4, "bu_lds_kb": 0, "bu_lds_grid": 512, "bu_div": 4, "bu_slab": 4}.get(k, 0))
+            ms[cfg].append((time.perf_counter() - t) * 1e3)
+            tm = sp.last_timing()
+            hop_ms[cfg].append([h["ms"] for h in tm["hops"]])
+            res[cfg] = (r.n_rows, r.edges_scanned, tm)
+            for k, v in saved.items():
+                sp.set_option(k, v)
+    ref = res[""][0]
+    for cfg in cfgs:
+        rows, edges, tm = res[cfg]
+        hops = [round(statistics.median(h[i] for h in hop_ms[cfg]), 4) for i in range(len(hop_ms[cfg][0]))]
+        print(json.dumps({"config": cfg or "default", "ms_median": statistics.median(ms[cfg]), "ms_min": min(ms[cfg]),
+                          "rows": rows, "rows_ok": rows == ref, "edges": edges, "hop_ms_median": hops,
+                          "hops": [(h["mode"], h["c"]) for h in tm["hops"]]}), flush=True)
     sp.close()
 
 
