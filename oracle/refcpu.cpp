@@ -829,6 +829,7 @@ struct BoundProcessor {
   const ora_store* st;
   bool outBound;
   bool stats = false;            // QueryStatsProcessor instead of QueryBoundProcessor
+  bool onlyVertexProps = false;  // QueryVertexPropsProcessor (QueryVertexPropsProcessor.cpp:16-28)
   const int32_t* statTypes = nullptr;
   int32_t edgeType = 0;
   std::vector<TagCtx> tagCtxs;
@@ -1100,6 +1101,11 @@ struct BoundProcessor {
       }
       if (w.size() > 1) vresp.vertexData = w.encode();
     }
+    if (onlyVertexProps) {  // QueryBoundProcessor.cpp:33-37
+      std::lock_guard<std::mutex> lg(lock);
+      vertices.push_back(std::move(vresp));
+      return KV_OK;
+    }
     if (!edgeProps.empty()) {
       std::string rs;
       auto code = collectEdgeProps(part, vid, edgeType, &fctx,
@@ -1194,7 +1200,7 @@ static int32_t partOf(int64_t vid, int32_t numParts) {
 static std::vector<ora_result> getNeighbors(const ora_store* st, const std::vector<int64_t>& vids,
                                             int32_t edgeType, const std::vector<ora_prop_def>& cols,
                                             int32_t numHosts, int32_t maxHandlers,
-                                            int32_t minPerBucket) {
+                                            int32_t minPerBucket, bool onlyVertexProps = false) {
   std::map<int32_t, std::map<int32_t, std::vector<int64_t>>> clusters;  // host -> part -> ids
   for (auto v : vids) {
     int32_t part = partOf(v, st->numParts);
@@ -1211,6 +1217,7 @@ static std::vector<ora_result> getNeighbors(const ora_store* st, const std::vect
       proc.st = st;
       proc.outBound = edgeType > 0;
       proc.edgeType = edgeType;
+      proc.onlyVertexProps = onlyVertexProps;
       processRequest(proc, parts, cols.data(), cols.size(), nullptr, 0, maxHandlers,
                      minPerBucket, &resps[i]);
     });
@@ -1649,9 +1656,37 @@ ora_result* ora_go(ora_store* st, const int64_t* starts, size_t nStarts, int32_t
   ExprRefs refs;
   if (filter) collectRefs(*filter, refs);
   for (auto& y : ycols) collectRefs(*y, refs);
-  if (!refs.srcTag.empty() || !refs.dstTag.empty() || refs.input || refs.variable) {
+  if (refs.input || refs.variable) {
     out->code = -2;
-    out->error = "unsupported reference ($^/$$/$-/$var)";
+    out->error = "unsupported reference ($-/$var)";
+    return out;
+  }
+  // getStepOutProps / getDstProps (GoExecutor.cpp:454-527): tag props grouped per tag name,
+  // index = position in the vertex row; unknown tag -> "No schema found"
+  std::vector<std::string> tagPropNames;  // stable storage for the PropDef names
+  tagPropNames.reserve(refs.srcTag.size() + refs.dstTag.size());
+  std::vector<ora_prop_def> srcCols, dstCols;
+  std::map<std::pair<std::string, std::string>, int> srcIndex, dstIndex;
+  auto tagCols = [&](const std::set<std::pair<std::string, std::string>>& refsSet,
+                     std::vector<ora_prop_def>& colsOut,
+                     std::map<std::pair<std::string, std::string>, int>& index) {
+    std::map<std::string, std::vector<std::string>> byTag;
+    for (auto& tp : refsSet) byTag[tp.first].push_back(tp.second);
+    int i = -1;
+    for (auto& t : byTag) {
+      auto id = st->tagByName.find(t.first);
+      if (id == st->tagByName.end()) return false;
+      for (auto& prop : t.second) {
+        tagPropNames.push_back(prop);
+        colsOut.push_back(ora_prop_def{tagPropNames.back().c_str(), DEST, id->second});
+        index[{t.first, prop}] = ++i;
+      }
+    }
+    return true;
+  };
+  if (!tagCols(refs.srcTag, srcCols, srcIndex) || !tagCols(refs.dstTag, dstCols, dstIndex)) {
+    out->code = -5;
+    out->error = "No schema found";
     return out;
   }
   std::vector<int64_t> cur(starts, starts + nStarts);
@@ -1667,7 +1702,9 @@ ora_result* ora_go(ora_store* st, const int64_t* starts, size_t nStarts, int32_t
     if (final)
       for (auto& ap : refs.alias) names.push_back(ap.second);
     std::vector<ora_prop_def> cols;
-    for (auto& n : names) cols.push_back(ora_prop_def{n.c_str(), EDGE, 0});
+    cols.push_back(ora_prop_def{names[0].c_str(), EDGE, 0});
+    if (final) cols.insert(cols.end(), srcCols.begin(), srcCols.end());
+    for (size_t ni = 1; ni < names.size(); ni++) cols.push_back(ora_prop_def{names[ni].c_str(), EDGE, 0});
     auto resps = getNeighbors(st, cur, et, cols, numHosts, maxH, minPer);
     size_t ok = 0;
     for (auto& r : resps) ok += r.failed.empty() ? 1 : 0;
@@ -1692,13 +1729,47 @@ ora_result* ora_go(ora_store* st, const int64_t* starts, size_t nStarts, int32_t
       if (cur.empty()) break;  // onEmptyInputs
       continue;
     }
+    // onStepOutResponse final step with $$ props: fetchVertexProps over the response's dst ids
+    // (GoExecutor.cpp:377-386, 531-566), kept in a VertexHolder (:785-828)
+    std::unordered_map<int64_t, std::string> holder;
+    SchemaPtr holderSchema;
+    if (!dstCols.empty()) {
+      std::unordered_set<int64_t> set;
+      for (auto& r : resps) {
+        auto es = toSchema(r.edgeSchema);
+        for (auto& v : r.vertices)
+          rowSetForEach(v.edgeData, es, [&](const RowReader& row) { set.insert(std::get<0>(row.getByName("_dst").v)); });
+      }
+      if (set.empty()) break;  // onEmptyInputs
+      std::vector<int64_t> dstids(set.begin(), set.end());
+      auto vr = getNeighbors(st, dstids, 0, dstCols, numHosts, maxH, minPer, /*onlyVertexProps=*/true);
+      size_t vok = 0;
+      for (auto& r : vr) vok += r.failed.empty() ? 1 : 0;
+      if (!vr.empty() && vok == 0) {
+        out->code = -3;
+        out->error = "Get dest props failed";
+        return out;
+      }
+      for (auto& r : vr) {
+        if (r.vertices.empty()) continue;
+        if (!holderSchema) holderSchema = toSchema(r.vertexSchema);
+        for (auto& v : r.vertices)
+          if (!v.vertexData.empty()) holder[v.vid] = v.vertexData;
+      }
+    }
     // processFinalResult + setupInterimResult (GoExecutor.cpp:585-656, 669-782)
     SchemaPtr outSchema;
     std::unordered_set<std::string> uniq;
     for (auto& r : resps) {
       auto es = toSchema(r.edgeSchema);
+      auto vs = toSchema(r.vertexSchema);
       for (auto& v : r.vertices) {
         bool failed = false;
+        // a vertex without any requested tag has no vertex_data: the reference builds a
+        // RowReader over the empty row and aborts (RowReader.cpp:207-214); reported as an error
+        std::unique_ptr<RowReader> vreader;
+        if (!srcCols.empty() && !v.vertexData.empty())
+          vreader = std::make_unique<RowReader>(v.vertexData.data(), v.vertexData.size(), vs);
         rowSetForEach(v.edgeData, es, [&](const RowReader& row) {
           if (failed) return;
           scanned++;
@@ -1708,6 +1779,26 @@ ora_result* ora_go(ora_store* st, const int64_t* starts, size_t nStarts, int32_t
             if (res.ok()) return res;
             return ERR("get edge prop failed");
           };
+          g.getSrcTagProp = [&](const std::string& tag, const std::string& prop) -> OptVal {
+            auto it = srcIndex.find({tag, prop});
+            if (it == srcIndex.end() || !vreader) return ERR("src tag prop missing");
+            auto res = vreader->getByIndex(it->second);
+            if (res.ok()) return res;
+            return ERR(tag + "." + prop + " was not exist");
+          };
+          g.getDstTagProp = [&](const std::string& tag, const std::string& prop) -> OptVal {
+            auto it = dstIndex.find({tag, prop});
+            if (it == dstIndex.end()) return ERR("dst tag prop missing");
+            int64_t dst = std::get<0>(row.getByName("_dst").v);
+            auto h = holder.find(dst);
+            if (h == holder.end()) return ERR("vertex was not found");
+            RowReader rr(h->second.data(), h->second.size(), holderSchema);
+            auto res = rr.getByIndex(it->second);
+            if (res.ok()) return res;
+            return ERR("get prop failed");
+          };
+          g.getInputProp = [&](const std::string&) -> OptVal { return ERR("$- unsupported"); };
+          g.getVariableProp = [&](const std::string&) -> OptVal { return ERR("$var unsupported"); };
           if (filter) {
             auto fv = eval(*filter, g);
             if (!fv.ok()) {

@@ -8,8 +8,9 @@ Source of the data: src/graph/test/TraverseTestBase.h:207-300 (players/teams) an
 (serve/like edges, in insertion order).  Vertex ids are the reference's
 ``std::hash<std::string>()(name)`` (TraverseTestBase.h:58, :180), computed by compiling a
 two-line g++ program so libstdc++'s hash is used exactly.  The expected GO results are the
-ones asserted in src/graph/test/GoTest.cpp (line numbers recorded per case); cases that need
-$^/$$ tag props keep only their edge-derived columns.
+ones asserted in src/graph/test/GoTest.cpp (line numbers recorded per case); the tag_* cases
+keep their $^/$$ tag-prop columns, the older entries of the same queries only their
+edge-derived columns.
 """
 import json
 import re
@@ -80,6 +81,23 @@ def main():
                                         ["Tony Parker"], ["Tim Duncan"]]},
             "distinct_boris_serve_dst": {"line": "GoTest.cpp:213-226 (edge column only)",
                                          "rows": [["Spurs"], ["Hornets"], ["Trail Blazers"]]},
+            # cases with $^ / $$ tag props, full rows
+            "tag_serve_boris": {"line": "GoTest.cpp:42-56",
+                                "rows": [["Boris Diaw", 2003, 2005, "Hawks"],
+                                         ["Boris Diaw", 2005, 2008, "Suns"],
+                                         ["Boris Diaw", 2008, 2012, "Hornets"],
+                                         ["Boris Diaw", 2012, 2016, "Spurs"],
+                                         ["Boris Diaw", 2016, 2017, "Jazz"]]},
+            "tag_serve_rondo_where": {"line": "GoTest.cpp:57-72",
+                                      "rows": [["Rajon Rondo", 2014, 2015, "Mavericks"],
+                                               ["Rajon Rondo", 2015, 2016, "Kings"],
+                                               ["Rajon Rondo", 2016, 2017, "Bulls"],
+                                               ["Rajon Rondo", 2017, 2018, "Pelicans"]]},
+            "tag_distinct_nobody": {"line": "GoTest.cpp:221-230", "rows": []},
+            "tag_distinct_pipe_dst_team": {"line": "GoTest.cpp:231-246",
+                                           "rows": [["Spurs", "Spurs"], ["Hornets", "Hornets"],
+                                                    ["Trail Blazers", "Trail Blazers"]]},
+            "tag_vertex_not_exist": {"line": "GoTest.cpp:272-289", "rows": []},
             "derived_go3_boris_like": {"line": "derived from the data by P12 (SURVEY 8c)",
                                        "rows": [["Tony Parker"], ["Manu Ginobili"], ["Tim Duncan"],
                                                 ["Tony Parker"], ["Tim Duncan"], ["Tim Duncan"],

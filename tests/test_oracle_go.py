@@ -110,3 +110,57 @@ def test_where_error_fails_query(nba):
     w = (X.AliasProp("like", "nope") > 1).encode()
     r = st.go([vid["Tim Duncan"]], 1, F.NBA_LIKE, where=w)
     assert r.code != 0
+
+
+# ---- $^ / $$ tag props (GoExecutor::getStepOutProps / fetchVertexProps) ----------
+def tag_yields():
+    return [X.SourceProp("player", "name").encode(), X.AliasProp("serve", "start_year").encode(),
+            X.AliasProp("serve", "end_year").encode(), X.DestProp("team", "name").encode()]
+
+
+def test_tag_props_yield(nba):
+    st, vid, d = nba
+    r = st.go([vid["Boris Diaw"]], 1, F.NBA_SERVE, yields=tag_yields())
+    assert r.code == 0, r.error
+    assert names(vid, r.rows()) == expect(d, "tag_serve_boris")
+    w = ((X.AliasProp("serve", "start_year") >= 2013) & (X.AliasProp("serve", "end_year") <= 2018)).encode()
+    r = st.go([vid["Rajon Rondo"]], 1, F.NBA_SERVE, where=w, yields=tag_yields())
+    assert names(vid, r.rows()) == expect(d, "tag_serve_rondo_where")
+
+
+def test_tag_props_distinct(nba):
+    st, vid, d = nba
+    ys = [X.SourceProp("player", "name").encode(), X.DestProp("team", "name").encode()]
+    r = st.go([vid["Nobody"]], 1, F.NBA_SERVE, yields=ys, distinct=True)
+    assert r.code == 0 and names(vid, r.rows()) == expect(d, "tag_distinct_nobody")
+    r = pipe(st, [vid["Boris Diaw"]], [F.NBA_LIKE, F.NBA_LIKE, F.NBA_SERVE], distinct_last=True,
+             ylast=[X.EdgeDst("serve").encode(), X.DestProp("team", "name").encode()])
+    assert names(vid, r.rows()) == expect(d, "tag_distinct_pipe_dst_team")
+
+
+def test_tag_props_vertex_not_exist(nba):
+    st, vid, d = nba
+    nid = d["nonexist_hash"]
+    for distinct in (False, True):
+        r = st.go([nid], 1, F.NBA_SERVE, yields=tag_yields(), distinct=distinct)
+        assert r.code == 0 and names(vid, r.rows()) == expect(d, "tag_vertex_not_exist")
+
+
+def test_tag_props_where_and_errors(nba):
+    st, vid, d = nba
+    # WHERE over both ends' tags: teammates older than 35 liking each other
+    w = ((X.SourceProp("player", "age") > 35) & (X.DestProp("player", "age") > 35)).encode()
+    ys = [X.SourceProp("player", "name").encode(), X.DestProp("player", "name").encode()]
+    r = st.go([vid["Tim Duncan"], vid["Tony Parker"], vid["Manu Ginobili"]], 1, F.NBA_LIKE, where=w, yields=ys)
+    assert r.code == 0, r.error
+    ages = {p["name"]: p["age"] for p in d["players"]}
+    likes = {(a, b) for a, b, _ in d["like"]}
+    want = sorted((a, b) for a, b in likes if a in ("Tim Duncan", "Tony Parker", "Manu Ginobili")
+                  and ages[a] > 35 and ages.get(b, 0) > 35)
+    assert sorted(r.rows()) == want
+    # unknown tag name -> "No schema found" (GoExecutor.cpp:475-478)
+    r = st.go([vid["Tim Duncan"]], 1, F.NBA_LIKE, yields=[X.DestProp("coach", "name").encode()])
+    assert r.code != 0
+    # $$.team.name on a player vertex: the dst has no team row -> evaluation error fails the query
+    r = st.go([vid["Tim Duncan"]], 1, F.NBA_LIKE, yields=[X.DestProp("team", "name").encode()])
+    assert r.code != 0
