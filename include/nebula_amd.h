@@ -87,11 +87,18 @@ int32_t nbg_rank_of_part(int32_t part, int32_t world_size);   /* CreateSpaceProc
 int32_t nbg_schema_set_edge(nbg_ctx* ctx, int32_t edge_type, int32_t schema_ver,
                             int32_t nfields, const char* const* names, const int32_t* types);
 
+/* Vertex tag schema (SchemaManager::getTagSchema, src/meta/SchemaManager.h:32-36) plus the tag's
+ * name, which graphd resolves $^.tag.prop / $$.tag.prop with (SchemaManager::toTagID,
+ * GoExecutor.cpp:475-478).  Vertex keys of registered tags (NebulaKeyUtils.h:14-17, 24 bytes) are
+ * decoded by nbg_snapshot_load_part into per-vertex columns used by GO's $^ / $$ props.       */
+int32_t nbg_schema_set_tag(nbg_ctx* ctx, int32_t tag_id, const char* tag_name, int32_t schema_ver,
+                           int32_t nfields, const char* const* names, const int32_t* types);
+
 /* ---- snapshot builder --------------------------------------------------------------------
  * Consumes a partition's KV pairs in the reference byte layout (NebulaKeyUtils.h:14-21 keys,
  * dataman RowWriter rows) -- what RocksEngine::prefix iterates (RocksEngine.cpp:191-200) --
  * and builds the GPU-resident CSR + SoA property columns.  Keys/values are concatenated blobs
- * with n+1 offsets.  Vertex keys and other edge types are ignored.  Call once per part (any
+ * with n+1 offsets.  Keys of unregistered tags / edge types are ignored.  Call once per part (any
  * order), then nbg_snapshot_finalize.                                                       */
 int32_t nbg_snapshot_load_part(nbg_ctx* ctx, int32_t part, const uint8_t* key_bytes,
                                const uint64_t* key_offsets, const uint8_t* val_bytes,

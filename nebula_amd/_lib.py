@@ -27,7 +27,7 @@ OWNER_SOURCE, OWNER_DEST, OWNER_EDGE = 1, 2, 3
 EXPORTS = [
     "nbg_ctx_create", "nbg_ctx_destroy", "nbg_last_error", "nbg_comm_unique_id", "nbg_comm_init",
     "nbg_comm_init_local",
-    "nbg_part_of", "nbg_rank_of_part", "nbg_schema_set_edge", "nbg_snapshot_load_part",
+    "nbg_part_of", "nbg_rank_of_part", "nbg_schema_set_edge", "nbg_schema_set_tag", "nbg_snapshot_load_part",
     "nbg_snapshot_gen_rmat", "nbg_snapshot_finalize", "nbg_snapshot_info_get",
     "nbg_snapshot_out_degree", "nbg_rows_free", "nbg_get_bound", "nbg_bound_stats", "nbg_go", "nbg_shortest_path",
     "nbg_last_timing", "nbg_set_option",
@@ -106,6 +106,7 @@ def load(path: str | os.PathLike | None = None):
         "nbg_part_of": (i32, [i64, i32]),
         "nbg_rank_of_part": (i32, [i32, i32]),
         "nbg_schema_set_edge": (i32, [vp, i32, i32, i32, C.POINTER(C.c_char_p), C.POINTER(i32)]),
+        "nbg_schema_set_tag": (i32, [vp, i32, C.c_char_p, i32, i32, C.POINTER(C.c_char_p), C.POINTER(i32)]),
         "nbg_snapshot_load_part": (i32, [vp, i32, vp, vp, vp, vp, sz]),
         "nbg_snapshot_gen_rmat": (i32, [vp, i32, i32, u64, i32]),
         "nbg_snapshot_finalize": (i32, [vp]),

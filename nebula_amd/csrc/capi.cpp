@@ -119,6 +119,31 @@ int32_t nbg_schema_set_edge(nbg_ctx* ctx, int32_t edge_type, int32_t schema_ver,
   });
 }
 
+int32_t nbg_schema_set_tag(nbg_ctx* ctx, int32_t tag_id, const char* tag_name, int32_t schema_ver,
+                           int32_t nfields, const char* const* names, const int32_t* types) {
+  return guarded(ctx, [&](Ctx& c) {
+    if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
+    if (tag_id <= 0 || !tag_name || !*tag_name) throw Error(NBG_E_INVALID_ARG, "tag id must be > 0 with a name");
+    if (nfields < 0 || nfields > 64 || (nfields > 0 && (!names || !types))) throw Error(NBG_E_INVALID_ARG, "bad fields");
+    for (auto& kv : c.tags)
+      if (kv.first != tag_id && kv.second.name == tag_name) throw Error(NBG_E_INVALID_ARG, "duplicate tag name");
+    nbg::TagSpace& ts = c.tags[tag_id];
+    if (ts.stage.n) throw Error(NBG_E_STATE, "schema changed after data was loaded");
+    ts.id = tag_id;
+    ts.name = tag_name;
+    ts.schema_ver = schema_ver;
+    ts.fields.clear();
+    for (int32_t i = 0; i < nfields; i++) {
+      int32_t t = types[i];
+      if (t != NBG_T_BOOL && t != NBG_T_INT && t != NBG_T_VID && t != NBG_T_FLOAT && t != NBG_T_DOUBLE &&
+          t != NBG_T_STRING && t != NBG_T_TIMESTAMP)
+        throw Error(NBG_E_UNSUPPORTED, "unsupported field type");
+      ts.fields.push_back(nbg::Field{names[i] ? names[i] : "", t});
+    }
+    return NBG_OK;
+  });
+}
+
 int32_t nbg_snapshot_load_part(nbg_ctx* ctx, int32_t part, const uint8_t* key_bytes, const uint64_t* key_offsets,
                                const uint8_t* val_bytes, const uint64_t* val_offsets, size_t n) {
   return guarded(ctx, [&](Ctx& c) {

@@ -183,6 +183,7 @@ struct Staging {
   int64_t n = 0;
   DevBuf src, dst, rank, ver;          // int64 each; rank/ver may stay empty (constant)
   DevBuf part;                         // int32 part of the key (empty: hash rule)
+  DevBuf seq;                          // int64 load sequence number of the KV pair (write order)
   bool rank_const = true, ver_const = true;
   int64_t rank_value = 0, ver_value = 0;
   std::vector<DevBuf> props;           // int64 bits per field (double bits for DOUBLE/FLOAT)
@@ -213,6 +214,24 @@ struct EdgeSpace {
   DevBuf slab_col;                 // int32, -1 past the row's end
   std::vector<DevBuf> slab_props;  // per out prop with a transposed copy, same width
   DevBuf odeg;                     // uint32 [owned rows]: out-degree, 0 where row_ok == 0
+};
+
+// Vertex tag props: per tag, one row per vertex = the bytewise-first version under
+// the vertex key prefix (part, vid, tag) of the vid's own part -- what collectVertexProps reads
+// (QueryBaseProcessor.inl:309-333).  Columns span the whole gidx space so $^ (src) and $$ (dst)
+// props are one indexed load; `present` = the vertex has the row and the field decoded.
+struct TagSpace {
+  int32_t id = 0;
+  int32_t schema_ver = 0;
+  std::string name;
+  std::vector<Field> fields;
+  Staging stage;              // src = vid, ver, part, rank = load sequence number (write order)
+  std::vector<PropCol> cols;  // per field, [n_global]; data int64 bits, present uint8
+};
+// flat (tag, prop) table the expression compiler resolves $^.tag.prop / $$.tag.prop against
+struct TagFieldRef {
+  std::string tag, prop;
+  int32_t type;
 };
 
 struct Timing {
@@ -260,6 +279,10 @@ struct Ctx {
   DevBuf heap;                   // device copy of all loaded value blobs (STRING props)
   size_t heap_used = 0;
   std::map<int32_t, EdgeSpace> edges;
+  std::map<int32_t, TagSpace> tags;
+  int64_t load_seq = 0;               // KV pairs loaded so far (write order across parts)
+  std::vector<TagFieldRef> tag_refs;  // flat (tag, prop) table, tag-id order then field order
+  DevBuf tag_table;                   // device descriptors of tag_refs' columns (first query)
   double build_seconds = 0;
 
   // workspaces for queries

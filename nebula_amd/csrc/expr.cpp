@@ -117,6 +117,7 @@ std::unique_ptr<Node> dec(uint8_t kind, Cur& c) {
 
 struct Compiler {
   const std::vector<Field>& fields;
+  const std::vector<TagFieldRef>* tags = nullptr;
   bool graphd;     // graphd AST semantics (GoExecutor) vs storage-decoded filter
   bool out_bound;
   Program prog;
@@ -232,9 +233,32 @@ struct Compiler {
         return VT_ERR;
       }
       case kSourceProp:
-      case kDestProp:
-        fail(graphd ? NBG_E_UNSUPPORTED : NBG_E_UNSUPPORTED, "$^ / $$ tag props are not supported yet");
+      case kDestProp: {
+        // graphd: getStepOutProps / getDstProps resolve the tag name (GoExecutor.cpp:470-527);
+        // storage filters with tag props stay unsupported on the device
+        if (!graphd || !tags) {
+          fail(NBG_E_UNSUPPORTED, "$^ / $$ tag props in a storage filter");
+          return VT_ERR;
+        }
+        bool known_tag = false;
+        for (size_t i = 0; i < tags->size(); i++) {
+          const TagFieldRef& t = (*tags)[i];
+          if (t.tag != x.alias) continue;
+          known_tag = true;
+          if (t.prop != x.prop) continue;
+          emit(x.kind == kSourceProp ? P_SRCTAG : P_DSTTAG, 0, int16_t(i));
+          push();
+          if (t.type == NBG_T_DOUBLE || t.type == NBG_T_FLOAT) return VT_DOUBLE;
+          if (t.type == NBG_T_BOOL) return VT_BOOL;
+          if (t.type == NBG_T_STRING) return VT_STR;
+          return VT_INT;
+        }
+        // unknown tag: "No schema found" (GoExecutor.cpp:475-478); unknown prop of a known tag:
+        // checkAndBuildContexts -> E_IMPROPER_DATA_TYPE on every part (QueryBaseProcessor.inl:56-66)
+        if (known_tag) fail(NBG_E_IMPROPER_DATA_TYPE, "unknown tag prop " + x.alias + "." + x.prop);
+        else fail(NBG_E_TAG_PROP_NOT_FOUND, "no schema found for tag " + x.alias);
         return VT_ERR;
+      }
       case kInputProp:
       case kVariableProp:
         // checkExp rejects these in storage filters; graphd needs pipe inputs (not supported)
@@ -280,7 +304,7 @@ struct Compiler {
 
 // Compiles an encoded expression.  Returns NBG_OK or an error code (msg filled).
 int32_t compile_expr(const uint8_t* buf, size_t len, const std::vector<Field>& fields, bool graphd,
-                     bool out_bound, Program* out, std::string* msg) {
+                     bool out_bound, Program* out, std::string* msg, const std::vector<TagFieldRef>* tags) {
   std::unique_ptr<Node> root;
   try {
     Cur c{buf, buf + len};
@@ -291,6 +315,7 @@ int32_t compile_expr(const uint8_t* buf, size_t len, const std::vector<Field>& f
     return graphd ? NBG_E_INVALID_ARG : NBG_E_INVALID_FILTER;  // Expression::decode -> E_INVALID_FILTER
   }
   Compiler cc(fields, graphd, out_bound);
+  cc.tags = tags;
   for (int i = 0; i < kMaxConsts; i++) cc.prog.ctype[i] = -1;
   cc.prog.result_type = cc.gen(*root);
   if (cc.code != NBG_OK) {

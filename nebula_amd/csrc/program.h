@@ -28,6 +28,8 @@ enum POp : uint8_t {
   P_ARITH = 7,   // sub = ADD/SUB/MUL/DIV/MOD
   P_REL = 8,     // sub = LT/LE/GT/GE/EQ/NE
   P_LOGIC = 9,   // sub = AND/OR
+  P_SRCTAG = 10, // push $^.tag.prop: tag column arg (Ctx::tag_refs) at the edge's src vertex
+  P_DSTTAG = 11, // push $$.tag.prop: tag column arg at the edge's dst vertex
 };
 
 constexpr int kMaxIns = 48;

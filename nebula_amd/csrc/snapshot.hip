@@ -74,6 +74,7 @@ static void stage_reserve(Ctx& c, Staging& s, size_t nfields, size_t extra, bool
   grow_copy(c, s.rank, cap * 8);
   grow_copy(c, s.ver, cap * 8);
   grow_copy(c, s.part, cap * 4);
+  grow_copy(c, s.seq, cap * 8);
   if (with_props) {
     s.props.resize(nfields);
     s.present.resize(nfields);
@@ -96,6 +97,7 @@ struct StageOut {
   int64_t* dst;
   int64_t* rank;
   int64_t* ver;
+  int64_t* seq;
   int64_t* props[kMaxFields];
   uint8_t* present[kMaxFields];
   int64_t* str_len[kMaxFields];
@@ -206,7 +208,7 @@ __device__ void decode_row(const uint8_t* row, int64_t len, const SchemaDev& sch
 __global__ void k_decode_kv(const uint8_t* __restrict__ kb, const uint64_t* __restrict__ koff,
                             const uint8_t* __restrict__ vb, const uint64_t* __restrict__ voff,
                             int64_t n, int32_t etype, int32_t sver, SchemaDev sch, int64_t heap_base,
-                            StageOut outS, unsigned long long* out_cnt, StageOut inS,
+                            int64_t seq0, StageOut outS, unsigned long long* out_cnt, StageOut inS,
                             unsigned long long* in_cnt, unsigned long long* err) {
   int64_t stride = int64_t(gridDim.x) * blockDim.x;
   int64_t n_rounds = (n + stride - 1) / stride;
@@ -239,6 +241,7 @@ __global__ void k_decode_kv(const uint8_t* __restrict__ kb, const uint64_t* __re
       outS.dst[so] = dst;
       outS.rank[so] = rank;
       outS.ver[so] = ver;
+      outS.seq[so] = seq0 + i;
       uint64_t v0 = voff[i], v1 = voff[i + 1];
       const uint8_t* row = vb + v0;
       int64_t len = int64_t(v1 - v0);
@@ -258,7 +261,40 @@ __global__ void k_decode_kv(const uint8_t* __restrict__ kb, const uint64_t* __re
       inS.dst[si] = dst;
       inS.rank[si] = rank;
       inS.ver[si] = ver;
+      inS.seq[si] = seq0 + i;
     }
+  }
+}
+
+// Vertex keys (NebulaKeyUtils.h:14-17: part i32 | vid i64 | tag i32 | ver i64, 24 bytes) of one
+// tag -> staged (vid, ver, part, load sequence) + decoded row fields.
+__global__ void k_decode_vkv(const uint8_t* __restrict__ kb, const uint64_t* __restrict__ koff,
+                             const uint8_t* __restrict__ vb, const uint64_t* __restrict__ voff, int64_t n,
+                             int32_t tag, int32_t sver, SchemaDev sch, int64_t heap_base, int64_t seq0,
+                             StageOut o, unsigned long long* cnt, unsigned long long* err) {
+  int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  int64_t n_rounds = (n + stride - 1) / stride;
+  for (int64_t r = 0; r < n_rounds; r++) {
+    int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    bool hit = false;
+    if (i < n && koff[i + 1] - koff[i] == 24) hit = ld_unaligned<int32_t>(kb + koff[i] + 12) == tag;
+    int64_t so = wave_append(cnt, hit);
+    if (!hit) continue;
+    const uint8_t* k = kb + koff[i];
+    o.part[so] = ld_unaligned<int32_t>(k);
+    o.src[so] = ld_unaligned<int64_t>(k + 4);
+    o.ver[so] = ld_unaligned<int64_t>(k + 16);
+    o.seq[so] = seq0 + i;
+    const uint8_t* row = vb + voff[i];
+    int64_t len = int64_t(voff[i + 1] - voff[i]);
+    if (len > 0) {
+      int verBytes = row[0] >> 5;
+      int32_t rv = 0;
+      if (verBytes > 0 && verBytes + 1 <= len)
+        for (int b = 0; b < verBytes; b++) rv |= int32_t(uint32_t(row[1 + b]) << (8 * b));
+      if (rv != sver) atomicAdd(err + 1, 1ull);
+    }
+    decode_row(row, len, sch, heap_base + int64_t(voff[i]), o, so, err);
   }
 }
 
@@ -269,6 +305,7 @@ static StageOut stage_ptrs(Staging& s, size_t nf) {
   o.dst = s.dst.as<int64_t>();
   o.rank = s.rank.as<int64_t>();
   o.ver = s.ver.as<int64_t>();
+  o.seq = s.seq.as<int64_t>();
   for (size_t f = 0; f < nf && f < size_t(kMaxFields); f++) {
     o.props[f] = f < s.props.size() ? s.props[f].as<int64_t>() : nullptr;
     o.present[f] = f < s.present.size() ? s.present[f].as<uint8_t>() : nullptr;
@@ -283,7 +320,7 @@ void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
   if (part < 0 || part > c.num_parts) throw Error(NBG_E_PART_NOT_FOUND, "part out of range");
   if (owner_of_part(part, c.world) != c.rank)
     throw Error(NBG_E_PART_NOT_FOUND, "part " + std::to_string(part) + " is not owned by this rank");
-  if (c.edges.empty()) throw Error(NBG_E_STATE, "no edge schema registered");
+  if (c.edges.empty() && c.tags.empty()) throw Error(NBG_E_STATE, "no edge or tag schema registered");
   if (n == 0) return;
   double t0 = now_s();
   size_t kbytes = koff[n], vbytes = voff[n];
@@ -318,7 +355,7 @@ void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
     StageOut si = stage_ptrs(es.in_stage, 0);
     k_decode_kv<<<grid_for(int64_t(n)), 256, 0, c.stream>>>(
         dk.as<uint8_t>(), dko.as<uint64_t>(), c.heap.as<uint8_t>() + heap_base, dvo.as<uint64_t>(),
-        int64_t(n), es.type, es.schema_ver, sch, heap_base, so, d, si, d + 1, d + 2);
+        int64_t(n), es.type, es.schema_ver, sch, heap_base, c.load_seq, so, d, si, d + 1, d + 2);
     NBG_HIP(hipGetLastError());
     unsigned long long h[4];
     NBG_HIP(hipMemcpyAsync(h, d, 32, hipMemcpyDeviceToHost, c.stream));
@@ -330,6 +367,27 @@ void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
     es.out_stage.rank_const = es.out_stage.ver_const = false;
     es.in_stage.rank_const = es.in_stage.ver_const = false;
   }
+  for (auto& kvp : c.tags) {
+    TagSpace& ts = kvp.second;
+    size_t nf = ts.fields.size();
+    SchemaDev sch{};
+    sch.nfields = int32_t(nf);
+    for (size_t f = 0; f < nf; f++) sch.types[f] = ts.fields[f].type;
+    stage_reserve(c, ts.stage, nf, n, true, ts.fields);
+    NBG_HIP(hipMemsetAsync(cnt.p, 0, 64, c.stream));
+    unsigned long long* d = cnt.as<unsigned long long>();
+    NBG_HIP(hipMemcpyAsync(d, &ts.stage.n, 8, hipMemcpyHostToDevice, c.stream));
+    k_decode_vkv<<<grid_for(int64_t(n)), 256, 0, c.stream>>>(
+        dk.as<uint8_t>(), dko.as<uint64_t>(), c.heap.as<uint8_t>() + heap_base, dvo.as<uint64_t>(), int64_t(n),
+        ts.id, ts.schema_ver, sch, heap_base, c.load_seq, stage_ptrs(ts.stage, nf), d, d + 2);
+    NBG_HIP(hipGetLastError());
+    unsigned long long h[4];
+    NBG_HIP(hipMemcpyAsync(h, d, 32, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    if (h[3] != 0) throw Error(NBG_E_UNSUPPORTED, "tag row schema version differs from the registered version");
+    ts.stage.n = int64_t(h[0]);
+  }
+  c.load_seq += int64_t(n);
   c.build_seconds += now_s() - t0;
 }
 
@@ -416,6 +474,7 @@ void snapshot_gen_rmat(Ctx& c, int32_t scale, int32_t ef, uint64_t seed, int32_t
     s.rank.release();
     s.ver.release();
     s.part.release();
+    s.seq.release();
     s.rank_const = s.ver_const = true;
     s.rank_value = 0;
     s.ver_value = INT64_MAX - 1;
@@ -571,6 +630,10 @@ __global__ void k_edge_keys(const int64_t* src, const int64_t* dst, int64_t n, c
     perm[i] = uint32_t(i);
     dst_g[i] = dg;
   }
+}
+__global__ void k_seq_desc_keys(const int64_t* seq, int64_t n, uint64_t* keys) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    keys[i] = ~uint64_t(seq[i]);
 }
 // multi-pass LSD helpers: gather a 64-bit key through the current permutation
 __global__ void k_gather_key_bswap(const int64_t* vals, const uint32_t* perm, uint64_t* keys, int64_t n) {
@@ -735,8 +798,16 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
     uint32_t* pin = permA.as<uint32_t>();
     uint32_t* pout = permB.as<uint32_t>();
     // start from reverse load order: stable passes then put the LAST write of identical keys
-    // first, so keep-first implements WriteBatch last-write-wins (RocksEngine.cpp:216-230)
-    k_iota_rev_u32<<<grid_for(n), 256, 0, c.stream>>>(pin, n);
+    // first, so keep-first implements WriteBatch last-write-wins (RocksEngine.cpp:216-230).
+    // The decode stage appends tuples in wave order, not load order, so the start permutation
+    // is the staged load sequence numbers sorted descending.
+    if (s.seq.bytes >= size_t(n) * 8) {
+      k_iota_u32<<<grid_for(n), 256, 0, c.stream>>>(permB.as<uint32_t>(), n);
+      k_seq_desc_keys<<<grid_for(n), 256, 0, c.stream>>>(s.seq.as<int64_t>(), n, keyC.as<uint64_t>());
+      radix_pairs<uint64_t, uint32_t>(c, keyC.as<uint64_t>(), keyB.as<uint64_t>(), permB.as<uint32_t>(), pin, n, 64);
+    } else {
+      k_iota_rev_u32<<<grid_for(n), 256, 0, c.stream>>>(pin, n);
+    }
     auto pass_bswap = [&](const DevBuf& vals) {
       k_gather_key_bswap<<<grid_for(n), 256, 0, c.stream>>>(vals.as<int64_t>(), pin, keyC.as<uint64_t>(), n);
       radix_pairs<uint64_t, uint32_t>(c, keyC.as<uint64_t>(), keyB.as<uint64_t>(), pin, pout, n, 64);
@@ -1239,6 +1310,154 @@ static void order_by_degree(Ctx& c, DevBuf& owned, int64_t n_owned) {
   NBG_HIP(hipGetLastError());
 }
 
+// Tag columns over the gidx space.  Winner per vertex = the first key of the prefix
+// (part, vid, tag) in RocksDB bytewise order: smallest LE version bytes, and among identical keys
+// the last write (WriteBatch last-write-wins, RocksEngine.cpp:216-230).  Rows stored in a part
+// other than the vid's own are never reached by the prefix scan (the request part is
+// hash(vid), StorageClient.cpp:238-243), and vids outside every edge have no gidx: both dropped.
+__global__ void k_tag_gather(const int32_t* win, int64_t ng, const int64_t* props, const uint8_t* present,
+                             int64_t* data, uint8_t* pres_out) {
+  for (int64_t g = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; g < ng; g += int64_t(gridDim.x) * blockDim.x) {
+    int32_t w = win[g];
+    bool ok = w >= 0 && present[w] != 0;
+    data[g] = ok ? props[w] : 0;
+    pres_out[g] = ok;
+  }
+}
+__global__ void k_tag_str_len(const int32_t* win, int64_t ng, const uint8_t* present, const int64_t* lens,
+                              int64_t* out) {
+  for (int64_t g = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; g <= ng; g += int64_t(gridDim.x) * blockDim.x) {
+    int32_t w = g < ng ? win[g] : -1;
+    out[g] = (w >= 0 && present[w]) ? lens[w] : 0;
+  }
+}
+__global__ void k_tag_str_copy(const int32_t* win, int64_t ng, const uint8_t* heap, const int64_t* heap_off,
+                               const int64_t* off, uint8_t* out) {
+  for (int64_t g = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; g < ng; g += int64_t(gridDim.x) * blockDim.x) {
+    int64_t len = off[g + 1] - off[g];
+    if (len <= 0) continue;
+    const uint8_t* s = heap + heap_off[win[g]];
+    for (int64_t j = 0; j < len; j++) out[off[g] + j] = s[j];
+  }
+}
+
+// world > 1: every rank fills its owned gidx slice [base[r], base[r+1]); allgather the slices
+// so each rank holds the whole column ($$ props of dsts owned elsewhere)
+static void replicate_owned(Ctx& c, DevBuf& col, size_t w) {
+  std::vector<size_t> rb(size_t(c.world)), ro(size_t(c.world));
+  for (int r = 0; r < c.world; r++) {
+    ro[size_t(r)] = size_t(c.base[size_t(r)]) * w;
+    rb[size_t(r)] = size_t(c.base[size_t(r) + 1] - c.base[size_t(r)]) * w;
+  }
+  DevBuf send;
+  send.alloc(std::max<size_t>(rb[size_t(c.rank)], 8));
+  if (rb[size_t(c.rank)])
+    NBG_HIP(hipMemcpyAsync(send.p, col.as<uint8_t>() + ro[size_t(c.rank)], rb[size_t(c.rank)], hipMemcpyDeviceToDevice,
+                           c.stream));
+  comm_allgatherv_bytes(c, send.p, rb[size_t(c.rank)], col.p, rb.data(), ro.data());
+}
+
+static void build_tag_columns(Ctx& c) {
+  c.tag_refs.clear();
+  const int64_t ng = c.n_global;
+  for (auto& kvp : c.tags) {
+    TagSpace& ts = kvp.second;
+    const int64_t n = ts.stage.n;
+    std::vector<int32_t> win(size_t(std::max<int64_t>(ng, 1)), -1);
+    if (n > 0 && ng > 0) {
+      DevBuf dg;
+      dg.alloc(size_t(n) * 4);
+      lookup_gidx(c, ts.stage.src.as<int64_t>(), dg.as<int32_t>(), n);
+      const size_t nn = static_cast<size_t>(n);
+      std::vector<int32_t> g(nn), part(nn);
+      std::vector<int64_t> vid(nn), ver(nn), seq(nn);
+      NBG_HIP(hipMemcpyAsync(g.data(), dg.p, size_t(n) * 4, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipMemcpyAsync(part.data(), ts.stage.part.p, size_t(n) * 4, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipMemcpyAsync(vid.data(), ts.stage.src.p, size_t(n) * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipMemcpyAsync(ver.data(), ts.stage.ver.p, size_t(n) * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipMemcpyAsync(seq.data(), ts.stage.seq.p, size_t(n) * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      for (int64_t i = 0; i < n; i++) {
+        int32_t gi = g[size_t(i)];
+        if (gi < 0 || part[size_t(i)] != part_of_vid(vid[size_t(i)], c.num_parts)) continue;
+        int32_t& w = win[size_t(gi)];
+        if (w < 0) {
+          w = int32_t(i);
+          continue;
+        }
+        uint64_t a = __builtin_bswap64(uint64_t(ver[size_t(i)])), b = __builtin_bswap64(uint64_t(ver[size_t(w)]));
+        if (a < b || (a == b && seq[size_t(i)] > seq[size_t(w)])) w = int32_t(i);
+      }
+    }
+    DevBuf dwin;
+    dwin.alloc(size_t(std::max<int64_t>(ng, 1)) * 4);
+    NBG_HIP(hipMemcpyAsync(dwin.p, win.data(), size_t(std::max<int64_t>(ng, 1)) * 4, hipMemcpyHostToDevice, c.stream));
+    ts.cols.clear();
+    for (size_t f = 0; f < ts.fields.size(); f++) {
+      PropCol pc;
+      pc.name = ts.fields[f].name;
+      pc.type = ts.fields[f].type;
+      pc.width = 8;
+      pc.data.alloc(size_t(std::max<int64_t>(ng, 1)) * 8);
+      pc.present.alloc(size_t(std::max<int64_t>(ng, 1)));
+      if (n == 0 || ng == 0) {
+        NBG_HIP(hipMemsetAsync(pc.data.p, 0, pc.data.bytes, c.stream));
+        NBG_HIP(hipMemsetAsync(pc.present.p, 0, pc.present.bytes, c.stream));
+      } else {
+        k_tag_gather<<<grid_for(ng), 256, 0, c.stream>>>(dwin.as<int32_t>(), ng, ts.stage.props[f].as<int64_t>(),
+                                                          ts.stage.present[f].as<uint8_t>(), pc.data.as<int64_t>(),
+                                                          pc.present.as<uint8_t>());
+      }
+      if (pc.type == NBG_T_STRING) {
+        DevBuf lens;
+        lens.alloc(size_t(ng + 1) * 8);
+        pc.str_off.alloc(size_t(ng + 1) * 8);
+        if (n == 0 || ng == 0) {
+          NBG_HIP(hipMemsetAsync(lens.p, 0, lens.bytes, c.stream));
+        } else {
+          k_tag_str_len<<<grid_for(ng + 1), 256, 0, c.stream>>>(dwin.as<int32_t>(), ng, ts.stage.present[f].as<uint8_t>(),
+                                                                 ts.stage.str_len[f].as<int64_t>(), lens.as<int64_t>());
+        }
+        exclusive_scan<int64_t>(c, lens.as<int64_t>(), pc.str_off.as<int64_t>(), ng + 1);
+        int64_t total = 0;
+        NBG_HIP(hipMemcpyAsync(&total, pc.str_off.as<int64_t>() + ng, 8, hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipStreamSynchronize(c.stream));
+        pc.str_bytes.alloc(size_t(total) + 8);
+        if (total > 0)
+          k_tag_str_copy<<<grid_for(ng), 256, 0, c.stream>>>(dwin.as<int32_t>(), ng, c.heap.as<uint8_t>(),
+                                                              ts.stage.props[f].as<int64_t>(), pc.str_off.as<int64_t>(),
+                                                              pc.str_bytes.as<uint8_t>());
+        if (c.world > 1) {
+          // lengths of every rank's owned slice -> global offsets; bytes by owner block
+          replicate_owned(c, lens, 8);
+          exclusive_scan<int64_t>(c, lens.as<int64_t>(), pc.str_off.as<int64_t>(), ng + 1);
+          std::vector<int64_t> goff(size_t(ng) + 1);
+          NBG_HIP(hipMemcpyAsync(goff.data(), pc.str_off.p, size_t(ng + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+          NBG_HIP(hipStreamSynchronize(c.stream));
+          std::vector<size_t> rb(size_t(c.world)), ro(size_t(c.world));
+          for (int r = 0; r < c.world; r++) {
+            ro[size_t(r)] = size_t(goff[size_t(c.base[size_t(r)])]);
+            rb[size_t(r)] = size_t(goff[size_t(c.base[size_t(r) + 1])]) - ro[size_t(r)];
+          }
+          DevBuf all;
+          all.alloc(size_t(goff[size_t(ng)]) + 8);
+          comm_allgatherv_bytes(c, pc.str_bytes.p, size_t(total), all.p, rb.data(), ro.data());
+          pc.str_bytes = std::move(all);
+        }
+      }
+      if (c.world > 1) {
+        replicate_owned(c, pc.data, 8);
+        replicate_owned(c, pc.present, 1);
+      }
+      NBG_HIP(hipGetLastError());
+      c.tag_refs.push_back(TagFieldRef{ts.name, pc.name, pc.type});
+      ts.cols.push_back(std::move(pc));
+    }
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    ts.stage = Staging{};
+  }
+}
+
 void snapshot_finalize(Ctx& c) {
   if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
   double t0 = now_s();
@@ -1380,6 +1599,7 @@ void snapshot_finalize(Ctx& c) {
   NBG_HIP(hipMemcpyAsync(&c.ht_min_gidx, dmin.p, 4, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
   c.ht_has_min = c.ht_min_gidx >= 0;
+  build_tag_columns(c);
   // 5. bytewise order rank of every vertex (for CSR row order = RocksDB key order)
   DevBuf brank;
   {

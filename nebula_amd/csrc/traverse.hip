@@ -31,7 +31,8 @@
 namespace nbg {
 
 int32_t compile_expr(const uint8_t* buf, size_t len, const std::vector<Field>& fields, bool graphd,
-                     bool out_bound, Program* out, std::string* msg);
+                     bool out_bound, Program* out, std::string* msg,
+                     const std::vector<TagFieldRef>* tags = nullptr);
 Program program_dst();
 FastPred classify_pred(const Program& p, const std::vector<Field>& fields);
 
@@ -68,6 +69,7 @@ struct EvalEnv {
   const int64_t* vid_of;
   const int32_t* col;
   const int64_t* rank;
+  const PropDev* tprops;  // tag columns over the gidx space (Ctx::tag_refs order), or null
 };
 
 __device__ inline int64_t load_int(const void* data, int width, int64_t i) {
@@ -188,6 +190,8 @@ __device__ Val eval_program(const Program* __restrict__ P, const EvalEnv& env, i
       case P_SRC: st[sp++] = mk(VT_INT, env.vid_of[src_g]); break;
       case P_RANK: st[sp++] = mk(VT_INT, env.rank ? env.rank[ge] : 0); break;
       case P_TYPE: st[sp++] = mk(VT_INT, env.etype); break;
+      case P_SRCTAG: st[sp++] = load_prop(env.tprops[in.arg], src_g); break;
+      case P_DSTTAG: st[sp++] = load_prop(env.tprops[in.arg], dst_g); break;
       case P_UNARY: {
         Val& a = st[sp - 1];
         if (a.t == VT_ERR) break;
@@ -1240,6 +1244,7 @@ __global__ void k_local_to_vid(const int32_t* loc, int64_t n, int64_t lo, const 
 struct ColOut {
   void* data;
   int32_t type;  // VT_*
+  int64_t* len;  // VT_STR: byte length per row (`data` holds the device address of the bytes)
 };
 constexpr int kMaxYields = 16;
 struct YieldArgs {
@@ -1260,7 +1265,16 @@ __global__ void k_materialize(const int32_t* rows_src, const int64_t* rows_edge,
       }
       if (v.t == VT_BOOL) static_cast<uint8_t*>(ya.cols[c].data)[i] = uint8_t(v.b != 0);
       else static_cast<int64_t*>(ya.cols[c].data)[i] = v.b;
+      if (v.t == VT_STR) ya.cols[c].len[i] = v.len;
     }
+  }
+}
+// STRING YIELD columns: (address, length) per row -> packed bytes at exclusive-scan offsets
+__global__ void k_str_pack(const int64_t* addr, const int64_t* off, int64_t n, uint8_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const uint8_t* s = reinterpret_cast<const uint8_t*>(uintptr_t(addr[i]));
+    const int64_t len = off[i + 1] - off[i];
+    for (int64_t j = 0; j < len; j++) out[off[i] + j] = s[j];
   }
 }
 // fast path for YIELD e._dst (the default YIELD)
@@ -1275,15 +1289,30 @@ __global__ void k_yield_dst(const int64_t* rows_edge, int64_t n, const int32_t* 
 __device__ inline uint64_t row_hash(const YieldArgs& ya, int64_t i) {
   uint64_t h = 0x12345678ull;
   for (int c = 0; c < ya.ncols; c++) {
-    uint64_t w = ya.cols[c].type == VT_BOOL ? static_cast<const uint8_t*>(ya.cols[c].data)[i]
-                                            : uint64_t(static_cast<const int64_t*>(ya.cols[c].data)[i]);
+    uint64_t w;
+    if (ya.cols[c].type == VT_STR) {  // by content: equal strings may sit at different addresses
+      const uint8_t* p = reinterpret_cast<const uint8_t*>(uintptr_t(static_cast<const int64_t*>(ya.cols[c].data)[i]));
+      const int64_t len = ya.cols[c].len[i];
+      w = 0xcbf29ce484222325ull ^ uint64_t(len);
+      for (int64_t k = 0; k < len; k++) w = (w ^ p[k]) * 0x100000001b3ull;
+    } else {
+      w = ya.cols[c].type == VT_BOOL ? static_cast<const uint8_t*>(ya.cols[c].data)[i]
+                                     : uint64_t(static_cast<const int64_t*>(ya.cols[c].data)[i]);
+    }
     h = splitmix64(h ^ w);
   }
   return h;
 }
 __device__ inline bool row_eq(const YieldArgs& ya, int64_t i, int64_t j) {
   for (int c = 0; c < ya.ncols; c++) {
-    if (ya.cols[c].type == VT_BOOL) {
+    if (ya.cols[c].type == VT_STR) {
+      const int64_t li = ya.cols[c].len[i];
+      if (li != ya.cols[c].len[j]) return false;
+      const uint8_t* a = reinterpret_cast<const uint8_t*>(uintptr_t(static_cast<const int64_t*>(ya.cols[c].data)[i]));
+      const uint8_t* b = reinterpret_cast<const uint8_t*>(uintptr_t(static_cast<const int64_t*>(ya.cols[c].data)[j]));
+      for (int64_t k = 0; k < li; k++)
+        if (a[k] != b[k]) return false;
+    } else if (ya.cols[c].type == VT_BOOL) {
       if (static_cast<const uint8_t*>(ya.cols[c].data)[i] != static_cast<const uint8_t*>(ya.cols[c].data)[j]) return false;
     } else if (static_cast<const int64_t*>(ya.cols[c].data)[i] != static_cast<const int64_t*>(ya.cols[c].data)[j]) {
       return false;
@@ -1330,6 +1359,16 @@ EvalEnv make_env(Ctx& c, EdgeSpace& es, Csr& csr, int32_t etype) {
     NBG_HIP(hipMemcpy(csr.prop_table.p, tab.data(), sizeof(PropDev) * tab.size(), hipMemcpyHostToDevice));
   }
   env.props = csr.prop_table.as<PropDev>();
+  if (!c.tag_refs.empty() && !c.tag_table.p) {
+    std::vector<PropDev> tab;
+    for (auto& kv : c.tags)
+      for (const PropCol& p : kv.second.cols)
+        tab.push_back(PropDev{p.type, p.width, p.data.p, p.present.as<uint8_t>(), p.str_off.as<int64_t>(),
+                              p.str_bytes.as<uint8_t>()});
+    c.tag_table.alloc(sizeof(PropDev) * tab.size());
+    NBG_HIP(hipMemcpy(c.tag_table.p, tab.data(), sizeof(PropDev) * tab.size(), hipMemcpyHostToDevice));
+  }
+  env.tprops = c.tag_table.as<PropDev>();
   env.etype = etype;
   env.vid_of = c.vid_of.as<int64_t>();
   env.col = csr.col.as<int32_t>();
@@ -1742,7 +1781,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   int32_t deferred = NBG_OK;
   std::string deferred_msg;
   if (has_where) {
-    int32_t rc = compile_expr(s.where, s.where_len, es.fields, true, true, &where, &msg);
+    int32_t rc = compile_expr(s.where, s.where_len, es.fields, true, true, &where, &msg, &c.tag_refs);
     if (rc == NBG_E_UNSUPPORTED || rc == NBG_E_INVALID_ARG) throw Error(rc, "WHERE: " + msg);
     if (rc != NBG_OK) {
       deferred = rc;
@@ -1757,13 +1796,14 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     if (s.n_yields > size_t(kMaxYields)) throw Error(NBG_E_UNSUPPORTED, "too many YIELD columns");
     for (size_t i = 0; i < s.n_yields; i++) {
       Program p{};
-      int32_t rc = compile_expr(s.yields[i], s.yield_lens[i], es.fields, true, true, &p, &msg);
+      int32_t rc = compile_expr(s.yields[i], s.yield_lens[i], es.fields, true, true, &p, &msg, &c.tag_refs);
       if (rc == NBG_E_UNSUPPORTED || rc == NBG_E_INVALID_ARG) throw Error(rc, "YIELD: " + msg);
       if (rc != NBG_OK && deferred == NBG_OK) {
         deferred = rc;
         deferred_msg = "YIELD: " + msg;
       }
-      if (rc == NBG_OK && p.result_type == VT_STR) throw Error(NBG_E_UNSUPPORTED, "STRING YIELD columns");
+      if (rc == NBG_OK && p.result_type == VT_STR && s.distinct && c.world > 1)
+        throw Error(NBG_E_UNSUPPORTED, "DISTINCT over STRING YIELD columns across ranks");
       yields.push_back(p);
     }
   }
@@ -1969,6 +2009,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   bool distinct_dst = s.distinct && yields.size() == 1 && yields[0].n == 1 && yields[0].ins[0].op == P_DST;
   auto* h = new HostRows();
   int64_t nrows = 0;
+  std::vector<DevBuf> slen(yields.size());  // STRING yield columns: byte length per row
   try {
     if (distinct_dst) {
       // DISTINCT e._dst: mark surviving dsts, compact the whole vertex space (no deg filter).
@@ -2090,8 +2131,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         DevBuf b;
         if (dst_only) b = std::move(fused);
         else b.alloc(size_t(nrows + 1) * (t == VT_BOOL ? 1 : 8));
-        ya.cols[h->types.size()] = ColOut{b.p, t};
-        h->types.push_back(t == VT_DOUBLE ? NBG_T_DOUBLE : t == VT_BOOL ? NBG_T_BOOL : NBG_T_VID);
+        const size_t k = h->types.size();
+        if (t == VT_STR) slen[k].alloc(size_t(nrows + 1) * 8);
+        ya.cols[k] = ColOut{b.p, t, slen[k].as<int64_t>()};
+        h->types.push_back(t == VT_DOUBLE ? NBG_T_DOUBLE : t == VT_BOOL ? NBG_T_BOOL : t == VT_STR ? NBG_T_STRING : NBG_T_VID);
         h->dev.push_back(std::move(b));
       }
       if (nrows && !dst_only) {
@@ -2139,6 +2182,16 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
             NBG_HIP(rocprim::select(c.ws_tmp.p, tb, h->dev[cc].as<int64_t>(), keep.as<uint8_t>(), nb.as<int64_t>(),
                                     cnt.as<uint64_t>(), size_t(nrows), c.stream));
           }
+          if (ya.cols[cc].type == VT_STR) {
+            DevBuf nl;
+            nl.alloc(size_t(nrows + 1) * 8);
+            NBG_HIP(rocprim::select(nullptr, tb, slen[cc].as<int64_t>(), keep.as<uint8_t>(), nl.as<int64_t>(),
+                                    cnt.as<uint64_t>(), size_t(nrows), c.stream));
+            c.ws_tmp.ensure(tb);
+            NBG_HIP(rocprim::select(c.ws_tmp.p, tb, slen[cc].as<int64_t>(), keep.as<uint8_t>(), nl.as<int64_t>(),
+                                    cnt.as<uint64_t>(), size_t(nrows), c.stream));
+            slen[cc] = std::move(nl);
+          }
           uint64_t kc = 0;
           NBG_HIP(hipMemcpyAsync(&kc, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
           NBG_HIP(hipStreamSynchronize(c.stream));
@@ -2157,9 +2210,52 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   float ms = 0;
   hipEventElapsedTime(&ms, c.ev[0], c.ev[1]);
   c.timing.total_ms = ms;
+  // STRING columns: (address, length) rows -> packed bytes + n+1 offsets
+  const size_t ncols_out = h->types.size();
+  std::vector<int64_t> soff_dev_idx(ncols_out, -1);
+  try {
+    for (size_t cc = 0; cc < ncols_out; cc++) {
+      if (h->types[cc] != NBG_T_STRING) continue;
+      DevBuf off, bytes;
+      off.alloc(size_t(nrows + 1) * 8);
+      NBG_HIP(hipMemsetAsync(slen[cc].as<int64_t>() + nrows, 0, 8, c.stream));
+      exclusive_scan_dev<int64_t>(c, slen[cc].as<int64_t>(), off.as<int64_t>(), nrows + 1);
+      int64_t total = 0;
+      NBG_HIP(hipMemcpyAsync(&total, off.as<int64_t>() + nrows, 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      bytes.alloc(size_t(total) + 8);
+      if (nrows && total)
+        k_str_pack<<<grid_cap(nrows), 256, 0, c.stream>>>(h->dev[cc].as<int64_t>(), off.as<int64_t>(), nrows,
+                                                          bytes.as<uint8_t>());
+      NBG_HIP(hipGetLastError());
+      h->dev[cc] = std::move(bytes);
+      soff_dev_idx[cc] = int64_t(h->dev.size());
+      h->dev.push_back(std::move(off));
+    }
+    NBG_HIP(hipStreamSynchronize(c.stream));
+  } catch (...) {
+    delete h;
+    throw;
+  }
   // hand the columns out
   bool on_dev = s.keep_on_device != 0;
-  for (size_t cc = 0; cc < h->types.size(); cc++) {
+  for (size_t cc = 0; cc < ncols_out; cc++) {
+    if (soff_dev_idx[cc] >= 0) {  // STRING
+      DevBuf& off = h->dev[size_t(soff_dev_idx[cc])];
+      if (on_dev) {
+        h->cols.push_back(h->dev[cc].p);
+        h->str_off.push_back(off.as<int64_t>());
+      } else {
+        h->host_off.emplace_back(size_t(nrows) + 1);
+        NBG_HIP(hipMemcpy(h->host_off.back().data(), off.p, size_t(nrows + 1) * 8, hipMemcpyDeviceToHost));
+        const size_t total = size_t(h->host_off.back()[size_t(nrows)]);
+        h->host.emplace_back(total + 8);
+        if (total) NBG_HIP(hipMemcpy(h->host.back().data(), h->dev[cc].p, total, hipMemcpyDeviceToHost));
+        h->cols.push_back(h->host.back().data());
+        h->str_off.push_back(h->host_off.back().data());
+      }
+      continue;
+    }
     h->str_off.push_back(nullptr);
     if (on_dev) {
       h->cols.push_back(h->dev[cc].p);

@@ -158,6 +158,13 @@ class GraphSpace:
         types = (C.c_int32 * max(len(fields), 1))(*[t for _, t in fields])
         self._check(self.L.nbg_schema_set_edge(self.h, edge_type, ver, len(fields), names, types))
 
+    def set_tag_schema(self, tag_id: int, name: str, fields: Sequence[tuple[str, int]], ver: int = 0):
+        """Tag schema + name (SchemaManager::getTagSchema / toTagID): enables $^.name.prop and
+        $$.name.prop in GO WHERE / YIELD."""
+        names = (C.c_char_p * max(len(fields), 1))(*[f.encode() for f, _ in fields])
+        types = (C.c_int32 * max(len(fields), 1))(*[t for _, t in fields])
+        self._check(self.L.nbg_schema_set_tag(self.h, tag_id, name.encode(), ver, len(fields), names, types))
+
     def load_part(self, part: int, pairs):
         kb, koff, vb, voff = pairs if isinstance(pairs, tuple) else pack_kv(pairs)
         n = len(koff) - 1
