@@ -242,3 +242,40 @@ def test_sharded_shortest_path(rmat_group, oracle12):
         row = [x for x in row if x is not None]
         want[(row[0], row[1], row[2], tuple(row[3:]))] += 1
     assert got == want
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_tag_props(world):
+    """$^ / $$ tag props with sharded ownership: each rank decodes the vertex keys of its own
+    parts and the tag columns are replicated by owner slice, so $$ props of dsts owned by
+    another rank resolve (the reference's fetchVertexProps asks the dst's host)."""
+    import test_gpu_tags as T
+    parts, vids = T.random_space_kv(3)
+    fields = [("name", O.STRING), ("score", O.INT), ("wt", O.DOUBLE)]
+    st = O.Store(T.PARTS)
+    st.set_edge_schema(T.ET, [("weight", O.INT)], name="e")
+    st.set_tag_schema(T.PERSON, fields, name="person")
+    for p, kv in parts.items():
+        if kv:
+            st.put(p, kv)
+    st.finalize()
+    g = Group(world, parts=T.PARTS)
+    try:
+        def load(r, s):
+            s.set_edge_schema(T.ET, [("weight", O.INT)])
+            s.set_tag_schema(T.PERSON, "person", fields)
+            for p, kv in parts.items():
+                if kv and p % world == r:
+                    s.load_part(p, kv)
+            s.finalize()
+        g.each(load)
+        for qi in (0, 1, 3):
+            steps, where, ys, distinct = T.QUERIES[qi]
+            starts = vids[::23]
+            res = g.go(starts, steps, T.ET, where=where, yields=ys, distinct=distinct)
+            ref = st.go(starts, steps, T.ET, where=X.encode(where), yields=[y.encode() for y in ys],
+                        distinct=distinct)
+            assert ref.code == 0, ref.error
+            assert union_rows(res) == ms(ref.rows())
+    finally:
+        g.close()
