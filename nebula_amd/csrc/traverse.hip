@@ -1079,17 +1079,30 @@ __global__ __launch_bounds__(256) void k_bits_compact(const uint32_t* __restrict
     if (threadIdx.x == 0) s_base = total ? atomicAdd(n_out, (unsigned long long)total) : 0ull;
     __syncthreads();
     if (total) {
+      // U word pairs per step: the step's U vid_of loads are issued before any of its stores,
+      // so each lane keeps U HBM requests in flight instead of one load -> store chain per pair
+      constexpr int U = 4;
       const unsigned long long base = s_base;
       const int half = lane >> 5, bit = lane & 31;
-      for (int j = wv * (kTileWords / 4); j < (wv + 1) * (kTileWords / 4); j += 2) {
-        const int wi = j + half;
-        const uint32_t xw = sw[wi];
-        if (__ballot(xw != 0) == 0) continue;
-        if ((xw >> bit) & 1u) {
-          const unsigned long long p = base + so[wi] + __popc(xw & ((1u << bit) - 1u));
+      for (int j = wv * (kTileWords / 4); j < (wv + 1) * (kTileWords / 4); j += 2 * U) {
+        bool has[U];
+        unsigned long long p[U];
+        int64_t val[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int wi = j + 2 * u + half;
+          const uint32_t xw = sw[wi];
+          has[u] = (xw >> bit) & 1u;
+          p[u] = base + so[wi] + __popc(xw & ((1u << bit) - 1u));
           const int64_t v = (t * kTileWords + wi) * 32 + bit;
-          if (MODE == 0) static_cast<int32_t*>(out)[p] = int32_t(v);
-          else static_cast<int64_t*>(out)[p] = vid_of[lo + v];
+          val[u] = v;
+          if (MODE == 1 && has[u]) val[u] = vid_of[lo + v];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          if (!has[u]) continue;
+          if (MODE == 0) static_cast<int32_t*>(out)[p[u]] = int32_t(val[u]);
+          else static_cast<int64_t*>(out)[p[u]] = val[u];
         }
       }
     }
@@ -1115,7 +1128,7 @@ __global__ void k_degrees(const int32_t* F, int64_t nF, const int64_t* row_ptr, 
 __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64_t n, const int64_t* row_ptr,
                                                  const uint8_t* row_ok, int require_deg, int32_t* out,
                                                  unsigned long long* n_out, unsigned long long* partials,
-                                                 uint16_t* bits) {
+                                                 uint16_t* bits, const uint32_t* __restrict__ odeg) {
   // tile = 256 threads x 4 chunks of 16 bytes = 16384 vertices; one returning atomic per tile;
   // n_set (partials[0]) and the kept out-degree sum (partials[1]) go to per-block partials.
   __shared__ uint32_t lds[8];
@@ -1141,7 +1154,28 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
         for (int b = 0; b < 4; b++)
           if ((words[a] >> (8 * b)) & 0xff) setmask |= 1u << (a * 4 + b);
       uint32_t keepmask = setmask;
-      if (require_deg && setmask) {
+      if (require_deg && setmask && odeg) {
+        // out-degrees (0 where row_ok == 0) of the chunk's 16 vertices: four 16-byte loads issued
+        // together, instead of a dependent row_ptr pair per set vertex (hub tiles are dense)
+        uint32_t dg[16];
+        if ((ch + 1) * 16 <= n) {
+          const uint4* p4 = reinterpret_cast<const uint4*>(odeg + ch * 16);
+#pragma unroll
+          for (int a = 0; a < 4; a++) {
+            const uint4 v4 = p4[a];
+            dg[a * 4 + 0] = v4.x, dg[a * 4 + 1] = v4.y, dg[a * 4 + 2] = v4.z, dg[a * 4 + 3] = v4.w;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 16; j++) dg[j] = ch * 16 + j < n ? odeg[ch * 16 + j] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+          if (!((setmask >> j) & 1u)) continue;
+          if (dg[j] == 0) keepmask &= ~(1u << j);
+          else acc[1] += dg[j];
+        }
+      } else if (require_deg && setmask) {
         for (uint32_t m = setmask; m; m &= m - 1) {
           const int j = __ffs(m) - 1;
           const int64_t v = ch * 16 + j;
@@ -1576,12 +1610,13 @@ int64_t degree_scan(Ctx& c, const int32_t* F, int64_t nF, const Csr& csr, DevBuf
 }
 
 void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* row_ptr, const uint8_t* row_ok,
-                    int require_deg, int32_t* out, uint16_t* bits, unsigned long long* Kd) {
+                    int require_deg, int32_t* out, uint16_t* bits, unsigned long long* Kd,
+                    const uint32_t* odeg = nullptr) {
   // counters: Kd[0] list length (atomic), Kd[12] vertices set, Kd[13] kept out-degree sum
   unsigned long long* partials = c.ws_partials.as<unsigned long long>();
   int64_t ntiles = ((n + 15) / 16 + 1023) / 1024;
   int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, kAggBlocks)));
-  k_compact<<<grid, 256, 0, c.stream>>>(map, lo, n, row_ptr, row_ok, require_deg, out, Kd, partials, bits);
+  k_compact<<<grid, 256, 0, c.stream>>>(map, lo, n, row_ptr, row_ok, require_deg, out, Kd, partials, bits, odeg);
   k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, Kd + 12);
   NBG_HIP(hipGetLastError());
 }
@@ -1841,7 +1876,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       k_list_starts<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, F, K.d);
     } else {
       k_mark_gidx<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, map);
-      launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, F, bits16, K.d);
+      launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, F, bits16, K.d, es.odeg.as<uint32_t>());
     }
     NBG_HIP(hipGetLastError());
     NBG_HIP(hipMemcpyAsync(K.h, K.d, 128, hipMemcpyDeviceToHost, c.stream));
@@ -1858,7 +1893,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   auto finish_empty = [&]() -> int32_t {
     auto* h = new HostRows();
     for (auto& p : yields) {
-      h->types.push_back(p.result_type == VT_DOUBLE ? NBG_T_DOUBLE : p.result_type == VT_BOOL ? NBG_T_BOOL : NBG_T_VID);
+      h->types.push_back(p.result_type == VT_DOUBLE ? NBG_T_DOUBLE
+                         : p.result_type == VT_BOOL ? NBG_T_BOOL
+                         : p.result_type == VT_STR  ? NBG_T_STRING
+                                                    : NBG_T_VID);
       h->cols.push_back(nullptr);
       h->str_off.push_back(nullptr);
     }
@@ -1973,7 +2011,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       cur ^= 1;
       F = c.ws_front[cur].as<int32_t>();
       NBG_HIP(hipMemsetAsync(K.d, 0, 32, c.stream));
-      launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, F, reinterpret_cast<uint16_t*>(bitsA), K.d);
+      launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, F, reinterpret_cast<uint16_t*>(bitsA), K.d,
+                     es.odeg.as<uint32_t>());
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 128, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
       nF = int64_t(K.h[0]);

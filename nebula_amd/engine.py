@@ -62,7 +62,9 @@ class RowSet:
                 self.device_ptrs.append(ptr)
                 self.columns.append(None)
                 continue
-            if t == _lib.T_STRING:
+            if t == _lib.T_STRING and (self.n_rows == 0 or not rows.str_offsets[c]):
+                self.columns.append([])
+            elif t == _lib.T_STRING:
                 offs = np.ctypeslib.as_array(rows.str_offsets[c], shape=(self.n_rows + 1,)).copy()
                 raw = C.string_at(ptr, int(offs[-1])) if self.n_rows else b""
                 self.columns.append([raw[offs[i]:offs[i + 1]].decode() for i in range(self.n_rows)])

@@ -82,6 +82,10 @@ def test_nba_tag_vertex_not_exist(nba):
     for distinct in (False, True):
         rs = sp.go([d["nonexist_hash"]], 1, F.NBA_SERVE, yields=tag_yields(), distinct=distinct)
         assert names(vid, rs.rows()) == golden(d, "tag_vertex_not_exist")
+        # frontier empties before the final step (onEmptyInputs): typed empty STRING columns
+        rs = sp.go([d["nonexist_hash"], vid["Spurs"]], 2, F.NBA_LIKE, yields=[X.DestProp("player", "name")],
+                   distinct=distinct)
+        assert rs.n_rows == 0 and rs.rows() == []
 
 
 @pytest.mark.parametrize("steps", [1, 2, 3])
