@@ -58,6 +58,10 @@ nbg_ctx* nbg_ctx_create(int32_t device, int32_t num_parts, int32_t rank, int32_t
     return nullptr;
   }
   memset(ctx->c.host_counters, 0, 64 * 8);
+  // pinned staging for a query's small host->device inputs (starts, compiled programs): copies
+  // from pageable memory go through a driver bounce buffer and block the calling thread
+  if (hipHostMalloc(&ctx->c.host_stage, nbg::kHostStageBytes, hipHostMallocDefault) != hipSuccess)
+    ctx->c.host_stage = nullptr;
   return ctx;
 }
 
@@ -67,7 +71,9 @@ void nbg_ctx_destroy(nbg_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->c.stream);
   nbg::comm_destroy(ctx->c);
   for (auto& e : ctx->c.ev) (void)hipEventDestroy(e);
+  for (auto& e : ctx->c.tev) (void)hipEventDestroy(e);
   if (ctx->c.host_counters) (void)hipHostFree(ctx->c.host_counters);
+  if (ctx->c.host_stage) (void)hipHostFree(ctx->c.host_stage);
   (void)hipStreamDestroy(ctx->c.stream);
   delete ctx;
 }
@@ -220,7 +226,9 @@ int32_t nbg_get_bound(nbg_ctx* ctx, int32_t edge_type, const int32_t* parts, con
     if (!out || (n && (!parts || !vids)) || (ncols && !cols) || (filter_len && !filter))
       throw Error(NBG_E_INVALID_ARG, "bad arguments");
     memset(out, 0, sizeof(*out));
-    return nbg::get_bound_run(c, edge_type, parts, vids, n, filter, filter_len, cols, ncols, out);
+    const int32_t rc = nbg::get_bound_run(c, edge_type, parts, vids, n, filter, filter_len, cols, ncols, out);
+    nbg::timing_resolve(c);
+    return rc;
   });
 }
 
@@ -231,7 +239,9 @@ int32_t nbg_bound_stats(nbg_ctx* ctx, int32_t edge_type, const int32_t* parts, c
     if (!out || (n && (!parts || !vids)) || (ncols && (!cols || !stat_types)) || (filter_len && !filter))
       throw Error(NBG_E_INVALID_ARG, "bad arguments");
     memset(out, 0, sizeof(*out));
-    return nbg::get_bound_run(c, edge_type, parts, vids, n, filter, filter_len, cols, ncols, out, stat_types);
+    const int32_t rc = nbg::get_bound_run(c, edge_type, parts, vids, n, filter, filter_len, cols, ncols, out, stat_types);
+    nbg::timing_resolve(c);
+    return rc;
   });
 }
 
@@ -241,7 +251,9 @@ int32_t nbg_go(nbg_ctx* ctx, const nbg_go_spec* spec, nbg_rows* out) {
         (spec->n_yields && (!spec->yields || !spec->yield_lens)))
       throw Error(NBG_E_INVALID_ARG, "bad arguments");
     memset(out, 0, sizeof(*out));
-    return nbg::go_run(c, *spec, out);
+    const int32_t rc = nbg::go_run(c, *spec, out);
+    nbg::timing_resolve(c);
+    return rc;
   });
 }
 

@@ -258,6 +258,8 @@ struct Timing {
   }
 };
 
+constexpr size_t kHostStageBytes = size_t(1) << 20;
+
 struct Ctx {
   int32_t device = 0, num_parts = 1, rank = 0, world = 1;
   hipStream_t stream = nullptr;
@@ -310,8 +312,31 @@ struct Ctx {
   } sp;
   Timing timing;
   hipEvent_t ev[8] = {};
+  // deferred kernel timing: event pairs recorded around expansion launches and read once the
+  // query's stream has drained, so timing never makes the host wait on a launch
+  struct PendingTime {
+    size_t a, b;
+    int32_t hop;  // Timing::hops index the time belongs to (-1: none)
+  };
+  std::vector<hipEvent_t> tev;
+  size_t tev_used = 0;
+  std::vector<PendingTime> tpend;
   std::shared_ptr<BufPool> pool = std::make_shared<BufPool>();
   unsigned long long* host_counters = nullptr;  // pinned, 64 entries
+  void* host_stage = nullptr;                   // pinned, kHostStageBytes (query inputs)
+  size_t host_stage_used = 0;
+  // async host->device copy of a query input through the pinned stage when it fits (the stage
+  // is reset at every query start; the stream drains before a query returns)
+  void h2d(void* dst, const void* src, size_t bytes) {
+    if (host_stage && host_stage_used + bytes <= kHostStageBytes) {
+      uint8_t* p = static_cast<uint8_t*>(host_stage) + host_stage_used;
+      memcpy(p, src, bytes);
+      host_stage_used += (bytes + 255) & ~size_t(255);
+      NBG_HIP(hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, stream));
+    } else {
+      NBG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+    }
+  }
   std::map<std::string, int64_t> options;
 
   int64_t owned_lo() const { return base.empty() ? 0 : base[size_t(rank)]; }
@@ -336,6 +361,8 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
                       nbg_rows* out, const int32_t* stats = nullptr);
 int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src, const int64_t* dst, size_t n,
                           int32_t max_steps, nbg_rows* out);
+void timing_reset(Ctx& c);
+void timing_resolve(Ctx& c);
 // comm.cpp
 void comm_alltoallv_bytes(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off,
                           void* recv, const size_t* recv_bytes, const size_t* recv_off);

@@ -1621,23 +1621,31 @@ void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* 
   NBG_HIP(hipGetLastError());
 }
 
+// records a pooled timing event on the query stream; returns its pool index
+size_t timing_event(Ctx& c) {
+  if (c.tev_used == c.tev.size()) {
+    hipEvent_t e;
+    NBG_HIP(hipEventCreate(&e));
+    c.tev.push_back(e);
+  }
+  NBG_HIP(hipEventRecord(c.tev[c.tev_used], c.stream));
+  return c.tev_used++;
+}
+
 template <int MODE>
 void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Program* dprog, const EvalEnv& env,
                    int64_t E) {
   int64_t ntiles = (E + kTile - 1) / kTile;
   int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, int64_t(c.opt("expand_grid", 256 * 8)))));
-  hipEventRecord(c.ev[2], c.stream);
+  const size_t ia = timing_event(c);
   switch (pk) {
     case PK_NONE: k_expand<MODE, PK_NONE><<<grid, kThreads, 0, c.stream>>>(a, fp, dprog, env); break;
     case PK_FAST: k_expand<MODE, PK_FAST><<<grid, kThreads, 0, c.stream>>>(a, fp, dprog, env); break;
     default: k_expand<MODE, PK_VM><<<grid, kThreads, 0, c.stream>>>(a, fp, dprog, env); break;
   }
   NBG_HIP(hipGetLastError());
-  hipEventRecord(c.ev[3], c.stream);
-  NBG_HIP(hipEventSynchronize(c.ev[3]));
-  float ms = 0;
-  hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
-  c.timing.expand_ms += ms;
+  const size_t ib = timing_event(c);
+  c.tpend.push_back(Ctx::PendingTime{ia, ib, c.timing.n_hops});  // read by timing_resolve
   c.timing.expand_launches++;
 }
 
@@ -1806,6 +1814,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   EdgeSpace& es = it->second;
   Csr& csr = es.out;
   c.timing = Timing{};
+  timing_reset(c);
+  if (c.host_stage_used) NBG_HIP(hipStreamSynchronize(c.stream));  // a failed query's copies
+  c.host_stage_used = 0;
   hipEventRecord(c.ev[0], c.stream);
 
   // compile WHERE / YIELD (errors are deferred to the final step, as the reference only
@@ -1862,7 +1873,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   int64_t* d_starts = c.ws_starts.as<int64_t>();
   int32_t* d_sg = reinterpret_cast<int32_t*>(d_starts + std::max<int64_t>(ns, 1));
   if (ns) {
-    NBG_HIP(hipMemcpyAsync(d_starts, s.starts, size_t(ns) * 8, hipMemcpyHostToDevice, c.stream));
+    c.h2d(d_starts, s.starts, size_t(ns) * 8);
     lookup_gidx(c, d_starts, d_sg, ns);
   }
   int cur = 0;
@@ -1972,12 +1983,15 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       hipEventRecord(c.ev[2], c.stream);
       launch_bu_slab(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, nullptr, K.d,
                      defer ? pb.as<unsigned long long>() : nullptr);
+      if (!defer) hipEventRecord(c.ev[3], c.stream);
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 64, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
-      if (defer) bu_finish(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, pb.as<unsigned long long>(), K.h,
-                           K.d + 40);
-      hipEventRecord(c.ev[3], c.stream);
-      NBG_HIP(hipEventSynchronize(c.ev[3]));
+      if (defer) {
+        bu_finish(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, pb.as<unsigned long long>(), K.h,
+                  K.d + 40);
+        hipEventRecord(c.ev[3], c.stream);
+        NBG_HIP(hipEventSynchronize(c.ev[3]));
+      }
       float ms = 0;
       hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
       c.timing.expand_ms += ms;
@@ -2039,9 +2053,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   DevBuf dprog;
   if (pk == PK_VM || !default_yield) {
     dprog.alloc(sizeof(Program) * (yields.size() + 1));
-    NBG_HIP(hipMemcpyAsync(dprog.p, &where, sizeof(Program), hipMemcpyHostToDevice, c.stream));
-    NBG_HIP(hipMemcpyAsync(dprog.as<Program>() + 1, yields.data(), sizeof(Program) * yields.size(),
-                           hipMemcpyHostToDevice, c.stream));
+    c.h2d(dprog.p, &where, sizeof(Program));
+    c.h2d(dprog.as<Program>() + 1, yields.data(), sizeof(Program) * yields.size());
   }
   int pred_w = pk == PK_FAST ? fp.width : 0;
   c.timing.edges_scanned += uint64_t(E);
@@ -2311,6 +2324,22 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   return NBG_OK;
 }
 
+void timing_reset(Ctx& c) {
+  c.tev_used = 0;
+  c.tpend.clear();
+}
+// adds the deferred expansion times to expand_ms and their hops (after the query's last sync)
+void timing_resolve(Ctx& c) {
+  for (const auto& p : c.tpend) {
+    float ms = 0;
+    if (hipEventSynchronize(c.tev[p.b]) == hipSuccess && hipEventElapsedTime(&ms, c.tev[p.a], c.tev[p.b]) == hipSuccess) {
+      c.timing.expand_ms += ms;
+      if (p.hop >= 0 && p.hop < c.timing.n_hops && p.hop < NBG_MAX_HOP_STATS) c.timing.hops[p.hop].ms += ms;
+    }
+  }
+  timing_reset(c);
+}
+
 // ------------------------------------------------------------------------------------------
 // getBound (QueryBoundProcessor)
 // ------------------------------------------------------------------------------------------
@@ -2556,6 +2585,9 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
   NBG_HIP(hipStreamSynchronize(c.stream));
   int64_t E = hoff[size_t(N)];
   c.timing = Timing{};
+  timing_reset(c);
+  if (c.host_stage_used) NBG_HIP(hipStreamSynchronize(c.stream));  // a failed query's copies
+  c.host_stage_used = 0;
   c.timing.edges_scanned = uint64_t(E);
   // compress away zero-degree request entries for the expansion (tile owner search needs deg>=1)
   std::vector<int32_t> hF(static_cast<size_t>(N));
