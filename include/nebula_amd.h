@@ -201,6 +201,18 @@ typedef struct {
   size_t n_yields;
   int32_t distinct;
   int32_t keep_on_device; /* 1: leave result columns in HBM (bench / chained queries)        */
+  /* $-.prop / $var.prop (GoExecutor::getPropFromInterim, GoExecutor.cpp:831-838): the piped or
+   * variable input rows, one per starts[i] (the FROM column).  A start vid's props come from its
+   * LAST row (InterimResult::buildIndex, InterimResult.cpp:146-160).  Column types NBG_T_VID /
+   * NBG_T_INT / NBG_T_DOUBLE (int64 / double arrays), NBG_T_BOOL (uint8) or NBG_T_STRING (bytes
+   * + n_starts+1 int64 offsets).  Only with steps == 1: a multi-step GO resolves them through a
+   * VertexBackTracker whose result depends on response order (GoExecutor.h:174-193).
+   * n_inputs = 0: no input table (zero-initialised specs stay valid).                        */
+  size_t n_inputs;
+  const char* const* input_names;
+  const int32_t* input_types;
+  const void* const* input_cols;
+  const int64_t* const* input_str_offsets;
 } nbg_go_spec;
 int32_t nbg_go(nbg_ctx* ctx, const nbg_go_spec* spec, nbg_rows* out);
 

@@ -65,7 +65,10 @@ class GoSpec(C.Structure):
     _fields_ = [("edge_type", C.c_int32), ("steps", C.c_int32), ("starts", C.c_void_p),
                 ("n_starts", C.c_size_t), ("where", C.c_void_p), ("where_len", C.c_size_t),
                 ("yields", C.POINTER(C.c_void_p)), ("yield_lens", C.POINTER(C.c_size_t)),
-                ("n_yields", C.c_size_t), ("distinct", C.c_int32), ("keep_on_device", C.c_int32)]
+                ("n_yields", C.c_size_t), ("distinct", C.c_int32), ("keep_on_device", C.c_int32),
+                ("n_inputs", C.c_size_t), ("input_names", C.POINTER(C.c_char_p)),
+                ("input_types", C.POINTER(C.c_int32)), ("input_cols", C.POINTER(C.c_void_p)),
+                ("input_str_offsets", C.POINTER(C.c_void_p))]
 
 
 class HopStat(C.Structure):

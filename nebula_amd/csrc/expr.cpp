@@ -118,6 +118,7 @@ std::unique_ptr<Node> dec(uint8_t kind, Cur& c) {
 struct Compiler {
   const std::vector<Field>& fields;
   const std::vector<TagFieldRef>* tags = nullptr;
+  const std::vector<Field>* inputs = nullptr;  // $- / $var input columns (graphd)
   bool graphd;     // graphd AST semantics (GoExecutor) vs storage-decoded filter
   bool out_bound;
   Program prog;
@@ -260,10 +261,29 @@ struct Compiler {
         return VT_ERR;
       }
       case kInputProp:
-      case kVariableProp:
-        // checkExp rejects these in storage filters; graphd needs pipe inputs (not supported)
-        fail(graphd ? NBG_E_UNSUPPORTED : NBG_E_INVALID_FILTER, "$- / $var props");
+      case kVariableProp: {
+        // checkExp rejects these in storage filters (QueryBaseProcessor.inl:235-238)
+        if (!graphd) {
+          fail(NBG_E_INVALID_FILTER, "$- / $var props in a storage filter");
+          return VT_ERR;
+        }
+        if (!inputs) {
+          fail(NBG_E_UNSUPPORTED, "$- / $var props without an input table");
+          return VT_ERR;
+        }
+        for (size_t i = 0; i < inputs->size(); i++) {
+          if ((*inputs)[i].name != x.prop) continue;
+          emit(P_INPUT, 0, int16_t(i));
+          push();
+          const int32_t t = (*inputs)[i].type;
+          if (t == NBG_T_DOUBLE || t == NBG_T_FLOAT) return VT_DOUBLE;
+          if (t == NBG_T_BOOL) return VT_BOOL;
+          if (t == NBG_T_STRING) return VT_STR;
+          return VT_INT;
+        }
+        fail(NBG_E_INVALID_ARG, "unknown input column " + x.prop);
         return VT_ERR;
+      }
       case kUnary: {
         int32_t t = gen(*x.l);
         emit(P_UNARY, x.op, 0);
@@ -304,7 +324,8 @@ struct Compiler {
 
 // Compiles an encoded expression.  Returns NBG_OK or an error code (msg filled).
 int32_t compile_expr(const uint8_t* buf, size_t len, const std::vector<Field>& fields, bool graphd,
-                     bool out_bound, Program* out, std::string* msg, const std::vector<TagFieldRef>* tags) {
+                     bool out_bound, Program* out, std::string* msg, const std::vector<TagFieldRef>* tags,
+                     const std::vector<Field>* inputs) {
   std::unique_ptr<Node> root;
   try {
     Cur c{buf, buf + len};
@@ -316,6 +337,7 @@ int32_t compile_expr(const uint8_t* buf, size_t len, const std::vector<Field>& f
   }
   Compiler cc(fields, graphd, out_bound);
   cc.tags = tags;
+  cc.inputs = inputs;
   for (int i = 0; i < kMaxConsts; i++) cc.prog.ctype[i] = -1;
   cc.prog.result_type = cc.gen(*root);
   if (cc.code != NBG_OK) {

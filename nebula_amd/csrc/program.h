@@ -30,6 +30,7 @@ enum POp : uint8_t {
   P_LOGIC = 9,   // sub = AND/OR
   P_SRCTAG = 10, // push $^.tag.prop: tag column arg (Ctx::tag_refs) at the edge's src vertex
   P_DSTTAG = 11, // push $$.tag.prop: tag column arg at the edge's dst vertex
+  P_INPUT = 12,  // push $-.prop / $var.prop: input column arg at the row of the edge's src vid
 };
 
 constexpr int kMaxIns = 48;

@@ -32,7 +32,7 @@ namespace nbg {
 
 int32_t compile_expr(const uint8_t* buf, size_t len, const std::vector<Field>& fields, bool graphd,
                      bool out_bound, Program* out, std::string* msg,
-                     const std::vector<TagFieldRef>* tags = nullptr);
+                     const std::vector<TagFieldRef>* tags = nullptr, const std::vector<Field>* inputs = nullptr);
 Program program_dst();
 FastPred classify_pred(const Program& p, const std::vector<Field>& fields);
 
@@ -70,7 +70,24 @@ struct EvalEnv {
   const int32_t* col;
   const int64_t* rank;
   const PropDev* tprops;  // tag columns over the gidx space (Ctx::tag_refs order), or null
+  // $- / $var input table: open-addressing index src gidx -> its last input row, and columns
+  const int32_t* in_keys;
+  const int32_t* in_rows;
+  uint32_t in_mask;
+  const PropDev* iprops;
 };
+__device__ inline uint32_t gidx_hash(int32_t g) { return uint32_t(g) * 2654435761u; }
+// row of the input table whose FROM vid is gidx g (-1: none)
+__device__ inline int32_t input_row(const EvalEnv& env, int32_t g) {
+  uint32_t h = gidx_hash(g) & env.in_mask;
+  for (uint32_t probe = 0; probe <= env.in_mask; probe++) {
+    const int32_t k = env.in_keys[h];
+    if (k == g) return env.in_rows[h];
+    if (k < 0) return -1;
+    h = (h + 1) & env.in_mask;
+  }
+  return -1;
+}
 
 __device__ inline int64_t load_int(const void* data, int width, int64_t i) {
   switch (width) {
@@ -192,6 +209,11 @@ __device__ Val eval_program(const Program* __restrict__ P, const EvalEnv& env, i
       case P_TYPE: st[sp++] = mk(VT_INT, env.etype); break;
       case P_SRCTAG: st[sp++] = load_prop(env.tprops[in.arg], src_g); break;
       case P_DSTTAG: st[sp++] = load_prop(env.tprops[in.arg], dst_g); break;
+      case P_INPUT: {
+        const int32_t row = input_row(env, src_g);
+        st[sp++] = row < 0 ? mk(VT_ERR, 0) : load_prop(env.iprops[in.arg], row);
+        break;
+      }
       case P_UNARY: {
         Val& a = st[sp - 1];
         if (a.t == VT_ERR) break;
@@ -1376,6 +1398,24 @@ __global__ void k_row_dest(YieldArgs ya, int64_t n, uint32_t G, uint32_t* dest) 
     dest[i] = uint32_t((row_hash(ya, i) >> 17) % G);
 }
 
+// input table index: gidx of starts[i] -> i, the LAST row of a vid winning
+// (InterimResult::buildIndex overwrites vidToRowIndex_ row by row, InterimResult.cpp:158-160)
+__global__ void k_input_index(const int32_t* sg, int64_t n, int32_t* keys, int32_t* rows, uint32_t mask) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t g = sg[i];
+    if (g < 0) continue;
+    uint32_t h = gidx_hash(g) & mask;
+    while (true) {
+      const int32_t prev = atomicCAS(keys + h, -1, g);
+      if (prev == -1 || prev == g) {
+        atomicMax(rows + h, int32_t(i));
+        break;
+      }
+      h = (h + 1) & mask;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // host drivers
 // ------------------------------------------------------------------------------------------
@@ -1824,10 +1864,23 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   Program where{};
   bool has_where = s.where_len > 0;
   std::string msg;
+  // $- / $var input table columns (validated here, uploaded once the starts are resolved)
+  std::vector<Field> in_fields;
+  if (s.n_inputs) {
+    if (!s.input_names || !s.input_types || !s.input_cols) throw Error(NBG_E_INVALID_ARG, "input table");
+    for (size_t i = 0; i < s.n_inputs; i++) {
+      const int32_t t = s.input_types[i];
+      if (t != NBG_T_VID && t != NBG_T_INT && t != NBG_T_DOUBLE && t != NBG_T_BOOL && t != NBG_T_STRING)
+        throw Error(NBG_E_UNSUPPORTED, "input column type");
+      if (t == NBG_T_STRING && (!s.input_str_offsets || !s.input_str_offsets[i]))
+        throw Error(NBG_E_INVALID_ARG, "input STRING column without offsets");
+      in_fields.push_back(Field{s.input_names[i] ? s.input_names[i] : "", t});
+    }
+  }
   int32_t deferred = NBG_OK;
   std::string deferred_msg;
   if (has_where) {
-    int32_t rc = compile_expr(s.where, s.where_len, es.fields, true, true, &where, &msg, &c.tag_refs);
+    int32_t rc = compile_expr(s.where, s.where_len, es.fields, true, true, &where, &msg, &c.tag_refs, in_fields.empty() ? nullptr : &in_fields);
     if (rc == NBG_E_UNSUPPORTED || rc == NBG_E_INVALID_ARG) throw Error(rc, "WHERE: " + msg);
     if (rc != NBG_OK) {
       deferred = rc;
@@ -1842,7 +1895,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     if (s.n_yields > size_t(kMaxYields)) throw Error(NBG_E_UNSUPPORTED, "too many YIELD columns");
     for (size_t i = 0; i < s.n_yields; i++) {
       Program p{};
-      int32_t rc = compile_expr(s.yields[i], s.yield_lens[i], es.fields, true, true, &p, &msg, &c.tag_refs);
+      int32_t rc = compile_expr(s.yields[i], s.yield_lens[i], es.fields, true, true, &p, &msg, &c.tag_refs, in_fields.empty() ? nullptr : &in_fields);
       if (rc == NBG_E_UNSUPPORTED || rc == NBG_E_INVALID_ARG) throw Error(rc, "YIELD: " + msg);
       if (rc != NBG_OK && deferred == NBG_OK) {
         deferred = rc;
@@ -1932,6 +1985,52 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   a.mark_check = int32_t(c.opt("mark_check", 0));
   FastArgs fp{};
   EvalEnv env = make_env(c, es, csr, s.edge_type);
+  bool uses_input = false;
+  for (int i = 0; i < where.n && has_where; i++) uses_input |= where.ins[i].op == P_INPUT;
+  for (auto& p : yields)
+    for (int i = 0; i < p.n; i++) uses_input |= p.ins[i].op == P_INPUT;
+  DevBuf in_keys, in_rows, in_tab;
+  std::vector<DevBuf> in_cols;
+  if (uses_input) {
+    if (s.steps != 1) throw Error(NBG_E_UNSUPPORTED, "$- / $var props with STEPS > 1 (VertexBackTracker)");
+    uint32_t cap = 64;
+    while (cap < uint32_t(2 * std::max<int64_t>(ns, 1))) cap <<= 1;
+    in_keys.alloc(size_t(cap) * 4);
+    in_rows.alloc(size_t(cap) * 4);
+    NBG_HIP(hipMemsetAsync(in_keys.p, 0xff, size_t(cap) * 4, c.stream));
+    NBG_HIP(hipMemsetAsync(in_rows.p, 0xff, size_t(cap) * 4, c.stream));
+    if (ns) k_input_index<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, in_keys.as<int32_t>(), in_rows.as<int32_t>(), cap - 1);
+    NBG_HIP(hipGetLastError());
+    std::vector<PropDev> tab;
+    for (size_t i = 0; i < s.n_inputs; i++) {
+      const int32_t t = s.input_types[i];
+      const size_t w = t == NBG_T_BOOL ? 1 : 8;
+      DevBuf col, off;
+      PropDev pd{t, int32_t(w), nullptr, nullptr, nullptr, nullptr};
+      if (t != NBG_T_STRING) {
+        col.alloc(std::max<size_t>(size_t(ns) * w, 8));
+        if (ns) NBG_HIP(hipMemcpyAsync(col.p, s.input_cols[i], size_t(ns) * w, hipMemcpyHostToDevice, c.stream));
+        pd.data = col.p;
+      } else {
+        const int64_t* ho = s.input_str_offsets[i];
+        off.alloc(size_t(ns + 1) * 8);
+        NBG_HIP(hipMemcpyAsync(off.p, ho, size_t(ns + 1) * 8, hipMemcpyHostToDevice, c.stream));
+        col.alloc(size_t(ho[ns]) + 8);
+        if (ho[ns]) NBG_HIP(hipMemcpyAsync(col.p, s.input_cols[i], size_t(ho[ns]), hipMemcpyHostToDevice, c.stream));
+        pd = PropDev{t, 8, nullptr, nullptr, off.as<int64_t>(), col.as<uint8_t>()};
+      }
+      tab.push_back(pd);
+      in_cols.push_back(std::move(col));
+      in_cols.push_back(std::move(off));
+    }
+    in_tab.alloc(sizeof(PropDev) * tab.size());
+    NBG_HIP(hipMemcpyAsync(in_tab.p, tab.data(), sizeof(PropDev) * tab.size(), hipMemcpyHostToDevice, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));  // `tab` is pageable host memory
+    env.in_keys = in_keys.as<int32_t>();
+    env.in_rows = in_rows.as<int32_t>();
+    env.in_mask = cap - 1;
+    env.iprops = in_tab.as<PropDev>();
+  }
 
   // Frontier state: a list of local rows (top-down) and/or a bitmap (bottom-up).  E = sum of
   // the frontier's out-degrees = the adjacency entries the hop scans (TEPS numerator).

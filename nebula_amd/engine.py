@@ -240,8 +240,37 @@ class GraphSpace:
         finally:
             self.L.nbg_rows_free(C.byref(rows))
 
+    @staticmethod
+    def _input_table(inputs, n):
+        """[(name, NBG_T_*, values)] -> ctypes arrays of the nbg_go_spec input table (+ keepalive)."""
+        names = (C.c_char_p * len(inputs))(*[nm.encode() for nm, _, _ in inputs])
+        types = (C.c_int32 * len(inputs))(*[t for _, t, _ in inputs])
+        cols = (C.c_void_p * len(inputs))()
+        offs = (C.c_void_p * len(inputs))()
+        keep = [names, types, cols, offs]
+        for i, (nm, t, vals) in enumerate(inputs):
+            if len(vals) != n:
+                raise ValueError(f"input column {nm} has {len(vals)} rows, starts has {n}")
+            if t == _lib.T_STRING:
+                bs = [v.encode() if isinstance(v, str) else bytes(v) for v in vals]
+                o = np.zeros(n + 1, dtype=np.int64)
+                o[1:] = np.cumsum([len(b) for b in bs]) if bs else []
+                blob = np.frombuffer(b"".join(bs) + b"\0", dtype=np.uint8)
+                cols[i], offs[i] = blob.ctypes.data, o.ctypes.data
+                keep += [blob, o]
+            else:
+                dt = np.float64 if t == _lib.T_DOUBLE else np.uint8 if t == _lib.T_BOOL else np.int64
+                a = np.ascontiguousarray(vals, dtype=dt)
+                if a.size == 0:
+                    a = np.zeros(1, dtype=dt)
+                cols[i] = a.ctypes.data
+                keep.append(a)
+        return names, types, cols, offs, keep
+
     def go(self, starts, steps: int, edge_type: int, where=None, yields: Iterable = (), distinct: bool = False,
-           keep_on_device: bool = False) -> RowSet:
+           keep_on_device: bool = False, inputs=None) -> RowSet:
+        """GO ... FROM starts. `inputs`: the piped / variable rows ($-.prop / $var.prop), one per start,
+        as [(name, NBG_T_*, values)] (GoExecutor::getPropFromInterim)."""
         starts = np.ascontiguousarray(starts, dtype=np.int64)
         w = X.encode(where)
         wb = np.frombuffer(w + b"\0", dtype=np.uint8)
@@ -251,6 +280,11 @@ class GraphSpace:
         yl = (C.c_size_t * max(len(ys), 1))(*[len(y) for y in ys])
         spec = _lib.GoSpec(edge_type, steps, _p(starts), len(starts), _p(wb), len(w), yp, yl, len(ys),
                            int(distinct), int(keep_on_device))
+        if inputs:
+            names, types, cols, offs, _keep = self._input_table(inputs, len(starts))
+            spec.n_inputs = len(inputs)
+            spec.input_names, spec.input_types = names, types
+            spec.input_cols, spec.input_str_offsets = cols, offs
         rows = _lib.Rows()
         self._check(self.L.nbg_go(self.h, C.byref(spec), C.byref(rows)))
         try:

@@ -728,6 +728,10 @@ struct ora_store {
   std::map<std::pair<int32_t, int32_t>, refcpu::SchemaPtr> tagSchemas;
   std::map<int32_t, int32_t> tagLatest;
   std::map<std::string, int32_t> tagByName;
+  // $- / $var input rows of the next ora_go call (InterimResult rows, column name -> values)
+  std::vector<std::string> inNames;
+  std::vector<std::vector<refcpu::Val>> inCols;
+  size_t inRows = 0;
   std::map<int32_t, std::string> edgeNames;
   uint64_t seq = 0;
 };
@@ -1236,6 +1240,30 @@ using namespace refcpu;
 // ============================================================================================
 extern "C" {
 
+void ora_go_set_inputs(ora_store* st, size_t nRows, size_t nCols, const char* const* names,
+                       const int32_t* types, const void* const* cols, const int64_t* const* strOffsets) {
+  st->inNames.clear();
+  st->inCols.clear();
+  st->inRows = nRows;
+  for (size_t c = 0; c < nCols; c++) {
+    st->inNames.push_back(names[c]);
+    std::vector<Val> vals;
+    for (size_t r = 0; r < nRows; r++) {
+      switch (types[c]) {
+        case T_DOUBLE: vals.push_back(Val{static_cast<const double*>(cols[c])[r]}); break;
+        case T_BOOL: vals.push_back(Val{static_cast<const uint8_t*>(cols[c])[r] != 0}); break;
+        case T_STRING: {
+          const int64_t* o = strOffsets[c];
+          vals.push_back(Val{std::string(static_cast<const char*>(cols[c]) + o[r], size_t(o[r + 1] - o[r]))});
+          break;
+        }
+        default: vals.push_back(Val{static_cast<const int64_t*>(cols[c])[r]});
+      }
+    }
+    st->inCols.push_back(std::move(vals));
+  }
+}
+
 ora_store* ora_store_new(int32_t numParts) {
   auto* st = new ora_store();
   st->numParts = numParts;
@@ -1656,11 +1684,31 @@ ora_result* ora_go(ora_store* st, const int64_t* starts, size_t nStarts, int32_t
   ExprRefs refs;
   if (filter) collectRefs(*filter, refs);
   for (auto& y : ycols) collectRefs(*y, refs);
+  // InterimResult::buildIndex (InterimResult.cpp:125-195): vid of the FROM column (= starts[i]
+  // for row i) -> row, the last row of a vid winning; getPropFromInterim (GoExecutor.cpp:831-838)
+  std::vector<std::string> inNames = std::move(st->inNames);
+  std::vector<std::vector<Val>> inCols = std::move(st->inCols);
+  const size_t inRows = st->inRows;
+  st->inNames.clear();
+  st->inCols.clear();
+  st->inRows = 0;
+  std::unordered_map<int64_t, size_t> inIndex;
   if (refs.input || refs.variable) {
-    out->code = -2;
-    out->error = "unsupported reference ($-/$var)";
-    return out;
+    if (inNames.empty() || inRows != nStarts || steps != 1) {
+      // multi-step: VertexBackTracker (GoExecutor.h:174-193) depends on response order
+      out->code = -2;
+      out->error = "unsupported reference ($-/$var without an input table or with STEPS > 1)";
+      return out;
+    }
+    for (size_t i = 0; i < nStarts; i++) inIndex[starts[i]] = i;
   }
+  auto inputProp = [&](int64_t vid, const std::string& prop) -> OptVal {
+    auto r = inIndex.find(vid);
+    if (r == inIndex.end()) return ERR("vid not in the input index");
+    for (size_t c = 0; c < inNames.size(); c++)
+      if (inNames[c] == prop) return OK(inCols[c][r->second]);
+    return ERR("unknown input column " + prop);
+  };
   // getStepOutProps / getDstProps (GoExecutor.cpp:454-527): tag props grouped per tag name,
   // index = position in the vertex row; unknown tag -> "No schema found"
   std::vector<std::string> tagPropNames;  // stable storage for the PropDef names
@@ -1797,8 +1845,8 @@ ora_result* ora_go(ora_store* st, const int64_t* starts, size_t nStarts, int32_t
             if (res.ok()) return res;
             return ERR("get prop failed");
           };
-          g.getInputProp = [&](const std::string&) -> OptVal { return ERR("$- unsupported"); };
-          g.getVariableProp = [&](const std::string&) -> OptVal { return ERR("$var unsupported"); };
+          g.getInputProp = [&](const std::string& prop) -> OptVal { return inputProp(v.vid, prop); };
+          g.getVariableProp = [&](const std::string& prop) -> OptVal { return inputProp(v.vid, prop); };
           if (filter) {
             auto fv = eval(*filter, g);
             if (!fv.ok()) {

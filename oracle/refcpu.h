@@ -80,6 +80,10 @@ int32_t ora_gen_buckets(const int32_t* parts, const int64_t* vids, size_t n,
                         int32_t max_handlers, int32_t min_per_bucket, int32_t* sizes_out);
 
 // ---- graphd GO (GoExecutor + StorageClient restatement) ------------------------------------
+/* $- / $var input rows for the NEXT ora_go call only (one row per start; types 3 VID, 2 INT,
+ * 5 DOUBLE, 1 BOOL as int64 / double / uint8 arrays, 6 STRING as bytes + n+1 offsets) */
+void ora_go_set_inputs(ora_store* st, size_t n_rows, size_t n_cols, const char* const* names,
+                       const int32_t* types, const void* const* cols, const int64_t* const* str_offsets);
 ora_result* ora_go(ora_store* st, const int64_t* starts, size_t n_starts, int32_t steps,
                    int32_t edge_type, const uint8_t* where, size_t where_len,
                    const uint8_t* const* yields, const size_t* yield_lens, size_t n_yields,

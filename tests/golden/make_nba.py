@@ -98,6 +98,28 @@ def main():
                                            "rows": [["Spurs", "Spurs"], ["Hornets", "Hornets"],
                                                     ["Trail Blazers", "Trail Blazers"]]},
             "tag_vertex_not_exist": {"line": "GoTest.cpp:272-289", "rows": []},
+            # $-.prop / $var.prop references: input = GO FROM Tim Duncan, Chris Paul
+            # OVER like YIELD $^.player.name AS name, like._dst AS id
+            "ref_input_yield": {"line": "GoTest.cpp:317-340 (and $var form :364-387)",
+                                "rows": [["Tim Duncan", "Manu Ginobili", "Tim Duncan"],
+                                         ["Tim Duncan", "Tony Parker", "LaMarcus Aldridge"],
+                                         ["Tim Duncan", "Tony Parker", "Manu Ginobili"],
+                                         ["Tim Duncan", "Tony Parker", "Tim Duncan"],
+                                         ["Chris Paul", "LeBron James", "Ray Allen"],
+                                         ["Chris Paul", "Carmelo Anthony", "Chris Paul"],
+                                         ["Chris Paul", "Carmelo Anthony", "LeBron James"],
+                                         ["Chris Paul", "Carmelo Anthony", "Dwyane Wade"],
+                                         ["Chris Paul", "Dwyane Wade", "Chris Paul"],
+                                         ["Chris Paul", "Dwyane Wade", "LeBron James"],
+                                         ["Chris Paul", "Dwyane Wade", "Carmelo Anthony"]]},
+            "ref_input_where": {"line": "GoTest.cpp:341-361 (and $var form :388-407)",
+                                "rows": [["Tim Duncan", "Tony Parker", "LaMarcus Aldridge"],
+                                         ["Tim Duncan", "Tony Parker", "Manu Ginobili"],
+                                         ["Chris Paul", "LeBron James", "Ray Allen"],
+                                         ["Chris Paul", "Carmelo Anthony", "LeBron James"],
+                                         ["Chris Paul", "Carmelo Anthony", "Dwyane Wade"],
+                                         ["Chris Paul", "Dwyane Wade", "LeBron James"],
+                                         ["Chris Paul", "Dwyane Wade", "Carmelo Anthony"]]},
             "derived_go3_boris_like": {"line": "derived from the data by P12 (SURVEY 8c)",
                                        "rows": [["Tony Parker"], ["Manu Ginobili"], ["Tim Duncan"],
                                                 ["Tony Parker"], ["Tim Duncan"], ["Tim Duncan"],

@@ -59,6 +59,7 @@ def lib():
             "ora_bound_stats": (vp, [vp, i32, i32, vp, vp, sz, vp, sz, vp, vp, sz, i32, i32]),
             "ora_gen_buckets": (i32, [vp, vp, sz, i32, i32, vp]),
             "ora_go": (vp, [vp, vp, sz, i32, i32, vp, sz, vp, vp, sz, i32, i32, i32, i32, P(u64)]),
+            "ora_go_set_inputs": (None, [vp, sz, sz, P(C.c_char_p), P(i32), P(vp), P(vp)]),
             "ora_shortest_path": (vp, [vp, vp, vp, sz, i32, i32]),
             "ora_res_code": (i32, [vp]),
             "ora_res_error": (C.c_char_p, [vp]),
@@ -321,8 +322,31 @@ class Store:
         return Result(h)
 
     def go(self, starts, steps, etype, where=b"", yields=(), distinct=False, hosts=1,
-           handlers=10, min_per_bucket=3):
+           handlers=10, min_per_bucket=3, inputs=None):
+        """inputs: the $- / $var rows, one per start, as [(name, type, values)]."""
         starts = np.ascontiguousarray(starts, dtype=np.int64)
+        keep = []
+        if inputs:
+            n = len(starts)
+            names = _cstrs([nm for nm, _, _ in inputs])
+            types = (C.c_int32 * len(inputs))(*[t for _, t, _ in inputs])
+            cols = (C.c_void_p * len(inputs))()
+            offs = (C.c_void_p * len(inputs))()
+            for i, (nm, t, vals) in enumerate(inputs):
+                if t == STRING:
+                    bs = [v.encode() for v in vals]
+                    o = np.zeros(n + 1, dtype=np.int64)
+                    o[1:] = np.cumsum([len(b) for b in bs]) if bs else []
+                    blob = np.frombuffer(b"".join(bs) + b"\0", dtype=np.uint8)
+                    cols[i], offs[i] = blob.ctypes.data, o.ctypes.data
+                    keep += [blob, o]
+                else:
+                    dt = np.float64 if t == DOUBLE else np.uint8 if t == BOOL else np.int64
+                    a = np.ascontiguousarray(list(vals) or [0], dtype=dt)
+                    cols[i] = a.ctypes.data
+                    keep.append(a)
+            keep += [names, types, cols, offs]
+            lib().ora_go_set_inputs(self.h, n, len(inputs), names, types, cols, offs)
         ys = [bytes(y) for y in yields]
         yb = (C.c_void_p * max(len(ys), 1))()
         ylen = (C.c_size_t * max(len(ys), 1))()

@@ -230,3 +230,59 @@ def test_random_tag_missing_rows_error():
         assert ms(rs.rows()) == ms(ref.rows())
     finally:
         sp.close()
+
+
+# ------------------------------------------------------------------------------------------
+# $-.prop / $var.prop: GoTest ReferencePipeInYieldAndWhere /
+# ReferenceVariableInYieldAndWhere, input rows = the first GO's (name, id) rows
+# ------------------------------------------------------------------------------------------
+def test_nba_reference_input_and_variable(nba):
+    sp, st, vid, d = nba
+    first = sp.go([vid["Tim Duncan"], vid["Chris Paul"]], 1, F.NBA_LIKE,
+                  yields=[X.SourceProp("player", "name"), X.EdgeDst("like")])
+    rows = first.rows()
+    starts = [r[1] for r in rows]
+    inputs = [("name", O.STRING, [r[0] for r in rows]), ("id", O.VID, starts)]
+    for ref in (X.InputProp("name"), X.VariableProp("var", "name")):
+        ys = [ref, X.SourceProp("player", "name"), X.DestProp("player", "name")]
+        rs = sp.go(starts, 1, F.NBA_LIKE, yields=ys, inputs=inputs)
+        assert names(vid, rs.rows()) == golden(d, "ref_input_yield")
+        w = ref.ne(X.DestProp("player", "name"))
+        rs = sp.go(starts, 1, F.NBA_LIKE, where=w, yields=ys, inputs=inputs)
+        assert names(vid, rs.rows()) == golden(d, "ref_input_where")
+        ref_rs = st.go(starts, 1, F.NBA_LIKE, where=w.encode(), yields=[y.encode() for y in ys], inputs=inputs)
+        assert ms(rs.rows()) == ms(ref_rs.rows())
+
+
+def test_nba_reference_input_duplicates_and_types(nba):
+    sp, st, vid, d = nba
+    # a vid piped twice: its LAST input row supplies $-.props (InterimResult::buildIndex);
+    # numeric / bool / double input columns in WHERE and YIELD arithmetic
+    starts = [vid["Tim Duncan"], vid["Tony Parker"], vid["Tim Duncan"], vid["Boris Diaw"]]
+    inputs = [("tag", O.STRING, ["a", "b", "c", "d"]), ("n", O.VID, [10, 20, 30, 40]),
+              ("x", O.DOUBLE, [0.5, 1.5, 2.5, 3.5]), ("f", O.BOOL, [True, False, False, True])]
+    ys = [X.InputProp("tag"), X.InputProp("n") + X.AliasProp("like", "likeness"), X.InputProp("x"),
+          X.InputProp("f"), X.EdgeDst("like")]
+    for distinct in (False, True):
+        for w in (None, X.InputProp("n") > 15, X.InputProp("f")):
+            rs = sp.go(starts, 1, F.NBA_LIKE, where=w, yields=ys, distinct=distinct, inputs=inputs)
+            ref = st.go(starts, 1, F.NBA_LIKE, where=X.encode(w), yields=[y.encode() for y in ys],
+                        distinct=distinct, inputs=inputs)
+            assert ref.code == 0, ref.error
+            assert ms(rs.rows()) == ms(ref.rows())
+            assert all(r[0] != "a" for r in rs.rows())  # Tim's last row is "c"
+
+
+def test_nba_reference_input_errors(nba):
+    sp, st, vid, d = nba
+    starts = [vid["Tim Duncan"]]
+    inputs = [("name", O.STRING, ["x"])]
+    with pytest.raises(NbgError) as e:  # no input table
+        sp.go(starts, 1, F.NBA_LIKE, yields=[X.InputProp("name")])
+    assert e.value.code == -1003
+    with pytest.raises(NbgError) as e:  # multi-step: VertexBackTracker order dependence
+        sp.go(starts, 2, F.NBA_LIKE, yields=[X.InputProp("name")], inputs=inputs)
+    assert e.value.code == -1003
+    with pytest.raises(NbgError) as e:  # unknown input column
+        sp.go(starts, 1, F.NBA_LIKE, yields=[X.InputProp("nope")], inputs=inputs)
+    assert e.value.code == -1001

@@ -5,6 +5,7 @@ from collections import Counter
 import pytest
 
 import fixtures as F
+import oracle as O
 from nebula_amd import expr as X
 
 
@@ -164,3 +165,30 @@ def test_tag_props_where_and_errors(nba):
     # $$.team.name on a player vertex: the dst has no team row -> evaluation error fails the query
     r = st.go([vid["Tim Duncan"]], 1, F.NBA_LIKE, yields=[X.DestProp("team", "name").encode()])
     assert r.code != 0
+
+
+# ---- $-.prop / $var.prop (GoExecutor::getPropFromInterim, InterimResult index) -----
+def ref_first(st, vid):
+    """GO FROM Tim Duncan, Chris Paul OVER like YIELD $^.player.name AS name, like._dst AS id"""
+    r = st.go([vid["Tim Duncan"], vid["Chris Paul"]], 1, F.NBA_LIKE,
+              yields=[X.SourceProp("player", "name").encode(), X.EdgeDst("like").encode()])
+    assert r.code == 0, r.error
+    rows = r.rows()
+    return [row[1] for row in rows], [("name", O.STRING, [row[0] for row in rows]),
+                                      ("id", O.VID, [row[1] for row in rows])]
+
+
+def test_reference_input_and_variable(nba):
+    st, vid, d = nba
+    ys = lambda ref: [ref, X.SourceProp("player", "name"), X.DestProp("player", "name")]
+    for ref in (X.InputProp("name"), X.VariableProp("var", "name")):
+        starts, inputs = ref_first(st, vid)
+        r = st.go(starts, 1, F.NBA_LIKE, yields=[y.encode() for y in ys(ref)], inputs=inputs)
+        assert r.code == 0, r.error
+        assert names(vid, r.rows()) == expect(d, "ref_input_yield")
+        w = ref.ne(X.DestProp("player", "name")).encode()
+        r = st.go(starts, 1, F.NBA_LIKE, where=w, yields=[y.encode() for y in ys(ref)], inputs=inputs)
+        assert names(vid, r.rows()) == expect(d, "ref_input_where")
+    # without an input table, or with STEPS > 1, the reference path is not restated
+    assert st.go(starts, 1, F.NBA_LIKE, yields=[X.InputProp("name").encode()]).code != 0
+    assert st.go(starts, 2, F.NBA_LIKE, yields=[X.InputProp("name").encode()], inputs=inputs).code != 0
