@@ -39,7 +39,8 @@ def pmc_traffic(workload: str, prefixes):
     the same workload (profiles/<tag>_summary.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
     separate --pmc passes, tools/gpu_profile.sh + tools/profile_summary.py).  None if absent."""
     best = None
-    for f in sorted((ROOT / "profiles").glob("*_summary.json"), key=lambda p: p.stat().st_mtime):
+    # newest round tag last (r01b < r01c < ...); file mtimes are meaningless in a fresh checkout
+    for f in sorted((ROOT / "profiles").glob("*_summary.json"), key=lambda p: p.name):
         try:
             d = json.loads(f.read_text())
         except ValueError:
