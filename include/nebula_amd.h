@@ -148,6 +148,16 @@ typedef struct {
   int64_t* path_offsets;  /* n_rows+1 */
   int64_t* path_vids;
   void* _impl;
+  /* get_bound SOURCE/DEST tag props (VertexData.vertex_data, QueryBoundProcessor.cpp:19-31): one
+   * value per vertex_ids entry and requested tag prop, in request order; host memory.  Types as
+   * for the edge columns (STRING: vertex_str_offsets[c] has n_vertices+1 offsets).
+   * vertex_col_present[c][i] = 0 when the vertex has no row of that tag in the request's part
+   * (the reference then leaves the prop out of the vertex row).                              */
+  int32_t n_vertex_cols;
+  int32_t* vertex_col_types;
+  void** vertex_cols;
+  int64_t** vertex_str_offsets;
+  uint8_t** vertex_col_present;
 } nbg_rows;
 void nbg_rows_free(nbg_rows* rows);
 
@@ -156,8 +166,10 @@ void nbg_rows_free(nbg_rows* rows);
  * (src/storage/QueryBaseProcessor.inl:462-505, QueryBoundProcessor.cpp:16-106).
  * parts/vids: the request's parts map flattened (pair i = (parts[i], vids[i])).
  * edge_type < 0: in-bound scan (StorageClient.cpp:118).  filter: Expression::encode bytes or
- * empty.  Return columns are EDGE-owned props (key props _src/_dst/_rank/_type or schema props);
- * SOURCE/DEST tag props return NBG_E_UNSUPPORTED in this version.  Request-level errors are
+ * empty.  Return columns are EDGE-owned props (key props _src/_dst/_rank/_type or schema props)
+ * and SOURCE/DEST tag props (tag_id + name; returned per vertex in vertex_cols; unknown tag ->
+ * E_TAG_PROP_NOT_FOUND, unknown prop -> E_IMPROPER_DATA_TYPE on every part).  Tag props inside
+ * the push-down filter return NBG_E_UNSUPPORTED.  Request-level errors are
  * reported per part in failed_codes (QueryBaseProcessor.inl:470-477), not as the return.    */
 typedef struct {
   const char* name;

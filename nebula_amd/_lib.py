@@ -54,7 +54,10 @@ class Rows(C.Structure):
                 ("vertex_row_offsets", C.POINTER(C.c_int64)), ("n_failed", C.c_int32),
                 ("failed_parts", C.POINTER(C.c_int32)), ("failed_codes", C.POINTER(C.c_int32)),
                 ("edges_scanned", C.c_uint64), ("path_offsets", C.POINTER(C.c_int64)),
-                ("path_vids", C.POINTER(C.c_int64)), ("_impl", C.c_void_p)]
+                ("path_vids", C.POINTER(C.c_int64)), ("_impl", C.c_void_p),
+                ("n_vertex_cols", C.c_int32), ("vertex_col_types", C.POINTER(C.c_int32)),
+                ("vertex_cols", C.POINTER(C.c_void_p)), ("vertex_str_offsets", C.POINTER(C.POINTER(C.c_int64))),
+                ("vertex_col_present", C.POINTER(C.POINTER(C.c_uint8)))]
 
 
 class PropDef(C.Structure):

@@ -226,7 +226,9 @@ struct TagSpace {
   std::string name;
   std::vector<Field> fields;
   Staging stage;              // src = vid, ver, part, rank = load sequence number (write order)
-  std::vector<PropCol> cols;  // per field, [n_global]; data int64 bits, present uint8
+  std::vector<PropCol> cols;  // per field, [n_global]; data int64 bits, present uint8:
+                              // 0 none, 1 row of the vid's own part, 2 row of a foreign part only
+  DevBuf part;                // int32 [n_global]: the part the vertex's row came from
 };
 // flat (tag, prop) table the expression compiler resolves $^.tag.prop / $$.tag.prop against
 struct TagFieldRef {

@@ -17,6 +17,13 @@ struct HostRows {
   std::vector<int64_t> row_vertex, vertex_ids, vertex_row_offsets;
   std::vector<int32_t> failed_parts, failed_codes;
   std::vector<int64_t> path_offsets, path_vids;  // nbg_shortest_path
+  // get_bound tag props per returned vertex
+  std::vector<int32_t> vertex_types;
+  std::vector<std::vector<uint8_t>> vertex_host, vertex_present;
+  std::vector<std::vector<int64_t>> vertex_host_off;
+  std::vector<void*> vertex_cols;
+  std::vector<int64_t*> vertex_str_off;
+  std::vector<uint8_t*> vertex_pres;
 };
 
 inline void fill_rows(nbg_rows* out, HostRows* h, int64_t nrows, bool on_device) {
@@ -37,6 +44,19 @@ inline void fill_rows(nbg_rows* out, HostRows* h, int64_t nrows, bool on_device)
   out->path_offsets = h->path_offsets.empty() ? nullptr : h->path_offsets.data();
   out->path_vids = h->path_vids.empty() ? nullptr : h->path_vids.data();
   out->_impl = h;
+  h->vertex_cols.clear();
+  h->vertex_str_off.clear();
+  h->vertex_pres.clear();
+  for (size_t i = 0; i < h->vertex_types.size(); i++) {
+    h->vertex_cols.push_back(h->vertex_host[i].data());
+    h->vertex_str_off.push_back(h->vertex_host_off[i].empty() ? nullptr : h->vertex_host_off[i].data());
+    h->vertex_pres.push_back(h->vertex_present[i].data());
+  }
+  out->n_vertex_cols = int32_t(h->vertex_types.size());
+  out->vertex_col_types = h->vertex_types.empty() ? nullptr : h->vertex_types.data();
+  out->vertex_cols = h->vertex_cols.empty() ? nullptr : h->vertex_cols.data();
+  out->vertex_str_offsets = h->vertex_str_off.empty() ? nullptr : h->vertex_str_off.data();
+  out->vertex_col_present = h->vertex_pres.empty() ? nullptr : h->vertex_pres.data();
 }
 
 }  // namespace nbg

@@ -1315,13 +1315,13 @@ static void order_by_degree(Ctx& c, DevBuf& owned, int64_t n_owned) {
 // the last write (WriteBatch last-write-wins, RocksEngine.cpp:216-230).  Rows stored in a part
 // other than the vid's own are never reached by the prefix scan (the request part is
 // hash(vid), StorageClient.cpp:238-243), and vids outside every edge have no gidx: both dropped.
-__global__ void k_tag_gather(const int32_t* win, int64_t ng, const int64_t* props, const uint8_t* present,
-                             int64_t* data, uint8_t* pres_out) {
+__global__ void k_tag_gather(const int32_t* win, const uint8_t* state, int64_t ng, const int64_t* props,
+                             const uint8_t* present, int64_t* data, uint8_t* pres_out) {
   for (int64_t g = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; g < ng; g += int64_t(gridDim.x) * blockDim.x) {
     int32_t w = win[g];
     bool ok = w >= 0 && present[w] != 0;
     data[g] = ok ? props[w] : 0;
-    pres_out[g] = ok;
+    pres_out[g] = ok ? state[g] : 0;
   }
 }
 __global__ void k_tag_str_len(const int32_t* win, int64_t ng, const uint8_t* present, const int64_t* lens,
@@ -1364,6 +1364,8 @@ static void build_tag_columns(Ctx& c) {
     TagSpace& ts = kvp.second;
     const int64_t n = ts.stage.n;
     std::vector<int32_t> win(size_t(std::max<int64_t>(ng, 1)), -1);
+    std::vector<uint8_t> wstate(size_t(std::max<int64_t>(ng, 1)), 0);  // 1 own part, 2 foreign part
+    std::vector<int32_t> tpart(size_t(std::max<int64_t>(ng, 1)), 0);
     if (n > 0 && ng > 0) {
       DevBuf dg;
       dg.alloc(size_t(n) * 4);
@@ -1377,21 +1379,48 @@ static void build_tag_columns(Ctx& c) {
       NBG_HIP(hipMemcpyAsync(ver.data(), ts.stage.ver.p, size_t(n) * 8, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipMemcpyAsync(seq.data(), ts.stage.seq.p, size_t(n) * 8, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
+      // candidate order: rows of the vid's own part first (GO reads those), else the smallest
+      // foreign part (a getBound request naming that part reads it); then the prefix scan's
+      // first key (smallest LE version bytes), identical keys by last write
+      auto foreign = [&](int64_t i) { return part[size_t(i)] != part_of_vid(vid[size_t(i)], c.num_parts); };
+      // world > 1: a rank keeps only its owned slice (replicate_owned gathers slices); a row in a
+      // foreign part held by another rank is not visible there (getBound on that part only)
+      const int64_t olo = c.owned_lo(), ohi = c.owned_hi();
       for (int64_t i = 0; i < n; i++) {
         int32_t gi = g[size_t(i)];
-        if (gi < 0 || part[size_t(i)] != part_of_vid(vid[size_t(i)], c.num_parts)) continue;
+        if (gi < 0 || (c.world > 1 && (gi < olo || gi >= ohi))) continue;
         int32_t& w = win[size_t(gi)];
         if (w < 0) {
           w = int32_t(i);
           continue;
         }
+        const bool fi = foreign(i), fw = foreign(w);
+        if (fi != fw) {
+          if (!fi) w = int32_t(i);
+          continue;
+        }
+        if (fi && part[size_t(i)] != part[size_t(w)]) {
+          if (part[size_t(i)] < part[size_t(w)]) w = int32_t(i);
+          continue;
+        }
         uint64_t a = __builtin_bswap64(uint64_t(ver[size_t(i)])), b = __builtin_bswap64(uint64_t(ver[size_t(w)]));
         if (a < b || (a == b && seq[size_t(i)] > seq[size_t(w)])) w = int32_t(i);
       }
+      for (int64_t gi = 0; gi < ng; gi++) {
+        const int32_t w = win[size_t(gi)];
+        if (w < 0) continue;
+        wstate[size_t(gi)] = foreign(w) ? 2 : 1;
+        tpart[size_t(gi)] = part[size_t(w)];
+      }
     }
-    DevBuf dwin;
+    DevBuf dwin, dstate;
     dwin.alloc(size_t(std::max<int64_t>(ng, 1)) * 4);
+    dstate.alloc(size_t(std::max<int64_t>(ng, 1)));
+    ts.part.alloc(size_t(std::max<int64_t>(ng, 1)) * 4);
     NBG_HIP(hipMemcpyAsync(dwin.p, win.data(), size_t(std::max<int64_t>(ng, 1)) * 4, hipMemcpyHostToDevice, c.stream));
+    NBG_HIP(hipMemcpyAsync(dstate.p, wstate.data(), size_t(std::max<int64_t>(ng, 1)), hipMemcpyHostToDevice, c.stream));
+    NBG_HIP(hipMemcpyAsync(ts.part.p, tpart.data(), size_t(std::max<int64_t>(ng, 1)) * 4, hipMemcpyHostToDevice, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));  // host vectors are pageable
     ts.cols.clear();
     for (size_t f = 0; f < ts.fields.size(); f++) {
       PropCol pc;
@@ -1404,7 +1433,8 @@ static void build_tag_columns(Ctx& c) {
         NBG_HIP(hipMemsetAsync(pc.data.p, 0, pc.data.bytes, c.stream));
         NBG_HIP(hipMemsetAsync(pc.present.p, 0, pc.present.bytes, c.stream));
       } else {
-        k_tag_gather<<<grid_for(ng), 256, 0, c.stream>>>(dwin.as<int32_t>(), ng, ts.stage.props[f].as<int64_t>(),
+        k_tag_gather<<<grid_for(ng), 256, 0, c.stream>>>(dwin.as<int32_t>(), dstate.as<uint8_t>(), ng,
+                                                          ts.stage.props[f].as<int64_t>(),
                                                           ts.stage.present[f].as<uint8_t>(), pc.data.as<int64_t>(),
                                                           pc.present.as<uint8_t>());
       }
@@ -1453,6 +1483,7 @@ static void build_tag_columns(Ctx& c) {
       c.tag_refs.push_back(TagFieldRef{ts.name, pc.name, pc.type});
       ts.cols.push_back(std::move(pc));
     }
+    if (c.world > 1) replicate_owned(c, ts.part, 4);
     NBG_HIP(hipStreamSynchronize(c.stream));
     ts.stage = Staging{};
   }

@@ -207,8 +207,15 @@ __device__ Val eval_program(const Program* __restrict__ P, const EvalEnv& env, i
       case P_SRC: st[sp++] = mk(VT_INT, env.vid_of[src_g]); break;
       case P_RANK: st[sp++] = mk(VT_INT, env.rank ? env.rank[ge] : 0); break;
       case P_TYPE: st[sp++] = mk(VT_INT, env.etype); break;
-      case P_SRCTAG: st[sp++] = load_prop(env.tprops[in.arg], src_g); break;
-      case P_DSTTAG: st[sp++] = load_prop(env.tprops[in.arg], dst_g); break;
+      case P_SRCTAG:
+      case P_DSTTAG: {
+        // only a row of the vertex's own part is visible to GO (presence byte 1; 2 = a row that
+        // only a getBound naming its foreign part reads)
+        const PropDev& tp = env.tprops[in.arg];
+        const int32_t g = in.op == P_SRCTAG ? src_g : dst_g;
+        st[sp++] = tp.present[g] == 1 ? load_prop(tp, g) : mk(VT_ERR, 0);
+        break;
+      }
       case P_INPUT: {
         const int32_t row = input_row(env, src_g);
         st[sp++] = row < 0 ? mk(VT_ERR, 0) : load_prop(env.iprops[in.arg], row);
@@ -2572,6 +2579,111 @@ __global__ void k_clamp_len(int64_t* l, int64_t m) {
     if (l[i] < 0) l[i] = 0;
 }
 
+// tag column values of the returned vertices (gidx list): value bits, presence state, part, and
+// STRING (offset, length) into the column's bytes
+__global__ void k_tag_fetch(const int32_t* g, int64_t m, const int64_t* data, const uint8_t* present,
+                            const int32_t* tpart, const int64_t* str_off, int64_t* val, uint8_t* state,
+                            int32_t* part, int64_t* soff, int64_t* slen) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t x = g[i];
+    const bool ok = x >= 0;
+    val[i] = ok ? data[x] : 0;
+    state[i] = ok ? present[x] : 0;
+    part[i] = ok ? tpart[x] : -1;
+    if (str_off) {
+      soff[i] = ok ? str_off[x] : 0;
+      slen[i] = ok ? str_off[x + 1] - str_off[x] : 0;
+    }
+  }
+}
+__global__ void k_bytes_gather(const int64_t* soff, const int64_t* doff, int64_t m, const uint8_t* src, uint8_t* dst) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    for (int64_t j = 0; j < doff[i + 1] - doff[i]; j++) dst[doff[i] + j] = src[soff[i] + j];
+}
+
+// Fills h->vertex_* for the returned vertices (h->vertex_ids, request parts vparts): a value is
+// visible when the vertex's row sits in the request's part -- collectVertexProps scans
+// prefix(request part, vid, tag) (QueryBaseProcessor.inl:309-333) -- else absent (the reference
+// then skips the prop in the vertex row, RowWriter without it).
+template <typename F>
+void fetch_vertex_tags(Ctx& c, HostRows* h, const std::vector<int32_t>& vparts, F col_of, size_t ncols) {
+  const int64_t nv = int64_t(h->vertex_ids.size());
+  DevBuf dv, dg, val, stt, prt, soff, slen;
+  const size_t cap = size_t(std::max<int64_t>(nv, 1));
+  dv.alloc(cap * 8);
+  dg.alloc(cap * 4);
+  val.alloc(cap * 8);
+  stt.alloc(cap);
+  prt.alloc(cap * 4);
+  soff.alloc(cap * 8);
+  slen.alloc(cap * 8);
+  if (nv) {
+    NBG_HIP(hipMemcpyAsync(dv.p, h->vertex_ids.data(), size_t(nv) * 8, hipMemcpyHostToDevice, c.stream));
+    lookup_gidx(c, dv.as<int64_t>(), dg.as<int32_t>(), nv);
+  }
+  for (size_t t = 0; t < ncols; t++) {
+    const auto tf = col_of(t);
+    const TagSpace& ts = *tf.first;
+    const PropCol& pc = ts.cols[tf.second];
+    const bool is_str = pc.type == NBG_T_STRING;
+    std::vector<int64_t> hv(cap), hoff(cap), hlen(cap);
+    std::vector<uint8_t> hs(cap);
+    std::vector<int32_t> hp(cap);
+    if (nv) {
+      k_tag_fetch<<<grid_cap(nv), 256, 0, c.stream>>>(dg.as<int32_t>(), nv, pc.data.as<int64_t>(), pc.present.as<uint8_t>(),
+                                                      ts.part.as<int32_t>(), is_str ? pc.str_off.as<int64_t>() : nullptr,
+                                                      val.as<int64_t>(), stt.as<uint8_t>(), prt.as<int32_t>(),
+                                                      soff.as<int64_t>(), slen.as<int64_t>());
+      NBG_HIP(hipGetLastError());
+      NBG_HIP(hipMemcpyAsync(hv.data(), val.p, size_t(nv) * 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipMemcpyAsync(hs.data(), stt.p, size_t(nv), hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipMemcpyAsync(hp.data(), prt.p, size_t(nv) * 4, hipMemcpyDeviceToHost, c.stream));
+      if (is_str) {
+        NBG_HIP(hipMemcpyAsync(hoff.data(), soff.p, size_t(nv) * 8, hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipMemcpyAsync(hlen.data(), slen.p, size_t(nv) * 8, hipMemcpyDeviceToHost, c.stream));
+      }
+      NBG_HIP(hipStreamSynchronize(c.stream));
+    }
+    std::vector<uint8_t> pres(cap, 0);
+    for (int64_t i = 0; i < nv; i++) {
+      const int32_t rp = vparts[size_t(i)];
+      const bool own = hs[size_t(i)] == 1 && rp == part_of_vid(h->vertex_ids[size_t(i)], c.num_parts);
+      const bool foreign = hs[size_t(i)] == 2 && rp == hp[size_t(i)];
+      pres[size_t(i)] = own || foreign;
+    }
+    h->vertex_types.push_back(pc.type == NBG_T_FLOAT                               ? NBG_T_DOUBLE
+                              : (pc.type == NBG_T_VID || pc.type == NBG_T_TIMESTAMP) ? NBG_T_INT
+                                                                                     : pc.type);
+    h->vertex_present.push_back(pres);
+    if (is_str) {
+      std::vector<int64_t> offs(size_t(nv) + 1, 0);
+      for (int64_t i = 0; i < nv; i++) offs[size_t(i + 1)] = offs[size_t(i)] + (pres[size_t(i)] ? hlen[size_t(i)] : 0);
+      std::vector<uint8_t> bytes(size_t(offs[size_t(nv)]) + 8);
+      if (offs[size_t(nv)]) {
+        DevBuf ddo, dbytes;
+        ddo.alloc(size_t(nv + 1) * 8);
+        dbytes.alloc(size_t(offs[size_t(nv)]) + 8);
+        NBG_HIP(hipMemcpyAsync(ddo.p, offs.data(), size_t(nv + 1) * 8, hipMemcpyHostToDevice, c.stream));
+        k_bytes_gather<<<grid_cap(nv), 256, 0, c.stream>>>(soff.as<int64_t>(), ddo.as<int64_t>(), nv,
+                                                           pc.str_bytes.as<uint8_t>(), dbytes.as<uint8_t>());
+        NBG_HIP(hipMemcpyAsync(bytes.data(), dbytes.p, size_t(offs[size_t(nv)]), hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipStreamSynchronize(c.stream));
+      }
+      h->vertex_host.push_back(std::move(bytes));
+      h->vertex_host_off.push_back(std::move(offs));
+    } else {
+      std::vector<uint8_t> raw(cap * 8);
+      if (pc.type == NBG_T_BOOL) {
+        for (int64_t i = 0; i < nv; i++) raw[size_t(i)] = uint8_t(hv[size_t(i)] != 0);
+      } else {
+        memcpy(raw.data(), hv.data(), size_t(nv) * 8);
+      }
+      h->vertex_host.push_back(std::move(raw));
+      h->vertex_host_off.emplace_back();
+    }
+  }
+}
+
 int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* vids, size_t n, const uint8_t* filter,
                       size_t flen, const nbg_prop_def* cols, size_t ncols, nbg_rows* out, const int32_t* stats) {
   PoolScope pool_scope(c.pool);
@@ -2598,10 +2710,28 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
   EdgeSpace& es = it->second;
   Csr& csr = in_bound ? es.in : es.out;
   BoundCols bc{};
+  // SOURCE / DEST tag props: the vertex row of each returned vertex (tagContexts_,
+  // QueryBaseProcessor.inl:40-70; QueryBoundProcessor.cpp:19-31)
+  struct TagReq {
+    const TagSpace* ts;
+    size_t field;
+  };
+  std::vector<TagReq> treq;
   for (size_t i = 0; i < ncols; i++) {
     if (cols[i].owner != NBG_OWNER_EDGE) {
-      delete h;
-      throw Error(NBG_E_UNSUPPORTED, "SOURCE/DEST tag props are not supported yet");
+      if (stats) {
+        delete h;
+        throw Error(NBG_E_UNSUPPORTED, "SOURCE/DEST tag props in bound stats");
+      }
+      auto tit = c.tags.find(cols[i].tag_id);
+      if (tit == c.tags.end()) return fail_all(NBG_E_TAG_PROP_NOT_FOUND);
+      const std::string tname = cols[i].name ? cols[i].name : "";
+      size_t fi = tit->second.fields.size();
+      for (size_t f = 0; f < tit->second.fields.size(); f++)
+        if (tit->second.fields[f].name == tname) fi = f;
+      if (fi == tit->second.fields.size()) return fail_all(NBG_E_IMPROPER_DATA_TYPE);
+      treq.push_back(TagReq{&tit->second, fi});
+      continue;
     }
     std::string name = cols[i].name ? cols[i].name : "";
     BoundCol b{};
@@ -2859,6 +2989,18 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
     }
   }
   h->vertex_row_offsets.push_back(m);
+  if (!treq.empty()) {
+    // request part of each returned vertex (its first request entry)
+    std::vector<int32_t> vparts;
+    last = -1;
+    for (int64_t r = 0; r < m; r++) {
+      int64_t k = howner[size_t(r)];
+      if (k != last) vparts.push_back(parts[centry[size_t(k)]]);
+      last = k;
+    }
+    fetch_vertex_tags(c, h, vparts, [&](size_t t) { return std::make_pair(treq[t].ts, treq[t].field); },
+                      treq.size());
+  }
   fill_rows(out, h, m, false);
   out->edges_scanned = uint64_t(E);
   return NBG_OK;

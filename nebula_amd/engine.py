@@ -84,6 +84,26 @@ class RowSet:
         self.vertex_row_offsets = (np.ctypeslib.as_array(rows.vertex_row_offsets, shape=(nv + 1,)).copy()
                                    if nv else np.zeros(1, np.int64))
         self.failed = [(rows.failed_parts[i], rows.failed_codes[i]) for i in range(rows.n_failed)]
+        # getBound tag props: vertex_columns[c][i] for vertex_ids[i] (None: no row of that tag)
+        self.vertex_columns = []
+        for c in range(rows.n_vertex_cols):
+            t = rows.vertex_col_types[c]
+            pres = rows.vertex_col_present[c]
+            ptr = rows.vertex_cols[c]
+            col = []
+            for i in range(nv):
+                if not pres[i]:
+                    col.append(None)
+                elif t == _lib.T_STRING:
+                    o = rows.vertex_str_offsets[c]
+                    col.append(C.string_at(ptr + o[i], o[i + 1] - o[i]).decode() if o[i + 1] > o[i] else "")
+                elif t == _lib.T_BOOL:
+                    col.append(bool(C.cast(ptr, C.POINTER(C.c_uint8))[i]))
+                elif t == _lib.T_DOUBLE:
+                    col.append(float(C.cast(ptr, C.POINTER(C.c_double))[i]))
+                else:
+                    col.append(int(C.cast(ptr, C.POINTER(C.c_int64))[i]))
+            self.vertex_columns.append(col)
 
     def rows(self):
         out = []

@@ -153,6 +153,8 @@ def test_nba_yield_distinct_multicol(nba):
 def qb():
     sp = GraphSpace(6)
     sp.set_edge_schema(F.EDGE_TYPE, F.qb_edge_schema())
+    for tag in range(3001, 3010):
+        sp.set_tag_schema(tag, str(tag), F.qb_tag_schema(tag))
     for part, data in F.qb_kv_parts().items():
         sp.load_part(part, data)
     sp.finalize()
@@ -204,6 +206,44 @@ def test_get_bound_matches_reference(qb, filt):
                 assert row[1] == 0
                 assert list(row[2:7]) == [row[0] + 2 * i for i in range(5)]
                 assert list(row[7:]) == [f"string_col_{(i + 5) * 2}_2" for i in range(5)]
+
+
+@pytest.mark.parametrize("out_bound", [True, False])
+def test_get_bound_tag_props(qb, out_bound):
+    # checkResponse's vertex part (QueryBoundTest.cpp:111-178): SOURCE tag props of every vertex,
+    # read from the request's part (the fixture stores vertices outside their hash part)
+    sp, st = qb
+    parts, vids, cols = F.qb_request(out_bound)
+    et = F.EDGE_TYPE if out_bound else -F.EDGE_TYPE
+    g = sp.get_bound(et, parts, vids, cols)
+    r = st.get_bound(et, parts, vids, cols, in_bound=not out_bound)
+    assert g.failed == r.failed() == []
+    assert len(g.vertex_ids) == 30 and len(g.vertex_columns) == 3
+    ref = dict(r.vertices())
+    for i, vid in enumerate(g.vertex_ids):
+        vals = [col[i] for col in g.vertex_columns]
+        assert vals == [int(vid) + 3001, int(vid) + 3003 + 2, "tag_string_col_4"]
+        assert tuple(vals) == tuple(ref[int(vid)])
+    assert by_vertex(g) == oracle_by_vertex(r)
+    # the same vertices asked under their hash part: only those whose fixture part happens to be
+    # their hash part have rows there (edges and tags alike)
+    hp = [O.part_of(v, 6) for v in vids]
+    g = sp.get_bound(et, hp, vids, cols)
+    r = st.get_bound(et, hp, vids, cols, in_bound=not out_bound)
+    ref = dict(r.vertices())
+    assert sorted(int(v) for v in g.vertex_ids) == sorted(ref)
+    for i, vid in enumerate(g.vertex_ids):
+        assert tuple(col[i] for col in g.vertex_columns) == tuple(ref[int(vid)])
+    assert by_vertex(g) == oracle_by_vertex(r)
+
+
+def test_get_bound_tag_prop_errors(qb):
+    sp, st = qb
+    parts, vids, _ = F.qb_request()
+    g = sp.get_bound(F.EDGE_TYPE, parts, vids, edge_cols() + [("tag_3001_col_0", O.SOURCE, 4242)])
+    assert sorted(g.failed) == [(0, -22), (1, -22), (2, -22)]
+    g = sp.get_bound(F.EDGE_TYPE, parts, vids, edge_cols() + [("nope", O.SOURCE, 3001)])
+    assert sorted(g.failed) == [(0, -23), (1, -23), (2, -23)]
 
 
 def test_get_bound_in_bound(qb):
