@@ -168,8 +168,9 @@ void nbg_rows_free(nbg_rows* rows);
  * edge_type < 0: in-bound scan (StorageClient.cpp:118).  filter: Expression::encode bytes or
  * empty.  Return columns are EDGE-owned props (key props _src/_dst/_rank/_type or schema props)
  * and SOURCE/DEST tag props (tag_id + name; returned per vertex in vertex_cols; unknown tag ->
- * E_TAG_PROP_NOT_FOUND, unknown prop -> E_IMPROPER_DATA_TYPE on every part).  Tag props inside
- * the push-down filter return NBG_E_UNSUPPORTED.  Request-level errors are
+ * E_TAG_PROP_NOT_FOUND, unknown prop -> E_IMPROPER_DATA_TYPE on every part).  $^ tag props in
+ * the push-down filter read the request part's vertex row ($$ -> E_INVALID_FILTER, as checkExp,
+ * QueryBaseProcessor.inl:160-238).  Request-level errors are
  * reported per part in failed_codes (QueryBaseProcessor.inl:470-477), not as the return.    */
 typedef struct {
   const char* name;

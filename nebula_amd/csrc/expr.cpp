@@ -236,9 +236,14 @@ struct Compiler {
       case kSourceProp:
       case kDestProp: {
         // graphd: getStepOutProps / getDstProps resolve the tag name (GoExecutor.cpp:470-527);
-        // storage filters with tag props stay unsupported on the device
-        if (!graphd || !tags) {
-          fail(NBG_E_UNSUPPORTED, "$^ / $$ tag props in a storage filter");
+        // storage filters: checkExp accepts $^ of a known tag prop and rejects $$
+        // (QueryBaseProcessor.inl:190-238 -> E_INVALID_FILTER)
+        if (!graphd && x.kind == kDestProp) {
+          fail(NBG_E_INVALID_FILTER, "$$ in a storage filter");
+          return VT_ERR;
+        }
+        if (!tags) {
+          fail(NBG_E_UNSUPPORTED, "$^ / $$ tag props without tag schemas");
           return VT_ERR;
         }
         bool known_tag = false;
@@ -256,7 +261,8 @@ struct Compiler {
         }
         // unknown tag: "No schema found" (GoExecutor.cpp:475-478); unknown prop of a known tag:
         // checkAndBuildContexts -> E_IMPROPER_DATA_TYPE on every part (QueryBaseProcessor.inl:56-66)
-        if (known_tag) fail(NBG_E_IMPROPER_DATA_TYPE, "unknown tag prop " + x.alias + "." + x.prop);
+        if (!graphd) fail(NBG_E_INVALID_FILTER, "unknown tag prop in a storage filter");
+        else if (known_tag) fail(NBG_E_IMPROPER_DATA_TYPE, "unknown tag prop " + x.alias + "." + x.prop);
         else fail(NBG_E_TAG_PROP_NOT_FOUND, "no schema found for tag " + x.alias);
         return VT_ERR;
       }

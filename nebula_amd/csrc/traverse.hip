@@ -61,6 +61,7 @@ struct PropDev {
   const uint8_t* present;
   const int64_t* str_off;
   const uint8_t* str_bytes;
+  const int32_t* part;  // tag columns: the part of each vertex's row (TagSpace::part)
 };
 struct EvalEnv {
   const PropDev* props;  // device table, one entry per schema field (Csr::prop_table)
@@ -75,6 +76,11 @@ struct EvalEnv {
   const int32_t* in_rows;
   uint32_t in_mask;
   const PropDev* iprops;
+  // storage (getBound) filters: a $^ tag row is visible when it sits in the request's part,
+  // which for an edge row is the part of the row's keys (Csr::row_part, local row = src - lo)
+  int32_t storage;
+  int64_t lo;
+  const int32_t* row_part;
 };
 __device__ inline uint32_t gidx_hash(int32_t g) { return uint32_t(g) * 2654435761u; }
 // row of the input table whose FROM vid is gidx g (-1: none)
@@ -213,7 +219,9 @@ __device__ Val eval_program(const Program* __restrict__ P, const EvalEnv& env, i
         // only a getBound naming its foreign part reads)
         const PropDev& tp = env.tprops[in.arg];
         const int32_t g = in.op == P_SRCTAG ? src_g : dst_g;
-        st[sp++] = tp.present[g] == 1 ? load_prop(tp, g) : mk(VT_ERR, 0);
+        const bool vis = env.storage ? tp.present[g] != 0 && tp.part[g] == env.row_part[src_g - env.lo]
+                                     : tp.present[g] == 1;
+        st[sp++] = vis ? load_prop(tp, g) : mk(VT_ERR, 0);
         break;
       }
       case P_INPUT: {
@@ -1445,7 +1453,7 @@ EvalEnv make_env(Ctx& c, EdgeSpace& es, Csr& csr, int32_t etype) {
     for (auto& kv : c.tags)
       for (const PropCol& p : kv.second.cols)
         tab.push_back(PropDev{p.type, p.width, p.data.p, p.present.as<uint8_t>(), p.str_off.as<int64_t>(),
-                              p.str_bytes.as<uint8_t>()});
+                              p.str_bytes.as<uint8_t>(), kv.second.part.as<int32_t>()});
     c.tag_table.alloc(sizeof(PropDev) * tab.size());
     NBG_HIP(hipMemcpy(c.tag_table.p, tab.data(), sizeof(PropDev) * tab.size(), hipMemcpyHostToDevice));
   }
@@ -2772,7 +2780,7 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
   FastArgs fp{};
   if (flen) {
     std::string msg;
-    int32_t rc = compile_expr(filter, flen, es.fields, false, !in_bound, &fprog, &msg);
+    int32_t rc = compile_expr(filter, flen, es.fields, false, !in_bound, &fprog, &msg, &c.tag_refs);
     if (rc == NBG_E_UNSUPPORTED) {
       delete h;
       throw Error(rc, "filter: " + msg);
@@ -2838,6 +2846,9 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
   NBG_HIP(hipMemcpyAsync(dcoff.p, coff.data(), size_t(nF + 1) * 8, hipMemcpyHostToDevice, c.stream));
   flags.alloc(size_t(E + 1));
   EvalEnv env = make_env(c, es, csr, in_bound ? -es.type : es.type);
+  env.storage = 1;
+  env.lo = c.owned_lo();
+  env.row_part = csr.row_part.as<int32_t>();
   DevBuf dprog;
   dprog.alloc(sizeof(Program));
   NBG_HIP(hipMemcpyAsync(dprog.p, &fprog, sizeof(Program), hipMemcpyHostToDevice, c.stream));

@@ -237,6 +237,35 @@ def test_get_bound_tag_props(qb, out_bound):
     assert by_vertex(g) == oracle_by_vertex(r)
 
 
+@pytest.mark.parametrize("case", ["only_tag", "tag_and_edge", "tag_string", "tag_or_edge"])
+def test_get_bound_tag_filters(qb, case):
+    # QueryBoundTest FilterOnlyTag (:260-291) / FilterTagAndEdge (:345-385): the push-down filter
+    # reads $^ props of the request part's vertex row; an evaluation error keeps the edge
+    sp, st = qb
+    parts, vids, cols = F.qb_request()
+    tag = X.Relational(X.GE, X.SourceProp("3001", "tag_3001_col_0"), X.Primary(20 + 3001))
+    edge = X.Relational(X.GE, X.AliasProp("e101", "col_0"), X.Primary(10007))
+    filt = {"only_tag": tag, "tag_and_edge": X.Logical(X.AND, tag, edge),
+            "tag_string": X.SourceProp("3005", "tag_3005_col_4").eq("tag_string_col_4"),
+            "tag_or_edge": X.Logical(X.OR, X.SourceProp("3002", "tag_3002_col_1") < 3010, edge)}[case]
+    g = sp.get_bound(F.EDGE_TYPE, parts, vids, cols, filt)
+    r = st.get_bound(F.EDGE_TYPE, parts, vids, cols, filt=filt.encode())
+    assert g.failed == r.failed() == []
+    assert by_vertex(g) == oracle_by_vertex(r)
+    ref = dict(r.vertices())
+    for i, vid in enumerate(g.vertex_ids):
+        assert tuple(col[i] for col in g.vertex_columns) == tuple(ref[int(vid)])
+    if case == "only_tag":  # check_response(res, 10, 12, 10001, 7, True)
+        assert len(g.vertex_ids) == 10 and all(len(v) == 7 for v in by_vertex(g).values())
+    if case == "tag_and_edge":  # check_response(res, 10, 12, 10007, 1, True)
+        assert len(g.vertex_ids) == 10 and all(len(v) == 1 for v in by_vertex(g).values())
+    # $$ and unknown tag props are invalid storage filters (checkExp)
+    for bad in (X.DestProp("3001", "tag_3001_col_0") > 1, X.SourceProp("3001", "nope") > 1,
+                X.SourceProp("9999", "tag_3001_col_0") > 1):
+        g = sp.get_bound(F.EDGE_TYPE, parts, vids, cols, bad)
+        assert sorted(g.failed) == [(0, -31), (1, -31), (2, -31)]
+
+
 def test_get_bound_tag_prop_errors(qb):
     sp, st = qb
     parts, vids, _ = F.qb_request()
