@@ -109,6 +109,19 @@ int32_t nbg_snapshot_load_part(nbg_ctx* ctx, int32_t part, const uint8_t* key_by
 int32_t nbg_snapshot_gen_rmat(nbg_ctx* ctx, int32_t scale, int32_t edge_factor, uint64_t seed,
                               int32_t edge_type);
 int32_t nbg_snapshot_finalize(nbg_ctx* ctx);
+/* Write path.  nbg_snapshot_write_part takes one part's batch of the KV puts
+ * AddEdgesProcessor::process / AddVerticesProcessor::process hand to doPut
+ * (AddEdgesProcessor.cpp:15-31, AddVerticesProcessor.cpp:16-38: keys carry version
+ * INT64_MAX - now_us; an identical key overwrites) in the same blob layout as load_part.
+ * Before the first finalize it is load_part.  After it the snapshot must have been finalized
+ * with option "writable" = 1 (which keeps the decoded tuples on the device); the batch is
+ * decoded behind them and becomes visible at nbg_snapshot_commit, which rebuilds the CSRs from
+ * the device-resident tuples (queries in between read the previous commit).  Commit is
+ * collective when world > 1.  Errors: NBG_E_STATE (not writable), NBG_E_PART_NOT_FOUND.     */
+int32_t nbg_snapshot_write_part(nbg_ctx* ctx, int32_t part, const uint8_t* key_bytes,
+                                const uint64_t* key_offsets, const uint8_t* val_bytes,
+                                const uint64_t* val_offsets, size_t n);
+int32_t nbg_snapshot_commit(nbg_ctx* ctx);
 
 typedef struct {
   int64_t num_vertices;     /* global vertex count (vertices appearing in any edge)          */

@@ -28,7 +28,8 @@ EXPORTS = [
     "nbg_ctx_create", "nbg_ctx_destroy", "nbg_last_error", "nbg_comm_unique_id", "nbg_comm_init",
     "nbg_comm_init_local",
     "nbg_part_of", "nbg_rank_of_part", "nbg_schema_set_edge", "nbg_schema_set_tag", "nbg_snapshot_load_part",
-    "nbg_snapshot_gen_rmat", "nbg_snapshot_finalize", "nbg_snapshot_info_get",
+    "nbg_snapshot_gen_rmat", "nbg_snapshot_finalize", "nbg_snapshot_write_part", "nbg_snapshot_commit",
+    "nbg_snapshot_info_get",
     "nbg_snapshot_out_degree", "nbg_rows_free", "nbg_get_bound", "nbg_bound_stats", "nbg_go", "nbg_shortest_path",
     "nbg_last_timing", "nbg_set_option",
 ]
@@ -116,6 +117,8 @@ def load(path: str | os.PathLike | None = None):
         "nbg_snapshot_load_part": (i32, [vp, i32, vp, vp, vp, vp, sz]),
         "nbg_snapshot_gen_rmat": (i32, [vp, i32, i32, u64, i32]),
         "nbg_snapshot_finalize": (i32, [vp]),
+        "nbg_snapshot_write_part": (i32, [vp, i32, vp, vp, vp, vp, sz]),
+        "nbg_snapshot_commit": (i32, [vp]),
         "nbg_snapshot_info_get": (i32, [vp, i32, C.POINTER(SnapshotInfo)]),
         "nbg_snapshot_out_degree": (i64, [vp, i32, i64]),
         "nbg_rows_free": (None, [C.POINTER(Rows)]),

@@ -173,6 +173,22 @@ int32_t nbg_snapshot_finalize(nbg_ctx* ctx) {
   });
 }
 
+int32_t nbg_snapshot_write_part(nbg_ctx* ctx, int32_t part, const uint8_t* key_bytes, const uint64_t* key_offsets,
+                                const uint8_t* val_bytes, const uint64_t* val_offsets, size_t n) {
+  return guarded(ctx, [&](Ctx& c) {
+    if (n && (!key_bytes || !key_offsets || !val_offsets)) throw Error(NBG_E_INVALID_ARG, "null KV arrays");
+    nbg::snapshot_write_part(c, part, key_bytes, key_offsets, val_bytes, val_offsets, n);
+    return NBG_OK;
+  });
+}
+
+int32_t nbg_snapshot_commit(nbg_ctx* ctx) {
+  return guarded(ctx, [&](Ctx& c) {
+    nbg::snapshot_commit(c);
+    return NBG_OK;
+  });
+}
+
 int32_t nbg_snapshot_info_get(nbg_ctx* ctx, int32_t edge_type, nbg_snapshot_info* out) {
   return guarded(ctx, [&](Ctx& c) {
     if (!out) throw Error(NBG_E_INVALID_ARG, "null out");

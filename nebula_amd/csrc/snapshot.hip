@@ -64,8 +64,45 @@ static void grow_copy(Ctx& c, DevBuf& b, size_t need) {
   b = std::move(nb);
 }
 
+__global__ void k_hash_part(const int64_t* src, int32_t* part, int64_t n, int32_t parts) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    part[i] = int32_t(uint64_t(src[i]) % uint64_t(parts) + 1);
+}
+
+// A device-generated stage (snapshot_gen_rmat) keeps rank / version as constants, the key part
+// implicit (hash rule), no sequence numbers and no present bytes.  Before decoded KV tuples are
+// appended behind it (a write batch), spell those columns out: the generated tuples precede every
+// later write (sequence 0), their part is the hash part of the key's vertex.
+static void materialize_stage(Ctx& c, Staging& s, size_t nfields, bool with_props) {
+  if (s.n == 0 || s.seq.p) return;
+  const int64_t n = s.n;
+  const size_t cap = std::max(s.cap, size_t(n));
+  s.rank.alloc(cap * 8);
+  s.ver.alloc(cap * 8);
+  s.part.alloc(cap * 4);
+  s.seq.alloc(cap * 8);
+  fill<int64_t>(c, s.rank.as<int64_t>(), s.rank_value, n);
+  fill<int64_t>(c, s.ver.as<int64_t>(), s.ver_value, n);
+  fill<int64_t>(c, s.seq.as<int64_t>(), 0, n);
+  k_hash_part<<<grid_for(n), 256, 0, c.stream>>>(s.src.as<int64_t>(), s.part.as<int32_t>(), n, c.num_parts);
+  NBG_HIP(hipGetLastError());
+  if (with_props) {
+    s.present.resize(std::max(s.present.size(), nfields));
+    for (size_t f = 0; f < nfields; f++)
+      if (!s.present[f].p) {
+        s.present[f].alloc(cap);
+        fill<uint8_t>(c, s.present[f].as<uint8_t>(), 1, n);
+      }
+  }
+  s.rank_const = s.ver_const = false;
+  s.cap = cap;
+  c.load_seq = std::max<int64_t>(c.load_seq, 1);
+  NBG_HIP(hipStreamSynchronize(c.stream));
+}
+
 static void stage_reserve(Ctx& c, Staging& s, size_t nfields, size_t extra, bool with_props,
                           const std::vector<Field>& fields) {
+  materialize_stage(c, s, nfields, with_props);
   size_t need = size_t(s.n) + extra;
   if (need <= s.cap) return;
   size_t cap = std::max(need, s.cap * 2);
@@ -314,9 +351,8 @@ static StageOut stage_ptrs(Staging& s, size_t nf) {
   return o;
 }
 
-void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t* koff,
+static void decode_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t* koff,
                         const uint8_t* vb, const uint64_t* voff, size_t n) {
-  if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
   if (part < 0 || part > c.num_parts) throw Error(NBG_E_PART_NOT_FOUND, "part out of range");
   if (owner_of_part(part, c.world) != c.rank)
     throw Error(NBG_E_PART_NOT_FOUND, "part " + std::to_string(part) + " is not owned by this rank");
@@ -389,6 +425,140 @@ void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
   }
   c.load_seq += int64_t(n);
   c.build_seconds += now_s() - t0;
+}
+
+void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t* koff,
+                        const uint8_t* vb, const uint64_t* voff, size_t n) {
+  if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
+  decode_part(c, part, kb, koff, vb, voff, n);
+}
+
+// ------------------------------------------------------------------------------------------
+// Write path.  AddEdgesProcessor / AddVerticesProcessor turn a request into one
+// batch of KV puts per part (AddEdgesProcessor.cpp:15-31, AddVerticesProcessor.cpp:16-38; the
+// version in the key is INT64_MAX - now_us, so a newer write of the same edge sorts first and
+// an identical key overwrites).  A writable snapshot keeps the decoded tuples of everything
+// loaded so far (the "log") next to the CSRs; a write batch is decoded by the same k_decode_kv /
+// k_decode_vkv behind the log with later load sequence numbers, so the CSR build's version
+// dedup (bytewise-first key, last write of an identical key) gives exactly what the prefix scan
+// of the written RocksDB part returns.  nbg_snapshot_commit rebuilds the vertex map, CSRs,
+// transposes and tag columns from the log on the device -- nothing is re-uploaded -- and until
+// then queries keep reading the previous commit (a RocksDB snapshot's view).
+// ------------------------------------------------------------------------------------------
+static void clone_buf(Ctx& c, const DevBuf& from, DevBuf& to) {
+  to.release();
+  if (!from.p || !from.bytes) return;
+  to.alloc(from.bytes);
+  NBG_HIP(hipMemcpyAsync(to.p, from.p, from.bytes, hipMemcpyDeviceToDevice, c.stream));
+}
+static void clone_bufs(Ctx& c, const std::vector<DevBuf>& from, std::vector<DevBuf>& to) {
+  to.clear();
+  to.resize(from.size());
+  for (size_t i = 0; i < from.size(); i++) clone_buf(c, from[i], to[i]);
+}
+static void clone_staging(Ctx& c, const Staging& from, Staging& to) {
+  to.n = from.n;
+  clone_buf(c, from.src, to.src);
+  clone_buf(c, from.dst, to.dst);
+  clone_buf(c, from.rank, to.rank);
+  clone_buf(c, from.ver, to.ver);
+  clone_buf(c, from.part, to.part);
+  clone_buf(c, from.seq, to.seq);
+  to.rank_const = from.rank_const;
+  to.ver_const = from.ver_const;
+  to.rank_value = from.rank_value;
+  to.ver_value = from.ver_value;
+  clone_bufs(c, from.props, to.props);
+  clone_bufs(c, from.present, to.present);
+  clone_bufs(c, from.str_len, to.str_len);
+  to.cap = from.cap;
+}
+// staging <- log (the tuples of the last commit), value heap included
+static void restore_log(Ctx& c) {
+  for (auto& kv : c.edges) {
+    clone_staging(c, kv.second.out_log, kv.second.out_stage);
+    clone_staging(c, kv.second.in_log, kv.second.in_stage);
+  }
+  for (auto& kv : c.tags) clone_staging(c, kv.second.log, kv.second.stage);
+  clone_buf(c, c.heap_log, c.heap);
+  c.heap_used = c.heap_log_used;
+  NBG_HIP(hipStreamSynchronize(c.stream));
+}
+static void save_log(Ctx& c) {
+  for (auto& kv : c.edges) {
+    clone_staging(c, kv.second.out_stage, kv.second.out_log);
+    clone_staging(c, kv.second.in_stage, kv.second.in_log);
+  }
+  for (auto& kv : c.tags) clone_staging(c, kv.second.stage, kv.second.log);
+  clone_buf(c, c.heap, c.heap_log);
+  c.heap_log_used = c.heap_used;
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  c.has_log = true;
+}
+// drop everything snapshot_finalize derives from the staged tuples
+static void reset_derived(Ctx& c) {
+  c.vid_of.release();
+  c.ht_keys.release();
+  c.ht_vals.release();
+  c.ht_cap = 0;
+  c.ht_has_min = false;
+  c.ht_min_gidx = -1;
+  c.tag_table.release();
+  for (auto& kv : c.edges) {
+    EdgeSpace& es = kv.second;
+    es.out = Csr();
+    es.in = Csr();
+    es.rep_out = Csr();
+    es.rep_in = Csr();
+    es.has_rep = false;
+    es.tr = Csr();
+    es.t_eid.release();
+    es.has_tr = es.has_t_eid = false;
+    es.out_nnz_global = -1;
+    es.slab_k = 0;
+    es.slab_col.release();
+    es.slab_props.clear();
+    es.odeg.release();
+  }
+  for (auto& kv : c.tags) {
+    kv.second.cols.clear();
+    kv.second.part.release();
+  }
+  c.sp_dist[0].release();
+  c.sp_dist[1].release();
+  c.sp_dist_bytes = 0;
+  c.sp_dirty = false;
+  c.sp = Ctx::SpWork();
+}
+
+void snapshot_write_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t* koff,
+                         const uint8_t* vb, const uint64_t* voff, size_t n) {
+  if (!c.finalized) {  // before the first commit a write batch is one more loaded batch
+    decode_part(c, part, kb, koff, vb, voff, n);
+    return;
+  }
+  if (!c.has_log) throw Error(NBG_E_STATE, "snapshot is not writable (set option writable=1 before finalize)");
+  if (!c.pending_writes) {
+    restore_log(c);
+    c.pending_writes = true;
+  }
+  decode_part(c, part, kb, koff, vb, voff, n);
+}
+
+void snapshot_commit(Ctx& c) {
+  if (!c.finalized) {
+    snapshot_finalize(c);
+    return;
+  }
+  if (!c.has_log) throw Error(NBG_E_STATE, "snapshot is not writable (set option writable=1 before finalize)");
+  // collective when world > 1: every rank rebuilds, with or without writes of its own
+  if (!c.pending_writes) restore_log(c);
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  reset_derived(c);
+  c.pending_writes = false;
+  c.finalized = false;
+  snapshot_finalize(c);
+  c.commits++;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1492,6 +1662,7 @@ static void build_tag_columns(Ctx& c) {
 void snapshot_finalize(Ctx& c) {
   if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
   double t0 = now_s();
+  if (c.opt("writable", 0)) save_log(c);
   // 1. referenced vids (src/dst of every staged tuple), sign-flipped for unsigned sort
   int64_t total = 0;
   for (auto& kv : c.edges) total += 2 * (kv.second.out_stage.n + kv.second.in_stage.n);

@@ -198,6 +198,18 @@ class GraphSpace:
     def finalize(self):
         self._check(self.L.nbg_snapshot_finalize(self.h))
 
+    def write_part(self, part: int, pairs):
+        """One part's batch of AddEdges / AddVertices KV puts (AddEdgesProcessor.cpp:15-31,
+        AddVerticesProcessor.cpp:16-38); visible to queries after commit().  Needs
+        set_option("writable", 1) before finalize()."""
+        kb, koff, vb, voff = pairs if isinstance(pairs, tuple) else pack_kv(pairs)
+        n = len(koff) - 1
+        self._check(self.L.nbg_snapshot_write_part(self.h, part, _p(kb), _p(koff), _p(vb), _p(voff), n))
+
+    def commit(self):
+        """Rebuild the device snapshot from the written log (collective when world_size > 1)."""
+        self._check(self.L.nbg_snapshot_commit(self.h))
+
     def info(self, edge_type: int) -> dict:
         si = _lib.SnapshotInfo()
         self._check(self.L.nbg_snapshot_info_get(self.h, edge_type, C.byref(si)))

@@ -279,3 +279,54 @@ def test_sharded_tag_props(world):
             assert union_rows(res) == ms(ref.rows())
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_writes_commit(world):
+    """Write path with sharded ownership: each rank takes the write batches of its
+    own parts (StorageClient routes an AddEdges part to its leader); commit is collective and
+    rebuilds the vertex map / CSRs / tag slices on every rank, new vertices included."""
+    import random
+
+    import test_gpu_tags as T
+    import test_gpu_writes as W
+    base, vids = T.random_space_kv(8)
+    rng = random.Random(2)
+    new_vids = [rng.randrange(-2**62, 2**62) for _ in range(25)]
+    batch = W.write_batch(rng, vids, new_vids, W.BASE_VER - 10)
+    g = Group(world, parts=T.PARTS)
+    try:
+        def load(r, s):
+            s.set_option("writable", 1)
+            s.set_edge_schema(T.ET, [("weight", O.INT)])
+            s.set_tag_schema(T.PERSON, "person", W.FIELDS)
+            for p, kv in base.items():
+                if kv and p % world == r:
+                    s.load_part(p, kv)
+            s.finalize()
+
+        # round 1: every rank writes its parts; round 2: only rank 0's parts get writes, the
+        # other ranks still join the collective commit
+        batch2 = W.write_batch(rng, vids + new_vids, [], W.BASE_VER - 20)
+        batch2 = {p: kv for p, kv in batch2.items() if p % world == 0}
+
+        def write(b):
+            def run(r, s):
+                for p, kv in b.items():
+                    if kv and p % world == r:
+                        s.write_part(p, kv)
+                s.commit()
+            return run
+        g.each(load)
+        g.each(write(batch))
+        g.each(write(batch2))
+        st = W.fresh_oracle([base, batch, batch2])
+        starts = vids[::19] + new_vids[:4]
+        for steps, where, ys, distinct in W.QUERIES:
+            res = g.go(starts, steps, T.ET, where=where, yields=ys, distinct=distinct)
+            ref = st.go(starts, steps, T.ET, where=X.encode(where), yields=[y.encode() for y in ys],
+                        distinct=distinct)
+            assert ref.code == 0, ref.error
+            assert union_rows(res) == ms(ref.rows())
+    finally:
+        g.close()

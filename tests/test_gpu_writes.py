@@ -1,0 +1,202 @@
+"""GPU parity of the write path: AddEdges / AddVertices KV batches applied to a
+finalized snapshot (nbg_snapshot_write_part + nbg_snapshot_commit).
+
+The reference writes `edgeKey(part, src, type, rank, dst, INT64_MAX - now_us)` /
+`vertexKey(part, vid, tag, INT64_MAX - now_us)` puts per part (AddEdgesProcessor.cpp:15-31,
+AddVerticesProcessor.cpp:16-38), so a later write of the same edge carries a smaller version and
+is read first by the prefix scan, and an identical key overwrites.  The oracle is the same
+store built from base + write batches in write order; after each commit GO, getBound and
+FIND SHORTEST PATH must match it exactly, and before the commit queries must still see the
+previous commit.
+"""
+import random
+from collections import Counter
+
+import numpy as np
+import pytest
+
+import oracle as O
+from nebula_amd import GraphSpace, NbgError, synth
+from nebula_amd import expr as X
+from test_gpu_tags import ET, PARTS, PERSON, random_space_kv
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = [("name", O.STRING), ("score", O.INT), ("wt", O.DOUBLE)]
+BASE_VER = 2**63 - 2
+
+
+def ms(rows):
+    return Counter(tuple(r) for r in rows)
+
+
+def write_batch(rng, vids, new_vids, ver):
+    """One AddEdges + AddVertices round: new edges (also to brand-new vertices), newer versions
+    of existing edges, identical-key rewrites, new / updated tag rows."""
+    part = lambda v: O.part_of(v, PARTS)  # noqa: E731
+    batch = {p: [] for p in range(1, PARTS + 1)}
+    every = vids + new_vids
+    for _ in range(600):
+        s, t = rng.choice(every), rng.choice(every)
+        kind = rng.random()
+        v = BASE_VER if kind < 0.2 else ver  # 20%: identical key of a base edge -> overwrite
+        w = rng.randrange(1000, 2000)
+        batch[part(s)].append((O.edge_key(part(s), s, ET, 0, t, v), O.encode_row([w])))
+        batch[part(t)].append((O.edge_key(part(t), t, -ET, 0, s, v), b""))
+    for v in new_vids + rng.sample(vids, 40):
+        p = part(v)
+        batch[p].append((O.vertex_key(p, v, PERSON, ver), O.encode_row([f"w{abs(v) % 13}", rng.randrange(100), 1.5])))
+    return batch
+
+
+def fresh_oracle(history):
+    st = O.Store(PARTS)
+    st.set_edge_schema(ET, [("weight", O.INT)], name="e")
+    st.set_tag_schema(PERSON, FIELDS, name="person")
+    merged = {p: [] for p in range(1, PARTS + 1)}
+    for parts in history:
+        for p, kv in parts.items():
+            merged[p].extend(kv)
+    for p, kv in merged.items():
+        if kv:
+            st.put(p, kv)
+    st.finalize()
+    return st
+
+
+QUERIES = [
+    (1, None, [X.SourceProp("person", "name"), X.DestProp("person", "score"), X.AliasProp("e", "weight")], False),
+    (2, X.AliasProp("e", "weight") > 900, [X.EdgeDst("e"), X.DestProp("person", "name")], False),
+    (3, None, [X.EdgeDst("e")], True),
+]
+
+
+def check_go(sp, st, starts):
+    for steps, where, ys, distinct in QUERIES:
+        rs = sp.go(starts, steps, ET, where=where, yields=ys, distinct=distinct)
+        ref = st.go(starts, steps, ET, where=X.encode(where), yields=[y.encode() for y in ys], distinct=distinct)
+        assert ref.code == 0, ref.error
+        assert ms(rs.rows()) == ms(ref.rows())
+
+
+def check_bound(sp, st, vids):
+    q = vids[::7]
+    parts = [O.part_of(v, PARTS) for v in q]
+    cols = [("_dst", O.EDGE, 0), ("weight", O.EDGE, 0)]
+    g = sp.get_bound(ET, parts, q, cols)
+    r = st.get_bound(ET, parts, q, cols)
+    assert g.failed == r.failed() == []
+    rows = g.rows()
+    got = {int(v): rows[g.vertex_row_offsets[i]:g.vertex_row_offsets[i + 1]] for i, v in enumerate(g.vertex_ids)}
+    want = {}
+    for i, row in enumerate(r.rows()):
+        want.setdefault(r.row_vertex(i), []).append(row)
+    assert got == want
+
+
+def test_writes_commit_and_snapshot_view():
+    rng = random.Random(11)
+    base, vids = random_space_kv(21)
+    sp = GraphSpace(PARTS)
+    try:
+        sp.set_option("writable", 1)
+        sp.set_edge_schema(ET, [("weight", O.INT)])
+        sp.set_tag_schema(PERSON, "person", FIELDS)
+        for p, kv in base.items():
+            if kv:
+                sp.load_part(p, kv)
+        sp.finalize()
+        history = [base]
+        st = fresh_oracle(history)
+        starts = vids[::19]
+        check_go(sp, st, starts)
+        seen = set(vids)
+        for rnd in range(3):
+            new_vids = []
+            while len(new_vids) < 30:
+                v = rng.randrange(-2**62, 2**62)
+                if v not in seen:
+                    seen.add(v)
+                    new_vids.append(v)
+            batch = write_batch(rng, vids, new_vids, BASE_VER - 10 * (rnd + 1))
+            for p, kv in batch.items():
+                if kv:
+                    sp.write_part(p, kv)
+            check_go(sp, st, starts)  # not committed yet: the previous snapshot
+            sp.commit()
+            history.append(batch)
+            st = fresh_oracle(history)
+            check_go(sp, st, starts + new_vids[:5])
+            check_bound(sp, st, vids + new_vids)
+            vids = vids + new_vids
+        sp.commit()  # empty commit: same snapshot
+        check_go(sp, st, starts)
+    finally:
+        sp.close()
+
+
+def test_write_requires_writable():
+    base, vids = random_space_kv(4, n_vertices=50, n_edges=200)
+    sp = GraphSpace(PARTS)
+    try:
+        sp.set_edge_schema(ET, [("weight", O.INT)])
+        sp.set_tag_schema(PERSON, "person", FIELDS)
+        for p, kv in base.items():
+            if kv:
+                sp.write_part(p, kv)  # before finalize: a load
+        sp.finalize()
+        p = O.part_of(vids[0], PARTS)
+        with pytest.raises(NbgError) as e:
+            sp.write_part(p, [(O.edge_key(p, vids[0], ET, 0, vids[1], 5), O.encode_row([1]))])
+        assert e.value.code == -1002
+        with pytest.raises(NbgError) as e:
+            sp.commit()
+        assert e.value.code == -1002
+    finally:
+        sp.close()
+
+
+@pytest.mark.parametrize("scale", [10, 19])
+def test_rmat_writes_paths_and_go(scale):
+    """Writes on top of the device-generated RMAT snapshot: shortest paths and GO after commit.
+    Scale 19 (8.4 M tuples) is past one launch of the capped build grids."""
+    follow = 1
+    sp = GraphSpace(64)
+    try:
+        sp.set_option("writable", 1)
+        sp.set_edge_schema(follow, [("weight", O.INT)])
+        sp.gen_rmat(scale, 16, 1, follow)
+        sp.finalize()
+        s, t = synth.pairs(scale, 16, 1, 100)
+        rng = random.Random(5)
+        batch = {}
+        for i in range(100):  # shortcut edges between the pair endpoints
+            a, b = int(s[rng.randrange(len(s))]), int(t[rng.randrange(len(t))])
+            pa, pb = O.part_of(a, 64), O.part_of(b, 64)
+            batch.setdefault(pa, []).append((O.edge_key(pa, a, follow, 0, b, BASE_VER - 1), O.encode_row([7])))
+            batch.setdefault(pb, []).append((O.edge_key(pb, b, -follow, 0, a, BASE_VER - 1), b""))
+        for p, kv in batch.items():
+            sp.write_part(p, kv)
+        sp.commit()
+        st = O.Store(64)
+        st.set_edge_schema(follow, [("weight", O.INT)], name="follow")
+        st.load_rmat(scale, 16, 1, follow)
+        for p, kv in batch.items():
+            st.put(p, kv)
+        st.finalize()
+        got = sp.shortest_path(s, t, follow, 4).rows()
+        r = st.shortest_path(np.asarray(s, np.int64), np.asarray(t, np.int64), follow, 4)
+        want = []
+        for row in r.rows():
+            row = [x for x in row if x is not None]
+            want.append((row[0], row[1], row[2], tuple(row[3:])))
+        assert got == want
+        starts = [int(x) for x in s[:8]]
+        ys = [X.EdgeDst("follow"), X.AliasProp("follow", "weight")]
+        for steps in (1, 2):
+            rs = sp.go(starts, steps, follow, yields=ys)
+            ref = st.go(starts, steps, follow, yields=[y.encode() for y in ys])
+            assert ref.code == 0, ref.error
+            assert ms(rs.rows()) == ms(ref.rows())
+    finally:
+        sp.close()

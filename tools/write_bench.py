@@ -1,0 +1,105 @@
+"""Write-path cost on the RMAT snapshot: a writable snapshot takes a batch of
+AddEdges puts (out-edge key + weight row, in-edge key + empty row, version INT64_MAX - 1 - 1 so
+it is the newest version, AddEdgesProcessor.cpp:15-31) through nbg_snapshot_write_part, then
+nbg_snapshot_commit rebuilds the CSRs from the device-resident log.  Prints one JSON line with
+the initial build, the write-batch decode and the commit times, and GO 3 STEPS before / after.
+
+    python tools/write_bench.py --scale 24 --edges 1048576
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from nebula_amd import GraphSpace, synth  # noqa: E402
+
+PARTS, FOLLOW, SEED = 64, 1, 1
+KEY = np.dtype([("part", "<i4"), ("src", "<i8"), ("type", "<i4"), ("rank", "<i8"), ("dst", "<i8"),
+                ("ver", "<i8")])
+
+
+def varint_rows(w):
+    """RowWriter row of schema (weight int): header byte 0 + LEB128 varint (w < 2^14)."""
+    lo = (w & 0x7F) | np.where(w >= 128, 0x80, 0)
+    hi = w >> 7
+    n = np.where(w >= 128, 3, 2).astype(np.uint64)
+    out = np.zeros((len(w), 3), np.uint8)
+    out[:, 1] = lo
+    out[:, 2] = hi
+    mask = np.ones((len(w), 3), bool)
+    mask[:, 2] = w >= 128
+    return out[mask], np.concatenate([[0], np.cumsum(n)]).astype(np.uint64)
+
+
+def batches(src, dst, w, ver):
+    out = {}
+    for s, d, et, with_val in ((src, dst, FOLLOW, True), (dst, src, -FOLLOW, False)):
+        part = (s.astype(np.uint64) % np.uint64(PARTS) + np.uint64(1)).astype(np.int32)
+        for p in np.unique(part):
+            sel = part == p
+            k = np.zeros(int(sel.sum()), KEY)
+            k["part"], k["src"], k["type"], k["dst"], k["ver"] = p, s[sel], et, d[sel], ver
+            kb = np.frombuffer(k.tobytes() + b"\0", np.uint8)
+            koff = (np.arange(len(k) + 1) * 40).astype(np.uint64)
+            if with_val:
+                vb, voff = varint_rows(w[sel])
+                vb = np.concatenate([vb, [0]]).astype(np.uint8)
+            else:
+                vb, voff = np.zeros(1, np.uint8), np.zeros(len(k) + 1, np.uint64)
+            out.setdefault(int(p), []).append((kb, koff, vb, voff))
+    return out
+
+
+def go3(sp, starts):
+    sp.go(starts, 3, FOLLOW)  # warm
+    t = time.perf_counter()
+    rs = sp.go(starts, 3, FOLLOW)
+    return (time.perf_counter() - t) * 1e3, rs.n_rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scale", type=int, default=24)
+    ap.add_argument("--edges", type=int, default=1 << 20)
+    a = ap.parse_args()
+    sp = GraphSpace(PARTS)
+    sp.set_option("writable", 1)
+    sp.set_edge_schema(FOLLOW, [("weight", 2)])
+    t0 = time.perf_counter()
+    sp.gen_rmat(a.scale, 16, SEED, FOLLOW)
+    sp.finalize()
+    build_s = time.perf_counter() - t0
+    info0 = sp.info(FOLLOW)
+    starts = [int(x) for x in synth.seeds(a.scale, 16, SEED, 1)]
+    go_before = go3(sp, starts)
+    rng = np.random.default_rng(3)
+    s, _ = synth.pairs(a.scale, 16, SEED, a.edges, pick_seed=5)
+    _, d = synth.pairs(a.scale, 16, SEED, a.edges, pick_seed=6)
+    w = rng.integers(1000, 2000, a.edges)
+    bs = batches(np.asarray(s, np.int64), np.asarray(d, np.int64), w, 2**63 - 3)
+    t1 = time.perf_counter()
+    for p, lst in bs.items():
+        for blob in lst:
+            sp.write_part(p, blob)
+    write_s = time.perf_counter() - t1
+    t2 = time.perf_counter()
+    sp.commit()
+    commit_s = time.perf_counter() - t2
+    info1 = sp.info(FOLLOW)
+    go_after = go3(sp, starts)
+    print(json.dumps({
+        "workload": f"rmat{a.scale} + AddEdges batch of {a.edges} edges (out + in keys)",
+        "initial_build_s": round(build_s, 3), "write_part_s": round(write_s, 3), "commit_s": round(commit_s, 3),
+        "out_edges_before": info0["local_out_edges"], "out_edges_after": info1["local_out_edges"],
+        "device_bytes_before": info0["device_bytes"], "device_bytes_after": info1["device_bytes"],
+        "go3_ms_before": round(go_before[0], 3), "go3_rows_before": go_before[1],
+        "go3_ms_after": round(go_after[0], 3), "go3_rows_after": go_after[1],
+    }))
+
+
+if __name__ == "__main__":
+    main()
