@@ -200,3 +200,31 @@ def test_rmat_writes_paths_and_go(scale):
             assert ms(rs.rows()) == ms(ref.rows())
     finally:
         sp.close()
+
+
+def test_write_versions_known_answer():
+    """The oracle KAT of tests/test_oracle_storage.py::test_write_path_versions through the
+    device write path: base load, then a write batch with a newer version (smaller low byte), an
+    identical-key rewrite and a newer version whose bytes sort later (the older row stays)."""
+    t0 = (2**63 - 1 - 1_700_000_000_000_000) & ~0xFF | 0x40
+    t1 = t0 & ~0xFF
+    src, part = 11, O.part_of(11, 4)
+    base = [(O.edge_key(part, src, 7, 0, 21, t0), O.encode_row([1])),
+            (O.edge_key(part, src, 7, 0, 22, t0), O.encode_row([2])),
+            (O.edge_key(part, src, 7, 0, 23, t1), O.encode_row([5]))]
+    writes = [(O.edge_key(part, src, 7, 0, 21, t0 - 5), O.encode_row([3])),
+              (O.edge_key(part, src, 7, 0, 22, t0), O.encode_row([4])),
+              (O.edge_key(part, src, 7, 0, 23, t1 - 1), O.encode_row([6]))]
+    sp = GraphSpace(4)
+    try:
+        sp.set_option("writable", 1)
+        sp.set_edge_schema(7, [("w", O.INT)])
+        sp.load_part(part, base)
+        sp.finalize()
+        cols = [("_dst", O.EDGE, 0), ("w", O.EDGE, 0)]
+        assert [tuple(r) for r in sp.get_bound(7, [part], [src], cols).rows()] == [(21, 1), (22, 2), (23, 5)]
+        sp.write_part(part, writes)
+        sp.commit()
+        assert [tuple(r) for r in sp.get_bound(7, [part], [src], cols).rows()] == [(21, 3), (22, 4), (23, 5)]
+    finally:
+        sp.close()

@@ -163,3 +163,28 @@ def test_stats_validation_and_in_bound(oracle):
     f = (X.AliasProp("e101", "col_3") > 100).encode()
     r = st.bound_stats(F.EDGE_TYPE, parts, vids, [("_rank", O.EDGE, 0), ("col_9", O.EDGE, 0)], [1, 3], filt=f)
     assert r.rows()[0][0] == 0 and r.rows()[0][1] != r.rows()[0][1]  # nothing passes: AVG = 0/0 = NaN
+
+
+def test_write_path_versions(oracle):
+    """What the write path feeds the snapshot: AddEdgesProcessor keys carry
+    version INT64_MAX - now_us appended little-endian (AddEdgesProcessor.cpp:15-31), and the scan
+    keeps the bytewise-first version per (rank, dst) (P3, QueryBaseProcessor.inl:349-362) -- the
+    newer write when its low version byte is smaller, the older one when the version bytes wrap
+    (e.g. ...00 vs ...FF); rewriting an identical key overwrites (RocksDB put).  The GPU write
+    path (tests/test_gpu_writes.py) is checked against an oracle that does all three."""
+    st = O.Store(4)
+    st.set_edge_schema(7, [("w", O.INT)], name="e")
+    t0 = (2**63 - 1 - 1_700_000_000_000_000) & ~0xFF | 0x40  # INT64_MAX - now_us, low byte 0x40
+    t1 = t0 & ~0xFF                                           # low byte 0x00
+    src, part = 11, O.part_of(11, 4)
+    kv = [(O.edge_key(part, src, 7, 0, 21, t0), O.encode_row([1])),          # first AddEdges
+          (O.edge_key(part, src, 7, 0, 22, t0), O.encode_row([2])),
+          (O.edge_key(part, src, 7, 0, 23, t1), O.encode_row([5])),
+          (O.edge_key(part, src, 7, 0, 21, t0 - 5), O.encode_row([3])),      # later: 0x3b < 0x40
+          (O.edge_key(part, src, 7, 0, 22, t0), O.encode_row([4])),          # identical key again
+          (O.edge_key(part, src, 7, 0, 23, t1 - 1), O.encode_row([6]))]      # later, but 0xff > 0x00
+    st.put(part, kv)
+    st.finalize()
+    res = st.get_bound(7, [part], [src], [("_dst", O.EDGE, 0), ("w", O.EDGE, 0)])
+    assert res.failed() == []
+    assert [tuple(r) for r in res.rows()] == [(21, 3), (22, 4), (23, 5)]
