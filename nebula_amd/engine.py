@@ -16,6 +16,8 @@ Everything executes in libnebula_amd.so on the GPU; there is no Python or CPU co
 from __future__ import annotations
 
 import ctypes as C
+import struct
+import time
 from dataclasses import dataclass, field
 from typing import Iterable, Sequence
 
@@ -131,6 +133,10 @@ class GraphSpace:
         if not self.h:
             raise RuntimeError("nbg_ctx_create failed: no MI355X visible or bad arguments "
                                "(the engine has no CPU path)")
+
+    def part_of(self, vid: int) -> int:
+        """StorageClient partition rule: vid % num_parts + 1 over the unsigned bits (nbg_part_of)."""
+        return int(self.L.nbg_part_of(vid, self.num_parts))
 
     # ---- lifecycle -------------------------------------------------------------------
     def close(self):
@@ -460,6 +466,114 @@ class QueryStatsProcessor:
         if rs.n_rows == 0:
             return QueryStatsResponse(failed, [], None)
         return QueryStatsResponse(failed, list(zip(kept, rs.types)), rs.rows()[0])
+
+
+# ---- write path ----------------------------------------------------------------
+INT64_MAX = (1 << 63) - 1
+_EDGE_KEY = struct.Struct("<iqiqqq")    # NebulaKeyUtils::edgeKey (NebulaKeyUtils.h:14-21)
+_VERTEX_KEY = struct.Struct("<iqiq")    # NebulaKeyUtils::vertexKey
+
+
+@dataclass
+class EdgeKey:
+    """storage::cpp2::EdgeKey (storage.thrift:111-118); edge_type < 0 is the in-edge."""
+    src: int
+    edge_type: int
+    ranking: int
+    dst: int
+
+
+@dataclass
+class Edge:
+    key: EdgeKey
+    props: bytes = b""   # RowWriter-encoded row (empty for in-edges)
+
+
+@dataclass
+class AddEdgesRequest:
+    """storage::cpp2::AddEdgesRequest (storage.thrift:158-164): part -> edges."""
+    parts: dict
+    overwritable: bool = True
+
+    @classmethod
+    def insert(cls, space: "GraphSpace", edge_type: int, edges) -> "AddEdgesRequest":
+        """INSERT EDGE as graphd sends it (InsertEdgeExecutor.cpp:143-162): per (src, dst, rank,
+        props) an out-edge under src's part and an in-edge (-type, empty props) under dst's."""
+        parts: dict = {}
+        for src, dst, rank, props in edges:
+            parts.setdefault(space.part_of(src), []).append(Edge(EdgeKey(src, edge_type, rank, dst), props))
+            parts.setdefault(space.part_of(dst), []).append(Edge(EdgeKey(dst, -edge_type, rank, src), b""))
+        return cls(parts)
+
+
+@dataclass
+class Tag:
+    tag_id: int
+    props: bytes
+
+
+@dataclass
+class Vertex:
+    id: int
+    tags: list
+
+
+@dataclass
+class AddVerticesRequest:
+    """storage::cpp2::AddVerticesRequest (storage.thrift:150-156): part -> vertices."""
+    parts: dict
+    overwritable: bool = True
+
+
+@dataclass
+class ExecResponse:
+    failed_codes: list
+
+
+def _now_version() -> int:
+    return INT64_MAX - time.time_ns() // 1000   # INT64_MAX - WallClock::fastNowInMicroSec()
+
+
+class _WriteProcessor:
+    def __init__(self, space: "GraphSpace", commit: bool = True, version: int | None = None):
+        self.space, self.commit, self.version = space, commit, version
+
+    @classmethod
+    def instance(cls, space: "GraphSpace", commit: bool = True, version: int | None = None):
+        return cls(space, commit, version)
+
+    def _put(self, per_part) -> ExecResponse:
+        failed = []
+        for part, pairs in per_part.items():
+            try:
+                self.space.write_part(part, pairs)
+            except NbgError as e:   # doPut's per-part result (BaseProcessor.h:47-73)
+                failed.append({"part_id": part, "code": e.code})
+        if self.commit:
+            self.space.commit()
+        return ExecResponse(failed)
+
+
+class AddEdgesProcessor(_WriteProcessor):
+    """AddEdgesProcessor::process (AddEdgesProcessor.cpp:15-31): one version INT64_MAX - now_us
+    per request, key edgeKey(part, src, type, rank, dst, version), value = the edge's props.
+    The puts become visible to queries at the space's next commit (commit=True: at once)."""
+
+    def process(self, req: AddEdgesRequest) -> ExecResponse:
+        ver = self.version if self.version is not None else _now_version()
+        return self._put({part: [(_EDGE_KEY.pack(part, e.key.src, e.key.edge_type, e.key.ranking, e.key.dst, ver),
+                                  e.props) for e in edges]
+                          for part, edges in req.parts.items() if edges})
+
+
+class AddVerticesProcessor(_WriteProcessor):
+    """AddVerticesProcessor::process (AddVerticesProcessor.cpp:16-38): key vertexKey(part, vid,
+    tag, INT64_MAX - now_us) per (vertex, tag), value = the tag's props."""
+
+    def process(self, req: AddVerticesRequest) -> ExecResponse:
+        ver = self.version if self.version is not None else _now_version()
+        return self._put({part: [(_VERTEX_KEY.pack(part, v.id, t.tag_id, ver), t.props) for v in vs for t in v.tags]
+                          for part, vs in req.parts.items() if vs})
 
 
 class GoExecutor:

@@ -72,3 +72,16 @@ def test_invalid_context_arguments(lib):
     assert not lib.nbg_ctx_create(0, 0, 0, 1)      # no parts
     assert not lib.nbg_ctx_create(0, 64, 2, 2)     # rank out of range
     assert lib.nbg_go(None, None, None) == -1001   # NBG_E_INVALID_ARG on a null context
+
+
+def test_write_processor_keys_match_oracle(oracle):
+    """AddEdgesProcessor / AddVerticesProcessor mirrors pack NebulaKeyUtils keys byte-for-byte as
+    the oracle's restatement does (NebulaKeyUtils.h:14-21); no device call."""
+    import oracle as O
+    from nebula_amd import engine
+    for part, src, et, rank, dst, ver in [(1, 5, 3, 0, 7, 2**63 - 2), (64, -9, -3, 2, 2**62, 0),
+                                          (7, -2**63, 1, -1, 2**63 - 1, 12345)]:
+        assert engine._EDGE_KEY.pack(part, src, et, rank, dst, ver) == O.edge_key(part, src, et, rank, dst, ver)
+    assert engine._VERTEX_KEY.pack(3, -4, 5, 6) == O.vertex_key(3, -4, 5, 6)
+    v = engine._now_version()
+    assert 0 < engine.INT64_MAX - v < 10**17  # INT64_MAX - now_us

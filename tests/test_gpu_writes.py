@@ -228,3 +228,50 @@ def test_write_versions_known_answer():
         assert [tuple(r) for r in sp.get_bound(7, [part], [src], cols).rows()] == [(21, 3), (22, 4), (23, 5)]
     finally:
         sp.close()
+
+
+def test_add_processors_match_oracle():
+    """Host mirrors of the write operators: InsertEdgeExecutor's out/in edge pair
+    (AddEdgesRequest.insert, InsertEdgeExecutor.cpp:143-162) through AddEdgesProcessor, tag rows
+    through AddVerticesProcessor, one version per request; a part this space does not have comes
+    back in failed_codes and the other parts are still written."""
+    from nebula_amd import (AddEdgesProcessor, AddEdgesRequest, AddVerticesProcessor, AddVerticesRequest, Edge,
+                            EdgeKey, Tag, Vertex)
+    base, vids = random_space_kv(6)
+    rng = random.Random(9)
+    new_vids = [rng.randrange(-2**62, 2**62) for _ in range(20)]
+    ver_e, ver_v = BASE_VER - 100, BASE_VER - 101
+    edges = [(rng.choice(vids + new_vids), rng.choice(vids + new_vids), rng.randrange(3),
+              O.encode_row([rng.randrange(2000)])) for _ in range(300)]
+    verts = {}
+    for v in new_vids + vids[:30]:
+        verts.setdefault(O.part_of(v, PARTS), []).append(
+            Vertex(v, [Tag(PERSON, O.encode_row([f"n{abs(v) % 7}", rng.randrange(100), 0.25]))]))
+    # the oracle's view: the same puts, in the same order
+    batch = {p: [] for p in range(1, PARTS + 1)}
+    for s, t, rank, props in edges:
+        batch[O.part_of(s, PARTS)].append((O.edge_key(O.part_of(s, PARTS), s, ET, rank, t, ver_e), props))
+        batch[O.part_of(t, PARTS)].append((O.edge_key(O.part_of(t, PARTS), t, -ET, rank, s, ver_e), b""))
+    for p, vs in verts.items():
+        for v in vs:
+            batch[p].append((O.vertex_key(p, v.id, PERSON, ver_v), v.tags[0].props))
+    st = fresh_oracle([base, batch])
+    sp = GraphSpace(PARTS)
+    try:
+        sp.set_option("writable", 1)
+        sp.set_edge_schema(ET, [("weight", O.INT)])
+        sp.set_tag_schema(PERSON, "person", FIELDS)
+        for p, kv in base.items():
+            if kv:
+                sp.load_part(p, kv)
+        sp.finalize()
+        req = AddEdgesRequest.insert(sp, ET, edges)
+        req.parts[PARTS + 3] = [Edge(EdgeKey(1, ET, 0, 2), O.encode_row([1]))]
+        resp = AddEdgesProcessor.instance(sp, commit=False, version=ver_e).process(req)
+        assert resp.failed_codes == [{"part_id": PARTS + 3, "code": -14}]  # E_PART_NOT_FOUND
+        resp = AddVerticesProcessor.instance(sp, version=ver_v).process(AddVerticesRequest(verts))
+        assert resp.failed_codes == []
+        check_go(sp, st, vids[::19] + new_vids[:5])
+        check_bound(sp, st, vids + new_vids)
+    finally:
+        sp.close()
