@@ -105,7 +105,8 @@ static void stage_reserve(Ctx& c, Staging& s, size_t nfields, size_t extra, bool
   materialize_stage(c, s, nfields, with_props);
   size_t need = size_t(s.n) + extra;
   if (need <= s.cap) return;
-  size_t cap = std::max(need, s.cap * 2);
+  // 1.25x growth: a write batch appended behind a device-sized stage must not double it
+  size_t cap = std::max(need, s.cap + s.cap / 4);
   grow_copy(c, s.src, cap * 8);
   grow_copy(c, s.dst, cap * 8);
   grow_copy(c, s.rank, cap * 8);
@@ -445,33 +446,36 @@ void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
 // transposes and tag columns from the log on the device -- nothing is re-uploaded -- and until
 // then queries keep reading the previous commit (a RocksDB snapshot's view).
 // ------------------------------------------------------------------------------------------
-static void clone_buf(Ctx& c, const DevBuf& from, DevBuf& to) {
+// copies hold the first `n` elements only (a stage's capacity is not carried into the log)
+static void clone_buf(Ctx& c, const DevBuf& from, DevBuf& to, size_t n = SIZE_MAX, size_t w = 1) {
   to.release();
   if (!from.p || !from.bytes) return;
-  to.alloc(from.bytes);
-  NBG_HIP(hipMemcpyAsync(to.p, from.p, from.bytes, hipMemcpyDeviceToDevice, c.stream));
+  const size_t b = n == SIZE_MAX ? from.bytes : std::min(from.bytes, std::max<size_t>(n, 1) * w);
+  to.alloc(b);
+  NBG_HIP(hipMemcpyAsync(to.p, from.p, b, hipMemcpyDeviceToDevice, c.stream));
 }
-static void clone_bufs(Ctx& c, const std::vector<DevBuf>& from, std::vector<DevBuf>& to) {
+static void clone_bufs(Ctx& c, const std::vector<DevBuf>& from, std::vector<DevBuf>& to, size_t n, size_t w) {
   to.clear();
   to.resize(from.size());
-  for (size_t i = 0; i < from.size(); i++) clone_buf(c, from[i], to[i]);
+  for (size_t i = 0; i < from.size(); i++) clone_buf(c, from[i], to[i], n, w);
 }
 static void clone_staging(Ctx& c, const Staging& from, Staging& to) {
+  const size_t n = size_t(from.n);
   to.n = from.n;
-  clone_buf(c, from.src, to.src);
-  clone_buf(c, from.dst, to.dst);
-  clone_buf(c, from.rank, to.rank);
-  clone_buf(c, from.ver, to.ver);
-  clone_buf(c, from.part, to.part);
-  clone_buf(c, from.seq, to.seq);
+  clone_buf(c, from.src, to.src, n, 8);
+  clone_buf(c, from.dst, to.dst, n, 8);
+  clone_buf(c, from.rank, to.rank, n, 8);
+  clone_buf(c, from.ver, to.ver, n, 8);
+  clone_buf(c, from.part, to.part, n, 4);
+  clone_buf(c, from.seq, to.seq, n, 8);
   to.rank_const = from.rank_const;
   to.ver_const = from.ver_const;
   to.rank_value = from.rank_value;
   to.ver_value = from.ver_value;
-  clone_bufs(c, from.props, to.props);
-  clone_bufs(c, from.present, to.present);
-  clone_bufs(c, from.str_len, to.str_len);
-  to.cap = from.cap;
+  clone_bufs(c, from.props, to.props, n, 8);
+  clone_bufs(c, from.present, to.present, n, 1);
+  clone_bufs(c, from.str_len, to.str_len, n, 8);
+  to.cap = n;
 }
 // staging <- log (the tuples of the last commit), value heap included
 static void restore_log(Ctx& c) {
@@ -490,7 +494,7 @@ static void save_log(Ctx& c) {
     clone_staging(c, kv.second.in_stage, kv.second.in_log);
   }
   for (auto& kv : c.tags) clone_staging(c, kv.second.stage, kv.second.log);
-  clone_buf(c, c.heap, c.heap_log);
+  clone_buf(c, c.heap, c.heap_log, c.heap_used + 8, 1);
   c.heap_log_used = c.heap_used;
   NBG_HIP(hipStreamSynchronize(c.stream));
   c.has_log = true;
