@@ -197,7 +197,6 @@ struct EdgeSpace {
   int32_t schema_ver = 0;
   std::vector<Field> fields;
   Staging out_stage, in_stage;
-  Staging out_log, in_log;  // writable snapshots: the decoded tuples the CSRs were built from
   Csr out, in;
   // world > 1: replicas of every rank's out / in CSR over the whole gidx space (built on the
   // first FIND SHORTEST PATH, which shards its pairs over the ranks)
@@ -227,7 +226,6 @@ struct TagSpace {
   std::string name;
   std::vector<Field> fields;
   Staging stage;              // src = vid, ver, part, rank = load sequence number (write order)
-  Staging log;                // writable snapshots: copy of `stage` taken at finalize
   std::vector<PropCol> cols;  // per field, [n_global]; data int64 bits, present uint8:
                               // 0 none, 1 row of the vid's own part, 2 row of a foreign part only
   DevBuf part;                // int32 [n_global]: the part the vertex's row came from
@@ -290,11 +288,10 @@ struct Ctx {
   std::vector<TagFieldRef> tag_refs;  // flat (tag, prop) table, tag-id order then field order
   DevBuf tag_table;                   // device descriptors of tag_refs' columns (first query)
   double build_seconds = 0;
-  // write path: with option writable=1 finalize keeps a device copy of every
-  // decoded tuple and the value heap; nbg_snapshot_write_part decodes later write batches behind
-  // it and nbg_snapshot_commit rebuilds the CSRs from the log.  Queries read the last commit.
-  DevBuf heap_log;
-  size_t heap_log_used = 0;
+  // write path: with option writable=1 finalize builds the CSRs without consuming
+  // the decoded tuples and the value heap (the stages are the write log);
+  // nbg_snapshot_write_part decodes later write batches behind them and nbg_snapshot_commit
+  // rebuilds the CSRs from the stages.  Queries read the last commit.
   bool has_log = false;
   bool pending_writes = false;
   int64_t commits = 0;

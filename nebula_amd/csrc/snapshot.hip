@@ -439,66 +439,14 @@ void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
 // batch of KV puts per part (AddEdgesProcessor.cpp:15-31, AddVerticesProcessor.cpp:16-38; the
 // version in the key is INT64_MAX - now_us, so a newer write of the same edge sorts first and
 // an identical key overwrites).  A writable snapshot keeps the decoded tuples of everything
-// loaded so far (the "log") next to the CSRs; a write batch is decoded by the same k_decode_kv /
+// loaded so far (the stages, read-only to the CSR build: the "log") next to the CSRs; a write
+// batch is decoded by the same k_decode_kv /
 // k_decode_vkv behind the log with later load sequence numbers, so the CSR build's version
 // dedup (bytewise-first key, last write of an identical key) gives exactly what the prefix scan
 // of the written RocksDB part returns.  nbg_snapshot_commit rebuilds the vertex map, CSRs,
 // transposes and tag columns from the log on the device -- nothing is re-uploaded -- and until
 // then queries keep reading the previous commit (a RocksDB snapshot's view).
 // ------------------------------------------------------------------------------------------
-// copies hold the first `n` elements only (a stage's capacity is not carried into the log)
-static void clone_buf(Ctx& c, const DevBuf& from, DevBuf& to, size_t n = SIZE_MAX, size_t w = 1) {
-  to.release();
-  if (!from.p || !from.bytes) return;
-  const size_t b = n == SIZE_MAX ? from.bytes : std::min(from.bytes, std::max<size_t>(n, 1) * w);
-  to.alloc(b);
-  NBG_HIP(hipMemcpyAsync(to.p, from.p, b, hipMemcpyDeviceToDevice, c.stream));
-}
-static void clone_bufs(Ctx& c, const std::vector<DevBuf>& from, std::vector<DevBuf>& to, size_t n, size_t w) {
-  to.clear();
-  to.resize(from.size());
-  for (size_t i = 0; i < from.size(); i++) clone_buf(c, from[i], to[i], n, w);
-}
-static void clone_staging(Ctx& c, const Staging& from, Staging& to) {
-  const size_t n = size_t(from.n);
-  to.n = from.n;
-  clone_buf(c, from.src, to.src, n, 8);
-  clone_buf(c, from.dst, to.dst, n, 8);
-  clone_buf(c, from.rank, to.rank, n, 8);
-  clone_buf(c, from.ver, to.ver, n, 8);
-  clone_buf(c, from.part, to.part, n, 4);
-  clone_buf(c, from.seq, to.seq, n, 8);
-  to.rank_const = from.rank_const;
-  to.ver_const = from.ver_const;
-  to.rank_value = from.rank_value;
-  to.ver_value = from.ver_value;
-  clone_bufs(c, from.props, to.props, n, 8);
-  clone_bufs(c, from.present, to.present, n, 1);
-  clone_bufs(c, from.str_len, to.str_len, n, 8);
-  to.cap = n;
-}
-// staging <- log (the tuples of the last commit), value heap included
-static void restore_log(Ctx& c) {
-  for (auto& kv : c.edges) {
-    clone_staging(c, kv.second.out_log, kv.second.out_stage);
-    clone_staging(c, kv.second.in_log, kv.second.in_stage);
-  }
-  for (auto& kv : c.tags) clone_staging(c, kv.second.log, kv.second.stage);
-  clone_buf(c, c.heap_log, c.heap);
-  c.heap_used = c.heap_log_used;
-  NBG_HIP(hipStreamSynchronize(c.stream));
-}
-static void save_log(Ctx& c) {
-  for (auto& kv : c.edges) {
-    clone_staging(c, kv.second.out_stage, kv.second.out_log);
-    clone_staging(c, kv.second.in_stage, kv.second.in_log);
-  }
-  for (auto& kv : c.tags) clone_staging(c, kv.second.stage, kv.second.log);
-  clone_buf(c, c.heap, c.heap_log, c.heap_used + 8, 1);
-  c.heap_log_used = c.heap_used;
-  NBG_HIP(hipStreamSynchronize(c.stream));
-  c.has_log = true;
-}
 // drop everything snapshot_finalize derives from the staged tuples
 static void reset_derived(Ctx& c) {
   c.vid_of.release();
@@ -542,11 +490,8 @@ void snapshot_write_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t
     return;
   }
   if (!c.has_log) throw Error(NBG_E_STATE, "snapshot is not writable (set option writable=1 before finalize)");
-  if (!c.pending_writes) {
-    restore_log(c);
-    c.pending_writes = true;
-  }
-  decode_part(c, part, kb, koff, vb, voff, n);
+  decode_part(c, part, kb, koff, vb, voff, n);  // behind the kept tuples; the CSRs are untouched
+  c.pending_writes = true;
 }
 
 void snapshot_commit(Ctx& c) {
@@ -556,7 +501,6 @@ void snapshot_commit(Ctx& c) {
   }
   if (!c.has_log) throw Error(NBG_E_STATE, "snapshot is not writable (set option writable=1 before finalize)");
   // collective when world > 1: every rank rebuilds, with or without writes of its own
-  if (!c.pending_writes) restore_log(c);
   NBG_HIP(hipStreamSynchronize(c.stream));
   reset_derived(c);
   c.pending_writes = false;
@@ -920,7 +864,7 @@ static void minmax_i64(Ctx& c, const int64_t* d, int64_t n, int64_t& mn, int64_t
 
 // Builds one CSR from a staging area.  Returns after freeing the staging buffers.
 static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool with_props, Csr& out,
-                      const uint32_t* byterank) {
+                      const uint32_t* byterank, bool consume = true) {
   int64_t n = s.n;
   int64_t lo = c.owned_lo(), hi = c.owned_hi();
   out.n_rows = hi - lo;
@@ -1124,15 +1068,17 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
   NBG_HIP(hipStreamSynchronize(c.stream));
   NBG_HIP(hipGetLastError());
   // free staging
-  s.src.release();
-  s.dst.release();
-  s.rank.release();
-  s.ver.release();
-  s.part.release();
-  s.props.clear();
-  s.present.clear();
-  s.str_len.clear();
-  s.n = 0;
+  if (consume) {  // a writable snapshot keeps its decoded tuples (the write log) for the next commit
+    s.src.release();
+    s.dst.release();
+    s.rank.release();
+    s.ver.release();
+    s.part.release();
+    s.props.clear();
+    s.present.clear();
+    s.str_len.clear();
+    s.n = 0;
+  }
   s.cap = 0;
 }
 
@@ -1659,14 +1605,14 @@ static void build_tag_columns(Ctx& c) {
     }
     if (c.world > 1) replicate_owned(c, ts.part, 4);
     NBG_HIP(hipStreamSynchronize(c.stream));
-    ts.stage = Staging{};
+    if (!c.opt("writable", 0)) ts.stage = Staging{};
   }
 }
 
 void snapshot_finalize(Ctx& c) {
   if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
   double t0 = now_s();
-  if (c.opt("writable", 0)) save_log(c);
+  const bool keep = c.opt("writable", 0) != 0;
   // 1. referenced vids (src/dst of every staged tuple), sign-flipped for unsigned sort
   int64_t total = 0;
   for (auto& kv : c.edges) total += 2 * (kv.second.out_stage.n + kv.second.in_stage.n);
@@ -1825,12 +1771,15 @@ void snapshot_finalize(Ctx& c) {
   // 6. CSRs
   for (auto& kv : c.edges) {
     EdgeSpace& es = kv.second;
-    build_csr(c, es.out_stage, es.fields, true, es.out, brank.as<uint32_t>());
-    build_csr(c, es.in_stage, es.fields, false, es.in, brank.as<uint32_t>());
+    build_csr(c, es.out_stage, es.fields, true, es.out, brank.as<uint32_t>(), !keep);
+    build_csr(c, es.in_stage, es.fields, false, es.in, brank.as<uint32_t>(), !keep);
     if (c.opt("bottom_up", 1)) build_transpose(c, es);
   }
-  c.heap.release();
-  c.heap_used = 0;
+  if (!keep) {
+    c.heap.release();
+    c.heap_used = 0;
+  }
+  c.has_log = keep;
   c.ws_tmp.release();
   NBG_HIP(hipStreamSynchronize(c.stream));
   c.finalized = true;
