@@ -9,10 +9,17 @@ entries scanned over all hops / wall time; the frontier never leaves
 
     python bench.py                       # N=1
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+    python bench.py --plain --scale 22    # configs[1] (C2)
+    python bench.py --plain --scale 28 --hops 2 --hubs 8   # configs[4] (C5)
+    python bench.py --workload paths      # configs[3] (C4)
+
+After the timed region the same query runs once more with its result copied to the host and is
+checked against tests/golden/rmat_digests.json (the oracle's digest of that config) -> "parity".
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -25,6 +32,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+GOLDEN = ROOT / "tests" / "golden" / "rmat_digests.json"
 
 
 def hop_kernels(h):
@@ -39,7 +47,7 @@ def pmc_traffic(workload: str, prefixes):
     the same workload (profiles/<tag>_summary.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
     separate --pmc passes, tools/gpu_profile.sh + tools/profile_summary.py).  None if absent."""
     best = None
-    # newest round tag last (r01b < r01c < ...); file mtimes are meaningless in a fresh checkout
+    # newest round tag last (r01b < r01c < ... < r02a); file mtimes are meaningless in a checkout
     for f in sorted((ROOT / "profiles").glob("*_summary.json"), key=lambda p: p.name):
         try:
             d = json.loads(f.read_text())
@@ -48,52 +56,106 @@ def pmc_traffic(workload: str, prefixes):
         b = d.get("bench") or {}
         if (b.get("config") or {}).get("workload") != workload:
             continue
-        tot, hit = 0.0, 0
+        tot, raw, hit = 0.0, 0.0, 0
         for pre in prefixes:
             ks = [k for k in d.get("query_kernels", []) if k["kernel"].startswith(pre)
                   and k.get("fetch_bytes_x2") is not None]
             if ks:
                 k = max(ks, key=lambda k: k["total_ms"])
                 tot += k["fetch_bytes_x2"] + (k.get("write_bytes") or 0.0)
+                raw += k["fetch_bytes_x2"] / 2 + (k.get("write_bytes") or 0.0)
                 hit += 1
         if hit == len(prefixes):
-            best = {"bytes": tot, "source": f"profiles/{f.name}"}
+            best = {"bytes": tot, "raw_bytes": raw, "source": f"profiles/{f.name}"}
     return best
 
 
-def cpu_baseline(scale: int, seeds: int, where_k: int):
-    """The oracle (CPU restatement of storaged+graphd, faithful mode: 10 bucket handlers,
-    single-threaded graphd loop) on a bounded sample of the same query."""
+# ---- CPU baseline -----------------------------------------------------------------------------
+def host_cpu():
+    """(usable cores of this process, cores of the machine, CPU model)"""
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count() or 1
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, os.cpu_count() or usable, model
+
+
+def best_of(fn, reps=3):
+    fn()  # warm-up
+    best, out = None, None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        out = fn()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return best, out
+
+
+def cpu_baseline(scale: int, where_k: int, golden: dict):
+    """The oracle (oracle/refcpu.cpp: the CPU restatement of storaged + graphd over the
+    reference's KV layout) timed on this host on a bounded sample, best of 3 after 1 warm-up:
+      * faithful: 1 storaged host x max_handlers_per_req = 10 bucket threads, min 3 vertices per
+        bucket (QueryBaseProcessor.cpp:9-10), graphd loop single-threaded (GraphFlags.cpp:19);
+      * all-cores: the same with one bucket thread per usable core.
+    Sample: the bench query's shape (GO 3 STEPS ... WHERE weight > k YIELD DISTINCT _dst, 64
+    seeds) and configs[0] (C1: GO 2 STEPS FROM 16 seeds) on RMAT-`scale`."""
     sys.path.insert(0, str(ROOT / "tests"))
-    import numpy as np  # noqa: F401
     import oracle as O
     from nebula_amd import expr as X
     from nebula_amd import synth
 
+    usable, machine, model = host_cpu()
     st = O.Store(64)
     st.set_edge_schema(1, [("weight", O.INT)], name="follow")
-    t0 = time.time()
-    st.load_rmat(scale, 16, 1, 1, versions=1, threads=min(8, os.cpu_count() or 1))
-    load_s = time.time() - t0
-    starts = synth.seeds(scale, 16, 1, seeds)
+    t0 = time.perf_counter()
+    st.load_rmat(scale, 16, 1, 1, versions=1, threads=min(16, usable))
+    load_s = time.perf_counter() - t0
     w = (X.AliasProp("follow", "weight") > where_k).encode()
     y = [X.EdgeDst("follow").encode()]
-    best = None
-    scanned = 0
-    for _ in range(2):
-        t0 = time.time()
-        r = st.go(starts, 3, 1, where=w, yields=y, distinct=True, hosts=1, handlers=10, min_per_bucket=3)
-        dt = time.time() - t0
-        scanned = r.edges_scanned
-        best = dt if best is None else min(best, dt)
+    cases = {
+        "c3_shape": dict(starts=synth.seeds(scale, 16, 1, 64), steps=3, where=w, yields=y, distinct=True,
+                         golden=f"go3_where{where_k}_distinct_s{scale}"),
+        "c1": dict(starts=synth.seeds(scale, 16, 1, 16), steps=2, where=b"", yields=(), distinct=False,
+                   golden=f"go2_plain_s{scale}"),
+    }
+    res = {}
+    for name, cs in cases.items():
+        row = {}
+        for mode, handlers in (("faithful", 10), ("all_cores", usable)):
+            dt, r = best_of(lambda: st.go(cs["starts"], cs["steps"], 1, where=cs["where"], yields=cs["yields"],
+                                          distinct=cs["distinct"], hosts=1, handlers=handlers, min_per_bucket=3))
+            row[mode] = {"gteps": r.edges_scanned / dt / 1e9, "seconds": dt, "threads": min(handlers, usable) + 1}
+            row["edges_scanned"] = r.edges_scanned
+            row["rows"] = r.nrows
+            g = golden.get(cs["golden"])
+            row["parity"] = ("no golden" if g is None else
+                             "digest ok" if O.digest(r.int_col(0)) == g["sha256"] and r.nrows == g["n_rows"]
+                             else "mismatch")
+        res[name] = row
+    c3 = res["c3_shape"]
     return {
-        "value": scanned / best / 1e9,
+        "value": c3["faithful"]["gteps"],
         "unit": "GTEPS",
-        "cores": min(10, os.cpu_count() or 1),
+        "cores": c3["faithful"]["threads"],
         "kind": "port",
-        "sample": f"oracle GO 3 STEPS WHERE weight>{where_k} YIELD DISTINCT _dst from {seeds} seeds on "
-                  f"RMAT-{scale} (ef16), 1 storaged host x 10 handlers, graphd 1 thread; "
-                  f"{scanned} edges scanned in {best:.2f}s (best of 2); KV load {load_s:.1f}s",
+        "sample": f"oracle (KV-store restatement of storaged+graphd) GO 3 STEPS WHERE weight>{where_k} YIELD "
+                  f"DISTINCT _dst from 64 seeds on RMAT-{scale} (ef16), faithful mode (1 storaged host x 10 bucket "
+                  f"threads + 1 graphd thread), best of 3 after 1 warm-up; KV load {load_s:.1f}s",
+        "host_cores": usable,
+        "machine_cores": machine,
+        "cpu_model": model,
+        "faithful": {"c3_shape": c3["faithful"], "c1": res["c1"]["faithful"]},
+        "all_cores": {"c3_shape": c3["all_cores"], "c1": res["c1"]["all_cores"]},
+        "config": {"scale": scale, "c3_shape": {k: c3[k] for k in ("edges_scanned", "rows", "parity")},
+                   "c1": {k: res["c1"][k] for k in ("edges_scanned", "rows", "parity")}},
     }
 
 
@@ -103,19 +165,57 @@ def cpu_baseline_paths(scale: int, npairs: int, max_steps: int):
     import oracle as O
     from nebula_amd import synth
 
+    usable, machine, model = host_cpu()
     st = O.Store(64)
     st.set_edge_schema(1, [("weight", O.INT)], name="follow")
-    st.load_rmat(scale, 16, 1, 1, versions=1, threads=min(8, os.cpu_count() or 1))
+    st.load_rmat(scale, 16, 1, 1, versions=1, threads=min(16, usable))
     s, t = synth.pairs(scale, 16, 1, npairs)
-    t0 = time.time()
-    st.shortest_path(s, t, 1, max_steps)
-    dt = time.time() - t0
-    return {"value": npairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port",
-            "sample": f"oracle FIND SHORTEST PATH {npairs} pairs on RMAT-{scale} (ef16) UPTO {max_steps} STEPS "
-                      f"in {dt:.2f}s"}
+    dt, _ = best_of(lambda: st.shortest_path(s, t, 1, max_steps))
+    return {"value": npairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port", "host_cores": usable,
+            "machine_cores": machine, "cpu_model": model,
+            "sample": f"oracle FIND SHORTEST PATH {npairs} pairs on RMAT-{scale} (ef16) UPTO {max_steps} STEPS, "
+                      f"best of 3 after 1 warm-up: {dt:.2f}s"}
 
 
-def bench_paths(args, sp, info, build_s, rank, world, dist=None):
+# ---- parity of the timed query ----------------------------------------------------------------
+def gather_column(col, dist, world):
+    if dist is None or world == 1:
+        return col
+    parts = [None] * world
+    dist.all_gather_object(parts, col)
+    return np.concatenate(parts)
+
+
+def parity_go(sp, run_host, key, golden, dist, world, rank, plain_rows_check):
+    """re-run the timed query with its result on the host; compare with the committed digest of
+    the config, or (no digest committed) the size-independent property of the workload"""
+    r = run_host()
+    col = gather_column(np.asarray(r.columns[0], dtype=np.int64), dist, world)
+    out = {"golden": key}
+    g = golden.get(key)
+    if g is not None:
+        ok = len(col) == g["n_rows"] and O_digest(col) == g["sha256"]
+        out.update(status="digest ok" if ok else "mismatch", rows=int(len(col)), sha256=O_digest(col)[:16])
+        return out
+    # property check: a plain GO's final-hop rows are one per (frontier vertex, edge), i.e. the
+    # out-degree sum of the final frontier (hop stat c[1] of a top-down hop, c[1] of the previous
+    # bottom-up hop), which the engine reports independently of the rows it wrote
+    out["status"] = "no golden"
+    if plain_rows_check is not None:
+        want = plain_rows_check()
+        out.update(property="rows == out-degree sum of the final frontier",
+                   status="property ok" if want == len(col) else "property mismatch", rows=int(len(col)),
+                   expected=int(want))
+    return out
+
+
+def O_digest(vids) -> str:
+    a = np.sort(np.asarray(vids, dtype=np.int64)).astype("<i8")
+    return hashlib.sha256(a.tobytes()).hexdigest()
+
+
+# ---- FIND SHORTEST PATH -------------------------------------------------------------------------
+def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
     """BASELINE.json configs[3]: FIND SHORTEST PATH, 1024 (src, dst) pairs on RMAT-26.  With
     world > 1 the pairs are sharded i % world over the ranks (each answers its own against the
     replicated CSRs, no collective in the timed region): strong scaling of a fixed pair set."""
@@ -140,7 +240,8 @@ def bench_paths(args, sp, info, build_s, rank, world, dist=None):
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-    hops = r.hops
+    # parity: the last timed result (host copy) against the committed digest
+    hops, paths, srcs = r.hops, r.paths, r.src
     if dist is not None:
         import torch
         tt = torch.tensor([dt], dtype=torch.float64)
@@ -150,8 +251,21 @@ def bench_paths(args, sp, info, build_s, rank, world, dist=None):
         dist.all_reduce(te, op=dist.ReduceOp.SUM)
         edges = int(te.item())
         hl = [None] * world
-        dist.all_gather_object(hl, hops.tolist())
-        hops = np.array([h for part in hl for h in part], dtype=np.int64)
+        dist.all_gather_object(hl, (hops.tolist(), [p.tolist() for p in paths]))
+        # rank q answered pairs q, q + world, ...: back to input order
+        hops = np.full(args.pairs, -2, dtype=np.int64)
+        paths = [None] * args.pairs
+        for q, (hq, pq) in enumerate(hl):
+            for j, (h, p) in enumerate(zip(hq, pq)):
+                hops[q + j * world] = h
+                paths[q + j * world] = np.asarray(p, dtype=np.int64)
+    key = f"paths{args.pairs}_s{args.scale}"
+    parity = {"golden": key, "status": "no golden"}
+    if key in golden:
+        h = hashlib.sha256(np.asarray(hops, dtype="<i8").tobytes())
+        for p in paths:
+            h.update(np.asarray(p, dtype="<i8").tobytes())
+        parity["status"] = "digest ok" if h.hexdigest() == golden[key]["sha256"] else "mismatch"
     achieved = exp_bytes / (exp_ms / 1e3) / 1e9 if exp_ms > 0 else 0.0
     out = {
         "metric": "FIND SHORTEST PATH pairs/s (batched bidirectional BFS) on RMAT-26",
@@ -173,11 +287,12 @@ def bench_paths(args, sp, info, build_s, rank, world, dist=None):
             "vertices": info["num_vertices"],
             "edges_examined_per_query": edges // max(args.steps, 1),
             "gteps": edges / dt / 1e9,
-            "reachable": int((hops >= 0).sum()),
-            "hops_histogram": {int(h): int((hops == h).sum()) for h in sorted(set(hops.tolist()))},
+            "reachable": int((np.asarray(hops) >= 0).sum()),
+            "hops_histogram": {int(h): int((np.asarray(hops) == h).sum()) for h in sorted(set(np.asarray(hops).tolist()))},
             "bfs_iterations": iters,
             "snapshot_build_s": round(build_s, 2),
         },
+        "parity": parity,
         "roofline": {
             "bound": "hbm", "kernel": "k_sp_expand", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": None,
@@ -203,10 +318,13 @@ def main():
     ap.add_argument("--scale", type=int, default=26)
     ap.add_argument("--edge-factor", type=int, default=16)
     ap.add_argument("--seeds", type=int, default=64)
+    ap.add_argument("--hubs", type=int, default=0,
+                    help="replace the first N seeds with the N highest-out-degree vertices (configs[4]: 8)")
     ap.add_argument("--where", type=int, default=499)
     ap.add_argument("--hops", type=int, default=3)
-    ap.add_argument("--cpu-scale", type=int, default=20)
+    ap.add_argument("--cpu-scale", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--option", action="append", default=[], help="engine option key=value")
     ap.add_argument("--workload", choices=["go", "paths"], default="go",
                     help="go: BASELINE metric (GO 3 STEPS); paths: configs[3] FIND SHORTEST PATH")
@@ -229,6 +347,7 @@ def main():
     from nebula_amd import expr as X
     from nebula_amd import synth
 
+    golden = json.loads(GOLDEN.read_text()) if GOLDEN.exists() else {}
     sp = GraphSpace(64, device=local, rank=rank, world_size=world)
     if world > 1:
         uid = [GraphSpace.comm_unique_id() if rank == 0 else None]
@@ -245,15 +364,29 @@ def main():
     build_s = time.time() - t0
     info = sp.info(FOLLOW)
     if args.workload == "paths":
-        return bench_paths(args, sp, info, build_s, rank, world, dist)
+        return bench_paths(args, sp, info, build_s, rank, world, golden, dist)
     starts = synth.seeds(args.scale, args.edge_factor, 1, args.seeds)
+    hubs = []
+    if args.hubs:
+        # the top-N out-degree vertices (global: every rank sees the same vid -> degree via its
+        # own rows; the owner's answer is the true degree, others report -1 / 0)
+        cand = synth.hub_candidates(args.scale, 1)
+        deg = np.array([sp.out_degree(FOLLOW, int(v)) for v in cand], dtype=np.int64)
+        if dist is not None:
+            import torch
+            td = torch.tensor(deg)
+            dist.all_reduce(td, op=dist.ReduceOp.MAX)
+            deg = td.numpy()
+        order = np.argsort(-deg, kind="stable")[:args.hubs]
+        hubs = [(int(cand[i]), int(deg[i])) for i in order]
+        starts = np.concatenate([np.array([h for h, _ in hubs], dtype=np.int64), starts[args.hubs:]])
     # --plain: no WHERE, default YIELD follow._dst rows without DISTINCT (configs[1] / configs[4])
     where = None if args.plain else X.AliasProp("follow", "weight") > args.where
     yields = [X.EdgeDst("follow")]
 
-    def one():
+    def one(keep=True):
         return sp.go(starts, args.hops, FOLLOW, where=where, yields=yields, distinct=not args.plain,
-                     keep_on_device=True)
+                     keep_on_device=keep)
 
     for _ in range(args.warmup):
         one()
@@ -268,9 +401,10 @@ def main():
     rows = 0
     exp_ms = 0.0
     exp_bytes = 0
-    tot_ms = 0.0
+    tot_ms = comm_ms = 0.0
+    comm_bytes = 0
     bu_steps = 0
-    hop_ms, hop_bytes = {}, {}
+    hop_ms, hop_bytes, k_ms, k_bytes = {}, {}, {}, {}
     for _ in range(args.steps):
         r = one()
         t = sp.last_timing()
@@ -279,11 +413,15 @@ def main():
         exp_ms += t["expand_ms"]
         exp_bytes += t["expand_bytes"]
         tot_ms += t["total_ms"]
+        comm_ms += t["comm_ms"]
+        comm_bytes += t["comm_bytes"]
         bu_steps = t["bu_steps"]
         hop_stats = t["hops"]
         for i, h in enumerate(hop_stats):
             hop_ms[i] = hop_ms.get(i, 0.0) + h["ms"]
             hop_bytes[i] = hop_bytes.get(i, 0) + h["bytes"]
+            k_ms[i] = k_ms.get(i, 0.0) + h["kernel_ms"]
+            k_bytes[i] = k_bytes.get(i, 0) + h["kernel_bytes"]
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -296,18 +434,66 @@ def main():
         edges, rows = int(te[0].item()), int(te[1].item())
     gteps = edges / dt / 1e9
     achieved = exp_bytes / (exp_ms / 1e3) / 1e9 if exp_ms > 0 else 0.0
-    # dominant kernel: the hop with the largest summed time (the final bottom-up hop here)
-    dom = max(range(len(hop_stats)), key=lambda i: hop_ms[i]) if hop_stats else None
+    K = max(args.steps, 1)
+    # dominant kernel: the kernel with the largest summed time (the final bottom-up hop's
+    # k_bu_slab for the bench query); its hop (kernel + compaction) is reported beside it
+    dom = max(range(len(hop_stats)), key=lambda i: k_ms[i]) if hop_stats else None
     workload = (f"GO {args.hops} STEPS FROM {args.seeds} seeds OVER follow WHERE follow.weight > "
                 f"{args.where} YIELD DISTINCT follow._dst; RMAT-{args.scale} ef{args.edge_factor}")
     if args.plain:
-        workload = (f"GO {args.hops} STEPS FROM {args.seeds} seeds OVER follow (YIELD follow._dst rows); "
-                    f"RMAT-{args.scale} ef{args.edge_factor}")
+        workload = (f"GO {args.hops} STEPS FROM {args.seeds} seeds{' incl. top-%d degree' % args.hubs if args.hubs else ''} "
+                    f"OVER follow (YIELD follow._dst rows); RMAT-{args.scale} ef{args.edge_factor}")
+    roof = None
     if dom is not None:
         dh = hop_stats[dom]
-        dom_ach = hop_bytes[dom] / (hop_ms[dom] / 1e3) / 1e9 if hop_ms[dom] > 0 else 0.0
         dom_names = hop_kernels(dh)
-        tr = pmc_traffic(workload, dom_names)
+        kach = k_bytes[dom] / (k_ms[dom] / 1e3) / 1e9 if k_ms[dom] > 0 else 0.0
+        hach = hop_bytes[dom] / (hop_ms[dom] / 1e3) / 1e9 if hop_ms[dom] > 0 else 0.0
+        tr = pmc_traffic(workload, dom_names[:1])
+        roof = {
+            "bound": "hbm",
+            "kernel": dom_names[0].rstrip("<,") + f" (hop {dom + 1} of {len(hop_stats)})",
+            "achieved": kach,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": kach / HBM_PEAK_GBS,
+            "traffic": tr["bytes"] if tr else None,
+            "traffic_raw_fetch_plus_write": tr["raw_bytes"] if tr else None,
+            "traffic_source": tr["source"] + " (FETCH_SIZE x2 + WRITE_SIZE per launch)" if tr else None,
+            "algorithmic_bytes_per_launch": k_bytes[dom] // K,
+            "launch_ms": k_ms[dom] / K,
+            "hop": {"kernels": " + ".join(k.rstrip("<,") for k in dom_names), "achieved": hach,
+                    "frac": hach / HBM_PEAK_GBS, "bytes": hop_bytes[dom] // K, "ms": hop_ms[dom] / K},
+            "all_expansion_kernels": {"achieved": achieved, "frac": achieved / HBM_PEAK_GBS},
+            "algorithmic_bytes_per_query": exp_bytes // K,
+            "expand_ms_per_query": exp_ms / K,
+            "device_ms_per_query": tot_ms / K,
+            "bottom_up_hops": bu_steps,
+            "hops": hop_stats,
+        }
+    parity = {"status": "skipped"}
+    if not args.no_parity:
+        key = (f"go{args.hops}_plain_s{args.scale}" if args.plain else
+               f"go{args.hops}_where{args.where}_distinct_s{args.scale}")
+        if args.hubs or args.seeds != 64:
+            key += f"_seeds{args.seeds}_hubs{args.hubs}"
+
+        def plain_check():
+            # rows of a plain GO = one per (final frontier vertex, edge): the final hop's
+            # out-degree sum, which the engine takes from the CSR offsets (hop stat c[1]),
+            # independently of the rows the expansion wrote (summed over ranks)
+            v = int(sp.last_timing()["hops"][-1]["c"][1])
+            if dist is not None:
+                import torch
+                tv = torch.tensor([v], dtype=torch.int64)
+                dist.all_reduce(tv, op=dist.ReduceOp.SUM)
+                v = int(tv.item())
+            return v
+        try:
+            parity = parity_go(sp, lambda: one(False), key, golden, dist, world, rank,
+                               plain_check if args.plain else None)
+        except Exception as e:  # the check must not hide the GPU number
+            parity = {"status": f"error: {e}"}
     if rank == 0:
         out = {
             "metric": "GTEPS for GO 3 STEPS on RMAT-26 at 1/2/4/8 GPUs; % of HBM roofline",
@@ -326,34 +512,22 @@ def main():
                 "workload": workload,
                 "vertices": info["num_vertices"],
                 "edges_after_collapse": info["local_out_edges"] if world == 1 else None,
-                "edges_scanned_per_query": edges // max(args.steps, 1),
+                "edges_scanned_per_query": edges // K,
                 "result_rows": rows,
                 "snapshot_build_s": round(build_s, 2),
                 "parallelism": f"part%{world} sharding, RCCL frontier exchange" if world > 1 else "1 GPU",
+                "hub_seeds": hubs or None,
             },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": " + ".join(k.rstrip("<,") for k in dom_names) + f" (hop {dom + 1} of {len(hop_stats)})",
-                "achieved": dom_ach,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": dom_ach / HBM_PEAK_GBS,
-                "traffic": tr["bytes"] if tr else None,
-                "traffic_source": tr["source"] + " (FETCH_SIZE x2 + WRITE_SIZE per launch)" if tr else None,
-                "algorithmic_bytes_per_launch": hop_bytes[dom] // max(args.steps, 1),
-                "launch_ms": hop_ms[dom] / max(args.steps, 1),
-                "all_expansion_kernels": {"achieved": achieved, "frac": achieved / HBM_PEAK_GBS},
-                "algorithmic_bytes_per_query": exp_bytes // max(args.steps, 1),
-                "expand_ms_per_query": exp_ms / max(args.steps, 1),
-                "device_ms_per_query": tot_ms / max(args.steps, 1),
-                "bottom_up_hops": bu_steps,
-                "hops": hop_stats,
-            },
+            "parity": parity,
+            "roofline": roof,
             "cpu_baseline": None,
         }
+        if world > 1:
+            out["comm"] = {"backend": "rccl (nbg_comm_init over ncclCommInitRank)", "ranks": world,
+                           "comm_ms_per_query_rank0": comm_ms / K, "comm_bytes_per_query_rank0": comm_bytes // K}
         if world == 1 and not args.no_cpu and not args.plain:
             try:
-                out["cpu_baseline"] = cpu_baseline(args.cpu_scale, args.seeds, args.where)
+                out["cpu_baseline"] = cpu_baseline(args.cpu_scale, args.where, golden)
             except Exception as e:  # the baseline must not hide the GPU number
                 out["cpu_baseline"] = {"error": str(e)}
         print(json.dumps(out), flush=True)

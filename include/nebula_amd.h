@@ -265,6 +265,8 @@ typedef struct {
   double ms;         /* HIP-event time of the hop's expansion kernels                      */
   uint64_t bytes;    /* their algorithmic bytes                       */
   uint64_t c[6];
+  double kernel_ms;      /* the hop's dominant kernel alone (k_bu_slab / k_expand)          */
+  uint64_t kernel_bytes; /* that kernel's algorithmic bytes                                  */
 } nbg_hop_stat;
 #define NBG_MAX_HOP_STATS 16
 typedef struct {

@@ -171,9 +171,19 @@ struct Csr {
   DevBuf row_ok;    // uint8 [n_rows] row_part == hash part; empty when all rows follow the rule
   std::vector<PropCol> props;
   DevBuf prop_table;  // device copy of the column descriptors (built on first query)
+  // Older versions (multi-version data only): the tuples that are not the bytewise-first
+  // version of their (src, rank, dst) group, in key order.  collectEdgeProps reads them until
+  // its first emit (the firstLoop rule, QueryBaseProcessor.inl:349-402), so a push-down filter
+  // can return an older version of a row's first passing group.  ov_edge = the group's edge
+  // index (nondecreasing); ov_props: one column per schema field (INT-like as int64 bits).
+  int64_t ov_n = 0;
+  DevBuf ov_edge;
+  std::vector<PropCol> ov_props;
+  DevBuf ov_prop_table;
   size_t bytes() const {
-    size_t b = row_ptr.bytes + col.bytes + rank.bytes + row_part.bytes + row_ok.bytes;
+    size_t b = row_ptr.bytes + col.bytes + rank.bytes + row_part.bytes + row_ok.bytes + ov_edge.bytes;
     for (auto& p : props) b += p.data.bytes + p.present.bytes + p.str_off.bytes + p.str_bytes.bytes;
+    for (auto& p : ov_props) b += p.data.bytes + p.present.bytes + p.str_off.bytes + p.str_bytes.bytes;
     return b;
   }
 };
@@ -247,7 +257,10 @@ struct Timing {
   int32_t n_hops = 0;
   nbg_hop_stat hops[NBG_MAX_HOP_STATS] = {};
   uint64_t hop_bytes_mark = 0;  // expand_bytes at the previous hop record
-  void hop(int32_t mode, bool final_hop, double ms, const unsigned long long* c6) {
+  // kernel_ms < 0: the hop is one kernel (its time and bytes are the hop's; a top-down hop's
+  // time is filled in later by timing_resolve)
+  void hop(int32_t mode, bool final_hop, double ms, const unsigned long long* c6, double kernel_ms = -1,
+           uint64_t kernel_bytes = 0) {
     const uint64_t b = expand_bytes - hop_bytes_mark;
     hop_bytes_mark = expand_bytes;
     if (n_hops >= NBG_MAX_HOP_STATS) return;
@@ -257,6 +270,8 @@ struct Timing {
     h.ms = ms;
     h.bytes = b;
     for (int i = 0; i < 6; i++) h.c[i] = c6 ? c6[i] : 0;
+    h.kernel_ms = kernel_ms < 0 ? ms : kernel_ms;
+    h.kernel_bytes = kernel_ms < 0 ? b : kernel_bytes;
   }
 };
 

@@ -862,6 +862,87 @@ static void minmax_i64(Ctx& c, const int64_t* d, int64_t n, int64_t& mn, int64_t
   mx = h[1];
 }
 
+// older-version flags over the sorted tuples: not kept (a later version of a kept group) and
+// not an overwritten identical key (same version as its predecessor: WriteBatch last write wins
+// puts the visible write first).  escan[i] = keep[i] (inclusive-scanned by the caller -> the
+// group's edge index + 1).
+__global__ void k_old_version_flags(const uint32_t* perm, const uint8_t* keep, const int64_t* ver, int64_t n,
+                                    uint8_t* ov, int64_t* escan) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    escan[i] = keep[i];
+    ov[i] = !keep[i] && i > 0 && ver[perm[i]] != ver[perm[i - 1]];
+  }
+}
+__global__ void k_dec_i64(int64_t* p, int64_t n) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) p[i] -= 1;
+}
+
+// SoA prop columns of the staged tuples kp[0..m) (in that order): INT-like values narrowed to
+// the smallest width holding [min, max] when `narrow`, DOUBLE as bits, STRING as offsets + bytes
+static void gather_props(Ctx& c, Staging& s, const std::vector<Field>& fields, const uint32_t* kp, int64_t m,
+                         bool narrow, std::vector<PropCol>& props_out) {
+  DevBuf tmp;
+  tmp.alloc(size_t(m) * 8 + 8);
+  for (size_t f = 0; f < fields.size(); f++) {
+    PropCol pc;
+    pc.name = fields[f].name;
+    pc.type = fields[f].type;
+    k_gather_i64<<<grid_for(m), 256, 0, c.stream>>>(s.props[f].as<int64_t>(), kp, tmp.as<int64_t>(), m);
+    bool has_present = f < s.present.size() && s.present[f].p != nullptr;
+    if (has_present) {
+      pc.present.alloc(size_t(m) + 1);
+      k_gather_u8<<<grid_for(m), 256, 0, c.stream>>>(s.present[f].as<uint8_t>(), kp, pc.present.as<uint8_t>(), m);
+    }
+    if (pc.type == NBG_T_STRING) {
+      DevBuf lens, offs_src;
+      lens.alloc(size_t(m) * 8 + 8);
+      offs_src.alloc(size_t(m) * 8 + 8);
+      k_gather_i64<<<grid_for(m), 256, 0, c.stream>>>(s.str_len[f].as<int64_t>(), kp, lens.as<int64_t>(), m);
+      NBG_HIP(hipMemcpyAsync(offs_src.p, tmp.p, size_t(m) * 8, hipMemcpyDeviceToDevice, c.stream));
+      DevBuf l2;
+      l2.alloc(size_t(m + 1) * 8);
+      k_str_lengths<<<grid_for(m), 256, 0, c.stream>>>(lens.as<int64_t>(),
+                                                             has_present ? pc.present.as<uint8_t>() : nullptr,
+                                                             m, l2.as<int64_t>());
+      NBG_HIP(hipMemsetAsync(l2.as<int64_t>() + m, 0, 8, c.stream));
+      pc.str_off.alloc(size_t(m + 1) * 8);
+      exclusive_scan<int64_t>(c, l2.as<int64_t>(), pc.str_off.as<int64_t>(), m + 1);
+      int64_t total = 0;
+      NBG_HIP(hipMemcpyAsync(&total, pc.str_off.as<int64_t>() + m, 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      pc.str_bytes.alloc(size_t(total) + 8);
+      k_str_copy<<<grid_for(m), 256, 0, c.stream>>>(c.heap.as<uint8_t>(), offs_src.as<int64_t>(),
+                                                           pc.str_off.as<int64_t>(), m, pc.str_bytes.as<uint8_t>());
+      pc.width = 0;
+    } else if (pc.type == NBG_T_DOUBLE || pc.type == NBG_T_FLOAT) {
+      pc.width = 8;
+      pc.data.alloc(size_t(m) * 8 + 8);
+      NBG_HIP(hipMemcpyAsync(pc.data.p, tmp.p, size_t(m) * 8, hipMemcpyDeviceToDevice, c.stream));
+    } else {
+      // INT / VID / TIMESTAMP / BOOL: narrow to the smallest width holding [min, max]
+      int64_t mn = 0, mx = 0;
+      if (m) minmax_i64(c, tmp.as<int64_t>(), m, mn, mx);
+      pc.minv = mn;
+      pc.maxv = mx;
+      int w = 8;
+      if (mn >= INT8_MIN && mx <= INT8_MAX) w = 1;
+      else if (mn >= INT16_MIN && mx <= INT16_MAX) w = 2;
+      else if (mn >= INT32_MIN && mx <= INT32_MAX) w = 4;
+      if (c.opt("narrow_props", 1) == 0 || !narrow) w = 8;
+      pc.width = w;
+      pc.data.alloc(size_t(m) * size_t(w) + 16);
+      int g = grid_for(m);
+      switch (w) {
+        case 1: k_narrow<int8_t><<<g, 256, 0, c.stream>>>(tmp.as<int64_t>(), pc.data.as<int8_t>(), m); break;
+        case 2: k_narrow<int16_t><<<g, 256, 0, c.stream>>>(tmp.as<int64_t>(), pc.data.as<int16_t>(), m); break;
+        case 4: k_narrow<int32_t><<<g, 256, 0, c.stream>>>(tmp.as<int64_t>(), pc.data.as<int32_t>(), m); break;
+        default: NBG_HIP(hipMemcpyAsync(pc.data.p, tmp.p, size_t(m) * 8, hipMemcpyDeviceToDevice, c.stream));
+      }
+    }
+    props_out.push_back(std::move(pc));
+  }
+}
+
 // Builds one CSR from a staging area.  Returns after freeing the staging buffers.
 static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool with_props, Csr& out,
                       const uint32_t* byterank, bool consume = true) {
@@ -954,6 +1035,51 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
   uint64_t m = 0;
   NBG_HIP(hipMemcpyAsync(&m, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
+  // older versions (multi-version data): tuples that are neither kept nor an overwritten
+  // identical key, with the edge index of their group (the firstLoop side table, Csr::ov_*)
+  out.ov_n = 0;
+  out.ov_edge.release();
+  out.ov_props.clear();
+  DevBuf ovp;
+  if (with_props && !s.ver_const && int64_t(m) < n) {
+    DevBuf ovf, escan, ove, ocnt;
+    ovf.alloc(size_t(n));
+    escan.alloc(size_t(n) * 8);
+    k_old_version_flags<<<grid_for(n), 256, 0, c.stream>>>(perm, keep.as<uint8_t>(), s.ver.as<int64_t>(), n,
+                                                           ovf.as<uint8_t>(), escan.as<int64_t>());
+    size_t tb2 = 0;
+    NBG_HIP(rocprim::inclusive_scan(nullptr, tb2, escan.as<int64_t>(), escan.as<int64_t>(), size_t(n),
+                                    rocprim::plus<int64_t>(), c.stream));
+    c.ws_tmp.ensure(tb2);
+    NBG_HIP(rocprim::inclusive_scan(c.ws_tmp.p, tb2, escan.as<int64_t>(), escan.as<int64_t>(), size_t(n),
+                                    rocprim::plus<int64_t>(), c.stream));
+    ovp.alloc(size_t(n) * 4);
+    ove.alloc(size_t(n) * 8);
+    ocnt.alloc(8);
+    tb2 = 0;
+    NBG_HIP(rocprim::select(nullptr, tb2, perm, ovf.as<uint8_t>(), ovp.as<uint32_t>(), ocnt.as<uint64_t>(), size_t(n),
+                            c.stream));
+    c.ws_tmp.ensure(tb2);
+    NBG_HIP(rocprim::select(c.ws_tmp.p, tb2, perm, ovf.as<uint8_t>(), ovp.as<uint32_t>(), ocnt.as<uint64_t>(),
+                            size_t(n), c.stream));
+    tb2 = 0;
+    NBG_HIP(rocprim::select(nullptr, tb2, escan.as<int64_t>(), ovf.as<uint8_t>(), ove.as<int64_t>(),
+                            ocnt.as<uint64_t>(), size_t(n), c.stream));
+    c.ws_tmp.ensure(tb2);
+    NBG_HIP(rocprim::select(c.ws_tmp.p, tb2, escan.as<int64_t>(), ovf.as<uint8_t>(), ove.as<int64_t>(),
+                            ocnt.as<uint64_t>(), size_t(n), c.stream));
+    uint64_t no = 0;
+    NBG_HIP(hipMemcpyAsync(&no, ocnt.p, 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    if (no) {
+      out.ov_n = int64_t(no);
+      out.ov_edge.alloc(size_t(no) * 8 + 8);
+      NBG_HIP(hipMemcpyAsync(out.ov_edge.p, ove.p, size_t(no) * 8, hipMemcpyDeviceToDevice, c.stream));
+      k_dec_i64<<<grid_for(int64_t(no)), 256, 0, c.stream>>>(out.ov_edge.as<int64_t>(), int64_t(no));
+    } else {
+      ovp.release();
+    }
+  }
   keyB.release();
   permA.release();
   permB.release();
@@ -1003,68 +1129,9 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
     fill<int64_t>(c, out.rank.as<int64_t>(), s.rank_value, int64_t(m));
   }
   // props
-  if (with_props) {
-    DevBuf tmp;
-    tmp.alloc(size_t(m) * 8 + 8);
-    for (size_t f = 0; f < fields.size(); f++) {
-      PropCol pc;
-      pc.name = fields[f].name;
-      pc.type = fields[f].type;
-      k_gather_i64<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(s.props[f].as<int64_t>(), kp, tmp.as<int64_t>(), int64_t(m));
-      bool has_present = f < s.present.size() && s.present[f].p != nullptr;
-      if (has_present) {
-        pc.present.alloc(size_t(m) + 1);
-        k_gather_u8<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(s.present[f].as<uint8_t>(), kp, pc.present.as<uint8_t>(), int64_t(m));
-      }
-      if (pc.type == NBG_T_STRING) {
-        DevBuf lens, offs_src;
-        lens.alloc(size_t(m) * 8 + 8);
-        offs_src.alloc(size_t(m) * 8 + 8);
-        k_gather_i64<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(s.str_len[f].as<int64_t>(), kp, lens.as<int64_t>(), int64_t(m));
-        NBG_HIP(hipMemcpyAsync(offs_src.p, tmp.p, size_t(m) * 8, hipMemcpyDeviceToDevice, c.stream));
-        DevBuf l2;
-        l2.alloc(size_t(m + 1) * 8);
-        k_str_lengths<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(lens.as<int64_t>(),
-                                                               has_present ? pc.present.as<uint8_t>() : nullptr,
-                                                               int64_t(m), l2.as<int64_t>());
-        NBG_HIP(hipMemsetAsync(l2.as<int64_t>() + m, 0, 8, c.stream));
-        pc.str_off.alloc(size_t(m + 1) * 8);
-        exclusive_scan<int64_t>(c, l2.as<int64_t>(), pc.str_off.as<int64_t>(), int64_t(m) + 1);
-        int64_t total = 0;
-        NBG_HIP(hipMemcpyAsync(&total, pc.str_off.as<int64_t>() + m, 8, hipMemcpyDeviceToHost, c.stream));
-        NBG_HIP(hipStreamSynchronize(c.stream));
-        pc.str_bytes.alloc(size_t(total) + 8);
-        k_str_copy<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(c.heap.as<uint8_t>(), offs_src.as<int64_t>(),
-                                                             pc.str_off.as<int64_t>(), int64_t(m), pc.str_bytes.as<uint8_t>());
-        pc.width = 0;
-      } else if (pc.type == NBG_T_DOUBLE || pc.type == NBG_T_FLOAT) {
-        pc.width = 8;
-        pc.data.alloc(size_t(m) * 8 + 8);
-        NBG_HIP(hipMemcpyAsync(pc.data.p, tmp.p, size_t(m) * 8, hipMemcpyDeviceToDevice, c.stream));
-      } else {
-        // INT / VID / TIMESTAMP / BOOL: narrow to the smallest width holding [min, max]
-        int64_t mn = 0, mx = 0;
-        if (m) minmax_i64(c, tmp.as<int64_t>(), int64_t(m), mn, mx);
-        pc.minv = mn;
-        pc.maxv = mx;
-        int w = 8;
-        if (mn >= INT8_MIN && mx <= INT8_MAX) w = 1;
-        else if (mn >= INT16_MIN && mx <= INT16_MAX) w = 2;
-        else if (mn >= INT32_MIN && mx <= INT32_MAX) w = 4;
-        if (c.opt("narrow_props", 1) == 0) w = 8;
-        pc.width = w;
-        pc.data.alloc(size_t(m) * size_t(w) + 16);
-        int g = grid_for(int64_t(m));
-        switch (w) {
-          case 1: k_narrow<int8_t><<<g, 256, 0, c.stream>>>(tmp.as<int64_t>(), pc.data.as<int8_t>(), int64_t(m)); break;
-          case 2: k_narrow<int16_t><<<g, 256, 0, c.stream>>>(tmp.as<int64_t>(), pc.data.as<int16_t>(), int64_t(m)); break;
-          case 4: k_narrow<int32_t><<<g, 256, 0, c.stream>>>(tmp.as<int64_t>(), pc.data.as<int32_t>(), int64_t(m)); break;
-          default: NBG_HIP(hipMemcpyAsync(pc.data.p, tmp.p, size_t(m) * 8, hipMemcpyDeviceToDevice, c.stream));
-        }
-      }
-      out.props.push_back(std::move(pc));
-    }
-  }
+  if (with_props) gather_props(c, s, fields, kp, int64_t(m), true, out.props);
+  // older versions of multi-version groups (firstLoop side table, selected above)
+  if (out.ov_n) gather_props(c, s, fields, ovp.as<uint32_t>(), out.ov_n, false, out.ov_props);
   NBG_HIP(hipStreamSynchronize(c.stream));
   NBG_HIP(hipGetLastError());
   // free staging

@@ -19,6 +19,7 @@
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_select.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -1269,6 +1270,20 @@ __global__ void k_list_starts(const int32_t* g, int64_t n, int64_t lo, int64_t h
     if (keep) out[s] = loc;
   }
 }
+// rows the hop-1 scans return for a start list WITH its duplicates: each duplicate start rescans
+// its prefix (GoExecutor.cpp:98-104 dedups the starts only under DISTINCT), so the edges scanned
+// (the TEPS numerator, and what the reference's storage returns) count them, while the device
+// expands the deduplicated frontier (P12 makes the next frontier a set either way)
+__global__ void k_starts_degree(const int32_t* g, int64_t n, int64_t lo, int64_t hi, const int64_t* row_ptr,
+                                const uint8_t* row_ok, unsigned long long* sum) {
+  unsigned long long acc = 0;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t x = g[i];
+    if (x >= lo && x < hi && (row_ok == nullptr || row_ok[x - lo])) acc += (unsigned long long)(row_ptr[x - lo + 1] - row_ptr[x - lo]);
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(sum, acc);
+}
 
 // ---- multi-rank frontier exchange ----------------------------------------------------------
 // global byte-map -> 32-bit mark words (one word per thread), clearing the map
@@ -1708,7 +1723,7 @@ void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Progr
 // (no synchronisation); returns the grid used
 int launch_bu_slab(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
                    const FastArgs& fp, const void* slab_w, unsigned long long* out,
-                   unsigned long long* pbits = nullptr) {
+                   unsigned long long* pbits = nullptr, hipEvent_t after_kernel = nullptr) {
   // rows per lane (R) and eagerly loaded slab slots (EAGER) are options (bu_r, bu_eager[_fast])
   constexpr int R = 2;  // rows per lane
   const int EG = int(c.opt(pk == PK_FAST ? "bu_eager_fast" : "bu_eager", 1));
@@ -1766,6 +1781,7 @@ int launch_bu_slab(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
 #undef NBG_BU_W
 #undef NBG_BU
 #undef NBG_BU_K
+  if (after_kernel) NBG_HIP(hipEventRecord(after_kernel, c.stream));
   k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, out);
   NBG_HIP(hipGetLastError());
   return grid;
@@ -1928,7 +1944,6 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   DevBuf degbuf;
   uint8_t* map = c.ws_map.as<uint8_t>();
   uint16_t* bits16 = c.ws_bits_send.as<uint16_t>();  // frontier bitmap written by k_compact
-  const uint32_t* fbits = c.ws_bits_send.as<uint32_t>();
   const int64_t* row_ptr = csr.row_ptr.as<int64_t>();
   const bool bu_ok = es.has_tr && c.opt("bottom_up", 1) != 0;
   const int64_t bu_div = std::max<int64_t>(1, c.opt("bu_div", 4));  // bottom-up when E >= nnz / bu_div
@@ -1949,19 +1964,25 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   int32_t* F = c.ws_front[0].as<int32_t>();
   int64_t nF = 0;
   int64_t nset_global = ns;  // "starts_ non-empty" (GoExecutor.cpp:93-97)
-  NBG_HIP(hipMemsetAsync(K.d, 0, 64, c.stream));
+  int64_t hop1_scanned = -1;  // hop-1 rows with duplicate starts rescanned (k_starts_degree)
+  NBG_HIP(hipMemsetAsync(K.d, 0, 256, c.stream));
   if (ns) {
     if (s.steps == 1 && !s.distinct) {
       k_list_starts<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, F, K.d);
     } else {
       k_mark_gidx<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, map);
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, F, bits16, K.d, es.odeg.as<uint32_t>());
+      if (!s.distinct)
+        k_starts_degree<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, K.d + 30);
     }
     NBG_HIP(hipGetLastError());
-    NBG_HIP(hipMemcpyAsync(K.h, K.d, 128, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipMemcpyAsync(K.h, K.d, 256, hipMemcpyDeviceToHost, c.stream));
     NBG_HIP(hipStreamSynchronize(c.stream));
     nF = int64_t(K.h[0]);
-    if (!(s.steps == 1 && !s.distinct)) E_known = int64_t(K.h[13]);
+    if (!(s.steps == 1 && !s.distinct)) {
+      E_known = int64_t(K.h[13]);
+      if (!s.distinct) hop1_scanned = int64_t(K.h[30]);
+    }
   }
   unsigned long long* red = K.d + 24;  // scratch of the cross-rank sums
   if (es.out_nnz_global < 0) {
@@ -2049,7 +2070,6 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
 
   // Frontier state: a list of local rows (top-down) and/or a bitmap (bottom-up).  E = sum of
   // the frontier's out-degrees = the adjacency entries the hop scans (TEPS numerator).
-  unsigned long long* partials = c.ws_partials.as<unsigned long long>();
   uint32_t* bitsA = c.ws_bits_send.as<uint32_t>();
   uint32_t* bitsB = c.ws_bits_recv.as<uint32_t>();
   bool have_list = true, off_ready = false;
@@ -2085,7 +2105,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   allsum(c, &Eg, 1, red);
   for (int32_t step = 1; step < s.steps; step++) {
     c.timing.steps_run++;
-    c.timing.edges_scanned += uint64_t(E);
+    c.timing.edges_scanned += uint64_t(step == 1 && hop1_scanned >= 0 ? hop1_scanned : E);
     if (Eg == 0) return finish_empty();  // every frontier vertex lacks out-edges
     if (want_bu(Eg)) {
       // bottom-up: frontier bitmap in, next frontier bitmap out
@@ -2096,7 +2116,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       if (defer) pb.alloc(size_t((tr.n_rows + 63) / 64 + 1) * 8);
       hipEventRecord(c.ev[2], c.stream);
       launch_bu_slab(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, nullptr, K.d,
-                     defer ? pb.as<unsigned long long>() : nullptr);
+                     defer ? pb.as<unsigned long long>() : nullptr, c.ev[6]);
       if (!defer) hipEventRecord(c.ev[3], c.stream);
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 64, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
@@ -2106,13 +2126,15 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         hipEventRecord(c.ev[3], c.stream);
         NBG_HIP(hipEventSynchronize(c.ev[3]));
       }
-      float ms = 0;
+      float ms = 0, kms = 0;
       hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
+      hipEventElapsedTime(&kms, c.ev[2], c.ev[6]);
       c.timing.expand_ms += ms;
       c.timing.expand_launches++;
       c.timing.bu_steps++;
-      c.timing.expand_bytes += bu_slab_bytes(K.h, tr.n_rows, 0, true);
-      c.timing.hop(1, false, ms, K.h);
+      const uint64_t kb = bu_slab_bytes(K.h, tr.n_rows, 0, true);
+      c.timing.expand_bytes += kb;
+      c.timing.hop(1, false, ms, K.h, kms, kb);
       std::swap(bitsA, bitsB);
       have_list = false;
       off_ready = false;
@@ -2198,7 +2220,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         if (defer) pb.alloc(size_t((tr.n_rows + 63) / 64 + 1) * 8);
         hipEventRecord(c.ev[2], c.stream);
         launch_bu_slab(c, es, fb, bitsB, nullptr, pk, tfp, slab_w, K.d + 8,
-                       defer ? pb.as<unsigned long long>() : nullptr);
+                       defer ? pb.as<unsigned long long>() : nullptr, c.ev[6]);
         unsigned long long h2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (defer) {
           NBG_HIP(hipMemcpyAsync(K.h + 8, K.d + 8, 64, hipMemcpyDeviceToHost, c.stream));
@@ -2212,16 +2234,17 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         hipEventRecord(c.ev[3], c.stream);
         NBG_HIP(hipMemcpyAsync(K.h, K.d, 128, hipMemcpyDeviceToHost, c.stream));
         NBG_HIP(hipStreamSynchronize(c.stream));  // K.h is pinned: the copy is truly asynchronous
-        float ms = 0;
+        float ms = 0, kms = 0;
         hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
+        hipEventElapsedTime(&kms, c.ev[2], c.ev[6]);
         c.timing.expand_ms += ms;
         c.timing.expand_launches++;
         c.timing.bu_steps++;
         nrows = int64_t(K.h[0]);
         if (defer) memcpy(K.h + 8, h2, sizeof(h2));
-        c.timing.expand_bytes += bu_slab_bytes(K.h + 8, tr.n_rows, pk == PK_FAST ? tfp.width : 0, false) +
-                                 uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
-        c.timing.hop(1, true, ms, K.h + 8);
+        const uint64_t kb = bu_slab_bytes(K.h + 8, tr.n_rows, pk == PK_FAST ? tfp.width : 0, false);
+        c.timing.expand_bytes += kb + uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
+        c.timing.hop(1, true, ms, K.h + 8, kms, kb);
       } else {
         ensure_off();
         a.F = F;
@@ -2498,35 +2521,52 @@ struct BoundCols {
   int32_t n;
   BoundCol c[kMaxBoundCols];
 };
-__global__ void k_bound_rows(const int64_t* kept_slots, const int64_t* owner, int64_t m, const int64_t* off,
-                             const int32_t* F, const int64_t* row_ptr, int64_t lo, EvalEnv env, BoundCols bc,
-                             int64_t* ge_out) {
+// flattened slot -> edge index of the kept rows
+__global__ void k_slot_ge(const int64_t* kept_slots, const int64_t* owner, int64_t m, const int64_t* off,
+                          const int32_t* F, const int64_t* row_ptr, int64_t* ge) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
-    int64_t k = owner[i];
-    int32_t f = F[k];
-    int64_t ge = row_ptr[f] + (kept_slots[i] - off[k]);
-    ge_out[i] = ge;
+    const int64_t k = owner[i];
+    ge[i] = row_ptr[F[k]] + (kept_slots[i] - off[k]);
+  }
+}
+// one value of a getBound column for row i: edge ge's key props, and its props either from the
+// CSR (old < 0) or from the older-version side table (row old, Csr::ov_*)
+__device__ inline int64_t bound_value(const BoundCol& b, int64_t ge, int64_t old, int32_t f, int64_t lo,
+                                      const EvalEnv& env, const PropDev* oprops, bool& present) {
+  present = true;
+  switch (b.kind) {
+    case 1: return env.vid_of[env.col[ge]];
+    case 2: return env.vid_of[lo + f];
+    case 3: return env.rank ? env.rank[ge] : 0;
+    case 4: return env.etype;
+    default: {
+      const PropDev& p = old < 0 ? env.props[b.prop] : oprops[b.prop];
+      const int64_t x = old < 0 ? ge : old;
+      if (p.present && !p.present[x]) {
+        present = false;
+        return INT64_MIN;
+      }
+      if (p.type == NBG_T_STRING) return x;
+      if (p.type == NBG_T_DOUBLE || p.type == NBG_T_FLOAT) return static_cast<const int64_t*>(p.data)[x];
+      return load_int(p.data, p.width, x);
+    }
+  }
+}
+__global__ void k_bound_rows(const int64_t* ge_in, const int64_t* old_in, const int64_t* owner, int64_t m,
+                             const int32_t* F, int64_t lo, EvalEnv env, const PropDev* oprops, BoundCols bc) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t ge = ge_in[i];
+    const int64_t old = old_in ? old_in[i] : -1;
+    const int32_t f = F[owner[i]];
     for (int c = 0; c < bc.n; c++) {
       const BoundCol& b = bc.c[c];
-      int64_t v = 0;
-      switch (b.kind) {
-        case 1: v = env.vid_of[env.col[ge]]; break;
-        case 2: v = env.vid_of[lo + f]; break;
-        case 3: v = env.rank ? env.rank[ge] : 0; break;
-        case 4: v = env.etype; break;
-        default: {
-          const PropDev& p = env.props[b.prop];
-          if (p.type == NBG_T_STRING) {
-            b.str_len[i] = (p.present && !p.present[ge]) ? -1 : p.str_off[ge + 1] - p.str_off[ge];
-            continue;
-          }
-          if (p.present && !p.present[ge]) {
-            v = INT64_MIN;
-          } else if (p.type == NBG_T_DOUBLE || p.type == NBG_T_FLOAT) {
-            v = static_cast<const int64_t*>(p.data)[ge];
-          } else {
-            v = load_int(p.data, p.width, ge);
-          }
+      bool present;
+      const int64_t v = bound_value(b, ge, old, f, lo, env, oprops, present);
+      if (b.kind == 0) {
+        const PropDev& p = old < 0 ? env.props[b.prop] : oprops[b.prop];
+        if (p.type == NBG_T_STRING) {
+          b.str_len[i] = present ? p.str_off[v + 1] - p.str_off[v] : -1;
+          continue;
         }
       }
       if (b.type == NBG_T_BOOL) static_cast<uint8_t*>(b.out)[i] = uint8_t(v != 0);
@@ -2535,31 +2575,20 @@ __global__ void k_bound_rows(const int64_t* kept_slots, const int64_t* owner, in
   }
 }
 // outBoundStats / inBoundStats (QueryStatsProcessor.cpp:69-125, StatsCollector Collector.h:66-94):
-// over the kept edge slots, the int64 sum (wrapping, as the reference's int64 adds) and the count
-// of present values of column c.  acc[2c] = sum, acc[2c+1] = count.  Doubles only count (a double
+// over the kept rows, the int64 sum (wrapping, as the reference's int64 adds) and the count of
+// present values of column c.  acc[2c] = sum, acc[2c+1] = count.  Doubles only count (a double
 // reaching the reference's int64-initialised sum throws, reported by the caller).
-__global__ void k_bound_stats(const int64_t* kept_slots, const int64_t* owner, int64_t m, const int64_t* off,
-                              const int32_t* F, const int64_t* row_ptr, int64_t lo, EvalEnv env, BoundCol b,
+__global__ void k_bound_stats(const int64_t* ge_in, const int64_t* old_in, const int64_t* owner, int64_t m,
+                              const int32_t* F, int64_t lo, EvalEnv env, const PropDev* oprops, BoundCol b,
                               unsigned long long* acc) {
   unsigned long long sum = 0, cnt = 0;
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t k = owner[i];
-    const int32_t f = F[k];
-    const int64_t ge = row_ptr[f] + (kept_slots[i] - off[k]);
-    int64_t v = 0;
-    bool present = true;
-    switch (b.kind) {
-      case 1: v = env.vid_of[env.col[ge]]; break;
-      case 2: v = env.vid_of[lo + f]; break;
-      case 3: v = env.rank ? env.rank[ge] : 0; break;
-      case 4: v = env.etype; break;
-      default: {
-        const PropDev& p = env.props[b.prop];
-        present = !(p.present && !p.present[ge]);
-        if (present && p.type != NBG_T_STRING && p.type != NBG_T_DOUBLE && p.type != NBG_T_FLOAT &&
-            p.type != NBG_T_BOOL)
-          v = load_int(p.data, p.width, ge);
-      }
+    const int64_t old = old_in ? old_in[i] : -1;
+    bool present;
+    int64_t v = bound_value(b, ge_in[i], old, F[owner[i]], lo, env, oprops, present);
+    if (b.kind == 0) {
+      const int32_t t = (old < 0 ? env.props[b.prop] : oprops[b.prop]).type;
+      if (t == NBG_T_STRING || t == NBG_T_DOUBLE || t == NBG_T_FLOAT || t == NBG_T_BOOL) v = 0;
     }
     if (present) {
       sum += (unsigned long long)v;
@@ -2574,11 +2603,87 @@ __global__ void k_bound_stats(const int64_t* kept_slots, const int64_t* owner, i
   }
 }
 
-__global__ void k_str_gather(const int64_t* ge, int64_t m, const int64_t* src_off, const uint8_t* src_bytes,
+// collectEdgeProps' firstLoop (QueryBaseProcessor.inl:349-402): until a key is emitted the scan
+// does not skip a group's older versions, so when every key before it fails the filter (all
+// versions of the earlier groups and the newer versions of its own group), the first older
+// version that passes is emitted, ahead of the row's ordinary rows.  One thread per request
+// entry (frontier entry k = local row F[k], flags of its edges at off[k]..): walks its edges in
+// key order until the first kept one; per edge whose first version failed, its older versions.
+// x_old[k] = the emitted older version's side-table row (-1: none), x_ge[k] = its edge.
+template <int PK>
+__global__ void k_first_loop(const int32_t* F, const int64_t* off, int64_t nF, const int64_t* row_ptr,
+                             const uint8_t* flags, const int64_t* ov_edge, int64_t ov_n, const Program* prog,
+                             EvalEnv oenv, FastArgs ofp, int64_t lo, int64_t* x_old, int64_t* x_ge) {
+  for (int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; k < nF; k += int64_t(gridDim.x) * blockDim.x) {
+    x_old[k] = -1;
+    const int32_t f = F[k];
+    const int64_t b = row_ptr[f], e = row_ptr[f + 1];
+    int64_t l = 0, h = ov_n;  // first older version at or after edge b
+    while (l < h) {
+      const int64_t mid = (l + h) >> 1;
+      if (ov_edge[mid] < b) l = mid + 1; else h = mid;
+    }
+    int64_t x = b;  // edges [b, x) checked: their first versions failed
+    for (int64_t o = l; o < ov_n && ov_edge[o] < e;) {
+      const int64_t ge = ov_edge[o];
+      bool kept = false;
+      for (; x <= ge && !kept; x++) kept = flags[off[k] + (x - b)] != 0;
+      if (kept) break;  // an ordinary row comes first: firstLoop ends there
+      bool hit = false;
+      for (; o < ov_n && ov_edge[o] == ge && !hit; o++) {
+        bool pass;
+        if (PK == PK_FAST) {
+          pass = (ofp.present && !ofp.present[o]) ? true
+                                                   : fast_cmp(ofp.op, static_cast<const int64_t*>(ofp.data)[o], ofp.k);
+        } else {
+          const Val v = eval_program(prog, oenv, o, int32_t(lo) + f, 0);
+          pass = v.t == VT_ERR ? true : as_bool(v);  // storage: an eval error keeps the edge
+        }
+        if (pass) {
+          x_old[k] = o;
+          x_ge[k] = ge;
+          hit = true;
+        }
+      }
+      if (hit) break;
+    }
+  }
+}
+// merged row list: entry k's older-version row (if any) goes first, then its kept rows.
+// cx = inclusive count of entries with an older-version row.
+__global__ void k_merge_kept(const int64_t* ge, const int64_t* owner, int64_t m, const int64_t* cx, int64_t* mge,
+                             int64_t* mold, int64_t* mowner) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t k = owner[i];
+    const int64_t pos = i + cx[k];
+    mge[pos] = ge[i];
+    mold[pos] = -1;
+    mowner[pos] = k;
+  }
+}
+__global__ void k_merge_old(const int64_t* x_old, const int64_t* x_ge, int64_t nF, const int64_t* owner, int64_t m,
+                            const int64_t* cx, int64_t* mge, int64_t* mold, int64_t* mowner) {
+  for (int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; k < nF; k += int64_t(gridDim.x) * blockDim.x) {
+    if (x_old[k] < 0) continue;
+    int64_t l = 0, h = m;  // kept rows of entries < k
+    while (l < h) {
+      const int64_t mid = (l + h) >> 1;
+      if (owner[mid] < k) l = mid + 1; else h = mid;
+    }
+    const int64_t pos = l + cx[k] - 1;
+    mge[pos] = x_ge[k];
+    mold[pos] = x_old[k];
+    mowner[pos] = k;
+  }
+}
+
+__global__ void k_str_gather(const int64_t* ge, const int64_t* old, int64_t m, const int64_t* src_off,
+                             const uint8_t* src_bytes, const int64_t* osrc_off, const uint8_t* osrc_bytes,
                              const int64_t* dst_off, uint8_t* dst) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
     int64_t len = dst_off[i + 1] - dst_off[i];
-    const uint8_t* s = src_bytes + src_off[ge[i]];
+    const bool o = old && old[i] >= 0;
+    const uint8_t* s = o ? osrc_bytes + osrc_off[old[i]] : src_bytes + src_off[ge[i]];
     for (int64_t j = 0; j < len; j++) dst[dst_off[i] + j] = s[j];
   }
 }
@@ -2884,18 +2989,84 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
   }
   owner.alloc(size_t(m + 1) * 8);
   geb.alloc(size_t(m + 1) * 8);
+  if (m) {
+    k_slot_owner<<<grid_cap(m), 256, 0, c.stream>>>(slots.as<int64_t>(), m, dcoff.as<int64_t>(), nF, owner.as<int64_t>());
+    k_slot_ge<<<grid_cap(m), 256, 0, c.stream>>>(slots.as<int64_t>(), owner.as<int64_t>(), m, dcoff.as<int64_t>(),
+                                                 dcF.as<int32_t>(), csr.row_ptr.as<int64_t>(), geb.as<int64_t>());
+    NBG_HIP(hipGetLastError());
+  }
+  // firstLoop (multi-version data under a push-down filter): older versions emitted ahead of a
+  // request entry's rows (QueryBaseProcessor.inl:349-402); the reader only exists for out-bound
+  // rows with a value, so in-bound scans never evaluate the filter
+  DevBuf oldb, ovtab;
+  const PropDev* oprops = nullptr;
+  if (flen && !in_bound && csr.ov_n > 0 && nF > 0) {
+    std::vector<PropDev> tab;
+    for (const PropCol& p : csr.ov_props)
+      tab.push_back(PropDev{p.type, p.width, p.data.p, p.present.as<uint8_t>(), p.str_off.as<int64_t>(),
+                            p.str_bytes.as<uint8_t>()});
+    ovtab.alloc(sizeof(PropDev) * std::max<size_t>(tab.size(), 1));
+    if (!tab.empty()) c.h2d(ovtab.p, tab.data(), sizeof(PropDev) * tab.size());
+    oprops = ovtab.as<PropDev>();
+    EvalEnv oenv = env;
+    oenv.props = oprops;
+    FastArgs ofp{};
+    if (pk == PK_FAST) {
+      const FastPred f = classify_pred(fprog, es.fields);
+      const PropCol& oc = csr.ov_props[size_t(f.col)];
+      ofp = FastArgs{oc.data.p, oc.present.as<uint8_t>(), 8, f.op, f.k};
+    }
+    DevBuf xo, xg, cx;
+    xo.alloc(size_t(nF) * 8);
+    xg.alloc(size_t(nF) * 8);
+    cx.alloc(size_t(nF) * 8);
+    if (pk == PK_FAST)
+      k_first_loop<PK_FAST><<<grid_cap(nF), 256, 0, c.stream>>>(dcF.as<int32_t>(), dcoff.as<int64_t>(), nF,
+                                                                csr.row_ptr.as<int64_t>(), flags.as<uint8_t>(),
+                                                                csr.ov_edge.as<int64_t>(), csr.ov_n, dprog.as<Program>(),
+                                                                oenv, ofp, lo, xo.as<int64_t>(), xg.as<int64_t>());
+    else
+      k_first_loop<PK_VM><<<grid_cap(nF), 256, 0, c.stream>>>(dcF.as<int32_t>(), dcoff.as<int64_t>(), nF,
+                                                              csr.row_ptr.as<int64_t>(), flags.as<uint8_t>(),
+                                                              csr.ov_edge.as<int64_t>(), csr.ov_n, dprog.as<Program>(),
+                                                              oenv, ofp, lo, xo.as<int64_t>(), xg.as<int64_t>());
+    NBG_HIP(hipGetLastError());
+    auto has = rocprim::make_transform_iterator(xo.as<int64_t>(), [] __device__(int64_t v) -> int64_t { return v >= 0; });
+    size_t tb = 0;
+    NBG_HIP(rocprim::inclusive_scan(nullptr, tb, has, cx.as<int64_t>(), size_t(nF), rocprim::plus<int64_t>(), c.stream));
+    c.ws_tmp.ensure(tb);
+    NBG_HIP(rocprim::inclusive_scan(c.ws_tmp.p, tb, has, cx.as<int64_t>(), size_t(nF), rocprim::plus<int64_t>(), c.stream));
+    int64_t X = 0;
+    NBG_HIP(hipMemcpyAsync(&X, cx.as<int64_t>() + nF - 1, 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    if (X > 0) {
+      DevBuf mge, mold, mown;
+      mge.alloc(size_t(m + X + 1) * 8);
+      mold.alloc(size_t(m + X + 1) * 8);
+      mown.alloc(size_t(m + X + 1) * 8);
+      if (m)
+        k_merge_kept<<<grid_cap(m), 256, 0, c.stream>>>(geb.as<int64_t>(), owner.as<int64_t>(), m, cx.as<int64_t>(),
+                                                        mge.as<int64_t>(), mold.as<int64_t>(), mown.as<int64_t>());
+      k_merge_old<<<grid_cap(nF), 256, 0, c.stream>>>(xo.as<int64_t>(), xg.as<int64_t>(), nF, owner.as<int64_t>(), m,
+                                                      cx.as<int64_t>(), mge.as<int64_t>(), mold.as<int64_t>(),
+                                                      mown.as<int64_t>());
+      NBG_HIP(hipGetLastError());
+      m += X;
+      geb = std::move(mge);
+      owner = std::move(mown);
+      oldb = std::move(mold);
+    }
+  }
+  const int64_t* oldp = oldb.as<int64_t>();
   if (stats) {
     // one row: per column SUM (INT) / COUNT (INT) / AVG (DOUBLE), in request order (retIndex)
     DevBuf acc;
     acc.alloc(size_t(2 * bc.n + 2) * 8);
     NBG_HIP(hipMemsetAsync(acc.p, 0, size_t(2 * bc.n + 2) * 8, c.stream));
     if (m) {
-      k_slot_owner<<<grid_cap(m), 256, 0, c.stream>>>(slots.as<int64_t>(), m, dcoff.as<int64_t>(), nF,
-                                                      owner.as<int64_t>());
       for (int i = 0; i < bc.n; i++)
-        k_bound_stats<<<grid_cap(m, 256, 1024), 256, 0, c.stream>>>(slots.as<int64_t>(), owner.as<int64_t>(), m,
-                                                                    dcoff.as<int64_t>(), dcF.as<int32_t>(),
-                                                                    csr.row_ptr.as<int64_t>(), lo, env, bc.c[i],
+        k_bound_stats<<<grid_cap(m, 256, 1024), 256, 0, c.stream>>>(geb.as<int64_t>(), oldp, owner.as<int64_t>(), m,
+                                                                    dcF.as<int32_t>(), lo, env, oprops, bc.c[i],
                                                                     acc.as<unsigned long long>() + 2 * i);
       NBG_HIP(hipGetLastError());
     }
@@ -2943,10 +3114,8 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
   }
   std::vector<int64_t> howner(static_cast<size_t>(m));
   if (m) {
-    k_slot_owner<<<grid_cap(m), 256, 0, c.stream>>>(slots.as<int64_t>(), m, dcoff.as<int64_t>(), nF, owner.as<int64_t>());
-    k_bound_rows<<<grid_cap(m), 256, 0, c.stream>>>(slots.as<int64_t>(), owner.as<int64_t>(), m, dcoff.as<int64_t>(),
-                                                  dcF.as<int32_t>(), csr.row_ptr.as<int64_t>(), lo, env, bc,
-                                                  geb.as<int64_t>());
+    k_bound_rows<<<grid_cap(m), 256, 0, c.stream>>>(geb.as<int64_t>(), oldp, owner.as<int64_t>(), m,
+                                                  dcF.as<int32_t>(), lo, env, oprops, bc);
     NBG_HIP(hipGetLastError());
     NBG_HIP(hipMemcpyAsync(howner.data(), owner.p, size_t(m) * 8, hipMemcpyDeviceToHost, c.stream));
   }
@@ -2970,8 +3139,11 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
       NBG_HIP(hipMemcpy(doffs.p, offs.data(), size_t(m + 1) * 8, hipMemcpyHostToDevice));
       const PropCol& pc = csr.props[size_t(b.prop)];
       if (m)
-        k_str_gather<<<grid_cap(m), 256, 0, c.stream>>>(geb.as<int64_t>(), m, pc.str_off.as<int64_t>(),
-                                                        pc.str_bytes.as<uint8_t>(), doffs.as<int64_t>(), dbytes.as<uint8_t>());
+        k_str_gather<<<grid_cap(m), 256, 0, c.stream>>>(
+            geb.as<int64_t>(), oldp, m, pc.str_off.as<int64_t>(), pc.str_bytes.as<uint8_t>(),
+            oldp ? csr.ov_props[size_t(b.prop)].str_off.as<int64_t>() : nullptr,
+            oldp ? csr.ov_props[size_t(b.prop)].str_bytes.as<uint8_t>() : nullptr, doffs.as<int64_t>(),
+            dbytes.as<uint8_t>());
       NBG_HIP(hipStreamSynchronize(c.stream));
       h->host.emplace_back(size_t(offs[size_t(m)]) + 8);
       if (offs[size_t(m)]) NBG_HIP(hipMemcpy(h->host.back().data(), dbytes.p, size_t(offs[size_t(m)]), hipMemcpyDeviceToHost));

@@ -229,7 +229,8 @@ class GraphSpace:
         self._check(self.L.nbg_last_timing(self.h, C.byref(t)))
         d = {k: getattr(t, k) for k, _ in t._fields_ if k not in ("hops", "n_hops")}
         d["hops"] = [{"mode": "bottom-up" if h.mode else "top-down", "final": bool(h.final_hop), "ms": h.ms,
-                      "bytes": int(h.bytes), "c": list(h.c)} for h in t.hops[:t.n_hops]]
+                      "bytes": int(h.bytes), "c": list(h.c), "kernel_ms": h.kernel_ms,
+                      "kernel_bytes": int(h.kernel_bytes)} for h in t.hops[:t.n_hops]]
         return d
 
     # ---- queries ---------------------------------------------------------------------
@@ -458,8 +459,9 @@ class QueryStatsProcessor:
             vids += list(vs)
         cols = [(c.name, c.owner, c.tag_id) for c, _ in req.return_columns]
         stats = [st for _, st in req.return_columns]
-        et = req.edge_type if self.bound_type == OUT_BOUND else -req.edge_type
-        rs = self.space.bound_stats(et, parts, vids, cols, stats, req.filter)
+        # the client already sends -edge_type for an in-bound request (StorageClient.cpp:116) and the
+        # processor scans req.edge_type as is (QueryBaseProcessor.inl:39-40), as QueryBoundProcessor
+        rs = self.space.bound_stats(req.edge_type, parts, vids, cols, stats, req.filter)
         kept = [c.name for c, _ in req.return_columns
                 if self.bound_type == OUT_BOUND or c.owner != _lib.OWNER_EDGE or c.name.startswith("_")]
         failed = [{"part_id": p, "code": c} for p, c in rs.failed]

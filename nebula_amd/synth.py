@@ -76,3 +76,12 @@ def pairs(scale: int, edge_factor: int, graph_seed: int, n: int, pick_seed: int 
     a = rng.integers(0, edge_factor << scale, n, dtype=np.uint64)
     b = rng.integers(0, edge_factor << scale, n, dtype=np.uint64)
     return edges(scale, graph_seed, a)[0], edges(scale, graph_seed, b)[1]
+
+
+def hub_candidates(scale: int, graph_seed: int):
+    """vids of the RMAT indices with at most one 1-bit (0 and 2^k): the expected out-degree of
+    index u is E * 0.76^(zero bits) * 0.24^(one bits), so the highest-degree vertices are, with
+    overwhelming probability, among these scale + 1 candidates.  C5's "top-8 degree" seeds are
+    the 8 of them with the largest out-degree in the built snapshot."""
+    idx = np.array([0] + [1 << k for k in range(scale)], dtype=np.uint64)
+    return vid(idx, graph_seed)

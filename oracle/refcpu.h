@@ -94,6 +94,23 @@ ora_result* ora_go(ora_store* st, const int64_t* starts, size_t n_starts, int32_
 ora_result* ora_shortest_path(ora_store* st, const int64_t* src, const int64_t* dst,
                               size_t npairs, int32_t edge_type, int32_t max_steps);
 
+// ---- index-space restatement of GO / FIND SHORTEST PATH on the synthetic RMAT graph -----
+// (oracle/rmat_graph.cpp): for parity at the configured sizes, where the KV store above does
+// not fit.  Checked against the KV-store restatement at small scales (tests).
+typedef struct ora_rmat_graph ora_rmat_graph;
+ora_rmat_graph* ora_rmat_graph_new(int32_t scale, int32_t edge_factor, uint64_t seed, int32_t threads);
+void ora_rmat_graph_free(ora_rmat_graph* g);
+void ora_rmat_graph_info(const ora_rmat_graph* g, int64_t* n_vertices, int64_t* n_edges);
+int64_t ora_rmat_graph_out_degree(const ora_rmat_graph* g, int64_t idx);
+// GO steps [WHERE weight > where_gt] YIELD _dst [DISTINCT]: sorted result vids in *out
+int64_t ora_rmat_graph_go(const ora_rmat_graph* g, const int64_t* starts, size_t n_starts, int32_t steps,
+                          int32_t has_where, int64_t where_gt, int32_t distinct, int32_t threads,
+                          int64_t** out, uint64_t* edges_scanned);
+void ora_rmat_graph_shortest_path(ora_rmat_graph* g, const int64_t* src, const int64_t* dst, size_t n,
+                                  int32_t max_steps, int32_t threads, int64_t* hops, int64_t* path_off,
+                                  int64_t** path_vids);
+void ora_free(void* p);
+
 // ---- results --------------------------------------------------------------------------------
 int32_t ora_res_code(const ora_result* r);          // 0 ok, else error code
 const char* ora_res_error(const ora_result* r);

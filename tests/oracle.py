@@ -21,8 +21,8 @@ SOURCE, DEST, EDGE = 1, 2, 3
 
 
 def build() -> Path:
-    src = ROOT / "oracle" / "refcpu.cpp"
-    if not LIB.exists() or LIB.stat().st_mtime < src.stat().st_mtime:
+    srcs = [ROOT / "oracle" / f for f in ("refcpu.cpp", "rmat_graph.cpp", "refcpu.h", "rmat_def.h")]
+    if not LIB.exists() or any(LIB.stat().st_mtime < s.stat().st_mtime for s in srcs):
         subprocess.run(["make", "-C", str(ROOT / "oracle")], check=True,
                        stdout=subprocess.DEVNULL)
     return LIB
@@ -86,6 +86,13 @@ def lib():
             "ora_res_schema_name": (C.c_char_p, [vp, i32, i32]),
             "ora_res_schema_type": (i32, [vp, i32, i32]),
             "ora_res_free": (None, [vp]),
+            "ora_rmat_graph_new": (vp, [i32, i32, u64, i32]),
+            "ora_rmat_graph_free": (None, [vp]),
+            "ora_rmat_graph_info": (None, [vp, P(i64), P(i64)]),
+            "ora_rmat_graph_out_degree": (i64, [vp, i64]),
+            "ora_rmat_graph_go": (i64, [vp, vp, sz, i32, i32, i64, i32, i32, P(P(i64)), P(u64)]),
+            "ora_rmat_graph_shortest_path": (None, [vp, vp, vp, sz, i32, i32, vp, vp, P(P(i64))]),
+            "ora_free": (None, [vp]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -373,6 +380,66 @@ class Store:
 
 class PropDef(C.Structure):
     _fields_ = [("name", C.c_char_p), ("owner", C.c_int32), ("tag_id", C.c_int32)]
+
+
+class RmatGraph:
+    """Index-space restatement of GO / FIND SHORTEST PATH on the synthetic RMAT graph
+    (oracle/rmat_graph.cpp) -- the checker at the configured sizes (RMAT-18..26)."""
+
+    def __init__(self, scale, edge_factor=16, seed=1, threads=None):
+        self.scale = scale
+        self.threads = threads or min(16, os.cpu_count() or 1)
+        self.h = lib().ora_rmat_graph_new(scale, edge_factor, seed, self.threads)
+        if not self.h:
+            raise ValueError("bad RMAT parameters")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ora_rmat_graph_free(self.h)
+            self.h = None
+
+    def info(self):
+        nv, ne = C.c_int64(), C.c_int64()
+        lib().ora_rmat_graph_info(self.h, C.byref(nv), C.byref(ne))
+        return {"num_vertices": nv.value, "num_edges": ne.value}
+
+    def go(self, starts, steps, where_gt=None, distinct=False):
+        """sorted int64 result vids of GO steps [WHERE weight > where_gt] YIELD _dst [DISTINCT]
+        and the edges scanned (rows the storage returned over all hops)"""
+        starts = np.ascontiguousarray(starts, dtype=np.int64)
+        out = C.POINTER(C.c_int64)()
+        scanned = C.c_uint64()
+        n = lib().ora_rmat_graph_go(self.h, _ptr(starts), len(starts), steps, int(where_gt is not None),
+                                    int(where_gt or 0), int(distinct), self.threads, C.byref(out),
+                                    C.byref(scanned))
+        try:
+            res = np.ctypeslib.as_array(out, shape=(n,)).copy() if n > 0 else np.zeros(0, dtype=np.int64)
+        finally:
+            lib().ora_free(C.cast(out, C.c_void_p))
+        return res, scanned.value
+
+    def shortest_path(self, src, dst, max_steps):
+        """(hops int64[n], [path vids per pair]) -- ora_shortest_path's definition"""
+        src = np.ascontiguousarray(src, dtype=np.int64)
+        dst = np.ascontiguousarray(dst, dtype=np.int64)
+        n = len(src)
+        hops = np.empty(max(n, 1), dtype=np.int64)
+        off = np.empty(n + 1, dtype=np.int64)
+        pv = C.POINTER(C.c_int64)()
+        lib().ora_rmat_graph_shortest_path(self.h, _ptr(src), _ptr(dst), n, max_steps, self.threads, _ptr(hops),
+                                           _ptr(off), C.byref(pv))
+        try:
+            flat = np.ctypeslib.as_array(pv, shape=(max(int(off[-1]), 1),))[:int(off[-1])].copy()
+        finally:
+            lib().ora_free(C.cast(pv, C.c_void_p))
+        return hops[:n], [flat[off[i]:off[i + 1]] for i in range(n)]
+
+
+def digest(vids) -> str:
+    """SHA-256 of a result column as sorted little-endian int64 (the committed golden form)."""
+    import hashlib
+    a = np.sort(np.asarray(vids, dtype=np.int64)).astype("<i8")
+    return hashlib.sha256(a.tobytes()).hexdigest()
 
 
 def rmat_edges(scale, edge_factor, seed):

@@ -187,6 +187,12 @@ def oracle_by_vertex(res):
     X.Relational(X.GE, X.AliasProp("e101", "col_0"), X.Primary(10007)),
     X.Relational(X.LT, X.AliasProp("e101", "col_2"), X.Primary(10005)) | (X.AliasProp("e101", "col_14").eq("string_col_14_2")),
     X.AliasProp("e101", "col_11") > X.Primary("string_col_11_1"),
+    # firstLoop (QueryBaseProcessor.inl:349-402): the newest version (2) fails, so the scan keeps
+    # reading versions until one passes and emits it -- one older-version row per vertex
+    X.AliasProp("e101", "col_14").eq("string_col_14_1"),
+    X.AliasProp("e101", "col_14").eq("string_col_14_0"),
+    X.Relational(X.GE, X.AliasProp("e101", "col_0"), X.Primary(10003)) & X.AliasProp("e101", "col_10").eq("string_col_10_0"),
+    X.Relational(X.GE, X.AliasProp("e101", "col_0"), X.Primary(10006)) | X.AliasProp("e101", "col_12").eq("string_col_12_1"),
 ])
 def test_get_bound_matches_reference(qb, filt):
     sp, st = qb
@@ -393,6 +399,31 @@ def test_rmat_multiversion_first_version_wins():
         g = sp.go(starts, steps, FOLLOW, where=w, yields=y)
         r = st.go(starts, steps, FOLLOW, where=w.encode(), yields=[x.encode() for x in y])
         assert ms(g.rows()) == ms(r.rows())
+    sp.close()
+
+
+@pytest.mark.parametrize("k", [0, 500, 900, 998])
+def test_rmat_multiversion_get_bound_first_loop(k):
+    """push-down filters over 3-version data (older versions carry other weights): the fast typed
+    compare and the VM both follow collectEdgeProps' firstLoop rule, in getBound and in stats"""
+    st = oracle_rmat(10, versions=3)
+    sp = GraphSpace(64)
+    sp.set_edge_schema(FOLLOW, [("weight", O.INT)])
+    for p in range(1, 65):
+        sp.load_part(p, st.dump_part(p))
+    sp.finalize()
+    starts = seeds_from(10, 48, seed=13)
+    parts = [O.part_of(v, 64) for v in starts]
+    cols = [("_dst", O.EDGE, 0), ("weight", O.EDGE, 0), ("_rank", O.EDGE, 0)]
+    for f in (X.AliasProp("follow", "weight") > k,                       # fast typed compare
+              (X.AliasProp("follow", "weight") % 7).eq(k % 7) | (X.AliasProp("follow", "weight") > k)):  # VM
+        g = sp.get_bound(FOLLOW, parts, starts, cols, f)
+        r = st.get_bound(FOLLOW, parts, starts, cols, filt=f.encode())
+        assert vertex_groups_gpu(g) == vertex_groups_oracle(r)
+        gs = sp.bound_stats(FOLLOW, parts, starts, [("weight", O.EDGE, 0), ("_dst", O.EDGE, 0)], [1, 2], f)
+        rs = st.bound_stats(FOLLOW, parts, starts, [("weight", O.EDGE, 0), ("_dst", O.EDGE, 0)], [1, 2],
+                            filt=f.encode())
+        assert gs.rows() == rs.rows()
     sp.close()
 
 

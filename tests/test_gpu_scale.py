@@ -1,0 +1,186 @@
+"""GPU parity at the configured sizes (BASELINE.json configs, SURVEY 8c "Large (RMAT-22+) ...
+checked by digest").
+
+The HIP path (through the C ABI) is compared with the oracle's index-space restatement
+(oracle/rmat_graph.cpp, pinned to the faithful KV-store restatement by
+tests/test_oracle_rmat_graph.py) on the same RMAT graphs:
+
+* RMAT-18/20: full result arrays, run here (seconds on the CPU), plus the committed digests;
+* RMAT-22/26: the committed digests of tests/golden/rmat_digests.json (generated in the build
+  container by tests/golden/make_rmat_digests.py), since /root/reference and a host large
+  enough for the restatement at RMAT-26 are not on the GPU box.
+
+Bar: bit-exact sorted result columns (P18: the reference's result check sorts both sides), and
+the same edges_scanned (the TEPS numerator of the bench line).
+"""
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle as O
+from nebula_amd import GraphSpace
+from nebula_amd import expr as X
+from nebula_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+FOLLOW = 1
+GOLD = json.loads((Path(__file__).resolve().parent / "golden" / "rmat_digests.json").read_text())
+W499 = X.AliasProp("follow", "weight") > 499
+
+
+def rmat_space(scale, **opts):
+    sp = GraphSpace(64)
+    for k, v in opts.items():
+        sp.set_option(k, v)
+    sp.set_edge_schema(FOLLOW, [("weight", O.INT)])
+    sp.gen_rmat(scale, 16, 1, FOLLOW)
+    sp.finalize()
+    return sp
+
+
+def bench_query(sp, scale, seeds=64):
+    starts = synth.seeds(scale, 16, 1, seeds)
+    return sp.go(starts, 3, FOLLOW, where=W499, yields=[X.EdgeDst("follow")], distinct=True)
+
+
+def check_gold(name, col, scanned):
+    g = GOLD[name]
+    assert len(col) == g["n_rows"], name
+    assert O.digest(col) == g["sha256"], name
+    assert scanned == g["edges_scanned"], name
+
+
+@pytest.fixture(scope="module")
+def rmat20():
+    sp = rmat_space(20)
+    g = O.RmatGraph(20, 16, 1)
+    yield sp, g
+    sp.close()
+
+
+@pytest.mark.parametrize("force", [0, 1, -1])
+def test_bench_query_rmat20(rmat20, force):
+    """configs[2]'s query (the bench line's workload) at RMAT-20, in every direction mode"""
+    sp, g = rmat20
+    sp.set_option("bu_force", force)
+    try:
+        r = bench_query(sp, 20)
+    finally:
+        sp.set_option("bu_force", 0)
+    want, scanned = g.go(synth.seeds(20, 16, 1, 64), 3, where_gt=499, distinct=True)
+    assert np.array_equal(np.sort(r.columns[0]), want)
+    assert r.edges_scanned == scanned
+    check_gold("go3_where499_distinct_s20", r.columns[0], r.edges_scanned)
+
+
+@pytest.mark.parametrize("k", [0, 900, 998])
+def test_where_thresholds_rmat20(rmat20, k):
+    """thresholds that keep almost every edge / leave rows pending past the bottom-up slab"""
+    sp, g = rmat20
+    starts = synth.seeds(20, 16, 1, 64)
+    for steps in (2, 3):
+        r = sp.go(starts, steps, FOLLOW, where=X.AliasProp("follow", "weight") > k,
+                  yields=[X.EdgeDst("follow")], distinct=True)
+        want, scanned = g.go(starts, steps, where_gt=k, distinct=True)
+        assert np.array_equal(np.sort(r.columns[0]), want)
+        assert r.edges_scanned == scanned
+
+
+def test_bench_query_rmat20_faithful_oracle(rmat20):
+    """the same query against the faithful storaged + graphd restatement (KV store, processors)"""
+    sp, _ = rmat20
+    st = O.Store(64)
+    st.set_edge_schema(FOLLOW, [("weight", O.INT)], name="follow")
+    st.load_rmat(20, 16, 1, FOLLOW)
+    starts = synth.seeds(20, 16, 1, 64)
+    r = st.go(starts, 3, FOLLOW, where=W499.encode(), yields=[X.EdgeDst("follow").encode()], distinct=True)
+    g = bench_query(sp, 20)
+    assert np.array_equal(np.sort(g.columns[0]), np.sort(r.int_col(0)))
+    assert g.edges_scanned == r.edges_scanned
+
+
+@pytest.fixture(scope="module")
+def rmat18():
+    sp = rmat_space(18)
+    g = O.RmatGraph(18, 16, 1)
+    yield sp, g
+    sp.close()
+
+
+@pytest.mark.parametrize("steps", [1, 2, 3])
+def test_plain_rows_rmat18(rmat18, steps):
+    """configs[1]'s shape (GO N STEPS, default YIELD _dst rows, no DISTINCT): every row"""
+    sp, g = rmat18
+    starts = synth.seeds(18, 16, 1, 64)
+    r = sp.go(starts, steps, FOLLOW)
+    want, scanned = g.go(starts, steps)
+    assert np.array_equal(np.sort(r.columns[0]), want)
+    assert r.edges_scanned == scanned
+    if steps == 3:
+        check_gold("go3_plain_s18", r.columns[0], r.edges_scanned)
+
+
+def test_shortest_path_1024_pairs_rmat18(rmat18):
+    """configs[3]'s shape: 1024 (src, dst) pairs, hops and canonical paths"""
+    sp, g = rmat18
+    s, t = synth.pairs(18, 16, 1, 1024)
+    r = sp.shortest_path(s, t, FOLLOW, 8)
+    hops, paths = g.shortest_path(s, t, 8)
+    assert np.array_equal(r.hops, hops)
+    for i in range(len(s)):
+        assert np.array_equal(r.paths[i], paths[i]), i
+    gold = GOLD["paths1024_s18"]
+    import hashlib
+    h = hashlib.sha256(np.asarray(r.hops, dtype="<i8").tobytes())
+    for p in r.paths:
+        h.update(np.asarray(p, dtype="<i8").tobytes())
+    assert h.hexdigest() == gold["sha256"]
+
+
+def test_configs1_rmat22_plain_digest():
+    """configs[1]: GO 3 STEPS FROM 64 seeds OVER follow on RMAT-22 (64 M rows), by digest"""
+    sp = rmat_space(22)
+    try:
+        r = sp.go(synth.seeds(22, 16, 1, 64), 3, FOLLOW)
+        check_gold("go3_plain_s22", r.columns[0], r.edges_scanned)
+        r = bench_query(sp, 22)
+        check_gold("go3_where499_distinct_s22", r.columns[0], r.edges_scanned)
+    finally:
+        sp.close()
+
+
+@pytest.mark.skipif("paths1024_s22" not in GOLD, reason="digest not generated")
+def test_configs3_rmat22_paths_digest():
+    sp = rmat_space(22)
+    try:
+        s, t = synth.pairs(22, 16, 1, 1024)
+        r = sp.shortest_path(s, t, FOLLOW, 8)
+        import hashlib
+        h = hashlib.sha256(np.asarray(r.hops, dtype="<i8").tobytes())
+        for p in r.paths:
+            h.update(np.asarray(p, dtype="<i8").tobytes())
+        assert h.hexdigest() == GOLD["paths1024_s22"]["sha256"]
+    finally:
+        sp.close()
+
+
+def test_configs2_rmat26_bench_query_digest():
+    """configs[2] at its size (the bench line's query on RMAT-26, 1 GPU), by digest; also the
+    shortest paths of configs[3] on the same graph when their digest is committed"""
+    sp = rmat_space(26)
+    try:
+        r = bench_query(sp, 26)
+        check_gold("go3_where499_distinct_s26", r.columns[0], r.edges_scanned)
+        if "paths1024_s26" in GOLD:
+            s, t = synth.pairs(26, 16, 1, 1024)
+            p = sp.shortest_path(s, t, FOLLOW, 8)
+            import hashlib
+            h = hashlib.sha256(np.asarray(p.hops, dtype="<i8").tobytes())
+            for q in p.paths:
+                h.update(np.asarray(q, dtype="<i8").tobytes())
+            assert h.hexdigest() == GOLD["paths1024_s26"]["sha256"]
+    finally:
+        sp.close()

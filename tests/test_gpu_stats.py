@@ -12,6 +12,7 @@ import pytest
 import fixtures as F
 import oracle as O
 from nebula_amd import AVG, COUNT, SUM, GetNeighborsRequest, GraphSpace, NbgError, PropDef, QueryStatsProcessor
+from nebula_amd.engine import IN_BOUND
 from nebula_amd import expr as X
 
 pytestmark = pytest.mark.gpu
@@ -138,3 +139,24 @@ def test_query_stats_processor_shape(qs):
     assert resp.failed_codes == []
     assert [n for n, _ in resp.schema] == ["col_4", "_dst"]
     assert resp.row == (4 * 210, 210)
+
+
+def test_query_stats_processor_in_bound():
+    """IN_BOUND: the request carries -edge_type (StorageClient.cpp:116) and is scanned as is
+    (QueryBaseProcessor.inl:39-40); QueryBoundTest's fixture has 5 in-edges x 3 versions each"""
+    sp = GraphSpace(6)
+    sp.set_edge_schema(F.EDGE_TYPE, F.qb_edge_schema())
+    for part, data in F.qb_kv_parts().items():
+        sp.load_part(part, data)
+    sp.finalize()
+    try:
+        parts, vids, _ = F.qb_request(False)
+        req_parts = {}
+        for p, v in zip(parts, vids):
+            req_parts.setdefault(p, []).append(v)
+        req = GetNeighborsRequest(0, req_parts, -F.EDGE_TYPE, return_columns=[(PropDef(O.EDGE, "_dst"), COUNT)])
+        resp = QueryStatsProcessor.instance(sp, IN_BOUND).process(req)
+        assert resp.failed_codes == []
+        assert resp.row == (30 * 5,)
+    finally:
+        sp.close()
