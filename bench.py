@@ -72,11 +72,16 @@ def pmc_traffic(workload: str, prefixes):
 
 # ---- CPU baseline -----------------------------------------------------------------------------
 def host_cpu():
-    """(usable cores of this process, cores of the machine, CPU model)"""
+    """(usable cores of this process, cores of the machine, CPU model).  The GPU box pins a
+    process's CPU share through OMP_NUM_THREADS (16 per GPU) while its affinity mask shows the
+    whole machine, so the share is the smaller of the two."""
     try:
         usable = len(os.sched_getaffinity(0))
     except AttributeError:
         usable = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        usable = min(usable, int(share))
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -99,35 +104,39 @@ def best_of(fn, reps=3):
     return best, out
 
 
-def cpu_baseline(scale: int, where_k: int, golden: dict):
+def cpu_baseline(scale: int, where_k: int, golden: dict, c1_scale: int = 16):
     """The oracle (oracle/refcpu.cpp: the CPU restatement of storaged + graphd over the
     reference's KV layout) timed on this host on a bounded sample, best of 3 after 1 warm-up:
       * faithful: 1 storaged host x max_handlers_per_req = 10 bucket threads, min 3 vertices per
         bucket (QueryBaseProcessor.cpp:9-10), graphd loop single-threaded (GraphFlags.cpp:19);
       * all-cores: the same with one bucket thread per usable core.
     Sample: the bench query's shape (GO 3 STEPS ... WHERE weight > k YIELD DISTINCT _dst, 64
-    seeds) and configs[0] (C1: GO 2 STEPS FROM 16 seeds) on RMAT-`scale`."""
+    seeds) on RMAT-`scale`, and configs[0] (C1: GO 2 STEPS FROM 16 seeds) on RMAT-`c1_scale`."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle as O
     from nebula_amd import expr as X
     from nebula_amd import synth
 
     usable, machine, model = host_cpu()
-    st = O.Store(64)
-    st.set_edge_schema(1, [("weight", O.INT)], name="follow")
-    t0 = time.perf_counter()
-    st.load_rmat(scale, 16, 1, 1, versions=1, threads=min(16, usable))
-    load_s = time.perf_counter() - t0
+    stores, load_s = {}, 0.0
+    for sc in sorted({scale, c1_scale}):
+        st = O.Store(64)
+        st.set_edge_schema(1, [("weight", O.INT)], name="follow")
+        t0 = time.perf_counter()
+        st.load_rmat(sc, 16, 1, 1, versions=1, threads=min(16, usable))
+        load_s += time.perf_counter() - t0
+        stores[sc] = st
     w = (X.AliasProp("follow", "weight") > where_k).encode()
     y = [X.EdgeDst("follow").encode()]
     cases = {
-        "c3_shape": dict(starts=synth.seeds(scale, 16, 1, 64), steps=3, where=w, yields=y, distinct=True,
-                         golden=f"go3_where{where_k}_distinct_s{scale}"),
-        "c1": dict(starts=synth.seeds(scale, 16, 1, 16), steps=2, where=b"", yields=(), distinct=False,
-                   golden=f"go2_plain_s{scale}"),
+        "c3_shape": dict(scale=scale, starts=synth.seeds(scale, 16, 1, 64), steps=3, where=w, yields=y,
+                         distinct=True, golden=f"go3_where{where_k}_distinct_s{scale}"),
+        "c1": dict(scale=c1_scale, starts=synth.seeds(c1_scale, 16, 1, 16), steps=2, where=b"", yields=(),
+                   distinct=False, golden=f"go2_plain_s{c1_scale}"),
     }
     res = {}
     for name, cs in cases.items():
+        st = stores[cs["scale"]]
         row = {}
         for mode, handlers in (("faithful", 10), ("all_cores", usable)):
             dt, r = best_of(lambda: st.go(cs["starts"], cs["steps"], 1, where=cs["where"], yields=cs["yields"],
@@ -154,8 +163,8 @@ def cpu_baseline(scale: int, where_k: int, golden: dict):
         "cpu_model": model,
         "faithful": {"c3_shape": c3["faithful"], "c1": res["c1"]["faithful"]},
         "all_cores": {"c3_shape": c3["all_cores"], "c1": res["c1"]["all_cores"]},
-        "config": {"scale": scale, "c3_shape": {k: c3[k] for k in ("edges_scanned", "rows", "parity")},
-                   "c1": {k: res["c1"][k] for k in ("edges_scanned", "rows", "parity")}},
+        "config": {"c3_shape": {"scale": scale, **{k: c3[k] for k in ("edges_scanned", "rows", "parity")}},
+                   "c1": {"scale": c1_scale, **{k: res["c1"][k] for k in ("edges_scanned", "rows", "parity")}}},
     }
 
 
@@ -302,7 +311,7 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
     }
     if not args.no_cpu and world == 1:
         try:
-            out["cpu_baseline"] = cpu_baseline_paths(args.cpu_scale, 64, args.max_steps)
+            out["cpu_baseline"] = cpu_baseline_paths(min(args.cpu_scale, 16), 64, args.max_steps)
         except Exception as e:
             out["cpu_baseline"] = {"error": str(e)}
     if rank == 0:
@@ -322,7 +331,7 @@ def main():
                     help="replace the first N seeds with the N highest-out-degree vertices (configs[4]: 8)")
     ap.add_argument("--where", type=int, default=499)
     ap.add_argument("--hops", type=int, default=3)
-    ap.add_argument("--cpu-scale", type=int, default=16)
+    ap.add_argument("--cpu-scale", type=int, default=18)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--option", action="append", default=[], help="engine option key=value")

@@ -166,6 +166,7 @@ struct Csr {
   int64_t nnz = 0;
   DevBuf row_ptr;   // int64 [n_rows+1]
   DevBuf col;       // int32 [nnz] global vertex index of the other end
+  DevBuf col_vid;   // int64 [nnz] vid of the other end (out CSR; rows path), or empty
   DevBuf rank;      // int64 [nnz] or empty (all zero)
   DevBuf row_part;  // int32 [n_rows]: the part holding the row's keys
   DevBuf row_ok;    // uint8 [n_rows] row_part == hash part; empty when all rows follow the rule
@@ -181,7 +182,7 @@ struct Csr {
   std::vector<PropCol> ov_props;
   DevBuf ov_prop_table;
   size_t bytes() const {
-    size_t b = row_ptr.bytes + col.bytes + rank.bytes + row_part.bytes + row_ok.bytes + ov_edge.bytes;
+    size_t b = row_ptr.bytes + col.bytes + col_vid.bytes + rank.bytes + row_part.bytes + row_ok.bytes + ov_edge.bytes;
     for (auto& p : props) b += p.data.bytes + p.present.bytes + p.str_off.bytes + p.str_bytes.bytes;
     for (auto& p : ov_props) b += p.data.bytes + p.present.bytes + p.str_off.bytes + p.str_bytes.bytes;
     return b;
@@ -224,6 +225,20 @@ struct EdgeSpace {
   DevBuf slab_col;                 // int32, -1 past the row's end
   std::vector<DevBuf> slab_props;  // per out prop with a transposed copy, same width
   DevBuf odeg;                     // uint32 [owned rows]: out-degree, 0 where row_ok == 0
+  // paired slab: the first 4 entries of every transposed row, row-major in two halves (slots
+  // 0-1 -> pair_col[0], slots 2-3 -> pair_col[1], 2 x int32 per row, -1 past the row's end),
+  // and the transposed INT-like props the same way (pair_props[h][field], 2 values per row)
+  DevBuf pair_col[2];
+  std::vector<DevBuf> pair_props[2];
+  // quantised predicate packing (bottom-up hops): the words of pair_col and tcol_q carry the
+  // source gidx in their low q_gbits bits and, above it, q_bits bits of the bucket of transposed
+  // prop q_field's value: bucket(v) = (v - q_min) * 2^q_bits / q_range (monotone), so a
+  // compare against a constant is decided from the bucket except in the one bucket holding the
+  // constant.  q_field < 0: words unpacked (plain gidx).  tcol_q: tr.col packed the same way.
+  int32_t q_field = -1, q_gbits = 0, q_bits = 0;
+  int64_t q_min = 0;
+  uint64_t q_range = 1;
+  DevBuf tcol_q;
 };
 
 // Vertex tag props: per tag, one row per vertex = the bytewise-first version under
@@ -324,6 +339,7 @@ struct Ctx {
   DevBuf ws_bits_xchg;  // world > 1: received mark segments [world][owned/32]
   DevBuf ws_starts;
   DevBuf ws_partials;  // per-block partial sums of the aggregated kernels
+  DevBuf ws_pend;      // deferred bottom-up rows: pending bits + compacted list
   // FIND SHORTEST PATH distance bytes [side][pair][owned row], kept 0xFF between calls, and
   // its tuple lists (kept across calls; allocated outside the query pool)
   DevBuf sp_dist[2];

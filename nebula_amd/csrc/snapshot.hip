@@ -9,6 +9,8 @@
 // Stage 2 (finalize): vertex set, vid<->gidx map, sort each rank's tuples into the reference's
 //   key order, keep the bytewise-first version of every (src, rank, dst)
 //   (QueryBaseProcessor.inl:349-362, P3), emit CSR + narrowed SoA property columns.
+#include <climits>
+
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_reduce.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -55,10 +57,12 @@ static void fill(Ctx& c, T* p, T v, int64_t n) {
   k_fill<T><<<grid_for(n), 256, 0, c.stream>>>(p, v, n);
 }
 
-static void grow_copy(Ctx& c, DevBuf& b, size_t need) {
+// grows b to at least `need` bytes keeping its contents: exactly `need` (the caller sized it), or
+// 1.25x the old size when that is larger (amortised appends of many small batches)
+static void grow_copy(Ctx& c, DevBuf& b, size_t need, bool exact = false) {
   if (need <= b.bytes) return;
   DevBuf nb;
-  nb.alloc(std::max(need, b.bytes * 2));
+  nb.alloc(exact ? need : std::max(need, b.bytes + b.bytes / 4));
   if (b.bytes) NBG_HIP(hipMemcpyAsync(nb.p, b.p, b.bytes, hipMemcpyDeviceToDevice, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
   b = std::move(nb);
@@ -107,20 +111,20 @@ static void stage_reserve(Ctx& c, Staging& s, size_t nfields, size_t extra, bool
   if (need <= s.cap) return;
   // 1.25x growth: a write batch appended behind a device-sized stage must not double it
   size_t cap = std::max(need, s.cap + s.cap / 4);
-  grow_copy(c, s.src, cap * 8);
-  grow_copy(c, s.dst, cap * 8);
-  grow_copy(c, s.rank, cap * 8);
-  grow_copy(c, s.ver, cap * 8);
-  grow_copy(c, s.part, cap * 4);
-  grow_copy(c, s.seq, cap * 8);
+  grow_copy(c, s.src, cap * 8, true);
+  grow_copy(c, s.dst, cap * 8, true);
+  grow_copy(c, s.rank, cap * 8, true);
+  grow_copy(c, s.ver, cap * 8, true);
+  grow_copy(c, s.part, cap * 4, true);
+  grow_copy(c, s.seq, cap * 8, true);
   if (with_props) {
     s.props.resize(nfields);
     s.present.resize(nfields);
     s.str_len.resize(nfields);
     for (size_t f = 0; f < nfields; f++) {
-      grow_copy(c, s.props[f], cap * 8);
-      grow_copy(c, s.present[f], cap);
-      if (fields[f].type == NBG_T_STRING) grow_copy(c, s.str_len[f], cap * 8);
+      grow_copy(c, s.props[f], cap * 8, true);
+      grow_copy(c, s.present[f], cap, true);
+      if (fields[f].type == NBG_T_STRING) grow_copy(c, s.str_len[f], cap * 8, true);
     }
   }
   s.cap = cap;
@@ -247,7 +251,8 @@ __global__ void k_decode_kv(const uint8_t* __restrict__ kb, const uint64_t* __re
                             const uint8_t* __restrict__ vb, const uint64_t* __restrict__ voff,
                             int64_t n, int32_t etype, int32_t sver, SchemaDev sch, int64_t heap_base,
                             int64_t seq0, StageOut outS, unsigned long long* out_cnt, StageOut inS,
-                            unsigned long long* in_cnt, unsigned long long* err) {
+                            unsigned long long* in_cnt, unsigned long long* err, int32_t req_part, int32_t parts,
+                            int32_t world, int32_t my_rank) {
   int64_t stride = int64_t(gridDim.x) * blockDim.x;
   int64_t n_rounds = (n + stride - 1) / stride;
   for (int64_t r = 0; r < n_rounds; r++) {
@@ -268,6 +273,9 @@ __global__ void k_decode_kv(const uint8_t* __restrict__ kb, const uint64_t* __re
           ver = ld_unaligned<int64_t>(k + 32);
           is_out = type == etype;
           is_in = !is_out;
+          // a part holds only keys of its own prefix, and with several ranks this rank can only
+          // host rows of the vertices it owns (err[2]: the whole batch is refused)
+          if (kpart != req_part || (world > 1 && dev_owner(src, parts, world) != my_rank)) atomicAdd(err + 2, 1ull);
         }
       }
     }
@@ -309,7 +317,7 @@ __global__ void k_decode_kv(const uint8_t* __restrict__ kb, const uint64_t* __re
 __global__ void k_decode_vkv(const uint8_t* __restrict__ kb, const uint64_t* __restrict__ koff,
                              const uint8_t* __restrict__ vb, const uint64_t* __restrict__ voff, int64_t n,
                              int32_t tag, int32_t sver, SchemaDev sch, int64_t heap_base, int64_t seq0,
-                             StageOut o, unsigned long long* cnt, unsigned long long* err) {
+                             StageOut o, unsigned long long* cnt, unsigned long long* err, int32_t req_part) {
   int64_t stride = int64_t(gridDim.x) * blockDim.x;
   int64_t n_rounds = (n + stride - 1) / stride;
   for (int64_t r = 0; r < n_rounds; r++) {
@@ -319,6 +327,7 @@ __global__ void k_decode_vkv(const uint8_t* __restrict__ kb, const uint64_t* __r
     int64_t so = wave_append(cnt, hit);
     if (!hit) continue;
     const uint8_t* k = kb + koff[i];
+    if (ld_unaligned<int32_t>(k) != req_part) atomicAdd(err + 2, 1ull);
     o.part[so] = ld_unaligned<int32_t>(k);
     o.src[so] = ld_unaligned<int64_t>(k + 4);
     o.ver[so] = ld_unaligned<int64_t>(k + 16);
@@ -375,6 +384,21 @@ static void decode_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
   c.heap_used += vbytes;
   DevBuf cnt;
   cnt.alloc(64);
+  // A RocksDB write batch for one part is all or nothing: remember where every stage ended, and
+  // on any refusal roll them (and the value heap) back.  The load sequence advances either way,
+  // so a later batch never reuses this one's numbers (identical-key order stays unambiguous).
+  struct Mark {
+    Staging* s;
+    int64_t n;
+  };
+  std::vector<Mark> marks;
+  for (auto& kvp : c.edges) {
+    marks.push_back(Mark{&kvp.second.out_stage, kvp.second.out_stage.n});
+    marks.push_back(Mark{&kvp.second.in_stage, kvp.second.in_stage.n});
+  }
+  for (auto& kvp : c.tags) marks.push_back(Mark{&kvp.second.stage, kvp.second.stage.n});
+  const size_t heap_mark = size_t(heap_base);
+  try {
   for (auto& kvp : c.edges) {
     EdgeSpace& es = kvp.second;
     size_t nf = es.fields.size();
@@ -392,15 +416,18 @@ static void decode_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
     StageOut si = stage_ptrs(es.in_stage, 0);
     k_decode_kv<<<grid_for(int64_t(n)), 256, 0, c.stream>>>(
         dk.as<uint8_t>(), dko.as<uint64_t>(), c.heap.as<uint8_t>() + heap_base, dvo.as<uint64_t>(),
-        int64_t(n), es.type, es.schema_ver, sch, heap_base, c.load_seq, so, d, si, d + 1, d + 2);
+        int64_t(n), es.type, es.schema_ver, sch, heap_base, c.load_seq, so, d, si, d + 1, d + 2, part, c.num_parts,
+        c.world, c.rank);
     NBG_HIP(hipGetLastError());
-    unsigned long long h[4];
-    NBG_HIP(hipMemcpyAsync(h, d, 32, hipMemcpyDeviceToHost, c.stream));
+    unsigned long long h[5];
+    NBG_HIP(hipMemcpyAsync(h, d, 40, hipMemcpyDeviceToHost, c.stream));
     NBG_HIP(hipStreamSynchronize(c.stream));
+    es.out_stage.n = int64_t(h[0]);  // the marks roll back a refused batch
+    es.in_stage.n = int64_t(h[1]);
     if (h[3] != 0)
       throw Error(NBG_E_UNSUPPORTED, "row schema version differs from the registered version");
-    es.out_stage.n = int64_t(h[0]);
-    es.in_stage.n = int64_t(h[1]);
+    if (h[4] != 0)
+      throw Error(NBG_E_PART_NOT_FOUND, "edge key of another part, or of a vertex another rank owns");
     es.out_stage.rank_const = es.out_stage.ver_const = false;
     es.in_stage.rank_const = es.in_stage.ver_const = false;
   }
@@ -416,13 +443,20 @@ static void decode_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
     NBG_HIP(hipMemcpyAsync(d, &ts.stage.n, 8, hipMemcpyHostToDevice, c.stream));
     k_decode_vkv<<<grid_for(int64_t(n)), 256, 0, c.stream>>>(
         dk.as<uint8_t>(), dko.as<uint64_t>(), c.heap.as<uint8_t>() + heap_base, dvo.as<uint64_t>(), int64_t(n),
-        ts.id, ts.schema_ver, sch, heap_base, c.load_seq, stage_ptrs(ts.stage, nf), d, d + 2);
+        ts.id, ts.schema_ver, sch, heap_base, c.load_seq, stage_ptrs(ts.stage, nf), d, d + 2, part);
     NBG_HIP(hipGetLastError());
-    unsigned long long h[4];
-    NBG_HIP(hipMemcpyAsync(h, d, 32, hipMemcpyDeviceToHost, c.stream));
+    unsigned long long h[5];
+    NBG_HIP(hipMemcpyAsync(h, d, 40, hipMemcpyDeviceToHost, c.stream));
     NBG_HIP(hipStreamSynchronize(c.stream));
-    if (h[3] != 0) throw Error(NBG_E_UNSUPPORTED, "tag row schema version differs from the registered version");
     ts.stage.n = int64_t(h[0]);
+    if (h[3] != 0) throw Error(NBG_E_UNSUPPORTED, "tag row schema version differs from the registered version");
+    if (h[4] != 0) throw Error(NBG_E_PART_NOT_FOUND, "vertex key of another part");
+  }
+  } catch (...) {
+    for (auto& m : marks) m.s->n = m.n;
+    c.heap_used = heap_mark;
+    c.load_seq += int64_t(n);
+    throw;
   }
   c.load_seq += int64_t(n);
   c.build_seconds += now_s() - t0;
@@ -470,6 +504,13 @@ static void reset_derived(Ctx& c) {
     es.slab_k = 0;
     es.slab_col.release();
     es.slab_props.clear();
+    es.tcol_q.release();
+    es.q_field = -1;
+    es.q_gbits = es.q_bits = 0;
+    for (int h = 0; h < 2; h++) {
+      es.pair_col[h].release();
+      es.pair_props[h].clear();
+    }
     es.odeg.release();
   }
   for (auto& kv : c.tags) {
@@ -496,6 +537,10 @@ void snapshot_write_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t
 
 void snapshot_commit(Ctx& c) {
   if (!c.finalized) {
+    // first finalize, or a retry after a commit whose rebuild failed half-way (e.g. E_NOMEM):
+    // whatever that attempt derived is dropped before building again
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    reset_derived(c);
     snapshot_finalize(c);
     return;
   }
@@ -825,6 +870,10 @@ __global__ void k_gather_u8(const uint8_t* in, const uint32_t* perm, uint8_t* ou
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
     out[i] = in[perm[i]];
 }
+__global__ void k_col_vid(const int32_t* col, const int64_t* vid_of, int64_t m, int64_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = vid_of[col[i]];
+}
 template <typename T>
 __global__ void k_narrow(const int64_t* in, T* out, int64_t m) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
@@ -946,6 +995,7 @@ static void gather_props(Ctx& c, Staging& s, const std::vector<Field>& fields, c
 // Builds one CSR from a staging area.  Returns after freeing the staging buffers.
 static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool with_props, Csr& out,
                       const uint32_t* byterank, bool consume = true) {
+  out = Csr();  // a commit retried after a failed build must not extend a half-built CSR
   int64_t n = s.n;
   int64_t lo = c.owned_lo(), hi = c.owned_hi();
   out.n_rows = hi - lo;
@@ -1117,6 +1167,13 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
   // col
   out.col.alloc(size_t(m) * 4 + 4);
   k_gather_i32<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(dstg.as<int32_t>(), kp, out.col.as<int32_t>(), int64_t(m));
+  // the out CSR's dst vids as a column of their own: a plain GO's rows (YIELD _dst) stream it
+  // instead of gathering vid_of[col[e]] (one random line per row)
+  if (with_props && c.opt("rows_vid_col", 1) && m) {
+    out.col_vid.alloc(size_t(m) * 8 + 8);
+    k_col_vid<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(out.col.as<int32_t>(), c.vid_of.as<int64_t>(), int64_t(m),
+                                                        out.col_vid.as<int64_t>());
+  }
   // rank
   if (!s.rank_const) {
     out.rank.alloc(size_t(m) * 8 + 8);
@@ -1145,8 +1202,8 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
     s.present.clear();
     s.str_len.clear();
     s.n = 0;
+    s.cap = 0;
   }
-  s.cap = 0;
 }
 
 __global__ void k_edge_src(const int64_t* row_ptr, int64_t n_rows, int32_t* esrc) {
@@ -1222,6 +1279,62 @@ __global__ void k_build_slab(const int64_t* trp, const T* src, int64_t n, int K,
   for (int64_t d = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; d < n; d += int64_t(gridDim.x) * blockDim.x) {
     const int64_t b = trp[d], e = trp[d + 1];
     for (int k = 0; k < K; k++) slab[size_t(k) * size_t(n) + size_t(d)] = b + k < e ? src[b + k] : none;
+  }
+}
+// min / max of a narrowed INT column (width 1/2/4/8)
+__global__ void k_minmax_w(const void* data, int w, int64_t m, long long* mm) {
+  long long lo = LLONG_MAX, hi = LLONG_MIN;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    long long v = w == 1 ? static_cast<const int8_t*>(data)[i]
+                : w == 2 ? static_cast<const int16_t*>(data)[i]
+                : w == 4 ? static_cast<const int32_t*>(data)[i]
+                         : static_cast<const int64_t*>(data)[i];
+    lo = v < lo ? v : lo;
+    hi = v > hi ? v : hi;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(mm, lo);
+    atomicMax(mm + 1, hi);
+  }
+}
+// the quantised bucket of v: floor((v - min) * 2^bits / range) (range 0 = 2^64)
+__host__ __device__ inline uint32_t q_bucket(int64_t v, int64_t vmin, uint64_t range, int bits) {
+  const unsigned __int128 d = (unsigned __int128)(uint64_t(v) - uint64_t(vmin)) << bits;
+  const unsigned __int128 r = range ? (unsigned __int128)range : ((unsigned __int128)1 << 64);
+  return uint32_t(d / r);
+}
+// packed transposed column: (bucket << gbits) | src gidx
+__global__ void k_pack_col(const int32_t* col, const void* data, int w, int64_t m, int64_t vmin, uint64_t range,
+                           int gbits, int qbits, int32_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t v = w == 1 ? static_cast<const int8_t*>(data)[i]
+                    : w == 2 ? static_cast<const int16_t*>(data)[i]
+                    : w == 4 ? static_cast<const int32_t*>(data)[i]
+                             : static_cast<const int64_t*>(data)[i];
+    out[i] = int32_t((q_bucket(v, vmin, range, qbits) << gbits) | uint32_t(col[i]));
+  }
+}
+// paired slab: row d's first 4 entries as two row-major halves (slots 0-1 in lo, 2-3 in hi)
+template <typename T>
+__global__ void k_build_pair(const int64_t* trp, const T* src, int64_t n, T* lo, T* hi, T none) {
+  for (int64_t d = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; d < n; d += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t b = trp[d], e = trp[d + 1];
+#pragma unroll
+    for (int q = 0; q < 4; q++) (q < 2 ? lo : hi)[size_t(d) * 2 + (q & 1)] = b + q < e ? src[b + q] : none;
+  }
+}
+static void build_pair_w(Ctx& c, const int64_t* trp, const void* src, int64_t n, void* lo, void* hi, int w) {
+  int g = grid_for(n);
+  switch (w) {
+    case 1: k_build_pair<int8_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int8_t*>(src), n, static_cast<int8_t*>(lo), static_cast<int8_t*>(hi), 0); break;
+    case 2: k_build_pair<int16_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int16_t*>(src), n, static_cast<int16_t*>(lo), static_cast<int16_t*>(hi), 0); break;
+    case 4: k_build_pair<int32_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int32_t*>(src), n, static_cast<int32_t*>(lo), static_cast<int32_t*>(hi), 0); break;
+    default: k_build_pair<int64_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int64_t*>(src), n, static_cast<int64_t*>(lo), static_cast<int64_t*>(hi), 0);
   }
 }
 static void build_slab_w(Ctx& c, const int64_t* trp, const void* src, int64_t n, int K, void* slab, int w) {
@@ -1425,6 +1538,60 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
       int w = t.props[f].width;
       es.slab_props[f].alloc(size_t(es.slab_k) * size_t(n_own) * size_t(w) + 16);
       if (n_own) build_slab_w(c, t.row_ptr.as<int64_t>(), t.props[f].data.p, n_own, es.slab_k, es.slab_props[f].p, w);
+    }
+  }
+  // the paired slab (k_bu_pair), packed with the quantised bucket of the first INT-like
+  // transposed prop when the gidx leaves >= 3 spare bits below bit 31
+  for (int h = 0; h < 2; h++) {
+    es.pair_col[h].release();
+    es.pair_props[h].clear();
+    es.pair_props[h].resize(o.props.size());
+  }
+  es.q_field = -1;
+  es.q_gbits = es.q_bits = 0;
+  es.tcol_q.release();
+  if (c.opt("bu_pair", 1) && c.opt("bu_pack", 1) && R > 0) {
+    int gb = 1;
+    while ((int64_t(1) << gb) < std::max<int64_t>(c.n_global, 2)) gb++;
+    const int qb = std::min(8, 31 - gb);
+    int f = -1;
+    for (size_t i = 0; i < t.props.size() && f < 0; i++)
+      if (t.props[i].data.p) f = int(i);
+    if (qb >= 3 && f >= 0) {
+      const PropCol& pc = t.props[size_t(f)];
+      DevBuf mm;
+      mm.alloc(16);
+      const long long init[2] = {LLONG_MAX, LLONG_MIN};
+      NBG_HIP(hipMemcpyAsync(mm.p, init, 16, hipMemcpyHostToDevice, c.stream));
+      k_minmax_w<<<grid_for(R), 256, 0, c.stream>>>(pc.data.p, pc.width, R, mm.as<long long>());
+      long long h[2];
+      NBG_HIP(hipMemcpyAsync(h, mm.p, 16, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      es.q_field = f;
+      es.q_gbits = gb;
+      es.q_bits = qb;
+      es.q_min = h[0];
+      es.q_range = uint64_t(h[1]) - uint64_t(h[0]) + 1;  // 0 = the whole 2^64 range
+      es.tcol_q.alloc(size_t(R) * 4 + 16);
+      k_pack_col<<<grid_for(R), 256, 0, c.stream>>>(t.col.as<int32_t>(), pc.data.p, pc.width, R, es.q_min, es.q_range,
+                                                   gb, qb, es.tcol_q.as<int32_t>());
+      NBG_HIP(hipGetLastError());
+    }
+  }
+  if (c.opt("bu_pair", 1)) {
+    for (int h = 0; h < 2; h++) es.pair_col[h].alloc(size_t(n_own) * 8 + 16);
+    const int32_t* src_col = es.q_field >= 0 ? es.tcol_q.as<int32_t>() : t.col.as<int32_t>();
+    if (n_own)
+      k_build_pair<int32_t><<<grid_for(n_own), 256, 0, c.stream>>>(t.row_ptr.as<int64_t>(), src_col, n_own,
+                                                                   es.pair_col[0].as<int32_t>(),
+                                                                   es.pair_col[1].as<int32_t>(), -1);
+    for (size_t f = 0; f < o.props.size(); f++) {
+      if (!t.props[f].data.p) continue;
+      const int w = t.props[f].width;
+      for (int h = 0; h < 2; h++) es.pair_props[h][f].alloc(size_t(n_own) * 2 * size_t(w) + 16);
+      if (n_own)
+        build_pair_w(c, t.row_ptr.as<int64_t>(), t.props[f].data.p, n_own, es.pair_props[0][f].p,
+                     es.pair_props[1][f].p, w);
     }
   }
   NBG_HIP(hipStreamSynchronize(c.stream));

@@ -344,6 +344,7 @@ struct ExpandArgs {
   int32_t mark_check;      // read the byte before storing it
   int64_t* out_vid;        // EXP_ROWS fused YIELD _dst: write vid_of[dst] instead of (src, edge)
   const int64_t* vid_of;
+  const int64_t* col_vid;  // per-edge dst vid (Csr::col_vid) or null: vid_of[col[e]]
 };
 struct FastArgs {
   const void* data;
@@ -353,7 +354,7 @@ struct FastArgs {
   int64_t k;
 };
 
-__device__ inline bool fast_cmp(int op, int64_t a, int64_t k) {
+__host__ __device__ inline bool fast_cmp(int op, int64_t a, int64_t k) {
   switch (op) {
     case 0: return a < k;
     case 1: return a <= k;
@@ -362,6 +363,31 @@ __device__ inline bool fast_cmp(int op, int64_t a, int64_t k) {
     case 4: return a == k;
     default: return a != k;
   }
+}
+
+// Quantised predicate on packed bottom-up words (EdgeSpace::q_*): the low gbits bits are the
+// source gidx, the bits above the bucket of the predicate column's value.  The compare decides
+// every bucket below ulo (`below`: 1 pass, 0 fail) and above uhi (`above`); buckets in
+// [ulo, uhi] hold the constant and need the exact value (-1).  Host-built per query
+// (make_qargs); all scalars, so the test is two compares, no table loads.  Unpacked words:
+// gmask all ones, ulo 0, uhi INT_MAX (every word undecided).
+struct QArgs {
+  uint32_t gmask = 0xffffffffu;
+  int32_t gbits = 0;
+  int32_t ulo = 0, uhi = INT32_MAX;
+  int32_t below = -1, above = -1;
+};
+__device__ inline int32_t q_gidx(int32_t s, const QArgs& q) { return s & int32_t(q.gmask); }
+// 1 pass, 0 fail, -1 undecided (load the value)
+__device__ inline int q_test(int32_t s, const QArgs& q) {
+  const int32_t b = int32_t(uint32_t(s) >> q.gbits);
+  return b < q.ulo ? q.below : (b > q.uhi ? q.above : -1);
+}
+
+// raw buffer resource over p (gfx9 word 3; bounds left to the caller): loads through it are
+// buffer instructions, which the compiler never merges with LDS reads into a flat load
+__device__ inline __amdgpu_buffer_rsrc_t raw_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
 }
 
 template <int MODE, int PK>
@@ -469,7 +495,10 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
           pass = as_bool(v);
         }
       }
-      if (MODE == EXP_MARK) {
+      if (MODE == EXP_ROWS && PK == PK_NONE && a.out_vid) {
+        // every edge is a row: the row of flattened edge e is row e (no append, no atomics)
+        if (valid) a.out_vid[e] = a.col_vid ? a.col_vid[ge] : a.vid_of[a.col[ge]];
+      } else if (MODE == EXP_MARK) {
         if (pass) {
           if (a.mark_check) {
             if (a.map[d] == 0) a.map[d] = 1;
@@ -483,7 +512,7 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
         if (valid) a.flags[e] = pass;
       }
     }
-    if (MODE == EXP_ROWS) {
+    if (MODE == EXP_ROWS && !(PK == PK_NONE && a.out_vid)) {
       // block-aggregated append: one returning atomic per tile (a single counter serialises at
       // ~90 appends / us, so a per-wave append made row output the bottleneck)
       const uint32_t c0 = __popc(pm);
@@ -515,7 +544,8 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
         int64_t rsk;
         locate(j, srck, rsk);
         if (a.out_vid) {
-          a.out_vid[pos] = a.vid_of[a.col[rsk + e0 + j]];
+          const int64_t ge = rsk + e0 + j;
+          a.out_vid[pos] = a.col_vid ? a.col_vid[ge] : a.vid_of[a.col[ge]];
         } else {
           a.rows_src[pos] = srck;
           a.rows_edge[pos] = rsk + e0 + j;
@@ -640,6 +670,126 @@ __global__ __launch_bounds__(1024) void k_reduce_partials(const unsigned long lo
   }
 }
 
+// The rests of a tile's rows: rows still pending after their slab slots scan [rb, re) of their
+// transposed row.  Long rests (> kLongRest entries) are scanned by the whole wave, 64 entries a
+// step; short ones by 16-lane groups, four rows at a time, so the tile's latency chain is paid
+// once per four pending rows instead of once per row.  Both stop at the row's first hit.
+template <int PK, int W, int R, typename InFront>
+__device__ inline void bu_rest_scan(const bool (&pend)[R], bool (&found)[R], const int64_t (&rb)[R],
+                                    const int64_t (&re)[R], const int32_t* __restrict__ tcol, const FastArgs& fp,
+                                    int ru, uint32_t (&acc)[6], InFront in_front, const QArgs& q) {
+  // entry test: frontier probe + predicate; a packed word settles the predicate from its bucket
+  // before the probe, else the value is read after a probe hit
+  auto entry = [&](int32_t raw, int64_t ex) -> bool {
+    const int32_t g = q_gidx(raw, q);
+    if (PK != PK_FAST) return in_front(g);
+    const int t = q_test(raw, q);
+    if (t == 0) return false;
+    if (!in_front(g)) return false;
+    if (t == 1) return true;
+    acc[5]++;
+    return fast_cmp(fp.op, load_w<W>(fp.data, fp.width, ex), fp.k);
+  };
+  const int lane = threadIdx.x & 63;
+  constexpr int kLongRest = 256, GL = 16, NG = 64 / GL;
+  unsigned long long pml[R], pms[R];
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    const bool lng = pend[j] && re[j] - rb[j] > kLongRest;
+    pml[j] = __ballot(lng);
+    pms[j] = __ballot(pend[j] && !lng);
+  }
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    unsigned long long pm = pml[j];
+    while (pm) {
+      const int src = __ffsll((long long)pm) - 1;
+      pm &= pm - 1;
+      const int64_t b = __shfl((long long)rb[j], src), e = __shfl((long long)re[j], src);
+      acc[3] += lane == 0;
+      bool f = false;
+      for (int64_t x = b; x < e && !f; x += 64 * ru) {
+        int32_t sr[kRestMax];
+#pragma unroll
+        for (int u = 0; u < kRestMax; u++) {
+          const int64_t ex = x + u * 64 + lane;
+          sr[u] = (u < ru && ex < e) ? tcol[ex] : -1;
+        }
+        bool h = false;
+#pragma unroll
+        for (int u = 0; u < kRestMax; u++) {
+          const int64_t ex = x + u * 64 + lane;
+          if (sr[u] < 0) continue;
+          acc[4]++;
+          if (entry(sr[u], ex)) h = true;
+        }
+        f = __ballot(h) != 0;
+      }
+      if (lane == src) found[j] = f;
+    }
+  }
+  {
+    const int grp = lane / GL, gl = lane % GL;
+    for (;;) {
+      int my_j = -1, my_src = 0, taken = 0;
+#pragma unroll
+      for (int j = 0; j < R; j++) {
+        while (pms[j] && taken < NG) {
+          const int sidx = __ffsll((long long)pms[j]) - 1;
+          if (taken == grp) {
+            my_j = j;
+            my_src = sidx;
+          }
+          pms[j] &= pms[j] - 1;
+          taken++;
+        }
+      }
+      if (taken == 0) break;
+      int64_t b = 0, e = 0;
+#pragma unroll
+      for (int j = 0; j < R; j++) {
+        const int64_t bj = __shfl((long long)rb[j], my_src), ej = __shfl((long long)re[j], my_src);
+        if (my_j == j) {
+          b = bj;
+          e = ej;
+        }
+      }
+      acc[3] += gl == 0 && my_j >= 0;
+      bool f = false;
+      for (int64_t x = b;; x += GL * ru) {
+        const bool act = !f && x < e;
+        if (__ballot(act) == 0) break;
+        bool h = false;
+        if (act) {
+          int32_t sr[kRestMax];
+#pragma unroll
+          for (int u = 0; u < kRestMax; u++) {
+            const int64_t ex = x + u * GL + gl;
+            sr[u] = (u < ru && ex < e) ? tcol[ex] : -1;
+          }
+#pragma unroll
+          for (int u = 0; u < kRestMax; u++) {
+            const int64_t ex = x + u * GL + gl;
+            if (sr[u] < 0) continue;
+            acc[4]++;
+            if (entry(sr[u], ex)) h = true;
+          }
+        }
+        const unsigned long long hb = __ballot(h);
+        if (act && ((hb >> (grp * GL)) & ((1ull << GL) - 1ull))) f = true;
+      }
+#pragma unroll
+      for (int g = 0; g < NG; g++) {
+        const int sj = __shfl(my_j, g * GL), ss = __shfl(my_src, g * GL);
+        const int fg = __shfl(int(f), g * GL);
+#pragma unroll
+        for (int j = 0; j < R; j++)
+          if (sj == j && lane == ss) found[j] = fg != 0;
+      }
+    }
+  }
+}
+
 // Bottom-up hop over the slab (first K hub-first entries of each transposed row, slot-major)
 // with a fallback scan of the rows' remaining entries; writes the next frontier as ballot words.
 // The hop is latency bound (each row is a chain slab -> frontier bit), so a wave owns tiles of
@@ -671,9 +821,12 @@ __global__ __launch_bounds__(256, WPE) void k_bu_slab(const int32_t* __restrict_
   extern __shared__ uint32_t s_fb[];
   for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
   if (cw) __syncthreads();
+  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
   auto in_front = [&](int32_t sv) -> bool {
-    const int32_t wi = sv >> 5;
-    const uint32_t w = wi < cw ? s_fb[wi] : fbits[wi];
+    const int32_t wi = sv >> 5;  // LDS and global reads kept apart (k_bu_quad's in_front)
+    uint32_t w;
+    if (wi < cw) w = s_fb[wi];
+    else w = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, wi * 4, 0, 0);
     return (w >> (sv & 31)) & 1u;
   };
   // per-lane counters (32-bit except the out-degree sum; widened for the block partials)
@@ -798,120 +951,7 @@ __global__ __launch_bounds__(256, WPE) void k_bu_slab(const int32_t* __restrict_
         if (rb[j] >= re[j]) pend[j] = false;
       }
     }
-    // Long rests (> kLongRest entries) are scanned by the whole wave, 64 entries a step; short
-    // ones by 16-lane groups, four rows at a time, so the tile's latency chain is paid once per
-    // four pending rows instead of once per row.  Both stop at the row's first hit.
-    constexpr int kLongRest = 256, GL = 16, NG = 64 / GL;
-    unsigned long long pml[R], pms[R];
-#pragma unroll
-    for (int j = 0; j < R; j++) {
-      const bool lng = pend[j] && re[j] - rb[j] > kLongRest;
-      pml[j] = __ballot(lng);
-      pms[j] = __ballot(pend[j] && !lng);
-    }
-#pragma unroll
-    for (int j = 0; j < R; j++) {
-      unsigned long long pm = pml[j];
-      while (pm) {
-        const int src = __ffsll((long long)pm) - 1;
-        pm &= pm - 1;
-        const int64_t b = __shfl((long long)rb[j], src), e = __shfl((long long)re[j], src);
-        acc[3] += lane == 0;
-        bool f = false;
-        for (int64_t x = b; x < e && !f; x += 64 * ru) {
-          int32_t sr[kRestMax];
-#pragma unroll
-          for (int u = 0; u < kRestMax; u++) {
-            const int64_t ex = x + u * 64 + lane;
-            sr[u] = (u < ru && ex < e) ? tcol[ex] : -1;
-          }
-          bool h = false;
-#pragma unroll
-          for (int u = 0; u < kRestMax; u++) {
-            const int64_t ex = x + u * 64 + lane;
-            if (sr[u] < 0) continue;
-            acc[4]++;
-            if (in_front(sr[u])) {
-              if (PK == PK_FAST) {
-                acc[5]++;
-                if (fast_cmp(fp.op, load_w<W>(fp.data, fp.width, ex), fp.k)) h = true;
-              } else {
-                h = true;
-              }
-            }
-          }
-          f = __ballot(h) != 0;
-        }
-        if (lane == src) found[j] = f;
-      }
-    }
-    {
-      const int grp = lane / GL, gl = lane % GL;
-      for (;;) {
-        int my_j = -1, my_src = 0, taken = 0;
-#pragma unroll
-        for (int j = 0; j < R; j++) {
-          while (pms[j] && taken < NG) {
-            const int sidx = __ffsll((long long)pms[j]) - 1;
-            if (taken == grp) {
-              my_j = j;
-              my_src = sidx;
-            }
-            pms[j] &= pms[j] - 1;
-            taken++;
-          }
-        }
-        if (taken == 0) break;
-        int64_t b = 0, e = 0;
-#pragma unroll
-        for (int j = 0; j < R; j++) {
-          const int64_t bj = __shfl((long long)rb[j], my_src), ej = __shfl((long long)re[j], my_src);
-          if (my_j == j) {
-            b = bj;
-            e = ej;
-          }
-        }
-        acc[3] += gl == 0 && my_j >= 0;
-        bool f = false;
-        for (int64_t x = b;; x += GL * ru) {
-          const bool act = !f && x < e;
-          if (__ballot(act) == 0) break;
-          bool h = false;
-          if (act) {
-            int32_t sr[kRestMax];
-#pragma unroll
-            for (int u = 0; u < kRestMax; u++) {
-              const int64_t ex = x + u * GL + gl;
-              sr[u] = (u < ru && ex < e) ? tcol[ex] : -1;
-            }
-#pragma unroll
-            for (int u = 0; u < kRestMax; u++) {
-              const int64_t ex = x + u * GL + gl;
-              if (sr[u] < 0) continue;
-              acc[4]++;
-              if (in_front(sr[u])) {
-                if (PK == PK_FAST) {
-                  acc[5]++;
-                  if (fast_cmp(fp.op, load_w<W>(fp.data, fp.width, ex), fp.k)) h = true;
-                } else {
-                  h = true;
-                }
-              }
-            }
-          }
-          const unsigned long long hb = __ballot(h);
-          if (act && ((hb >> (grp * GL)) & ((1ull << GL) - 1ull))) f = true;
-        }
-#pragma unroll
-        for (int g = 0; g < NG; g++) {
-          const int sj = __shfl(my_j, g * GL), ss = __shfl(my_src, g * GL);
-          const int fg = __shfl(int(f), g * GL);
-#pragma unroll
-          for (int j = 0; j < R; j++)
-            if (sj == j && lane == ss) found[j] = fg != 0;
-        }
-      }
-    }
+    bu_rest_scan<PK, W, R>(pend, found, rb, re, tcol, fp, ru, acc, in_front, QArgs{});
     // next frontier words
 #pragma unroll
     for (int j = 0; j < R; j++) {
@@ -923,6 +963,471 @@ __global__ __launch_bounds__(256, WPE) void k_bu_slab(const int32_t* __restrict_
       acc[0] += found[j];
       odsum += o;
     }
+  }
+  unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
+  block_store_partials(acc64, 6, lds, partials);
+}
+
+// spread the 32 bits of x to the even bit positions of a 64-bit word (scalar: x is wave-uniform)
+__device__ inline unsigned long long spread_even(unsigned long long x) {
+  x &= 0xffffffffull;
+  x = (x | (x << 16)) & 0x0000ffff0000ffffull;
+  x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
+  x = (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
+  x = (x | (x << 2)) & 0x3333333333333333ull;
+  x = (x | (x << 1)) & 0x5555555555555555ull;
+  return x;
+}
+// the two 64-row words of a 128-row unit whose rows 2l / 2l+1 sit in lane l (ballots e / o)
+__device__ inline void unit_words(unsigned long long e, unsigned long long o, unsigned long long& w0,
+                                  unsigned long long& w1) {
+  w0 = spread_even(e) | (spread_even(o) << 1);
+  w1 = spread_even(e >> 32) | (spread_even(o >> 32) << 1);
+}
+
+// Bottom-up hop over the quad slab: the first 4 hub-first in-neighbours of every transposed row
+// stored row-major in two halves (slots 0-1 and 2-3, 8 B per row each).  A lane owns two
+// adjacent rows, so each half arrives in one 16-byte load per lane (the streaming width the HBM
+// path needs: 8-byte loads held the kernel near 3 TB/s even with no probes at all).  With the
+// predicate column packed into the slot words (QP: EdgeSpace::q_*) a slot is decided from its
+// bucket without reading the value; a slot in the buckets holding the compare's constant makes
+// the row pending (the rest pass reads it); without packing the prop halves are loaded with the
+// slots (W bytes per slot).  The predicate is applied before any frontier probe, and a row's
+// probes carry no branches: hub words (the first cw bitmap words: vertices are numbered by
+// descending out-degree) from LDS, the others by buffer loads (non-candidates aim out of bounds).
+// Software pipelined: a wave issues the slab loads of its next unit before probing the current
+// one; R units of 128 rows per lane-iteration.  EH = 2 loads both halves eagerly; EH = 1 the
+// second half only for lanes with a row still pending after the first.  Rows pending after their
+// 4 slots: DEFER leaves a bit in pbits (k_bu_rest_words scans them), else the wave scans their
+// rests here (bu_rest_scan).  Outputs: the next frontier as 64-row words; partials as
+// k_bu_slab's ([3]: rows pending after the slots).
+template <int PK, int W, int QP, int R, int EH, int DEFER>
+__global__ __launch_bounds__(1024, 8) void k_bu_quad(
+    const uint2* __restrict__ slab_lo, const uint2* __restrict__ slab_hi, const void* __restrict__ w_lo,
+    const void* __restrict__ w_hi, const int64_t* __restrict__ trp, const int32_t* __restrict__ tcol, int64_t n,
+    const uint32_t* __restrict__ fbits, unsigned long long* __restrict__ nbits, const uint32_t* __restrict__ odeg,
+    FastArgs fp, QArgs q, unsigned long long* partials, int cw, int ru, unsigned long long* __restrict__ pbits) {
+  __shared__ unsigned long long lds[kSlots * 16];
+  extern __shared__ uint32_t s_fb[];
+  for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
+  auto in_front = [&](int32_t g) -> bool {
+    const int32_t wi = g >> 5;
+    uint32_t w;
+    if (wi < cw) w = s_fb[wi];
+    else w = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, wi * 4, 0, 0);
+    return (w >> (g & 31)) & 1u;
+  };
+  // predicate values of a half: 2 slots of W bytes in one load (unpacked words only)
+  using HW = typename std::conditional<W == 1, uint16_t,
+             typename std::conditional<W == 2, uint32_t, typename std::conditional<W == 4, uint2, uint4>::type>::type>::type;
+  auto wval = [](const HW& h, int k) -> int64_t {
+    if constexpr (W == 1) return int64_t(int8_t(k ? h >> 8 : h));
+    else if constexpr (W == 2) return int64_t(int16_t(k ? h >> 16 : h));
+    else if constexpr (W == 4) return int64_t(int32_t(k ? h.y : h.x));
+    else return k ? int64_t((uint64_t(h.w) << 32) | h.z) : int64_t((uint64_t(h.y) << 32) | h.x);
+  };
+  constexpr bool LOADW = PK == PK_FAST && !QP;
+  constexpr bool ODEG = PK == PK_NONE;  // non-final hops filter on out-degree
+  constexpr int RL = 2 * R;             // rows per lane
+  static_assert(EH == 2 || PK == PK_NONE, "the lazy second half is for predicate-free hops");
+  const int diag = int(fp.width >> 16);  // profiling only (bu_pair_diag): 1 no probes, 2 LDS probes only
+  // branch-free frontier probe of slot word sw (want: it is a candidate)
+  auto probe = [&](int32_t sw, bool want) -> bool {
+    if (diag & 1) return false;
+    const int32_t g = q_gidx(sw, q);
+    const int32_t wi = g >> 5;
+    const bool hub = wi < cw;
+    const uint32_t lw = s_fb[hub ? wi : 0];
+    const uint32_t gw = (diag & 2) ? 0u : __builtin_amdgcn_raw_buffer_load_b32(fb_rs, want && !hub ? uint32_t(wi) * 4u : 0xfffffff0u, 0, 0);
+    return want && (((hub ? lw : gw) >> (g & 31)) & 1u);
+  };
+  // is slot word sw (slot k of a row whose half values are h) a candidate?  QP: decided by the
+  // bucket; a slot in the constant's buckets is not, but sets `und`
+  auto want = [&](int32_t sw, bool live, int k, const HW& h, bool& und) -> bool {
+    if (!live || sw < 0) return false;
+    if (PK != PK_FAST) return true;
+    if (QP) {
+      const int t = q_test(sw, q);
+      und |= t < 0;
+      return t > 0;
+    }
+    return fast_cmp(fp.op, wval(h, k), fp.k);
+  };
+  const int lane = threadIdx.x & 63;
+  // row of slot j (j < RL) of a lane in unit-group t: unit j / 2, parity j % 2
+  auto row_of = [&](int64_t t, int j) -> int64_t { return (t * R + (j >> 1)) * 128 + 2 * lane + (j & 1); };
+  struct Tile {
+    uint4 lo[R], hi[R];  // rows 2l / 2l+1: .xy / .zw
+    HW wl[RL], wh[RL];
+    uint2 od[R];
+  };
+  const uint4 kNone = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+  auto load2 = [&](const uint2* base, int64_t d0) -> uint4 {
+    if (d0 + 1 < n) return reinterpret_cast<const uint4*>(base)[d0 >> 1];
+    if (d0 < n) {
+      const uint2 v = base[d0];
+      return make_uint4(v.x, v.y, 0xffffffffu, 0xffffffffu);
+    }
+    return kNone;
+  };
+  auto load_tile = [&](int64_t t, Tile& T) {
+#pragma unroll
+    for (int u = 0; u < R; u++) {
+      const int64_t d0 = row_of(t, 2 * u);
+      T.lo[u] = load2(slab_lo, d0);
+      T.hi[u] = EH == 2 ? load2(slab_hi, d0) : kNone;
+      if (ODEG && odeg) {
+        T.od[u] = make_uint2(0, 0);
+        if (d0 + 1 < n) T.od[u] = reinterpret_cast<const uint2*>(odeg)[d0 >> 1];
+        else if (d0 < n) T.od[u].x = odeg[d0];
+      } else {
+        T.od[u] = make_uint2(1, 1);
+      }
+      if (LOADW) {
+#pragma unroll
+        for (int p = 0; p < 2; p++) {
+          if (d0 + p < n) {
+            T.wl[2 * u + p] = static_cast<const HW*>(w_lo)[d0 + p];
+            T.wh[2 * u + p] = static_cast<const HW*>(w_hi)[d0 + p];
+          }
+        }
+      }
+    }
+  };
+  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long odsum = 0;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  const int64_t ntiles = (n + 128 * R - 1) / (128 * R);
+  Tile cur;
+  if (wave < ntiles) load_tile(wave, cur);
+  for (int64_t t = wave; t < ntiles; t += nwaves) {
+    Tile nxt;
+    if (t + nwaves < ntiles) load_tile(t + nwaves, nxt);  // in flight while this unit probes
+    int64_t d[RL];
+    bool found[RL], pend[RL], und[RL];
+    uint32_t od[RL];
+#pragma unroll
+    for (int j = 0; j < RL; j++) {
+      const int u = j >> 1, p = j & 1;
+      d[j] = row_of(t, j);
+      od[j] = p ? cur.od[u].y : cur.od[u].x;
+      // a non-final hop keeps only vertices with out-edges (they alone extend the frontier; an
+      // all-zero-degree frontier ends the query either way, P17): other rows are not probed
+      const bool live = d[j] < n && od[j] > 0;
+      if (d[j] < n) acc[2] += EH == 2 ? 4 : 2;
+      const int32_t s0 = int32_t(p ? cur.lo[u].z : cur.lo[u].x), s1 = int32_t(p ? cur.lo[u].w : cur.lo[u].y);
+      const int32_t s2 = int32_t(p ? cur.hi[u].z : cur.hi[u].x), s3 = int32_t(p ? cur.hi[u].w : cur.hi[u].y);
+      bool uu = false;
+      const bool w0 = want(s0, live, 0, cur.wl[j], uu), w1 = want(s1, live, 1, cur.wl[j], uu);
+      const bool w2 = EH == 2 && want(s2, live, 0, cur.wh[j], uu), w3 = EH == 2 && want(s3, live, 1, cur.wh[j], uu);
+      found[j] = (int(probe(s0, w0)) | int(probe(s1, w1)) | int(EH == 2 && probe(s2, w2)) |
+                  int(EH == 2 && probe(s3, w3))) != 0;
+      und[j] = uu;
+      pend[j] = live && !found[j] && ((EH == 2 ? s3 >= 0 : s1 >= 0) || uu);
+    }
+    if (EH == 1) {
+      bool anyp = false;
+#pragma unroll
+      for (int j = 0; j < RL; j++) anyp |= pend[j];
+      if (__ballot(anyp)) {
+        uint4 hi[R];
+#pragma unroll
+        for (int u = 0; u < R; u++)
+          if (pend[2 * u] || pend[2 * u + 1]) hi[u] = load2(slab_hi, d[2 * u]);
+#pragma unroll
+        for (int j = 0; j < RL; j++) {
+          if (!pend[j]) continue;
+          const int u = j >> 1, p = j & 1;
+          acc[2] += 2;
+          const int32_t s2 = int32_t(p ? hi[u].z : hi[u].x), s3 = int32_t(p ? hi[u].w : hi[u].y);
+          found[j] = (int(probe(s2, s2 >= 0)) | int(probe(s3, s3 >= 0))) != 0;
+          pend[j] = !found[j] && s3 >= 0;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RL; j++) acc[3] += pend[j];
+    if (DEFER) {
+#pragma unroll
+      for (int u = 0; u < R; u++) {
+        unsigned long long w0, w1;
+        unit_words(__ballot(pend[2 * u]), __ballot(pend[2 * u + 1]), w0, w1);
+        const int64_t d0 = (t * R + u) * 128;
+        if (lane == 0 && d0 < n) pbits[d0 >> 6] = w0;
+        if (lane == 1 && d0 + 64 < n) pbits[(d0 >> 6) + 1] = w1;
+      }
+    } else {
+      int64_t rb[RL], re[RL];
+#pragma unroll
+      for (int j = 0; j < RL; j++) {
+        rb[j] = re[j] = 0;
+        if (pend[j]) {
+          rb[j] = trp[d[j]] + (und[j] ? 0 : 4);
+          re[j] = trp[d[j] + 1];
+          if (rb[j] >= re[j]) pend[j] = false;
+        }
+      }
+      const uint32_t a3 = acc[3];
+      bu_rest_scan<PK, W, RL>(pend, found, rb, re, tcol, fp, ru, acc, in_front, q);
+      acc[3] = a3;
+    }
+#pragma unroll
+    for (int u = 0; u < R; u++) {
+      unsigned long long w0, w1;
+      unit_words(__ballot(found[2 * u]), __ballot(found[2 * u + 1]), w0, w1);
+      const int64_t d0 = (t * R + u) * 128;
+      if (lane == 0 && d0 < n) nbits[d0 >> 6] = w0;
+      if (lane == 1 && d0 + 64 < n) nbits[(d0 >> 6) + 1] = w1;
+    }
+#pragma unroll
+    for (int j = 0; j < RL; j++) {
+      acc[0] += found[j];
+      if (ODEG && odeg && found[j]) odsum += od[j];
+    }
+    cur = nxt;
+  }
+  unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
+  block_store_partials(acc64, 6, lds, partials);
+}
+
+// Deferred quad hop as a D-deep software pipeline (k_bu_quad's work for DEFER, EH = 2, no
+// eager prop halves).  Vector-memory loads complete in issue order, so a wave that refills its
+// tile registers before probing waits for the refill along with the probes: here each tile's
+// probes are issued first, then the tile D steps ahead is loaded into the registers just
+// consumed, then the probe results are used, so D - 1 tiles of slab loads stay in flight behind
+// every probe round.  Two adjacent rows per lane (16-byte loads of each half).
+template <int PK, int QP, int D>
+__global__ __launch_bounds__(1024, 4) void k_bu_ring(
+    const uint2* __restrict__ slab_lo, const uint2* __restrict__ slab_hi, int64_t n,
+    const uint32_t* __restrict__ fbits, unsigned long long* __restrict__ nbits, const uint32_t* __restrict__ odeg,
+    QArgs q, unsigned long long* partials, int cw, unsigned long long* __restrict__ pbits, int diag) {
+  __shared__ unsigned long long lds[kSlots * 16];
+  extern __shared__ uint32_t s_fb[];
+  for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
+  constexpr bool ODEG = PK == PK_NONE;
+  const int lane = threadIdx.x & 63;
+  struct Tile {
+    uint4 lo, hi;  // rows 2l / 2l+1: .xy / .zw
+    uint2 od;
+  };
+  const uint4 kNone = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
+  auto load2 = [&](const uint2* base, int64_t d0) -> uint4 {
+    if (d0 + 1 < n) return reinterpret_cast<const uint4*>(base)[d0 >> 1];
+    if (d0 < n) {
+      const uint2 v = base[d0];
+      return make_uint4(v.x, v.y, 0xffffffffu, 0xffffffffu);
+    }
+    return kNone;
+  };
+  auto load_tile = [&](int64_t t, Tile& T) {
+    const int64_t d0 = t * 128 + 2 * lane;
+    T.lo = load2(slab_lo, d0);
+    T.hi = load2(slab_hi, d0);
+    T.od = make_uint2(1, 1);
+    if (ODEG && odeg) {
+      T.od = make_uint2(0, 0);
+      if (d0 + 1 < n) T.od = reinterpret_cast<const uint2*>(odeg)[d0 >> 1];
+      else if (d0 < n) T.od.x = odeg[d0];
+    }
+  };
+  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long odsum = 0;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  const int64_t ntiles = (n + 127) / 128;
+  Tile ring[D];
+#pragma unroll
+  for (int k = 0; k < D; k++)
+    if (wave + k * nwaves < ntiles) load_tile(wave + k * nwaves, ring[k]);
+  for (int64_t t0 = wave; t0 < ntiles; t0 += D * nwaves) {
+#pragma unroll
+    for (int k = 0; k < D; k++) {
+      const int64_t t = t0 + k * nwaves;
+      if (t >= ntiles) break;
+      // probes of the tile's 8 slots: word index, bit, candidate flag, raw words
+      uint32_t word[8], bit[8], cand = 0, und = 0, has4 = 0, live = 0;
+      uint32_t od[2];
+#pragma unroll
+      for (int p = 0; p < 2; p++) {
+        const int64_t d = t * 128 + 2 * lane + p;
+        od[p] = p ? ring[k].od.y : ring[k].od.x;
+        const bool lv = d < n && od[p] > 0;
+        live |= uint32_t(lv) << p;
+        const int32_t sw[4] = {int32_t(p ? ring[k].lo.z : ring[k].lo.x), int32_t(p ? ring[k].lo.w : ring[k].lo.y),
+                               int32_t(p ? ring[k].hi.z : ring[k].hi.x), int32_t(p ? ring[k].hi.w : ring[k].hi.y)};
+        has4 |= uint32_t(sw[3] >= 0) << p;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          bool w = lv && sw[j] >= 0;
+          if (PK == PK_FAST) {
+            const int tq = q_test(sw[j], q);
+            if (w && tq < 0) und |= 1u << p;
+            w = w && tq > 0;
+          }
+          const int32_t g = q_gidx(sw[j], q);
+          const int32_t wi = g >> 5;
+          const bool hub = wi < cw;
+          bit[4 * p + j] = uint32_t(g & 31) | (hub ? 32u : 0u);
+          cand |= uint32_t(w) << (4 * p + j);
+          if (diag & 1) {
+            word[4 * p + j] = 0;
+          } else {
+            const uint32_t lw = s_fb[hub ? wi : 0];
+            const uint32_t gw = (diag & 2) ? 0u : __builtin_amdgcn_raw_buffer_load_b32(fb_rs, w && !hub ? uint32_t(wi) * 4u : 0xfffffff0u, 0, 0);
+            word[4 * p + j] = hub ? lw : gw;
+          }
+        }
+      }
+      // refill this slot of the ring (issued after the probes: they do not wait for it)
+      if (t + D * nwaves < ntiles) load_tile(t + D * nwaves, ring[k]);
+      bool found[2], pend[2];
+#pragma unroll
+      for (int p = 0; p < 2; p++) {
+        bool f = false;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int e = 4 * p + j;
+          f |= ((cand >> e) & 1u) && ((word[e] >> (bit[e] & 31u)) & 1u);
+        }
+        found[p] = f;
+        pend[p] = ((live >> p) & 1u) && !f && (((has4 >> p) & 1u) || ((und >> p) & 1u));
+        const int64_t d = t * 128 + 2 * lane + p;
+        if (d < n) acc[2] += 4;
+        acc[0] += f;
+        acc[3] += pend[p];
+        if (ODEG && odeg && f) odsum += od[p];
+      }
+      unsigned long long w0, w1;
+      const int64_t d0 = t * 128;
+      unit_words(__ballot(pend[0]), __ballot(pend[1]), w0, w1);
+      if (lane == 0 && d0 < n) pbits[d0 >> 6] = w0;
+      if (lane == 1 && d0 + 64 < n) pbits[(d0 >> 6) + 1] = w1;
+      unit_words(__ballot(found[0]), __ballot(found[1]), w0, w1);
+      if (lane == 2 && d0 < n) nbits[d0 >> 6] = w0;
+      if (lane == 3 && d0 + 64 < n) nbits[(d0 >> 6) + 1] = w1;
+    }
+  }
+  unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
+  block_store_partials(acc64, 6, lds, partials);
+}
+
+// Second pass of a deferred quad hop, straight from the pending bits (no list, no global
+// atomics): a wave owns 64 consecutive pbits words (4096 rows), ranks their pending rows (wave
+// prefix sum of the words' popcounts), and scans them 64 at a time, lane per row, in chunks of
+// kLaneChunk entries of the (packed) transposed column: the chunk's loads are independent, a
+// packed word settles the predicate from its bucket (the value is read only in the constant's
+// bucket); at most kLaneSteps chunks, then bu_rest_scan for long rests.  Found rows OR into the
+// wave's 64 next-frontier words in LDS, which the owning lanes merge into nbits (one writer per
+// word).  A row's scan starts at entry rest_from (4: its quad slots are settled; 0 with the
+// quantised predicate, whose undecided slots are read here).  Partials as k_bu_quad's (the
+// pending rows were counted there).
+constexpr int kLaneChunk = 8;
+constexpr int kLaneSteps = 4;
+template <int PK, int W, int OCC>
+__global__ __launch_bounds__(1024, OCC) void k_bu_rest_words(const unsigned long long* __restrict__ pbits, int64_t n,
+                                                           const int64_t* __restrict__ trp,
+                                                           const int32_t* __restrict__ tcol,
+                                                           const uint32_t* __restrict__ fbits, unsigned long long* nbits,
+                                                           const uint32_t* __restrict__ odeg, FastArgs fp, QArgs q,
+                                                           unsigned long long* partials, int cw, int ru,
+                                                           int rest_from) {
+  __shared__ unsigned long long lds[kSlots * 16];
+  __shared__ unsigned long long s_found[16][64];
+  extern __shared__ uint32_t s_fb[];
+  for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
+  __syncthreads();
+  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
+  auto in_front = [&](int32_t g) -> bool {
+    // hub words from the LDS copy (ds_read), the rest by a buffer load: two plain loads would be
+    // merged into one flat load (select of the pointers), which takes the texture path for LDS
+    // addresses too and waits on both counters
+    const int32_t wi = g >> 5;
+    uint32_t w;
+    if (wi < cw) w = s_fb[wi];
+    else w = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, wi * 4, 0, 0);
+    return (w >> (g & 31)) & 1u;
+  };
+  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long odsum = 0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nwords = (n + 63) / 64;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t cbase = wave * 64; cbase < nwords; cbase += nwaves * 64) {
+    const int64_t myw = cbase + lane;
+    const unsigned long long pw = myw < nwords ? pbits[myw] : 0ull;
+    s_found[wv][lane] = 0ull;
+    uint32_t total;
+    const uint32_t pre = wave_excl_scan(uint32_t(__popcll(pw)), total);
+    for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+      // the (k0 + lane)-th pending row of the chunk: its word (binary search over the lanes'
+      // exclusive prefix sums) and the matching set bit of that word
+      const uint32_t p = k0 + uint32_t(lane);
+      bool pend[1] = {p < total}, found[1] = {false};
+      int64_t rb[1] = {0}, re[1] = {0};
+      int wsel = 0;
+      {
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1) {
+          const uint32_t pv = __shfl(pre, wsel + st);
+          if (wsel + st < 64 && pv <= p) wsel += st;
+        }
+      }
+      const unsigned long long wbits = __shfl((long long)pw, wsel);
+      const uint32_t kk = p - __shfl(pre, wsel);  // the kk-th set bit of wbits
+      int bit = 0;
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1)
+        if (uint32_t(__popcll(wbits & ((1ull << (bit + st)) - 1ull))) <= kk) bit += st;
+      const int32_t r = int32_t((cbase + wsel) * 64 + bit);
+      if (pend[0]) {
+        rb[0] = trp[r] + rest_from;
+        re[0] = trp[r + 1];
+        pend[0] = rb[0] < re[0];
+      }
+      for (int step = 0; step < kLaneSteps; step++) {
+        if (__ballot(pend[0]) == 0) break;
+        if (pend[0]) {
+          int32_t sv[kLaneChunk];
+#pragma unroll
+          for (int k = 0; k < kLaneChunk; k++) sv[k] = rb[0] + k < re[0] ? tcol[rb[0] + k] : -1;
+          int hit = 0;
+#pragma unroll
+          for (int k = 0; k < kLaneChunk; k++) {
+            if (sv[k] < 0) continue;
+            acc[4]++;
+            const int tq = PK == PK_FAST ? q_test(sv[k], q) : 1;
+            if (tq == 0 || !in_front(q_gidx(sv[k], q))) continue;
+            if (tq == 1) {
+              hit = 1;
+              continue;
+            }
+            acc[5]++;  // the value is read only after a frontier hit, in the constant's bucket
+            hit |= int(fast_cmp(fp.op, load_w<W>(fp.data, fp.width, rb[0] + k), fp.k));
+          }
+          rb[0] += kLaneChunk;
+          if (hit) found[0] = true;
+          pend[0] = !hit && rb[0] < re[0];
+        }
+      }
+      const uint32_t a3 = acc[3];
+      bu_rest_scan<PK, W, 1>(pend, found, rb, re, tcol, fp, ru, acc, in_front, q);
+      acc[3] = a3;  // the pending rows were counted by the first pass
+      if (found[0]) {
+        atomicOr(&s_found[wv][wsel], 1ull << (r & 63));
+        acc[0]++;
+        if (odeg) odsum += odeg[r];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long fw = s_found[wv][lane];
+    if (fw) nbits[myw] |= fw;
+    __builtin_amdgcn_wave_barrier();
   }
   unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
   block_store_partials(acc64, 6, lds, partials);
@@ -1786,6 +2291,205 @@ int launch_bu_slab(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
   NBG_HIP(hipGetLastError());
   return grid;
 }
+// The per-query bucket masks of a packed predicate column (EdgeSpace::q_*): bucket b holds the
+// values min + [ceil(b * range / 2^bits), ceil((b + 1) * range / 2^bits) - 1]; it passes (fails)
+// when every value in it passes (fails) the compare, else the kernels read the exact value.
+QArgs make_qargs(const EdgeSpace& es, int pk, int fcol, const FastArgs& fp) {
+  QArgs q;
+  if (es.q_field < 0) return q;
+  q.gmask = (1u << es.q_gbits) - 1u;
+  q.gbits = es.q_gbits;
+  if (pk != PK_FAST || fcol != es.q_field) return q;  // packed words, every value read
+  using u128 = unsigned __int128;
+  const u128 R = es.q_range ? u128(es.q_range) : (u128(1) << 64);
+  const int bits = es.q_bits, nb = 1 << bits;
+  auto edge = [&](uint64_t b) -> u128 { return ((u128(b) * R) + ((u128(1) << bits) - 1)) >> bits; };  // ceil
+  // per bucket: 1 pass, 0 fail, -1 undecided, 2 empty (no value lands there: either answer)
+  std::vector<int> dec(size_t(nb), 2);
+  for (int b = 0; b < nb; b++) {
+    const u128 o0 = edge(uint64_t(b)), o1 = edge(uint64_t(b) + 1);
+    if (o0 >= o1) continue;
+    const int64_t lo = int64_t(uint64_t(es.q_min) + uint64_t(o0));
+    const int64_t hi = int64_t(uint64_t(es.q_min) + uint64_t(o1 - 1));
+    const int64_t k = fp.k;
+    bool pass, fail;
+    if (fp.op == 4) {  // ==
+      pass = lo == k && hi == k;
+      fail = k < lo || k > hi;
+    } else if (fp.op == 5) {  // !=
+      pass = k < lo || k > hi;
+      fail = lo == k && hi == k;
+    } else {  // monotone compares: both ends decide the bucket
+      const bool x = fast_cmp(fp.op, lo, k), z = fast_cmp(fp.op, hi, k);
+      pass = x && z;
+      fail = !x && !z;
+    }
+    dec[size_t(b)] = pass ? 1 : fail ? 0 : -1;
+  }
+  // below: the first non-empty bucket's answer, up to the first bucket answering otherwise;
+  // above: the last one's, down to the last bucket answering otherwise; between: undecided
+  int first = 2, last = 2;
+  for (int b = 0; b < nb && first == 2; b++) first = dec[size_t(b)];
+  for (int b = nb - 1; b >= 0 && last == 2; b--) last = dec[size_t(b)];
+  if (first == 2) return q;  // no values at all
+  int ulo = nb, uhi = nb - 1;
+  for (int b = 0; b < nb; b++)
+    if (dec[size_t(b)] != 2 && dec[size_t(b)] != first) {
+      ulo = b;
+      break;
+    }
+  for (int b = nb - 1; b >= 0; b--)
+    if (dec[size_t(b)] != 2 && dec[size_t(b)] != last) {
+      uhi = b;
+      break;
+    }
+  q.ulo = ulo;
+  q.uhi = ulo == nb ? nb - 1 : uhi;
+  q.below = first;
+  q.above = ulo == nb ? first : last;
+  return q;
+}
+
+// bottom-up hop over the quad slab (k_bu_quad): persistent grid of 2 x 1024-thread blocks per
+// CU, each with an LDS copy of the frontier bitmap's first bu_pair_lds_kb KiB (the hubs).
+// Deferred (bu_pair_defer for a non-final hop, bu_pair_defer_final for the final one) the rows
+// pending after their 4 slots are left as bits and scanned by k_bu_rest_words, so the first pass
+// is one load -> probe round per tile.  Launches the kernels and the partials reduction into
+// out[0..8) (no synchronisation).
+int launch_bu_pair(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
+                   const FastArgs& fp, int fcol, unsigned long long* out, hipEvent_t after_kernel = nullptr) {
+  const Csr& tr = es.tr;
+  const bool fast = pk == PK_FAST;
+  const int EH = fast ? 2 : int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_pair_eh", 1), 2)));
+  bool defer = c.opt(odeg ? "bu_pair_defer" : "bu_pair_defer_final", 1) != 0;
+  const QArgs q = make_qargs(es, pk, fcol, fp);
+  const bool QP = fast && q.gbits && fcol == es.q_field && c.opt("bu_qpred", 1) != 0;
+  // 128-row units per lane-iteration (2 rows per lane each): 1 with eager prop halves
+  // (registers), else bu_pair_r (1 or 2)
+  const int R = fast && !QP ? 1 : int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_pair_r", 1), 2)));
+  unsigned long long* partials = c.ws_partials.as<unsigned long long>();
+  const int64_t fb_words = (c.n_global + 31) / 32;
+  const int cw = int(std::min<int64_t>(c.opt("bu_pair_lds_kb", 64) * 256, std::min<int64_t>(fb_words, 38 * 1024)));
+  const int64_t tiles = (tr.n_rows + 128 * R - 1) / (128 * R);
+  const int64_t waves_per_block = 16;
+  const int64_t gcap = std::min<int64_t>(c.opt("bu_pair_grid", 512), kAggBlocks / 2);
+  const int grid = int(std::max<int64_t>(1, std::min<int64_t>((tiles + waves_per_block - 1) / waves_per_block, gcap)));
+  int g1 = grid;  // blocks of the first pass (their partials come first)
+  const uint2* lo = es.pair_col[0].as<uint2>();
+  const uint2* hi = es.pair_col[1].as<uint2>();
+  const void* wlo = fast && fcol >= 0 ? es.pair_props[0][size_t(fcol)].p : nullptr;
+  const void* whi = fast && fcol >= 0 ? es.pair_props[1][size_t(fcol)].p : nullptr;
+  if (fast && !wlo) throw Error(NBG_E_DEVICE, "quad slab without the predicate column");
+  const int64_t* trp = tr.row_ptr.as<int64_t>();
+  const int32_t* tc = q.gbits ? es.tcol_q.as<int32_t>() : tr.col.as<int32_t>();
+  auto* nb = reinterpret_cast<unsigned long long*>(nbits);
+  const int ru = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_unroll", 1), kRestMax)));
+  const size_t shm = size_t(std::max(cw, 1)) * 4;  // s_fb[0] is read (unused) when cw = 0
+  unsigned long long* pbits = nullptr;
+  if (defer) {
+    c.ws_pend.ensure(size_t((tr.n_rows + 63) / 64 + 1) * 8);
+    pbits = c.ws_pend.as<unsigned long long>();
+  }
+  auto big_lds = [&](auto kern) {
+    if (shm > 48 * 1024)
+      NBG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(shm)));
+  };
+  FastArgs fpd = fp;
+  fpd.width |= int32_t(c.opt("bu_pair_diag", 0) & 3) << 16;
+  auto go = [&](auto kern) {
+    big_lds(kern);
+    kern<<<grid, 1024, shm, c.stream>>>(lo, hi, wlo, whi, trp, tc, tr.n_rows, fb, nb, odeg, fpd, q, partials, cw, ru,
+                                        pbits);
+  };
+  int grid2 = 0;
+  const bool occ4 = c.opt("bu_rest_occ", 8) == 4;  // 128-VGPR rest pass: no spills, half the waves
+  auto rest = [&](auto kern) {
+    if (!defer) return;
+    big_lds(kern);
+    grid2 = int(std::min<int64_t>(c.opt("bu_rest_grid", 512), kAggBlocks / 2));
+    // partials of the second pass sit behind the first pass's blocks: one reduction adds both
+    kern<<<grid2, 1024, shm, c.stream>>>(pbits, tr.n_rows, trp, tc, fb, nb, odeg, fp, q, partials + g1, cw, ru,
+                                         QP ? 0 : 4);
+  };
+  // the pipelined deferred kernel (k_bu_ring) for predicate-free and packed-predicate hops
+  const int ring_d = int(c.opt("bu_ring", 3));
+  const bool ring = defer && ring_d > 0 && (!fast || QP);
+  // one 1024-thread block per CU (4 waves per SIMD: the registers of D tiles in flight), so a
+  // block's LDS can hold more hub words
+  const int rcw = int(std::min<int64_t>(c.opt("bu_ring_lds_kb", 128) * 256, std::min<int64_t>(fb_words, 38 * 1024)));
+  const int rgrid = int(std::max<int64_t>(1, std::min<int64_t>(((tr.n_rows + 127) / 128 + waves_per_block - 1) / waves_per_block,
+                                                               std::min<int64_t>(c.opt("bu_ring_grid", 256), kAggBlocks / 2))));
+  const size_t rshm = size_t(std::max(rcw, 1)) * 4;
+  auto go_ring = [&](auto kern) {
+    if (rshm > 48 * 1024)
+      NBG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(rshm)));
+    g1 = rgrid;
+    kern<<<rgrid, 1024, rshm, c.stream>>>(lo, hi, tr.n_rows, fb, nb, odeg, q, partials, rcw, pbits,
+                                          int(c.opt("bu_pair_diag", 0) & 3));
+  };
+#define NBG_RING(PKV, QPV)                                   \
+  switch (ring_d) {                                          \
+    case 1: go_ring(k_bu_ring<PKV, QPV, 1>); break;          \
+    case 2: go_ring(k_bu_ring<PKV, QPV, 2>); break;          \
+    case 3: go_ring(k_bu_ring<PKV, QPV, 3>); break;          \
+    default: go_ring(k_bu_ring<PKV, QPV, 4>); break;         \
+  }
+  const int sel = (defer ? 1 : 0) + (R == 2 ? 2 : 0);
+#define NBG_QR(PKV, W, QPV, EHV)                               \
+  switch (sel) {                                               \
+    case 0: go(k_bu_quad<PKV, W, QPV, 1, EHV, 0>); break;     \
+    case 1: go(k_bu_quad<PKV, W, QPV, 1, EHV, 1>); break;     \
+    case 2: go(k_bu_quad<PKV, W, QPV, 2, EHV, 0>); break;     \
+    default: go(k_bu_quad<PKV, W, QPV, 2, EHV, 1>); break;    \
+  }
+#define NBG_QF(W)                                                                                   \
+  {                                                                                                 \
+    if (QP) { NBG_QR(PK_FAST, W, 1, 2) }                                                            \
+    else if (defer) go(k_bu_quad<PK_FAST, W, 0, 1, 2, 1>);                                          \
+    else go(k_bu_quad<PK_FAST, W, 0, 1, 2, 0>);                                                     \
+    if (occ4) rest(k_bu_rest_words<PK_FAST, W, 4>); else rest(k_bu_rest_words<PK_FAST, W, 8>);     \
+  }
+  if (ring) {
+    if (fast) { NBG_RING(PK_FAST, 1) }
+    else { NBG_RING(PK_NONE, 0) }
+#define NBG_REST(PKV, W) \
+  if (occ4) rest(k_bu_rest_words<PKV, W, 4>); else rest(k_bu_rest_words<PKV, W, 8>);
+    if (fast) {
+      switch (fp.width) {
+        case 1: NBG_REST(PK_FAST, 1) break;
+        case 2: NBG_REST(PK_FAST, 2) break;
+        case 4: NBG_REST(PK_FAST, 4) break;
+        default: NBG_REST(PK_FAST, 8) break;
+      }
+    } else {
+      NBG_REST(PK_NONE, 0)
+    }
+#undef NBG_REST
+  } else if (fast) {
+    switch (fp.width) {
+      case 1: NBG_QF(1); break;
+      case 2: NBG_QF(2); break;
+      case 4: NBG_QF(4); break;
+      default: NBG_QF(8); break;
+    }
+  } else {
+    if (EH == 1) { NBG_QR(PK_NONE, 0, 0, 1) }
+    else { NBG_QR(PK_NONE, 0, 0, 2) }
+    if (occ4) rest(k_bu_rest_words<PK_NONE, 0, 4>);
+    else rest(k_bu_rest_words<PK_NONE, 0, 8>);
+  }
+#undef NBG_QR
+#undef NBG_RING
+#undef NBG_QF
+#undef NBG_QD
+  NBG_HIP(hipGetLastError());
+  if (after_kernel) NBG_HIP(hipEventRecord(after_kernel, c.stream));
+  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, g1 + grid2, out);
+  NBG_HIP(hipGetLastError());
+  return g1 + grid2;
+}
 // Second pass of a deferred slab hop (h: the first pass's reduced counters on the host, h[3] =
 // pending rows).  Adds the rows it finds into h[0] / h[1] and its reads into h[4] / h[5], so the
 // counters read as one hop.  Synchronises once.
@@ -2115,8 +2819,11 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       DevBuf pb;
       if (defer) pb.alloc(size_t((tr.n_rows + 63) / 64 + 1) * 8);
       hipEventRecord(c.ev[2], c.stream);
-      launch_bu_slab(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, nullptr, K.d,
-                     defer ? pb.as<unsigned long long>() : nullptr, c.ev[6]);
+      if (!defer && c.opt("bu_kernel", 1) == 1 && es.pair_col[0].p)
+        launch_bu_pair(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, K.d, c.ev[6]);
+      else
+        launch_bu_slab(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, nullptr, K.d,
+                       defer ? pb.as<unsigned long long>() : nullptr, c.ev[6]);
       if (!defer) hipEventRecord(c.ev[3], c.stream);
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 64, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
@@ -2219,8 +2926,12 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         DevBuf pb;
         if (defer) pb.alloc(size_t((tr.n_rows + 63) / 64 + 1) * 8);
         hipEventRecord(c.ev[2], c.stream);
-        launch_bu_slab(c, es, fb, bitsB, nullptr, pk, tfp, slab_w, K.d + 8,
-                       defer ? pb.as<unsigned long long>() : nullptr, c.ev[6]);
+        if (!defer && c.opt("bu_kernel", 1) == 1 && es.pair_col[0].p &&
+            (pk != PK_FAST || es.pair_props[0][size_t(fpk.col)].p))
+          launch_bu_pair(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8, c.ev[6]);
+        else
+          launch_bu_slab(c, es, fb, bitsB, nullptr, pk, tfp, slab_w, K.d + 8,
+                         defer ? pb.as<unsigned long long>() : nullptr, c.ev[6]);
         unsigned long long h2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (defer) {
           NBG_HIP(hipMemcpyAsync(K.h + 8, K.d + 8, 64, hipMemcpyDeviceToHost, c.stream));
@@ -2290,6 +3001,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         fused.alloc(size_t(E + 64) * 8);
         a.out_vid = fused.as<int64_t>();
         a.vid_of = c.vid_of.as<int64_t>();
+        a.col_vid = csr.col_vid.as<int64_t>();
       } else {
         c.ws_rows.ensure(size_t(E + 64) * 12);
         rows_edge = c.ws_rows.as<int64_t>();
@@ -2300,19 +3012,26 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       a.rows_cnt = K.d + 2;
       NBG_HIP(hipMemsetAsync(K.d, 0, 48, c.stream));
       const double ms0 = c.timing.expand_ms;
-      if (E > 0) {
-        launch_expand<EXP_ROWS>(c, a, pk, fp, dprog.as<Program>(), env, E);
-        c.timing.expand_bytes += expand_bytes(nF, E, pred_w, EXP_ROWS);
-      }
-      const unsigned long long hs[6] = {(unsigned long long)nF, (unsigned long long)E, 0, 0, 0, 0};
-      c.timing.hop(0, true, c.timing.expand_ms - ms0, hs);
+      if (E > 0) launch_expand<EXP_ROWS>(c, a, pk, fp, dprog.as<Program>(), env, E);
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
       int64_t errs = int64_t(K.h[4]);
       allsum(c, &errs, 1, red);
       if (errs) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
-      nrows = int64_t(K.h[2]);
-      c.timing.expand_bytes += uint64_t(nrows) * (dst_only ? 12 : 12);  // dst_only: 4 B col re-read + 8 B vid
+      const bool direct = dst_only && pk == PK_NONE;  // every edge is a row, written at its index
+      nrows = direct ? E : int64_t(K.h[2]);
+      // the hop's bytes: frontier entries + per edge the col (+ predicate);
+      // per row its 8 B vid write and where the vid comes from: the 8 B dst-vid column read
+      // instead of col (direct rows), else an 8 B vid_of gather behind the col read (a 4 B
+      // (src) + 8 B (edge) row pair without the fused _dst)
+      if (E > 0) {
+        if (direct && csr.col_vid.p)
+          c.timing.expand_bytes += uint64_t(nF) * 28 + uint64_t(E) * 16;
+        else
+          c.timing.expand_bytes += expand_bytes(nF, E, pred_w, EXP_ROWS) + uint64_t(nrows) * (dst_only ? 16 : 12);
+      }
+      const unsigned long long hs[6] = {(unsigned long long)nF, (unsigned long long)E, uint64_t(nrows), 0, 0, 0};
+      c.timing.hop(0, true, c.timing.expand_ms - ms0, hs);
       YieldArgs ya{};
       ya.ncols = int32_t(yields.size());
       for (auto& p : yields) {

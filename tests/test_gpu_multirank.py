@@ -330,3 +330,52 @@ def test_sharded_writes_commit(world):
             assert union_rows(res) == ms(ref.rows())
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_write_misrouted_key_refused(world):
+    """a write batch carrying a key of a vertex another rank owns is refused at write time on the
+    writing rank (E_PART_NOT_FOUND), nothing is appended, and the collective commit still runs on
+    every rank with the accepted batches (no rank fails inside the commit's collectives)"""
+    import test_gpu_tags as T
+    import test_gpu_writes as W
+    base, vids = T.random_space_kv(5, n_vertices=200, n_edges=1200)
+    mine = [v for v in vids if (O.part_of(v, T.PARTS) % world) == 0]
+    other = [v for v in vids if (O.part_of(v, T.PARTS) % world) == 1]
+    p0 = O.part_of(mine[0], T.PARTS)
+    ver = W.BASE_VER - 30
+    bad = [(O.edge_key(p0, other[0], T.ET, 0, mine[1], ver), O.encode_row([5]))]  # src owned by rank 1
+    good = [(O.edge_key(p0, mine[0], T.ET, 0, mine[2], ver), O.encode_row([6]))]
+    g = Group(world, parts=T.PARTS)
+    codes = {}
+    try:
+        def load(r, s):
+            s.set_option("writable", 1)
+            s.set_edge_schema(T.ET, [("weight", O.INT)])
+            s.set_tag_schema(T.PERSON, "person", W.FIELDS)
+            for p, kv in base.items():
+                if kv and p % world == r:
+                    s.load_part(p, kv)
+            s.finalize()
+
+        def write(r, s):
+            if r == 0:
+                try:
+                    s.write_part(p0, good + bad)
+                except NbgError as e:
+                    codes[r] = e.code
+                s.write_part(p0, good)
+            s.commit()
+        g.each(load)
+        g.each(write)
+        assert codes == {0: -14}
+        st = W.fresh_oracle([base, {p0: good}])
+        starts = vids[::13] + [mine[0]]
+        for steps, where, ys, distinct in W.QUERIES:
+            res = g.go(starts, steps, T.ET, where=where, yields=ys, distinct=distinct)
+            ref = st.go(starts, steps, T.ET, where=X.encode(where), yields=[y.encode() for y in ys],
+                        distinct=distinct)
+            assert ref.code == 0, ref.error
+            assert union_rows(res) == ms(ref.rows())
+    finally:
+        g.close()

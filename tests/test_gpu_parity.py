@@ -507,7 +507,8 @@ def test_rmat_bottom_up_rest_pass(rmat12, defer, r, eager):
     """rows that outlive the slab: the deferred edge-balanced second pass (k_bu_rest) and the
     inline wave scan agree with the oracle for every lane/slot shape of k_bu_slab"""
     sp, st = rmat12
-    opts = {"bu_force": 1, "bu_defer": defer, "bu_r": r, "bu_eager_fast": eager, "bu_eager": min(eager, 2)}
+    opts = {"bu_force": 1, "bu_defer": defer, "bu_r": r, "bu_eager_fast": eager, "bu_eager": min(eager, 2),
+            "bu_kernel": 0}
     for k, v in opts.items():
         sp.set_option(k, v)
     try:
@@ -525,5 +526,61 @@ def test_rmat_bottom_up_rest_pass(rmat12, defer, r, eager):
         # the high threshold leaves rows pending past the slab, so the rest pass really ran
         assert any(h["mode"] == "bottom-up" and h["c"][3] > 0 for h in hops)
     finally:
-        for k, v in {"bu_force": 0, "bu_defer": 0, "bu_r": 2, "bu_eager_fast": 1, "bu_eager": 1}.items():
+        for k, v in {"bu_force": 0, "bu_defer": 0, "bu_r": 2, "bu_eager_fast": 1, "bu_eager": 1, "bu_kernel": 1}.items():
+            sp.set_option(k, v)
+
+
+@pytest.mark.parametrize("defer,defer_final,eh,lds,r,occ", [(1, 0, 1, 64, 2, 8), (1, 1, 2, 64, 1, 4),
+                                                         (0, 1, 2, 16, 2, 8), (0, 0, 1, 0, 1, 8),
+                                                         (1, 1, 1, 0, 2, 4)])
+def test_rmat_bottom_up_quad_shapes(rmat12, defer, defer_final, eh, lds, r, occ):
+    """the quad-slab bottom-up kernel (k_bu_quad + k_bu_rest_words) for every row / half /
+    LDS-cache / deferral shape, with and without the final-hop predicate, against the oracle"""
+    sp, st = rmat12
+    opts = {"bu_force": 1, "bu_kernel": 1, "bu_pair_defer": defer, "bu_pair_defer_final": defer_final,
+            "bu_pair_eh": eh, "bu_pair_lds_kb": lds, "bu_pair_r": r, "bu_rest_occ": occ}
+    for k, v in opts.items():
+        sp.set_option(k, v)
+    try:
+        starts = sorted(set(seeds_from(12, 48, seed=23)))
+        for k in (0, 499, 990):
+            w = X.AliasProp("follow", "weight") > k
+            for steps in (2, 3):
+                g = sp.go(starts, steps, FOLLOW, where=w, yields=[X.EdgeDst("follow")], distinct=True)
+                r_ = st.go(starts, steps, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()],
+                           distinct=True)
+                assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
+                assert g.edges_scanned == r_.edges_scanned
+        g = sp.go(starts, 3, FOLLOW)
+        r_ = st.go(starts, 3, FOLLOW)
+        assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
+    finally:
+        for k, v in {"bu_force": 0, "bu_pair_defer": 1, "bu_pair_defer_final": 0, "bu_pair_eh": 1,
+                     "bu_pair_lds_kb": 64, "bu_pair_r": 1, "bu_rest_occ": 8}.items():
+            sp.set_option(k, v)
+
+
+@pytest.mark.parametrize("qpred", [1, 0])
+def test_rmat_bottom_up_packed_predicate(rmat12, qpred):
+    """the quantised predicate (slot words carry the bucket of follow.weight): every compare op,
+    constants below, inside, on the edges of and above the value range, deferred and inline rest
+    scans; bu_qpred=0 reads every value instead (same words, gidx masked)"""
+    sp, st = rmat12
+    starts = sorted(set(seeds_from(12, 48, seed=29)))
+    wcol = X.AliasProp("follow", "weight")
+    try:
+        sp.set_option("bu_force", 1)
+        sp.set_option("bu_qpred", qpred)
+        for dfin in (0, 1):
+            sp.set_option("bu_pair_defer_final", dfin)
+            for k in (-5, 0, 1, 3, 4, 255, 499, 500, 998, 999, 1000, 5000):
+                for w in (wcol > k, wcol >= k, wcol < k, wcol <= k, wcol.eq(k), wcol.ne(k)):
+                    g = sp.go(starts, 2, FOLLOW, where=w, yields=[X.EdgeDst("follow")], distinct=True)
+                    r_ = st.go(starts, 2, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()],
+                               distinct=True)
+                    assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0))), (k, w)
+                    assert g.edges_scanned == r_.edges_scanned
+                    assert any(h["mode"] == "bottom-up" and h["final"] for h in sp.last_timing()["hops"])
+    finally:
+        for k, v in {"bu_force": 0, "bu_qpred": 1, "bu_pair_defer_final": 0}.items():
             sp.set_option(k, v)

@@ -275,3 +275,49 @@ def test_add_processors_match_oracle():
         check_bound(sp, st, vids + new_vids)
     finally:
         sp.close()
+
+
+def _with_schema_version(row: bytes, ver: int) -> bytes:
+    """a RowWriter row re-headed with a 1-byte schema version (RowWriter.cpp:49-75: header bits
+    5-7 = version bytes; rows of < 16 fields carry no block offsets)"""
+    return bytes([row[0] | (1 << 5), ver]) + row[1:]
+
+
+def test_write_batch_all_or_nothing():
+    """A refused write batch leaves nothing behind (a RocksDB WriteBatch per part is atomic):
+    a tag row with another schema version, or a key whose part field is not the batch's part,
+    fails the whole batch, and the next commit sees only the accepted batches"""
+    base, vids = random_space_kv(12, n_vertices=300, n_edges=2000)
+    rng = random.Random(3)
+    sp = GraphSpace(PARTS)
+    try:
+        sp.set_option("writable", 1)
+        sp.set_edge_schema(ET, [("weight", O.INT)])
+        sp.set_tag_schema(PERSON, "person", FIELDS)
+        for p, kv in base.items():
+            if kv:
+                sp.load_part(p, kv)
+        sp.finalize()
+        v0 = vids[0]
+        p0 = O.part_of(v0, PARTS)
+        ver = BASE_VER - 50
+        good_edges = [(O.edge_key(p0, v0, ET, 0, t, ver), O.encode_row([1500 + i])) for i, t in enumerate(vids[1:20])]
+        bad_tag = (O.vertex_key(p0, v0, PERSON, ver), _with_schema_version(O.encode_row(["x", 1, 2.0]), 3))
+        with pytest.raises(NbgError) as e:
+            sp.write_part(p0, good_edges + [bad_tag])
+        assert e.value.code == -1003
+        wrong_part = (O.edge_key(p0 % PARTS + 1, v0, ET, 0, vids[5], ver), O.encode_row([7]))
+        with pytest.raises(NbgError) as e:
+            sp.write_part(p0, good_edges[:3] + [wrong_part])
+        assert e.value.code == -14
+        # an accepted batch re-writing some of the refused keys with other values
+        accepted = [(k, O.encode_row([99])) for k, _ in good_edges[::2]]
+        sp.write_part(p0, accepted)
+        sp.commit()
+        st = fresh_oracle([base, {p0: accepted}])
+        check_go(sp, st, vids[::17] + [v0])
+        check_bound(sp, st, vids)
+        sp.commit()  # a second commit of the same log: identical snapshot
+        check_go(sp, st, vids[::17] + [v0])
+    finally:
+        sp.close()

@@ -18,7 +18,9 @@ sys.path.insert(0, str(ROOT))
 # engine defaults of the swept options (traverse.hip / snapshot.hip), restored after each config
 DEFAULTS = {"bu_r": 2, "bu_eager_fast": 1, "bu_eager": 1, "bu_nt": 0, "bu_defer": 0, "bu_grid": 4096,
             "bu_tiles_per_wave": 4, "bu_lds_kb": 0, "bu_lds_grid": 512, "bu_div": 4, "bu_slab": 4,
-            "bu_lazy": 3, "bu_unroll": 1, "bu_wpe": 8}
+            "bu_lazy": 3, "bu_unroll": 1, "bu_wpe": 8, "bu_kernel": 1, "bu_pair_eh": 1,
+            "bu_pair_lds_kb": 64, "bu_pair_grid": 512, "bu_pair_defer": 1, "bu_pair_defer_final": 0,
+            "bu_rest_grid": 512, "bu_pair_r": 1, "bu_rest_occ": 8, "bu_qpred": 1}
 
 
 def main():
@@ -43,6 +45,7 @@ def main():
     # interleaved: every rep runs each config once, so clock / neighbour drift hits all alike
     ms = {c: [] for c in cfgs}
     hop_ms = {c: [] for c in cfgs}
+    kern_ms = {}
     res = {}
     for _ in range(args.reps):
         for cfg in cfgs:
@@ -56,6 +59,7 @@ def main():
             ms[cfg].append((time.perf_counter() - t) * 1e3)
             tm = sp.last_timing()
             hop_ms[cfg].append([h["ms"] for h in tm["hops"]])
+            kern_ms.setdefault(cfg, []).append([h["kernel_ms"] for h in tm["hops"]])
             res[cfg] = (r.n_rows, r.edges_scanned, tm)
             for k, v in saved.items():
                 sp.set_option(k, v)
@@ -63,8 +67,10 @@ def main():
     for cfg in cfgs:
         rows, edges, tm = res[cfg]
         hops = [round(statistics.median(h[i] for h in hop_ms[cfg]), 4) for i in range(len(hop_ms[cfg][0]))]
+        kms = [round(statistics.median(h[i] for h in kern_ms[cfg]), 4) for i in range(len(kern_ms[cfg][0]))]
         print(json.dumps({"config": cfg or "default", "ms_median": statistics.median(ms[cfg]), "ms_min": min(ms[cfg]),
                           "rows": rows, "rows_ok": rows == ref, "edges": edges, "hop_ms_median": hops,
+                          "kernel_ms_median": kms,
                           "hops": [(h["mode"], h["c"]) for h in tm["hops"]]}), flush=True)
     sp.close()
 
