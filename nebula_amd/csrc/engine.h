@@ -288,6 +288,15 @@ struct Timing {
     h.kernel_ms = kernel_ms < 0 ? ms : kernel_ms;
     h.kernel_bytes = kernel_ms < 0 ? b : kernel_bytes;
   }
+  // rocprof names of the last hop's kernels: the dominant one first, then the others ("; ")
+  void name_last_hop(const std::string& k0, const std::string& k1 = "", const char* k2 = nullptr) {
+    if (n_hops == 0 || n_hops > NBG_MAX_HOP_STATS) return;
+    std::string s = k0;
+    if (!k1.empty()) s += "; " + k1;
+    if (k2) s += std::string("; ") + k2;
+    nbg_hop_stat& h = hops[n_hops - 1];
+    snprintf(h.kernels, sizeof h.kernels, "%s", s.c_str());
+  }
 };
 
 constexpr size_t kHostStageBytes = size_t(1) << 20;
@@ -352,6 +361,8 @@ struct Ctx {
   } sp;
   Timing timing;
   hipEvent_t ev[8] = {};
+  std::string bu_kernel_name, bu_rest_name;  // rocprof names of the last bottom-up launch
+  int bu_slot_w = 0;                          // predicate bytes loaded beside each slab word
   // deferred kernel timing: event pairs recorded around expansion launches and read once the
   // query's stream has drained, so timing never makes the host wait on a launch
   struct PendingTime {

@@ -2287,8 +2287,14 @@ int launch_bu_slab(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
 #undef NBG_BU
 #undef NBG_BU_K
   if (after_kernel) NBG_HIP(hipEventRecord(after_kernel, c.stream));
+  NBG_HIP(hipEventRecord(c.ev[7], c.stream));
   k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, out);
   NBG_HIP(hipGetLastError());
+  char nm[96];
+  snprintf(nm, sizeof nm, "nbg::k_bu_slab<%d, %d, 2, %d, %d>", pk, pk == PK_FAST ? std::min(std::max(EG, 1), 4) : std::min(std::max(EG, 1), 2),
+           pk == PK_FAST ? int(fp.width) : 0, wpe == 8 || wpe == 7 ? wpe : 6);
+  c.bu_kernel_name = nm;
+  c.bu_rest_name.clear();
   return grid;
 }
 // The per-query bucket masks of a packed predicate column (EdgeSpace::q_*): bucket b holds the
@@ -2406,6 +2412,7 @@ int launch_bu_pair(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
   const bool occ4 = c.opt("bu_rest_occ", 8) == 4;  // 128-VGPR rest pass: no spills, half the waves
   auto rest = [&](auto kern) {
     if (!defer) return;
+    NBG_HIP(hipEventRecord(c.ev[7], c.stream));  // end of the first pass
     big_lds(kern);
     grid2 = int(std::min<int64_t>(c.opt("bu_rest_grid", 512), kAggBlocks / 2));
     // partials of the second pass sit behind the first pass's blocks: one reduction adds both
@@ -2413,7 +2420,7 @@ int launch_bu_pair(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
                                          QP ? 0 : 4);
   };
   // the pipelined deferred kernel (k_bu_ring) for predicate-free and packed-predicate hops
-  const int ring_d = int(c.opt("bu_ring", 3));
+  const int ring_d = int(c.opt("bu_ring", 0));
   const bool ring = defer && ring_d > 0 && (!fast || QP);
   // one 1024-thread block per CU (4 waves per SIMD: the registers of D tiles in flight), so a
   // block's LDS can hold more hub words
@@ -2485,9 +2492,27 @@ int launch_bu_pair(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
 #undef NBG_QF
 #undef NBG_QD
   NBG_HIP(hipGetLastError());
+  if (!defer) NBG_HIP(hipEventRecord(c.ev[7], c.stream));
   if (after_kernel) NBG_HIP(hipEventRecord(after_kernel, c.stream));
   k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, g1 + grid2, out);
   NBG_HIP(hipGetLastError());
+  // rocprof names of the two passes (hop stats: bench.py matches them against kernel traces)
+  const int W = fast ? int(fp.width) : 0;
+  char nm[96];
+  if (ring)
+    snprintf(nm, sizeof nm, "nbg::k_bu_ring<%d, %d, %d>", pk, fast ? 1 : 0, std::min(std::max(ring_d, 1), 4));
+  else if (fast)
+    snprintf(nm, sizeof nm, "nbg::k_bu_quad<%d, %d, %d, %d, 2, %d>", pk, W, QP ? 1 : 0, QP ? R : 1, defer ? 1 : 0);
+  else
+    snprintf(nm, sizeof nm, "nbg::k_bu_quad<%d, 0, 0, %d, %d, %d>", pk, R, EH, defer ? 1 : 0);
+  c.bu_kernel_name = nm;
+  c.bu_slot_w = fast && !QP ? int(fp.width) : 0;
+  if (defer) {
+    snprintf(nm, sizeof nm, "nbg::k_bu_rest_words<%d, %d, %d>", pk, W, occ4 ? 4 : 8);
+    c.bu_rest_name = nm;
+  } else {
+    c.bu_rest_name.clear();
+  }
   return g1 + grid2;
 }
 // Second pass of a deferred slab hop (h: the first pass's reduced counters on the host, h[3] =
@@ -2530,6 +2555,19 @@ void bu_finish(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const
   h[5] += r[3];
 }
 
+// byte models of a quad / ring hop's two passes from their counters.
+// First pass: slab words (4 B, + the predicate width when the values are loaded beside the
+// slots, c.bu_slot_w), the frontier bitmap once, the next-frontier and pending bits written,
+// the out-degree (4 B/row) at a non-final hop.  Rest pass: a row_ptr pair per pending row,
+// 4 B per entry read, predicate values read.
+uint64_t bu_first_bytes(const Ctx& c, const unsigned long long* h, int64_t n_rows, bool with_odeg) {
+  if (c.bu_rest_name.empty() && c.bu_kernel_name.rfind("nbg::k_bu_slab", 0) == 0) return 0;  // slab model below
+  return h[2] * (4 + uint64_t(c.bu_slot_w)) + 2 * (uint64_t(n_rows) / 8) +
+         (c.bu_rest_name.empty() ? 0 : uint64_t(n_rows) / 8) + (with_odeg ? uint64_t(n_rows) * 4 : 0);
+}
+uint64_t bu_rest_bytes(const unsigned long long* h, int pred_width) {
+  return h[3] * 16 + h[4] * 4 + h[5] * uint64_t(pred_width);
+}
 // byte model of one slab hop from its counters
 uint64_t bu_slab_bytes(const unsigned long long* h, int64_t n_rows, int pred_width, bool with_odeg) {
   return h[2] * (4 + uint64_t(pred_width)) + h[3] * 16 + h[4] * 4 + h[5] * uint64_t(pred_width) +
@@ -2835,13 +2873,15 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       }
       float ms = 0, kms = 0;
       hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
-      hipEventElapsedTime(&kms, c.ev[2], c.ev[6]);
+      hipEventElapsedTime(&kms, c.ev[2], c.ev[7]);
       c.timing.expand_ms += ms;
       c.timing.expand_launches++;
       c.timing.bu_steps++;
-      const uint64_t kb = bu_slab_bytes(K.h, tr.n_rows, 0, true);
-      c.timing.expand_bytes += kb;
+      uint64_t kb = bu_first_bytes(c, K.h, tr.n_rows, true), hb = kb + bu_rest_bytes(K.h, 0);
+      if (kb == 0) kb = hb = bu_slab_bytes(K.h, tr.n_rows, 0, true);
+      c.timing.expand_bytes += hb;
       c.timing.hop(1, false, ms, K.h, kms, kb);
+      c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name);
       std::swap(bitsA, bitsB);
       have_list = false;
       off_ready = false;
@@ -2947,15 +2987,19 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         NBG_HIP(hipStreamSynchronize(c.stream));  // K.h is pinned: the copy is truly asynchronous
         float ms = 0, kms = 0;
         hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
-        hipEventElapsedTime(&kms, c.ev[2], c.ev[6]);
+        hipEventElapsedTime(&kms, c.ev[2], c.ev[7]);
         c.timing.expand_ms += ms;
         c.timing.expand_launches++;
         c.timing.bu_steps++;
         nrows = int64_t(K.h[0]);
         if (defer) memcpy(K.h + 8, h2, sizeof(h2));
-        const uint64_t kb = bu_slab_bytes(K.h + 8, tr.n_rows, pk == PK_FAST ? tfp.width : 0, false);
-        c.timing.expand_bytes += kb + uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
+        const int pw = pk == PK_FAST ? tfp.width : 0;
+        uint64_t kb = bu_first_bytes(c, K.h + 8, tr.n_rows, false), hb = kb + bu_rest_bytes(K.h + 8, pw);
+        if (kb == 0) kb = hb = bu_slab_bytes(K.h + 8, tr.n_rows, pw, false);
+        // + the DISTINCT _dst output (k_bits_compact<1>): next bits once, vid_of read + vid written
+        c.timing.expand_bytes += hb + uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
         c.timing.hop(1, true, ms, K.h + 8, kms, kb);
+        c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name, "nbg::k_bits_compact<1>");
       } else {
         ensure_off();
         a.F = F;

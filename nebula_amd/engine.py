@@ -230,7 +230,9 @@ class GraphSpace:
         d = {k: getattr(t, k) for k, _ in t._fields_ if k not in ("hops", "n_hops")}
         d["hops"] = [{"mode": "bottom-up" if h.mode else "top-down", "final": bool(h.final_hop), "ms": h.ms,
                       "bytes": int(h.bytes), "c": list(h.c), "kernel_ms": h.kernel_ms,
-                      "kernel_bytes": int(h.kernel_bytes)} for h in t.hops[:t.n_hops]]
+                      "kernel_bytes": int(h.kernel_bytes),
+                      "kernels": [k for k in h.kernels.decode().split("; ") if k] or ["nbg::k_expand"]}
+                     for h in t.hops[:t.n_hops]]
         return d
 
     # ---- queries ---------------------------------------------------------------------

@@ -65,6 +65,17 @@ __global__ __launch_bounds__(1024) void k_tiles(const uint2* __restrict__ lo, co
   if (x == 0x12345678u) out[0] = x;
 }
 
+// random 4-byte probes into a table of tw words (the frontier-bitmap probes of the bottom-up
+// kernels): m probes, word index = a multiplicative hash of the probe number
+__global__ void k_probe(const unsigned* __restrict__ table, int64_t tw, int64_t m, unsigned* out) {
+  unsigned x = 0;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
+    const uint64_t h = uint64_t(i) * 0x9E3779B97F4A7C15ull;
+    x ^= table[(h >> 20) % uint64_t(tw)];
+  }
+  if (x == 0x12345678u) out[0] = x;
+}
+
 template <typename F>
 static float time_ms(F f, int reps) {
   hipEvent_t a, b;
@@ -116,6 +127,16 @@ int main(int argc, char** argv) {
     line("tiles_8B_lanes_bits", grid, 1024, bytes2, ms);
     ms = time_ms([&] { k_tiles<2, 1><<<grid, 1024>>>(lo, hi, n, bits, out); }, reps);
     line("tiles_16B_lanes_bits", grid, 1024, bytes2, ms);
+  }
+  // random probes: 4 MiB table (the RMAT-26 frontier bitmap) and 1 GiB (no cache reuse)
+  for (int64_t tw : {int64_t(1) << 20, int64_t(1) << 28}) {
+    unsigned* table;
+    CK(hipMalloc(&table, tw * 4));
+    CK(hipMemset(table, 3, tw * 4));
+    const int64_t m = int64_t(1) << 25;
+    float ms = time_ms([&] { k_probe<<<4096, 256>>>(table, tw, m, out); }, reps);
+    line(tw == (int64_t(1) << 20) ? "probe4_table4MiB" : "probe4_table1GiB", 4096, 256, double(m) * 4, ms);
+    CK(hipFree(table));
   }
   CK(hipFree(lo));
   CK(hipFree(hi));
