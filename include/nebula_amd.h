@@ -258,13 +258,14 @@ int32_t nbg_shortest_path(nbg_ctx* ctx, int32_t edge_type, const int64_t* src,
 /* one hop of the last nbg_go: mode 0 = top-down expansion of a frontier list, 1 = bottom-up
  * over the transposed CSR.  c[]: top-down {frontier, entries, next frontier, 0, 0, 0};
  * bottom-up {found, next-hop out-degree sum, slab words read, rows scanned past the slab,
- * entries read past the slab, predicate values read past the slab}.                        */
+ * entries read past the slab, predicate values read past the slab, first-pass frontier probes
+ * answered by L2, first-pass probes answered from the LDS hub copy}.                       */
 typedef struct {
   int32_t mode;
   int32_t final_hop;
   double ms;         /* HIP-event time of the hop's expansion kernels                      */
   uint64_t bytes;    /* their algorithmic bytes                       */
-  uint64_t c[6];
+  uint64_t c[8];
   double kernel_ms;      /* the hop's dominant kernel alone (first pass of a bottom-up hop)  */
   uint64_t kernel_bytes; /* that kernel's algorithmic bytes                                  */
   char kernels[160];     /* rocprof names of the hop's kernels, dominant first, "; "-separated

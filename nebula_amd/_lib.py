@@ -77,7 +77,7 @@ class GoSpec(C.Structure):
 
 class HopStat(C.Structure):
     _fields_ = [("mode", C.c_int32), ("final_hop", C.c_int32), ("ms", C.c_double), ("bytes", C.c_uint64),
-                ("c", C.c_uint64 * 6), ("kernel_ms", C.c_double), ("kernel_bytes", C.c_uint64),
+                ("c", C.c_uint64 * 8), ("kernel_ms", C.c_double), ("kernel_bytes", C.c_uint64),
                 ("kernels", C.c_char * 160)]
 
 

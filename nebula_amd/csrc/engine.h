@@ -225,6 +225,8 @@ struct EdgeSpace {
   DevBuf slab_col;                 // int32, -1 past the row's end
   std::vector<DevBuf> slab_props;  // per out prop with a transposed copy, same width
   DevBuf odeg;                     // uint32 [owned rows]: out-degree, 0 where row_ok == 0
+                                   // (padded with 0 to whole 128-row tiles)
+  int64_t bu_live_tiles = 0;       // 128-row tiles up to the last row with out-degree > 0
   // paired slab: the first 4 entries of every transposed row, row-major in two halves (slots
   // 0-1 -> pair_col[0], slots 2-3 -> pair_col[1], 2 x int32 per row, -1 past the row's end),
   // and the transposed INT-like props the same way (pair_props[h][field], 2 values per row)
@@ -284,7 +286,7 @@ struct Timing {
     h.final_hop = final_hop ? 1 : 0;
     h.ms = ms;
     h.bytes = b;
-    for (int i = 0; i < 6; i++) h.c[i] = c6 ? c6[i] : 0;
+    for (int i = 0; i < 8; i++) h.c[i] = c6 ? c6[i] : 0;
     h.kernel_ms = kernel_ms < 0 ? ms : kernel_ms;
     h.kernel_bytes = kernel_ms < 0 ? b : kernel_bytes;
   }

@@ -1252,6 +1252,14 @@ static bool copy_prop(const PropCol& p) {
   return intlike && !p.present.p;
 }
 
+// 1 + the last row with a non-zero out-degree (atomic max; rows past it never extend a frontier)
+__global__ void k_last_live(const uint32_t* odeg, int64_t n, unsigned long long* last) {
+  unsigned long long m = 0;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    if (odeg[i]) m = (unsigned long long)(i + 1);
+  if (m) atomicMax(last, m);
+}
+
 __global__ void k_out_deg(const int64_t* row_ptr, const uint8_t* row_ok, int64_t n, uint32_t* deg,
                           unsigned int* maxd) {
   unsigned int m = 0;
@@ -1369,12 +1377,17 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
     return b;
   };
   // out-degrees (0 for rows outside hash(vid)'s part) of every vertex of the gidx space
-  es.odeg.alloc(size_t(n_own + 1) * 4);
+  // padded to whole 128-row tiles (k_bu_lean loads two rows per lane without bounds checks)
+  const int64_t n_pad = (n_own + 127) / 128 * 128;
+  es.odeg.alloc(size_t(n_pad + 1) * 4);
+  NBG_HIP(hipMemsetAsync(es.odeg.p, 0, size_t(n_pad + 1) * 4, c.stream));
   DevBuf gdeg, dmax;
-  dmax.alloc(8);
-  NBG_HIP(hipMemsetAsync(dmax.p, 0, 8, c.stream));
+  dmax.alloc(16);
+  NBG_HIP(hipMemsetAsync(dmax.p, 0, 16, c.stream));
   k_out_deg<<<grid_for(n_own), 256, 0, c.stream>>>(o.row_ptr.as<int64_t>(), o.row_ok.as<uint8_t>(), n_own,
                                                   es.odeg.as<uint32_t>(), dmax.as<unsigned int>());
+  k_last_live<<<grid_for(n_own), 256, 0, c.stream>>>(es.odeg.as<uint32_t>(), n_own,
+                                                    reinterpret_cast<unsigned long long*>(dmax.as<unsigned int>() + 2));
   const uint32_t* gdegp = es.odeg.as<uint32_t>();
   if (G > 1) {
     gdeg.alloc(size_t(c.n_global + 1) * 4);
@@ -1387,8 +1400,11 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
     gdegp = gdeg.as<uint32_t>();
   }
   uint32_t maxd = 0;
+  unsigned long long last_live = 0;  // 1 + the last row with out-edges
   NBG_HIP(hipMemcpyAsync(&maxd, dmax.p, 4, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipMemcpyAsync(&last_live, dmax.as<unsigned int>() + 2, 8, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
+  es.bu_live_tiles = int64_t((last_live + 127) / 128);
   if (G > 1) maxd = UINT32_MAX;  // other ranks' degrees may exceed the local maximum
   // the transposed edge list: tdst (local row), tsrc (global), and the order props come in
   DevBuf tdst, tsrc;
@@ -1579,7 +1595,13 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
     }
   }
   if (c.opt("bu_pair", 1)) {
-    for (int h = 0; h < 2; h++) es.pair_col[h].alloc(size_t(n_own) * 8 + 16);
+    // padded to whole 128-row tiles with empty slots (-1)
+    const int64_t n_pad = (n_own + 127) / 128 * 128;
+    for (int h = 0; h < 2; h++) {
+      es.pair_col[h].alloc(size_t(n_pad) * 8 + 16);
+      NBG_HIP(hipMemsetAsync(es.pair_col[h].as<uint8_t>() + size_t(n_own) * 8, 0xff, size_t(n_pad - n_own) * 8 + 16,
+                             c.stream));
+    }
     const int32_t* src_col = es.q_field >= 0 ? es.tcol_q.as<int32_t>() : t.col.as<int32_t>();
     if (n_own)
       k_build_pair<int32_t><<<grid_for(n_own), 256, 0, c.stream>>>(t.row_ptr.as<int64_t>(), src_col, n_own,

@@ -377,11 +377,27 @@ struct QArgs {
   int32_t ulo = 0, uhi = INT32_MAX;
   int32_t below = -1, above = -1;
 };
+// The kernels' copy of QArgs in scalar registers.  Read through the by-value kernel argument,
+// q_test's select between `below` and `above` compiled to a per-lane select of two kernarg
+// addresses and a vector load, i.e. one dependent load and a vmcnt(0) wait per slot word.
+__device__ inline QArgs q_sgpr(const QArgs& a) {
+  QArgs r;
+  r.gmask = __builtin_amdgcn_readfirstlane(a.gmask);
+  r.gbits = __builtin_amdgcn_readfirstlane(a.gbits);
+  r.ulo = __builtin_amdgcn_readfirstlane(a.ulo);
+  r.uhi = __builtin_amdgcn_readfirstlane(a.uhi);
+  r.below = __builtin_amdgcn_readfirstlane(a.below);
+  r.above = __builtin_amdgcn_readfirstlane(a.above);
+  return r;
+}
 __device__ inline int32_t q_gidx(int32_t s, const QArgs& q) { return s & int32_t(q.gmask); }
 // 1 pass, 0 fail, -1 undecided (load the value)
 __device__ inline int q_test(int32_t s, const QArgs& q) {
   const int32_t b = int32_t(uint32_t(s) >> q.gbits);
-  return b < q.ulo ? q.below : (b > q.uhi ? q.above : -1);
+  int r = -1;
+  r = b > q.uhi ? q.above : r;
+  r = b < q.ulo ? q.below : r;
+  return r;
 }
 
 // raw buffer resource over p (gfx9 word 3; bounds left to the caller): loads through it are
@@ -1006,7 +1022,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_quad(
     const uint2* __restrict__ slab_lo, const uint2* __restrict__ slab_hi, const void* __restrict__ w_lo,
     const void* __restrict__ w_hi, const int64_t* __restrict__ trp, const int32_t* __restrict__ tcol, int64_t n,
     const uint32_t* __restrict__ fbits, unsigned long long* __restrict__ nbits, const uint32_t* __restrict__ odeg,
-    FastArgs fp, QArgs q, unsigned long long* partials, int cw, int ru, unsigned long long* __restrict__ pbits) {
+    FastArgs fp, QArgs q_arg, unsigned long long* partials, int cw, int ru, unsigned long long* __restrict__ pbits) {
+  const QArgs q = q_sgpr(q_arg);
   __shared__ unsigned long long lds[kSlots * 16];
   extern __shared__ uint32_t s_fb[];
   for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
@@ -1203,7 +1220,8 @@ template <int PK, int QP, int D>
 __global__ __launch_bounds__(1024, 4) void k_bu_ring(
     const uint2* __restrict__ slab_lo, const uint2* __restrict__ slab_hi, int64_t n,
     const uint32_t* __restrict__ fbits, unsigned long long* __restrict__ nbits, const uint32_t* __restrict__ odeg,
-    QArgs q, unsigned long long* partials, int cw, unsigned long long* __restrict__ pbits, int diag) {
+    QArgs q_arg, unsigned long long* partials, int cw, unsigned long long* __restrict__ pbits, int diag) {
+  const QArgs q = q_sgpr(q_arg);
   __shared__ unsigned long long lds[kSlots * 16];
   extern __shared__ uint32_t s_fb[];
   for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
@@ -1316,6 +1334,347 @@ __global__ __launch_bounds__(1024, 4) void k_bu_ring(
   block_store_partials(acc64, 6, lds, partials);
 }
 
+// Lean first pass of a bottom-up hop over the quad slab (bu_kernel = 2, the default).  Same
+// work as k_bu_quad (DEFER) with the instruction stream cut to what the hop needs, because the
+// quad kernel was issue-bound (with no probes at all it still ran at ~2.2 TB/s):
+//  * the slab halves and the out-degrees are padded to whole 128-row tiles at build (pad slots
+//    -1, degree 0), so the tile loads carry no bounds checks and no branches;
+//  * a lane owns rows l and l + 64 of a 128-row tile (8-byte loads per half), so the two ballots
+//    are the tile's two 64-row frontier words as they are;
+//  * U tiles per iteration: every slab load of the U tiles is issued, then every probe, then the
+//    bit tests (sched_barrier keeps the scheduler from pulling the consumers up to the loads,
+//    which put a vmcnt(0) wait behind every probe);
+//  * every probe is a buffer load whose offset is out of bounds for a non-candidate slot (the
+//    hardware returns 0: no branch; an LDS copy of the hub end of the bitmap measured no gain);
+//  * a non-final hop (PK_NONE) reads the second half only for rows still pending after the
+//    first (almost none: hub-first slot 0 is nearly always in a dense frontier), and only the
+//    tiles below es.bu_live_tiles (vertices are numbered by descending out-degree, so the rows
+//    with no out-edges - which never extend the frontier - form the tail); dead tiles get zero
+//    words;
+//  * the final hop (PK_FAST over the packed predicate buckets, QP) decides each slot by two
+//    scalar compares of its bucket; undecided buckets and rows with more than 4 entries are left
+//    pending for k_bu_rest_words (rest_from 0).
+// Outputs: next-frontier and pending words; partials [0] found, [1] their out-degree sum,
+// [2] slab words read, [3] pending rows.
+// HUB: the block keeps the first cw words of the bitmap (the highest-out-degree vertices) in LDS
+// and answers candidates there from it; the global probe of such a slot is out of bounds.
+// Partials [6] / [7]: candidate probes sent to L2 / answered from LDS.
+template <int PK, int U, int HUB>
+__global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ lo, const uint2* __restrict__ hi,
+                                                     int64_t ntiles, int64_t work_tiles,
+                                                     const uint32_t* __restrict__ fbits,
+                                                     unsigned long long* __restrict__ nbits,
+                                                     unsigned long long* __restrict__ pbits,
+                                                     const uint32_t* __restrict__ odeg, QArgs q_arg,
+                                                     unsigned long long* __restrict__ partials, int cw) {
+  __shared__ unsigned long long lds[kSlots * 16];
+  extern __shared__ uint32_t s_fb[];
+  if (HUB) {
+    for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
+    __syncthreads();
+  }
+  const QArgs q = q_sgpr(q_arg);
+  constexpr bool FINAL = PK == PK_FAST;
+  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  uint32_t nfound = 0, npend = 0, nwords = 0, nglob = 0, nhub = 0;
+  unsigned long long odsum = 0;
+  // bitmap-word offset of slot word sw of a live row: out of bounds unless it is a candidate
+  // answered by L2; the LDS word index (HUB) in `hw` (-1: not a hub candidate); `und` collects
+  // undecided buckets (final hop)
+  auto off = [&](int32_t sw, bool live, bool& und, int32_t& hw) -> uint32_t {
+    bool c = live && sw >= 0;
+    if (FINAL) {
+      const int t = q_test(sw, q);
+      und = und || (c && t < 0);
+      c = c && t > 0;
+    }
+    const int32_t wi = q_gidx(sw, q) >> 5;
+    const bool hub = HUB && wi < cw;
+    hw = c && hub ? wi : -1;
+    nglob += c && !hub;
+    nhub += c && hub;
+    return c && !hub ? uint32_t(wi) * 4u : 0xfffffff0u;
+  };
+  auto ld_ = [&](uint32_t o) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(fb_rs, o, 0, 0); };
+  auto hit = [](uint32_t w, int32_t sw) -> bool { return (w >> (uint32_t(sw) & 31u)) & 1u; };
+  for (int64_t t0 = wave * U; t0 < work_tiles; t0 += nwaves * U) {
+    uint2 a[U][2], b[U][2];
+    uint32_t od[U][2];
+    bool v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      v[u] = t0 + u < work_tiles;
+      const int64_t r = (v[u] ? t0 + u : t0) * 128 + lane;  // a past-the-end tile re-reads t0 (discarded)
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        a[u][h] = lo[r + 64 * h];
+        if (FINAL) b[u][h] = hi[r + 64 * h];
+        od[u][h] = FINAL ? 1u : odeg[r + 64 * h];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t w[U][2][4];
+    int32_t hw[U][2][4];
+    bool und[U][2];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const bool live = v[u] && od[u][h] > 0;
+        und[u][h] = false;
+        w[u][h][0] = ld_(off(int32_t(a[u][h].x), live, und[u][h], hw[u][h][0]));
+        w[u][h][1] = ld_(off(int32_t(a[u][h].y), live, und[u][h], hw[u][h][1]));
+        if (FINAL) {
+          w[u][h][2] = ld_(off(int32_t(b[u][h].x), live, und[u][h], hw[u][h][2]));
+          w[u][h][3] = ld_(off(int32_t(b[u][h].y), live, und[u][h], hw[u][h][3]));
+        }
+      }
+    if (HUB) {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+#pragma unroll
+          for (int k = 0; k < (FINAL ? 4 : 2); k++) {
+            const uint32_t lw = s_fb[hw[u][h][k] < 0 ? 0 : hw[u][h][k]];
+            w[u][h][k] = hw[u][h][k] < 0 ? w[u][h][k] : lw;
+          }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    bool f[U][2], pend[U][2];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        bool x = hit(w[u][h][0], int32_t(a[u][h].x)) || hit(w[u][h][1], int32_t(a[u][h].y));
+        if (FINAL) {
+          x = x || hit(w[u][h][2], int32_t(b[u][h].x)) || hit(w[u][h][3], int32_t(b[u][h].y));
+          pend[u][h] = v[u] && !x && (int32_t(b[u][h].y) >= 0 || und[u][h]);
+        } else {
+          // rows with a third slot to test: live, not found, slot 1 present
+          pend[u][h] = v[u] && !x && od[u][h] > 0 && int32_t(a[u][h].y) >= 0;
+        }
+        f[u][h] = x;
+      }
+      nwords += v[u] ? (FINAL ? 8u : 4u) : 0u;
+    }
+    if (!FINAL) {
+      // second half, lazily: only lanes with a pending row load it (rarely any at all)
+      bool anyp = false;
+#pragma unroll
+      for (int u = 0; u < U; u++) anyp = anyp || pend[u][0] || pend[u][1];
+      if (__ballot(anyp)) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            b[u][h] = make_uint2(0xffffffffu, 0xffffffffu);
+            if (pend[u][h]) b[u][h] = hi[(t0 + u) * 128 + lane + 64 * h];
+          }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            bool dummy = false;
+            w[u][h][2] = ld_(off(int32_t(b[u][h].x), pend[u][h], dummy, hw[u][h][2]));
+            w[u][h][3] = ld_(off(int32_t(b[u][h].y), pend[u][h], dummy, hw[u][h][3]));
+            if (HUB) {
+#pragma unroll
+              for (int k = 2; k < 4; k++) {
+                const uint32_t lw = s_fb[hw[u][h][k] < 0 ? 0 : hw[u][h][k]];
+                w[u][h][k] = hw[u][h][k] < 0 ? w[u][h][k] : lw;
+              }
+            }
+          }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const bool g = hit(w[u][h][2], int32_t(b[u][h].x)) || hit(w[u][h][3], int32_t(b[u][h].y));
+            nwords += pend[u][h] ? 2u : 0u;
+            f[u][h] = f[u][h] || (pend[u][h] && g);
+            // still pending: not found in the second half and a fifth entry may exist
+            pend[u][h] = pend[u][h] && !g && int32_t(b[u][h].y) >= 0;
+          }
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; u++) pend[u][0] = pend[u][1] = false;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (!v[u]) continue;  // wave-uniform
+      const int64_t t = t0 + u;
+      const unsigned long long f0 = __ballot(f[u][0]), f1 = __ballot(f[u][1]);
+      const unsigned long long p0 = __ballot(pend[u][0]), p1 = __ballot(pend[u][1]);
+      if (lane < 2) {
+        nbits[2 * t + lane] = lane ? f1 : f0;
+        pbits[2 * t + lane] = lane ? p1 : p0;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        nfound += f[u][h];
+        npend += pend[u][h];
+        if (!FINAL) odsum += f[u][h] ? od[u][h] : 0u;
+      }
+    }
+  }
+  // tiles past the live rows (non-final hops): nothing can be found there
+  for (int64_t t = work_tiles + wave; t < ntiles; t += nwaves)
+    if (lane < 2) {
+      nbits[2 * t + lane] = 0ull;
+      pbits[2 * t + lane] = 0ull;
+    }
+  unsigned long long acc64[8] = {nfound, odsum, nwords, npend, 0, 0, nglob, nhub};
+  block_store_partials(acc64, 8, lds, partials);
+}
+
+// Second pass of a lean bottom-up hop (bu_kernel = 2): the rows k_bu_lean left pending.  A wave
+// owns 64 consecutive pending-bit words (4096 rows) and ranks their pending rows (wave prefix
+// sum of the words' popcounts); 64 pending rows at a time, a lane scans its row's entries
+// [row_ptr + rest_from, row_ptr + 1) in chunks of kLeanChunk: all chunk loads issued, then all
+// probes (buffer loads out of bounds for non-candidates, LDS for hub words), then the tests, as
+// in k_bu_lean; a value is read only for a frontier hit in the constant's bucket.  After
+// kLeanSteps chunks the rows still pending (long in-edge lists) go to bu_rest_scan (whole wave /
+// 16-lane groups).  Found rows OR into the wave's 64 next-frontier words in LDS, merged into
+// nbits by the owning lanes (one writer per word).  Partials as k_bu_rest_words's.
+constexpr int kLeanChunk = 8;
+template <int PK, int W, int HUB>
+__global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long long* __restrict__ pbits, int64_t n,
+                                                          const int64_t* __restrict__ trp,
+                                                          const int32_t* __restrict__ tcol,
+                                                          const uint32_t* __restrict__ fbits, unsigned long long* nbits,
+                                                          const uint32_t* __restrict__ odeg, FastArgs fp, QArgs q_arg,
+                                                          unsigned long long* partials, int cw, int ru, int rest_from,
+                                                          int steps) {
+  const QArgs q = q_sgpr(q_arg);
+  __shared__ unsigned long long lds[kSlots * 16];
+  __shared__ unsigned long long s_found[16][64];
+  extern __shared__ uint32_t s_fb[];
+  if (HUB) {
+    for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
+    __syncthreads();
+  }
+  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
+  auto in_front = [&](int32_t g) -> bool {
+    const int32_t wi = g >> 5;
+    uint32_t w;
+    if (HUB && wi < cw) w = s_fb[wi];
+    else w = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, wi * 4, 0, 0);
+    return (w >> (g & 31)) & 1u;
+  };
+  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long odsum = 0;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nwords = (n + 63) / 64;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t cbase = wave * 64; cbase < nwords; cbase += nwaves * 64) {
+    const int64_t myw = cbase + lane;
+    const unsigned long long pw = myw < nwords ? pbits[myw] : 0ull;
+    s_found[wv][lane] = 0ull;
+    uint32_t total;
+    const uint32_t pre = wave_excl_scan(uint32_t(__popcll(pw)), total);
+    for (uint32_t k0 = 0; k0 < total; k0 += 64) {
+      // the (k0 + lane)-th pending row of the chunk: its word (binary search over the lanes'
+      // exclusive prefix sums) and the matching set bit of that word
+      const uint32_t p = k0 + uint32_t(lane);
+      bool pend[1] = {p < total}, found[1] = {false};
+      int64_t rb[1] = {0}, re[1] = {0};
+      int wsel = 0;
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1) {
+        const uint32_t pv = __shfl(pre, wsel + st);
+        if (wsel + st < 64 && pv <= p) wsel += st;
+      }
+      const unsigned long long wbits = __shfl((long long)pw, wsel);
+      const uint32_t kk = p - __shfl(pre, wsel);  // the kk-th set bit of wbits
+      int bit = 0;
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1)
+        if (uint32_t(__popcll(wbits & ((1ull << (bit + st)) - 1ull))) <= kk) bit += st;
+      const int32_t r = int32_t((cbase + wsel) * 64 + bit);
+      if (pend[0]) {
+        rb[0] = trp[r] + rest_from;
+        re[0] = trp[r + 1];
+        pend[0] = rb[0] < re[0];
+      }
+      for (int step = 0; step < steps; step++) {
+        if (__ballot(pend[0]) == 0) break;
+        int32_t sv[kLeanChunk];
+#pragma unroll
+        for (int k = 0; k < kLeanChunk; k++) {
+          const int64_t e = rb[0] + k < re[0] ? rb[0] + k : re[0] - 1;  // in-row: same lines
+          sv[k] = pend[0] ? tcol[e] : -1;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        uint32_t w[kLeanChunk];
+        int tq[kLeanChunk];
+#pragma unroll
+        for (int k = 0; k < kLeanChunk; k++) {
+          const bool valid = pend[0] && rb[0] + k < re[0];
+          acc[4] += valid;
+          tq[k] = PK == PK_FAST ? q_test(sv[k], q) : 1;
+          const bool cand = valid && tq[k] != 0;
+          const int32_t wi = q_gidx(sv[k], q) >> 5;
+          const bool hub = HUB && wi < cw;
+          const uint32_t gw = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, cand && !hub ? uint32_t(wi) * 4u : 0xfffffff0u,
+                                                                   0, 0);
+          if (HUB) {
+            const uint32_t lw = s_fb[cand && hub ? wi : 0];
+            w[k] = cand && hub ? lw : gw;
+          } else {
+            w[k] = gw;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        bool h = false, need = false;
+        uint32_t und = 0;
+#pragma unroll
+        for (int k = 0; k < kLeanChunk; k++) {
+          const bool inf = (w[k] >> (uint32_t(sv[k]) & 31u)) & 1u;
+          h = h || (inf && tq[k] > 0);
+          if (PK == PK_FAST && inf && tq[k] < 0) {
+            und |= 1u << k;
+            need = true;
+          }
+        }
+        if (PK == PK_FAST && __ballot(need && !h)) {
+          // frontier hits in the constant's bucket: the exact value decides
+          if (!h) {
+#pragma unroll
+            for (int k = 0; k < kLeanChunk; k++)
+              if ((und >> k) & 1u) {
+                acc[5]++;
+                h = h || fast_cmp(fp.op, load_w<W>(fp.data, fp.width, rb[0] + k), fp.k);
+              }
+          }
+        }
+        if (h) found[0] = true;
+        rb[0] += kLeanChunk;
+        pend[0] = pend[0] && !h && rb[0] < re[0];
+      }
+      const uint32_t a3 = acc[3];
+      bu_rest_scan<PK, W, 1>(pend, found, rb, re, tcol, fp, ru, acc, in_front, q);
+      acc[3] = a3;  // the pending rows were counted by the first pass
+      if (found[0]) {
+        atomicOr(&s_found[wv][wsel], 1ull << (r & 63));
+        acc[0]++;
+        if (odeg) odsum += odeg[r];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const unsigned long long fw = s_found[wv][lane];
+    if (fw) nbits[myw] |= fw;
+    __builtin_amdgcn_wave_barrier();
+  }
+  unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
+  block_store_partials(acc64, 6, lds, partials);
+}
+
 // Second pass of a deferred quad hop, straight from the pending bits (no list, no global
 // atomics): a wave owns 64 consecutive pbits words (4096 rows), ranks their pending rows (wave
 // prefix sum of the words' popcounts), and scans them 64 at a time, lane per row, in chunks of
@@ -1333,9 +1692,10 @@ __global__ __launch_bounds__(1024, OCC) void k_bu_rest_words(const unsigned long
                                                            const int64_t* __restrict__ trp,
                                                            const int32_t* __restrict__ tcol,
                                                            const uint32_t* __restrict__ fbits, unsigned long long* nbits,
-                                                           const uint32_t* __restrict__ odeg, FastArgs fp, QArgs q,
+                                                           const uint32_t* __restrict__ odeg, FastArgs fp, QArgs q_arg,
                                                            unsigned long long* partials, int cw, int ru,
                                                            int rest_from) {
+  const QArgs q = q_sgpr(q_arg);
   __shared__ unsigned long long lds[kSlots * 16];
   __shared__ unsigned long long s_found[16][64];
   extern __shared__ uint32_t s_fb[];
@@ -2515,6 +2875,104 @@ int launch_bu_pair(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
   }
   return g1 + grid2;
 }
+// bottom-up hop with the lean first pass (k_bu_lean) and the pending rows' rests in
+// k_bu_rest_words; counters reduced into out[0..8).  Returns false (nothing launched) when the
+// hop needs what the lean kernel does not do: a predicate that is not the packed column.
+bool launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
+                    const FastArgs& fp, int fcol, unsigned long long* out, hipEvent_t after_kernel) {
+  const Csr& tr = es.tr;
+  const bool fast = pk == PK_FAST;
+  if (pk != PK_NONE && pk != PK_FAST) return false;
+  if (!es.pair_col[0].p || (!fast && !odeg)) return false;
+  const QArgs q = make_qargs(es, pk, fcol, fp);
+  if (fast && !(q.gbits && fcol == es.q_field && c.opt("bu_qpred", 1) != 0)) return false;
+  const int64_t ntiles = (tr.n_rows + 127) / 128;
+  const int64_t work = fast ? ntiles : std::min(ntiles, es.bu_live_tiles);
+  const int U = c.opt(fast ? "bu_lean_u_final" : "bu_lean_u", 1) == 1 ? 1 : 2;
+  const int64_t waves = std::max<int64_t>(1, (work + U - 1) / U);
+  // hub words in LDS (bu_lean_lds_kb KiB, 0 = off): 1024-thread blocks, two per CU
+  const int64_t fb_words = (c.n_global + 31) / 32;
+  const int cw = int(std::min<int64_t>(c.opt(fast ? "bu_lean_lds_kb_final" : "bu_lean_lds_kb", 64) * 256,
+                                       std::min<int64_t>(fb_words, 36 * 1024)));
+  const int bs = cw > 0 ? 1024 : 256;
+  const int grid = int(std::max<int64_t>(
+      1, std::min<int64_t>((waves + bs / 64 - 1) / (bs / 64),
+                           std::min<int64_t>(cw > 0 ? 512 : c.opt("bu_lean_grid", 2048), kAggBlocks / 2))));
+  const size_t shm = size_t(std::max(cw, 1)) * 4;
+  c.ws_pend.ensure(size_t(ntiles * 2 + 2) * 8);
+  unsigned long long* pbits = c.ws_pend.as<unsigned long long>();
+  unsigned long long* partials = c.ws_partials.as<unsigned long long>();
+  auto* nb = reinterpret_cast<unsigned long long*>(nbits);
+  const uint2* lo = es.pair_col[0].as<uint2>();
+  const uint2* hi = es.pair_col[1].as<uint2>();
+  const uint32_t* od = fast ? nullptr : odeg;
+  auto go = [&](auto kern) {
+    if (shm > 48 * 1024)
+      NBG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(shm)));
+    kern<<<grid, bs, shm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, od, q, partials, cw);
+  };
+  const int sel = (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
+#define NBG_LEAN(PKV)                               \
+  switch (sel) {                                    \
+    case 0: go(k_bu_lean<PKV, 1, 0>); break;        \
+    case 1: go(k_bu_lean<PKV, 2, 0>); break;        \
+    case 2: go(k_bu_lean<PKV, 1, 1>); break;        \
+    default: go(k_bu_lean<PKV, 2, 1>); break;       \
+  }
+  if (fast) {
+    NBG_LEAN(PK_FAST)
+  } else {
+    NBG_LEAN(PK_NONE)
+  }
+#undef NBG_LEAN
+  NBG_HIP(hipGetLastError());
+  NBG_HIP(hipEventRecord(c.ev[7], c.stream));  // end of the first pass
+  const int64_t* trp = tr.row_ptr.as<int64_t>();
+  const int32_t* tc = q.gbits ? es.tcol_q.as<int32_t>() : tr.col.as<int32_t>();
+  const int ru = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_unroll", 1), kRestMax)));
+  const int grid2 = int(std::min<int64_t>(c.opt("bu_rest_grid", 512), kAggBlocks / 2));
+  const int W = fast ? int(fp.width) : 0;
+  const int rest_from = fast ? 0 : 4;  // the final hop re-reads undecided slots from the column
+  const int rcw = int(std::min<int64_t>(c.opt(fast ? "bu_rest_lds_kb_final" : "bu_rest_lds_kb", fast ? 64 : 0) * 256,
+                                        std::min<int64_t>(fb_words, 36 * 1024)));
+  const size_t rshm = size_t(std::max(rcw, 1)) * 4;
+  const int rsteps = int(std::max<int64_t>(1, c.opt("bu_rest_steps", 4)));
+  auto rest = [&](auto kern) {
+    if (rshm > 48 * 1024)
+      NBG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  int(rshm)));
+    kern<<<grid2, 1024, rshm, c.stream>>>(pbits, tr.n_rows, trp, tc, fb, nb, odeg, fp, q, partials + grid, rcw, ru,
+                                          rest_from, rsteps);
+  };
+#define NBG_REST(PKV, WV)                          \
+  if (rcw > 0) rest(k_bu_rest_lean<PKV, WV, 1>);   \
+  else rest(k_bu_rest_lean<PKV, WV, 0>)
+  if (fast) {
+    switch (W) {
+      case 1: NBG_REST(PK_FAST, 1); break;
+      case 2: NBG_REST(PK_FAST, 2); break;
+      case 4: NBG_REST(PK_FAST, 4); break;
+      default: NBG_REST(PK_FAST, 8); break;
+    }
+  } else {
+    NBG_REST(PK_NONE, 0);
+  }
+#undef NBG_REST
+  NBG_HIP(hipGetLastError());
+  if (after_kernel) NBG_HIP(hipEventRecord(after_kernel, c.stream));
+  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid + grid2, out);
+  NBG_HIP(hipGetLastError());
+  char nm[96];
+  snprintf(nm, sizeof nm, "nbg::k_bu_lean<%d, %d, %d>", pk, U, cw > 0 ? 1 : 0);
+  c.bu_kernel_name = nm;
+  snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d>", pk, fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0,
+           rcw > 0 ? 1 : 0);
+  c.bu_rest_name = nm;
+  c.bu_slot_w = 0;
+  return true;
+}
+
 // Second pass of a deferred slab hop (h: the first pass's reduced counters on the host, h[3] =
 // pending rows).  Adds the rows it finds into h[0] / h[1] and its reads into h[4] / h[5], so the
 // counters read as one hop.  Synchronises once.
@@ -2857,7 +3315,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       DevBuf pb;
       if (defer) pb.alloc(size_t((tr.n_rows + 63) / 64 + 1) * 8);
       hipEventRecord(c.ev[2], c.stream);
-      if (!defer && c.opt("bu_kernel", 1) == 1 && es.pair_col[0].p)
+      const int64_t bk = c.opt("bu_kernel", 2);
+      if (!defer && bk == 2 &&
+          launch_bu_lean(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, K.d, c.ev[6])) {
+      } else if (!defer && bk >= 1 && es.pair_col[0].p)
         launch_bu_pair(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, K.d, c.ev[6]);
       else
         launch_bu_slab(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, nullptr, K.d,
@@ -2901,7 +3362,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, E);
         c.timing.expand_bytes += expand_bytes(nF, E, 0, EXP_MARK);
       }
-      const unsigned long long hs[6] = {(unsigned long long)nF, (unsigned long long)E, 0, 0, 0, 0};
+      const unsigned long long hs[8] = {(unsigned long long)nF, (unsigned long long)E, 0, 0, 0, 0, 0, 0};
       c.timing.hop(0, false, c.timing.expand_ms - ms0, hs);
       exchange_marks(c, map);
       // next frontier = set of dsts (P12): compact, drop rows without out-edges, bitmap too
@@ -2966,8 +3427,11 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         DevBuf pb;
         if (defer) pb.alloc(size_t((tr.n_rows + 63) / 64 + 1) * 8);
         hipEventRecord(c.ev[2], c.stream);
-        if (!defer && c.opt("bu_kernel", 1) == 1 && es.pair_col[0].p &&
-            (pk != PK_FAST || es.pair_props[0][size_t(fpk.col)].p))
+        const int64_t bk = c.opt("bu_kernel", 2);
+        if (!defer && bk == 2 &&
+            launch_bu_lean(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8, c.ev[6])) {
+        } else if (!defer && bk >= 1 && es.pair_col[0].p &&
+                   (pk != PK_FAST || es.pair_props[0][size_t(fpk.col)].p))
           launch_bu_pair(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8, c.ev[6]);
         else
           launch_bu_slab(c, es, fb, bitsB, nullptr, pk, tfp, slab_w, K.d + 8,
@@ -3010,7 +3474,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
           launch_expand<EXP_MARK>(c, a, pk, fp, dprog.as<Program>(), env, E);
           c.timing.expand_bytes += expand_bytes(nF, E, pred_w, EXP_MARK);
         }
-        const unsigned long long hs[6] = {(unsigned long long)nF, (unsigned long long)E, 0, 0, 0, 0};
+        const unsigned long long hs[8] = {(unsigned long long)nF, (unsigned long long)E, 0, 0, 0, 0, 0, 0};
         c.timing.hop(0, true, c.timing.expand_ms - ms0, hs);
         exchange_marks(c, map);
         DevBuf lst;
@@ -3074,7 +3538,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         else
           c.timing.expand_bytes += expand_bytes(nF, E, pred_w, EXP_ROWS) + uint64_t(nrows) * (dst_only ? 16 : 12);
       }
-      const unsigned long long hs[6] = {(unsigned long long)nF, (unsigned long long)E, uint64_t(nrows), 0, 0, 0};
+      const unsigned long long hs[8] = {(unsigned long long)nF, (unsigned long long)E, uint64_t(nrows), 0, 0, 0, 0, 0};
       c.timing.hop(0, true, c.timing.expand_ms - ms0, hs);
       YieldArgs ya{};
       ya.ncols = int32_t(yields.size());

@@ -18,10 +18,10 @@ sys.path.insert(0, str(ROOT))
 # engine defaults of the swept options (traverse.hip / snapshot.hip), restored after each config
 DEFAULTS = {"bu_r": 2, "bu_eager_fast": 1, "bu_eager": 1, "bu_nt": 0, "bu_defer": 0, "bu_grid": 4096,
             "bu_tiles_per_wave": 4, "bu_lds_kb": 0, "bu_lds_grid": 512, "bu_div": 4, "bu_slab": 4,
-            "bu_lazy": 3, "bu_unroll": 1, "bu_wpe": 8, "bu_kernel": 1, "bu_pair_eh": 1,
+            "bu_lazy": 3, "bu_unroll": 1, "bu_wpe": 8, "bu_kernel": 2, "bu_lean_u": 1, "bu_lean_grid": 2048, "bu_lean_lds_kb": 64, "bu_lean_lds_kb_final": 64, "bu_lean_u_final": 1, "bu_rest_lds_kb": 0, "bu_rest_lds_kb_final": 64, "bu_rest_steps": 4, "bu_pair_eh": 1,
             "bu_pair_lds_kb": 64, "bu_pair_grid": 512, "bu_pair_defer": 1, "bu_pair_defer_final": 1,
             "bu_rest_grid": 512, "bu_pair_r": 1, "bu_rest_occ": 8, "bu_qpred": 1, "bu_pair_diag": 0,
-            "bu_ring": 3, "bu_ring_lds_kb": 128, "bu_ring_grid": 256, "fuse_dst": 1, "mark_check": 0,
+            "bu_ring": 0, "bu_ring_lds_kb": 128, "bu_ring_grid": 256, "fuse_dst": 1, "mark_check": 0,
             "expand_grid": 2048, "rest_grid": 2048}
 
 
