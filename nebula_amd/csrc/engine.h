@@ -363,6 +363,7 @@ struct Ctx {
   } sp;
   Timing timing;
   hipEvent_t ev[8] = {};
+  DevBuf ws_tile_rows;  // k_expand: frontier entry of each tile's first slot
   std::string bu_kernel_name, bu_rest_name;  // rocprof names of the last bottom-up launch
   int bu_slot_w = 0;                          // predicate bytes loaded beside each slab word
   // deferred kernel timing: event pairs recorded around expansion launches and read once the
