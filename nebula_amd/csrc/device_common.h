@@ -58,4 +58,76 @@ __device__ inline int64_t wave_append(unsigned long long* counter, bool pred) {
   return int64_t(base + __popcll(below));
 }
 
+// ---- edge-balanced tiles over a frontier's flattened adjacency (k_expand, k_sp_expand) -------
+// tile_row[t] = the frontier entry holding slot t * TILE of the flattened range: every non-empty
+// entry k writes the tiles whose first slot falls in [off[k], off[k + 1]) (each tile start lies
+// in exactly one non-empty entry).  One coalesced pass over off[] instead of two dependent binary
+// searches of off[] by one thread at the head of every tile.
+template <int TILE>
+__global__ void k_tile_rows(const int64_t* __restrict__ off, int64_t nF, int32_t* __restrict__ tile_row) {
+  for (int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; k < nF; k += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t b = off[k], e = off[k + 1];
+    if (b == e) continue;
+    for (int64_t t = (b + TILE - 1) / TILE; t * TILE < e; t++) tile_row[t] = int32_t(k);
+  }
+}
+// The entries [i0, i0 + cnt) staged for tile t (slots [e0, e1) of E): i0 holds e0; the last one
+// holds e1 - 1, i.e. the entry before the one holding e1 when that one starts at e1 (entries of
+// zero degree in between are staged too, harmlessly: their slots are empty).
+__device__ inline void tile_entries(const int32_t* tile_row, const int64_t* off, int64_t nF, int64_t t, int64_t e1,
+                                    int64_t E, int64_t& i0, int64_t& cnt) {
+  i0 = tile_row[t];
+  int64_t i1 = nF - 1;
+  if (e1 < E) {
+    const int64_t r = tile_row[t + 1];
+    i1 = off[r] == e1 ? r - 1 : r;
+  }
+  cnt = i1 - i0 + 1;
+}
+// Owner map of a tile in LDS: s_off[k] (k < cnt <= TILE) holds entry k's first slot relative to
+// the tile (<= 0 for the entry holding slot 0); on return s_off[j] (j < TILE) is the entry owning
+// slot j: the largest k starting at or before j (entries of zero degree share their successor's
+// start; the max picks the non-empty one) - one atomicMax per entry and a block max-scan instead
+// of a binary search per slot.  Block-wide (THREADS threads, all of them must call it).
+template <int TILE, int THREADS>
+__device__ inline void tile_owner_map(int32_t* s_off, int cnt, int32_t* s_scan /* [THREADS / 64] */) {
+  constexpr int kRows = TILE / THREADS;
+  int st[kRows];
+#pragma unroll
+  for (int i = 0; i < kRows; i++) {
+    const int k = threadIdx.x + i * THREADS;
+    st[i] = k < cnt ? s_off[k] : TILE;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < TILE; j += THREADS) s_off[j] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kRows; i++)
+    if (st[i] < TILE) atomicMax(&s_off[st[i] < 0 ? 0 : st[i]], int(threadIdx.x + i * THREADS));
+  __syncthreads();
+  // inclusive max-scan: kRows consecutive slots per thread, then across the wave and the block
+  int m = 0;
+  int loc[kRows];
+#pragma unroll
+  for (int i = 0; i < kRows; i++) {
+    m = max(m, s_off[threadIdx.x * kRows + i]);
+    loc[i] = m;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int x = m;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x = max(x, y);
+  }
+  if (lane == 63) s_scan[wv] = x;
+  int prev = __shfl_up(x, 1);
+  if (lane == 0) prev = 0;
+  __syncthreads();
+  for (int w = 0; w < wv; w++) prev = max(prev, s_scan[w]);
+#pragma unroll
+  for (int i = 0; i < kRows; i++) s_off[threadIdx.x * kRows + i] = max(prev, loc[i]);
+  __syncthreads();
+}
+
 }  // namespace nbg

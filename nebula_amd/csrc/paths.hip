@@ -292,6 +292,7 @@ struct SpExpand {
   int64_t n;           // owned rows (pair stride of dist)
   int64_t lo;
   int32_t sweep;
+  const int32_t* tile_row;  // k_tile_rows: X entry holding each tile's first slot (null: search)
 };
 
 // One edge-balanced pass over the adjacency of every X tuple (tiles of kTileE entries).
@@ -304,13 +305,19 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
   __shared__ int64_t s_rs[kTileE];
   __shared__ uint64_t s_tup[kTileE];
   __shared__ int64_t s_hdr[2];
+  __shared__ int32_t s_scan[kT / 64];
   const int64_t nX = a.nX;
   const int64_t E = a.off[nX];
   const int64_t ntiles = (E + kTileE - 1) / kTileE;
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int64_t e0 = t * kTileE;
     const int64_t e1 = min(e0 + int64_t(kTileE), E);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && a.tile_row) {
+      int64_t i0, cnt;
+      tile_entries(a.tile_row, a.off, nX, t, e1, E, i0, cnt);
+      s_hdr[0] = i0;
+      s_hdr[1] = cnt;
+    } else if (threadIdx.x == 0) {
       int64_t lo = 0, hi = nX;  // off[lo] <= e0 < off[hi]
       while (hi - lo > 1) {
         const int64_t mid = (lo + hi) >> 1;
@@ -342,6 +349,7 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
       }
     }
     __syncthreads();
+    if (!big) tile_owner_map<kTileE, kT>(s_off, cnt_k, s_scan);  // s_off[j] = owner of slot j
     for (int r = 0; r < kIt; r++) {
       const int j = threadIdx.x + r * kT;
       const int64_t e = e0 + j;
@@ -350,12 +358,7 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
       uint64_t tu = 0;
       int64_t rsk = 0;
       if (valid && !big) {
-        int lo = 0, hi = cnt_k;
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (s_off[mid] <= j) lo = mid; else hi = mid;
-        }
-        k = lo;
+        k = s_off[j];
         tu = s_tup[k];
         rsk = s_rs[k];
       } else if (valid) {
@@ -847,6 +850,16 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       const int64_t tiles = (E + kTileE - 1) / kTileE;
       const int grid = int(std::max<int64_t>(1, std::min<int64_t>(tiles, c.opt("sp_grid", 256 * 8))));
       hipEventRecord(c.ev[2], c.stream);
+      a.tile_row = nullptr;
+      if (c.opt("expand_tile_rows", 1) && nX < (int64_t(1) << 31)) {
+        if (W.tile_rows.bytes < size_t(tiles + 2) * 4) {
+          PoolScope none(nullptr);
+          W.tile_rows.alloc(size_t(tiles + tiles / 4 + 64) * 4);
+        }
+        a.tile_row = W.tile_rows.as<int32_t>();
+        k_tile_rows<kTileE><<<int(std::max<int64_t>(1, std::min<int64_t>((nX + 255) / 256, 4096))), 256, 0, c.stream>>>(
+            a.off, nX, W.tile_rows.as<int32_t>());
+      }
       k_sp_expand<<<grid, kT, 0, c.stream>>>(a, st, bf, cnt);
       NBG_HIP(hipGetLastError());
       hipEventRecord(c.ev[3], c.stream);

@@ -426,17 +426,10 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
     const int64_t e0 = t * kTile;
     const int64_t e1 = min(e0 + int64_t(kTile), E);
     if (threadIdx.x == 0 && a.tile_row) {
-      // i0 = the entry holding slot e0; i1 = the one holding e1 - 1: the entry before the one
-      // holding e1 when that one starts at e1 (entries of zero degree in between are staged too,
-      // harmlessly: their slots are empty)
-      const int64_t i0 = a.tile_row[t];
-      int64_t i1 = nF - 1;
-      if (e1 < E) {
-        const int64_t r = a.tile_row[t + 1];
-        i1 = a.off[r] == e1 ? r - 1 : r;
-      }
+      int64_t i0, cnt;
+      tile_entries(a.tile_row, a.off, nF, t, e1, E, i0, cnt);
       s_hdr[0] = i0;
-      s_hdr[1] = i1 - i0 + 1;
+      s_hdr[1] = cnt;
     } else if (threadIdx.x == 0) {
       // i0 = last k with off[k] <= e0 ; i1 = last k with off[k] <= e1 - 1
       int64_t lo = 0, hi = nF;  // off[lo] <= e0 < off[hi] invariant (off[0] = 0, off[nF] = E)
@@ -471,50 +464,7 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
       }
     }
     __syncthreads();
-    if (!big) {
-      // owner map instead of a binary search per slot: the largest k starting at or before slot
-      // j (rows of zero degree share their successor's start; the max picks the non-empty one)
-      // (built in place of s_off: the starts are read into registers first)
-      constexpr int kRows = kTile / kThreads;  // cnt <= kTile
-      int st[kRows];
-#pragma unroll
-      for (int i = 0; i < kRows; i++) {
-        const int k = threadIdx.x + i * kThreads;
-        st[i] = k < cnt ? s_off[k] : kTile;
-      }
-      __syncthreads();
-      for (int j = threadIdx.x; j < kTile; j += kThreads) s_own[j] = 0;
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < kRows; i++)
-        if (st[i] < kTile) atomicMax(&s_own[st[i] < 0 ? 0 : st[i]], int(threadIdx.x + i * kThreads));
-      __syncthreads();
-      // inclusive max-scan over the kTile slots: kItems consecutive slots per thread, then the
-      // threads' maxima across the wave and the block
-      constexpr int kPer = kTile / kThreads;
-      int m = 0;
-      int loc[kPer];
-#pragma unroll
-      for (int i = 0; i < kPer; i++) {
-        m = max(m, s_own[threadIdx.x * kPer + i]);
-        loc[i] = m;
-      }
-      const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-      int x = m;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (lane >= o) x = max(x, y);
-      }
-      if (lane == 63) s_scan[wv] = x;
-      int prev = __shfl_up(x, 1);
-      if (lane == 0) prev = 0;
-      __syncthreads();
-      for (int w = 0; w < wv; w++) prev = max(prev, s_scan[w]);
-#pragma unroll
-      for (int i = 0; i < kPer; i++) s_own[threadIdx.x * kPer + i] = max(prev, loc[i]);
-      __syncthreads();
-    }
+    if (!big) tile_owner_map<kTile, kThreads>(s_off, cnt, s_scan);
     // owner of tile slot j: its frontier row and (row_ptr - off) so that ge = rsk + e
     auto locate = [&](int j, int32_t& srck, int64_t& rsk) {
       const int64_t e = e0 + j;
@@ -2623,18 +2573,6 @@ size_t timing_event(Ctx& c) {
   return c.tev_used++;
 }
 
-// tile_row[t] = the frontier entry holding slot t * kTile of the flattened edge range: every
-// non-empty entry k writes the tiles whose first slot falls in [off[k], off[k + 1]) (each tile
-// start lies in exactly one non-empty entry).  One coalesced pass over off[], instead of two
-// dependent binary searches of off[] at the head of every k_expand tile.
-__global__ void k_tile_rows(const int64_t* __restrict__ off, int64_t nF, int32_t* __restrict__ tile_row) {
-  for (int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; k < nF; k += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t b = off[k], e = off[k + 1];
-    if (b == e) continue;
-    for (int64_t t = (b + kTile - 1) / kTile; t * kTile < e; t++) tile_row[t] = int32_t(k);
-  }
-}
-
 template <int MODE>
 void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Program* dprog, const EvalEnv& env,
                    int64_t E) {
@@ -2644,7 +2582,7 @@ void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Progr
   if (c.opt("expand_tile_rows", 1) && a.nF < (int64_t(1) << 31)) {
     c.ws_tile_rows.ensure(size_t(ntiles + 2) * 4);
     a.tile_row = c.ws_tile_rows.as<int32_t>();
-    k_tile_rows<<<grid_cap(a.nF), 256, 0, c.stream>>>(a.off, a.nF, c.ws_tile_rows.as<int32_t>());
+    k_tile_rows<kTile><<<grid_cap(a.nF), 256, 0, c.stream>>>(a.off, a.nF, c.ws_tile_rows.as<int32_t>());
   }
   switch (pk) {
     case PK_NONE: k_expand<MODE, PK_NONE><<<grid, kThreads, 0, c.stream>>>(a, fp, dprog, env); break;
