@@ -1257,7 +1257,8 @@ __global__ void k_last_live(const uint32_t* odeg, int64_t n, unsigned long long*
   unsigned long long m = 0;
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
     if (odeg[i]) m = (unsigned long long)(i + 1);
-  if (m) atomicMax(last, m);
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor((long long)m, o));
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(last, m);  // one atomic per wave
 }
 
 __global__ void k_out_deg(const int64_t* row_ptr, const uint8_t* row_ok, int64_t n, uint32_t* deg,
