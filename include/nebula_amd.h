@@ -202,8 +202,11 @@ int32_t nbg_get_bound(nbg_ctx* ctx, int32_t edge_type, const int32_t* parts,
  * AVG -> DOUBLE (sum / count, NaN without rows); in-bound requests skip edge props.  SUM / AVG
  * over BOOL / STRING fail every part with E_IMPROPER_DATA_TYPE (validOperation,
  * QueryBaseProcessor.inl:18-35); SUM / AVG over DOUBLE values return NBG_E_UNSUPPORTED (the
- * reference's int64-initialised sum throws boost::bad_get).  SOURCE / DEST tag props:
- * NBG_E_UNSUPPORTED in this version.                                                        */
+ * reference's int64-initialised sum throws boost::bad_get).  SOURCE / DEST tag props
+ * (tag_id + name) reduce over the request entries of owned parts whose vertex row sits in the
+ * entry's part (collectVertexProps, QueryBaseProcessor.inl:309-333; QueryStatsProcessor.cpp:
+ * 69-82), duplicates counted per entry; unknown tag -> E_TAG_PROP_NOT_FOUND, unknown prop or
+ * SUM / AVG over BOOL / STRING -> E_IMPROPER_DATA_TYPE on every part.                        */
 int32_t nbg_bound_stats(nbg_ctx* ctx, int32_t edge_type, const int32_t* parts, const int64_t* vids,
                         size_t n, const uint8_t* filter, size_t filter_len, const nbg_prop_def* cols,
                         const int32_t* stat_types, size_t ncols, nbg_rows* out);

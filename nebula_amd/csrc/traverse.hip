@@ -4071,12 +4071,11 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
     size_t field;
   };
   std::vector<TagReq> treq;
+  // stats: the output columns in request order (retIndex): {0, edge column} or {1, tag column}
+  std::vector<std::pair<int, int>> sorder;
+  std::vector<int32_t> tstat;
   for (size_t i = 0; i < ncols; i++) {
     if (cols[i].owner != NBG_OWNER_EDGE) {
-      if (stats) {
-        delete h;
-        throw Error(NBG_E_UNSUPPORTED, "SOURCE/DEST tag props in bound stats");
-      }
       auto tit = c.tags.find(cols[i].tag_id);
       if (tit == c.tags.end()) return fail_all(NBG_E_TAG_PROP_NOT_FOUND);
       const std::string tname = cols[i].name ? cols[i].name : "";
@@ -4084,6 +4083,17 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
       for (size_t f = 0; f < tit->second.fields.size(); f++)
         if (tit->second.fields[f].name == tname) fi = f;
       if (fi == tit->second.fields.size()) return fail_all(NBG_E_IMPROPER_DATA_TYPE);
+      if (stats) {  // validOperation over the tag prop's type (QueryBaseProcessor.inl:62-64)
+        const int32_t st = stats[i];
+        if (st < 1 || st > 3) {
+          delete h;
+          throw Error(NBG_E_INVALID_ARG, "stat type must be SUM 1, COUNT 2 or AVG 3");
+        }
+        const int32_t t = tit->second.fields[fi].type;
+        if (st != 2 && (t == NBG_T_BOOL || t == NBG_T_STRING)) return fail_all(NBG_E_IMPROPER_DATA_TYPE);
+        sorder.emplace_back(1, int(treq.size()));
+        tstat.push_back(st);
+      }
       treq.push_back(TagReq{&tit->second, fi});
       continue;
     }
@@ -4119,6 +4129,7 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
       delete h;
       throw Error(NBG_E_UNSUPPORTED, "too many return columns");
     }
+    if (stats) sorder.emplace_back(0, bc.n);
     bc.c[bc.n++] = b;
   }
   Program fprog{};
@@ -4313,12 +4324,77 @@ int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* v
     }
     std::vector<unsigned long long> ha(size_t(2 * bc.n + 2));
     NBG_HIP(hipMemcpyAsync(ha.data(), acc.p, ha.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    // SOURCE / DEST tag columns (QueryStatsProcessor::processVertex, QueryStatsProcessor.cpp:69-82):
+    // every request entry of an owned part collects the newest version of its vertex row in that
+    // part (collectVertexProps, QueryBaseProcessor.inl:309-333) - visible when the row sits in
+    // the request's part, as for getBound's vertex columns - into the column's sum / count
+    // (StatsCollector, Collector.h:66-94); entries without the row add nothing
+    std::vector<int64_t> tsum(treq.size(), 0), tcnt(treq.size(), 0);
+    std::vector<std::vector<int64_t>> tval(treq.size());
+    std::vector<std::vector<uint8_t>> tstt(treq.size());
+    std::vector<std::vector<int32_t>> tprt(treq.size());
+    DevBuf tv, ts, tp;
+    if (!treq.empty() && N) {
+      tv.alloc(size_t(N) * 8);
+      ts.alloc(size_t(N));
+      tp.alloc(size_t(N) * 4);
+      for (size_t t = 0; t < treq.size(); t++) {
+        const TagSpace& tsp = *treq[t].ts;
+        const PropCol& pc = tsp.cols[treq[t].field];
+        k_tag_fetch<<<grid_cap(N), 256, 0, c.stream>>>(dg.as<int32_t>(), N, pc.data.as<int64_t>(), pc.present.as<uint8_t>(),
+                                                       tsp.part.as<int32_t>(), nullptr, tv.as<int64_t>(), ts.as<uint8_t>(),
+                                                       tp.as<int32_t>(), nullptr, nullptr);
+        NBG_HIP(hipGetLastError());
+        tval[t].resize(size_t(N));
+        tstt[t].resize(size_t(N));
+        tprt[t].resize(size_t(N));
+        NBG_HIP(hipMemcpyAsync(tval[t].data(), tv.p, size_t(N) * 8, hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipMemcpyAsync(tstt[t].data(), ts.p, size_t(N), hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipMemcpyAsync(tprt[t].data(), tp.p, size_t(N) * 4, hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipStreamSynchronize(c.stream));  // the host vectors are reused per column
+      }
+    }
     hipEventRecord(c.ev[1], c.stream);
     NBG_HIP(hipStreamSynchronize(c.stream));
+    for (size_t t = 0; t < treq.size() && N; t++) {
+      const int32_t ty = treq[t].ts->cols[treq[t].field].type;
+      for (int64_t i = 0; i < N; i++) {
+        const int32_t rp = parts[i];
+        if (rp < 0 || rp > c.num_parts || owner_of_part(rp, c.world) != c.rank) continue;  // failed part
+        const uint8_t stt = tstt[t][size_t(i)];
+        const bool vis = (stt == 1 && rp == part_of_vid(vids[i], c.num_parts)) || (stt == 2 && rp == tprt[t][size_t(i)]);
+        if (!vis) continue;
+        tcnt[t]++;
+        if (ty == NBG_T_DOUBLE || ty == NBG_T_FLOAT) {
+          if (tstat[t] != 2) {
+            delete h;
+            throw Error(NBG_E_UNSUPPORTED, "SUM/AVG over a double prop (the reference's int64 sum throws bad_get)");
+          }
+        } else if (ty != NBG_T_BOOL && ty != NBG_T_STRING) {
+          tsum[t] = int64_t(uint64_t(tsum[t]) + uint64_t(tval[t][size_t(i)]));
+        }
+      }
+    }
     float sms = 0;
     hipEventElapsedTime(&sms, c.ev[0], c.ev[1]);
     c.timing.total_ms = sms;
-    for (int i = 0; i < bc.n; i++) {
+    for (const auto& so : sorder) {
+      if (so.first == 1) {
+        const size_t t = size_t(so.second);
+        const int32_t st = tstat[t];
+        h->types.push_back(st == 3 ? NBG_T_DOUBLE : NBG_T_INT);
+        h->host.emplace_back(8);
+        if (st == 3) {
+          const double avg = double(tsum[t]) / double(int32_t(tcnt[t]));  // count_ is int32 (CommonUtils.h:51)
+          memcpy(h->host.back().data(), &avg, 8);
+        } else {
+          const int64_t v = st == 2 ? int64_t(int32_t(tcnt[t])) : tsum[t];
+          memcpy(h->host.back().data(), &v, 8);
+        }
+        h->str_off.push_back(nullptr);
+        continue;
+      }
+      const int i = so.second;
       const BoundCol& b = bc.c[i];
       const int64_t sum = int64_t(ha[size_t(2 * i)]);
       const int64_t cnt = int64_t(ha[size_t(2 * i + 1)]);

@@ -3,8 +3,9 @@ QueryStatsProcessor restatement, which is pinned by the reference's QueryStatsTe
 (src/storage/test/QueryStatsTest.cpp) in tests/test_oracle_storage.py.
 
 The device path takes the getBound scan with its filter push-down and reduces the kept edges on
-the GPU (k_bound_stats).  Tag (SOURCE/DEST) columns are §8f-1 and rejected as unsupported here,
-so the known-answer check uses the fixture's edge columns (col_2i summed over 210 edges = 2i*210).
+the GPU (k_bound_stats); SOURCE/DEST tag columns reduce the request entries' vertex rows
+(QueryStatsProcessor.cpp:69-82).  Known answers: QueryStatsTest's checkResponse (AVG of
+tag_3001_col_0 = 0.0 and of tag_3003_col_2 = 2.0; SUM of col_2i over 210 edges = 2i * 210).
 """
 import numpy as np
 import pytest
@@ -34,6 +35,8 @@ def same(a, b):
 def qs():
     sp = GraphSpace(6)
     sp.set_edge_schema(F.EDGE_TYPE, F.qb_edge_schema())
+    for tag in range(3001, 3010):
+        sp.set_tag_schema(tag, str(tag), F.qb_tag_schema(tag))
     for part, data in F.qs_kv_parts().items():
         sp.load_part(part, data)
     sp.finalize()
@@ -77,8 +80,47 @@ def test_stats_validation(qs):
     assert g.n_rows == 0 and sorted(g.failed) == sorted(r.failed()) == [(0, -23), (1, -23), (2, -23)]
     g = sp.bound_stats(F.EDGE_TYPE, parts, vids, [("no_such", O.EDGE, 0)], [COUNT])
     assert sorted(g.failed) == [(0, -23), (1, -23), (2, -23)]
-    with pytest.raises(NbgError):  # tag columns are §8f-1
-        sp.bound_stats(F.EDGE_TYPE, parts, vids, [("tag_3001_col_0", O.SOURCE, 3001)], [AVG])
+    # tag columns: unknown tag, unknown prop, SUM / AVG over a STRING prop (validOperation)
+    for cols, stats in (([("tag_3001_col_0", O.SOURCE, 4242)], [AVG]),
+                        ([("no_such", O.SOURCE, 3001)], [COUNT]),
+                        ([("tag_3001_col_3", O.SOURCE, 3001)], [SUM]),
+                        ([("col_0", O.EDGE, 0), ("tag_3001_col_4", O.DEST, 3001)], [SUM, AVG])):
+        g = sp.bound_stats(F.EDGE_TYPE, parts, vids, cols, stats)
+        r = st.bound_stats(F.EDGE_TYPE, parts, vids, cols, stats)
+        assert g.n_rows == 0 and sorted(g.failed) == sorted(r.failed()), cols
+        assert len(g.failed) == 3
+
+
+def test_stats_fixture_all_columns(qs):
+    """QueryStatsTest StatsSimpleTest's full request (2 SOURCE tag columns with AVG + 5 edge
+    columns with SUM) and checkResponse's expected values (QueryStatsTest.cpp:88-135)"""
+    sp, st = qs
+    parts, vids, cols, stats = F.qs_request()
+    g = sp.bound_stats(F.EDGE_TYPE, parts, vids, cols, stats)
+    assert g.failed == [] and g.n_rows == 1
+    assert g.types == [O.DOUBLE, O.DOUBLE] + [O.INT] * 5
+    assert g.rows()[0] == (0.0, 2.0) + tuple(i * 2 * 210 for i in range(5))
+    r = st.bound_stats(F.EDGE_TYPE, parts, vids, cols, stats)
+    same(g.rows()[0], r.rows()[0])
+
+
+def test_stats_tag_columns_vs_oracle(qs):
+    """tag columns mixed with edge columns and a filter, every stat, SOURCE and DEST owners,
+    duplicate entries, a vertex without rows, entries whose part does not hold the vertex's row,
+    a part out of range (failed, its entries not counted)"""
+    sp, st = qs
+    parts, vids, _, _ = F.qs_request()
+    parts = list(parts) + [0, 0, 1, 2, 1, 9]
+    vids = list(vids) + [3, 3, 5, 999, 20, 4]
+    cols = [("tag_3002_col_1", O.SOURCE, 3002), ("col_3", O.EDGE, 0), ("tag_3005_col_2", O.DEST, 3005),
+            ("tag_3007_col_5", O.SOURCE, 3007), ("tag_3002_col_1", O.SOURCE, 3002), ("_dst", O.EDGE, 0)]
+    stats = [SUM, AVG, AVG, COUNT, COUNT, COUNT]
+    for f in (b"", (X.AliasProp("e101", "col_3") > 2).encode()):
+        g = sp.bound_stats(F.EDGE_TYPE, parts, vids, cols, stats, f)
+        r = st.bound_stats(F.EDGE_TYPE, parts, vids, cols, stats, filt=f)
+        assert sorted(g.failed) == sorted(r.failed())
+        same(g.rows()[0], r.rows()[0])
+        assert g.types == [O.INT, O.DOUBLE, O.DOUBLE, O.INT, O.INT, O.INT]
 
 
 def test_stats_empty_request_and_no_rows(qs):
