@@ -247,6 +247,9 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
+    names = {2: "expand", 3: "probe", 4: "sweep"}
+    launches = [{"kind": names.get(h["mode_id"], h["mode"]), "ms": round(h["ms"], 4), "x": h["c"][0], "entries": h["c"][1],
+                 "claims": h["c"][2], "iter": h["c"][4]} for h in tm["hops"]]
     # parity: the last timed result (host copy) against the committed digest
     hops, paths, srcs = r.hops, r.paths, r.src
     if dist is not None:
@@ -297,6 +300,7 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
             "reachable": int((np.asarray(hops) >= 0).sum()),
             "hops_histogram": {int(h): int((np.asarray(hops) == h).sum()) for h in sorted(set(np.asarray(hops).tolist()))},
             "bfs_iterations": iters,
+            "launches": launches,
             "snapshot_build_s": round(build_s, 2),
         },
         "parity": parity,

@@ -262,7 +262,10 @@ int32_t nbg_shortest_path(nbg_ctx* ctx, int32_t edge_type, const int64_t* src,
  * over the transposed CSR.  c[]: top-down {frontier, entries, next frontier, 0, 0, 0};
  * bottom-up {found, next-hop out-degree sum, slab words read, rows scanned past the slab,
  * entries read past the slab, predicate values read past the slab, first-pass frontier probes
- * answered by L2, first-pass probes answered from the LDS hub copy}.                       */
+ * answered by L2, first-pass probes answered from the LDS hub copy}.
+ * nbg_shortest_path records one entry per launch instead: mode 2 = BFS expansion, 3 = meet
+ * probe, 4 = sweep; c[] = {tuples, adjacency entries, claims, meets so far, iteration,
+ * active pairs, 0, 0}.                                                                      */
 typedef struct {
   int32_t mode;
   int32_t final_hop;
@@ -285,7 +288,7 @@ typedef struct {
   int32_t bu_steps;       /* steps that ran bottom-up over the transposed CSR               */
   double comm_ms;         /* time in frontier exchanges / reductions between ranks          */
   uint64_t comm_bytes;    /* bytes this rank sent to other ranks                            */
-  int32_t n_hops;         /* entries of hops[] filled (nbg_go only)                          */
+  int32_t n_hops;         /* entries of hops[] filled (nbg_go, nbg_shortest_path)            */
   nbg_hop_stat hops[NBG_MAX_HOP_STATS];
 } nbg_timing;
 int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out);

@@ -31,6 +31,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 
 #include "device_common.h"
@@ -259,7 +260,9 @@ __global__ void k_sp_select(const uint64_t* __restrict__ live, int64_t nl, int32
       side = t_side(t);
       const int32_t s = st.state[p];
       if (sweep) {
-        go = s == SP_MET && int32_t(t_lvl(t)) < st.res[p];
+        // sweep = 2: stop one level short of src (the walk from src never reads dist_B(src),
+        // and the in-lists of src's shortest-path out-neighbours are typically hub rows)
+        go = s == SP_MET && int32_t(t_lvl(t)) < st.res[p] - (sweep - 1);
       } else if (s == SP_ACTIVE) {
         go = uint32_t(st.side[p]) == side;
         stay = !go;
@@ -592,6 +595,116 @@ __global__ __launch_bounds__(kWalkT) void k_sp_walk(SpState st, const int32_t* g
   }
 }
 
+// ---- edge-balanced walk: one step of every walking pair per launch --------------------------
+// Step i of pair p scans the out-row of its current vertex cur[p] for the smallest vid w with
+// dist_B(w) = L - i - 1.  The rows of all pairs are one flattened range cut into kTileE-entry
+// tiles (the expansion's tile-row table and LDS owner map), so a hub row on a path is spread over
+// many workgroups instead of one.  The last step (need = 0) is dst itself and is never scanned.
+__global__ void k_sp_walk_front(SpState st, int32_t i, const int32_t* cur, SpCsr gout, int64_t* wdeg,
+                                long long* best) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p > st.B) return;
+  int64_t d = 0;
+  if (p < st.B) {
+    best[p] = LLONG_MAX;
+    if (st.state[p] == SP_MET && st.res[p] - 1 > i && cur[p] >= 0) d = sp_deg(gout, uint32_t(cur[p]));
+  }
+  wdeg[p] = d;  // wdeg[B] = 0: the scan's total
+}
+
+// wave-aggregated atomicMin(arr[key], v) over the lanes with act
+__device__ inline void wave_min_keyed(long long* arr, uint32_t key, long long v, bool act) {
+  const int lane = threadIdx.x & 63;
+  uint64_t m = __ballot(act);
+  while (m) {
+    const int leader = __ffsll((long long)m) - 1;
+    const uint32_t k = uint32_t(__shfl(int(key), leader));
+    const bool mine = act && key == k;
+    long long x = mine ? v : LLONG_MAX;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const long long y = __shfl_xor(x, o);
+      x = y < x ? y : x;
+    }
+    if (lane == leader && x != LLONG_MAX) atomicMin(arr + k, x);
+    m &= ~__ballot(mine);
+    act = act && !mine;
+  }
+}
+
+__global__ __launch_bounds__(kT) void k_sp_walk_scan(SpState st, int32_t i, const int32_t* cur, const int64_t* off,
+                                                     const int32_t* tile_row, SpCsr gout, const uint8_t* dist_b,
+                                                     const int64_t* vid_of, int64_t n, int64_t lo, long long* best) {
+  __shared__ int32_t s_off[kTileE + 1];
+  __shared__ int64_t s_rs[kTileE];
+  __shared__ int32_t s_pair[kTileE];
+  __shared__ int64_t s_hdr[2];
+  __shared__ int32_t s_scan[kT / 64];
+  const int64_t nP = st.B;
+  const int64_t E = off[nP];
+  const int64_t ntiles = (E + kTileE - 1) / kTileE;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t e0 = t * kTileE;
+    const int64_t e1 = min(e0 + int64_t(kTileE), E);
+    if (threadIdx.x == 0) {
+      int64_t i0, cn;
+      tile_entries(tile_row, off, nP, t, e1, E, i0, cn);
+      s_hdr[0] = i0;
+      s_hdr[1] = cn;
+    }
+    __syncthreads();
+    const int64_t i0 = s_hdr[0];
+    const int cnt_k = int(s_hdr[1]);  // <= B + 1 <= kTileE (the host caps the batch for this)
+    for (int k = threadIdx.x; k <= cnt_k; k += kT) {
+      const int64_t o = off[i0 + k];
+      s_off[k] = int32_t(min(o - e0, int64_t(kTileE + 1)));
+      if (k < cnt_k) {
+        const int32_t v = cur[i0 + k];
+        s_pair[k] = int32_t(i0 + k);
+        s_rs[k] = (v >= 0 ? gout.row_ptr[v] : 0) - o;
+      }
+    }
+    __syncthreads();
+    tile_owner_map<kTileE, kT>(s_off, cnt_k, s_scan);
+    for (int r = 0; r < kIt; r++) {
+      const int j = threadIdx.x + r * kT;
+      const int64_t e = e0 + j;
+      const bool valid = e < e1;
+      uint32_t p = 0;
+      long long cand = LLONG_MAX;
+      bool hit = false;
+      if (valid) {
+        const int k = s_off[j];
+        p = uint32_t(s_pair[k]);
+        const uint32_t w = uint32_t(int64_t(gout.col[s_rs[k] + e]) - lo);
+        const uint8_t need = uint8_t(st.res[p] - i - 1);
+        if (dist_b[didx(st, p, w, n)] == need) {
+          hit = true;
+          cand = vid_of[lo + w];
+        }
+      }
+      wave_min_keyed(best, p, cand, hit);
+    }
+    __syncthreads();
+  }
+}
+
+// the step's choice: path vid and the next current vertex (vid -> gidx through the vertex hash)
+__global__ void k_sp_walk_pick(SpState st, int32_t i, int32_t* cur, const long long* best, const int64_t* path_off,
+                               int64_t* path, const int64_t* ht_keys, const int32_t* ht_vals, uint64_t ht_mask,
+                               bool ht_has_min, int32_t ht_min_gidx, int64_t lo, unsigned long long* cnt) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= st.B || st.state[p] != SP_MET || st.res[p] - 1 <= i || cur[p] < 0) return;
+  const long long b = best[p];
+  if (b == LLONG_MAX) {  // in-edge keys without the mirrored out-edge: the definition does not hold
+    atomicAdd(cnt + C_WALKERR, 1ull);
+    cur[p] = -1;
+    return;
+  }
+  path[path_off[p] + i + 1] = int64_t(b);
+  cur[p] = ht_lookup(ht_keys, ht_vals, ht_mask, int64_t(b), ht_has_min, ht_min_gidx) - int32_t(lo);
+}
+
 // reset every claimed distance byte of the batch
 __global__ void k_sp_clear(const uint64_t* arena, int64_t m, uint8_t* d0, uint8_t* d1, int64_t n, SpState st) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
@@ -864,11 +977,20 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       NBG_HIP(hipGetLastError());
       hipEventRecord(c.ev[3], c.stream);
     };
-    auto expand_time = [&]() {
+    auto expand_time = [&]() -> double {
       float ms = 0;
       hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
       c.timing.expand_ms += ms;
       c.timing.expand_launches++;
+      return ms;
+    };
+    // per-launch record in the hop stats: mode 2 = BFS expansion, 3 = meet probe, 4 = sweep;
+    // c[] = {X tuples, adjacency entries, claims, meets (total so far), iteration, active pairs}
+    auto sp_hop = [&](int32_t mode, double ms, int64_t nX, int64_t E, int64_t claims, int64_t it, int64_t act) {
+      const unsigned long long c8[8] = {(unsigned long long)nX, (unsigned long long)E, (unsigned long long)claims,
+                                        hc[C_MEET], (unsigned long long)it, (unsigned long long)act, 0, 0};
+      c.timing.hop(mode, false, ms, c8);
+      c.timing.name_last_hop(mode == 3 ? "nbg::(anonymous namespace)::k_sp_probe" : "nbg::(anonymous namespace)::k_sp_expand");
     };
     // pairs (of this batch) matching a host predicate over (state, pside, met) -> W.plist
     auto pair_list = [&](auto pred) -> int32_t {
@@ -963,6 +1085,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         c.timing.expand_launches++;
         c.timing.edges_scanned += hc[C_PE];
         c.timing.expand_bytes += uint64_t(nX) * 24 + hc[C_PE] * 5;
+        sp_hop(3, pms, nX, int64_t(hc[C_PE]), 0, iter, active);
         E = int64_t(hc[C_XE]);
         n_meet = int64_t(hc[C_MEET]);
         if (int64_t(hc[C_ARENA]) > W.cap_arena) arena_lost = true;
@@ -982,10 +1105,11 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       k_sp_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, max_steps, 0, iter, cnt);
       NBG_HIP(hipGetLastError());
       sync_counters();
-      if (E > 0) expand_time();
+      const double ems = E > 0 ? expand_time() : 0.0;
       const int64_t cl = int64_t(hc[C_LIVE0] + hc[C_LIVE1]) - carried[0] - carried[1];
       last_claims = cl;
       c.timing.expand_bytes += uint64_t(nX) * 32 + uint64_t(E) * 5 + uint64_t(cl) * 26;
+      if (E > 0) sp_hop(2, ems, nX, E, cl, iter, active);
       if (int64_t(hc[C_ARENA]) > W.cap_arena) arena_lost = true;  // the batch end resets every byte instead
       n_arena = std::min<int64_t>(int64_t(hc[C_ARENA]), W.cap_arena);
       for (int s = 0; s < 2; s++) {
@@ -1016,6 +1140,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
 
     // sweep: extend dist_B from the meet sets toward src along shortest paths only
     int64_t n_sw = n_meet;
+    const int32_t sweep_mode = c.opt("sp_sweep_src", 0) ? 1 : 2;
     DevBuf* cur = &W.meet;
     int nxt = 0;
     for (int32_t j = 1; n_sw > 0; j++) {
@@ -1023,7 +1148,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       NBG_HIP(hipMemsetAsync(cnt + C_X, 0, 24, c.stream));
       NBG_HIP(hipMemsetAsync(cnt + C_SWEEP, 0, 16, c.stream));  // C_SWEEP, C_XE
       refresh(nullptr, 0);
-      k_sp_select<<<grid_n(n_sw), 256, 0, c.stream>>>(cur->as<uint64_t>(), n_sw, 1, st, gout, gin, W.X.as<uint64_t>(),
+      k_sp_select<<<grid_n(n_sw), 256, 0, c.stream>>>(cur->as<uint64_t>(), n_sw, sweep_mode, st, gout, gin, W.X.as<uint64_t>(),
                                                        W.Xdeg.as<int64_t>(), W.cap_x, bf, cnt);
       NBG_HIP(hipGetLastError());
       sync_counters();
@@ -1037,8 +1162,9 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       launch_scan(nX);
       launch_expand(nX, E, 1);
       sync_counters();
-      expand_time();
+      const double sms = expand_time();
       c.timing.expand_bytes += uint64_t(nX) * 32 + uint64_t(E) * 6 + hc[C_SWEEP] * 18;
+      sp_hop(4, sms, nX, E, int64_t(hc[C_SWEEP]), j, 0);
       if (int64_t(hc[C_ARENA]) > W.cap_arena) arena_lost = true;
       n_arena = std::min<int64_t>(int64_t(hc[C_ARENA]), W.cap_arena);
       if (int64_t(hc[C_SWEEP]) > W.cap_sweep[nxt]) {
@@ -1072,15 +1198,56 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       dpath.alloc(size_t(plen) * 8);
       NBG_HIP(hipMemcpyAsync(doff.p, boff.data(), size_t(nb + 1) * 8, hipMemcpyHostToDevice, c.stream));
       NBG_HIP(hipMemsetAsync(cnt + C_WALKERR, 0, 8, c.stream));
-      k_sp_walk<<<int(nb), kWalkT, 0, c.stream>>>(st, dgs, doff.as<int64_t>(), dpath.as<int64_t>(), gout, d1,
-                                                         vid_of, n, lo, cnt);
+      int32_t maxL = 0;
+      for (int64_t p = 0; p < nb; p++)
+        if (hstate[size_t(p)] == SP_MET) maxL = std::max(maxL, hres_b[size_t(p)]);
+      if (c.opt("sp_walk_wg", 0) || nb >= kTileE) {  // a tile stages at most kTileE pair entries
+        k_sp_walk<<<int(nb), kWalkT, 0, c.stream>>>(st, dgs, doff.as<int64_t>(), dpath.as<int64_t>(), gout, d1,
+                                                    vid_of, n, lo, cnt);
+      } else if (maxL >= 2) {
+        // walk state: cur [B], best [B], degrees / offsets [B + 1], tile rows (all pairs' rows <= nnz)
+        const int64_t max_tiles = (cout->nnz + kTileE - 1) / kTileE + nb + 2;
+        const size_t wbytes = size_t(nb) * 4 + 64 + size_t(nb) * 8 + 64 + 2 * (size_t(nb + 1) * 8 + 64) +
+                              size_t(max_tiles) * 4 + 64;
+        DevBuf wk;
+        wk.alloc(wbytes);
+        char* q = static_cast<char*>(wk.p);
+        auto take = [&](size_t b) { char* r = q; q += (b + 63) & ~size_t(63); return r; };
+        int32_t* dcur = reinterpret_cast<int32_t*>(take(size_t(nb) * 4));
+        long long* dbest = reinterpret_cast<long long*>(take(size_t(nb) * 8));
+        int64_t* wdeg = reinterpret_cast<int64_t*>(take(size_t(nb + 1) * 8));
+        int64_t* woff = reinterpret_cast<int64_t*>(take(size_t(nb + 1) * 8));
+        int32_t* wtr = reinterpret_cast<int32_t*>(take(size_t(max_tiles) * 4));
+        NBG_HIP(hipMemcpyAsync(dcur, dgs, size_t(nb) * 4, hipMemcpyDeviceToDevice, c.stream));
+        size_t tb = 0;
+        NBG_HIP(rocprim::exclusive_scan(nullptr, tb, wdeg, woff, int64_t(0), size_t(nb + 1), rocprim::plus<int64_t>(),
+                                        c.stream));
+        c.ws_tmp.ensure(tb);
+        const int wgrid = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("sp_grid", 256 * 8), max_tiles)));
+        for (int32_t i = 0; i + 1 < maxL; i++) {
+          k_sp_walk_front<<<grid_n(nb + 1, 1 << 20), 256, 0, c.stream>>>(st, i, dcur, gout, wdeg, dbest);
+          NBG_HIP(rocprim::exclusive_scan(c.ws_tmp.p, tb, wdeg, woff, int64_t(0), size_t(nb + 1),
+                                          rocprim::plus<int64_t>(), c.stream));
+          k_tile_rows<kTileE><<<grid_n(nb), 256, 0, c.stream>>>(woff, nb, wtr);
+          k_sp_walk_scan<<<wgrid, kT, 0, c.stream>>>(st, i, dcur, woff, wtr, gout, d1, vid_of, n, lo, dbest);
+          k_sp_walk_pick<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(
+              st, i, dcur, dbest, doff.as<int64_t>(), dpath.as<int64_t>(), c.ht_keys.as<int64_t>(),
+              c.ht_vals.as<int32_t>(), uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, lo, cnt);
+          NBG_HIP(hipGetLastError());
+        }
+        sync_counters();  // wk is released at scope end: the walk must have drained
+      }
       NBG_HIP(hipGetLastError());
       NBG_HIP(hipMemcpyAsync(hpath.data() + base, dpath.p, size_t(plen) * 8, hipMemcpyDeviceToHost, c.stream));
       sync_counters();
       if (hc[C_WALKERR])
         throw Error(NBG_E_UNKNOWN, "shortest path: in-edge keys without mirrored out-edges on a shortest path");
-      for (int64_t p = 0; p < nb; p++)  // src == dst (vertex possibly unknown): the path is [src]
-        if (hres[b0 + size_t(p)] == 0) hpath[base + size_t(boff[size_t(p)])] = src[b0 + size_t(p)];
+      for (int64_t p = 0; p < nb; p++) {  // the ends: src (also the whole path of src == dst) and dst
+        const int64_t L = hres[b0 + size_t(p)];
+        if (L < 0) continue;
+        hpath[base + size_t(boff[size_t(p)])] = src[b0 + size_t(p)];
+        if (L > 0) hpath[base + size_t(boff[size_t(p)] + L)] = dst[b0 + size_t(p)];
+      }
     }
     for (int64_t p = 0; p < nb; p++) hoff.push_back(hoff.back() + boff[size_t(p) + 1] - boff[size_t(p)]);
     // reset the batch's distance bytes

@@ -228,7 +228,8 @@ class GraphSpace:
         t = _lib.Timing()
         self._check(self.L.nbg_last_timing(self.h, C.byref(t)))
         d = {k: getattr(t, k) for k, _ in t._fields_ if k not in ("hops", "n_hops")}
-        d["hops"] = [{"mode": "bottom-up" if h.mode else "top-down", "final": bool(h.final_hop), "ms": h.ms,
+        modes = {0: "top-down", 1: "bottom-up", 2: "sp-expand", 3: "sp-probe", 4: "sp-sweep"}
+        d["hops"] = [{"mode": modes.get(h.mode, h.mode), "mode_id": h.mode, "final": bool(h.final_hop), "ms": h.ms,
                       "bytes": int(h.bytes), "c": list(h.c), "kernel_ms": h.kernel_ms,
                       "kernel_bytes": int(h.kernel_bytes),
                       "kernels": [k for k in h.kernels.decode().split("; ") if k] or ["nbg::k_expand"]}
