@@ -220,6 +220,11 @@ struct EdgeSpace {
   bool has_tr = false;
   bool has_t_eid = false;
   int64_t out_nnz_global = -1;  // sum of out.nnz over ranks (direction heuristic)
+  // streamed RMAT (one rank, graphs past the tuple stage's 2^32 cap): gen_rmat only records the
+  // generator's parameters and finalize builds the CSRs bucket by bucket from regenerated samples
+  bool rmat_stream = false;
+  int32_t rmat_scale = 0, rmat_ef = 0;
+  uint64_t rmat_seed = 0;
   // bottom-up slab: the first slab_k entries of every transposed row, slot-major [k][row]
   int32_t slab_k = 0;
   DevBuf slab_col;                 // int32, -1 past the row's end

@@ -578,6 +578,22 @@ __device__ inline int64_t rmat_vid(uint64_t idx, uint64_t smix) {
   return int64_t(x);
 }
 
+// sample i of the generator: (u, v) in the index space [0, 2^scale)
+__device__ inline void rmat_sample(uint64_t i, int32_t scale, uint64_t seed, uint64_t& u, uint64_t& v) {
+  u = 0;
+  v = 0;
+  for (int32_t l = 0; l < scale; l += 2) {
+    uint64_t h = splitmix64(seed ^ (0xD6E8FEB86659FD93ull * (i + 1)) ^ (0xA0761D6478BD642Full * uint64_t(l + 1)));
+    rmat_pick(uint32_t(h >> 32), u, v);
+    if (l + 1 < scale) rmat_pick(uint32_t(h), u, v);
+  }
+}
+// the edge prop of sample (s, d): follow.weight (same value for every duplicate of the pair)
+__device__ inline int64_t rmat_weight(int64_t s, int64_t d, uint64_t seed) {
+  const uint64_t du = uint64_t(d);
+  return int64_t(splitmix64(uint64_t(s) ^ ((du << 32) | (du >> 32)) ^ seed) % 1000);
+}
+
 __global__ void k_gen_rmat(int64_t lo, int64_t hi, int32_t scale, uint64_t seed, uint64_t smix,
                            int32_t parts, int32_t world, int32_t rank, int64_t* osrc, int64_t* odst,
                            int64_t* oweight, unsigned long long* ocnt, int64_t* isrc, int64_t* idst,
@@ -590,13 +606,8 @@ __global__ void k_gen_rmat(int64_t lo, int64_t hi, int32_t scale, uint64_t seed,
     bool valid = j < n;
     int64_t s = 0, d = 0;
     if (valid) {
-      uint64_t i = uint64_t(lo + j);
-      uint64_t u = 0, v = 0;
-      for (int32_t l = 0; l < scale; l += 2) {
-        uint64_t h = splitmix64(seed ^ (0xD6E8FEB86659FD93ull * (i + 1)) ^ (0xA0761D6478BD642Full * uint64_t(l + 1)));
-        rmat_pick(uint32_t(h >> 32), u, v);
-        if (l + 1 < scale) rmat_pick(uint32_t(h), u, v);
-      }
+      uint64_t u, v;
+      rmat_sample(uint64_t(lo + j), scale, seed, u, v);
       s = rmat_vid(u, smix);
       d = rmat_vid(v, smix);
     }
@@ -607,8 +618,7 @@ __global__ void k_gen_rmat(int64_t lo, int64_t hi, int32_t scale, uint64_t seed,
     if (is_out && so < cap) {  // counts keep growing past cap: the host re-runs with the exact size
       osrc[so] = s;
       odst[so] = d;
-      uint64_t du = uint64_t(d);
-      oweight[so] = int64_t(splitmix64(uint64_t(s) ^ ((du << 32) | (du >> 32)) ^ seed) % 1000);
+      oweight[so] = rmat_weight(s, d, seed);
     }
     if (is_in && si < cap) {  // in-edge key (dst, -type, rank, src): key src = d, key dst = s
       isrc[si] = d;
@@ -630,7 +640,18 @@ void snapshot_gen_rmat(Ctx& c, int32_t scale, int32_t ef, uint64_t seed, int32_t
   int64_t expect = c.world == 1 ? E : E / c.world + E / (4 * c.world) + (1 << 20);
   Staging& so = es.out_stage;
   Staging& si = es.in_stage;
-  if (so.n != 0 || si.n != 0) throw Error(NBG_E_STATE, "RMAT must be the only source of this edge type");
+  if (so.n != 0 || si.n != 0 || es.rmat_stream) throw Error(NBG_E_STATE, "RMAT must be the only source of this edge type");
+  // streamed build: forced with rmat_stream = 1, automatic on one rank once the tuple stage
+  // would pass its 2^32 cap (2^31 samples and up: two CSR directions of 40+ B tuples)
+  const int64_t stream_opt = c.opt("rmat_stream", -1);
+  if (c.world == 1 && (stream_opt > 0 || (stream_opt < 0 && E >= (int64_t(1) << 31)))) {
+    if (c.opt("writable", 0)) throw Error(NBG_E_UNSUPPORTED, "streamed RMAT snapshot is read-only (writable = 1)");
+    es.rmat_stream = true;
+    es.rmat_scale = scale;
+    es.rmat_ef = ef;
+    es.rmat_seed = seed;
+    return;
+  }
   auto alloc_stage = [&](Staging& s, int64_t cap, bool props) {
     s.src.alloc(size_t(cap) * 8);
     s.dst.alloc(size_t(cap) * 8);
@@ -1866,10 +1887,360 @@ static void build_tag_columns(Ctx& c) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Streamed RMAT build (one rank).  The tuple stage holds 40+ bytes per sample in each CSR
+// direction and indexes tuples with 32-bit permutations, so RMAT-28 (2^32 samples) cannot pass
+// through it.  Here the generator is re-run instead of stored: one counting pass gives the vertex
+// set and the per-vertex sample counts, the vertex numbering is the staged build's (vids sorted,
+// then by descending sample out-degree), and each CSR direction is built in src-gidx buckets of
+// at most rmat_bucket samples: regenerate, keep the bucket's samples as 64-bit keys
+// (local src << 32 | bytewise rank of dst), radix sort, unique (= the version / identical-key
+// collapse of a generator that writes one version of rank 0), and emit row_ptr, col, the dst-vid
+// column and the weight (a function of (src, dst), recomputed).  Same CSR as the staged build.
+// ------------------------------------------------------------------------------------------
+__global__ void k_rmat_count(int64_t lo, int64_t hi, int32_t scale, uint64_t seed, uint8_t* present,
+                             uint32_t* odeg_u, uint32_t* ideg_u) {
+  for (int64_t i = lo + blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < hi; i += int64_t(gridDim.x) * blockDim.x) {
+    uint64_t u, v;
+    rmat_sample(uint64_t(i), scale, seed, u, v);
+    present[u] = 1;  // idempotent byte stores
+    present[v] = 1;
+    atomicAdd(odeg_u + u, 1u);
+    atomicAdd(ideg_u + v, 1u);
+  }
+}
+__global__ void k_rmat_vkeys(const uint32_t* idx, int64_t n, uint64_t smix, uint64_t* key) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    key[i] = uint64_t(rmat_vid(idx[i], smix)) ^ (1ull << 63);
+}
+__global__ void k_rmat_degkey(const uint32_t* idx, int64_t n, const uint32_t* odeg_u, uint32_t* key) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    key[i] = ~odeg_u[idx[i]];
+}
+// gidx g <-> index u; vid_of; per-gidx sample counts of both directions
+__global__ void k_rmat_number(const uint32_t* idx, int64_t n, uint64_t smix, const uint32_t* odeg_u,
+                              const uint32_t* ideg_u, int32_t* gidx_of_u, int64_t* vid_of, int64_t* ocnt,
+                              int64_t* icnt) {
+  for (int64_t g = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; g < n; g += int64_t(gridDim.x) * blockDim.x) {
+    const uint32_t u = idx[g];
+    gidx_of_u[u] = int32_t(g);
+    vid_of[g] = rmat_vid(u, smix);
+    ocnt[g] = odeg_u[u];
+    icnt[g] = ideg_u[u];
+  }
+}
+// brank_u[u] = bytewise rank of u's vid; gidx_of_rank = its inverse over the gidx space
+__global__ void k_rmat_rank_maps(const uint32_t* idx, int64_t n, const uint32_t* brank, uint32_t* brank_u,
+                                 int32_t* gidx_of_rank) {
+  for (int64_t g = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; g < n; g += int64_t(gridDim.x) * blockDim.x) {
+    brank_u[idx[g]] = brank[g];
+    gidx_of_rank[brank[g]] = int32_t(g);
+  }
+}
+// bucket starts: row g opens bucket excl[g] / cap when that differs from row g - 1's
+__global__ void k_rmat_cuts(const int64_t* excl, int64_t n, int64_t cap, int64_t* cut) {
+  for (int64_t g = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; g < n; g += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t k = excl[g] / cap;
+    if (g == 0 || excl[g - 1] / cap != k) cut[k] = g;
+  }
+}
+// the samples of bucket [ga, gb) of one direction (out: key src u, in: key src v) as sort keys
+__global__ void k_rmat_bucket(int64_t lo, int64_t hi, int32_t scale, uint64_t seed, int32_t dir,
+                              const int32_t* gidx_of_u, const uint32_t* brank_u, int64_t ga, int64_t gb, uint64_t* keys,
+                              unsigned long long* cnt, int64_t cap) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int64_t rounds = (hi - lo + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    const int64_t i = lo + r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    bool take = false;
+    uint64_t key = 0;
+    if (i < hi) {
+      uint64_t u, v;
+      rmat_sample(uint64_t(i), scale, seed, u, v);
+      const uint64_t sidx = dir ? v : u, didx = dir ? u : v;
+      const int64_t g = gidx_of_u[sidx];
+      take = g >= ga && g < gb;
+      if (take) key = (uint64_t(g - ga) << 32) | brank_u[didx];
+    }
+    const int64_t slot = wave_append(cnt, take);
+    if (take && slot < cap) keys[slot] = key;
+  }
+}
+// CSR rows [ga, gb) from the bucket's sorted unique keys (entries base .. base + m)
+__global__ void k_rmat_emit(const uint64_t* keys, int64_t m, int64_t ga, int64_t nrows, int64_t base,
+                            const int32_t* gidx_of_rank, const int64_t* vid_of, uint64_t seed, int64_t* row_ptr,
+                            int32_t* col, int64_t* col_vid, int16_t* w16) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= m; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t prev = i == 0 ? -1 : int64_t(keys[i - 1] >> 32);
+    const int64_t cur = i == m ? nrows : int64_t(keys[i] >> 32);
+    for (int64_t r = prev + 1; r <= cur; r++) row_ptr[ga + r] = base + i;
+    if (i == m) continue;
+    const int32_t d = gidx_of_rank[uint32_t(keys[i])];
+    col[base + i] = d;
+    if (col_vid) {
+      const int64_t dv = vid_of[d];
+      col_vid[base + i] = dv;
+      w16[base + i] = int16_t(rmat_weight(vid_of[ga + cur], dv, seed));
+    }
+  }
+}
+__global__ void k_i16_to_i8(const int16_t* in, int8_t* out, int64_t m) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = int8_t(in[i]);
+}
+
+static void finalize_rmat_stream(Ctx& c, EdgeSpace& es) {
+  if (c.world != 1) throw Error(NBG_E_UNSUPPORTED, "streamed RMAT build on more than one rank");
+  if (c.edges.size() != 1 || !c.tags.empty())
+    throw Error(NBG_E_UNSUPPORTED, "streamed RMAT must be the snapshot's only edge type, without tags");
+  const int32_t scale = es.rmat_scale;
+  const uint64_t seed = es.rmat_seed;
+  const int64_t E = int64_t(es.rmat_ef) << scale;
+  const int64_t NU = int64_t(1) << scale;
+  const uint64_t smix = splitmix64(seed) & ((1ull << 63) - 1);
+  const int64_t chunk = int64_t(1) << 28;
+  auto sample_grid = [](int64_t n) { return int(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 256 * 64))); };
+  // 1. counting pass
+  DevBuf present, odeg_u, ideg_u;
+  present.alloc(size_t(NU));
+  odeg_u.alloc(size_t(NU) * 4);
+  ideg_u.alloc(size_t(NU) * 4);
+  NBG_HIP(hipMemsetAsync(present.p, 0, size_t(NU), c.stream));
+  NBG_HIP(hipMemsetAsync(odeg_u.p, 0, size_t(NU) * 4, c.stream));
+  NBG_HIP(hipMemsetAsync(ideg_u.p, 0, size_t(NU) * 4, c.stream));
+  for (int64_t lo = 0; lo < E; lo += chunk) {
+    const int64_t hi = std::min(E, lo + chunk);
+    k_rmat_count<<<sample_grid(hi - lo), 256, 0, c.stream>>>(lo, hi, scale, seed, present.as<uint8_t>(),
+                                                             odeg_u.as<uint32_t>(), ideg_u.as<uint32_t>());
+  }
+  NBG_HIP(hipGetLastError());
+  // 2. vertex set in the staged build's numbering: vids ascending (signed), then stable by
+  // descending sample out-degree (order_by_degree), unless degree_order = 0
+  DevBuf idxA, idxB, cntb;
+  idxA.alloc(size_t(NU) * 4);
+  cntb.alloc(8);
+  {
+    size_t tb = 0;
+    rocprim::counting_iterator<uint32_t> it(0);
+    NBG_HIP(rocprim::select(nullptr, tb, it, present.as<uint8_t>(), idxA.as<uint32_t>(), cntb.as<uint64_t>(),
+                            size_t(NU), c.stream));
+    c.ws_tmp.ensure(tb);
+    NBG_HIP(rocprim::select(c.ws_tmp.p, tb, it, present.as<uint8_t>(), idxA.as<uint32_t>(), cntb.as<uint64_t>(),
+                            size_t(NU), c.stream));
+  }
+  uint64_t hn = 0;
+  NBG_HIP(hipMemcpyAsync(&hn, cntb.p, 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  present.release();
+  const int64_t n = int64_t(hn);
+  if (n == 0) throw Error(NBG_E_INVALID_ARG, "empty RMAT graph");
+  idxB.alloc(size_t(n) * 4);
+  {
+    DevBuf k1, k2;
+    k1.alloc(size_t(n) * 8);
+    k2.alloc(size_t(n) * 8);
+    k_rmat_vkeys<<<grid_for(n), 256, 0, c.stream>>>(idxA.as<uint32_t>(), n, smix, k1.as<uint64_t>());
+    radix_pairs<uint64_t, uint32_t>(c, k1.as<uint64_t>(), k2.as<uint64_t>(), idxA.as<uint32_t>(), idxB.as<uint32_t>(),
+                                    n, 64);
+  }
+  uint32_t* order = idxB.as<uint32_t>();
+  if (c.opt("degree_order", 1)) {
+    DevBuf d1, d2;
+    d1.alloc(size_t(n) * 4);
+    d2.alloc(size_t(n) * 4);
+    k_rmat_degkey<<<grid_for(n), 256, 0, c.stream>>>(idxB.as<uint32_t>(), n, odeg_u.as<uint32_t>(), d1.as<uint32_t>());
+    radix_pairs<uint32_t, uint32_t>(c, d1.as<uint32_t>(), d2.as<uint32_t>(), idxB.as<uint32_t>(), idxA.as<uint32_t>(),
+                                    n, 32);
+    order = idxA.as<uint32_t>();
+  }
+  // 3. vertex map (one rank: base = [0, n padded to 64])
+  c.counts.assign(1, n);
+  c.base.assign(2, 0);
+  c.base[1] = (n + 63) / 64 * 64;
+  c.n_global = c.base[1];
+  c.n_vertices = n;
+  if (c.n_global >= (int64_t(1) << 31)) throw Error(NBG_E_UNSUPPORTED, "more than 2^31 vertices");
+  c.vid_of.alloc(size_t(c.n_global) * 8);
+  fill<int64_t>(c, c.vid_of.as<int64_t>(), INT64_MIN, c.n_global);
+  DevBuf gidx_of_u, ocnt, icnt;
+  gidx_of_u.alloc(size_t(NU) * 4);
+  ocnt.alloc(size_t(c.n_global + 1) * 8);
+  icnt.alloc(size_t(c.n_global + 1) * 8);
+  NBG_HIP(hipMemsetAsync(ocnt.p, 0, size_t(c.n_global + 1) * 8, c.stream));
+  NBG_HIP(hipMemsetAsync(icnt.p, 0, size_t(c.n_global + 1) * 8, c.stream));
+  k_rmat_number<<<grid_for(n), 256, 0, c.stream>>>(order, n, smix, odeg_u.as<uint32_t>(), ideg_u.as<uint32_t>(),
+                                                   gidx_of_u.as<int32_t>(), c.vid_of.as<int64_t>(), ocnt.as<int64_t>(),
+                                                   icnt.as<int64_t>());
+  odeg_u.release();
+  ideg_u.release();
+  int64_t cap = 1024;
+  while (cap < 2 * c.n_global) cap <<= 1;
+  c.ht_cap = cap;
+  c.ht_keys.alloc(size_t(cap) * 8);
+  c.ht_vals.alloc(size_t(cap) * 4);
+  fill<int64_t>(c, c.ht_keys.as<int64_t>(), INT64_MIN, cap);
+  DevBuf dmin;
+  dmin.alloc(4);
+  int32_t neg = -1;
+  NBG_HIP(hipMemcpyAsync(dmin.p, &neg, 4, hipMemcpyHostToDevice, c.stream));
+  k_ht_insert<<<grid_for(n), 256, 0, c.stream>>>(c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(), uint64_t(cap - 1),
+                                                 c.vid_of.as<int64_t>(), n, 0, dmin.as<int32_t>());
+  NBG_HIP(hipMemcpyAsync(&c.ht_min_gidx, dmin.p, 4, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  c.ht_has_min = c.ht_min_gidx >= 0;
+  // 4. bytewise rank of every vertex (row order = RocksDB key order), per index and inverted
+  DevBuf brank_u, gidx_of_rank;
+  {
+    const int64_t ng = c.n_global;
+    DevBuf k1, k2, i1, i2, brank;
+    k1.alloc(size_t(ng) * 8);
+    k2.alloc(size_t(ng) * 8);
+    i1.alloc(size_t(ng) * 4);
+    i2.alloc(size_t(ng) * 4);
+    brank.alloc(size_t(ng) * 4);
+    k_bswap_keys<<<grid_for(ng), 256, 0, c.stream>>>(c.vid_of.as<int64_t>(), k1.as<uint64_t>(), i1.as<uint32_t>(), ng);
+    radix_pairs<uint64_t, uint32_t>(c, k1.as<uint64_t>(), k2.as<uint64_t>(), i1.as<uint32_t>(), i2.as<uint32_t>(), ng, 64);
+    k_scatter_rank<<<grid_for(ng), 256, 0, c.stream>>>(i2.as<uint32_t>(), brank.as<uint32_t>(), ng);
+    brank_u.alloc(size_t(NU) * 4);
+    gidx_of_rank.alloc(size_t(ng) * 4);
+    k_rmat_rank_maps<<<grid_for(n), 256, 0, c.stream>>>(order, n, brank.as<uint32_t>(), brank_u.as<uint32_t>(),
+                                                        gidx_of_rank.as<int32_t>());
+  }
+  idxA.release();
+  idxB.release();
+  // 5. the two CSR directions, bucket by bucket
+  const int64_t bucket_cap = std::max<int64_t>(c.opt("rmat_bucket", int64_t(1) << 30), 1 << 16);
+  const int64_t n_rows = c.n_global;
+  for (int dir = 0; dir < 2; dir++) {
+    Csr& out = dir ? es.in : es.out;
+    out = Csr();
+    out.n_rows = n_rows;
+    DevBuf excl;
+    excl.alloc(size_t(n_rows + 1) * 8);
+    exclusive_scan<int64_t>(c, (dir ? icnt : ocnt).as<int64_t>(), excl.as<int64_t>(), n_rows + 1);
+    int64_t total = 0;
+    NBG_HIP(hipMemcpyAsync(&total, excl.as<int64_t>() + n_rows, 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    if (total != E) throw Error(NBG_E_UNKNOWN, "streamed RMAT: sample counts do not add up");
+    const int64_t nb = (total + bucket_cap - 1) / bucket_cap;
+    DevBuf dcut;
+    dcut.alloc(size_t(nb + 1) * 8);
+    NBG_HIP(hipMemsetAsync(dcut.p, 0xff, size_t(nb + 1) * 8, c.stream));
+    k_rmat_cuts<<<grid_for(n_rows), 256, 0, c.stream>>>(excl.as<int64_t>(), n_rows, bucket_cap, dcut.as<int64_t>());
+    std::vector<int64_t> cut(size_t(nb + 1));
+    NBG_HIP(hipMemcpyAsync(cut.data(), dcut.p, size_t(nb) * 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    std::vector<int64_t> starts;
+    for (int64_t k = 0; k < nb; k++)
+      if (cut[size_t(k)] >= 0) starts.push_back(cut[size_t(k)]);
+    starts.push_back(n_rows);
+    // samples per bucket (upper bounds of the unique keys)
+    std::vector<int64_t> sb(starts.size());
+    for (size_t k = 0; k < starts.size(); k++)
+      NBG_HIP(hipMemcpyAsync(&sb[k], excl.as<int64_t>() + starts[k], 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    int64_t maxb = 0;
+    for (size_t k = 0; k + 1 < starts.size(); k++) maxb = std::max(maxb, sb[k + 1] - sb[k]);
+    excl.release();
+    // final arrays sized for every sample (trimmed nnz is known only at the end; the tail stays unused)
+    out.row_ptr.alloc(size_t(n_rows + 1) * 8);
+    NBG_HIP(hipMemsetAsync(out.row_ptr.p, 0, 8, c.stream));
+    out.col.alloc(size_t(E) * 4 + 4);
+    const bool with_props = dir == 0;
+    DevBuf w16;
+    if (with_props) {
+      if (c.opt("rows_vid_col", 1)) out.col_vid.alloc(size_t(E) * 8 + 8);
+      w16.alloc(size_t(E) * 2 + 16);
+    }
+    DevBuf kA, kB;
+    kA.alloc(size_t(std::max<int64_t>(maxb, 1)) * 8);
+    kB.alloc(size_t(std::max<int64_t>(maxb, 1)) * 8);
+    DevBuf bc;
+    bc.alloc(8);
+    int64_t base = 0;
+    for (size_t k = 0; k + 1 < starts.size(); k++) {
+      const int64_t ga = starts[k], gb = starts[k + 1], want = sb[k + 1] - sb[k];
+      if (want == 0) {  // rows without samples (a run of zero-degree rows)
+        k_rmat_emit<<<1, 64, 0, c.stream>>>(kB.as<uint64_t>(), 0, ga, gb - ga, base, gidx_of_rank.as<int32_t>(),
+                                            c.vid_of.as<int64_t>(), seed, out.row_ptr.as<int64_t>(),
+                                            out.col.as<int32_t>(), nullptr, nullptr);
+        continue;
+      }
+      NBG_HIP(hipMemsetAsync(bc.p, 0, 8, c.stream));
+      for (int64_t lo = 0; lo < E; lo += chunk) {
+        const int64_t hi = std::min(E, lo + chunk);
+        k_rmat_bucket<<<sample_grid(hi - lo), 256, 0, c.stream>>>(lo, hi, scale, seed, dir, gidx_of_u.as<int32_t>(),
+                                                                  brank_u.as<uint32_t>(), ga, gb, kA.as<uint64_t>(),
+                                                                  bc.as<unsigned long long>(), want);
+      }
+      int bits = 33;
+      while ((int64_t(1) << (bits - 32)) < gb - ga) bits++;
+      radix_keys<uint64_t>(c, kA.as<uint64_t>(), kB.as<uint64_t>(), want, std::min(bits, 64));
+      const int64_t m = unique_sorted<uint64_t>(c, kB.as<uint64_t>(), kA.as<uint64_t>(), want);
+      k_rmat_emit<<<grid_for(m + 1), 256, 0, c.stream>>>(kA.as<uint64_t>(), m, ga, gb - ga, base,
+                                                         gidx_of_rank.as<int32_t>(), c.vid_of.as<int64_t>(), seed,
+                                                         out.row_ptr.as<int64_t>(), out.col.as<int32_t>(),
+                                                         with_props ? out.col_vid.as<int64_t>() : nullptr,
+                                                         with_props ? w16.as<int16_t>() : nullptr);
+      NBG_HIP(hipGetLastError());
+      base += m;
+    }
+    out.nnz = base;
+    // row_part by the hash rule (every generated key sits in hash(vid)'s part: row_ok stays empty)
+    out.row_part.alloc(size_t(n_rows + 1) * 4);
+    k_row_part_default<<<grid_for(n_rows), 256, 0, c.stream>>>(c.vid_of.as<int64_t>(), n_rows, c.num_parts,
+                                                               out.row_part.as<int32_t>());
+    if (with_props) {  // weight: narrowed to the width its range needs, as gather_props does
+      PropCol pc;
+      pc.name = es.fields[0].name;
+      pc.type = es.fields[0].type;
+      DevBuf mm;
+      mm.alloc(16);
+      long long hm[2] = {LLONG_MAX, LLONG_MIN};
+      NBG_HIP(hipMemcpyAsync(mm.p, hm, 16, hipMemcpyHostToDevice, c.stream));
+      if (base) k_minmax_w<<<grid_for(base), 256, 0, c.stream>>>(w16.p, 2, base, mm.as<long long>());
+      NBG_HIP(hipMemcpyAsync(hm, mm.p, 16, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      pc.minv = base ? hm[0] : 0;
+      pc.maxv = base ? hm[1] : 0;
+      if (c.opt("narrow_props", 1) == 0) {
+        throw Error(NBG_E_UNSUPPORTED, "streamed RMAT with narrow_props = 0");
+      } else if (pc.minv >= INT8_MIN && pc.maxv <= INT8_MAX) {
+        pc.width = 1;
+        pc.data.alloc(size_t(base) + 16);
+        if (base) k_i16_to_i8<<<grid_for(base), 256, 0, c.stream>>>(w16.as<int16_t>(), pc.data.as<int8_t>(), base);
+      } else {
+        pc.width = 2;
+        pc.data = std::move(w16);
+      }
+      out.props.push_back(std::move(pc));
+    }
+    NBG_HIP(hipStreamSynchronize(c.stream));
+  }
+  // 6. out-degrees (compaction's degree reads); no transposed CSR: GO runs top-down here
+  const int64_t n_pad = (n_rows + 127) / 128 * 128;
+  es.odeg.alloc(size_t(n_pad + 1) * 4);
+  NBG_HIP(hipMemsetAsync(es.odeg.p, 0, size_t(n_pad + 1) * 4, c.stream));
+  k_out_deg<<<grid_for(n_rows), 256, 0, c.stream>>>(es.out.row_ptr.as<int64_t>(), nullptr, n_rows,
+                                                    es.odeg.as<uint32_t>(), nullptr);
+  es.has_tr = false;
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  NBG_HIP(hipGetLastError());
+}
+
 void snapshot_finalize(Ctx& c) {
   if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
   double t0 = now_s();
   const bool keep = c.opt("writable", 0) != 0;
+  for (auto& kv : c.edges)
+    if (kv.second.rmat_stream) {
+      finalize_rmat_stream(c, kv.second);
+      c.has_log = false;
+      c.ws_tmp.release();
+      c.finalized = true;
+      c.build_seconds += now_s() - t0;
+      return;
+    }
   // 1. referenced vids (src/dst of every staged tuple), sign-flipped for unsigned sort
   int64_t total = 0;
   for (auto& kv : c.edges) total += 2 * (kv.second.out_stage.n + kv.second.in_stage.n);

@@ -91,42 +91,61 @@ void build_csr(int32_t scale, uint64_t E, int threads, bool reverse, uint64_t se
     }
     boff[size_t(NB)] = run;
   }
-  std::vector<uint64_t> keys(E);
-  parallel_for(int64_t(E), threads, [&](int64_t lo, int64_t hi, int t) {
-    uint64_t* o = toff.data() + size_t(t) * size_t(NB);
-    for (int64_t i = lo; i < hi; i++) {
-      const uint64_t k = key_of(uint64_t(i));
-      keys[o[k >> scale >> shift_b]++] = k;
-    }
-  });
-  std::vector<uint64_t> uniq(size_t(NB), 0);
-  std::atomic<int64_t> next{0};
-  parallel_for(threads, threads, [&](int64_t, int64_t, int) {
-    for (int64_t b; (b = next++) < NB;) {
-      uint64_t* a = keys.data() + boff[size_t(b)];
-      uint64_t* e = keys.data() + boff[size_t(b) + 1];
-      std::sort(a, e);
-      uniq[size_t(b)] = uint64_t(std::unique(a, e) - a);
-    }
-  });
-  std::vector<uint64_t> uoff(size_t(NB) + 1, 0);
-  for (int64_t b = 0; b < NB; b++) uoff[size_t(b) + 1] = uoff[size_t(b)] + uniq[size_t(b)];
+  // buckets are processed in groups of at most max_group_keys samples (one generator pass per
+  // group), so the key buffer stays far below the 8 B x E of a single pass at RMAT-28
+  uint64_t max_group_keys = uint64_t(1) << 30;
+  if (const char* e = getenv("ORA_RMAT_GROUP_KEYS")) max_group_keys = std::max<uint64_t>(strtoull(e, nullptr, 10), 1);
   const int64_t n = int64_t(1) << scale;
   row_ptr.assign(size_t(n) + 1, 0);
-  col.resize(uoff[size_t(NB)]);
-  next = 0;
-  parallel_for(threads, threads, [&](int64_t, int64_t, int) {
-    for (int64_t b; (b = next++) < NB;) {
-      const uint64_t* a = keys.data() + boff[size_t(b)];
-      uint64_t pos = uoff[size_t(b)];
-      const int64_t r0 = b << shift_b, r1 = (b + 1) << shift_b;
-      uint64_t j = 0;
-      for (int64_t r = r0; r < r1; r++) {
-        row_ptr[size_t(r)] = pos;
-        while (j < uniq[size_t(b)] && (a[j] >> scale) == uint64_t(r)) col[pos++] = uint32_t(a[j++] & lowmask);
+  col.resize(E);  // upper bound; trimmed to the unique count at the end (capacity stays)
+  std::vector<uint64_t> keys;
+  std::vector<uint64_t> uniq(size_t(NB), 0);
+  uint64_t pos_all = 0;
+  for (int64_t g0 = 0; g0 < NB;) {
+    int64_t g1 = g0 + 1;
+    while (g1 < NB && boff[size_t(g1) + 1] - boff[size_t(g0)] <= max_group_keys) g1++;
+    const uint64_t gbase = boff[size_t(g0)], gsize = boff[size_t(g1)] - gbase;
+    keys.resize(gsize);
+    parallel_for(int64_t(E), threads, [&](int64_t lo, int64_t hi, int t) {
+      std::vector<uint64_t> o(size_t(g1 - g0));
+      for (int64_t b = g0; b < g1; b++) o[size_t(b - g0)] = toff[size_t(t) * size_t(NB) + size_t(b)] - gbase;
+      for (int64_t i = lo; i < hi; i++) {
+        const uint64_t k = key_of(uint64_t(i));
+        const int64_t b = int64_t(k >> scale >> shift_b);
+        if (b >= g0 && b < g1) keys[o[size_t(b - g0)]++] = k;
       }
-    }
-  });
+    });
+    std::atomic<int64_t> next{g0};
+    parallel_for(threads, threads, [&](int64_t, int64_t, int) {
+      for (int64_t b; (b = next++) < g1;) {
+        uint64_t* a = keys.data() + (boff[size_t(b)] - gbase);
+        uint64_t* e = keys.data() + (boff[size_t(b) + 1] - gbase);
+        std::sort(a, e);
+        uniq[size_t(b)] = uint64_t(std::unique(a, e) - a);
+      }
+    });
+    std::vector<uint64_t> uoff(size_t(g1 - g0) + 1, pos_all);
+    for (int64_t b = g0; b < g1; b++) uoff[size_t(b - g0) + 1] = uoff[size_t(b - g0)] + uniq[size_t(b)];
+    next = g0;
+    parallel_for(threads, threads, [&](int64_t, int64_t, int) {
+      for (int64_t b; (b = next++) < g1;) {
+        const uint64_t* a = keys.data() + (boff[size_t(b)] - gbase);
+        uint64_t pos = uoff[size_t(b - g0)];
+        const int64_t r0 = b << shift_b, r1 = (b + 1) << shift_b;
+        uint64_t j = 0;
+        for (int64_t r = r0; r < r1; r++) {
+          row_ptr[size_t(r)] = pos;
+          while (j < uniq[size_t(b)] && (a[j] >> scale) == uint64_t(r)) col[pos++] = uint32_t(a[j++] & lowmask);
+        }
+      }
+    });
+    pos_all = uoff[size_t(g1 - g0)];
+    g0 = g1;
+  }
+  std::vector<uint64_t>().swap(keys);
+  col.resize(pos_all);
+  std::vector<uint64_t> uoff(size_t(NB) + 1, 0);
+  uoff[size_t(NB)] = pos_all;
   row_ptr[size_t(n)] = uoff[size_t(NB)];
 }
 
@@ -189,14 +208,12 @@ static std::vector<int64_t> idx_of(const ora_rmat_graph* g, const int64_t* vids,
   return out;
 }
 
-// GO steps FROM starts OVER the RMAT edge type [WHERE weight > where_gt] YIELD _dst [DISTINCT].
-// Writes the result vids sorted ascending into *out (malloc'd, ora_free) and returns their count.
-int64_t ora_rmat_graph_go(const ora_rmat_graph* g, const int64_t* starts, size_t n_starts, int32_t steps,
-                          int32_t has_where, int64_t where_gt, int32_t distinct, int32_t threads,
-                          int64_t** out, uint64_t* edges_scanned) {
-  if (threads < 1) threads = 1;
-  *out = nullptr;
-  *edges_scanned = 0;
+}  // extern "C"
+
+// the final hop's frontier (index space) of GO steps FROM starts, and the rows scanned over all hops
+static std::vector<int64_t> go_frontier(const ora_rmat_graph* g, const int64_t* starts, size_t n_starts, int32_t steps,
+                                        int32_t distinct, int32_t threads, uint64_t& scanned_out,
+                                        std::vector<uint8_t>& mark) {
   std::vector<int64_t> idx = idx_of(g, starts, n_starts, threads);
   // hop-1 scan list: the starts as given, deduplicated only under DISTINCT (P14)
   std::vector<int64_t> F;
@@ -211,7 +228,7 @@ int64_t ora_rmat_graph_go(const ora_rmat_graph* g, const int64_t* starts, size_t
     for (int64_t u : idx)
       if (u >= 0) F.push_back(u);
   }
-  std::vector<uint8_t> mark(size_t(g->n), 0);
+  mark.assign(size_t(g->n), 0);
   uint64_t scanned = 0;
   for (int32_t step = 1; step <= steps && !F.empty(); step++) {
     for (int64_t u : F) scanned += g->row_ptr[size_t(u) + 1] - g->row_ptr[size_t(u)];
@@ -228,6 +245,23 @@ int64_t ora_rmat_graph_go(const ora_rmat_graph* g, const int64_t* starts, size_t
     for (int64_t v = 0; v < g->n; v++)
       if (mark[size_t(v)]) F.push_back(v);
   }
+  scanned_out = scanned;
+  return F;
+}
+
+extern "C" {
+
+// GO steps FROM starts OVER the RMAT edge type [WHERE weight > where_gt] YIELD _dst [DISTINCT].
+// Writes the result vids sorted ascending into *out (malloc'd, ora_free) and returns their count.
+int64_t ora_rmat_graph_go(const ora_rmat_graph* g, const int64_t* starts, size_t n_starts, int32_t steps,
+                          int32_t has_where, int64_t where_gt, int32_t distinct, int32_t threads,
+                          int64_t** out, uint64_t* edges_scanned) {
+  if (threads < 1) threads = 1;
+  *out = nullptr;
+  *edges_scanned = 0;
+  std::vector<uint8_t> mark;
+  uint64_t scanned = 0;
+  std::vector<int64_t> F = go_frontier(g, starts, n_starts, steps, distinct, threads, scanned, mark);
   *edges_scanned = scanned;
   if (F.empty()) return 0;
   // final hop: rows (u, v) passing WHERE; YIELD _dst
@@ -272,6 +306,40 @@ int64_t ora_rmat_graph_go(const ora_rmat_graph* g, const int64_t* starts, size_t
   *out = static_cast<int64_t*>(malloc(sizeof(int64_t) * (res.size() ? res.size() : 1)));
   if (!res.empty()) memcpy(*out, res.data(), sizeof(int64_t) * res.size());
   return int64_t(res.size());
+}
+
+// Order-independent digest of a plain GO's final rows (YIELD _dst, no WHERE / DISTINCT), for
+// result sets too large to sort (configs[4]: billions of rows): out[0] = rows, out[1] = sum of
+// splitmix64(dst vid) mod 2^64, out[2] = xor of the same; *edges_scanned as ora_rmat_graph_go.
+void ora_rmat_graph_go_msum(const ora_rmat_graph* g, const int64_t* starts, size_t n_starts, int32_t steps,
+                            int32_t threads, uint64_t* out, uint64_t* edges_scanned) {
+  if (threads < 1) threads = 1;
+  std::vector<uint8_t> mark;
+  uint64_t scanned = 0;
+  std::vector<int64_t> F = go_frontier(g, starts, n_starts, steps, 0, threads, scanned, mark);
+  *edges_scanned = scanned;
+  std::vector<uint64_t> cnt(size_t(threads), 0), sum(size_t(threads), 0), x(size_t(threads), 0);
+  parallel_for(int64_t(F.size()), threads, [&](int64_t lo, int64_t hi, int t) {
+    uint64_t c = 0, sm = 0, xr = 0;
+    for (int64_t i = lo; i < hi; i++) {
+      const int64_t u = F[size_t(i)];
+      for (uint64_t e = g->row_ptr[size_t(u)]; e < g->row_ptr[size_t(u) + 1]; e++) {
+        const uint64_t h = splitmix64(uint64_t(rmatVid(g->col[e], g->seed)));
+        c++;
+        sm += h;
+        xr ^= h;
+      }
+    }
+    cnt[size_t(t)] = c;
+    sum[size_t(t)] = sm;
+    x[size_t(t)] = xr;
+  });
+  out[0] = out[1] = out[2] = 0;
+  for (int t = 0; t < threads; t++) {
+    out[0] += cnt[size_t(t)];
+    out[1] += sum[size_t(t)];
+    out[2] ^= x[size_t(t)];
+  }
 }
 
 // FIND SHORTEST PATH for n pairs (definition: ora_shortest_path in refcpu.cpp).  hops[i] = -1

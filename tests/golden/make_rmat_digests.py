@@ -47,7 +47,22 @@ CASES = {
     "paths1024_s18": (18, "paths", dict(pairs=1024, max_steps=8)),
     "paths1024_s22": (22, "paths", dict(pairs=1024, max_steps=8)),
     "paths1024_s26": (26, "paths", dict(pairs=1024, max_steps=8)),
+    # configs[4] (C5): GO 2 STEPS FROM 64 seeds incl. the top-8 out-degree vertices on RMAT-28
+    # (2.7 G rows: order-independent digest, oracle.msum)
+    "go2_plain_s28_seeds64_hubs8": (28, "go_msum", dict(seeds=64, hubs=8, steps=2)),
+    "go2_plain_s16_seeds64_hubs8": (16, "go_msum", dict(seeds=64, hubs=8, steps=2)),
 }
+
+
+def hub_starts(g, scale, seeds, hubs):
+    """bench.py --hubs: the top-N out-degree vertices among synth.hub_candidates (collapsed
+    degrees, stable order) replace the first N seeds"""
+    starts = synth.seeds(scale, 16, 1, seeds)
+    idx = [0] + [1 << k for k in range(scale)]
+    cand = synth.hub_candidates(scale, 1)
+    deg = np.array([g.out_degree(i) for i in idx], dtype=np.int64)
+    order = np.argsort(-deg, kind="stable")[:hubs]
+    return np.concatenate([cand[order].astype(np.int64), starts[hubs:]]), [(int(cand[i]), int(deg[i])) for i in order]
 
 
 def paths_digest(hops, paths) -> str:
@@ -58,6 +73,12 @@ def paths_digest(hops, paths) -> str:
 
 
 def run_case(g, name, kind, prm, scale):
+    if kind == "go_msum":
+        starts, hubs = hub_starts(g, scale, prm["seeds"], prm["hubs"])
+        t0 = time.time()
+        ms, scanned = g.go_msum(starts, prm["steps"])
+        return {"scale": scale, **prm, "n_rows": ms[0], "msum": [str(ms[1]), str(ms[2])], "hub_seeds": hubs,
+                "edges_scanned": int(scanned), "oracle_s": round(time.time() - t0, 2)}
     if kind == "go":
         starts = synth.seeds(scale, 16, 1, prm["seeds"])
         t0 = time.time()

@@ -91,6 +91,7 @@ def lib():
             "ora_rmat_graph_info": (None, [vp, P(i64), P(i64)]),
             "ora_rmat_graph_out_degree": (i64, [vp, i64]),
             "ora_rmat_graph_go": (i64, [vp, vp, sz, i32, i32, i64, i32, i32, P(P(i64)), P(u64)]),
+            "ora_rmat_graph_go_msum": (None, [vp, vp, sz, i32, i32, P(u64), P(u64)]),
             "ora_rmat_graph_shortest_path": (None, [vp, vp, vp, sz, i32, i32, vp, vp, P(P(i64))]),
             "ora_free": (None, [vp]),
         }
@@ -418,6 +419,18 @@ class RmatGraph:
             lib().ora_free(C.cast(out, C.c_void_p))
         return res, scanned.value
 
+    def go_msum(self, starts, steps):
+        """order-independent digest of a plain GO's rows (YIELD _dst): (rows, sum of
+        splitmix64(vid) mod 2^64, xor of the same), and the edges scanned -- see msum()"""
+        starts = np.ascontiguousarray(starts, dtype=np.int64)
+        out = (C.c_uint64 * 3)()
+        scanned = C.c_uint64()
+        lib().ora_rmat_graph_go_msum(self.h, _ptr(starts), len(starts), steps, self.threads, out, C.byref(scanned))
+        return (int(out[0]), int(out[1]), int(out[2])), scanned.value
+
+    def out_degree(self, idx):
+        return int(lib().ora_rmat_graph_out_degree(self.h, int(idx)))
+
     def shortest_path(self, src, dst, max_steps):
         """(hops int64[n], [path vids per pair]) -- ora_shortest_path's definition"""
         src = np.ascontiguousarray(src, dtype=np.int64)
@@ -460,3 +473,20 @@ def part_of(vid: int, num_parts: int) -> int:
 
 
 os.environ.setdefault("OMP_NUM_THREADS", "8")
+
+
+def msum(vids, chunk=1 << 26):
+    """(rows, sum of splitmix64(vid) mod 2^64, xor of the same) of a result column: the
+    order-independent digest of ora_rmat_graph_go_msum, for result sets too large to sort"""
+    v = np.asarray(vids, dtype=np.int64).view(np.uint64)
+    s = 0
+    x = np.uint64(0)
+    with np.errstate(over="ignore"):
+        for i in range(0, len(v), chunk):
+            z = v[i:i + chunk] + np.uint64(0x9E3779B97F4A7C15)
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            z = z ^ (z >> np.uint64(31))
+            s = (s + int(z.sum(dtype=np.uint64))) & ((1 << 64) - 1)
+            x ^= np.bitwise_xor.reduce(z) if len(z) else np.uint64(0)
+    return len(v), s, int(x)
