@@ -313,6 +313,7 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
         "data": "synthetic RMAT (Graph500 a/b/c=0.57/0.19/0.19, seed 1) generated on device",
         "config": {
             "parallelism": f"pairs sharded i % {world} over the ranks, replicated CSRs" if world > 1 else "1 GPU",
+            "communicator": sp.comm_info() if world > 1 else None,
             "workload": f"FIND SHORTEST PATH {args.pairs} pairs UPTO {args.max_steps} STEPS OVER follow; "
                         f"RMAT-{args.scale} ef{args.edge_factor}",
             "vertices": info["num_vertices"],
@@ -395,6 +396,7 @@ def main():
     sp.finalize()
     build_s = time.time() - t0
     info = sp.info(FOLLOW)
+    comm_seen = sp.comm_info() if world > 1 else None  # ncclCommCount of the engine's communicator
     if args.workload == "paths":
         return bench_paths(args, sp, info, build_s, rank, world, golden, dist)
     starts = synth.seeds(args.scale, args.edge_factor, 1, args.seeds)
@@ -556,6 +558,7 @@ def main():
         }
         if world > 1:
             out["comm"] = {"backend": "rccl (nbg_comm_init over ncclCommInitRank)", "ranks": world,
+                           "communicator": comm_seen,
                            "comm_ms_per_query_rank0": comm_ms / K, "comm_bytes_per_query_rank0": comm_bytes // K}
         if world == 1 and not args.no_cpu and not args.plain:
             try:

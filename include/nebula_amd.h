@@ -78,6 +78,10 @@ int32_t nbg_comm_init(nbg_ctx* ctx, const uint8_t unique_id[128]);
  * form a group whose collectives are device-to-device copies; the sharded algorithm then runs
  * unchanged with world_size ranks on a single GPU.  Each rank must call from its own thread. */
 int32_t nbg_comm_init_local(nbg_ctx* ctx, int64_t group_key);
+/* The context's communicator as the transport itself reports it: *ranks = ncclCommCount of
+ * the RCCL communicator (the LocalComm group size; 1 without one), *transport = 0 none,
+ * 1 RCCL, 2 LocalComm.  Lets a multi-GPU bench line show the rank count RCCL really formed.  */
+int32_t nbg_comm_info(nbg_ctx* ctx, int32_t* ranks, int32_t* transport);
 
 /* pure arithmetic helpers (host, no GPU needed) */
 int32_t nbg_part_of(int64_t vid, int32_t num_parts);          /* StorageClient.cpp:238-243 */

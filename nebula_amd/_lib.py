@@ -26,7 +26,7 @@ OWNER_SOURCE, OWNER_DEST, OWNER_EDGE = 1, 2, 3
 # every symbol the header declares (tests/test_capi.py checks the .so exports them all)
 EXPORTS = [
     "nbg_ctx_create", "nbg_ctx_destroy", "nbg_last_error", "nbg_comm_unique_id", "nbg_comm_init",
-    "nbg_comm_init_local",
+    "nbg_comm_init_local", "nbg_comm_info",
     "nbg_part_of", "nbg_rank_of_part", "nbg_schema_set_edge", "nbg_schema_set_tag", "nbg_snapshot_load_part",
     "nbg_snapshot_gen_rmat", "nbg_snapshot_finalize", "nbg_snapshot_write_part", "nbg_snapshot_commit",
     "nbg_snapshot_info_get",
@@ -111,6 +111,7 @@ def load(path: str | os.PathLike | None = None):
         "nbg_comm_unique_id": (i32, [vp]),
         "nbg_comm_init": (i32, [vp, vp]),
         "nbg_comm_init_local": (i32, [vp, i64]),
+        "nbg_comm_info": (i32, [vp, vp, vp]),
         "nbg_part_of": (i32, [i64, i32]),
         "nbg_rank_of_part": (i32, [i32, i32]),
         "nbg_schema_set_edge": (i32, [vp, i32, i32, i32, C.POINTER(C.c_char_p), C.POINTER(i32)]),

@@ -96,6 +96,14 @@ int32_t nbg_comm_init_local(nbg_ctx* ctx, int64_t group_key) {
   });
 }
 
+int32_t nbg_comm_info(nbg_ctx* ctx, int32_t* ranks, int32_t* transport) {
+  if (!ranks || !transport) return NBG_E_INVALID_ARG;
+  return guarded(ctx, [&](Ctx& c) {
+    nbg::comm_info(c, ranks, transport);
+    return NBG_OK;
+  });
+}
+
 int32_t nbg_part_of(int64_t vid, int32_t num_parts) {
   return num_parts > 0 ? nbg::part_of_vid(vid, num_parts) : NBG_E_INVALID_ARG;
 }

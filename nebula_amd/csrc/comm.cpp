@@ -34,11 +34,18 @@ struct CommImpl {
   virtual void alltoallv(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
                          const size_t* recv_bytes, const size_t* recv_off) = 0;
   virtual void allreduce_sum_i64(Ctx& c, int64_t* d, size_t n) = 0;
+  virtual int32_t ranks() const = 0;     // the communicator's own rank count
+  virtual int32_t transport() const = 0;  // 1 = RCCL, 2 = in-process LocalComm
 };
 
 // ------------------------------------------------------------------------------------------
 struct RcclComm : CommImpl {
   ncclComm_t comm = nullptr;
+  int32_t ranks() const override {
+    int n = 0;
+    return ncclCommCount(comm, &n) == ncclSuccess ? int32_t(n) : -1;
+  }
+  int32_t transport() const override { return 1; }
   ~RcclComm() override {
     if (comm) ncclCommDestroy(comm);
   }
@@ -104,6 +111,8 @@ static std::mutex g_groups_mu;
 static std::map<int64_t, std::shared_ptr<LocalGroup>> g_groups;
 
 struct LocalComm : CommImpl {
+  int32_t transport() const override { return 2; }
+  int32_t ranks() const override { return g ? int32_t(g->world) : -1; }
   std::shared_ptr<LocalGroup> g;
   void allgatherv(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
                   const size_t* recv_off) override {
@@ -203,6 +212,13 @@ void comm_init_local(Ctx& c, int64_t key) {
   auto* l = new LocalComm();
   l->g = g;
   c.comm = l;
+}
+
+// (ranks, transport) of the context's communicator: what ncclCommCount reports for RCCL
+void comm_info(const Ctx& c, int32_t* ranks, int32_t* transport) {
+  auto* impl = static_cast<const CommImpl*>(c.comm);
+  *ranks = impl ? impl->ranks() : 1;
+  *transport = impl ? impl->transport() : 0;
 }
 
 void comm_destroy(Ctx& c) {

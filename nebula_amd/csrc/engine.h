@@ -434,6 +434,7 @@ void comm_allreduce_sum_i64(Ctx& c, int64_t* d_vals, size_t n);
 void comm_allgatherv_bytes(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
                            const size_t* recv_off);
 void comm_init_local(Ctx& c, int64_t key);
+void comm_info(const Ctx& c, int32_t* ranks, int32_t* transport);
 void comm_destroy(Ctx& c);
 
 inline double now_s() {

@@ -164,6 +164,13 @@ class GraphSpace:
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         self._check(self.L.nbg_comm_init(self.h, buf))
 
+    def comm_info(self) -> dict:
+        """{"ranks": the communicator's own rank count (ncclCommCount for RCCL), "transport":
+        "none" | "rccl" | "local"}"""
+        r, t = C.c_int32(), C.c_int32()
+        self._check(self.L.nbg_comm_info(self.h, C.byref(r), C.byref(t)))
+        return {"ranks": r.value, "transport": {0: "none", 1: "rccl", 2: "local"}.get(t.value, t.value)}
+
     def comm_init_local(self, group_key: int):
         """In-process rank group on one device (tests of the sharded path)."""
         self._check(self.L.nbg_comm_init_local(self.h, int(group_key)))

@@ -107,6 +107,16 @@ def test_shard_sizes_cover_graph(rmat_group, oracle12):
     assert sum(i["local_in_edges"] for i in infos) == i1["local_in_edges"]
 
 
+def test_comm_info_reports_group(rmat_group):
+    """nbg_comm_info: the rank count the transport itself formed (LocalComm here; RCCL's
+    ncclCommCount on a multi-GPU launch, reported by bench.py's comm.communicator)"""
+    infos = rmat_group.each(lambda r, s: s.comm_info())
+    assert all(i == {"ranks": len(rmat_group.sp), "transport": "local"} for i in infos)
+    one = GraphSpace(64)
+    assert one.comm_info() == {"ranks": 1, "transport": "none"}
+    one.close()
+
+
 @pytest.mark.parametrize("force", [0, 1, -1])
 def test_sharded_go_distinct_dst(rmat_group, oracle12, force):
     g = rmat_group
