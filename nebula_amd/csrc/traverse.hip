@@ -77,6 +77,9 @@ struct EvalEnv {
   const int32_t* in_rows;
   uint32_t in_mask;
   const PropDev* iprops;
+  // STEPS > 1: root start (vid rank) of every final-frontier vertex and rank -> start gidx
+  const int32_t* in_root;
+  const int32_t* in_root_tab;
   // storage (getBound) filters: a $^ tag row is visible when it sits in the request's part,
   // which for an edge row is the part of the row's keys (Csr::row_part, local row = src - lo)
   int32_t storage;
@@ -226,7 +229,12 @@ __device__ Val eval_program(const Program* __restrict__ P, const EvalEnv& env, i
         break;
       }
       case P_INPUT: {
-        const int32_t row = input_row(env, src_g);
+        int32_t g0 = src_g;
+        if (env.in_root) {  // multi-step: the input row of the vertex's root start
+          const int32_t r = env.in_root[src_g];
+          g0 = r == INT32_MAX ? -1 : env.in_root_tab[r];
+        }
+        const int32_t row = g0 < 0 ? -1 : input_row(env, g0);
         st[sp++] = row < 0 ? mk(VT_ERR, 0) : load_prop(env.iprops[in.arg], row);
         break;
       }
@@ -347,6 +355,10 @@ struct ExpandArgs {
   const int64_t* col_vid;  // per-edge dst vid (Csr::col_vid) or null: vid_of[col[e]]
   const int32_t* tile_row; // [ntiles + 1]: frontier entry holding the first slot of each tile
                            // (k_tile_rows), or null: binary search of off[]
+  // multi-step $- / $var (VertexBackTracker, GoExecutor.h:174-193): root start of every marked
+  // dst = the smallest (by vid rank) root of its in-edges' srcs this hop, or null
+  const int32_t* root_cur;
+  int32_t* root_next;
 };
 struct FastArgs {
   const void* data;
@@ -527,6 +539,7 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
           } else {
             a.map[d] = 1;
           }
+          if (a.root_next) atomicMin(a.root_next + d, a.root_cur[a.lo + srck]);
         }
       } else if (MODE == EXP_ROWS) {
         if (pass) pm |= 1u << r;
@@ -2317,6 +2330,17 @@ __global__ void k_input_index(const int32_t* sg, int64_t n, int32_t* keys, int32
   }
 }
 
+// roots of the starts: rank of the start's vid among the distinct start vids (host-computed),
+// so a min over ranks is the min over root vids; tab[rank] = the start's gidx
+__global__ void k_root_init(const int32_t* sg, const int32_t* srank, int64_t n, int32_t* root, int32_t* tab) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int32_t g = sg[i];
+    if (g < 0) continue;
+    root[g] = srank[i];
+    tab[srank[i]] = g;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // host drivers
 // ------------------------------------------------------------------------------------------
@@ -3238,8 +3262,37 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     for (int i = 0; i < p.n; i++) uses_input |= p.ins[i].op == P_INPUT;
   DevBuf in_keys, in_rows, in_tab;
   std::vector<DevBuf> in_cols;
+  // STEPS > 1: graphd maps every dst of a non-final step back to a start (VertexBackTracker,
+  // GoExecutor.h:174-193, GoExecutor.cpp:420-424) in RPC response order, last write winning --
+  // order-dependent whenever a vertex is reached from several starts.  The build's rule
+  // (DESIGN.md): each hop reads the previous hop's roots and a dst takes the smallest root vid
+  // among its in-edges' srcs; it is the reference's answer whenever the root is unique.
+  const bool multi_root = uses_input && s.steps > 1;
+  DevBuf root_buf[2], root_tab;
+  int root_cur = 0;
+  if (multi_root && c.world > 1)
+    throw Error(NBG_E_UNSUPPORTED, "$- / $var props with STEPS > 1 across ranks");
+  if (multi_root) {
+    // rank of every start's vid among the distinct start vids
+    std::vector<int64_t> u(s.starts, s.starts + ns);
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    std::vector<int32_t> rk(size_t(std::max<int64_t>(ns, 1)));
+    for (int64_t i = 0; i < ns; i++)
+      rk[size_t(i)] = int32_t(std::lower_bound(u.begin(), u.end(), s.starts[i]) - u.begin());
+    DevBuf drk;
+    drk.alloc(rk.size() * 4);
+    NBG_HIP(hipMemcpyAsync(drk.p, rk.data(), rk.size() * 4, hipMemcpyHostToDevice, c.stream));
+    for (auto& b : root_buf) {
+      b.alloc(size_t(c.n_global + 1) * 4);
+      NBG_HIP(hipMemsetAsync(b.p, 0x7f, size_t(c.n_global + 1) * 4, c.stream));  // > every rank
+    }
+    root_tab.alloc(std::max<size_t>(u.size(), 1) * 4);
+    if (ns) k_root_init<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, drk.as<int32_t>(), ns, root_buf[0].as<int32_t>(),
+                                                           root_tab.as<int32_t>());
+    NBG_HIP(hipStreamSynchronize(c.stream));  // rk is pageable host memory
+  }
   if (uses_input) {
-    if (s.steps != 1) throw Error(NBG_E_UNSUPPORTED, "$- / $var props with STEPS > 1 (VertexBackTracker)");
     uint32_t cap = 64;
     while (cap < uint32_t(2 * std::max<int64_t>(ns, 1))) cap <<= 1;
     in_keys.alloc(size_t(cap) * 4);
@@ -3308,8 +3361,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     }
   };
   // direction choice is global (every rank must take the same branch: bottom-up allgathers)
-  auto want_bu = [&](int64_t eg) {
-    return eg > 0 && bu_ok && bu_force >= 0 && (bu_force > 0 || eg >= es.out_nnz_global / bu_div);
+  auto want_bu = [&](int64_t eg) {  // (multi-step roots need every in-edge: top-down only)
+    return eg > 0 && bu_ok && !multi_root && bu_force >= 0 && (bu_force > 0 || eg >= es.out_nnz_global / bu_div);
   };
   ensure_off();
   int64_t Eg = E;  // frontier out-degree sum over all ranks
@@ -3369,9 +3422,19 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       a.nF = nF;
       a.off = c.ws_off.as<int64_t>();
       const double ms0 = c.timing.expand_ms;
+      if (multi_root) {
+        NBG_HIP(hipMemsetAsync(root_buf[root_cur ^ 1].p, 0x7f, size_t(c.n_global + 1) * 4, c.stream));
+        a.root_cur = root_buf[root_cur].as<int32_t>();
+        a.root_next = root_buf[root_cur ^ 1].as<int32_t>();
+      }
       if (E > 0) {
         launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, E);
         c.timing.expand_bytes += expand_bytes(nF, E, 0, EXP_MARK);
+      }
+      if (multi_root) {
+        root_cur ^= 1;
+        a.root_cur = nullptr;
+        a.root_next = nullptr;
       }
       const unsigned long long hs[8] = {(unsigned long long)nF, (unsigned long long)E, 0, 0, 0, 0, 0, 0};
       c.timing.hop(0, false, c.timing.expand_ms - ms0, hs);
@@ -3398,6 +3461,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   }
   // ---- final step ----
   c.timing.steps_run++;
+  if (multi_root) {
+    env.in_root = root_buf[root_cur].as<int32_t>();
+    env.in_root_tab = root_tab.as<int32_t>();
+  }
   if (deferred != NBG_OK) throw Error(deferred, deferred_msg);
   FastPred fpk = has_where ? classify_pred(where, es.fields) : FastPred{};
   int pk = fpk.kind;

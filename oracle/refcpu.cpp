@@ -1649,15 +1649,30 @@ ora_result* ora_go(ora_store* st, const int64_t* starts, size_t nStarts, int32_t
   st->inRows = 0;
   std::unordered_map<int64_t, size_t> inIndex;
   if (refs.input || refs.variable) {
-    if (inNames.empty() || inRows != nStarts || steps != 1) {
-      // multi-step: VertexBackTracker (GoExecutor.h:174-193) depends on response order
+    if (inNames.empty() || inRows != nStarts) {
       out->code = -2;
-      out->error = "unsupported reference ($-/$var without an input table or with STEPS > 1)";
+      out->error = "unsupported reference ($-/$var without an input table)";
       return out;
     }
     for (size_t i = 0; i < nStarts; i++) inIndex[starts[i]] = i;
   }
-  auto inputProp = [&](int64_t vid, const std::string& prop) -> OptVal {
+  // STEPS > 1: VertexBackTracker (GoExecutor.h:174-193) maps every dst of a non-final step to a
+  // start (GoExecutor.cpp:420-424), in RPC response order with the last write winning, so the
+  // reference's answer depends on that order whenever a vertex is reached from several starts.
+  // Restated with the build's order-free rule: a step reads the previous step's
+  // roots and a dst takes the smallest root vid among the srcs of its in-edges -- the
+  // reference's own answer whenever the root is unique.
+  const bool backTrack = (refs.input || refs.variable) && steps != 1;
+  std::unordered_map<int64_t, int64_t> rootOf;
+  if (backTrack)
+    for (size_t i = 0; i < nStarts; i++) rootOf[starts[i]] = starts[i];
+  auto inputProp = [&](int64_t vid0, const std::string& prop) -> OptVal {
+    int64_t vid = vid0;
+    if (backTrack) {
+      auto rt = rootOf.find(vid0);
+      if (rt == rootOf.end()) return ERR("vid not traced back to a start");
+      vid = rt->second;
+    }
     auto r = inIndex.find(vid);
     if (r == inIndex.end()) return ERR("vid not in the input index");
     for (size_t c = 0; c < inNames.size(); c++)
@@ -1719,15 +1734,23 @@ ora_result* ora_go(ora_store* st, const int64_t* starts, size_t nStarts, int32_t
     if (!final) {
       // getDstIdsFromResp (GoExecutor.cpp:407-431)
       std::unordered_set<int64_t> set;
+      std::unordered_map<int64_t, int64_t> nextRoot;
       for (auto& r : resps) {
         auto es = toSchema(r.edgeSchema);
         for (auto& v : r.vertices)
           rowSetForEach(v.edgeData, es, [&](const RowReader& row) {
             scanned++;
             auto d = row.getByName("_dst");
-            set.insert(std::get<0>(d.v));
+            const int64_t dst = std::get<0>(d.v);
+            set.insert(dst);
+            if (backTrack) {
+              const int64_t rt = rootOf.at(v.vid);
+              auto it = nextRoot.find(dst);
+              if (it == nextRoot.end() || rt < it->second) nextRoot[dst] = rt;
+            }
           });
       }
+      if (backTrack) rootOf.swap(nextRoot);
       cur.assign(set.begin(), set.end());
       if (cur.empty()) break;  // onEmptyInputs
       continue;

@@ -280,9 +280,81 @@ def test_nba_reference_input_errors(nba):
     with pytest.raises(NbgError) as e:  # no input table
         sp.go(starts, 1, F.NBA_LIKE, yields=[X.InputProp("name")])
     assert e.value.code == -1003
-    with pytest.raises(NbgError) as e:  # multi-step: VertexBackTracker order dependence
-        sp.go(starts, 2, F.NBA_LIKE, yields=[X.InputProp("name")], inputs=inputs)
-    assert e.value.code == -1003
     with pytest.raises(NbgError) as e:  # unknown input column
         sp.go(starts, 1, F.NBA_LIKE, yields=[X.InputProp("nope")], inputs=inputs)
     assert e.value.code == -1001
+
+
+# ------------------------------------------------------------------------------------------
+# $-.prop / $var.prop with STEPS > 1 (VertexBackTracker, GoExecutor.h:174-193): the input row of
+# the vertex's root start; several roots -> the smallest root vid (the build's order-free rule,
+# DESIGN.md; the reference picks by RPC response order there)
+# ------------------------------------------------------------------------------------------
+def expected_multistep(sp, starts, names_in, steps, et):
+    """the rule restated from single-start GO results: root(v) after each non-final hop =
+    min vid over the roots of v's in-edge srcs in the previous frontier"""
+    name_of = {}
+    for s_, n_ in zip(starts, names_in):
+        name_of[s_] = n_  # the last input row of a vid wins (InterimResult::buildIndex)
+    root = {s_: s_ for s_ in starts}
+    for _ in range(steps - 1):
+        nxt = {}
+        for v, r in root.items():
+            rs = sp.go([v], 1, et)
+            for d in rs.columns[0]:
+                d = int(d)
+                nxt[d] = min(nxt.get(d, r), r)
+        root = nxt
+    rows = []
+    for v, r in root.items():
+        rs = sp.go([v], 1, et)
+        rows += [(name_of[r], int(d)) for d in rs.columns[0]]
+    return Counter(rows)
+
+
+@pytest.mark.parametrize("steps", [2, 3])
+def test_nba_multistep_input(nba, steps):
+    sp, st, vid, d = nba
+    who = ["Tim Duncan", "Tony Parker", "Chris Paul", "Manu Ginobili", "Tim Duncan"]
+    starts = [vid[w] for w in who]
+    tags = [f"row{i}" for i in range(len(who))]
+    inputs = [("tag", O.STRING, tags), ("n", O.INT, list(range(len(who))))]
+    ys = [X.InputProp("tag"), X.EdgeDst("like")]
+    rs = sp.go(starts, steps, F.NBA_LIKE, yields=ys, inputs=inputs)
+    assert ms(rs.rows()) == expected_multistep(sp, starts, tags, steps, F.NBA_LIKE)
+    for ref in (X.InputProp("n"), X.VariableProp("v", "n")):
+        for w in (None, ref > 1):
+            ys2 = [ref, X.InputProp("tag"), X.SourceProp("player", "name"), X.EdgeDst("like")]
+            rs = sp.go(starts, steps, F.NBA_LIKE, where=w, yields=ys2, inputs=inputs)
+            ref_rs = st.go(starts, steps, F.NBA_LIKE, where=X.encode(w), yields=[y.encode() for y in ys2],
+                           inputs=inputs)
+            assert ref_rs.code == 0, ref_rs.error
+            assert ms(rs.rows()) == ms(ref_rs.rows())
+
+
+@pytest.mark.parametrize("steps", [2, 3])
+def test_rmat_multistep_input_vs_oracle(steps):
+    """random graph, many starts sharing descendants (the tie rule decides most roots)"""
+    from nebula_amd import synth
+    scale = 11
+    sp = GraphSpace(16)
+    try:
+        sp.set_edge_schema(1, [("weight", O.INT)])
+        sp.gen_rmat(scale, 8, 3, 1)
+        sp.finalize()
+        st = O.Store(16)
+        st.set_edge_schema(1, [("weight", O.INT)], name="e")
+        st.load_rmat(scale, 8, 3, 1)
+        starts = list(synth.seeds(scale, 8, 3, 24))
+        inputs = [("n", O.INT, [int(i * 7 % 11) for i in range(len(starts))])]
+        ys = [X.InputProp("n"), X.AliasProp("e", "weight"), X.EdgeDst("e")]
+        for w in (None, X.InputProp("n") > 4, (X.InputProp("n") + X.AliasProp("e", "weight")) > 600):
+            for distinct in (False, True):
+                rs = sp.go(starts, steps, 1, where=w, yields=ys, distinct=distinct, inputs=inputs)
+                ref = st.go(starts, steps, 1, where=X.encode(w), yields=[y.encode() for y in ys],
+                            distinct=distinct, inputs=inputs)
+                assert ref.code == 0, ref.error
+                assert ms(rs.rows()) == ms(ref.rows())
+                assert rs.n_rows > 0
+    finally:
+        sp.close()
