@@ -2241,28 +2241,43 @@ void snapshot_finalize(Ctx& c) {
       c.build_seconds += now_s() - t0;
       return;
     }
-  // 1. referenced vids (src/dst of every staged tuple), sign-flipped for unsigned sort
-  int64_t total = 0;
-  for (auto& kv : c.edges) total += 2 * (kv.second.out_stage.n + kv.second.in_stage.n);
-  DevBuf vA, vB;
-  vA.alloc(size_t(std::max<int64_t>(total, 1)) * 8);
-  vB.alloc(size_t(std::max<int64_t>(total, 1)) * 8);
-  int64_t pos = 0;
+  // 1. referenced vids (src/dst of every staged tuple), sign-flipped for an unsigned sort.  One
+  // staged column at a time is sorted, deduplicated and merged into the running set, so the peak
+  // is 16 B per tuple of the largest column (not 16 B per vid reference of the whole snapshot:
+  // 69 GB for a writable RMAT-26, whose stages stay resident beside it)
+  DevBuf vA;
+  int64_t nuniq = 0;
   for (auto& kv : c.edges) {
     for (Staging* s : {&kv.second.out_stage, &kv.second.in_stage}) {
       if (s->n == 0) continue;
-      k_flip_copy<<<grid_for(s->n), 256, 0, c.stream>>>(s->src.as<int64_t>(), vA.as<uint64_t>() + pos, s->n, 0, 0, 0, 0);
-      pos += s->n;
-      k_flip_copy<<<grid_for(s->n), 256, 0, c.stream>>>(s->dst.as<int64_t>(), vA.as<uint64_t>() + pos, s->n, 0, 0, 0, 0);
-      pos += s->n;
+      for (const DevBuf* colp : {&s->src, &s->dst}) {
+        const int64_t n = s->n;
+        DevBuf t1, t2;
+        t1.alloc(size_t(n) * 8);
+        t2.alloc(size_t(n) * 8);
+        k_flip_copy<<<grid_for(n), 256, 0, c.stream>>>(colp->as<int64_t>(), t1.as<uint64_t>(), n, 0, 0, 0, 0);
+        radix_keys<uint64_t>(c, t1.as<uint64_t>(), t2.as<uint64_t>(), n, 64);
+        const int64_t m = unique_sorted<uint64_t>(c, t2.as<uint64_t>(), t1.as<uint64_t>(), n);
+        t2.release();
+        if (nuniq == 0) {
+          vA = std::move(t1);
+          nuniq = m;
+          continue;
+        }
+        DevBuf cat, srt;
+        cat.alloc(size_t(nuniq + m) * 8);
+        srt.alloc(size_t(nuniq + m) * 8);
+        NBG_HIP(hipMemcpyAsync(cat.p, vA.p, size_t(nuniq) * 8, hipMemcpyDeviceToDevice, c.stream));
+        NBG_HIP(hipMemcpyAsync(cat.as<uint64_t>() + nuniq, t1.p, size_t(m) * 8, hipMemcpyDeviceToDevice, c.stream));
+        t1.release();
+        vA.release();
+        radix_keys<uint64_t>(c, cat.as<uint64_t>(), srt.as<uint64_t>(), nuniq + m, 64);
+        nuniq = unique_sorted<uint64_t>(c, srt.as<uint64_t>(), cat.as<uint64_t>(), nuniq + m);
+        vA = std::move(cat);
+      }
     }
   }
-  int64_t nuniq = 0;
-  if (total > 0) {
-    radix_keys<uint64_t>(c, vA.as<uint64_t>(), vB.as<uint64_t>(), total, 64);
-    nuniq = unique_sorted<uint64_t>(c, vB.as<uint64_t>(), vA.as<uint64_t>(), total);
-  }
-  vB.release();
+  if (!vA.p) vA.alloc(8);
   // 2. owned set and global table
   std::vector<int64_t> counts(size_t(c.world), 0);
   DevBuf owned;
