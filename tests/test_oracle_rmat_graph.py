@@ -73,3 +73,24 @@ def test_shortest_path_matches_faithful(both):
     for i in range(len(s)):
         assert hops[i] == rows[i][2]
         assert list(paths[i]) == [v for v in rows[i][3:] if v is not None]
+
+
+def test_grouped_build_and_msum(both, monkeypatch):
+    """the grouped CSR build (bucket groups of ORA_RMAT_GROUP_KEYS samples, one generator pass
+    each: how RMAT-28 fits the build host) gives the single-pass build's graph, and the order-free
+    msum digest of a plain GO equals the msum of its materialised rows"""
+    scale, st, g = both
+    monkeypatch.setenv("ORA_RMAT_GROUP_KEYS", str(1 << 12))
+    g2 = O.RmatGraph(scale, 16, 1, threads=4)
+    assert g2.info() == g.info()
+    starts = synth.seeds(scale, 16, 1, 16)
+    for steps in (1, 2, 3):
+        r1, s1 = g.go(starts, steps)
+        r2, s2 = g2.go(starts, steps)
+        assert np.array_equal(r1, r2) and s1 == s2
+        ms, sc = g2.go_msum(starts, steps)
+        assert ms == O.msum(r1) and sc == s1
+    # msum is order-free and sensitive to the multiset
+    r1, _ = g.go(starts, 2)
+    assert O.msum(r1[::-1]) == O.msum(r1)
+    assert O.msum(r1[1:]) != O.msum(r1)
