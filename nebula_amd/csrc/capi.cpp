@@ -5,6 +5,7 @@
 
 namespace nbg {
 thread_local std::shared_ptr<BufPool> tl_pool;
+AllocClock g_alloc_clock;
 int32_t comm_unique_id(uint8_t out[128]);
 void comm_init(Ctx& c, const uint8_t id[128]);
 void free_rows_impl(void* impl);

@@ -14,6 +14,8 @@
 
 #include <chrono>
 #include <cstdint>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -76,6 +78,15 @@ struct BufPool {
   }
 };
 extern thread_local std::shared_ptr<BufPool> tl_pool;  // set for the duration of a query
+// host time spent in hipMalloc / hipFree of DevBufs (the build's phase trace reports it)
+struct AllocClock {
+  std::atomic<int64_t> alloc_ns{0}, free_ns{0}, allocs{0};
+};
+extern AllocClock g_alloc_clock;
+inline int64_t mono_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
 
 struct DevBuf {
   void* p = nullptr;
@@ -102,8 +113,13 @@ struct DevBuf {
   ~DevBuf() { release(); }
   void release() {
     if (p) {
-      if (pool) pool->put(p, bytes);
-      else (void)hipFree(p);
+      if (pool) {
+        pool->put(p, bytes);
+      } else {
+        const int64_t t0 = mono_ns();
+        (void)hipFree(p);
+        g_alloc_clock.free_ns += mono_ns() - t0;
+      }
     }
     p = nullptr;
     bytes = 0;
@@ -121,7 +137,10 @@ struct DevBuf {
         return;
       }
     }
+    const int64_t t0 = mono_ns();
     hipError_t e = hipMalloc(&p, b);
+    g_alloc_clock.alloc_ns += mono_ns() - t0;
+    g_alloc_clock.allocs++;
     if (e != hipSuccess) {
       p = nullptr;
       throw Error(NBG_E_NOMEM, "hipMalloc(" + std::to_string(b) + ") failed: " + hipGetErrorString(e));

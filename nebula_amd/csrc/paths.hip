@@ -245,7 +245,7 @@ __global__ void k_sp_regen(int mode, int side, int32_t j, const int32_t* plist, 
 // tuples; those of MET pairs short of src go to X.
 __global__ void k_sp_select(const uint64_t* __restrict__ live, int64_t nl, int32_t sweep, SpState st, SpCsr gout,
                             SpCsr gin, uint64_t* X, int64_t* Xdeg, int64_t cap_x, SpBufs bf,
-                            unsigned long long* cnt) {
+                            unsigned long long* cnt, const int32_t* push_pair = nullptr) {
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   const int64_t rounds = (nl + stride - 1) / stride;
   for (int64_t r = 0; r < rounds; r++) {
@@ -262,7 +262,7 @@ __global__ void k_sp_select(const uint64_t* __restrict__ live, int64_t nl, int32
       if (sweep) {
         // sweep = 2: stop one level short of src (the walk from src never reads dist_B(src),
         // and the in-lists of src's shortest-path out-neighbours are typically hub rows)
-        go = s == SP_MET && int32_t(t_lvl(t)) < st.res[p] - (sweep - 1);
+        go = s == SP_MET && int32_t(t_lvl(t)) < st.res[p] - (sweep - 1) && !(push_pair && push_pair[p]);
       } else if (s == SP_ACTIVE) {
         go = uint32_t(st.side[p]) == side;
         stay = !go;
@@ -282,6 +282,96 @@ __global__ void k_sp_select(const uint64_t* __restrict__ live, int64_t nl, int32
     if ((threadIdx.x & 63) == 0 && e) atomicAdd(cnt + C_XE, e);
     // carried tuples: every tuple of one launch has the same side (one list per side)
     put(bf.live_next[side], bf.cap_live[side], cnt, side ? C_LIVE1 : C_LIVE0, stay, t);
+  }
+}
+
+// ---- sweep direction per pair -----------------------------------------------------------------
+// A sweep step gives dist_B to the shortest-path vertices at forward depth k = f - j.  Pull scans
+// the in-rows of the level above (the current sweep list); push scans the out-rows of the forward
+// BFS's level-k vertices (the arena's side-0 tuples at depth k), claiming a vertex whose
+// out-neighbour has dist_B = L - k - 1.  Both claim the same vertices; each pair takes the side
+// with fewer adjacency entries.
+__device__ inline bool sweep_pull_go(const SpState& st, uint64_t t, int32_t sweep) {
+  const uint32_t p = t_pair(t);
+  return st.state[p] == SP_MET && int32_t(t_lvl(t)) < st.res[p] - (sweep - 1);
+}
+__global__ void k_sweep_pull_cost(const uint64_t* __restrict__ live, int64_t nl, int32_t sweep, SpState st,
+                                  SpCsr gin, unsigned long long* pull) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int64_t rounds = (nl + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    bool go = false;
+    uint32_t p = 0;
+    unsigned long long d = 0;
+    if (i < nl) {
+      const uint64_t t = live[i];
+      p = t_pair(t);
+      go = sweep_pull_go(st, t, sweep);
+      if (go) d = (unsigned long long)sp_deg(gin, t_row(t)) + 1;
+    }
+    wave_add_keyed(pull, p, d, go);
+  }
+}
+// forward level-k tuples of the arena (k = f - j) of pairs still sweeping
+__device__ inline bool sweep_push_tuple(const SpState& st, uint64_t t, int32_t j) {
+  if (t_side(t) != 0) return false;
+  const uint32_t p = t_pair(t);
+  if (st.state[p] != SP_MET) return false;
+  const int32_t k = st.lvl[p] - j;
+  return k >= 1 && int32_t(t_lvl(t)) == k;
+}
+__global__ void k_sweep_push_cost(const uint64_t* __restrict__ arena, int64_t na, int32_t j, SpState st,
+                                  SpCsr gout, const unsigned long long* pull, unsigned long long* push) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int64_t rounds = (na + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    bool go = false;
+    uint32_t p = 0;
+    unsigned long long d = 0;
+    if (i < na) {
+      const uint64_t t = arena[i];
+      go = sweep_push_tuple(st, t, j);
+      p = t_pair(t);
+      go = go && pull[p] > 0;  // pairs with nothing to pull are done sweeping
+      if (go) d = (unsigned long long)sp_deg(gout, t_row(t)) + 1;
+    }
+    wave_add_keyed(push, p, d, go);
+  }
+}
+__global__ void k_sweep_choose(const unsigned long long* pull, const unsigned long long* push, int32_t B,
+                               int32_t* push_pair) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < B) push_pair[p] = pull[p] > 0 && push[p] < pull[p];
+}
+// X += the forward level-k tuples of push pairs (their out-rows are the step's adjacency)
+__global__ void k_sweep_push_select(const uint64_t* __restrict__ arena, int64_t na, int32_t j, SpState st,
+                                    SpCsr gout, const int32_t* push_pair, uint64_t* X, int64_t* Xdeg,
+                                    int64_t cap_x, unsigned long long* cnt) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int64_t rounds = (na + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    bool go = false;
+    uint64_t t = 0;
+    int64_t d = 0;
+    if (i < na) {
+      t = arena[i];
+      go = sweep_push_tuple(st, t, j) && push_pair[t_pair(t)];
+      if (go) d = sp_deg(gout, t_row(t));
+    }
+    const int64_t xs = wave_append(cnt + C_X, go);
+    if (go) {
+      if (xs < cap_x) {
+        X[xs] = t;
+        Xdeg[xs] = d;
+      } else {
+        atomicOr(cnt + C_OVF, 2ull);
+      }
+    }
+    const unsigned long long e = wsum((unsigned long long)d);
+    if ((threadIdx.x & 63) == 0 && e) atomicAdd(cnt + C_XE, e);
   }
 }
 
@@ -381,12 +471,18 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
         const uint64_t idx = didx(st, p, w, a.n);
         if (!a.sweep) {
           claimed = claim_byte(a.dist[side], idx, l + 1);
-        } else {
+        } else if (side == 1) {  // pull: in-neighbour w of a level-(k+1) vertex, forward depth k
           const int32_t need = st.res[p] - int32_t(l) - 1;
           if (need >= 0 && a.dist[0][idx] == uint8_t(need)) claimed = claim_byte(a.dist[1], idx, l + 1);
+        } else {  // push: the tuple's own vertex u (forward depth l) if out-neighbour w is on a path
+          const int32_t need = st.res[p] - int32_t(l) - 1;
+          const uint32_t u = t_row(tu);
+          if (a.dist[1][idx] == uint8_t(need)) claimed = claim_byte(a.dist[1], didx(st, p, u, a.n), uint32_t(need + 1));
         }
       }
-      const uint64_t nt = mk_tup(side, p, l + 1, w);
+      // a push claim records u with dist_B = L - l; every other claim the neighbour at depth l + 1
+      const bool push_t = a.sweep && side == 0;
+      const uint64_t nt = push_t ? mk_tup(1, p, uint32_t(st.res[p]) - l, t_row(tu)) : mk_tup(side, p, l + 1, w);
       put(bf.arena, bf.cap_arena, cnt, C_ARENA, claimed, nt);
       if (a.sweep) {
         put(bf.sweep_next, bf.cap_sweep, cnt, C_SWEEP, claimed, nt);
@@ -1112,8 +1208,10 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       if (E > 0) sp_hop(2, ems, nX, E, cl, iter, active);
       if (int64_t(hc[C_ARENA]) > W.cap_arena) arena_lost = true;  // the batch end resets every byte instead
       n_arena = std::min<int64_t>(int64_t(hc[C_ARENA]), W.cap_arena);
+      bool regen_done = false;
       for (int s = 0; s < 2; s++) {
         if (int64_t(hc[C_LIVE0 + s]) <= W.cap_next[s]) continue;
+        regen_done = true;
         const int64_t total = int64_t(hc[C_LIVE0 + s]);
         reserve(c, W.live_next[s], W.cap_next[s], total + 64, carried[s]);
         const int32_t np = pair_list([s](int32_t stt, int32_t ps, int32_t) { return stt == SP_ACTIVE && ps == s; });
@@ -1121,13 +1219,14 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         regen(RG_LIVE, s, 0, np, W.live_next[s].as<uint64_t>(), W.cap_next[s], C_LIVE0 + s);
       }
       if (int64_t(hc[C_MEET]) > W.cap_meet) {
+        regen_done = true;
         reserve(c, W.meet, W.cap_meet, int64_t(hc[C_MEET]) + 64, n_meet);
         const int32_t tag = 2 + iter;
         const int32_t np = pair_list([tag](int32_t stt, int32_t, int32_t m) { return stt == SP_MET && m == tag; });
         set_counter(C_MEET, n_meet);
         regen(RG_MEET, 1, 0, np, W.meet.as<uint64_t>(), W.cap_meet, C_MEET);
       }
-      sync_counters();
+      if (regen_done) sync_counters();  // the regenerated lists' counts
       n_live[0] = int64_t(hc[C_LIVE0]);
       n_live[1] = int64_t(hc[C_LIVE1]);
       n_meet = int64_t(hc[C_MEET]);
@@ -1143,13 +1242,39 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     const int32_t sweep_mode = c.opt("sp_sweep_src", 0) ? 1 : 2;
     DevBuf* cur = &W.meet;
     int nxt = 0;
+    // per pair and step: pull (in-rows of the level above) or push (out-rows of the forward
+    // level, from the arena) -- needs every forward claim in the arena
+    const bool push_ok = c.opt("sp_sweep_push", 1) != 0 && !arena_lost && sweep_mode == 2;
+    DevBuf swc;
+    unsigned long long *pullc = nullptr, *pushc = nullptr;
+    int32_t* push_pair = nullptr;
+    if (push_ok) {
+      swc.alloc(size_t(nb) * 20 + 64);
+      pullc = swc.as<unsigned long long>();
+      pushc = pullc + nb;
+      push_pair = reinterpret_cast<int32_t*>(pushc + nb);
+    }
     for (int32_t j = 1; n_sw > 0; j++) {
-      ensure_x(n_sw);
+      const bool push_now = push_ok && !arena_lost;  // an arena overflow mid-sweep: pull only
+      ensure_x(n_sw + (push_now ? n_arena : 0));
       NBG_HIP(hipMemsetAsync(cnt + C_X, 0, 24, c.stream));
       NBG_HIP(hipMemsetAsync(cnt + C_SWEEP, 0, 16, c.stream));  // C_SWEEP, C_XE
       refresh(nullptr, 0);
+      if (push_now) {
+        NBG_HIP(hipMemsetAsync(pullc, 0, size_t(nb) * 16, c.stream));
+        k_sweep_pull_cost<<<grid_n(n_sw), 256, 0, c.stream>>>(cur->as<uint64_t>(), n_sw, sweep_mode, st, gin, pullc);
+        if (n_arena)
+          k_sweep_push_cost<<<grid_n(n_arena), 256, 0, c.stream>>>(W.arena.as<uint64_t>(), n_arena, j, st, gout, pullc,
+                                                                    pushc);
+        k_sweep_choose<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(pullc, pushc, int32_t(nb), push_pair);
+      }
       k_sp_select<<<grid_n(n_sw), 256, 0, c.stream>>>(cur->as<uint64_t>(), n_sw, sweep_mode, st, gout, gin, W.X.as<uint64_t>(),
-                                                       W.Xdeg.as<int64_t>(), W.cap_x, bf, cnt);
+                                                       W.Xdeg.as<int64_t>(), W.cap_x, bf, cnt,
+                                                       push_now ? push_pair : nullptr);
+      if (push_now && n_arena)
+        k_sweep_push_select<<<grid_n(n_arena), 256, 0, c.stream>>>(W.arena.as<uint64_t>(), n_arena, j, st, gout,
+                                                                    push_pair, W.X.as<uint64_t>(),
+                                                                    W.Xdeg.as<int64_t>(), W.cap_x, cnt);
       NBG_HIP(hipGetLastError());
       sync_counters();
       const int64_t nX = int64_t(hc[C_X]), E = int64_t(hc[C_XE]);

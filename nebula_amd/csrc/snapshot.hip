@@ -2232,6 +2232,24 @@ void snapshot_finalize(Ctx& c) {
   if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
   double t0 = now_s();
   const bool keep = c.opt("writable", 0) != 0;
+  // option build_trace: per-phase wall time on stderr (the stream drained at each mark)
+  const bool trace = c.opt("build_trace", 0) != 0;
+  double tmark = t0;
+  if (trace) {
+    g_alloc_clock.alloc_ns = 0;
+    g_alloc_clock.free_ns = 0;
+    g_alloc_clock.allocs = 0;
+  }
+  auto phase = [&](const char* name) {
+    if (!trace) return;
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    const double t = now_s();
+    const int64_t an = g_alloc_clock.alloc_ns.exchange(0), fn = g_alloc_clock.free_ns.exchange(0);
+    const int64_t na = g_alloc_clock.allocs.exchange(0);
+    fprintf(stderr, "[nbg build] %-22s %8.3f s  (hipMalloc %lld x %.3f s, hipFree %.3f s)\n", name, t - tmark,
+            (long long)na, an * 1e-9, fn * 1e-9);
+    tmark = t;
+  };
   for (auto& kv : c.edges)
     if (kv.second.rmat_stream) {
       finalize_rmat_stream(c, kv.second);
@@ -2278,6 +2296,7 @@ void snapshot_finalize(Ctx& c) {
     }
   }
   if (!vA.p) vA.alloc(8);
+  phase("vertex set");
   // 2. owned set and global table
   std::vector<int64_t> counts(size_t(c.world), 0);
   DevBuf owned;
@@ -2335,6 +2354,7 @@ void snapshot_finalize(Ctx& c) {
     vA.release();
   }
   if (c.opt("degree_order", 1)) order_by_degree(c, owned, n_owned);
+  phase("degree order");
   // 3. counts -> base; allgather owned tables into vid_of (rank-major; within a rank by
   // descending out-degree, or by vid with degree_order=0)
   if (c.world == 1) {
@@ -2394,7 +2414,9 @@ void snapshot_finalize(Ctx& c) {
   NBG_HIP(hipMemcpyAsync(&c.ht_min_gidx, dmin.p, 4, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
   c.ht_has_min = c.ht_min_gidx >= 0;
+  phase("vertex map + hash");
   build_tag_columns(c);
+  phase("tag columns");
   // 5. bytewise order rank of every vertex (for CSR row order = RocksDB key order)
   DevBuf brank;
   {
@@ -2411,12 +2433,16 @@ void snapshot_finalize(Ctx& c) {
       k_scatter_rank<<<grid_for(c.n_global), 256, 0, c.stream>>>(i2.as<uint32_t>(), brank.as<uint32_t>(), c.n_global);
     }
   }
+  phase("bytewise ranks");
   // 6. CSRs
   for (auto& kv : c.edges) {
     EdgeSpace& es = kv.second;
     build_csr(c, es.out_stage, es.fields, true, es.out, brank.as<uint32_t>(), !keep);
+    phase("out CSR");
     build_csr(c, es.in_stage, es.fields, false, es.in, brank.as<uint32_t>(), !keep);
+    phase("in CSR");
     if (c.opt("bottom_up", 1)) build_transpose(c, es);
+    phase("transpose + slabs");
   }
   if (!keep) {
     c.heap.release();

@@ -2127,6 +2127,36 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
   block_store_partials(acc, 2, lds64, partials);
 }
 
+// starts (gidx) -> deduplicated frontier: bitmap bits (set once, by a returning atomicOr) and
+// list of the starts with out-edges; Kd[0] list length, Kd[12] vertices, Kd[13] out-degree sum
+// (the counters launch_compact leaves)
+__global__ void k_starts_bits(const int32_t* g, int64_t n, int64_t lo, int64_t hi, const uint32_t* odeg,
+                              uint32_t* bits, int32_t* out, unsigned long long* Kd) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int64_t rounds = (n + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    bool keep = false;
+    int32_t loc = 0;
+    uint32_t od = 0;
+    if (i < n) {
+      const int32_t x = g[i];
+      if (x >= lo && x < hi) {
+        loc = int32_t(x - lo);
+        od = odeg[loc];
+        const uint32_t bit = 1u << (loc & 31);
+        keep = od && !(atomicOr(bits + (loc >> 5), bit) & bit);
+      }
+    }
+    const int64_t s = wave_append(Kd, keep);
+    if (keep) {
+      out[s] = loc;
+      atomicAdd(Kd + 12, 1ull);
+      atomicAdd(Kd + 13, (unsigned long long)od);
+    }
+  }
+}
+
 // starts (gidx) -> mark owned in the byte-map (dedup path) or list them (steps == 1 path)
 __global__ void k_mark_gidx(const int32_t* g, int64_t n, int64_t lo, int64_t hi, uint8_t* map) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
@@ -3204,6 +3234,14 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   if (ns) {
     if (s.steps == 1 && !s.distinct) {
       k_list_starts<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, F, K.d);
+    } else if (c.world == 1 && es.odeg.p && c.opt("starts_bits", 1) != 0) {
+      // one rank: dedup the starts through the frontier bitmap itself (a few hundred atomics)
+      // instead of marking the byte map and compacting the whole vertex space
+      NBG_HIP(hipMemsetAsync(bits16, 0, c.ws_bits_send.bytes, c.stream));
+      k_starts_bits<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, es.odeg.as<uint32_t>(),
+                                                        reinterpret_cast<uint32_t*>(bits16), F, K.d);
+      if (!s.distinct)
+        k_starts_degree<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, K.d + 30);
     } else {
       k_mark_gidx<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, map);
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, F, bits16, K.d, es.odeg.as<uint32_t>());
@@ -3473,7 +3511,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     fp = FastArgs{pc.data.p, pc.present.as<uint8_t>(), pc.width, fpk.op, fpk.k};
   }
   DevBuf dprog;
-  if (pk == PK_VM || !default_yield) {
+  // DISTINCT _dst reads no YIELD program (and the WHERE program only on the VM path)
+  const bool lone_dst_distinct = s.distinct && yields.size() == 1 && yields[0].n == 1 && yields[0].ins[0].op == P_DST;
+  if (pk == PK_VM || (!default_yield && !lone_dst_distinct)) {
     dprog.alloc(sizeof(Program) * (yields.size() + 1));
     c.h2d(dprog.p, &where, sizeof(Program));
     c.h2d(dprog.as<Program>() + 1, yields.data(), sizeof(Program) * yields.size());

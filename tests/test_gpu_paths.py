@@ -181,3 +181,26 @@ def test_meet_probe_on_and_off_match_oracle(rmat, probe, vmajor):
     finally:
         sp.set_option("sp_probe", 1)
         sp.set_option("sp_vmajor", 0)
+
+
+@pytest.mark.parametrize("push,walk_wg,sweep_src", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 0, 1), (1, 0, 1)])
+def test_sweep_direction_and_walk_variants(rmat, push, walk_wg, sweep_src):
+    """the sweep's per-pair push/pull choice (forced off: pull only), the workgroup-per-pair walk
+    and the sweep that runs down to src all give the oracle's paths"""
+    scale, sp, st = rmat
+    sp.set_option("sp_sweep_push", push)
+    sp.set_option("sp_walk_wg", walk_wg)
+    sp.set_option("sp_sweep_src", sweep_src)
+    try:
+        s, t = synth.pairs(scale, 16, 1, 300, pick_seed=23)
+        es, et_ = edge_case_pairs(scale)
+        src, dst = np.concatenate([s, es]), np.concatenate([t, et_])
+        for max_steps in (3, 8):
+            got = sp.shortest_path(src, dst, FOLLOW, max_steps).rows()
+            assert got == oracle_paths(st, src, dst, FOLLOW, max_steps)
+        hops = sp.last_timing()["hops"]
+        assert any(h["mode"] == "sp-sweep" for h in hops) or scale < 11
+    finally:
+        sp.set_option("sp_sweep_push", 1)
+        sp.set_option("sp_walk_wg", 0)
+        sp.set_option("sp_sweep_src", 0)

@@ -65,9 +65,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=int, default=24)
     ap.add_argument("--edges", type=int, default=1 << 20)
+    ap.add_argument("--trace", action="store_true", help="per-phase build / commit times on stderr")
     a = ap.parse_args()
     sp = GraphSpace(PARTS)
     sp.set_option("writable", 1)
+    if a.trace:
+        sp.set_option("build_trace", 1)
     sp.set_edge_schema(FOLLOW, [("weight", 2)])
     t0 = time.perf_counter()
     sp.gen_rmat(a.scale, 16, SEED, FOLLOW)
