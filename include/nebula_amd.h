@@ -134,6 +134,8 @@ typedef struct {
   int64_t local_in_edges;
   int64_t device_bytes;     /* HBM held by the snapshot on this rank                          */
   double build_seconds;
+  int64_t commits;          /* commits applied since finalize                                 */
+  int64_t merge_commits;    /* of them, merged into the committed order (no full rebuild)     */
 } nbg_snapshot_info;
 int32_t nbg_snapshot_info_get(nbg_ctx* ctx, int32_t edge_type, nbg_snapshot_info* out);
 /* CSR export for tests: out-degree of vid (-1 if unknown) */

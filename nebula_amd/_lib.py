@@ -44,7 +44,8 @@ class NbgError(RuntimeError):
 class SnapshotInfo(C.Structure):
     _fields_ = [("num_vertices", C.c_int64), ("local_vertices", C.c_int64),
                 ("local_out_edges", C.c_int64), ("local_in_edges", C.c_int64),
-                ("device_bytes", C.c_int64), ("build_seconds", C.c_double)]
+                ("device_bytes", C.c_int64), ("build_seconds", C.c_double),
+                ("commits", C.c_int64), ("merge_commits", C.c_int64)]
 
 
 class Rows(C.Structure):

@@ -1,4 +1,5 @@
 // capi.cpp -- extern "C" entry points declared in include/nebula_amd.h.
+#include <algorithm>
 #include <cstring>
 
 #include "engine.h"
@@ -6,6 +7,21 @@
 namespace nbg {
 thread_local std::shared_ptr<BufPool> tl_pool;
 AllocClock g_alloc_clock;
+namespace {
+std::mutex g_pools_mu;
+std::vector<BufPool*> g_pools;
+}  // namespace
+void pool_register(BufPool* p, bool add) {
+  std::lock_guard<std::mutex> lk(g_pools_mu);
+  if (add) g_pools.push_back(p);
+  else g_pools.erase(std::remove(g_pools.begin(), g_pools.end(), p), g_pools.end());
+}
+size_t pool_trim_all() {
+  std::lock_guard<std::mutex> lk(g_pools_mu);
+  size_t freed = 0;
+  for (BufPool* p : g_pools) freed += p->trim();
+  return freed;
+}
 int32_t comm_unique_id(uint8_t out[128]);
 void comm_init(Ctx& c, const uint8_t id[128]);
 void free_rows_impl(void* impl);
@@ -210,6 +226,8 @@ int32_t nbg_snapshot_info_get(nbg_ctx* ctx, int32_t edge_type, nbg_snapshot_info
     out->device_bytes = int64_t(it->second.out.bytes() + it->second.in.bytes() + c.vid_of.bytes + c.ht_keys.bytes +
                                 c.ht_vals.bytes);
     out->build_seconds = c.build_seconds;
+    out->commits = c.commits;
+    out->merge_commits = c.merge_commits;
     return NBG_OK;
   });
 }

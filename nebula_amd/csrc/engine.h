@@ -47,12 +47,17 @@ struct Error : std::runtime_error {
 // back to the context's pool and are reused by later queries on the same stream (stream order
 // makes the reuse safe).  Blocks allocated outside a query scope (the snapshot) use
 // hipMalloc/hipFree directly.
+struct BufPool;
+void pool_register(BufPool* p, bool add);
+size_t pool_trim_all();  // every live pool's cache back to the driver (an out-of-memory retry)
 struct BufPool {
   std::mutex mu;
   std::multimap<size_t, void*> blocks;
   size_t cached = 0;
   size_t limit = size_t(16) << 30;
+  BufPool() { pool_register(this, true); }
   ~BufPool() {
+    pool_register(this, false);
     for (auto& b : blocks) (void)hipFree(b.second);
   }
   void* get(size_t want, size_t& got) {
@@ -75,6 +80,15 @@ struct BufPool {
       }
     }
     (void)hipFree(p);
+  }
+  // hand every cached block back to the driver (a failed hipMalloc retries after this)
+  size_t trim() {
+    std::lock_guard<std::mutex> lk(mu);
+    const size_t freed = cached;
+    for (auto& b : blocks) (void)hipFree(b.second);
+    blocks.clear();
+    cached = 0;
+    return freed;
   }
 };
 extern thread_local std::shared_ptr<BufPool> tl_pool;  // set for the duration of a query
@@ -139,6 +153,10 @@ struct DevBuf {
     }
     const int64_t t0 = mono_ns();
     hipError_t e = hipMalloc(&p, b);
+    if (e == hipErrorOutOfMemory && pool_trim_all() > 0) {
+      (void)hipGetLastError();
+      e = hipMalloc(&p, b);
+    }
     g_alloc_clock.alloc_ns += mono_ns() - t0;
     g_alloc_clock.allocs++;
     if (e != hipSuccess) {
@@ -241,6 +259,14 @@ struct EdgeSpace {
   int64_t out_nnz_global = -1;  // sum of out.nnz over ranks (direction heuristic)
   // streamed RMAT (one rank, graphs past the tuple stage's 2^32 cap): gen_rmat only records the
   // generator's parameters and finalize builds the CSRs bucket by bucket from regenerated samples
+  // writable snapshots: the sorted tuple order of the last build per direction (0 out, 1 in):
+  // tuple permutation, (src_local << 32 | byterank(dst)) keys and dst gidx by tuple index.  A
+  // commit without new vertices merges its sorted batch into it instead of re-sorting every tuple
+  struct Order {
+    DevBuf perm, skey, dstg;
+    int64_t n = 0;
+  };
+  Order ord[2];
   bool rmat_stream = false;
   int32_t rmat_scale = 0, rmat_ef = 0;
   uint64_t rmat_seed = 0;
@@ -277,6 +303,7 @@ struct TagSpace {
   std::string name;
   std::vector<Field> fields;
   Staging stage;              // src = vid, ver, part, rank = load sequence number (write order)
+  int64_t committed_n = 0;    // stage.n at the last finalize / commit (merge-commit eligibility)
   std::vector<PropCol> cols;  // per field, [n_global]; data int64 bits, present uint8:
                               // 0 none, 1 row of the vid's own part, 2 row of a foreign part only
   DevBuf part;                // int32 [n_global]: the part the vertex's row came from
@@ -341,6 +368,7 @@ struct Ctx {
   std::vector<int64_t> base;     // G+1
   std::vector<int64_t> counts;   // vertices per rank
   DevBuf vid_of;                 // int64 [n_global]
+  DevBuf brank;                  // writable: bytewise rank of every gidx's vid (merge commits)
   DevBuf ht_keys, ht_vals;       // int64 / int32 [ht_cap]
   int64_t ht_cap = 0;
   bool ht_has_min = false;       // INT64_MIN vid present (the empty-slot sentinel)
@@ -360,6 +388,7 @@ struct Ctx {
   bool has_log = false;
   bool pending_writes = false;
   int64_t commits = 0;
+  int64_t merge_commits = 0;
 
   // workspaces for queries
   DevBuf ws_map;       // uint8 [n_global] visited / next-set bytemap
@@ -401,6 +430,10 @@ struct Ctx {
   size_t tev_used = 0;
   std::vector<PendingTime> tpend;
   std::shared_ptr<BufPool> pool = std::make_shared<BufPool>();
+  // snapshot build / commit temporaries: freed blocks stay with the process (a fresh multi-GB
+  // hipMalloc costs up to seconds: r03a trace), so the phases of a build and later commits of a
+  // writable snapshot reuse them.  Trimmed after a read-only build.
+  std::shared_ptr<BufPool> build_pool = std::make_shared<BufPool>();
   unsigned long long* host_counters = nullptr;  // pinned, 64 entries
   void* host_stage = nullptr;                   // pinned, kHostStageBytes (query inputs)
   size_t host_stage_used = 0;

@@ -11,6 +11,7 @@
 //   (QueryBaseProcessor.inl:349-362, P3), emit CSR + narrowed SoA property columns.
 #include <climits>
 
+#include <rocprim/device/device_merge.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_reduce.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -30,6 +31,14 @@ struct SchemaDev {
   int32_t nfields;
   int32_t types[kMaxFields];
 };
+
+// the context's build-time block cache (option build_pool_gb, 0 = plain hipMalloc / hipFree)
+static std::shared_ptr<BufPool> build_pool(Ctx& c) {
+  const int64_t gb = c.opt("build_pool_gb", 128);
+  if (gb <= 0) return nullptr;
+  c.build_pool->limit = size_t(gb) << 30;
+  return c.build_pool;
+}
 
 // ------------------------------------------------------------------------------------------
 // small generic kernels
@@ -464,6 +473,7 @@ static void decode_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
 
 void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t* koff,
                         const uint8_t* vb, const uint64_t* voff, size_t n) {
+  PoolScope build_scope(build_pool(c));  // staged tuples
   if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
   decode_part(c, part, kb, koff, vb, voff, n);
 }
@@ -482,7 +492,38 @@ void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
 // then queries keep reading the previous commit (a RocksDB snapshot's view).
 // ------------------------------------------------------------------------------------------
 // drop everything snapshot_finalize derives from the staged tuples
+static void reset_edge_derived(EdgeSpace& es) {
+  es.out = Csr();
+  es.in = Csr();
+  es.rep_out = Csr();
+  es.rep_in = Csr();
+  es.has_rep = false;
+  es.tr = Csr();
+  es.t_eid.release();
+  es.has_tr = es.has_t_eid = false;
+  es.out_nnz_global = -1;
+  es.slab_k = 0;
+  es.slab_col.release();
+  es.slab_props.clear();
+  es.tcol_q.release();
+  es.q_field = -1;
+  es.q_gbits = es.q_bits = 0;
+  for (int h = 0; h < 2; h++) {
+    es.pair_col[h].release();
+    es.pair_props[h].clear();
+  }
+  es.odeg.release();
+}
+
 static void reset_derived(Ctx& c) {
+  c.brank.release();
+  for (auto& kv : c.edges)
+    for (auto& o : kv.second.ord) {
+      o.perm.release();
+      o.skey.release();
+      o.dstg.release();
+      o.n = 0;
+    }
   c.vid_of.release();
   c.ht_keys.release();
   c.ht_vals.release();
@@ -490,29 +531,7 @@ static void reset_derived(Ctx& c) {
   c.ht_has_min = false;
   c.ht_min_gidx = -1;
   c.tag_table.release();
-  for (auto& kv : c.edges) {
-    EdgeSpace& es = kv.second;
-    es.out = Csr();
-    es.in = Csr();
-    es.rep_out = Csr();
-    es.rep_in = Csr();
-    es.has_rep = false;
-    es.tr = Csr();
-    es.t_eid.release();
-    es.has_tr = es.has_t_eid = false;
-    es.out_nnz_global = -1;
-    es.slab_k = 0;
-    es.slab_col.release();
-    es.slab_props.clear();
-    es.tcol_q.release();
-    es.q_field = -1;
-    es.q_gbits = es.q_bits = 0;
-    for (int h = 0; h < 2; h++) {
-      es.pair_col[h].release();
-      es.pair_props[h].clear();
-    }
-    es.odeg.release();
-  }
+  for (auto& kv : c.edges) reset_edge_derived(kv.second);
   for (auto& kv : c.tags) {
     kv.second.cols.clear();
     kv.second.part.release();
@@ -524,8 +543,15 @@ static void reset_derived(Ctx& c) {
   c.sp = Ctx::SpWork();
 }
 
+// Merge commit (one rank, edge writes only, no new vertex): the vertex numbering, vertex map
+// and tag columns stay; each edge CSR merges its sorted batch into the committed order
+// (build_csr merge mode) and the transposed CSR is rebuilt from the new out CSR.  Returns false
+// when the batch needs the full rebuild (new vertices, tag writes, several ranks).
+static bool commit_merge(Ctx& c);
+
 void snapshot_write_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t* koff,
                          const uint8_t* vb, const uint64_t* voff, size_t n) {
+  PoolScope build_scope(build_pool(c));  // staged tuples
   if (!c.finalized) {  // before the first commit a write batch is one more loaded batch
     decode_part(c, part, kb, koff, vb, voff, n);
     return;
@@ -547,6 +573,12 @@ void snapshot_commit(Ctx& c) {
   if (!c.has_log) throw Error(NBG_E_STATE, "snapshot is not writable (set option writable=1 before finalize)");
   // collective when world > 1: every rank rebuilds, with or without writes of its own
   NBG_HIP(hipStreamSynchronize(c.stream));
+  if (commit_merge(c)) {
+    c.pending_writes = false;
+    c.commits++;
+    c.merge_commits++;
+    return;
+  }
   reset_derived(c);
   c.pending_writes = false;
   c.finalized = false;
@@ -628,6 +660,7 @@ __global__ void k_gen_rmat(int64_t lo, int64_t hi, int32_t scale, uint64_t seed,
 }
 
 void snapshot_gen_rmat(Ctx& c, int32_t scale, int32_t ef, uint64_t seed, int32_t et) {
+  PoolScope build_scope(build_pool(c));  // staged tuples
   if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
   auto it = c.edges.find(et);
   if (it == c.edges.end()) throw Error(NBG_E_INVALID_ARG, "edge type not registered");
@@ -1014,8 +1047,36 @@ static void gather_props(Ctx& c, Staging& s, const std::vector<Field>& fields, c
 }
 
 // Builds one CSR from a staging area.  Returns after freeing the staging buffers.
+// (src, rank bytes, dst bytes, version bytes) order of two tuples: the merge commit's key (the
+// sort's last key, load sequence descending, is implied: a batch is newer than every committed
+// tuple and the merge puts it first among equals)
+struct GroupLess {
+  const uint64_t* skey;
+  const int64_t* rank;  // null: constant
+  const int64_t* ver;   // null: constant
+  __device__ bool operator()(uint32_t a, uint32_t b) const {
+    const uint64_t ka = skey[a], kb = skey[b];
+    if ((ka >> 32) != (kb >> 32)) return (ka >> 32) < (kb >> 32);
+    if (rank) {
+      const uint64_t ra = bswap64(uint64_t(rank[a])), rb = bswap64(uint64_t(rank[b]));
+      if (ra != rb) return ra < rb;
+    }
+    if (uint32_t(ka) != uint32_t(kb)) return uint32_t(ka) < uint32_t(kb);
+    if (ver) {
+      const uint64_t va = bswap64(uint64_t(ver[a])), vb = bswap64(uint64_t(ver[b]));
+      if (va != vb) return va < vb;
+    }
+    return false;
+  }
+};
+__global__ void k_iota_off_u32(uint32_t* p, int64_t n, int64_t off) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    p[i] = uint32_t(off + i);
+}
+
 static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool with_props, Csr& out,
-                      const uint32_t* byterank, bool consume = true) {
+                      const uint32_t* byterank, bool consume = true, EdgeSpace::Order* ord = nullptr,
+                      bool merge = false) {
   out = Csr();  // a commit retried after a failed build must not extend a half-built CSR
   int64_t n = s.n;
   int64_t lo = c.owned_lo(), hi = c.owned_hi();
@@ -1034,61 +1095,113 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
     return;
   }
   if (n >= (int64_t(1) << 32)) throw Error(NBG_E_UNSUPPORTED, "more than 2^32 edges on one rank");
-  // keys
-  DevBuf keyA, keyB, permA, permB, dstg, err;
-  keyA.alloc(size_t(n) * 8);
-  keyB.alloc(size_t(n) * 8);
-  permA.alloc(size_t(n) * 4);
-  permB.alloc(size_t(n) * 4);
-  dstg.alloc(size_t(n) * 4);
+  int srcbits = 1;
+  while ((int64_t(1) << srcbits) < std::max<int64_t>(out.n_rows, 2)) srcbits++;
+  DevBuf keyA, keyB, permA, permB, permM, dstg, err;
   err.alloc(8);
   NBG_HIP(hipMemsetAsync(err.p, 0, 8, c.stream));
-  k_edge_keys<<<grid_for(n), 256, 0, c.stream>>>(s.src.as<int64_t>(), s.dst.as<int64_t>(), n, c.ht_keys.as<int64_t>(),
-                                               c.ht_vals.as<int32_t>(), uint64_t(c.ht_cap - 1), c.ht_has_min,
-                                               c.ht_min_gidx, lo, hi, byterank, keyA.as<uint64_t>(),
-                                               permA.as<uint32_t>(), dstg.as<int32_t>(), err.as<unsigned long long>());
+  uint32_t* perm = nullptr;
+  DevBuf* perm_owner = nullptr;
+  DevBuf& skey_keep = keyA;  // (src_local << 32 | byterank(dst)) by tuple index
+  // LSD passes over the tuples listed in pin (m of them, global tuple indices, already ordered by
+  // load sequence descending): version bytes, dst bytes, rank bytes, then src; returns the buffer
+  // holding the result (pin or pout)
+  auto lsd = [&](uint32_t* pin, uint32_t* pout, int64_t m) -> uint32_t* {
+    DevBuf keyC;
+    keyC.alloc(size_t(m) * 8);
+    auto pass_bswap = [&](const DevBuf& vals) {
+      k_gather_key_bswap<<<grid_for(m), 256, 0, c.stream>>>(vals.as<int64_t>(), pin, keyC.as<uint64_t>(), m);
+      radix_pairs<uint64_t, uint32_t>(c, keyC.as<uint64_t>(), keyB.as<uint64_t>(), pin, pout, m, 64);
+      std::swap(pin, pout);
+    };
+    if (!s.ver_const) pass_bswap(s.ver);
+    pass_bswap(s.dst);
+    if (!s.rank_const) pass_bswap(s.rank);
+    k_gather_key_src<<<grid_for(m), 256, 0, c.stream>>>(skey_keep.as<uint64_t>(), pin, keyC.as<uint64_t>(), m);
+    radix_pairs<uint64_t, uint32_t>(c, keyC.as<uint64_t>(), keyB.as<uint64_t>(), pin, pout, m, srcbits);
+    return pout;
+  };
+  const int64_t n0 = ord ? ord->n : 0;
+  const bool do_merge = merge && ord && n0 > 0 && n0 < n && ord->perm.p && s.seq.bytes >= size_t(n) * 8;
+  if (do_merge) {
+    // merge commit: keys of the batch [n0, n) only, the batch sorted on its own (LSD, load
+    // sequence descending first), then merged into the committed order -- the batch first among
+    // equal groups (it is newer), which is the full sort's order
+    const int64_t mb = n - n0;
+    keyA.alloc(size_t(n) * 8);
+    dstg.alloc(size_t(n) * 4);
+    keyB.alloc(size_t(mb) * 8);
+    permA.alloc(size_t(mb) * 4);
+    permB.alloc(size_t(mb) * 4);
+    NBG_HIP(hipMemcpyAsync(keyA.p, ord->skey.p, size_t(n0) * 8, hipMemcpyDeviceToDevice, c.stream));
+    NBG_HIP(hipMemcpyAsync(dstg.p, ord->dstg.p, size_t(n0) * 4, hipMemcpyDeviceToDevice, c.stream));
+    k_edge_keys<<<grid_for(mb), 256, 0, c.stream>>>(
+        s.src.as<int64_t>() + n0, s.dst.as<int64_t>() + n0, mb, c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
+        uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, lo, hi, byterank, keyA.as<uint64_t>() + n0,
+        permA.as<uint32_t>(), dstg.as<int32_t>() + n0, err.as<unsigned long long>());
+    {
+      DevBuf keyC;
+      keyC.alloc(size_t(mb) * 8);
+      k_iota_off_u32<<<grid_for(mb), 256, 0, c.stream>>>(permB.as<uint32_t>(), mb, n0);
+      k_seq_desc_keys<<<grid_for(mb), 256, 0, c.stream>>>(s.seq.as<int64_t>() + n0, mb, keyC.as<uint64_t>());
+      radix_pairs<uint64_t, uint32_t>(c, keyC.as<uint64_t>(), keyB.as<uint64_t>(), permB.as<uint32_t>(),
+                                      permA.as<uint32_t>(), mb, 64);
+    }
+    uint32_t* batch = lsd(permA.as<uint32_t>(), permB.as<uint32_t>(), mb);
+    permM.alloc(size_t(n) * 4);
+    const GroupLess less{keyA.as<uint64_t>(), s.rank_const ? nullptr : s.rank.as<int64_t>(),
+                         s.ver_const ? nullptr : s.ver.as<int64_t>()};
+    size_t tb = 0;
+    NBG_HIP(rocprim::merge(nullptr, tb, batch, ord->perm.as<uint32_t>(), permM.as<uint32_t>(), size_t(mb), size_t(n0),
+                           less, c.stream));
+    c.ws_tmp.ensure(tb);
+    NBG_HIP(rocprim::merge(c.ws_tmp.p, tb, batch, ord->perm.as<uint32_t>(), permM.as<uint32_t>(), size_t(mb),
+                           size_t(n0), less, c.stream));
+    perm = permM.as<uint32_t>();
+    perm_owner = &permM;
+    ord->perm.release();
+    ord->skey.release();
+    ord->dstg.release();
+  } else {
+    keyA.alloc(size_t(n) * 8);
+    keyB.alloc(size_t(n) * 8);
+    permA.alloc(size_t(n) * 4);
+    permB.alloc(size_t(n) * 4);
+    dstg.alloc(size_t(n) * 4);
+    k_edge_keys<<<grid_for(n), 256, 0, c.stream>>>(s.src.as<int64_t>(), s.dst.as<int64_t>(), n, c.ht_keys.as<int64_t>(),
+                                                 c.ht_vals.as<int32_t>(), uint64_t(c.ht_cap - 1), c.ht_has_min,
+                                                 c.ht_min_gidx, lo, hi, byterank, keyA.as<uint64_t>(),
+                                                 permA.as<uint32_t>(), dstg.as<int32_t>(), err.as<unsigned long long>());
+  }
   NBG_HIP(hipGetLastError());
   uint64_t herr = 0;
   NBG_HIP(hipMemcpyAsync(&herr, err.p, 8, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
   if (herr) throw Error(NBG_E_PART_NOT_FOUND, "edge source not owned by this rank / unknown vertex");
-  int srcbits = 1;
-  while ((int64_t(1) << srcbits) < std::max<int64_t>(out.n_rows, 2)) srcbits++;
-  uint32_t* perm = nullptr;
-  DevBuf& skey_keep = keyA;  // (src_local << 32 | byterank(dst)) by tuple index
-  if (s.rank_const && s.ver_const) {
+  if (do_merge) {
+  } else if (s.rank_const && s.ver_const) {
     // single pass on (src_local, byterank(dst)) == the reference key order
     radix_pairs<uint64_t, uint32_t>(c, skey_keep.as<uint64_t>(), keyB.as<uint64_t>(), permA.as<uint32_t>(),
                                    permB.as<uint32_t>(), n, 32 + srcbits);
     perm = permB.as<uint32_t>();
+    perm_owner = &permB;
   } else {
-    // LSD passes: version bytes, dst bytes, rank bytes, then src (most significant)
-    DevBuf keyC;
-    keyC.alloc(size_t(n) * 8);
     uint32_t* pin = permA.as<uint32_t>();
-    uint32_t* pout = permB.as<uint32_t>();
     // start from reverse load order: stable passes then put the LAST write of identical keys
     // first, so keep-first implements WriteBatch last-write-wins (RocksEngine.cpp:216-230).
     // The decode stage appends tuples in wave order, not load order, so the start permutation
     // is the staged load sequence numbers sorted descending.
     if (s.seq.bytes >= size_t(n) * 8) {
+      DevBuf keyC;
+      keyC.alloc(size_t(n) * 8);
       k_iota_u32<<<grid_for(n), 256, 0, c.stream>>>(permB.as<uint32_t>(), n);
       k_seq_desc_keys<<<grid_for(n), 256, 0, c.stream>>>(s.seq.as<int64_t>(), n, keyC.as<uint64_t>());
       radix_pairs<uint64_t, uint32_t>(c, keyC.as<uint64_t>(), keyB.as<uint64_t>(), permB.as<uint32_t>(), pin, n, 64);
     } else {
       k_iota_rev_u32<<<grid_for(n), 256, 0, c.stream>>>(pin, n);
     }
-    auto pass_bswap = [&](const DevBuf& vals) {
-      k_gather_key_bswap<<<grid_for(n), 256, 0, c.stream>>>(vals.as<int64_t>(), pin, keyC.as<uint64_t>(), n);
-      radix_pairs<uint64_t, uint32_t>(c, keyC.as<uint64_t>(), keyB.as<uint64_t>(), pin, pout, n, 64);
-      std::swap(pin, pout);
-    };
-    if (!s.ver_const) pass_bswap(s.ver);
-    pass_bswap(s.dst);
-    if (!s.rank_const) pass_bswap(s.rank);
-    k_gather_key_src<<<grid_for(n), 256, 0, c.stream>>>(skey_keep.as<uint64_t>(), pin, keyC.as<uint64_t>(), n);
-    radix_pairs<uint64_t, uint32_t>(c, keyC.as<uint64_t>(), keyB.as<uint64_t>(), pin, pout, n, srcbits);
-    perm = pout;
+    perm = lsd(pin, permB.as<uint32_t>(), n);
+    perm_owner = perm == permA.as<uint32_t>() ? &permA : &permB;
   }
   // dedup (keep the first = bytewise-smallest version)
   DevBuf keep;
@@ -1152,8 +1265,8 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
     }
   }
   keyB.release();
-  permA.release();
-  permB.release();
+  if (perm_owner != &permA) permA.release();
+  if (perm_owner != &permB) permB.release();
   keep.release();
   out.nnz = int64_t(m);
   const uint32_t* kp = kept.as<uint32_t>();
@@ -1212,6 +1325,19 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
   if (out.ov_n) gather_props(c, s, fields, ovp.as<uint32_t>(), out.ov_n, false, out.ov_props);
   NBG_HIP(hipStreamSynchronize(c.stream));
   NBG_HIP(hipGetLastError());
+  // the sorted order for a later merge commit (writable snapshots only)
+  if (ord) {
+    ord->perm.release();
+    ord->skey.release();
+    ord->dstg.release();
+    ord->n = 0;
+    if (!consume && perm_owner) {
+      ord->perm = std::move(*perm_owner);
+      ord->skey = std::move(keyA);
+      ord->dstg = std::move(dstg);
+      ord->n = n;
+    }
+  }
   // free staging
   if (consume) {  // a writable snapshot keeps its decoded tuples (the write log) for the next commit
     s.src.release();
@@ -1887,6 +2013,79 @@ static void build_tag_columns(Ctx& c) {
   }
 }
 
+__global__ void k_count_unknown(const int64_t* src, const int64_t* dst, int64_t n, const int64_t* keys_ht,
+                                const int32_t* vals_ht, uint64_t mask, bool has_min, int32_t min_gidx,
+                                unsigned long long* cnt) {
+  unsigned long long u = 0;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    u += (ht_lookup(keys_ht, vals_ht, mask, src[i], has_min, min_gidx) < 0) +
+         (ht_lookup(keys_ht, vals_ht, mask, dst[i], has_min, min_gidx) < 0);
+  for (int o = 32; o > 0; o >>= 1) u += __shfl_xor(u, o);
+  if ((threadIdx.x & 63) == 0 && u) atomicAdd(cnt, u);
+}
+
+static bool commit_merge(Ctx& c) {
+  if (c.world != 1 || c.opt("merge_commit", 1) == 0 || !c.brank.p) return false;
+  for (auto& kv : c.tags)
+    if (kv.second.stage.n != kv.second.committed_n) return false;  // tag writes: full rebuild
+  DevBuf cnt;
+  cnt.alloc(8);
+  NBG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
+  for (auto& kv : c.edges) {
+    EdgeSpace& es = kv.second;
+    if (es.rmat_stream) return false;
+    for (int d = 0; d < 2; d++) {
+      const Staging& st = d ? es.in_stage : es.out_stage;
+      const int64_t n0 = es.ord[d].n;
+      if (st.n == n0) continue;
+      if (n0 <= 0 || !es.ord[d].perm.p || st.n < n0 || st.seq.bytes < size_t(st.n) * 8) return false;
+      k_count_unknown<<<grid_for(st.n - n0), 256, 0, c.stream>>>(
+          st.src.as<int64_t>() + n0, st.dst.as<int64_t>() + n0, st.n - n0, c.ht_keys.as<int64_t>(),
+          c.ht_vals.as<int32_t>(), uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, cnt.as<unsigned long long>());
+    }
+  }
+  unsigned long long unknown = 0;
+  NBG_HIP(hipMemcpyAsync(&unknown, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  if (unknown) return false;  // new vertices: the vertex numbering changes
+  PoolScope build_scope(build_pool(c));
+  c.finalized = false;  // a merge that throws leaves the next commit a full rebuild
+  const double t0 = now_s();
+  const bool trace = c.opt("build_trace", 0) != 0;
+  double tmark = t0;
+  auto phase = [&](const char* name) {
+    if (!trace) return;
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    const double t = now_s();
+    const int64_t an = g_alloc_clock.alloc_ns.exchange(0), fn = g_alloc_clock.free_ns.exchange(0);
+    const int64_t na = g_alloc_clock.allocs.exchange(0);
+    fprintf(stderr, "[nbg merge] %-22s %8.3f s  (hipMalloc %lld x %.3f s, hipFree %.3f s)\n", name, t - tmark,
+            (long long)na, an * 1e-9, fn * 1e-9);
+    tmark = t;
+  };
+  phase("checks");
+  for (auto& kv : c.edges) {
+    EdgeSpace& es = kv.second;
+    const bool out_changed = es.out_stage.n != es.ord[0].n, in_changed = es.in_stage.n != es.ord[1].n;
+    if (out_changed) {
+      reset_edge_derived(es);  // out CSR and everything derived from it (transpose, slabs)
+      Csr keep_in = std::move(es.in);
+      build_csr(c, es.out_stage, es.fields, true, es.out, c.brank.as<uint32_t>(), false, &es.ord[0], true);
+      es.in = std::move(keep_in);
+      phase("out CSR (merge)");
+    }
+    if (in_changed) build_csr(c, es.in_stage, es.fields, false, es.in, c.brank.as<uint32_t>(), false, &es.ord[1], true);
+    phase("in CSR (merge)");
+    if (out_changed && c.opt("bottom_up", 1)) build_transpose(c, es);
+    phase("transpose + slabs");
+  }
+  c.ws_tmp.release();
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  c.finalized = true;
+  c.build_seconds += now_s() - t0;
+  return true;
+}
+
 // ------------------------------------------------------------------------------------------
 // Streamed RMAT build (one rank).  The tuple stage holds 40+ bytes per sample in each CSR
 // direction and indexes tuples with 32-bit permutations, so RMAT-28 (2^32 samples) cannot pass
@@ -2230,6 +2429,13 @@ static void finalize_rmat_stream(Ctx& c, EdgeSpace& es) {
 
 void snapshot_finalize(Ctx& c) {
   if (c.finalized) throw Error(NBG_E_STATE, "snapshot already finalized");
+  PoolScope build_scope(build_pool(c));
+  struct TrimAfter {  // a read-only snapshot has no further builds: give the cache back
+    Ctx& c;
+    ~TrimAfter() {
+      if (!c.opt("writable", 0)) c.build_pool->trim();
+    }
+  } trim_after{c};
   double t0 = now_s();
   const bool keep = c.opt("writable", 0) != 0;
   // option build_trace: per-phase wall time on stderr (the stream drained at each mark)
@@ -2437,9 +2643,9 @@ void snapshot_finalize(Ctx& c) {
   // 6. CSRs
   for (auto& kv : c.edges) {
     EdgeSpace& es = kv.second;
-    build_csr(c, es.out_stage, es.fields, true, es.out, brank.as<uint32_t>(), !keep);
+    build_csr(c, es.out_stage, es.fields, true, es.out, brank.as<uint32_t>(), !keep, &es.ord[0]);
     phase("out CSR");
-    build_csr(c, es.in_stage, es.fields, false, es.in, brank.as<uint32_t>(), !keep);
+    build_csr(c, es.in_stage, es.fields, false, es.in, brank.as<uint32_t>(), !keep, &es.ord[1]);
     phase("in CSR");
     if (c.opt("bottom_up", 1)) build_transpose(c, es);
     phase("transpose + slabs");
@@ -2447,6 +2653,9 @@ void snapshot_finalize(Ctx& c) {
   if (!keep) {
     c.heap.release();
     c.heap_used = 0;
+  } else {
+    c.brank = std::move(brank);  // the batch keys of a merge commit
+    for (auto& kv : c.tags) kv.second.committed_n = kv.second.stage.n;
   }
   c.has_log = keep;
   c.ws_tmp.release();

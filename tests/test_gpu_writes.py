@@ -321,3 +321,69 @@ def test_write_batch_all_or_nothing():
         check_go(sp, st, vids[::17] + [v0])
     finally:
         sp.close()
+
+
+def edge_batch(rng, vids, ver, n=800):
+    """edge writes between existing vertices only: new edges, newer versions of existing ones
+    (bytewise order decides which version a scan reads first), identical-key rewrites"""
+    part = lambda v: O.part_of(v, PARTS)  # noqa: E731
+    batch = {p: [] for p in range(1, PARTS + 1)}
+    for _ in range(n):
+        s, t = rng.choice(vids), rng.choice(vids)
+        kind = rng.random()
+        v = BASE_VER if kind < 0.25 else (ver if kind < 0.8 else ver - 3)
+        w = rng.randrange(1000, 2000)
+        batch[part(s)].append((O.edge_key(part(s), s, ET, 0, t, v), O.encode_row([w])))
+        batch[part(t)].append((O.edge_key(part(t), t, -ET, 0, s, v), b""))
+    return batch
+
+
+@pytest.mark.parametrize("merge", [1, 0])
+def test_merge_commit_matches_full_rebuild_and_oracle(merge):
+    """a commit whose batch adds no vertex and no tag row merges the sorted batch into the
+    committed key order (merge_commits counts it); results equal the full rebuild's and the
+    oracle's, including getBound's firstLoop rows over older versions"""
+    rng = random.Random(29)
+    base, vids = random_space_kv(33)
+    sp = GraphSpace(PARTS)
+    try:
+        sp.set_option("writable", 1)
+        sp.set_option("merge_commit", merge)
+        sp.set_edge_schema(ET, [("weight", O.INT)])
+        sp.set_tag_schema(PERSON, "person", FIELDS)
+        for p, kv in base.items():
+            if kv:
+                sp.load_part(p, kv)
+        sp.finalize()
+        history = [base]
+        starts = vids[::17]
+        for rnd in range(3):
+            batch = edge_batch(rng, vids, BASE_VER - 7 * (rnd + 1))
+            for p, kv in batch.items():
+                if kv:
+                    sp.write_part(p, kv)
+            sp.commit()
+            history.append(batch)
+            st = fresh_oracle(history)
+            check_go(sp, st, starts)
+            check_bound(sp, st, vids)
+            # firstLoop: a filter that rejects the first version reads an older one
+            q = vids[::5]
+            parts = [O.part_of(v, PARTS) for v in q]
+            cols = [("_dst", O.EDGE, 0), ("weight", O.EDGE, 0)]
+            f = X.AliasProp("e", "weight") < 1500
+            g = sp.get_bound(ET, parts, q, cols, filter=f)
+            r = st.get_bound(ET, parts, q, cols, filt=f.encode())
+            assert ms(g.rows()) == ms(r.rows())
+        info = sp.info(ET)
+        assert info["commits"] == 3
+        assert info["merge_commits"] == (3 if merge else 0)
+        # a batch with a new vertex takes the full rebuild
+        v_new = 4242424242
+        p = O.part_of(vids[0], PARTS)
+        sp.write_part(p, [(O.edge_key(p, vids[0], ET, 0, v_new, BASE_VER - 50), O.encode_row([5]))])
+        sp.commit()
+        assert sp.info(ET)["merge_commits"] == (3 if merge else 0)
+        assert v_new in set(int(x) for x in sp.go([vids[0]], 1, ET).columns[0])
+    finally:
+        sp.close()
