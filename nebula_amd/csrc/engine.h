@@ -139,9 +139,18 @@ struct DevBuf {
     bytes = 0;
     pool.reset();
   }
+  // pooled blocks of 64 MiB and up are rounded up to 1/16 steps of their power of two, so a
+  // buffer that grows by a write batch still fits the block its predecessor left in the cache
+  static size_t pool_round(size_t b) {
+    if (b < (size_t(64) << 20)) return b;
+    size_t p2 = size_t(1) << (63 - __builtin_clzll(b));
+    const size_t step = p2 / 16;
+    return (b + step - 1) / step * step;
+  }
   void alloc(size_t b) {
     release();
     if (b == 0) return;
+    if (tl_pool) b = pool_round(b);
     if (tl_pool) {
       size_t got = 0;
       if (void* q = tl_pool->get(b, got)) {

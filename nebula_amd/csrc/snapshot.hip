@@ -970,16 +970,22 @@ static void minmax_i64(Ctx& c, const int64_t* d, int64_t n, int64_t& mn, int64_t
 // puts the visible write first).  escan[i] = keep[i] (inclusive-scanned by the caller -> the
 // group's edge index + 1).
 __global__ void k_old_version_flags(const uint32_t* perm, const uint8_t* keep, const int64_t* ver, int64_t n,
-                                    uint8_t* ov, int64_t* escan) {
+                                    uint8_t* ov, uint32_t* escan, unsigned long long* count) {
+  unsigned long long c = 0;
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
     escan[i] = keep[i];
-    ov[i] = !keep[i] && i > 0 && ver[perm[i]] != ver[perm[i - 1]];
+    const bool o = !keep[i] && i > 0 && ver[perm[i]] != ver[perm[i - 1]];
+    ov[i] = o;
+    c += o;
   }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, c);
 }
-__global__ void k_dec_i64(int64_t* p, int64_t n) {
-  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) p[i] -= 1;
+// the older versions' group edge indices: inclusive keep-scan - 1, widened
+__global__ void k_ov_edges(const uint32_t* e, int64_t n, int64_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    out[i] = int64_t(e[i]) - 1;
 }
-
 // SoA prop columns of the staged tuples kp[0..m) (in that order): INT-like values narrowed to
 // the smallest width holding [min, max] when `narrow`, DOUBLE as bits, STRING as offsets + bytes
 static void gather_props(Ctx& c, Staging& s, const std::vector<Field>& fields, const uint32_t* kp, int64_t m,
@@ -1128,13 +1134,20 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
     // sequence descending first), then merged into the committed order -- the batch first among
     // equal groups (it is newer), which is the full sort's order
     const int64_t mb = n - n0;
-    keyA.alloc(size_t(n) * 8);
-    dstg.alloc(size_t(n) * 4);
+    // the committed keys grow in place when their (pool-rounded) block has room for the batch
+    auto grow = [&](DevBuf& dst, DevBuf& old, size_t w) {
+      if (old.bytes >= size_t(n) * w) {
+        dst = std::move(old);
+      } else {
+        dst.alloc(size_t(n) * w);
+        NBG_HIP(hipMemcpyAsync(dst.p, old.p, size_t(n0) * w, hipMemcpyDeviceToDevice, c.stream));
+      }
+    };
+    grow(keyA, ord->skey, 8);
+    grow(dstg, ord->dstg, 4);
     keyB.alloc(size_t(mb) * 8);
     permA.alloc(size_t(mb) * 4);
     permB.alloc(size_t(mb) * 4);
-    NBG_HIP(hipMemcpyAsync(keyA.p, ord->skey.p, size_t(n0) * 8, hipMemcpyDeviceToDevice, c.stream));
-    NBG_HIP(hipMemcpyAsync(dstg.p, ord->dstg.p, size_t(n0) * 4, hipMemcpyDeviceToDevice, c.stream));
     k_edge_keys<<<grid_for(mb), 256, 0, c.stream>>>(
         s.src.as<int64_t>() + n0, s.dst.as<int64_t>() + n0, mb, c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
         uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, lo, hi, byterank, keyA.as<uint64_t>() + n0,
@@ -1228,40 +1241,39 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
   if (with_props && !s.ver_const && int64_t(m) < n) {
     DevBuf ovf, escan, ove, ocnt;
     ovf.alloc(size_t(n));
-    escan.alloc(size_t(n) * 8);
-    k_old_version_flags<<<grid_for(n), 256, 0, c.stream>>>(perm, keep.as<uint8_t>(), s.ver.as<int64_t>(), n,
-                                                           ovf.as<uint8_t>(), escan.as<int64_t>());
-    size_t tb2 = 0;
-    NBG_HIP(rocprim::inclusive_scan(nullptr, tb2, escan.as<int64_t>(), escan.as<int64_t>(), size_t(n),
-                                    rocprim::plus<int64_t>(), c.stream));
-    c.ws_tmp.ensure(tb2);
-    NBG_HIP(rocprim::inclusive_scan(c.ws_tmp.p, tb2, escan.as<int64_t>(), escan.as<int64_t>(), size_t(n),
-                                    rocprim::plus<int64_t>(), c.stream));
-    ovp.alloc(size_t(n) * 4);
-    ove.alloc(size_t(n) * 8);
+    escan.alloc(size_t(n) * 4);
     ocnt.alloc(8);
-    tb2 = 0;
-    NBG_HIP(rocprim::select(nullptr, tb2, perm, ovf.as<uint8_t>(), ovp.as<uint32_t>(), ocnt.as<uint64_t>(), size_t(n),
-                            c.stream));
-    c.ws_tmp.ensure(tb2);
-    NBG_HIP(rocprim::select(c.ws_tmp.p, tb2, perm, ovf.as<uint8_t>(), ovp.as<uint32_t>(), ocnt.as<uint64_t>(),
-                            size_t(n), c.stream));
-    tb2 = 0;
-    NBG_HIP(rocprim::select(nullptr, tb2, escan.as<int64_t>(), ovf.as<uint8_t>(), ove.as<int64_t>(),
-                            ocnt.as<uint64_t>(), size_t(n), c.stream));
-    c.ws_tmp.ensure(tb2);
-    NBG_HIP(rocprim::select(c.ws_tmp.p, tb2, escan.as<int64_t>(), ovf.as<uint8_t>(), ove.as<int64_t>(),
-                            ocnt.as<uint64_t>(), size_t(n), c.stream));
+    NBG_HIP(hipMemsetAsync(ocnt.p, 0, 8, c.stream));
+    k_old_version_flags<<<grid_for(n), 256, 0, c.stream>>>(perm, keep.as<uint8_t>(), s.ver.as<int64_t>(), n,
+                                                           ovf.as<uint8_t>(), escan.as<uint32_t>(),
+                                                           ocnt.as<unsigned long long>());
     uint64_t no = 0;
     NBG_HIP(hipMemcpyAsync(&no, ocnt.p, 8, hipMemcpyDeviceToHost, c.stream));
     NBG_HIP(hipStreamSynchronize(c.stream));
-    if (no) {
+    if (no) {  // buffers sized by the older-version count (kept edges < 2^32: 32-bit scan)
+      size_t tb2 = 0;
+      NBG_HIP(rocprim::inclusive_scan(nullptr, tb2, escan.as<uint32_t>(), escan.as<uint32_t>(), size_t(n),
+                                      rocprim::plus<uint32_t>(), c.stream));
+      c.ws_tmp.ensure(tb2);
+      NBG_HIP(rocprim::inclusive_scan(c.ws_tmp.p, tb2, escan.as<uint32_t>(), escan.as<uint32_t>(), size_t(n),
+                                      rocprim::plus<uint32_t>(), c.stream));
+      ovp.alloc(size_t(no) * 4 + 4);
+      ove.alloc(size_t(no) * 4 + 4);
+      tb2 = 0;
+      NBG_HIP(rocprim::select(nullptr, tb2, perm, ovf.as<uint8_t>(), ovp.as<uint32_t>(), ocnt.as<uint64_t>(), size_t(n),
+                              c.stream));
+      c.ws_tmp.ensure(tb2);
+      NBG_HIP(rocprim::select(c.ws_tmp.p, tb2, perm, ovf.as<uint8_t>(), ovp.as<uint32_t>(), ocnt.as<uint64_t>(),
+                              size_t(n), c.stream));
+      tb2 = 0;
+      NBG_HIP(rocprim::select(nullptr, tb2, escan.as<uint32_t>(), ovf.as<uint8_t>(), ove.as<uint32_t>(),
+                              ocnt.as<uint64_t>(), size_t(n), c.stream));
+      c.ws_tmp.ensure(tb2);
+      NBG_HIP(rocprim::select(c.ws_tmp.p, tb2, escan.as<uint32_t>(), ovf.as<uint8_t>(), ove.as<uint32_t>(),
+                              ocnt.as<uint64_t>(), size_t(n), c.stream));
       out.ov_n = int64_t(no);
       out.ov_edge.alloc(size_t(no) * 8 + 8);
-      NBG_HIP(hipMemcpyAsync(out.ov_edge.p, ove.p, size_t(no) * 8, hipMemcpyDeviceToDevice, c.stream));
-      k_dec_i64<<<grid_for(int64_t(no)), 256, 0, c.stream>>>(out.ov_edge.as<int64_t>(), int64_t(no));
-    } else {
-      ovp.release();
+      k_ov_edges<<<grid_for(int64_t(no)), 256, 0, c.stream>>>(ove.as<uint32_t>(), int64_t(no), out.ov_edge.as<int64_t>());
     }
   }
   keyB.release();

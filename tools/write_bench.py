@@ -66,6 +66,7 @@ def main():
     ap.add_argument("--scale", type=int, default=24)
     ap.add_argument("--edges", type=int, default=1 << 20)
     ap.add_argument("--trace", action="store_true", help="per-phase build / commit times on stderr")
+    ap.add_argument("--commits", type=int, default=1, help="successive write batch + commit rounds")
     a = ap.parse_args()
     sp = GraphSpace(PARTS)
     sp.set_option("writable", 1)
@@ -80,23 +81,28 @@ def main():
     starts = [int(x) for x in synth.seeds(a.scale, 16, SEED, 1)]
     go_before = go3(sp, starts)
     rng = np.random.default_rng(3)
-    s, _ = synth.pairs(a.scale, 16, SEED, a.edges, pick_seed=5)
-    _, d = synth.pairs(a.scale, 16, SEED, a.edges, pick_seed=6)
-    w = rng.integers(1000, 2000, a.edges)
-    bs = batches(np.asarray(s, np.int64), np.asarray(d, np.int64), w, 2**63 - 3)
-    t1 = time.perf_counter()
-    for p, lst in bs.items():
-        for blob in lst:
-            sp.write_part(p, blob)
-    write_s = time.perf_counter() - t1
-    t2 = time.perf_counter()
-    sp.commit()
-    commit_s = time.perf_counter() - t2
+    commit_times, write_times = [], []
+    for k in range(a.commits):
+        s, _ = synth.pairs(a.scale, 16, SEED, a.edges, pick_seed=5 + 2 * k)
+        _, d = synth.pairs(a.scale, 16, SEED, a.edges, pick_seed=6 + 2 * k)
+        w = rng.integers(1000, 2000, a.edges)
+        bs = batches(np.asarray(s, np.int64), np.asarray(d, np.int64), w, 2**63 - 3 - k)
+        t1 = time.perf_counter()
+        for p, lst in bs.items():
+            for blob in lst:
+                sp.write_part(p, blob)
+        write_times.append(round(time.perf_counter() - t1, 3))
+        t2 = time.perf_counter()
+        sp.commit()
+        commit_times.append(round(time.perf_counter() - t2, 3))
+    write_s, commit_s = write_times[0], commit_times[0]
     info1 = sp.info(FOLLOW)
     go_after = go3(sp, starts)
     print(json.dumps({
-        "workload": f"rmat{a.scale} + AddEdges batch of {a.edges} edges (out + in keys)",
+        "workload": f"rmat{a.scale} + {a.commits} x AddEdges batch of {a.edges} edges (out + in keys)",
         "initial_build_s": round(build_s, 3), "write_part_s": round(write_s, 3), "commit_s": round(commit_s, 3),
+        "commit_s_each": commit_times, "write_part_s_each": write_times,
+        "merge_commits": info1.get("merge_commits"),
         "out_edges_before": info0["local_out_edges"], "out_edges_after": info1["local_out_edges"],
         "device_bytes_before": info0["device_bytes"], "device_bytes_after": info1["device_bytes"],
         "go3_ms_before": round(go_before[0], 3), "go3_rows_before": go_before[1],
