@@ -210,6 +210,11 @@ struct RowWriter {
     cleanup(T_DOUBLE);
     return *this;
   }
+  RowWriter& writeFloat(float v) {  // what operator<<(double) writes under a FLOAT column
+    put(cord, v);
+    cleanup(T_FLOAT);
+    return *this;
+  }
   RowWriter& operator<<(bool v) {  // RowWriter.cpp:115-129
     int32_t t = colType(T_BOOL);
     if (t == T_BOOL) cord.push_back(char(v)); else cord.push_back(char(0));
@@ -1388,6 +1393,7 @@ size_t ora_encode_row(const int32_t* tags, const int64_t* iv, const double* dv,
     switch (tags[i]) {
       case T_INT: w << iv[i]; break;
       case T_DOUBLE: w << dv[i]; break;
+      case T_FLOAT: w.writeFloat(float(dv[i])); break;  // a FLOAT schema column: 4 bytes
       case T_BOOL: w << bool(iv[i] != 0); break;
       default: w << std::string(sv[i]); break;
     }

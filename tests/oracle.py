@@ -119,14 +119,17 @@ def vertex_key(part, vid, tag, ver) -> bytes:
 
 
 def encode_row(values) -> bytes:
-    """Schemaless RowWriter encoding of python values (int->INT, float->DOUBLE, bool, str)."""
+    """Schemaless RowWriter encoding of python values (int->INT, float->DOUBLE, numpy.float32->FLOAT,
+    bool, str)."""
     n = len(values)
     tags = (C.c_int32 * max(n, 1))()
     iv = (C.c_int64 * max(n, 1))()
     dv = (C.c_double * max(n, 1))()
     sv = (C.c_char_p * max(n, 1))()
     for i, v in enumerate(values):
-        if isinstance(v, bool):
+        if isinstance(v, np.float32):  # a FLOAT column (4 bytes)
+            tags[i], dv[i] = FLOAT, float(v)
+        elif isinstance(v, bool):
             tags[i], iv[i] = BOOL, int(v)
         elif isinstance(v, int):
             tags[i], iv[i] = INT, v
