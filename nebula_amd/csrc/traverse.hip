@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <unordered_map>
 
 #include "device_common.h"
 #include "engine.h"
@@ -1958,18 +1959,18 @@ __global__ __launch_bounds__(256) void k_bu_bits(const int64_t* __restrict__ trp
 
 // bitmap -> compacted list.  mode 0: local rows (a top-down hop's frontier; the bitmaps this
 // reads already exclude rows without out-edges); mode 1: vids of every set vertex (the DISTINCT
-// _dst output).  A tile of 1024 words (32768 vertices) per block-iteration: the words and their
+// _dst output).  A tile of 4096 words (131072 vertices) per block-iteration: the words and their
 // exclusive offsets go to LDS, one returning atomic reserves the tile's output range, then each
 // wave expands two words per step with one lane per bit, so consecutive set bits write
 // consecutive output slots (coalesced stores, coalesced vid_of reads).
 template <int MODE>
-__global__ __launch_bounds__(256) void k_bits_compact(const uint32_t* __restrict__ bits, int64_t n, int64_t lo,
-                                                      const int64_t* __restrict__ vid_of, void* out,
-                                                      unsigned long long* n_out) {
-  constexpr int kTileWords = 1024;
+__global__ __launch_bounds__(1024) void k_bits_compact(const uint32_t* __restrict__ bits, int64_t n, int64_t lo,
+                                                       const int64_t* __restrict__ vid_of, void* out,
+                                                       unsigned long long* n_out) {
+  constexpr int kTileWords = 4096;  // 1024 threads x 4 words: one counter atomic per 128 K vertices
   __shared__ uint32_t sw[kTileWords];
   __shared__ uint32_t so[kTileWords];
-  __shared__ uint32_t lds[8];
+  __shared__ uint32_t lds[16];
   __shared__ unsigned long long s_base;
   const int64_t nwords = (n + 31) / 32;
   const int64_t ntiles = (nwords + kTileWords - 1) / kTileWords;
@@ -2006,7 +2007,8 @@ __global__ __launch_bounds__(256) void k_bits_compact(const uint32_t* __restrict
       constexpr int U = 4;
       const unsigned long long base = s_base;
       const int half = lane >> 5, bit = lane & 31;
-      for (int j = wv * (kTileWords / 4); j < (wv + 1) * (kTileWords / 4); j += 2 * U) {
+      const int per_wave = kTileWords / int(blockDim.x >> 6);
+      for (int j = wv * per_wave; j < (wv + 1) * per_wave; j += 2 * U) {
         bool has[U];
         unsigned long long p[U];
         int64_t val[U];
@@ -2051,9 +2053,10 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
                                                  const uint8_t* row_ok, int require_deg, int32_t* out,
                                                  unsigned long long* n_out, unsigned long long* partials,
                                                  uint16_t* bits, const uint32_t* __restrict__ odeg) {
-  // tile = 256 threads x 4 chunks of 16 bytes = 16384 vertices; one returning atomic per tile;
+  // tile = 256 threads x 4 chunks of 16 bytes = 16384 vertices; one returning atomic per tile
+  // (1024-thread tiles, a quarter of the atomics, measured slower: 40 -> 47 us at hop 1);
   // n_set (partials[0]) and the kept out-degree sum (partials[1]) go to per-block partials.
-  __shared__ uint32_t lds[8];
+  __shared__ uint32_t lds[16];
   __shared__ unsigned long long lds64[kSlots * 16];
   __shared__ unsigned long long s_base;
   const int64_t nchunks = (n + 15) / 16;
@@ -2604,6 +2607,18 @@ int64_t degree_scan(Ctx& c, const int32_t* F, int64_t nF, const Csr& csr, DevBuf
   return E;
 }
 
+// raise a kernel's dynamic LDS limit once per process (the attribute call costs a host round
+// trip: done per launch it showed up as ~10 us gaps before every bottom-up pass)
+static void lds_limit(const void* kern, size_t shm) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, size_t> done;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = done.find(kern);
+  if (it != done.end() && it->second >= shm) return;
+  NBG_HIP(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)));
+  done[kern] = shm;
+}
+
 void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* row_ptr, const uint8_t* row_ok,
                     int require_deg, int32_t* out, uint16_t* bits, unsigned long long* Kd,
                     const uint32_t* odeg = nullptr) {
@@ -2823,8 +2838,7 @@ int launch_bu_pair(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
   }
   auto big_lds = [&](auto kern) {
     if (shm > 48 * 1024)
-      NBG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  int(shm)));
+      lds_limit(reinterpret_cast<const void*>(kern), shm);
   };
   FastArgs fpd = fp;
   fpd.width |= int32_t(c.opt("bu_pair_diag", 0) & 3) << 16;
@@ -2855,8 +2869,7 @@ int launch_bu_pair(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, c
   const size_t rshm = size_t(std::max(rcw, 1)) * 4;
   auto go_ring = [&](auto kern) {
     if (rshm > 48 * 1024)
-      NBG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  int(rshm)));
+      lds_limit(reinterpret_cast<const void*>(kern), rshm);
     g1 = rgrid;
     kern<<<rgrid, 1024, rshm, c.stream>>>(lo, hi, tr.n_rows, fb, nb, odeg, q, partials, rcw, pbits,
                                           int(c.opt("bu_pair_diag", 0) & 3));
@@ -2973,8 +2986,7 @@ bool launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
   const uint32_t* od = fast ? nullptr : odeg;
   auto go = [&](auto kern) {
     if (shm > 48 * 1024)
-      NBG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  int(shm)));
+      lds_limit(reinterpret_cast<const void*>(kern), shm);
     kern<<<grid, bs, shm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, od, q, partials, cw);
   };
   const int sel = (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
@@ -3005,8 +3017,7 @@ bool launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
   const int rsteps = int(std::max<int64_t>(1, c.opt("bu_rest_steps", 4)));
   auto rest = [&](auto kern) {
     if (rshm > 48 * 1024)
-      NBG_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  int(rshm)));
+      lds_limit(reinterpret_cast<const void*>(kern), rshm);
     kern<<<grid2, 1024, rshm, c.stream>>>(pbits, tr.n_rows, trp, tc, fb, nb, odeg, fp, q, partials + grid, rcw, ru,
                                           rest_from, rsteps);
   };
@@ -3051,7 +3062,7 @@ void bu_finish(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const
   deg.alloc(size_t(P + 1) * 8);
   off.alloc(size_t(P + 1) * 8);
   NBG_HIP(hipMemsetAsync(Kd, 0, 8, c.stream));
-  k_bits_compact<0><<<grid_cap((tr.n_rows + 31) / 32, 1024, 4096), 256, 0, c.stream>>>(
+  k_bits_compact<0><<<grid_cap((tr.n_rows + 31) / 32, 4096, 4096), 1024, 0, c.stream>>>(
       reinterpret_cast<const uint32_t*>(pbits), tr.n_rows, 0, nullptr, lst.as<int32_t>(), Kd);
   k_rest_deg<<<grid_cap(P + 1), 256, 0, c.stream>>>(lst.as<int32_t>(), P, tr.row_ptr.as<int64_t>(), es.slab_k,
                                                     deg.as<int64_t>());
@@ -3381,7 +3392,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     cur ^= 1;
     F = c.ws_front[cur].as<int32_t>();
     NBG_HIP(hipMemsetAsync(K.d, 0, 8, c.stream));
-    k_bits_compact<0><<<grid_cap((n_own + 31) / 32, 1024, 4096), 256, 0, c.stream>>>(bitsA, n_own, lo, nullptr, F,
+    k_bits_compact<0><<<grid_cap((n_own + 31) / 32, 4096, 4096), 1024, 0, c.stream>>>(bitsA, n_own, lo, nullptr, F,
                                                                                      K.d);
     NBG_HIP(hipMemcpyAsync(K.h, K.d, 8, hipMemcpyDeviceToHost, c.stream));
     NBG_HIP(hipStreamSynchronize(c.stream));
@@ -3561,7 +3572,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
           memcpy(h2, K.h + 8, sizeof(h2));
           bu_finish(c, es, fb, bitsB, nullptr, pk, tfp, pb.as<unsigned long long>(), h2, K.d + 40);
         }
-        k_bits_compact<1><<<grid_cap((tr.n_rows + 31) / 32, 1024, 4096), 256, 0, c.stream>>>(
+        k_bits_compact<1><<<grid_cap((tr.n_rows + 31) / 32, 4096, 4096), 1024, 0, c.stream>>>(
             bitsB, tr.n_rows, lo, c.vid_of.as<int64_t>(), vids.p, K.d);
         NBG_HIP(hipGetLastError());
         hipEventRecord(c.ev[3], c.stream);
