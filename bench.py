@@ -255,19 +255,22 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
         dist.barrier()
     t0 = time.perf_counter()
     edges = 0
+    for _ in range(args.steps):  # the timed region: K batches of pairs, nothing else
+        r = sp.shortest_path(s, t, 1, args.max_steps)
+        edges += r.edges_scanned
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    # per-launch statistics from as many untimed calls again
     exp_ms = exp_bytes = dev_ms = 0.0
     iters = 0
     for _ in range(args.steps):
-        r = sp.shortest_path(s, t, 1, args.max_steps)
+        sp.shortest_path(s, t, 1, args.max_steps)
         tm = sp.last_timing()
-        edges += r.edges_scanned
         exp_ms += tm["expand_ms"]
         exp_bytes += tm["expand_bytes"]
         dev_ms += tm["total_ms"]
         iters = tm["steps_run"]
-    if dist is not None:
-        dist.barrier()
-    dt = time.perf_counter() - t0
     names = {2: "expand", 3: "probe", 4: "sweep"}
     launches = [{"kind": names.get(h["mode_id"], h["mode"]), "ms": round(h["ms"], 4), "x": h["c"][0], "entries": h["c"][1],
                  "claims": h["c"][2], "iter": h["c"][4]} for h in tm["hops"]]
@@ -414,9 +417,10 @@ def main():
         order = np.argsort(-deg, kind="stable")[:args.hubs]
         hubs = [(int(cand[i]), int(deg[i])) for i in order]
         starts = np.concatenate([np.array([h for h, _ in hubs], dtype=np.int64), starts[args.hubs:]])
-    # --plain: no WHERE, default YIELD follow._dst rows without DISTINCT (configs[1] / configs[4])
-    where = None if args.plain else X.AliasProp("follow", "weight") > args.where
-    yields = [X.EdgeDst("follow")]
+    # --plain: no WHERE, default YIELD follow._dst rows without DISTINCT (configs[1] / configs[4]).
+    # Encoded once, as graphd hands the storage / engine the encoded Expression bytes.
+    where = None if args.plain else X.encode(X.AliasProp("follow", "weight") > args.where)
+    yields = [X.encode(X.EdgeDst("follow"))]
 
     def one(keep=True):
         return sp.go(starts, args.hops, FOLLOW, where=where, yields=yields, distinct=not args.plain,
@@ -433,6 +437,14 @@ def main():
     t0 = time.perf_counter()
     edges = 0
     rows = 0
+    for _ in range(args.steps):  # the timed region: K queries, nothing else
+        r = one()
+        edges += r.edges_scanned
+        rows = r.n_rows
+    barrier()
+    dt = time.perf_counter() - t0
+    # per-kernel statistics (HIP events the engine recorded) from as many untimed queries again,
+    # so reading them back does not sit inside the timed region
     exp_ms = 0.0
     exp_bytes = 0
     tot_ms = comm_ms = 0.0
@@ -440,10 +452,8 @@ def main():
     bu_steps = 0
     hop_ms, hop_bytes, k_ms, k_bytes = {}, {}, {}, {}
     for _ in range(args.steps):
-        r = one()
+        one()
         t = sp.last_timing()
-        edges += r.edges_scanned
-        rows = r.n_rows
         exp_ms += t["expand_ms"]
         exp_bytes += t["expand_bytes"]
         tot_ms += t["total_ms"]
@@ -456,8 +466,6 @@ def main():
             hop_bytes[i] = hop_bytes.get(i, 0) + h["bytes"]
             k_ms[i] = k_ms.get(i, 0.0) + h["kernel_ms"]
             k_bytes[i] = k_bytes.get(i, 0) + h["kernel_bytes"]
-    barrier()
-    dt = time.perf_counter() - t0
     if dist is not None:
         import torch
         tt = torch.tensor([dt], dtype=torch.float64)
