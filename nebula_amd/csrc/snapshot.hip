@@ -2080,10 +2080,10 @@ static bool commit_merge(Ctx& c) {
     EdgeSpace& es = kv.second;
     const bool out_changed = es.out_stage.n != es.ord[0].n, in_changed = es.in_stage.n != es.ord[1].n;
     if (out_changed) {
-      reset_edge_derived(es);  // out CSR and everything derived from it (transpose, slabs)
-      Csr keep_in = std::move(es.in);
-      build_csr(c, es.out_stage, es.fields, true, es.out, c.brank.as<uint32_t>(), false, &es.ord[0], true);
+      Csr keep_in = std::move(es.in);  // an unchanged in CSR survives the reset
+      reset_edge_derived(es);          // out CSR and everything derived from it (transpose, slabs)
       es.in = std::move(keep_in);
+      build_csr(c, es.out_stage, es.fields, true, es.out, c.brank.as<uint32_t>(), false, &es.ord[0], true);
       phase("out CSR (merge)");
     }
     if (in_changed) build_csr(c, es.in_stage, es.fields, false, es.in, c.brank.as<uint32_t>(), false, &es.ord[1], true);
