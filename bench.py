@@ -265,7 +265,7 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
     exp_ms = exp_bytes = dev_ms = 0.0
     iters = 0
     for _ in range(args.steps):
-        sp.shortest_path(s, t, 1, args.max_steps)
+        r = sp.shortest_path(s, t, 1, args.max_steps)
         tm = sp.last_timing()
         exp_ms += tm["expand_ms"]
         exp_bytes += tm["expand_bytes"]
@@ -274,7 +274,7 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
     names = {2: "expand", 3: "probe", 4: "sweep"}
     launches = [{"kind": names.get(h["mode_id"], h["mode"]), "ms": round(h["ms"], 4), "x": h["c"][0], "entries": h["c"][1],
                  "claims": h["c"][2], "iter": h["c"][4]} for h in tm["hops"]]
-    # parity: the last timed result (host copy) against the committed digest
+    # parity: the last result (host copy) against the committed digest
     hops, paths, srcs = r.hops, r.paths, r.src
     if dist is not None:
         import torch
@@ -448,15 +448,17 @@ def main():
     exp_ms = 0.0
     exp_bytes = 0
     tot_ms = comm_ms = 0.0
+    tot_each = []
     comm_bytes = 0
     bu_steps = 0
     hop_ms, hop_bytes, k_ms, k_bytes = {}, {}, {}, {}
     for _ in range(args.steps):
-        one()
+        r = one()  # held like the timed loop's, so its buffers cycle the same way
         t = sp.last_timing()
         exp_ms += t["expand_ms"]
         exp_bytes += t["expand_bytes"]
         tot_ms += t["total_ms"]
+        tot_each.append(round(t["total_ms"], 3))
         comm_ms += t["comm_ms"]
         comm_bytes += t["comm_bytes"]
         bu_steps = t["bu_steps"]
@@ -510,9 +512,11 @@ def main():
             "algorithmic_bytes_per_query": exp_bytes // K,
             "expand_ms_per_query": exp_ms / K,
             "device_ms_per_query": tot_ms / K,
+            "device_ms_each": tot_each,
             "bottom_up_hops": bu_steps,
             "hops": hop_stats,
         }
+    r = None  # release the last result before the parity query
     parity = {"status": "skipped"}
     if not args.no_parity:
         key = (f"go{args.hops}_plain_s{args.scale}" if args.plain else

@@ -438,6 +438,9 @@ struct Ctx {
   std::vector<hipEvent_t> tev;
   size_t tev_used = 0;
   std::vector<PendingTime> tpend;
+  // query temporaries and results (results return their blocks when released).  Capped by
+  // option query_pool_gb: a plain-rows result of RMAT-28 GO 2 STEPS is 21 GB, and re-allocating
+  // it per query stalled one hipMalloc in ~9 for 5.7 s (r03 HIP API trace)
   std::shared_ptr<BufPool> pool = std::make_shared<BufPool>();
   // snapshot build / commit temporaries: freed blocks stay with the process (a fresh multi-GB
   // hipMalloc costs up to seconds: r03a trace), so the phases of a build and later commits of a
@@ -467,6 +470,12 @@ struct Ctx {
     return it == options.end() ? d : it->second;
   }
 };
+
+// the context's query block cache, its cap read from option query_pool_gb (default 64 GiB)
+inline std::shared_ptr<BufPool>& query_pool(Ctx& c) {
+  c.pool->limit = size_t(std::max<int64_t>(0, c.opt("query_pool_gb", 64))) << 30;
+  return c.pool;
+}
 
 // ---- helpers implemented in the .hip files -------------------------------------------------
 // snapshot.hip

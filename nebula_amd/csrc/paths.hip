@@ -961,7 +961,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     W.plist.alloc(size_t(B) * 4 + 64);
     W.cap_state = B;
   }
-  PoolScope pool_scope(c.pool);
+  PoolScope pool_scope(query_pool(c));
   c.timing = Timing{};
   hipEventRecord(c.ev[0], c.stream);
 

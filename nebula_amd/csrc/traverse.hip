@@ -495,6 +495,24 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
         rsk = a.row_ptr[srck] - a.off[lo];
       }
     };
+    if constexpr (MODE == EXP_ROWS && PK == PK_NONE) {
+      if (a.out_vid && a.col_vid && !big) {
+        // plain dst-vid copy: all kItems loads of this thread in flight before the stores
+        int64_t v[kItems];
+#pragma unroll
+        for (int r = 0; r < kItems; r++) {
+          const int j = threadIdx.x + r * kThreads;
+          v[r] = e0 + j < e1 ? __builtin_nontemporal_load(a.col_vid + s_rs[s_own[j]] + e0 + j) : 0;
+        }
+#pragma unroll
+        for (int r = 0; r < kItems; r++) {
+          const int64_t e = e0 + threadIdx.x + r * kThreads;
+          if (e < e1) __builtin_nontemporal_store(v[r], a.out_vid + e);
+        }
+        __syncthreads();
+        continue;
+      }
+    }
     uint32_t pm = 0;  // ROWS: items of this thread that pass
 #pragma unroll 2
     for (int r = 0; r < kItems; r++) {
@@ -3152,7 +3170,7 @@ uint64_t expand_bytes(int64_t nF, int64_t E, int pred_width, int mode) {
 // GO N STEPS
 // ------------------------------------------------------------------------------------------
 int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
-  PoolScope pool_scope(c.pool);
+  PoolScope pool_scope(query_pool(c));
   if (!c.finalized) throw Error(NBG_E_STATE, "snapshot not finalized");
   if (s.steps < 1) throw Error(NBG_E_INVALID_ARG, "steps must be >= 1");
   if (s.edge_type <= 0) throw Error(NBG_E_INVALID_ARG, "GO ... REVERSELY is not supported (GoExecutor.cpp:203-205)");
@@ -4158,7 +4176,7 @@ void fetch_vertex_tags(Ctx& c, HostRows* h, const std::vector<int32_t>& vparts, 
 
 int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* vids, size_t n, const uint8_t* filter,
                       size_t flen, const nbg_prop_def* cols, size_t ncols, nbg_rows* out, const int32_t* stats) {
-  PoolScope pool_scope(c.pool);
+  PoolScope pool_scope(query_pool(c));
   if (!c.finalized) throw Error(NBG_E_STATE, "snapshot not finalized");
   auto* h = new HostRows();
   auto finish = [&](int64_t nrows) {
