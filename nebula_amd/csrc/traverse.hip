@@ -2073,22 +2073,32 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
                                                  uint16_t* bits, const uint32_t* __restrict__ odeg) {
   // tile = 256 threads x 4 chunks of 16 bytes = 16384 vertices; one returning atomic per tile
   // (1024-thread tiles, a quarter of the atomics, measured slower: 40 -> 47 us at hop 1);
-  // n_set (partials[0]) and the kept out-degree sum (partials[1]) go to per-block partials.
+  // n_set (partials[0]), the kept out-degree sum (partials[1]) and the kept count (partials[2])
+  // go to per-block partials.  out == nullptr: bitmap and counts only, no list (the list is built
+  // from the bitmap later if a top-down hop needs it: the per-tile list atomics were most of
+  // this kernel's time - 4096 tiles on one counter at RMAT-26)
   __shared__ uint32_t lds[16];
   __shared__ unsigned long long lds64[kSlots * 16];
   __shared__ unsigned long long s_base;
   const int64_t nchunks = (n + 15) / 16;
   const int64_t tile = int64_t(blockDim.x) * 4;
   const int64_t ntiles = (nchunks + tile - 1) / tile;
-  unsigned long long acc[2] = {0, 0};
+  unsigned long long acc[3] = {0, 0, 0};
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     uint32_t keep[4];
     uint32_t cnt = 0;
+    // the tile's four chunk loads issued together (the clearing stores below would otherwise
+    // order each load behind the previous chunk's store)
+    uint4 wq[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int64_t ch = t * tile + q * int64_t(blockDim.x) + threadIdx.x;
-      uint4 w = make_uint4(0, 0, 0, 0);
-      if (ch < nchunks) w = reinterpret_cast<const uint4*>(map + lo)[ch];
+      wq[q] = ch < nchunks ? reinterpret_cast<const uint4*>(map + lo)[ch] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int64_t ch = t * tile + q * int64_t(blockDim.x) + threadIdx.x;
+      const uint4 w = wq[q];
       const uint32_t words[4] = {w.x, w.y, w.z, w.w};
       uint32_t setmask = 0;
 #pragma unroll
@@ -2133,6 +2143,8 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
       keep[q] = keepmask;
       cnt += __popc(keepmask);
     }
+    acc[2] += cnt;
+    if (!out) continue;  // uniform: no block barrier is skipped by part of the block
     uint32_t total;
     const uint32_t pre = block_excl_scan_u32(cnt, total, lds);
     if (threadIdx.x == 0) s_base = total ? atomicAdd(n_out, (unsigned long long)total) : 0ull;
@@ -2145,7 +2157,7 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
     }
     __syncthreads();
   }
-  block_store_partials(acc, 2, lds64, partials);
+  block_store_partials(acc, 3, lds64, partials);
 }
 
 // starts (gidx) -> deduplicated frontier: bitmap bits (set once, by a returning atomicOr) and
@@ -2640,7 +2652,8 @@ static void lds_limit(const void* kern, size_t shm) {
 void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* row_ptr, const uint8_t* row_ok,
                     int require_deg, int32_t* out, uint16_t* bits, unsigned long long* Kd,
                     const uint32_t* odeg = nullptr) {
-  // counters: Kd[0] list length (atomic), Kd[12] vertices set, Kd[13] kept out-degree sum
+  // counters: Kd[0] list length (atomic), Kd[12] vertices set, Kd[13] kept out-degree sum,
+  // Kd[14] kept vertices (= the list length, also when out == nullptr writes no list)
   unsigned long long* partials = c.ws_partials.as<unsigned long long>();
   int64_t ntiles = ((n + 15) / 16 + 1023) / 1024;
   int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, kAggBlocks)));
@@ -3405,6 +3418,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   uint32_t* bitsB = c.ws_bits_recv.as<uint32_t>();
   bool have_list = true, off_ready = false;
   int64_t E = -1;
+  int64_t list_n = -1;  // length of the list the bitmap will compact to, when already counted
   auto ensure_list = [&]() {
     if (have_list) return;
     cur ^= 1;
@@ -3412,9 +3426,14 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     NBG_HIP(hipMemsetAsync(K.d, 0, 8, c.stream));
     k_bits_compact<0><<<grid_cap((n_own + 31) / 32, 4096, 4096), 1024, 0, c.stream>>>(bitsA, n_own, lo, nullptr, F,
                                                                                      K.d);
-    NBG_HIP(hipMemcpyAsync(K.h, K.d, 8, hipMemcpyDeviceToHost, c.stream));
-    NBG_HIP(hipStreamSynchronize(c.stream));
-    nF = int64_t(K.h[0]);
+    if (list_n >= 0) {
+      nF = list_n;  // counted by the compaction that wrote the bitmap: no round trip
+    } else {
+      NBG_HIP(hipMemcpyAsync(K.h, K.d, 8, hipMemcpyDeviceToHost, c.stream));
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      nF = int64_t(K.h[0]);
+    }
+    list_n = -1;
     have_list = true;
     off_ready = false;
   };
@@ -3476,6 +3495,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name);
       std::swap(bitsA, bitsB);
       have_list = false;
+      list_n = -1;  // the new bitmap's population is read back by ensure_list
       off_ready = false;
       E = int64_t(K.h[1]);
       E_known = E;
@@ -3510,18 +3530,24 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       cur ^= 1;
       F = c.ws_front[cur].as<int32_t>();
       NBG_HIP(hipMemsetAsync(K.d, 0, 32, c.stream));
-      launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, F, reinterpret_cast<uint16_t*>(bitsA), K.d,
-                     es.odeg.as<uint32_t>());
+      // when the next hop may go bottom-up it reads the bitmap alone: the list is left to
+      // ensure_list (option compact_list = 1 always writes it here).  One rank only: this
+      // bitmap is slice-relative, ensure_list's input is the bottom-up's global-indexed one
+      const bool lazy = c.world == 1 && bu_ok && !multi_root && c.opt("compact_list", 0) == 0;
+      launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
+                     K.d, es.odeg.as<uint32_t>());
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 128, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
-      nF = int64_t(K.h[0]);
+      nF = lazy ? 0 : int64_t(K.h[0]);
+      list_n = lazy ? int64_t(K.h[14]) : -1;
       E = int64_t(K.h[13]);
       E_known = E;
       int64_t g2[2] = {int64_t(K.h[12]), E};
       allsum(c, g2, 2, red);
       nset_global = g2[0];
       Eg = g2[1];
-      have_list = true;
+      have_list = !lazy;
+      if (lazy) cur ^= 1;  // ensure_list flips to the list buffer again
       off_ready = false;
     }
     if (nset_global == 0) return finish_empty();  // onEmptyInputs (GoExecutor.cpp:392-395)

@@ -123,6 +123,24 @@ def test_plain_rows_rmat18(rmat18, steps):
         check_gold("go3_plain_s18", r.columns[0], r.edges_scanned)
 
 
+@pytest.mark.parametrize("compact_list", [0, 1])
+@pytest.mark.parametrize("seeds", [2, 64])
+def test_frontier_list_lazy_or_eager_rmat18(rmat18, compact_list, seeds):
+    """a top-down hop's compaction leaves the next frontier as a bitmap only (compact_list 0) or
+    also as a list (1); a following top-down hop (few seeds) or bottom-up hop reads the same set"""
+    sp, g = rmat18
+    starts = synth.seeds(18, 16, 1, seeds)
+    sp.set_option("compact_list", compact_list)
+    try:
+        for steps in (2, 3, 4):
+            r = sp.go(starts, steps, FOLLOW)
+            want, scanned = g.go(starts, steps)
+            assert np.array_equal(np.sort(r.columns[0]), want)
+            assert r.edges_scanned == scanned
+    finally:
+        sp.set_option("compact_list", 0)
+
+
 def test_shortest_path_1024_pairs_rmat18(rmat18):
     """configs[3]'s shape: 1024 (src, dst) pairs, hops and canonical paths"""
     sp, g = rmat18
