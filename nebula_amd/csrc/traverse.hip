@@ -513,6 +513,22 @@ __global__ __launch_bounds__(kThreads) void k_expand(ExpandArgs a, FastArgs fp, 
         continue;
       }
     }
+    if constexpr (MODE == EXP_MARK && PK == PK_NONE) {
+      if (!a.mark_check && !a.root_next && !big) {
+        // unfiltered marking: the thread's kItems col loads in flight before its byte stores
+        int32_t d[kItems];
+#pragma unroll
+        for (int r = 0; r < kItems; r++) {
+          const int j = threadIdx.x + r * kThreads;
+          d[r] = e0 + j < e1 ? a.col[s_rs[s_own[j]] + e0 + j] : -1;
+        }
+#pragma unroll
+        for (int r = 0; r < kItems; r++)
+          if (d[r] >= 0) a.map[d[r]] = 1;
+        __syncthreads();
+        continue;
+      }
+    }
     uint32_t pm = 0;  // ROWS: items of this thread that pass
 #pragma unroll 2
     for (int r = 0; r < kItems; r++) {
