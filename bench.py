@@ -480,7 +480,7 @@ def main():
     achieved = exp_bytes / (exp_ms / 1e3) / 1e9 if exp_ms > 0 else 0.0
     K = max(args.steps, 1)
     # dominant kernel: the kernel with the largest summed time (the final bottom-up hop's
-    # k_bu_slab for the bench query); its hop (kernel + compaction) is reported beside it
+    # k_bu_lean for the bench query); its hop (kernel + compaction) is reported beside it
     dom = max(range(len(hop_stats)), key=lambda i: k_ms[i]) if hop_stats else None
     workload = (f"GO {args.hops} STEPS FROM {args.seeds} seeds OVER follow WHERE follow.weight > "
                 f"{args.where} YIELD DISTINCT follow._dst; RMAT-{args.scale} ef{args.edge_factor}")

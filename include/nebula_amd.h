@@ -298,6 +298,8 @@ typedef struct {
   nbg_hop_stat hops[NBG_MAX_HOP_STATS];
 } nbg_timing;
 int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out);
+/* engine option key = value (tuning knobs); value INT64_MIN removes the key, so the
+ * engine default applies again                                                              */
 int32_t nbg_set_option(nbg_ctx* ctx, const char* key, int64_t value);
 
 #ifdef __cplusplus

@@ -330,7 +330,8 @@ int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out) {
 int32_t nbg_set_option(nbg_ctx* ctx, const char* key, int64_t value) {
   return guarded(ctx, [&](Ctx& c) {
     if (!key) throw Error(NBG_E_INVALID_ARG, "null key");
-    c.options[key] = value;
+    if (value == INT64_MIN) c.options.erase(key);  // back to the engine default
+    else c.options[key] = value;
     return NBG_OK;
   });
 }

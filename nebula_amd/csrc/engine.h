@@ -279,18 +279,13 @@ struct EdgeSpace {
   bool rmat_stream = false;
   int32_t rmat_scale = 0, rmat_ef = 0;
   uint64_t rmat_seed = 0;
-  // bottom-up slab: the first slab_k entries of every transposed row, slot-major [k][row]
-  int32_t slab_k = 0;
-  DevBuf slab_col;                 // int32, -1 past the row's end
-  std::vector<DevBuf> slab_props;  // per out prop with a transposed copy, same width
   DevBuf odeg;                     // uint32 [owned rows]: out-degree, 0 where row_ok == 0
                                    // (padded with 0 to whole 128-row tiles)
   int64_t bu_live_tiles = 0;       // 128-row tiles up to the last row with out-degree > 0
-  // paired slab: the first 4 entries of every transposed row, row-major in two halves (slots
-  // 0-1 -> pair_col[0], slots 2-3 -> pair_col[1], 2 x int32 per row, -1 past the row's end),
-  // and the transposed INT-like props the same way (pair_props[h][field], 2 values per row)
+  // quad slab (bottom-up first pass): the first 4 entries of every transposed row, row-major in
+  // two halves (slots 0-1 -> pair_col[0], slots 2-3 -> pair_col[1], 2 x int32 per row, -1 past
+  // the row's end, padded to whole 128-row tiles)
   DevBuf pair_col[2];
-  std::vector<DevBuf> pair_props[2];
   // quantised predicate packing (bottom-up hops): the words of pair_col and tcol_q carry the
   // source gidx in their low q_gbits bits and, above it, q_bits bits of the bucket of transposed
   // prop q_field's value: bucket(v) = (v - q_min) * 2^q_bits / q_range (monotone), so a
@@ -428,7 +423,6 @@ struct Ctx {
   hipEvent_t ev[8] = {};
   DevBuf ws_tile_rows;  // k_expand: frontier entry of each tile's first slot
   std::string bu_kernel_name, bu_rest_name;  // rocprof names of the last bottom-up launch
-  int bu_slot_w = 0;                          // predicate bytes loaded beside each slab word
   // deferred kernel timing: event pairs recorded around expansion launches and read once the
   // query's stream has drained, so timing never makes the host wait on a launch
   struct PendingTime {

@@ -502,16 +502,10 @@ static void reset_edge_derived(EdgeSpace& es) {
   es.t_eid.release();
   es.has_tr = es.has_t_eid = false;
   es.out_nnz_global = -1;
-  es.slab_k = 0;
-  es.slab_col.release();
-  es.slab_props.clear();
   es.tcol_q.release();
   es.q_field = -1;
   es.q_gbits = es.q_bits = 0;
-  for (int h = 0; h < 2; h++) {
-    es.pair_col[h].release();
-    es.pair_props[h].clear();
-  }
+  for (int h = 0; h < 2; h++) es.pair_col[h].release();
   es.odeg.release();
 }
 
@@ -1440,15 +1434,6 @@ __global__ void k_gather_u32(const uint32_t* in, const uint32_t* perm, uint32_t*
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
     out[i] = in[perm[i]];
 }
-// ELL slab of the first K entries of every transposed row, slot-major ([k][row]) so a wave's
-// lanes (consecutive rows) read consecutive words; -1 past the row's end
-template <typename T>
-__global__ void k_build_slab(const int64_t* trp, const T* src, int64_t n, int K, T* slab, T none) {
-  for (int64_t d = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; d < n; d += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t b = trp[d], e = trp[d + 1];
-    for (int k = 0; k < K; k++) slab[size_t(k) * size_t(n) + size_t(d)] = b + k < e ? src[b + k] : none;
-  }
-}
 // min / max of a narrowed INT column (width 1/2/4/8)
 __global__ void k_minmax_w(const void* data, int w, int64_t m, long long* mm) {
   long long lo = LLONG_MAX, hi = LLONG_MIN;
@@ -1487,31 +1472,13 @@ __global__ void k_pack_col(const int32_t* col, const void* data, int w, int64_t 
     out[i] = int32_t((q_bucket(v, vmin, range, qbits) << gbits) | uint32_t(col[i]));
   }
 }
-// paired slab: row d's first 4 entries as two row-major halves (slots 0-1 in lo, 2-3 in hi)
+// quad slab: row d's first 4 entries as two row-major halves (slots 0-1 in lo, 2-3 in hi)
 template <typename T>
 __global__ void k_build_pair(const int64_t* trp, const T* src, int64_t n, T* lo, T* hi, T none) {
   for (int64_t d = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; d < n; d += int64_t(gridDim.x) * blockDim.x) {
     const int64_t b = trp[d], e = trp[d + 1];
 #pragma unroll
     for (int q = 0; q < 4; q++) (q < 2 ? lo : hi)[size_t(d) * 2 + (q & 1)] = b + q < e ? src[b + q] : none;
-  }
-}
-static void build_pair_w(Ctx& c, const int64_t* trp, const void* src, int64_t n, void* lo, void* hi, int w) {
-  int g = grid_for(n);
-  switch (w) {
-    case 1: k_build_pair<int8_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int8_t*>(src), n, static_cast<int8_t*>(lo), static_cast<int8_t*>(hi), 0); break;
-    case 2: k_build_pair<int16_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int16_t*>(src), n, static_cast<int16_t*>(lo), static_cast<int16_t*>(hi), 0); break;
-    case 4: k_build_pair<int32_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int32_t*>(src), n, static_cast<int32_t*>(lo), static_cast<int32_t*>(hi), 0); break;
-    default: k_build_pair<int64_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int64_t*>(src), n, static_cast<int64_t*>(lo), static_cast<int64_t*>(hi), 0);
-  }
-}
-static void build_slab_w(Ctx& c, const int64_t* trp, const void* src, int64_t n, int K, void* slab, int w) {
-  int g = grid_for(n);
-  switch (w) {
-    case 1: k_build_slab<int8_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int8_t*>(src), n, K, static_cast<int8_t*>(slab), 0); break;
-    case 2: k_build_slab<int16_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int16_t*>(src), n, K, static_cast<int16_t*>(slab), 0); break;
-    case 4: k_build_slab<int32_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int32_t*>(src), n, K, static_cast<int32_t*>(slab), 0); break;
-    default: k_build_slab<int64_t><<<g, 256, 0, c.stream>>>(trp, static_cast<const int64_t*>(src), n, K, static_cast<int64_t*>(slab), 0);
   }
 }
 
@@ -1700,33 +1667,13 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
   } else {
     es.has_t_eid = false;
   }
-  // the slab
-  es.slab_k = int32_t(std::max<int64_t>(0, std::min<int64_t>(c.opt("bu_slab", 4), 16)));
-  es.slab_props.clear();
-  es.slab_props.resize(o.props.size());
-  if (es.slab_k > 0) {
-    es.slab_col.alloc(size_t(es.slab_k) * size_t(n_own) * 4 + 16);
-    if (n_own)
-      k_build_slab<int32_t><<<grid_for(n_own), 256, 0, c.stream>>>(t.row_ptr.as<int64_t>(), t.col.as<int32_t>(), n_own,
-                                                                  es.slab_k, es.slab_col.as<int32_t>(), -1);
-    for (size_t f = 0; f < o.props.size(); f++) {
-      if (!t.props[f].data.p) continue;
-      int w = t.props[f].width;
-      es.slab_props[f].alloc(size_t(es.slab_k) * size_t(n_own) * size_t(w) + 16);
-      if (n_own) build_slab_w(c, t.row_ptr.as<int64_t>(), t.props[f].data.p, n_own, es.slab_k, es.slab_props[f].p, w);
-    }
-  }
-  // the paired slab (k_bu_pair), packed with the quantised bucket of the first INT-like
-  // transposed prop when the gidx leaves >= 3 spare bits below bit 31
-  for (int h = 0; h < 2; h++) {
-    es.pair_col[h].release();
-    es.pair_props[h].clear();
-    es.pair_props[h].resize(o.props.size());
-  }
+  // the quad slab of the bottom-up first pass (k_bu_lean), packed with the quantised bucket of
+  // the first INT-like transposed prop when the gidx leaves >= 3 spare bits below bit 31
+  for (int h = 0; h < 2; h++) es.pair_col[h].release();
   es.q_field = -1;
   es.q_gbits = es.q_bits = 0;
   es.tcol_q.release();
-  if (c.opt("bu_pair", 1) && c.opt("bu_pack", 1) && R > 0) {
+  if (c.opt("bu_pack", 1) && R > 0) {
     int gb = 1;
     while ((int64_t(1) << gb) < std::max<int64_t>(c.n_global, 2)) gb++;
     const int qb = std::min(8, 31 - gb);
@@ -1754,7 +1701,7 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
       NBG_HIP(hipGetLastError());
     }
   }
-  if (c.opt("bu_pair", 1)) {
+  {
     // padded to whole 128-row tiles with empty slots (-1)
     const int64_t n_pad = (n_own + 127) / 128 * 128;
     for (int h = 0; h < 2; h++) {
@@ -1767,14 +1714,6 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
       k_build_pair<int32_t><<<grid_for(n_own), 256, 0, c.stream>>>(t.row_ptr.as<int64_t>(), src_col, n_own,
                                                                    es.pair_col[0].as<int32_t>(),
                                                                    es.pair_col[1].as<int32_t>(), -1);
-    for (size_t f = 0; f < o.props.size(); f++) {
-      if (!t.props[f].data.p) continue;
-      const int w = t.props[f].width;
-      for (int h = 0; h < 2; h++) es.pair_props[h][f].alloc(size_t(n_own) * 2 * size_t(w) + 16);
-      if (n_own)
-        build_pair_w(c, t.row_ptr.as<int64_t>(), t.props[f].data.p, n_own, es.pair_props[0][f].p,
-                     es.pair_props[1][f].p, w);
-    }
   }
   NBG_HIP(hipStreamSynchronize(c.stream));
   NBG_HIP(hipGetLastError());

@@ -640,35 +640,6 @@ __device__ inline uint32_t wave_excl_scan(uint32_t x, uint32_t& total) {
   return v - x;
 }
 
-// Bottom-up step (direction-optimising BFS, Beamer et al.): every owned vertex d scans its
-// in-neighbours (transpose CSR) until one is in the frontier bitmap (and passes the predicate),
-// then marks itself.  No random writes: the frontier bitmap is read-only (L2/MALL resident) and
-// each thread writes only its own byte.  Same set as the top-down step: next = {d : exists s in F,
-// s -> d [, pred]}, i.e. getDstIdsFromResp's set (GoExecutor.cpp:407-431).
-template <int PK>
-__global__ __launch_bounds__(256) void k_bottom_up(const int64_t* __restrict__ trp, const int32_t* __restrict__ tcol,
-                                                   int64_t n, int64_t lo, const uint32_t* __restrict__ fbits,
-                                                   uint8_t* __restrict__ map, FastArgs fp,
-                                                   unsigned long long* examined) {
-  uint32_t ex = 0;
-  for (int64_t d = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; d < n; d += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t b = trp[d], end = trp[d + 1];
-    bool found = false;
-    for (int64_t e = b; e < end; e++) {
-      const int32_t s = tcol[e];
-      ex++;
-      if (!((fbits[s >> 5] >> (s & 31)) & 1u)) continue;
-      if (PK == PK_FAST && !fast_cmp(fp.op, load_int(fp.data, fp.width, e), fp.k)) continue;
-      found = true;
-      break;
-    }
-    if (found) map[lo + d] = 1;
-  }
-  uint32_t tot;
-  wave_excl_scan(ex, tot);
-  if ((threadIdx.x & 63) == 0 && tot) atomicAdd(examined, (unsigned long long)tot);
-}
-
 __device__ inline unsigned long long wave_sum_u64(unsigned long long x) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
@@ -679,8 +650,7 @@ __device__ inline unsigned long long wave_sum_u64(unsigned long long x) {
 // serialises at ~88 returning atomics/us on MI355X, MI355X_MICROARCH "dequeue") ----------------
 constexpr int kAggBlocks = 8192;  // max grid of the aggregated kernels (partials are [block][kSlots])
 constexpr int kSlots = 8;
-constexpr int kLazyMax = 3;  // k_bu_slab: max lazy slab slots loaded per round trip
-constexpr int kRestMax = 2;  // k_bu_slab: max 64- / 16-entry chunks of a rest loaded per step
+constexpr int kRestMax = 2;  // bu_rest_scan: max 64- / 16-entry chunks of a rest loaded per step
 
 __device__ inline uint32_t block_excl_scan_u32(uint32_t x, uint32_t& total, uint32_t* lds) {
   uint32_t wt;
@@ -860,537 +830,15 @@ __device__ inline void bu_rest_scan(const bool (&pend)[R], bool (&found)[R], con
   }
 }
 
-// Bottom-up hop over the slab (first K hub-first entries of each transposed row, slot-major)
-// with a fallback scan of the rows' remaining entries; writes the next frontier as ballot words.
-// The hop is latency bound (each row is a chain slab -> frontier bit), so a wave owns tiles of
-// 64 x R rows and issues the loads of all R rows (and of the first EAGER slots) before using
-// any of them; rows whose slab entries all miss are then scanned by the whole wave, 64
-// consecutive entries per step (coalesced), instead of by one lane.
-// Only existence matters (a vertex is in the next frontier if ANY in-edge qualifies), so the
-// slots need not be evaluated in order.
-// odeg == nullptr: final hop (keep every found vertex); otherwise keep found vertices with
-// out-edges and sum their out-degrees (the next hop's E).  partials: [0] found, [1] out-degree
-// sum, [2] slab words read (+ their predicate values), [3] rows scanned past the slab, [4] entries
-// read past the slab, [5] predicate values read past the slab.
-// WPE: minimum resident waves per SIMD the register allocation must allow (6..8; the final-hop
-// variant needs ~74 VGPRs unconstrained, i.e. 6 waves)
-template <int PK, int EAGER, int R, int W, int WPE>
-__global__ __launch_bounds__(256, WPE) void k_bu_slab(const int32_t* __restrict__ slab, const void* __restrict__ slab_w,
-                                                 int K, const int64_t* __restrict__ trp,
-                                                 const int32_t* __restrict__ tcol, int64_t n,
-                                                 const uint32_t* __restrict__ fbits,
-                                                 unsigned long long* __restrict__ nbits,
-                                                 const uint32_t* __restrict__ odeg, FastArgs fp,
-                                                 unsigned long long* partials, int nt,
-                                                 unsigned long long* __restrict__ pbits, int cw, int lb,
-                                                 int ru) {
-  __shared__ unsigned long long lds[kSlots * 16];
-  // the first cw words of the frontier bitmap (the hubs: vertices are numbered by descending
-  // out-degree and slab rows list hub sources first) are copied into LDS, so most lookups are
-  // LDS reads instead of random L2 / Infinity-cache requests
-  extern __shared__ uint32_t s_fb[];
-  for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
-  if (cw) __syncthreads();
-  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
-  auto in_front = [&](int32_t sv) -> bool {
-    const int32_t wi = sv >> 5;  // LDS and global reads kept apart (k_bu_quad's in_front)
-    uint32_t w;
-    if (wi < cw) w = s_fb[wi];
-    else w = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, wi * 4, 0, 0);
-    return (w >> (sv & 31)) & 1u;
-  };
-  // per-lane counters (32-bit except the out-degree sum; widened for the block partials)
-  // predicate values held in registers at their loaded width (32-bit unless W == 8)
-  using WT = typename std::conditional<W == 8, int64_t, int32_t>::type;
-  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
-  unsigned long long odsum = 0;
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  const int64_t ntiles = (n + 64 * R - 1) / (64 * R);
-  const int KE = K < EAGER ? K : EAGER;
-  for (int64_t t = wave; t < ntiles; t += nwaves) {
-    int64_t d[R];
-    bool found[R], pend[R];
-    uint32_t od[R];
-#pragma unroll
-    for (int j = 0; j < R; j++) {
-      d[j] = t * 64 * R + j * 64 + lane;
-      found[j] = false;
-      pend[j] = d[j] < n;
-      od[j] = 0;
-    }
-    // level 1: eager slots (+ predicate values, + out-degrees): independent loads
-    int32_t sv[R][EAGER];
-    WT wv[R][EAGER];
-#pragma unroll
-    for (int j = 0; j < R; j++) {
-      if (odeg && pend[j]) od[j] = nt ? __builtin_nontemporal_load(odeg + d[j]) : odeg[d[j]];
-#pragma unroll
-      for (int q = 0; q < EAGER; q++) {
-        sv[j][q] = -1;
-        wv[j][q] = 0;
-        if (pend[j] && q < KE) {
-          const int64_t si = int64_t(q) * n + d[j];
-          sv[j][q] = nt ? __builtin_nontemporal_load(slab + si) : slab[si];
-          if (PK == PK_FAST) wv[j][q] = WT(load_w<W>(slab_w, fp.width, si));
-        }
-      }
-    }
-    // level 2: frontier bits
-#pragma unroll
-    for (int j = 0; j < R; j++) {
-      bool exhausted = false;
-#pragma unroll
-      for (int q = 0; q < EAGER; q++) {
-        if (!pend[j] || q >= KE) continue;
-        const int32_t s = sv[j][q];
-        acc[2]++;
-        if (s < 0) {
-          exhausted = true;
-          continue;
-        }
-        if (in_front(s)) {
-          if (PK != PK_FAST || fast_cmp(fp.op, wv[j][q], fp.k)) found[j] = true;
-        }
-      }
-      pend[j] = pend[j] && !found[j] && !exhausted;
-    }
-    // lazy slots, lb (<= kLazyMax) levels per round trip, only while some row of the wave is
-    // still pending: the loads of a batch are independent (masked by pend), so a batch costs one
-    // slab -> bitmap chain instead of one per slot
-    for (int q0 = KE; q0 < K; q0 += lb) {
-      bool anyp = false;
-#pragma unroll
-      for (int j = 0; j < R; j++) anyp |= pend[j];
-      if (__ballot(anyp) == 0) break;
-      int32_t s1[R][kLazyMax];
-      WT w1[R][kLazyMax];
-#pragma unroll
-      for (int j = 0; j < R; j++) {
-#pragma unroll
-        for (int i = 0; i < kLazyMax; i++) {
-          s1[j][i] = -1;
-          w1[j][i] = 0;
-          if (pend[j] && i < lb && q0 + i < K) {
-            const int64_t si = int64_t(q0 + i) * n + d[j];
-            s1[j][i] = nt ? __builtin_nontemporal_load(slab + si) : slab[si];
-            if (PK == PK_FAST) w1[j][i] = WT(load_w<W>(slab_w, fp.width, si));
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < R; j++) {
-        bool h = false, ex = false;
-#pragma unroll
-        for (int i = 0; i < kLazyMax; i++) {
-          if (!pend[j] || i >= lb || q0 + i >= K) continue;
-          const int32_t s = s1[j][i];
-          acc[2]++;
-          if (s < 0) ex = true;  // slots past the row's end are -1 (and so are all later ones)
-          else if (in_front(s) && (PK != PK_FAST || fast_cmp(fp.op, w1[j][i], fp.k))) h = true;
-        }
-        if (h) found[j] = true;
-        if (h || ex) pend[j] = false;
-      }
-    }
-    // rows with more entries than the slab and no hit in it.  Deferred (pbits): one pending
-    // bit per row (a coalesced ballot word, no atomics) for the edge-balanced second pass
-    // k_bu_rest; rows of a non-final hop without out-edges are dropped (they cannot extend
-    // the frontier).  Otherwise the whole wave scans the rest of each such row in turn.
-    if (pbits) {
-#pragma unroll
-      for (int j = 0; j < R; j++) {
-        bool pj = pend[j] && (odeg == nullptr || od[j] > 0);
-        // only rows with entries past the slab (k_bu_rest's tiles assume no empty rows)
-        if (pj) pj = trp[d[j] + 1] - trp[d[j]] > K;
-        const unsigned long long pm = __ballot(pj);
-        const int64_t d0 = t * 64 * R + j * 64;
-        if (lane == 0 && d0 < n) pbits[d0 >> 6] = pm;
-        acc[3] += pj;
-        pend[j] = false;
-      }
-    }
-    int64_t rb[R], re[R];
-#pragma unroll
-    for (int j = 0; j < R; j++) {
-      rb[j] = re[j] = 0;
-      if (pend[j]) {
-        rb[j] = trp[d[j]] + K;
-        re[j] = trp[d[j] + 1];
-        if (rb[j] >= re[j]) pend[j] = false;
-      }
-    }
-    bu_rest_scan<PK, W, R>(pend, found, rb, re, tcol, fp, ru, acc, in_front, QArgs{});
-    // next frontier words
-#pragma unroll
-    for (int j = 0; j < R; j++) {
-      const uint32_t o = found[j] ? od[j] : 0u;
-      const bool keep = odeg ? o > 0 : found[j];
-      const unsigned long long km = __ballot(keep);
-      const int64_t d0 = t * 64 * R + j * 64;
-      if (lane == 0 && d0 < n) nbits[d0 >> 6] = km;
-      acc[0] += found[j];
-      odsum += o;
-    }
-  }
-  unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
-  block_store_partials(acc64, 6, lds, partials);
-}
-
-// spread the 32 bits of x to the even bit positions of a 64-bit word (scalar: x is wave-uniform)
-__device__ inline unsigned long long spread_even(unsigned long long x) {
-  x &= 0xffffffffull;
-  x = (x | (x << 16)) & 0x0000ffff0000ffffull;
-  x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
-  x = (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
-  x = (x | (x << 2)) & 0x3333333333333333ull;
-  x = (x | (x << 1)) & 0x5555555555555555ull;
-  return x;
-}
-// the two 64-row words of a 128-row unit whose rows 2l / 2l+1 sit in lane l (ballots e / o)
-__device__ inline void unit_words(unsigned long long e, unsigned long long o, unsigned long long& w0,
-                                  unsigned long long& w1) {
-  w0 = spread_even(e) | (spread_even(o) << 1);
-  w1 = spread_even(e >> 32) | (spread_even(o >> 32) << 1);
-}
-
-// Bottom-up hop over the quad slab: the first 4 hub-first in-neighbours of every transposed row
-// stored row-major in two halves (slots 0-1 and 2-3, 8 B per row each).  A lane owns two
-// adjacent rows, so each half arrives in one 16-byte load per lane (the streaming width the HBM
-// path needs: 8-byte loads held the kernel near 3 TB/s even with no probes at all).  With the
-// predicate column packed into the slot words (QP: EdgeSpace::q_*) a slot is decided from its
-// bucket without reading the value; a slot in the buckets holding the compare's constant makes
-// the row pending (the rest pass reads it); without packing the prop halves are loaded with the
-// slots (W bytes per slot).  The predicate is applied before any frontier probe, and a row's
-// probes carry no branches: hub words (the first cw bitmap words: vertices are numbered by
-// descending out-degree) from LDS, the others by buffer loads (non-candidates aim out of bounds).
-// Software pipelined: a wave issues the slab loads of its next unit before probing the current
-// one; R units of 128 rows per lane-iteration.  EH = 2 loads both halves eagerly; EH = 1 the
-// second half only for lanes with a row still pending after the first.  Rows pending after their
-// 4 slots: DEFER leaves a bit in pbits (k_bu_rest_words scans them), else the wave scans their
-// rests here (bu_rest_scan).  Outputs: the next frontier as 64-row words; partials as
-// k_bu_slab's ([3]: rows pending after the slots).
-template <int PK, int W, int QP, int R, int EH, int DEFER>
-__global__ __launch_bounds__(1024, 8) void k_bu_quad(
-    const uint2* __restrict__ slab_lo, const uint2* __restrict__ slab_hi, const void* __restrict__ w_lo,
-    const void* __restrict__ w_hi, const int64_t* __restrict__ trp, const int32_t* __restrict__ tcol, int64_t n,
-    const uint32_t* __restrict__ fbits, unsigned long long* __restrict__ nbits, const uint32_t* __restrict__ odeg,
-    FastArgs fp, QArgs q_arg, unsigned long long* partials, int cw, int ru, unsigned long long* __restrict__ pbits) {
-  const QArgs q = q_sgpr(q_arg);
-  __shared__ unsigned long long lds[kSlots * 16];
-  extern __shared__ uint32_t s_fb[];
-  for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
-  __syncthreads();
-  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
-  auto in_front = [&](int32_t g) -> bool {
-    const int32_t wi = g >> 5;
-    uint32_t w;
-    if (wi < cw) w = s_fb[wi];
-    else w = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, wi * 4, 0, 0);
-    return (w >> (g & 31)) & 1u;
-  };
-  // predicate values of a half: 2 slots of W bytes in one load (unpacked words only)
-  using HW = typename std::conditional<W == 1, uint16_t,
-             typename std::conditional<W == 2, uint32_t, typename std::conditional<W == 4, uint2, uint4>::type>::type>::type;
-  auto wval = [](const HW& h, int k) -> int64_t {
-    if constexpr (W == 1) return int64_t(int8_t(k ? h >> 8 : h));
-    else if constexpr (W == 2) return int64_t(int16_t(k ? h >> 16 : h));
-    else if constexpr (W == 4) return int64_t(int32_t(k ? h.y : h.x));
-    else return k ? int64_t((uint64_t(h.w) << 32) | h.z) : int64_t((uint64_t(h.y) << 32) | h.x);
-  };
-  constexpr bool LOADW = PK == PK_FAST && !QP;
-  constexpr bool ODEG = PK == PK_NONE;  // non-final hops filter on out-degree
-  constexpr int RL = 2 * R;             // rows per lane
-  static_assert(EH == 2 || PK == PK_NONE, "the lazy second half is for predicate-free hops");
-  const int diag = int(fp.width >> 16);  // profiling only (bu_pair_diag): 1 no probes, 2 LDS probes only
-  // branch-free frontier probe of slot word sw (want: it is a candidate)
-  auto probe = [&](int32_t sw, bool want) -> bool {
-    if (diag & 1) return false;
-    const int32_t g = q_gidx(sw, q);
-    const int32_t wi = g >> 5;
-    const bool hub = wi < cw;
-    const uint32_t lw = s_fb[hub ? wi : 0];
-    const uint32_t gw = (diag & 2) ? 0u : __builtin_amdgcn_raw_buffer_load_b32(fb_rs, want && !hub ? uint32_t(wi) * 4u : 0xfffffff0u, 0, 0);
-    return want && (((hub ? lw : gw) >> (g & 31)) & 1u);
-  };
-  // is slot word sw (slot k of a row whose half values are h) a candidate?  QP: decided by the
-  // bucket; a slot in the constant's buckets is not, but sets `und`
-  auto want = [&](int32_t sw, bool live, int k, const HW& h, bool& und) -> bool {
-    if (!live || sw < 0) return false;
-    if (PK != PK_FAST) return true;
-    if (QP) {
-      const int t = q_test(sw, q);
-      und |= t < 0;
-      return t > 0;
-    }
-    return fast_cmp(fp.op, wval(h, k), fp.k);
-  };
-  const int lane = threadIdx.x & 63;
-  // row of slot j (j < RL) of a lane in unit-group t: unit j / 2, parity j % 2
-  auto row_of = [&](int64_t t, int j) -> int64_t { return (t * R + (j >> 1)) * 128 + 2 * lane + (j & 1); };
-  struct Tile {
-    uint4 lo[R], hi[R];  // rows 2l / 2l+1: .xy / .zw
-    HW wl[RL], wh[RL];
-    uint2 od[R];
-  };
-  const uint4 kNone = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-  auto load2 = [&](const uint2* base, int64_t d0) -> uint4 {
-    if (d0 + 1 < n) return reinterpret_cast<const uint4*>(base)[d0 >> 1];
-    if (d0 < n) {
-      const uint2 v = base[d0];
-      return make_uint4(v.x, v.y, 0xffffffffu, 0xffffffffu);
-    }
-    return kNone;
-  };
-  auto load_tile = [&](int64_t t, Tile& T) {
-#pragma unroll
-    for (int u = 0; u < R; u++) {
-      const int64_t d0 = row_of(t, 2 * u);
-      T.lo[u] = load2(slab_lo, d0);
-      T.hi[u] = EH == 2 ? load2(slab_hi, d0) : kNone;
-      if (ODEG && odeg) {
-        T.od[u] = make_uint2(0, 0);
-        if (d0 + 1 < n) T.od[u] = reinterpret_cast<const uint2*>(odeg)[d0 >> 1];
-        else if (d0 < n) T.od[u].x = odeg[d0];
-      } else {
-        T.od[u] = make_uint2(1, 1);
-      }
-      if (LOADW) {
-#pragma unroll
-        for (int p = 0; p < 2; p++) {
-          if (d0 + p < n) {
-            T.wl[2 * u + p] = static_cast<const HW*>(w_lo)[d0 + p];
-            T.wh[2 * u + p] = static_cast<const HW*>(w_hi)[d0 + p];
-          }
-        }
-      }
-    }
-  };
-  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
-  unsigned long long odsum = 0;
-  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  const int64_t ntiles = (n + 128 * R - 1) / (128 * R);
-  Tile cur;
-  if (wave < ntiles) load_tile(wave, cur);
-  for (int64_t t = wave; t < ntiles; t += nwaves) {
-    Tile nxt;
-    if (t + nwaves < ntiles) load_tile(t + nwaves, nxt);  // in flight while this unit probes
-    int64_t d[RL];
-    bool found[RL], pend[RL], und[RL];
-    uint32_t od[RL];
-#pragma unroll
-    for (int j = 0; j < RL; j++) {
-      const int u = j >> 1, p = j & 1;
-      d[j] = row_of(t, j);
-      od[j] = p ? cur.od[u].y : cur.od[u].x;
-      // a non-final hop keeps only vertices with out-edges (they alone extend the frontier; an
-      // all-zero-degree frontier ends the query either way, P17): other rows are not probed
-      const bool live = d[j] < n && od[j] > 0;
-      if (d[j] < n) acc[2] += EH == 2 ? 4 : 2;
-      const int32_t s0 = int32_t(p ? cur.lo[u].z : cur.lo[u].x), s1 = int32_t(p ? cur.lo[u].w : cur.lo[u].y);
-      const int32_t s2 = int32_t(p ? cur.hi[u].z : cur.hi[u].x), s3 = int32_t(p ? cur.hi[u].w : cur.hi[u].y);
-      bool uu = false;
-      const bool w0 = want(s0, live, 0, cur.wl[j], uu), w1 = want(s1, live, 1, cur.wl[j], uu);
-      const bool w2 = EH == 2 && want(s2, live, 0, cur.wh[j], uu), w3 = EH == 2 && want(s3, live, 1, cur.wh[j], uu);
-      found[j] = (int(probe(s0, w0)) | int(probe(s1, w1)) | int(EH == 2 && probe(s2, w2)) |
-                  int(EH == 2 && probe(s3, w3))) != 0;
-      und[j] = uu;
-      pend[j] = live && !found[j] && ((EH == 2 ? s3 >= 0 : s1 >= 0) || uu);
-    }
-    if (EH == 1) {
-      bool anyp = false;
-#pragma unroll
-      for (int j = 0; j < RL; j++) anyp |= pend[j];
-      if (__ballot(anyp)) {
-        uint4 hi[R];
-#pragma unroll
-        for (int u = 0; u < R; u++)
-          if (pend[2 * u] || pend[2 * u + 1]) hi[u] = load2(slab_hi, d[2 * u]);
-#pragma unroll
-        for (int j = 0; j < RL; j++) {
-          if (!pend[j]) continue;
-          const int u = j >> 1, p = j & 1;
-          acc[2] += 2;
-          const int32_t s2 = int32_t(p ? hi[u].z : hi[u].x), s3 = int32_t(p ? hi[u].w : hi[u].y);
-          found[j] = (int(probe(s2, s2 >= 0)) | int(probe(s3, s3 >= 0))) != 0;
-          pend[j] = !found[j] && s3 >= 0;
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < RL; j++) acc[3] += pend[j];
-    if (DEFER) {
-#pragma unroll
-      for (int u = 0; u < R; u++) {
-        unsigned long long w0, w1;
-        unit_words(__ballot(pend[2 * u]), __ballot(pend[2 * u + 1]), w0, w1);
-        const int64_t d0 = (t * R + u) * 128;
-        if (lane == 0 && d0 < n) pbits[d0 >> 6] = w0;
-        if (lane == 1 && d0 + 64 < n) pbits[(d0 >> 6) + 1] = w1;
-      }
-    } else {
-      int64_t rb[RL], re[RL];
-#pragma unroll
-      for (int j = 0; j < RL; j++) {
-        rb[j] = re[j] = 0;
-        if (pend[j]) {
-          rb[j] = trp[d[j]] + (und[j] ? 0 : 4);
-          re[j] = trp[d[j] + 1];
-          if (rb[j] >= re[j]) pend[j] = false;
-        }
-      }
-      const uint32_t a3 = acc[3];
-      bu_rest_scan<PK, W, RL>(pend, found, rb, re, tcol, fp, ru, acc, in_front, q);
-      acc[3] = a3;
-    }
-#pragma unroll
-    for (int u = 0; u < R; u++) {
-      unsigned long long w0, w1;
-      unit_words(__ballot(found[2 * u]), __ballot(found[2 * u + 1]), w0, w1);
-      const int64_t d0 = (t * R + u) * 128;
-      if (lane == 0 && d0 < n) nbits[d0 >> 6] = w0;
-      if (lane == 1 && d0 + 64 < n) nbits[(d0 >> 6) + 1] = w1;
-    }
-#pragma unroll
-    for (int j = 0; j < RL; j++) {
-      acc[0] += found[j];
-      if (ODEG && odeg && found[j]) odsum += od[j];
-    }
-    cur = nxt;
-  }
-  unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
-  block_store_partials(acc64, 6, lds, partials);
-}
-
-// Deferred quad hop as a D-deep software pipeline (k_bu_quad's work for DEFER, EH = 2, no
-// eager prop halves).  Vector-memory loads complete in issue order, so a wave that refills its
-// tile registers before probing waits for the refill along with the probes: here each tile's
-// probes are issued first, then the tile D steps ahead is loaded into the registers just
-// consumed, then the probe results are used, so D - 1 tiles of slab loads stay in flight behind
-// every probe round.  Two adjacent rows per lane (16-byte loads of each half).
-template <int PK, int QP, int D>
-__global__ __launch_bounds__(1024, 4) void k_bu_ring(
-    const uint2* __restrict__ slab_lo, const uint2* __restrict__ slab_hi, int64_t n,
-    const uint32_t* __restrict__ fbits, unsigned long long* __restrict__ nbits, const uint32_t* __restrict__ odeg,
-    QArgs q_arg, unsigned long long* partials, int cw, unsigned long long* __restrict__ pbits, int diag) {
-  const QArgs q = q_sgpr(q_arg);
-  __shared__ unsigned long long lds[kSlots * 16];
-  extern __shared__ uint32_t s_fb[];
-  for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
-  __syncthreads();
-  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
-  constexpr bool ODEG = PK == PK_NONE;
-  const int lane = threadIdx.x & 63;
-  struct Tile {
-    uint4 lo, hi;  // rows 2l / 2l+1: .xy / .zw
-    uint2 od;
-  };
-  const uint4 kNone = make_uint4(0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu);
-  auto load2 = [&](const uint2* base, int64_t d0) -> uint4 {
-    if (d0 + 1 < n) return reinterpret_cast<const uint4*>(base)[d0 >> 1];
-    if (d0 < n) {
-      const uint2 v = base[d0];
-      return make_uint4(v.x, v.y, 0xffffffffu, 0xffffffffu);
-    }
-    return kNone;
-  };
-  auto load_tile = [&](int64_t t, Tile& T) {
-    const int64_t d0 = t * 128 + 2 * lane;
-    T.lo = load2(slab_lo, d0);
-    T.hi = load2(slab_hi, d0);
-    T.od = make_uint2(1, 1);
-    if (ODEG && odeg) {
-      T.od = make_uint2(0, 0);
-      if (d0 + 1 < n) T.od = reinterpret_cast<const uint2*>(odeg)[d0 >> 1];
-      else if (d0 < n) T.od.x = odeg[d0];
-    }
-  };
-  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
-  unsigned long long odsum = 0;
-  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  const int64_t ntiles = (n + 127) / 128;
-  Tile ring[D];
-#pragma unroll
-  for (int k = 0; k < D; k++)
-    if (wave + k * nwaves < ntiles) load_tile(wave + k * nwaves, ring[k]);
-  for (int64_t t0 = wave; t0 < ntiles; t0 += D * nwaves) {
-#pragma unroll
-    for (int k = 0; k < D; k++) {
-      const int64_t t = t0 + k * nwaves;
-      if (t >= ntiles) break;
-      // probes of the tile's 8 slots: word index, bit, candidate flag, raw words
-      uint32_t word[8], bit[8], cand = 0, und = 0, has4 = 0, live = 0;
-      uint32_t od[2];
-#pragma unroll
-      for (int p = 0; p < 2; p++) {
-        const int64_t d = t * 128 + 2 * lane + p;
-        od[p] = p ? ring[k].od.y : ring[k].od.x;
-        const bool lv = d < n && od[p] > 0;
-        live |= uint32_t(lv) << p;
-        const int32_t sw[4] = {int32_t(p ? ring[k].lo.z : ring[k].lo.x), int32_t(p ? ring[k].lo.w : ring[k].lo.y),
-                               int32_t(p ? ring[k].hi.z : ring[k].hi.x), int32_t(p ? ring[k].hi.w : ring[k].hi.y)};
-        has4 |= uint32_t(sw[3] >= 0) << p;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          bool w = lv && sw[j] >= 0;
-          if (PK == PK_FAST) {
-            const int tq = q_test(sw[j], q);
-            if (w && tq < 0) und |= 1u << p;
-            w = w && tq > 0;
-          }
-          const int32_t g = q_gidx(sw[j], q);
-          const int32_t wi = g >> 5;
-          const bool hub = wi < cw;
-          bit[4 * p + j] = uint32_t(g & 31) | (hub ? 32u : 0u);
-          cand |= uint32_t(w) << (4 * p + j);
-          if (diag & 1) {
-            word[4 * p + j] = 0;
-          } else {
-            const uint32_t lw = s_fb[hub ? wi : 0];
-            const uint32_t gw = (diag & 2) ? 0u : __builtin_amdgcn_raw_buffer_load_b32(fb_rs, w && !hub ? uint32_t(wi) * 4u : 0xfffffff0u, 0, 0);
-            word[4 * p + j] = hub ? lw : gw;
-          }
-        }
-      }
-      // refill this slot of the ring (issued after the probes: they do not wait for it)
-      if (t + D * nwaves < ntiles) load_tile(t + D * nwaves, ring[k]);
-      bool found[2], pend[2];
-#pragma unroll
-      for (int p = 0; p < 2; p++) {
-        bool f = false;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int e = 4 * p + j;
-          f |= ((cand >> e) & 1u) && ((word[e] >> (bit[e] & 31u)) & 1u);
-        }
-        found[p] = f;
-        pend[p] = ((live >> p) & 1u) && !f && (((has4 >> p) & 1u) || ((und >> p) & 1u));
-        const int64_t d = t * 128 + 2 * lane + p;
-        if (d < n) acc[2] += 4;
-        acc[0] += f;
-        acc[3] += pend[p];
-        if (ODEG && odeg && f) odsum += od[p];
-      }
-      unsigned long long w0, w1;
-      const int64_t d0 = t * 128;
-      unit_words(__ballot(pend[0]), __ballot(pend[1]), w0, w1);
-      if (lane == 0 && d0 < n) pbits[d0 >> 6] = w0;
-      if (lane == 1 && d0 + 64 < n) pbits[(d0 >> 6) + 1] = w1;
-      unit_words(__ballot(found[0]), __ballot(found[1]), w0, w1);
-      if (lane == 2 && d0 < n) nbits[d0 >> 6] = w0;
-      if (lane == 3 && d0 + 64 < n) nbits[(d0 >> 6) + 1] = w1;
-    }
-  }
-  unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
-  block_store_partials(acc64, 6, lds, partials);
-}
-
-// Lean first pass of a bottom-up hop over the quad slab (bu_kernel = 2, the default).  Same
-// work as k_bu_quad (DEFER) with the instruction stream cut to what the hop needs, because the
-// quad kernel was issue-bound (with no probes at all it still ran at ~2.2 TB/s):
+// Bottom-up hop (direction-optimising BFS, Beamer et al.): every owned vertex d looks for an
+// in-neighbour (transposed CSR) in the frontier bitmap whose edge passes the predicate, and is
+// in the next frontier iff it finds one -- the set getDstIdsFromResp builds
+// (GoExecutor.cpp:407-431), with no random writes: the frontier bitmap is read-only and each
+// wave writes only its own words.  Two passes: k_bu_lean over the quad slab (the first 4
+// hub-first in-neighbours of every transposed row, two 8-byte halves per row), then
+// k_bu_rest_lean over the rows it left pending.
+// The first pass's instruction stream is cut to what the hop needs (round 2: a general slab
+// kernel with per-slot branches and bounds checks was issue-bound at ~2.2 TB/s with no probes):
 //  * the slab halves and the out-degrees are padded to whole 128-row tiles at build (pad slots
 //    -1, degree 0), so the tile loads carry no bounds checks and no branches;
 //  * a lane owns rows l and l + 64 of a 128-row tile (8-byte loads per half), so the two ballots
@@ -1399,15 +847,17 @@ __global__ __launch_bounds__(1024, 4) void k_bu_ring(
 //    bit tests (sched_barrier keeps the scheduler from pulling the consumers up to the loads,
 //    which put a vmcnt(0) wait behind every probe);
 //  * every probe is a buffer load whose offset is out of bounds for a non-candidate slot (the
-//    hardware returns 0: no branch; an LDS copy of the hub end of the bitmap measured no gain);
+//    hardware returns 0: no branch);
 //  * a non-final hop (PK_NONE) reads the second half only for rows still pending after the
 //    first (almost none: hub-first slot 0 is nearly always in a dense frontier), and only the
 //    tiles below es.bu_live_tiles (vertices are numbered by descending out-degree, so the rows
 //    with no out-edges - which never extend the frontier - form the tail); dead tiles get zero
 //    words;
-//  * the final hop (PK_FAST over the packed predicate buckets, QP) decides each slot by two
-//    scalar compares of its bucket; undecided buckets and rows with more than 4 entries are left
-//    pending for k_bu_rest_words (rest_from 0).
+//  * the final hop (PK_FAST) decides each slot by two scalar compares of its packed bucket
+//    (QArgs); a frontier hit in an undecided bucket and rows with more than 4 entries are left
+//    pending for k_bu_rest_lean (rest_from 0).  A predicate on a column that is not the packed
+//    one makes every bucket undecided: the first pass then only clears rows with no frontier
+//    in-neighbour among their slots, and the rest pass reads the values.
 // Outputs: next-frontier and pending words; partials [0] found, [1] their out-degree sum,
 // [2] slab words read, [3] pending rows.
 // HUB: the block keeps the first cw words of the bitmap (the highest-out-degree vertices) in LDS
@@ -1436,14 +886,16 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
   uint32_t nfound = 0, npend = 0, nwords = 0, nglob = 0, nhub = 0;
   unsigned long long odsum = 0;
   // bitmap-word offset of slot word sw of a live row: out of bounds unless it is a candidate
-  // answered by L2; the LDS word index (HUB) in `hw` (-1: not a hub candidate); `und` collects
-  // undecided buckets (final hop)
-  auto off = [&](int32_t sw, bool live, bool& und, int32_t& hw) -> uint32_t {
+  // answered by L2; the LDS word index (HUB) in `hw` (-1: not a hub candidate).  Final hop: a
+  // slot whose bucket fails is no candidate; an undecided one (the constant's bucket, or every
+  // slot when the predicate column is not the packed one) is probed too and flagged in bit k of
+  // `und`, so only an undecided slot whose source IS in the frontier leaves the row pending
+  auto off = [&](int32_t sw, bool live, uint32_t& und, int k, int32_t& hw) -> uint32_t {
     bool c = live && sw >= 0;
     if (FINAL) {
       const int t = q_test(sw, q);
-      und = und || (c && t < 0);
-      c = c && t > 0;
+      und |= (c && t < 0) ? 1u << k : 0u;
+      c = c && t != 0;
     }
     const int32_t wi = q_gidx(sw, q) >> 5;
     const bool hub = HUB && wi < cw;
@@ -1472,18 +924,18 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
     __builtin_amdgcn_sched_barrier(0);
     uint32_t w[U][2][4];
     int32_t hw[U][2][4];
-    bool und[U][2];
+    uint32_t und[U][2];
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const bool live = v[u] && od[u][h] > 0;
-        und[u][h] = false;
-        w[u][h][0] = ld_(off(int32_t(a[u][h].x), live, und[u][h], hw[u][h][0]));
-        w[u][h][1] = ld_(off(int32_t(a[u][h].y), live, und[u][h], hw[u][h][1]));
+        und[u][h] = 0u;
+        w[u][h][0] = ld_(off(int32_t(a[u][h].x), live, und[u][h], 0, hw[u][h][0]));
+        w[u][h][1] = ld_(off(int32_t(a[u][h].y), live, und[u][h], 1, hw[u][h][1]));
         if (FINAL) {
-          w[u][h][2] = ld_(off(int32_t(b[u][h].x), live, und[u][h], hw[u][h][2]));
-          w[u][h][3] = ld_(off(int32_t(b[u][h].y), live, und[u][h], hw[u][h][3]));
+          w[u][h][2] = ld_(off(int32_t(b[u][h].x), live, und[u][h], 2, hw[u][h][2]));
+          w[u][h][3] = ld_(off(int32_t(b[u][h].y), live, und[u][h], 3, hw[u][h][3]));
         }
       }
     if (HUB) {
@@ -1503,11 +955,17 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
     for (int u = 0; u < U; u++) {
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        bool x = hit(w[u][h][0], int32_t(a[u][h].x)) || hit(w[u][h][1], int32_t(a[u][h].y));
+        bool x;
         if (FINAL) {
-          x = x || hit(w[u][h][2], int32_t(b[u][h].x)) || hit(w[u][h][3], int32_t(b[u][h].y));
-          pend[u][h] = v[u] && !x && (int32_t(b[u][h].y) >= 0 || und[u][h]);
+          // slot k in the frontier: found when its bucket passes, pending when undecided
+          const uint32_t hm = uint32_t(hit(w[u][h][0], int32_t(a[u][h].x))) |
+                              uint32_t(hit(w[u][h][1], int32_t(a[u][h].y))) << 1 |
+                              uint32_t(hit(w[u][h][2], int32_t(b[u][h].x))) << 2 |
+                              uint32_t(hit(w[u][h][3], int32_t(b[u][h].y))) << 3;
+          x = (hm & ~und[u][h]) != 0u;
+          pend[u][h] = v[u] && !x && (int32_t(b[u][h].y) >= 0 || (hm & und[u][h]) != 0u);
         } else {
+          x = hit(w[u][h][0], int32_t(a[u][h].x)) || hit(w[u][h][1], int32_t(a[u][h].y));
           // rows with a third slot to test: live, not found, slot 1 present
           pend[u][h] = v[u] && !x && od[u][h] > 0 && int32_t(a[u][h].y) >= 0;
         }
@@ -1532,9 +990,9 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
         for (int u = 0; u < U; u++)
 #pragma unroll
           for (int h = 0; h < 2; h++) {
-            bool dummy = false;
-            w[u][h][2] = ld_(off(int32_t(b[u][h].x), pend[u][h], dummy, hw[u][h][2]));
-            w[u][h][3] = ld_(off(int32_t(b[u][h].y), pend[u][h], dummy, hw[u][h][3]));
+            uint32_t dummy = 0u;
+            w[u][h][2] = ld_(off(int32_t(b[u][h].x), pend[u][h], dummy, 2, hw[u][h][2]));
+            w[u][h][3] = ld_(off(int32_t(b[u][h].y), pend[u][h], dummy, 3, hw[u][h][3]));
             if (HUB) {
 #pragma unroll
               for (int k = 2; k < 4; k++) {
@@ -1594,7 +1052,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
 // in k_bu_lean; a value is read only for a frontier hit in the constant's bucket.  After
 // kLeanSteps chunks the rows still pending (long in-edge lists) go to bu_rest_scan (whole wave /
 // 16-lane groups).  Found rows OR into the wave's 64 next-frontier words in LDS, merged into
-// nbits by the owning lanes (one writer per word).  Partials as k_bu_rest_words's.
+// nbits by the owning lanes (one writer per word).  Partials [0] found, [1] their out-degree
+// sum, [3] rows scanned by bu_rest_scan (counted by the first pass), [4] entries read, [5] values read.
 constexpr int kLeanChunk = 8;
 template <int PK, int W, int HUB>
 __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long long* __restrict__ pbits, int64_t n,
@@ -1727,268 +1186,6 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
   }
   unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
   block_store_partials(acc64, 6, lds, partials);
-}
-
-// Second pass of a deferred quad hop, straight from the pending bits (no list, no global
-// atomics): a wave owns 64 consecutive pbits words (4096 rows), ranks their pending rows (wave
-// prefix sum of the words' popcounts), and scans them 64 at a time, lane per row, in chunks of
-// kLaneChunk entries of the (packed) transposed column: the chunk's loads are independent, a
-// packed word settles the predicate from its bucket (the value is read only in the constant's
-// bucket); at most kLaneSteps chunks, then bu_rest_scan for long rests.  Found rows OR into the
-// wave's 64 next-frontier words in LDS, which the owning lanes merge into nbits (one writer per
-// word).  A row's scan starts at entry rest_from (4: its quad slots are settled; 0 with the
-// quantised predicate, whose undecided slots are read here).  Partials as k_bu_quad's (the
-// pending rows were counted there).
-constexpr int kLaneChunk = 8;
-constexpr int kLaneSteps = 4;
-template <int PK, int W, int OCC>
-__global__ __launch_bounds__(1024, OCC) void k_bu_rest_words(const unsigned long long* __restrict__ pbits, int64_t n,
-                                                           const int64_t* __restrict__ trp,
-                                                           const int32_t* __restrict__ tcol,
-                                                           const uint32_t* __restrict__ fbits, unsigned long long* nbits,
-                                                           const uint32_t* __restrict__ odeg, FastArgs fp, QArgs q_arg,
-                                                           unsigned long long* partials, int cw, int ru,
-                                                           int rest_from) {
-  const QArgs q = q_sgpr(q_arg);
-  __shared__ unsigned long long lds[kSlots * 16];
-  __shared__ unsigned long long s_found[16][64];
-  extern __shared__ uint32_t s_fb[];
-  for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
-  __syncthreads();
-  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
-  auto in_front = [&](int32_t g) -> bool {
-    // hub words from the LDS copy (ds_read), the rest by a buffer load: two plain loads would be
-    // merged into one flat load (select of the pointers), which takes the texture path for LDS
-    // addresses too and waits on both counters
-    const int32_t wi = g >> 5;
-    uint32_t w;
-    if (wi < cw) w = s_fb[wi];
-    else w = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, wi * 4, 0, 0);
-    return (w >> (g & 31)) & 1u;
-  };
-  uint32_t acc[6] = {0, 0, 0, 0, 0, 0};
-  unsigned long long odsum = 0;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t nwords = (n + 63) / 64;
-  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t cbase = wave * 64; cbase < nwords; cbase += nwaves * 64) {
-    const int64_t myw = cbase + lane;
-    const unsigned long long pw = myw < nwords ? pbits[myw] : 0ull;
-    s_found[wv][lane] = 0ull;
-    uint32_t total;
-    const uint32_t pre = wave_excl_scan(uint32_t(__popcll(pw)), total);
-    for (uint32_t k0 = 0; k0 < total; k0 += 64) {
-      // the (k0 + lane)-th pending row of the chunk: its word (binary search over the lanes'
-      // exclusive prefix sums) and the matching set bit of that word
-      const uint32_t p = k0 + uint32_t(lane);
-      bool pend[1] = {p < total}, found[1] = {false};
-      int64_t rb[1] = {0}, re[1] = {0};
-      int wsel = 0;
-      {
-#pragma unroll
-        for (int st = 32; st > 0; st >>= 1) {
-          const uint32_t pv = __shfl(pre, wsel + st);
-          if (wsel + st < 64 && pv <= p) wsel += st;
-        }
-      }
-      const unsigned long long wbits = __shfl((long long)pw, wsel);
-      const uint32_t kk = p - __shfl(pre, wsel);  // the kk-th set bit of wbits
-      int bit = 0;
-#pragma unroll
-      for (int st = 32; st > 0; st >>= 1)
-        if (uint32_t(__popcll(wbits & ((1ull << (bit + st)) - 1ull))) <= kk) bit += st;
-      const int32_t r = int32_t((cbase + wsel) * 64 + bit);
-      if (pend[0]) {
-        rb[0] = trp[r] + rest_from;
-        re[0] = trp[r + 1];
-        pend[0] = rb[0] < re[0];
-      }
-      for (int step = 0; step < kLaneSteps; step++) {
-        if (__ballot(pend[0]) == 0) break;
-        if (pend[0]) {
-          int32_t sv[kLaneChunk];
-#pragma unroll
-          for (int k = 0; k < kLaneChunk; k++) sv[k] = rb[0] + k < re[0] ? tcol[rb[0] + k] : -1;
-          int hit = 0;
-#pragma unroll
-          for (int k = 0; k < kLaneChunk; k++) {
-            if (sv[k] < 0) continue;
-            acc[4]++;
-            const int tq = PK == PK_FAST ? q_test(sv[k], q) : 1;
-            if (tq == 0 || !in_front(q_gidx(sv[k], q))) continue;
-            if (tq == 1) {
-              hit = 1;
-              continue;
-            }
-            acc[5]++;  // the value is read only after a frontier hit, in the constant's bucket
-            hit |= int(fast_cmp(fp.op, load_w<W>(fp.data, fp.width, rb[0] + k), fp.k));
-          }
-          rb[0] += kLaneChunk;
-          if (hit) found[0] = true;
-          pend[0] = !hit && rb[0] < re[0];
-        }
-      }
-      const uint32_t a3 = acc[3];
-      bu_rest_scan<PK, W, 1>(pend, found, rb, re, tcol, fp, ru, acc, in_front, q);
-      acc[3] = a3;  // the pending rows were counted by the first pass
-      if (found[0]) {
-        atomicOr(&s_found[wv][wsel], 1ull << (r & 63));
-        acc[0]++;
-        if (odeg) odsum += odeg[r];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    const unsigned long long fw = s_found[wv][lane];
-    if (fw) nbits[myw] |= fw;
-    __builtin_amdgcn_wave_barrier();
-  }
-  unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
-  block_store_partials(acc64, 6, lds, partials);
-}
-
-// Second pass of a deferred bottom-up hop: the rows k_bu_slab left pending (list F, nF rows),
-// entries past the slab [trp[r] + K, trp[r + 1]) spread edge-balanced over the workgroups exactly
-// like the top-down expansion (tiles of kTile entries, owner row by binary search in LDS), so the
-// long in-edge lists no longer serialise one wave.  A hit sets the row's flag in LDS; after the
-// tile one thread per hit row ORs the row's bit into the next-frontier words (returning atomic:
-// only the first setter counts the row).  partials: [0] rows found, [1] their out-degree sum,
-// [2] entries read, [3] predicate values read.
-template <int PK>
-__global__ __launch_bounds__(kThreads) void k_bu_rest(const int32_t* __restrict__ F, int64_t nF,
-                                                      const int64_t* __restrict__ off, const int64_t* __restrict__ trp,
-                                                      const int32_t* __restrict__ tcol, int K,
-                                                      const uint32_t* __restrict__ fbits, unsigned long long* nbits,
-                                                      const uint32_t* __restrict__ odeg, FastArgs fp,
-                                                      unsigned long long* partials) {
-  __shared__ int32_t s_off[kTile + 1];
-  __shared__ int64_t s_rs[kTile];
-  __shared__ int32_t s_row[kTile];
-  __shared__ uint8_t s_hit[kTile];
-  __shared__ int64_t s_hdr[2];
-  __shared__ unsigned long long lds[kSlots * 16];
-  unsigned long long acc[4] = {0, 0, 0, 0};
-  const int64_t E = off[nF];
-  const int64_t ntiles = (E + kTile - 1) / kTile;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int64_t e0 = t * kTile;
-    const int64_t e1 = min(e0 + int64_t(kTile), E);
-    if (threadIdx.x == 0) {
-      int64_t lo = 0, hi = nF;
-      while (hi - lo > 1) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (off[mid] <= e0) lo = mid; else hi = mid;
-      }
-      const int64_t i0 = lo;
-      hi = nF;
-      while (hi - lo > 1) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (off[mid] <= e1 - 1) lo = mid; else hi = mid;
-      }
-      s_hdr[0] = i0;
-      s_hdr[1] = lo - i0 + 1;
-    }
-    __syncthreads();
-    const int64_t i0 = s_hdr[0];
-    const int cnt = int(s_hdr[1]);
-    for (int k = threadIdx.x; k <= cnt; k += kThreads) {
-      const int64_t o = off[i0 + k];
-      s_off[k] = int32_t(min(o - e0, int64_t(kTile + 1)));
-      if (k < cnt) {
-        const int32_t r = F[i0 + k];
-        s_row[k] = r;
-        s_rs[k] = trp[r] + K - o;
-        s_hit[k] = 0;
-      }
-    }
-    __syncthreads();
-#pragma unroll 2
-    for (int q = 0; q < kItems; q++) {
-      const int j = threadIdx.x + q * kThreads;
-      const int64_t e = e0 + j;
-      if (e >= e1) continue;
-      int lo = 0, hi = cnt;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (s_off[mid] <= j) lo = mid; else hi = mid;
-      }
-      const int64_t ge = s_rs[lo] + e;
-      const int32_t sv = tcol[ge];
-      acc[2]++;
-      if ((fbits[sv >> 5] >> (sv & 31)) & 1u) {
-        bool h = true;
-        if (PK == PK_FAST) {
-          acc[3]++;
-          h = fast_cmp(fp.op, load_int(fp.data, fp.width, ge), fp.k);
-        }
-        if (h) s_hit[lo] = 1;
-      }
-    }
-    __syncthreads();
-    for (int k = threadIdx.x; k < cnt; k += kThreads) {
-      if (!s_hit[k]) continue;
-      const int32_t r = s_row[k];
-      const unsigned long long bit = 1ull << (r & 63);
-      const unsigned long long old = atomicOr(nbits + (r >> 6), bit);
-      if (!(old & bit)) {
-        acc[0]++;
-        acc[1] += odeg ? odeg[r] : 0u;
-      }
-    }
-    __syncthreads();
-  }
-  block_store_partials(acc, 4, lds, partials);
-}
-
-// remaining in-degree past the slab of each pending row; deg[nF] = 0
-__global__ void k_rest_deg(const int32_t* F, int64_t nF, const int64_t* trp, int K, int64_t* deg) {
-  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= nF; i += int64_t(gridDim.x) * blockDim.x) {
-    if (i == nF) {
-      deg[i] = 0;
-    } else {
-      const int32_t r = F[i];
-      deg[i] = max(int64_t(0), trp[r + 1] - trp[r] - K);
-    }
-  }
-}
-
-// Bottom-up hop writing the next frontier straight into a bitmap (one 64-bit ballot word per
-// wave: coalesced, no byte-map, no compaction).  partials per block: [0] vertices found (the
-// reference's "starts_ non-empty" test), [1] out-degree sum of the next frontier (direction
-// heuristic of the following hop), [2] adjacency entries examined.
-template <int PK>
-__global__ __launch_bounds__(256) void k_bu_bits(const int64_t* __restrict__ trp, const int32_t* __restrict__ tcol,
-                                                 int64_t n, const uint32_t* __restrict__ fbits,
-                                                 unsigned long long* __restrict__ nbits,
-                                                 const int64_t* __restrict__ row_ptr, const uint8_t* __restrict__ row_ok,
-                                                 FastArgs fp, unsigned long long* partials) {
-  __shared__ unsigned long long lds[kSlots * 16];
-  unsigned long long acc[3] = {0, 0, 0};  // found, esum, examined
-  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-  const int64_t rounds = (n + stride - 1) / stride;
-  const int lane = threadIdx.x & 63;
-  for (int64_t r = 0; r < rounds; r++) {
-    const int64_t d = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-    bool found = false;
-    if (d < n) {
-      const int64_t end = trp[d + 1];
-      for (int64_t e = trp[d]; e < end; e++) {
-        const int32_t s = tcol[e];
-        acc[2]++;
-        if (!((fbits[s >> 5] >> (s & 31)) & 1u)) continue;
-        if (PK == PK_FAST && !fast_cmp(fp.op, load_int(fp.data, fp.width, e), fp.k)) continue;
-        found = true;
-        break;
-      }
-    }
-    const bool keep = found && (row_ok == nullptr || row_ok[d]);
-    const unsigned long long km = __ballot(row_ptr ? keep : found);
-    const int64_t d0 = d - lane;
-    if (lane == 0 && d0 < n) nbits[d0 >> 6] = km;
-    if (found) acc[0]++;
-    if (keep && row_ptr) acc[1] += (unsigned long long)(row_ptr[d + 1] - row_ptr[d]);
-  }
-  block_store_partials(acc, 3, lds, partials);
 }
 
 // bitmap -> compacted list.  mode 0: local rows (a top-down hop's frontier; the bitmaps this
@@ -2711,80 +1908,6 @@ void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Progr
   c.timing.expand_launches++;
 }
 
-// bottom-up hop over the slab: launches the kernel and the partials reduction into out[0..8)
-// (no synchronisation); returns the grid used
-int launch_bu_slab(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
-                   const FastArgs& fp, const void* slab_w, unsigned long long* out,
-                   unsigned long long* pbits = nullptr, hipEvent_t after_kernel = nullptr) {
-  // rows per lane (R) and eagerly loaded slab slots (EAGER) are options (bu_r, bu_eager[_fast])
-  constexpr int R = 2;  // rows per lane
-  const int EG = int(c.opt(pk == PK_FAST ? "bu_eager_fast" : "bu_eager", 1));
-  const Csr& tr = es.tr;
-  unsigned long long* partials = c.ws_partials.as<unsigned long long>();
-  const int64_t tiles = (tr.n_rows + 64 * R - 1) / (64 * R);
-  const int64_t per_wave = std::max<int64_t>(1, c.opt("bu_tiles_per_wave", 4));
-  int grid = int(std::max<int64_t>(
-      1, std::min<int64_t>((tiles + per_wave - 1) / per_wave, std::min<int64_t>(c.opt("bu_grid", 4096), kAggBlocks))));
-  // LDS copy of the bitmap's hub words (bu_lds_kb KiB, 0 = off): fewer, persistent blocks
-  const int64_t fb_words = (c.n_global + 31) / 32;
-  const int cw = int(std::min<int64_t>(c.opt("bu_lds_kb", 0) * 256, std::min<int64_t>(fb_words, 36 * 1024)));
-  const int bs = 256;
-  if (cw > 0) {
-    grid = int(std::max<int64_t>(1, std::min<int64_t>((tiles + 4 * per_wave - 1) / (4 * per_wave),
-                                                      std::min<int64_t>(c.opt("bu_lds_grid", 512), kAggBlocks))));
-  }
-  auto* nb = reinterpret_cast<unsigned long long*>(nbits);
-  const int32_t* sc = es.slab_col.as<int32_t>();
-  const int64_t* trp = tr.row_ptr.as<int64_t>();
-  const int32_t* tc = tr.col.as<int32_t>();
-  const int nt = int(c.opt("bu_nt", 0));  // non-temporal slab / out-degree loads (keep L2 for the bitmap)
-  // lazy slab slots per round trip, and 64- / 16-entry chunks per step of a rest scan
-  const int lb = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_lazy", 3), kLazyMax)));
-  const int ru = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_unroll", 1), kRestMax)));
-  const int wpe = int(c.opt("bu_wpe", 8));
-#define NBG_BU_K(PKV, EV, WV, WP)                                                                      \
-  k_bu_slab<PKV, EV, 2, WV, WP><<<grid, bs, size_t(cw) * 4, c.stream>>>(sc, slab_w, es.slab_k, trp, tc, tr.n_rows, fb, \
-                                                                        nb, odeg, fp, partials, nt, pbits, cw, lb, ru)
-#define NBG_BU(PKV, EV, WV)                            \
-  switch (wpe) {                                       \
-    case 8: NBG_BU_K(PKV, EV, WV, 8); break;           \
-    case 7: NBG_BU_K(PKV, EV, WV, 7); break;           \
-    default: NBG_BU_K(PKV, EV, WV, 6); break;          \
-  }
-#define NBG_BU_W(EV)                      \
-  switch (fp.width) {                     \
-    case 1: NBG_BU(PK_FAST, EV, 1); break; \
-    case 2: NBG_BU(PK_FAST, EV, 2); break; \
-    case 4: NBG_BU(PK_FAST, EV, 4); break; \
-    default: NBG_BU(PK_FAST, EV, 8); break; \
-  }
-  if (pk == PK_FAST) {
-    switch (EG) {
-      case 1: NBG_BU_W(1); break;
-      case 2: NBG_BU_W(2); break;
-      default: NBG_BU_W(4); break;
-    }
-  } else {
-    switch (EG) {
-      case 2: NBG_BU(PK_NONE, 2, 0); break;
-      default: NBG_BU(PK_NONE, 1, 0); break;
-    }
-  }
-#undef NBG_BU_W
-#undef NBG_BU
-#undef NBG_BU_K
-  if (after_kernel) NBG_HIP(hipEventRecord(after_kernel, c.stream));
-  NBG_HIP(hipEventRecord(c.ev[7], c.stream));
-  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, out);
-  NBG_HIP(hipGetLastError());
-  char nm[96];
-  snprintf(nm, sizeof nm, "nbg::k_bu_slab<%d, %d, 2, %d, %d>", pk, pk == PK_FAST ? std::min(std::max(EG, 1), 4) : std::min(std::max(EG, 1), 2),
-           pk == PK_FAST ? int(fp.width) : 0, wpe == 8 || wpe == 7 ? wpe : 6);
-  c.bu_kernel_name = nm;
-  c.bu_rest_name.clear();
-  return grid;
-}
-// The per-query bucket masks of a packed predicate column (EdgeSpace::q_*): bucket b holds the
 // values min + [ceil(b * range / 2^bits), ceil((b + 1) * range / 2^bits) - 1]; it passes (fails)
 // when every value in it passes (fails) the compare, else the kernels read the exact value.
 QArgs make_qargs(const EdgeSpace& es, int pk, int fcol, const FastArgs& fp) {
@@ -2843,182 +1966,39 @@ QArgs make_qargs(const EdgeSpace& es, int pk, int fcol, const FastArgs& fp) {
   return q;
 }
 
-// bottom-up hop over the quad slab (k_bu_quad): persistent grid of 2 x 1024-thread blocks per
-// CU, each with an LDS copy of the frontier bitmap's first bu_pair_lds_kb KiB (the hubs).
-// Deferred (bu_pair_defer for a non-final hop, bu_pair_defer_final for the final one) the rows
-// pending after their 4 slots are left as bits and scanned by k_bu_rest_words, so the first pass
-// is one load -> probe round per tile.  Launches the kernels and the partials reduction into
-// out[0..8) (no synchronisation).
-int launch_bu_pair(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
-                   const FastArgs& fp, int fcol, unsigned long long* out, hipEvent_t after_kernel = nullptr) {
-  const Csr& tr = es.tr;
-  const bool fast = pk == PK_FAST;
-  const int EH = fast ? 2 : int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_pair_eh", 1), 2)));
-  bool defer = c.opt(odeg ? "bu_pair_defer" : "bu_pair_defer_final", 1) != 0;
-  const QArgs q = make_qargs(es, pk, fcol, fp);
-  const bool QP = fast && q.gbits && fcol == es.q_field && c.opt("bu_qpred", 1) != 0;
-  // 128-row units per lane-iteration (2 rows per lane each): 1 with eager prop halves
-  // (registers), else bu_pair_r (1 or 2)
-  const int R = fast && !QP ? 1 : int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_pair_r", 1), 2)));
-  unsigned long long* partials = c.ws_partials.as<unsigned long long>();
-  const int64_t fb_words = (c.n_global + 31) / 32;
-  const int cw = int(std::min<int64_t>(c.opt("bu_pair_lds_kb", 64) * 256, std::min<int64_t>(fb_words, 38 * 1024)));
-  const int64_t tiles = (tr.n_rows + 128 * R - 1) / (128 * R);
-  const int64_t waves_per_block = 16;
-  const int64_t gcap = std::min<int64_t>(c.opt("bu_pair_grid", 512), kAggBlocks / 2);
-  const int grid = int(std::max<int64_t>(1, std::min<int64_t>((tiles + waves_per_block - 1) / waves_per_block, gcap)));
-  int g1 = grid;  // blocks of the first pass (their partials come first)
-  const uint2* lo = es.pair_col[0].as<uint2>();
-  const uint2* hi = es.pair_col[1].as<uint2>();
-  const void* wlo = fast && fcol >= 0 ? es.pair_props[0][size_t(fcol)].p : nullptr;
-  const void* whi = fast && fcol >= 0 ? es.pair_props[1][size_t(fcol)].p : nullptr;
-  if (fast && !wlo) throw Error(NBG_E_DEVICE, "quad slab without the predicate column");
-  const int64_t* trp = tr.row_ptr.as<int64_t>();
-  const int32_t* tc = q.gbits ? es.tcol_q.as<int32_t>() : tr.col.as<int32_t>();
-  auto* nb = reinterpret_cast<unsigned long long*>(nbits);
-  const int ru = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_unroll", 1), kRestMax)));
-  const size_t shm = size_t(std::max(cw, 1)) * 4;  // s_fb[0] is read (unused) when cw = 0
-  unsigned long long* pbits = nullptr;
-  if (defer) {
-    c.ws_pend.ensure(size_t((tr.n_rows + 63) / 64 + 1) * 8);
-    pbits = c.ws_pend.as<unsigned long long>();
-  }
-  auto big_lds = [&](auto kern) {
-    if (shm > 48 * 1024)
-      lds_limit(reinterpret_cast<const void*>(kern), shm);
-  };
-  FastArgs fpd = fp;
-  fpd.width |= int32_t(c.opt("bu_pair_diag", 0) & 3) << 16;
-  auto go = [&](auto kern) {
-    big_lds(kern);
-    kern<<<grid, 1024, shm, c.stream>>>(lo, hi, wlo, whi, trp, tc, tr.n_rows, fb, nb, odeg, fpd, q, partials, cw, ru,
-                                        pbits);
-  };
-  int grid2 = 0;
-  const bool occ4 = c.opt("bu_rest_occ", 8) == 4;  // 128-VGPR rest pass: no spills, half the waves
-  auto rest = [&](auto kern) {
-    if (!defer) return;
-    NBG_HIP(hipEventRecord(c.ev[7], c.stream));  // end of the first pass
-    big_lds(kern);
-    grid2 = int(std::min<int64_t>(c.opt("bu_rest_grid", 512), kAggBlocks / 2));
-    // partials of the second pass sit behind the first pass's blocks: one reduction adds both
-    kern<<<grid2, 1024, shm, c.stream>>>(pbits, tr.n_rows, trp, tc, fb, nb, odeg, fp, q, partials + g1, cw, ru,
-                                         QP ? 0 : 4);
-  };
-  // the pipelined deferred kernel (k_bu_ring) for predicate-free and packed-predicate hops
-  const int ring_d = int(c.opt("bu_ring", 0));
-  const bool ring = defer && ring_d > 0 && (!fast || QP);
-  // one 1024-thread block per CU (4 waves per SIMD: the registers of D tiles in flight), so a
-  // block's LDS can hold more hub words
-  const int rcw = int(std::min<int64_t>(c.opt("bu_ring_lds_kb", 128) * 256, std::min<int64_t>(fb_words, 38 * 1024)));
-  const int rgrid = int(std::max<int64_t>(1, std::min<int64_t>(((tr.n_rows + 127) / 128 + waves_per_block - 1) / waves_per_block,
-                                                               std::min<int64_t>(c.opt("bu_ring_grid", 256), kAggBlocks / 2))));
-  const size_t rshm = size_t(std::max(rcw, 1)) * 4;
-  auto go_ring = [&](auto kern) {
-    if (rshm > 48 * 1024)
-      lds_limit(reinterpret_cast<const void*>(kern), rshm);
-    g1 = rgrid;
-    kern<<<rgrid, 1024, rshm, c.stream>>>(lo, hi, tr.n_rows, fb, nb, odeg, q, partials, rcw, pbits,
-                                          int(c.opt("bu_pair_diag", 0) & 3));
-  };
-#define NBG_RING(PKV, QPV)                                   \
-  switch (ring_d) {                                          \
-    case 1: go_ring(k_bu_ring<PKV, QPV, 1>); break;          \
-    case 2: go_ring(k_bu_ring<PKV, QPV, 2>); break;          \
-    case 3: go_ring(k_bu_ring<PKV, QPV, 3>); break;          \
-    default: go_ring(k_bu_ring<PKV, QPV, 4>); break;         \
-  }
-  const int sel = (defer ? 1 : 0) + (R == 2 ? 2 : 0);
-#define NBG_QR(PKV, W, QPV, EHV)                               \
-  switch (sel) {                                               \
-    case 0: go(k_bu_quad<PKV, W, QPV, 1, EHV, 0>); break;     \
-    case 1: go(k_bu_quad<PKV, W, QPV, 1, EHV, 1>); break;     \
-    case 2: go(k_bu_quad<PKV, W, QPV, 2, EHV, 0>); break;     \
-    default: go(k_bu_quad<PKV, W, QPV, 2, EHV, 1>); break;    \
-  }
-#define NBG_QF(W)                                                                                   \
-  {                                                                                                 \
-    if (QP) { NBG_QR(PK_FAST, W, 1, 2) }                                                            \
-    else if (defer) go(k_bu_quad<PK_FAST, W, 0, 1, 2, 1>);                                          \
-    else go(k_bu_quad<PK_FAST, W, 0, 1, 2, 0>);                                                     \
-    if (occ4) rest(k_bu_rest_words<PK_FAST, W, 4>); else rest(k_bu_rest_words<PK_FAST, W, 8>);     \
-  }
-  if (ring) {
-    if (fast) { NBG_RING(PK_FAST, 1) }
-    else { NBG_RING(PK_NONE, 0) }
-#define NBG_REST(PKV, W) \
-  if (occ4) rest(k_bu_rest_words<PKV, W, 4>); else rest(k_bu_rest_words<PKV, W, 8>);
-    if (fast) {
-      switch (fp.width) {
-        case 1: NBG_REST(PK_FAST, 1) break;
-        case 2: NBG_REST(PK_FAST, 2) break;
-        case 4: NBG_REST(PK_FAST, 4) break;
-        default: NBG_REST(PK_FAST, 8) break;
-      }
-    } else {
-      NBG_REST(PK_NONE, 0)
-    }
-#undef NBG_REST
-  } else if (fast) {
-    switch (fp.width) {
-      case 1: NBG_QF(1); break;
-      case 2: NBG_QF(2); break;
-      case 4: NBG_QF(4); break;
-      default: NBG_QF(8); break;
-    }
-  } else {
-    if (EH == 1) { NBG_QR(PK_NONE, 0, 0, 1) }
-    else { NBG_QR(PK_NONE, 0, 0, 2) }
-    if (occ4) rest(k_bu_rest_words<PK_NONE, 0, 4>);
-    else rest(k_bu_rest_words<PK_NONE, 0, 8>);
-  }
-#undef NBG_QR
-#undef NBG_RING
-#undef NBG_QF
-#undef NBG_QD
-  NBG_HIP(hipGetLastError());
-  if (!defer) NBG_HIP(hipEventRecord(c.ev[7], c.stream));
-  if (after_kernel) NBG_HIP(hipEventRecord(after_kernel, c.stream));
-  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, g1 + grid2, out);
-  NBG_HIP(hipGetLastError());
-  // rocprof names of the two passes (hop stats: bench.py matches them against kernel traces)
-  const int W = fast ? int(fp.width) : 0;
-  char nm[96];
-  if (ring)
-    snprintf(nm, sizeof nm, "nbg::k_bu_ring<%d, %d, %d>", pk, fast ? 1 : 0, std::min(std::max(ring_d, 1), 4));
-  else if (fast)
-    snprintf(nm, sizeof nm, "nbg::k_bu_quad<%d, %d, %d, %d, 2, %d>", pk, W, QP ? 1 : 0, QP ? R : 1, defer ? 1 : 0);
-  else
-    snprintf(nm, sizeof nm, "nbg::k_bu_quad<%d, 0, 0, %d, %d, %d>", pk, R, EH, defer ? 1 : 0);
-  c.bu_kernel_name = nm;
-  c.bu_slot_w = fast && !QP ? int(fp.width) : 0;
-  if (defer) {
-    snprintf(nm, sizeof nm, "nbg::k_bu_rest_words<%d, %d, %d>", pk, W, occ4 ? 4 : 8);
-    c.bu_rest_name = nm;
-  } else {
-    c.bu_rest_name.clear();
-  }
-  return g1 + grid2;
-}
-// bottom-up hop with the lean first pass (k_bu_lean) and the pending rows' rests in
-// k_bu_rest_words; counters reduced into out[0..8).  Returns false (nothing launched) when the
-// hop needs what the lean kernel does not do: a predicate that is not the packed column.
-bool launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
+// bottom-up hop: the first pass (k_bu_lean) over the quad slab and the pending rows' rests in
+// k_bu_rest_lean; counters reduced into out[0..8) (no synchronisation).  pk: PK_NONE (a
+// non-final hop: odeg keeps found rows with out-edges and sums their degrees) or PK_FAST (the
+// final hop's typed compare on transposed column fcol; decided from the packed buckets when fcol
+// is the packed column, else every value of a frontier hit is read by the rest pass).
+void launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
                     const FastArgs& fp, int fcol, unsigned long long* out, hipEvent_t after_kernel) {
   const Csr& tr = es.tr;
-  const bool fast = pk == PK_FAST;
-  if (pk != PK_NONE && pk != PK_FAST) return false;
-  if (!es.pair_col[0].p || (!fast && !odeg)) return false;
-  const QArgs q = make_qargs(es, pk, fcol, fp);
-  if (fast && !(q.gbits && fcol == es.q_field && c.opt("bu_qpred", 1) != 0)) return false;
+  if (pk != PK_NONE && pk != PK_FAST) throw Error(NBG_E_DEVICE, "bottom-up hop with a VM predicate");
+  if (!es.pair_col[0].p) throw Error(NBG_E_DEVICE, "bottom-up hop without the quad slab");
+  // the final hop (no odeg) runs the final-hop kernels; without a WHERE every bucket passes
+  const bool fast = pk == PK_FAST || !odeg;
+  QArgs q;
+  if (pk == PK_FAST) {
+    // bu_qpred = 0 (tests): ignore the buckets, every frontier hit reads its value
+    q = make_qargs(es, c.opt("bu_qpred", 1) != 0 ? pk : PK_NONE, fcol, fp);
+  } else {
+    q = make_qargs(es, PK_NONE, -1, fp);
+    if (fast) q.ulo = q.uhi = INT32_MAX, q.below = q.above = 1;
+  }
+  // rows pending after the slab rescan it only when a slot may be undecided (a predicate)
+  const int rest_from = pk == PK_FAST ? 0 : 4;
+  pk = fast ? PK_FAST : PK_NONE;
   const int64_t ntiles = (tr.n_rows + 127) / 128;
   const int64_t work = fast ? ntiles : std::min(ntiles, es.bu_live_tiles);
   const int U = c.opt(fast ? "bu_lean_u_final" : "bu_lean_u", 1) == 1 ? 1 : 2;
   const int64_t waves = std::max<int64_t>(1, (work + U - 1) / U);
   // hub words in LDS (bu_lean_lds_kb KiB, 0 = off): 1024-thread blocks, two per CU
   const int64_t fb_words = (c.n_global + 31) / 32;
+  // bu_hub_cap (tests): at most that many hub words, so small graphs exercise the L2 probes too
+  const int64_t hub_cap = std::max<int64_t>(0, c.opt("bu_hub_cap", 36 * 1024));
   const int cw = int(std::min<int64_t>(c.opt(fast ? "bu_lean_lds_kb_final" : "bu_lean_lds_kb", 64) * 256,
-                                       std::min<int64_t>(fb_words, 36 * 1024)));
+                                       std::min<int64_t>({fb_words, int64_t(36 * 1024), hub_cap})));
   const int bs = cw > 0 ? 1024 : 256;
   const int grid = int(std::max<int64_t>(
       1, std::min<int64_t>((waves + bs / 64 - 1) / (bs / 64),
@@ -3057,9 +2037,8 @@ bool launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
   const int ru = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_unroll", 1), kRestMax)));
   const int grid2 = int(std::min<int64_t>(c.opt("bu_rest_grid", 512), kAggBlocks / 2));
   const int W = fast ? int(fp.width) : 0;
-  const int rest_from = fast ? 0 : 4;  // the final hop re-reads undecided slots from the column
   const int rcw = int(std::min<int64_t>(c.opt(fast ? "bu_rest_lds_kb_final" : "bu_rest_lds_kb", fast ? 64 : 0) * 256,
-                                        std::min<int64_t>(fb_words, 36 * 1024)));
+                                        std::min<int64_t>({fb_words, int64_t(36 * 1024), hub_cap})));
   const size_t rshm = size_t(std::max(rcw, 1)) * 4;
   const int rsteps = int(std::max<int64_t>(1, c.opt("bu_rest_steps", 4)));
   auto rest = [&](auto kern) {
@@ -3092,98 +2071,18 @@ bool launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
   snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d>", pk, fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0,
            rcw > 0 ? 1 : 0);
   c.bu_rest_name = nm;
-  c.bu_slot_w = 0;
-  return true;
 }
 
-// Second pass of a deferred slab hop (h: the first pass's reduced counters on the host, h[3] =
-// pending rows).  Adds the rows it finds into h[0] / h[1] and its reads into h[4] / h[5], so the
-// counters read as one hop.  Synchronises once.
-void bu_finish(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
-               const FastArgs& fp, const unsigned long long* pbits, unsigned long long* h, unsigned long long* Kd) {
-  const int64_t P = int64_t(h[3]);
-  if (P <= 0) return;
-  const Csr& tr = es.tr;
-  DevBuf lst, deg, off;
-  lst.alloc(size_t(P + 64) * 4);
-  deg.alloc(size_t(P + 1) * 8);
-  off.alloc(size_t(P + 1) * 8);
-  NBG_HIP(hipMemsetAsync(Kd, 0, 8, c.stream));
-  k_bits_compact<0><<<grid_cap((tr.n_rows + 31) / 32, 4096, 4096), 1024, 0, c.stream>>>(
-      reinterpret_cast<const uint32_t*>(pbits), tr.n_rows, 0, nullptr, lst.as<int32_t>(), Kd);
-  k_rest_deg<<<grid_cap(P + 1), 256, 0, c.stream>>>(lst.as<int32_t>(), P, tr.row_ptr.as<int64_t>(), es.slab_k,
-                                                    deg.as<int64_t>());
-  exclusive_scan_dev<int64_t>(c, deg.as<int64_t>(), off.as<int64_t>(), P + 1);
-  unsigned long long* partials = c.ws_partials.as<unsigned long long>();
-  const int grid = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("rest_grid", 2048), kAggBlocks)));
-  if (pk == PK_FAST)
-    k_bu_rest<PK_FAST><<<grid, kThreads, 0, c.stream>>>(lst.as<int32_t>(), P, off.as<int64_t>(),
-                                                        tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), es.slab_k, fb,
-                                                        reinterpret_cast<unsigned long long*>(nbits), odeg, fp, partials);
-  else
-    k_bu_rest<PK_NONE><<<grid, kThreads, 0, c.stream>>>(lst.as<int32_t>(), P, off.as<int64_t>(),
-                                                        tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), es.slab_k, fb,
-                                                        reinterpret_cast<unsigned long long*>(nbits), odeg, fp, partials);
-  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, Kd + 1);
-  NBG_HIP(hipGetLastError());
-  NBG_HIP(hipMemcpyAsync(c.host_counters + 40, Kd, 8 * 6, hipMemcpyDeviceToHost, c.stream));
-  NBG_HIP(hipStreamSynchronize(c.stream));
-  if (int64_t(c.host_counters[40]) != P) throw Error(NBG_E_DEVICE, "bottom-up pending-row count mismatch");
-  const unsigned long long* r = c.host_counters + 41;
-  h[0] += r[0];
-  h[1] += r[1];
-  h[4] += r[2];
-  h[5] += r[3];
-}
-
-// byte models of a quad / ring hop's two passes from their counters.
-// First pass: slab words (4 B, + the predicate width when the values are loaded beside the
-// slots, c.bu_slot_w), the frontier bitmap once, the next-frontier and pending bits written,
-// the out-degree (4 B/row) at a non-final hop.  Rest pass: a row_ptr pair per pending row,
-// 4 B per entry read, predicate values read.
-uint64_t bu_first_bytes(const Ctx& c, const unsigned long long* h, int64_t n_rows, bool with_odeg) {
-  if (c.bu_rest_name.empty() && c.bu_kernel_name.rfind("nbg::k_bu_slab", 0) == 0) return 0;  // slab model below
-  return h[2] * (4 + uint64_t(c.bu_slot_w)) + 2 * (uint64_t(n_rows) / 8) +
-         (c.bu_rest_name.empty() ? 0 : uint64_t(n_rows) / 8) + (with_odeg ? uint64_t(n_rows) * 4 : 0);
+// byte models of a bottom-up hop's two passes from their counters.
+// First pass: 4 B per slab word read, the frontier bitmap once, the next-frontier and pending
+// bits written, the out-degree (4 B/row) at a non-final hop.  Rest pass: a row_ptr pair per
+// pending row, 4 B per entry read, predicate values read.
+uint64_t bu_first_bytes(const unsigned long long* h, int64_t n_rows, bool with_odeg) {
+  return h[2] * 4 + 3 * (uint64_t(n_rows) / 8) + (with_odeg ? uint64_t(n_rows) * 4 : 0);
 }
 uint64_t bu_rest_bytes(const unsigned long long* h, int pred_width) {
   return h[3] * 16 + h[4] * 4 + h[5] * uint64_t(pred_width);
 }
-// byte model of one slab hop from its counters
-uint64_t bu_slab_bytes(const unsigned long long* h, int64_t n_rows, int pred_width, bool with_odeg) {
-  return h[2] * (4 + uint64_t(pred_width)) + h[3] * 16 + h[4] * 4 + h[5] * uint64_t(pred_width) +
-         uint64_t(n_rows) / 8 + (with_odeg ? uint64_t(n_rows) * 4 : 0);
-}
-
-// bottom-up launch (timed like the expansion); returns adjacency entries examined
-uint64_t launch_bottom_up(Ctx& c, EdgeSpace& es, const uint32_t* fbits, uint8_t* map, int pk, const FastArgs& fp,
-                          unsigned long long* d_examined) {
-  const Csr& tr = es.tr;
-  NBG_HIP(hipMemsetAsync(d_examined, 0, 8, c.stream));
-  int grid = grid_cap(tr.n_rows, 256, int(c.opt("bu_grid", 256 * 16)));
-  hipEventRecord(c.ev[2], c.stream);
-  if (pk == PK_FAST)
-    k_bottom_up<PK_FAST><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows,
-                                                     c.owned_lo(), fbits, map, fp, d_examined);
-  else
-    k_bottom_up<PK_NONE><<<grid, 256, 0, c.stream>>>(tr.row_ptr.as<int64_t>(), tr.col.as<int32_t>(), tr.n_rows,
-                                                     c.owned_lo(), fbits, map, fp, d_examined);
-  NBG_HIP(hipGetLastError());
-  hipEventRecord(c.ev[3], c.stream);
-  uint64_t ex = 0;
-  NBG_HIP(hipMemcpyAsync(&ex, d_examined, 8, hipMemcpyDeviceToHost, c.stream));
-  NBG_HIP(hipEventSynchronize(c.ev[3]));
-  float ms = 0;
-  hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
-  c.timing.expand_ms += ms;
-  c.timing.expand_launches++;
-  c.timing.bu_steps++;
-  // byte model: row_ptr 8 B/row, frontier bitmap once, examined entries (col + predicate), mark
-  c.timing.expand_bytes += uint64_t(tr.n_rows) * 9 + uint64_t(tr.n_rows) / 8 +
-                           ex * (4 + uint64_t(pk == PK_FAST ? fp.width : 0));
-  return ex;
-}
-
 // algorithmic bytes of one expansion (DESIGN.md "byte model"): frontier id 4 B + row_ptr pair
 // 16 B + off 8 B per frontier entry; per edge: col 4 B (+ predicate column width) + the
 // output it makes (1 B map mark, or 12 B row, or 1 B flag).
@@ -3477,35 +2376,18 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // bottom-up: frontier bitmap in, next frontier bitmap out
       const Csr& tr = es.tr;
       const uint32_t* fb = global_bits(c, bitsA);
-      const bool defer = c.opt("bu_defer", 0) != 0;
-      DevBuf pb;
-      if (defer) pb.alloc(size_t((tr.n_rows + 63) / 64 + 1) * 8);
       hipEventRecord(c.ev[2], c.stream);
-      const int64_t bk = c.opt("bu_kernel", 2);
-      if (!defer && bk == 2 &&
-          launch_bu_lean(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, K.d, c.ev[6])) {
-      } else if (!defer && bk >= 1 && es.pair_col[0].p)
-        launch_bu_pair(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, K.d, c.ev[6]);
-      else
-        launch_bu_slab(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, nullptr, K.d,
-                       defer ? pb.as<unsigned long long>() : nullptr, c.ev[6]);
-      if (!defer) hipEventRecord(c.ev[3], c.stream);
+      launch_bu_lean(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, K.d, c.ev[6]);
+      hipEventRecord(c.ev[3], c.stream);
       NBG_HIP(hipMemcpyAsync(K.h, K.d, 64, hipMemcpyDeviceToHost, c.stream));
       NBG_HIP(hipStreamSynchronize(c.stream));
-      if (defer) {
-        bu_finish(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, pb.as<unsigned long long>(), K.h,
-                  K.d + 40);
-        hipEventRecord(c.ev[3], c.stream);
-        NBG_HIP(hipEventSynchronize(c.ev[3]));
-      }
       float ms = 0, kms = 0;
       hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
       hipEventElapsedTime(&kms, c.ev[2], c.ev[7]);
       c.timing.expand_ms += ms;
       c.timing.expand_launches++;
       c.timing.bu_steps++;
-      uint64_t kb = bu_first_bytes(c, K.h, tr.n_rows, true), hb = kb + bu_rest_bytes(K.h, 0);
-      if (kb == 0) kb = hb = bu_slab_bytes(K.h, tr.n_rows, 0, true);
+      const uint64_t kb = bu_first_bytes(K.h, tr.n_rows, true), hb = kb + bu_rest_bytes(K.h, 0);
       c.timing.expand_bytes += hb;
       c.timing.hop(1, false, ms, K.h, kms, kb);
       c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name);
@@ -3611,27 +2493,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         const Csr& tr = es.tr;
         NBG_HIP(hipMemsetAsync(K.d, 0, 8, c.stream));
         const uint32_t* fb = global_bits(c, bitsA);
-        const void* slab_w = pk == PK_FAST ? es.slab_props[size_t(fpk.col)].p : nullptr;
-        const bool defer = c.opt("bu_defer", 0) != 0;
-        DevBuf pb;
-        if (defer) pb.alloc(size_t((tr.n_rows + 63) / 64 + 1) * 8);
         hipEventRecord(c.ev[2], c.stream);
-        const int64_t bk = c.opt("bu_kernel", 2);
-        if (!defer && bk == 2 &&
-            launch_bu_lean(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8, c.ev[6])) {
-        } else if (!defer && bk >= 1 && es.pair_col[0].p &&
-                   (pk != PK_FAST || es.pair_props[0][size_t(fpk.col)].p))
-          launch_bu_pair(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8, c.ev[6]);
-        else
-          launch_bu_slab(c, es, fb, bitsB, nullptr, pk, tfp, slab_w, K.d + 8,
-                         defer ? pb.as<unsigned long long>() : nullptr, c.ev[6]);
-        unsigned long long h2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (defer) {
-          NBG_HIP(hipMemcpyAsync(K.h + 8, K.d + 8, 64, hipMemcpyDeviceToHost, c.stream));
-          NBG_HIP(hipStreamSynchronize(c.stream));
-          memcpy(h2, K.h + 8, sizeof(h2));
-          bu_finish(c, es, fb, bitsB, nullptr, pk, tfp, pb.as<unsigned long long>(), h2, K.d + 40);
-        }
+        launch_bu_lean(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8, c.ev[6]);
         k_bits_compact<1><<<grid_cap((tr.n_rows + 31) / 32, 4096, 4096), 1024, 0, c.stream>>>(
             bitsB, tr.n_rows, lo, c.vid_of.as<int64_t>(), vids.p, K.d);
         NBG_HIP(hipGetLastError());
@@ -3645,10 +2508,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         c.timing.expand_launches++;
         c.timing.bu_steps++;
         nrows = int64_t(K.h[0]);
-        if (defer) memcpy(K.h + 8, h2, sizeof(h2));
         const int pw = pk == PK_FAST ? tfp.width : 0;
-        uint64_t kb = bu_first_bytes(c, K.h + 8, tr.n_rows, false), hb = kb + bu_rest_bytes(K.h + 8, pw);
-        if (kb == 0) kb = hb = bu_slab_bytes(K.h + 8, tr.n_rows, pw, false);
+        const uint64_t kb = bu_first_bytes(K.h + 8, tr.n_rows, false), hb = kb + bu_rest_bytes(K.h + 8, pw);
         // + the DISTINCT _dst output (k_bits_compact<1>): next bits once, vid_of read + vid written
         c.timing.expand_bytes += hb + uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
         c.timing.hop(1, true, ms, K.h + 8, kms, kb);

@@ -129,6 +129,7 @@ class GraphSpace:
     def __init__(self, num_parts: int, device: int = 0, rank: int = 0, world_size: int = 1):
         self.L = _lib.load()
         self.num_parts, self.rank, self.world_size = num_parts, rank, world_size
+        self._options: set[str] = set()
         self.h = self.L.nbg_ctx_create(device, num_parts, rank, world_size)
         if not self.h:
             raise RuntimeError("nbg_ctx_create failed: no MI355X visible or bad arguments "
@@ -186,6 +187,17 @@ class GraphSpace:
 
     def set_option(self, key: str, value: int):
         self._check(self.L.nbg_set_option(self.h, key.encode(), int(value)))
+        self._options.add(key)
+
+    def unset_option(self, key: str):
+        """back to the engine's default for key"""
+        self._check(self.L.nbg_set_option(self.h, key.encode(), -(1 << 63)))
+        self._options.discard(key)
+
+    def reset_options(self):
+        """every option set through this handle back to the engine default"""
+        for k in list(self._options):
+            self.unset_option(k)
 
     # ---- schema + snapshot -----------------------------------------------------------
     def set_edge_schema(self, edge_type: int, fields: Sequence[tuple[str, int]], ver: int = 0):
@@ -429,6 +441,8 @@ class QueryBoundProcessor:
             parts += [p] * len(vs)
             vids += list(vs)
         cols = [(c.name, c.owner, c.tag_id) for c in req.return_columns]
+        # scanned as given for both bound types (QueryBaseProcessor.inl:39-40; the client negates for
+        # in-bound, StorageClient.cpp:116) -- INTEGRATION.md's GpuBoundProcessor stub does the same
         et = req.edge_type
         rs = self.space.get_bound(et, parts, vids, cols, req.filter)
         rows = rs.rows()

@@ -251,10 +251,12 @@ static std::vector<int64_t> go_frontier(const ora_rmat_graph* g, const int64_t* 
 
 extern "C" {
 
-// GO steps FROM starts OVER the RMAT edge type [WHERE weight > where_gt] YIELD _dst [DISTINCT].
+// GO steps FROM starts OVER the RMAT edge type [WHERE weight <op> k] YIELD _dst [DISTINCT].
+// has_where: 0 no WHERE, else the relational operator of RelationalExpression (Expressions.cpp:
+// 891-933, INT operands): 1 >, 2 >=, 3 <, 4 <=, 5 ==, 6 !=.
 // Writes the result vids sorted ascending into *out (malloc'd, ora_free) and returns their count.
 int64_t ora_rmat_graph_go(const ora_rmat_graph* g, const int64_t* starts, size_t n_starts, int32_t steps,
-                          int32_t has_where, int64_t where_gt, int32_t distinct, int32_t threads,
+                          int32_t has_where, int64_t where_k, int32_t distinct, int32_t threads,
                           int64_t** out, uint64_t* edges_scanned) {
   if (threads < 1) threads = 1;
   *out = nullptr;
@@ -265,7 +267,18 @@ int64_t ora_rmat_graph_go(const ora_rmat_graph* g, const int64_t* starts, size_t
   *edges_scanned = scanned;
   if (F.empty()) return 0;
   // final hop: rows (u, v) passing WHERE; YIELD _dst
-  auto pass = [&](int64_t su, int64_t dv) { return !has_where || rmatWeight(su, dv, g->seed) > where_gt; };
+  auto pass = [&](int64_t su, int64_t dv) {
+    if (!has_where) return true;
+    const int64_t w = rmatWeight(su, dv, g->seed);
+    switch (has_where) {
+      case 1: return w > where_k;
+      case 2: return w >= where_k;
+      case 3: return w < where_k;
+      case 4: return w <= where_k;
+      case 5: return w == where_k;
+      default: return w != where_k;
+    }
+  };
   std::vector<int64_t> res;
   if (distinct) {
     std::fill(mark.begin(), mark.end(), uint8_t(0));

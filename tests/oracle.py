@@ -407,15 +407,20 @@ class RmatGraph:
         lib().ora_rmat_graph_info(self.h, C.byref(nv), C.byref(ne))
         return {"num_vertices": nv.value, "num_edges": ne.value}
 
-    def go(self, starts, steps, where_gt=None, distinct=False):
-        """sorted int64 result vids of GO steps [WHERE weight > where_gt] YIELD _dst [DISTINCT]
-        and the edges scanned (rows the storage returned over all hops)"""
+    OPS = {">": 1, ">=": 2, "<": 3, "<=": 4, "==": 5, "!=": 6}
+
+    def go(self, starts, steps, where_gt=None, distinct=False, where=None):
+        """sorted int64 result vids of GO steps [WHERE weight > where_gt | WHERE weight <op> k for
+        where=(op, k)] YIELD _dst [DISTINCT] and the edges scanned (rows the storage returned
+        over all hops)"""
         starts = np.ascontiguousarray(starts, dtype=np.int64)
         out = C.POINTER(C.c_int64)()
         scanned = C.c_uint64()
-        n = lib().ora_rmat_graph_go(self.h, _ptr(starts), len(starts), steps, int(where_gt is not None),
-                                    int(where_gt or 0), int(distinct), self.threads, C.byref(out),
-                                    C.byref(scanned))
+        op, k = (0, 0) if where_gt is None else (1, where_gt)
+        if where is not None:
+            op, k = self.OPS[where[0]], where[1]
+        n = lib().ora_rmat_graph_go(self.h, _ptr(starts), len(starts), steps, op, int(k), int(distinct),
+                                    self.threads, C.byref(out), C.byref(scanned))
         try:
             res = np.ctypeslib.as_array(out, shape=(n,)).copy() if n > 0 else np.zeros(0, dtype=np.int64)
         finally:

@@ -478,109 +478,82 @@ def test_rmat_direction_modes_agree(rmat12, force):
         sp.set_option("bu_force", 0)
 
 
-@pytest.mark.parametrize("slab,order", [(0, 1), (1, 1), (3, 1), (4, 0)])
-def test_rmat_bottom_up_slab_widths(slab, order):
-    """the bottom-up slab (first K hub-first entries per transposed row) with its fallback scan
-    gives the oracle's results for any K, with and without the final-hop predicate"""
-    st = oracle_rmat(10)
-    sp = GraphSpace(64)
-    sp.set_option("bu_slab", slab)
-    sp.set_option("degree_order", order)
-    sp.set_edge_schema(FOLLOW, [("weight", O.INT)])
-    sp.gen_rmat(10, 16, SEED, FOLLOW)
-    sp.finalize()
-    sp.set_option("bu_force", 1)
-    starts = sorted(set(seeds_from(10, 24, seed=4)))
-    for k in (0, 499, 900):
+@pytest.fixture(autouse=True)
+def _reset_rmat12_options(request):
+    """rmat12 is module-scoped: engine options a test sets on it end with that test"""
+    yield
+    if "rmat12" in request.fixturenames:
+        request.getfixturevalue("rmat12")[0].reset_options()
+
+
+def final_bu_kernels(sp):
+    """rocprof names of the last query's final bottom-up hop (dominant first)"""
+    hops = [h for h in sp.last_timing()["hops"] if h["mode"] == "bottom-up" and h["final"]]
+    assert hops, "the final hop did not run bottom-up"
+    return hops[-1]["kernels"]
+
+
+@pytest.mark.parametrize("u,lds,rest_lds,rsteps,unroll,cap", [(1, 64, 64, 4, 1, 36 * 1024), (2, 64, 0, 1, 2, 36 * 1024),
+                                                              (1, 0, 64, 2, 1, 36 * 1024), (2, 1, 1, 4, 2, 8)])
+def test_rmat_bottom_up_shapes(rmat12, u, lds, rest_lds, rsteps, unroll, cap):
+    """the bottom-up kernels (k_bu_lean first pass + k_bu_rest_lean) for every tile / LDS hub /
+    rest-chunk shape, non-final and final hops, thresholds that leave rows pending past the slab,
+    against the oracle; the hop stats name the kernels that ran"""
+    sp, st = rmat12
+    for k, v in {"bu_force": 1, "bu_lean_u": u, "bu_lean_u_final": u, "bu_lean_lds_kb": lds,
+                 "bu_lean_lds_kb_final": lds, "bu_rest_lds_kb": rest_lds, "bu_rest_lds_kb_final": rest_lds,
+                 "bu_rest_steps": rsteps, "bu_unroll": unroll, "bu_hub_cap": cap}.items():
+        sp.set_option(k, v)
+    starts = sorted(set(seeds_from(12, 48, seed=23)))
+    pending = 0
+    for k in (0, 499, 990):
         w = X.AliasProp("follow", "weight") > k
-        for steps in (1, 2, 3):
+        for steps in (2, 3):
             g = sp.go(starts, steps, FOLLOW, where=w, yields=[X.EdgeDst("follow")], distinct=True)
-            r = st.go(starts, steps, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()], distinct=True)
-            assert np.array_equal(np.sort(g.columns[0]), np.sort(r.int_col(0)))
-            assert g.edges_scanned == r.edges_scanned
-    assert sp.last_timing()["bu_steps"] > 0
-    sp.close()
+            r_ = st.go(starts, steps, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()], distinct=True)
+            assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
+            assert g.edges_scanned == r_.edges_scanned
+            ks = final_bu_kernels(sp)
+            assert ks[0] == f"nbg::k_bu_lean<1, {u}, {1 if lds else 0}>", ks
+            assert ks[1].startswith("nbg::k_bu_rest_lean<1, "), ks
+            pending += sum(h["c"][3] for h in sp.last_timing()["hops"] if h["mode"] == "bottom-up")
+    assert pending > 0  # the rest pass had rows to scan
+    # DISTINCT _dst without WHERE: the final-hop kernels with every bucket passing
+    g = sp.go(starts, 3, FOLLOW, yields=[X.EdgeDst("follow")], distinct=True)
+    r_ = st.go(starts, 3, FOLLOW, yields=[X.EdgeDst("follow").encode()], distinct=True)
+    assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
+    assert final_bu_kernels(sp)[0] == f"nbg::k_bu_lean<1, {u}, {1 if lds else 0}>"
+    g = sp.go(starts, 3, FOLLOW)
+    r_ = st.go(starts, 3, FOLLOW)
+    assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
+    hops = [h for h in sp.last_timing()["hops"] if h["mode"] == "bottom-up"]
+    assert hops and hops[0]["kernels"][0] == f"nbg::k_bu_lean<0, {u}, {1 if lds else 0}>"
 
 
-@pytest.mark.parametrize("defer,r,eager", [(1, 2, 4), (0, 2, 4), (1, 1, 1), (1, 4, 2), (0, 4, 1)])
-def test_rmat_bottom_up_rest_pass(rmat12, defer, r, eager):
-    """rows that outlive the slab: the deferred edge-balanced second pass (k_bu_rest) and the
-    inline wave scan agree with the oracle for every lane/slot shape of k_bu_slab"""
-    sp, st = rmat12
-    opts = {"bu_force": 1, "bu_defer": defer, "bu_r": r, "bu_eager_fast": eager, "bu_eager": min(eager, 2),
-            "bu_kernel": 0}
-    for k, v in opts.items():
-        sp.set_option(k, v)
-    try:
-        starts = sorted(set(seeds_from(12, 48, seed=21)))
-        for k in (0, 499, 990):
-            w = X.AliasProp("follow", "weight") > k
-            for steps in (2, 3):
-                g = sp.go(starts, steps, FOLLOW, where=w, yields=[X.EdgeDst("follow")], distinct=True)
-                r_ = st.go(starts, steps, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()],
-                           distinct=True)
-                assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
-                assert g.edges_scanned == r_.edges_scanned
-                hops = sp.last_timing()["hops"]
-                assert any(h["mode"] == "bottom-up" for h in hops)
-        # the high threshold leaves rows pending past the slab, so the rest pass really ran
-        assert any(h["mode"] == "bottom-up" and h["c"][3] > 0 for h in hops)
-    finally:
-        for k, v in {"bu_force": 0, "bu_defer": 0, "bu_r": 2, "bu_eager_fast": 1, "bu_eager": 1, "bu_kernel": 1}.items():
-            sp.set_option(k, v)
-
-
-@pytest.mark.parametrize("defer,defer_final,eh,lds,r,occ", [(1, 0, 1, 64, 2, 8), (1, 1, 2, 64, 1, 4),
-                                                         (0, 1, 2, 16, 2, 8), (0, 0, 1, 0, 1, 8),
-                                                         (1, 1, 1, 0, 2, 4)])
-def test_rmat_bottom_up_quad_shapes(rmat12, defer, defer_final, eh, lds, r, occ):
-    """the quad-slab bottom-up kernel (k_bu_quad + k_bu_rest_words) for every row / half /
-    LDS-cache / deferral shape, with and without the final-hop predicate, against the oracle"""
-    sp, st = rmat12
-    opts = {"bu_force": 1, "bu_kernel": 1, "bu_pair_defer": defer, "bu_pair_defer_final": defer_final,
-            "bu_pair_eh": eh, "bu_pair_lds_kb": lds, "bu_pair_r": r, "bu_rest_occ": occ}
-    for k, v in opts.items():
-        sp.set_option(k, v)
-    try:
-        starts = sorted(set(seeds_from(12, 48, seed=23)))
-        for k in (0, 499, 990):
-            w = X.AliasProp("follow", "weight") > k
-            for steps in (2, 3):
-                g = sp.go(starts, steps, FOLLOW, where=w, yields=[X.EdgeDst("follow")], distinct=True)
-                r_ = st.go(starts, steps, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()],
-                           distinct=True)
-                assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
-                assert g.edges_scanned == r_.edges_scanned
-        g = sp.go(starts, 3, FOLLOW)
-        r_ = st.go(starts, 3, FOLLOW)
-        assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
-    finally:
-        for k, v in {"bu_force": 0, "bu_pair_defer": 1, "bu_pair_defer_final": 0, "bu_pair_eh": 1,
-                     "bu_pair_lds_kb": 64, "bu_pair_r": 1, "bu_rest_occ": 8}.items():
-            sp.set_option(k, v)
+OPS = {">": lambda c, k: c > k, ">=": lambda c, k: c >= k, "<": lambda c, k: c < k, "<=": lambda c, k: c <= k,
+       "==": lambda c, k: c.eq(k), "!=": lambda c, k: c.ne(k)}
 
 
 @pytest.mark.parametrize("qpred", [1, 0])
-def test_rmat_bottom_up_packed_predicate(rmat12, qpred):
-    """the quantised predicate (slot words carry the bucket of follow.weight): every compare op,
-    constants below, inside, on the edges of and above the value range, deferred and inline rest
-    scans; bu_qpred=0 reads every value instead (same words, gidx masked)"""
+@pytest.mark.parametrize("hub_cap", [36 * 1024, 16])
+def test_rmat_bottom_up_packed_predicate(rmat12, qpred, hub_cap):
+    """the shipped final bottom-up hop (k_bu_lean<1,..> + k_bu_rest_lean<1,..>, asserted by name)
+    with the quantised predicate (slot words carry the bucket of follow.weight): every compare op,
+    constants below, inside, on the edges of and above the value range; bu_qpred=0 reads every
+    value of a frontier hit instead (the path a predicate on an unpacked column takes); hub_cap
+    16 leaves all but the first 512 vertices to the global (L2) probe branch"""
     sp, st = rmat12
     starts = sorted(set(seeds_from(12, 48, seed=29)))
     wcol = X.AliasProp("follow", "weight")
-    try:
-        sp.set_option("bu_force", 1)
-        sp.set_option("bu_qpred", qpred)
-        for dfin in (0, 1):
-            sp.set_option("bu_pair_defer_final", dfin)
-            for k in (-5, 0, 1, 3, 4, 255, 499, 500, 998, 999, 1000, 5000):
-                for w in (wcol > k, wcol >= k, wcol < k, wcol <= k, wcol.eq(k), wcol.ne(k)):
-                    g = sp.go(starts, 2, FOLLOW, where=w, yields=[X.EdgeDst("follow")], distinct=True)
-                    r_ = st.go(starts, 2, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()],
-                               distinct=True)
-                    assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0))), (k, w)
-                    assert g.edges_scanned == r_.edges_scanned
-                    assert any(h["mode"] == "bottom-up" and h["final"] for h in sp.last_timing()["hops"])
-    finally:
-        for k, v in {"bu_force": 0, "bu_qpred": 1, "bu_pair_defer_final": 0}.items():
-            sp.set_option(k, v)
+    sp.set_option("bu_force", 1)
+    sp.set_option("bu_qpred", qpred)
+    sp.set_option("bu_hub_cap", hub_cap)
+    for k in (-5, 0, 1, 3, 4, 255, 499, 500, 998, 999, 1000, 5000):
+        for op, mk in OPS.items():
+            w = mk(wcol, k)
+            g = sp.go(starts, 2, FOLLOW, where=w, yields=[X.EdgeDst("follow")], distinct=True)
+            r_ = st.go(starts, 2, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()], distinct=True)
+            assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0))), (k, op)
+            assert g.edges_scanned == r_.edges_scanned
+            ks = final_bu_kernels(sp)
+            assert ks[0].startswith("nbg::k_bu_lean<1, ") and ks[1].startswith("nbg::k_bu_rest_lean<1, "), ks

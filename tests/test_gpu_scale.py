@@ -89,6 +89,38 @@ def test_where_thresholds_rmat20(rmat20, k):
         assert r.edges_scanned == scanned
 
 
+OPS = {">": lambda c, k: c > k, ">=": lambda c, k: c >= k, "<": lambda c, k: c < k, "<=": lambda c, k: c <= k,
+       "==": lambda c, k: c.eq(k), "!=": lambda c, k: c.ne(k)}
+
+
+@pytest.mark.parametrize("hub_cap", [None, 1024])
+@pytest.mark.parametrize("op", list(OPS))
+def test_every_operator_default_path_rmat20(rmat20, op, hub_cap):
+    """the shipped final bottom-up hop (asserted by kernel name) for every relational operator at
+    the bucket edges of weight's range -- GO 3 STEPS ... YIELD DISTINCT _dst against the
+    index-space oracle; with the LDS hub window capped at 1024 words (32 K vertices) most probes
+    take the global (L2) branch"""
+    sp, g = rmat20
+    starts = synth.seeds(20, 16, 1, 64)
+    wcol = X.AliasProp("follow", "weight")
+    if hub_cap:
+        sp.set_option("bu_hub_cap", hub_cap)
+    l2_probes = 0
+    try:
+        for k in (0, 15, 16, 499, 998, 999):
+            r = sp.go(starts, 3, FOLLOW, where=OPS[op](wcol, k), yields=[X.EdgeDst("follow")], distinct=True)
+            want, scanned = g.go(starts, 3, distinct=True, where=(op, k))
+            assert np.array_equal(np.sort(r.columns[0]), want), (op, k)
+            assert r.edges_scanned == scanned
+            hops = sp.last_timing()["hops"]
+            assert hops[-1]["mode"] == "bottom-up" and hops[-1]["final"]
+            assert hops[-1]["kernels"][0].startswith("nbg::k_bu_lean<1, "), hops[-1]["kernels"]
+            l2_probes += hops[-1]["c"][6]
+    finally:
+        sp.unset_option("bu_hub_cap")
+    assert l2_probes > 0 or not hub_cap  # first-pass probes answered by L2
+
+
 def test_bench_query_rmat20_faithful_oracle(rmat20):
     """the same query against the faithful storaged + graphd restatement (KV store, processors)"""
     sp, _ = rmat20

@@ -42,6 +42,23 @@ def test_go_distinct_where_matches_faithful(both, steps):
     assert scanned == r.edges_scanned
 
 
+@pytest.mark.parametrize("op", [">", ">=", "<", "<=", "==", "!="])
+def test_go_distinct_every_operator_matches_faithful(both, op):
+    """every relational operator (Expressions.cpp:891-933) at constants below, on the edges of,
+    inside and above the weight range [0, 999]"""
+    scale, st, g = both
+    starts = synth.seeds(scale, 16, 1, 48)
+    wcol = X.AliasProp("follow", "weight")
+    mk = {">": lambda k: wcol > k, ">=": lambda k: wcol >= k, "<": lambda k: wcol < k,
+          "<=": lambda k: wcol <= k, "==": lambda k: wcol.eq(k), "!=": lambda k: wcol.ne(k)}[op]
+    for k in (-5, 0, 499, 998, 999, 1000):
+        w = mk(k)
+        r = st.go(starts, 2, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()], distinct=True)
+        got, scanned = g.go(starts, 2, distinct=True, where=(op, k))
+        assert np.array_equal(got, np.sort(r.int_col(0))), (op, k)
+        assert scanned == r.edges_scanned
+
+
 @pytest.mark.parametrize("steps", [1, 2, 3])
 def test_go_plain_rows_match_faithful(both, steps):
     scale, st, g = both

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run the bench query a few times with engine options (profiling driver, GPU box only).
 
-    rocprofv3 --kernel-trace --stats -d gpurun_out/p -- python3 tools/run_query.py --option bu_pair_defer=0
+    rocprofv3 --kernel-trace --stats -d gpurun_out/p -- python3 tools/run_query.py --option bu_rest_steps=2
 
 The graph build happens before the timed queries; rocprof summaries of the run include both, so
 tools/profile_summary.py separates query kernels from build kernels by call count."""

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Option sweep of the GO benchmark query on one graph build (tuning aid, GPU box only).
 
-    python tools/sweep.py --scale 26 --config bu_r=1,bu_eager_fast=2 --config bu_nt=1 ...
+    python tools/sweep.py --scale 26 --config bu_lean_u_final=2 --config bu_rest_steps=2 ...
 
 Each --config is a comma list of engine options applied on top of the defaults; every config
 runs the BASELINE query `reps` times and prints one JSON line (median ms, hop stats)."""
@@ -14,16 +14,6 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
-
-# engine defaults of the swept options (traverse.hip / snapshot.hip), restored after each config
-DEFAULTS = {"bu_r": 2, "bu_eager_fast": 1, "bu_eager": 1, "bu_nt": 0, "bu_defer": 0, "bu_grid": 4096,
-            "bu_tiles_per_wave": 4, "bu_lds_kb": 0, "bu_lds_grid": 512, "bu_div": 4, "bu_slab": 4,
-            "bu_lazy": 3, "bu_unroll": 1, "bu_wpe": 8, "bu_kernel": 2, "bu_lean_u": 1, "bu_lean_grid": 2048, "bu_lean_lds_kb": 64, "bu_lean_lds_kb_final": 64, "bu_lean_u_final": 1, "bu_rest_lds_kb": 0, "bu_rest_lds_kb_final": 64, "bu_rest_steps": 4, "bu_pair_eh": 1,
-            "bu_pair_lds_kb": 64, "bu_pair_grid": 512, "bu_pair_defer": 1, "bu_pair_defer_final": 1,
-            "bu_rest_grid": 512, "bu_pair_r": 1, "bu_rest_occ": 8, "bu_qpred": 1, "bu_pair_diag": 0,
-            "bu_ring": 0, "bu_ring_lds_kb": 128, "bu_ring_grid": 256, "fuse_dst": 1, "mark_check": 0,
-            "expand_grid": 2048, "rest_grid": 2048}
-
 
 def main():
     ap = argparse.ArgumentParser()
@@ -52,7 +42,6 @@ def main():
     for _ in range(args.reps):
         for cfg in cfgs:
             opts = dict(kv.split("=") for kv in cfg.split(",") if kv)
-            saved = {k: DEFAULTS.get(k, 0) for k in opts}
             for k, v in opts.items():
                 sp.set_option(k, int(v))
             t = time.perf_counter()
@@ -63,8 +52,7 @@ def main():
             hop_ms[cfg].append([h["ms"] for h in tm["hops"]])
             kern_ms.setdefault(cfg, []).append([h["kernel_ms"] for h in tm["hops"]])
             res[cfg] = (r.n_rows, r.edges_scanned, tm)
-            for k, v in saved.items():
-                sp.set_option(k, v)
+            sp.reset_options()  # engine defaults again
     ref = res[""][0]
     for cfg in cfgs:
         rows, edges, tm = res[cfg]
