@@ -1629,7 +1629,7 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
     t.props.push_back(std::move(q));
   }
   t.row_ptr.alloc(size_t(t.n_rows + 1) * 8);
-  t.col.alloc(size_t(R + 1) * 4);
+  t.col.alloc(size_t(R) * 4 + 64);  // padded: the rest passes load whole aligned 16-byte groups
   DevBuf perm;
   perm.alloc(size_t(R + 1) * 4);
   if (R) {
@@ -1695,7 +1695,7 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
       es.q_bits = qb;
       es.q_min = h[0];
       es.q_range = uint64_t(h[1]) - uint64_t(h[0]) + 1;  // 0 = the whole 2^64 range
-      es.tcol_q.alloc(size_t(R) * 4 + 16);
+      es.tcol_q.alloc(size_t(R) * 4 + 64);
       k_pack_col<<<grid_for(R), 256, 0, c.stream>>>(t.col.as<int32_t>(), pc.data.p, pc.width, R, es.q_min, es.q_range,
                                                    gb, qb, es.tcol_q.as<int32_t>());
       NBG_HIP(hipGetLastError());

@@ -1055,6 +1055,19 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
 // nbits by the owning lanes (one writer per word).  Partials [0] found, [1] their out-degree
 // sum, [3] rows scanned by bu_rest_scan (counted by the first pass), [4] entries read, [5] values read.
 constexpr int kLeanChunk = 8;
+// The 8 entries [a, a + 8) of a transposed row's chunk, a a multiple of 4: two 16-byte loads
+// (one vector-memory instruction per 4 entries instead of one per entry -- the divergent
+// per-entry gathers, 64 distinct lines per instruction, held the rest passes at the L1's
+// per-line rate); the second only when the row continues past a + 4.  The columns are padded
+// so the first load may run past the last row.
+__device__ inline void load_chunk8(const int32_t* __restrict__ tcol, int64_t a, int64_t re, bool act,
+                                   int32_t (&sv)[kLeanChunk]) {
+  int4 x = make_int4(-1, -1, -1, -1), y = x;
+  if (act) x = *reinterpret_cast<const int4*>(tcol + a);
+  if (act && a + 4 < re) y = *reinterpret_cast<const int4*>(tcol + a + 4);
+  sv[0] = x.x, sv[1] = x.y, sv[2] = x.z, sv[3] = x.w;
+  sv[4] = y.x, sv[5] = y.y, sv[6] = y.z, sv[7] = y.w;
+}
 template <int PK, int W, int HUB>
 __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long long* __restrict__ pbits, int64_t n,
                                                           const int64_t* __restrict__ trp,
@@ -1062,15 +1075,19 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
                                                           const uint32_t* __restrict__ fbits, unsigned long long* nbits,
                                                           const uint32_t* __restrict__ odeg, FastArgs fp, QArgs q_arg,
                                                           unsigned long long* partials, int cw, int ru, int rest_from,
-                                                          int steps) {
+                                                          int steps, unsigned long long* dbg) {
   const QArgs q = q_sgpr(q_arg);
   __shared__ unsigned long long lds[kSlots * 16];
   __shared__ unsigned long long s_found[16][64];
   extern __shared__ uint32_t s_fb[];
+  const unsigned long long t_in = wall_clock64();
   if (HUB) {
     for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
     __syncthreads();
   }
+  const unsigned long long t_hub = wall_clock64();
+  uint32_t d_rows = 0, d_batches = 0, d_steps = 0, d_scan = 0;
+  unsigned long long t_scan = 0;
   const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
   auto in_front = [&](int32_t g) -> bool {
     const int32_t wi = g >> 5;
@@ -1110,25 +1127,26 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
       for (int st = 32; st > 0; st >>= 1)
         if (uint32_t(__popcll(wbits & ((1ull << (bit + st)) - 1ull))) <= kk) bit += st;
       const int32_t r = int32_t((cbase + wsel) * 64 + bit);
+      int64_t r0 = 0;  // the row's first entry to test; chunks start at the aligned a <= r0
       if (pend[0]) {
-        rb[0] = trp[r] + rest_from;
+        r0 = trp[r] + rest_from;
         re[0] = trp[r + 1];
-        pend[0] = rb[0] < re[0];
+        rb[0] = r0 & ~int64_t(3);
+        pend[0] = r0 < re[0];
       }
+      d_batches++;
+      d_rows += p < total;
       for (int step = 0; step < steps; step++) {
         if (__ballot(pend[0]) == 0) break;
+        d_steps++;
         int32_t sv[kLeanChunk];
-#pragma unroll
-        for (int k = 0; k < kLeanChunk; k++) {
-          const int64_t e = rb[0] + k < re[0] ? rb[0] + k : re[0] - 1;  // in-row: same lines
-          sv[k] = pend[0] ? tcol[e] : -1;
-        }
+        load_chunk8(tcol, rb[0], re[0], pend[0], sv);
         __builtin_amdgcn_sched_barrier(0);
         uint32_t w[kLeanChunk];
         int tq[kLeanChunk];
 #pragma unroll
         for (int k = 0; k < kLeanChunk; k++) {
-          const bool valid = pend[0] && rb[0] + k < re[0];
+          const bool valid = pend[0] && rb[0] + k >= r0 && rb[0] + k < re[0];
           acc[4] += valid;
           tq[k] = PK == PK_FAST ? q_test(sv[k], q) : 1;
           const bool cand = valid && tq[k] != 0;
@@ -1171,7 +1189,10 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
         pend[0] = pend[0] && !h && rb[0] < re[0];
       }
       const uint32_t a3 = acc[3];
+      const unsigned long long ts0 = wall_clock64();
       bu_rest_scan<PK, W, 1>(pend, found, rb, re, tcol, fp, ru, acc, in_front, q);
+      t_scan += wall_clock64() - ts0;
+      d_scan += acc[3] - a3;
       acc[3] = a3;  // the pending rows were counted by the first pass
       if (found[0]) {
         atomicOr(&s_found[wv][wsel], 1ull << (r & 63));
@@ -1183,6 +1204,17 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
     const unsigned long long fw = s_found[wv][lane];
     if (fw) nbits[myw] |= fw;
     __builtin_amdgcn_wave_barrier();
+  }
+  if (dbg) {  // diagnostics: per wave timestamps (wall_clock64) and work
+    const unsigned long long t_out = wall_clock64();
+    uint32_t tr = d_rows, te = acc[4];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tr += __shfl_xor(tr, o), te += __shfl_xor(te, o);
+    if (lane == 0) {
+      unsigned long long* d = dbg + wave * 8;
+      d[0] = t_in, d[1] = t_hub, d[2] = t_out, d[3] = tr, d[4] = d_batches << 16 | d_steps, d[5] = d_scan, d[6] = te,
+      d[7] = t_scan;
+    }
   }
   unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
   block_store_partials(acc64, 6, lds, partials);
@@ -1217,6 +1249,10 @@ __global__ __launch_bounds__(1024) void k_bits_compact(const uint32_t* __restric
 #pragma unroll
       for (int q = 0; q < 4; q++) x[q] = w0 + q < nwords ? bits[w0 + q] : 0u;
     }
+    // bits at or past n (a bitmap's unused tail may hold stale bits) are never listed
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if ((w0 + q + 1) * 32 > n && w0 + q < nwords) x[q] &= (1u << uint32_t(n - (w0 + q) * 32)) - 1u;
     uint32_t o[4], cnt = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -2004,7 +2040,7 @@ void launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
       1, std::min<int64_t>((waves + bs / 64 - 1) / (bs / 64),
                            std::min<int64_t>(cw > 0 ? 512 : c.opt("bu_lean_grid", 2048), kAggBlocks / 2))));
   const size_t shm = size_t(std::max(cw, 1)) * 4;
-  c.ws_pend.ensure(size_t(ntiles * 2 + 2) * 8);
+  c.ws_pend.ensure(size_t(ntiles * 2 + 2) * 8);  // the pending bits, 2 words per tile
   unsigned long long* pbits = c.ws_pend.as<unsigned long long>();
   unsigned long long* partials = c.ws_partials.as<unsigned long long>();
   auto* nb = reinterpret_cast<unsigned long long*>(nbits);
@@ -2041,14 +2077,22 @@ void launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
                                         std::min<int64_t>({fb_words, int64_t(36 * 1024), hub_cap})));
   const size_t rshm = size_t(std::max(rcw, 1)) * 4;
   const int rsteps = int(std::max<int64_t>(1, c.opt("bu_rest_steps", 4)));
+  // diagnostics (option bu_rest_dbg): per-wave records of the rest pass appended to $NBG_DBG_FILE
+  DevBuf dbg_buf;
+  unsigned long long* dbg = nullptr;
+  if (c.opt("bu_rest_dbg", 0)) {
+    dbg_buf.alloc(size_t(grid2) * 16 * 64);
+    NBG_HIP(hipMemsetAsync(dbg_buf.p, 0, size_t(grid2) * 16 * 64, c.stream));
+    dbg = dbg_buf.as<unsigned long long>();
+  }
   auto rest = [&](auto kern) {
     if (rshm > 48 * 1024)
       lds_limit(reinterpret_cast<const void*>(kern), rshm);
     kern<<<grid2, 1024, rshm, c.stream>>>(pbits, tr.n_rows, trp, tc, fb, nb, odeg, fp, q, partials + grid, rcw, ru,
-                                          rest_from, rsteps);
+                                          rest_from, rsteps, dbg);
   };
-#define NBG_REST(PKV, WV)                          \
-  if (rcw > 0) rest(k_bu_rest_lean<PKV, WV, 1>);   \
+#define NBG_REST(PKV, WV)                        \
+  if (rcw > 0) rest(k_bu_rest_lean<PKV, WV, 1>); \
   else rest(k_bu_rest_lean<PKV, WV, 0>)
   if (fast) {
     switch (W) {
@@ -2065,11 +2109,24 @@ void launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
   if (after_kernel) NBG_HIP(hipEventRecord(after_kernel, c.stream));
   k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid + grid2, out);
   NBG_HIP(hipGetLastError());
+  if (dbg) {
+    std::vector<unsigned long long> h(size_t(grid2) * 16 * 8);
+    NBG_HIP(hipMemcpyAsync(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    if (const char* fn = getenv("NBG_DBG_FILE")) {
+      if (FILE* f = fopen(fn, "ab")) {
+        const uint64_t hdr[2] = {uint64_t(pk), uint64_t(grid2) * 16};
+        fwrite(hdr, 8, 2, f);
+        fwrite(h.data(), 8, h.size(), f);
+        fclose(f);
+      }
+    }
+  }
   char nm[96];
   snprintf(nm, sizeof nm, "nbg::k_bu_lean<%d, %d, %d>", pk, U, cw > 0 ? 1 : 0);
   c.bu_kernel_name = nm;
-  snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d>", pk, fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0,
-           rcw > 0 ? 1 : 0);
+  const int wn = fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0;
+  snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d>", pk, wn, rcw > 0 ? 1 : 0);
   c.bu_rest_name = nm;
 }
 
