@@ -8,6 +8,7 @@ device by the snapshot builder.  A "step" of this benchmark is one full query.  
 entries scanned over all hops / wall time; the frontier never leaves HBM.
 
     python bench.py                       # N=1
+    python bench.py --gpus N              # spawns N ranks itself (one process per GPU)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
     python bench.py --plain --scale 22    # configs[1] (C2)
     python bench.py --plain --scale 28 --hops 2 --hubs 8   # configs[4] (C5)
@@ -155,7 +156,9 @@ def cpu_baseline(scale: int, where_k: int, golden: dict, c1_scale: int = 16):
         "kind": "port",
         "sample": f"oracle (KV-store restatement of storaged+graphd) GO 3 STEPS WHERE weight>{where_k} YIELD "
                   f"DISTINCT _dst from 64 seeds on RMAT-{scale} (ef16), faithful mode (1 storaged host x 10 bucket "
-                  f"threads + 1 graphd thread), best of 3 after 1 warm-up; KV load {load_s:.1f}s",
+                  f"threads + 1 graphd thread), best of 3 after 1 warm-up; KV load {load_s:.1f}s.  The sample graph is "
+                  f"smaller than the GPU's RMAT-26 (the oracle holds the KV bytes in host memory and scans them at "
+                  f"~3 M edges/s): GTEPS of the two are rates on different graph sizes, not a like-for-like speedup",
         "host_cores": usable,
         "machine_cores": machine,
         "cpu_model": model,
@@ -181,7 +184,8 @@ def cpu_baseline_paths(scale: int, npairs: int, max_steps: int):
     return {"value": npairs / dt, "unit": "pairs/s", "cores": 1, "kind": "port", "host_cores": usable,
             "machine_cores": machine, "cpu_model": model,
             "sample": f"oracle FIND SHORTEST PATH {npairs} pairs on RMAT-{scale} (ef16) UPTO {max_steps} STEPS, "
-                      f"best of 3 after 1 warm-up: {dt:.2f}s"}
+                      f"best of 3 after 1 warm-up: {dt:.2f}s; a smaller graph than the GPU's RMAT-26, so pairs/s "
+                      f"of the two are not a like-for-like speedup"}
 
 
 # ---- parity of the timed query ----------------------------------------------------------------
@@ -215,9 +219,11 @@ def parity_go(sp, run_host, key, golden, dist, world, rank, plain_rows_check):
     out["status"] = "no golden"
     if plain_rows_check is not None:
         want = plain_rows_check()
-        out.update(property="rows == out-degree sum of the final frontier",
-                   status="property ok" if want == len(col) else "property mismatch", rows=int(len(col)),
-                   expected=int(want))
+        # weak: a fused plain-_dst expansion writes exactly that many rows by construction, so this
+        # only catches a row-count slip, not a wrong frontier -- labelled as such
+        out.update(property="rows == out-degree sum of the final frontier (row count only; no digest)",
+                   status="unchecked (row count ok)" if want == len(col) else "property mismatch",
+                   rows=int(len(col)), expected=int(want))
     return out
 
 
@@ -346,6 +352,51 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
     sp.close()
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` without torch.distributed.run: N child processes of this script with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (one per GPU, as the launcher
+    sets them); rank 0's stdout (the JSON line) is passed through, the others' discarded.  The
+    parent never touches the GPU.  Returns the first non-zero child exit code, else 0."""
+    import subprocess
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    bad = [c for c in rcs if c != 0]
+    if bad:
+        print(f"bench.py: rank exit codes {rcs}", file=sys.stderr)
+    return bad[0] if bad else 0
+
+
+def launch_check(dist, rank, world, local) -> int:
+    """--launch-check: the ranks came up with consistent env and can talk (no GPU call)"""
+    total = world * (world - 1) // 2
+    seen = rank
+    if dist is not None:
+        import torch
+        t = torch.tensor([rank], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        seen = int(t.item())
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"launch_check": "ok" if seen == total else "mismatch", "world": world,
+                          "rank_sum": seen, "master_port": os.environ.get("MASTER_PORT")}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0 if seen == total else 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -368,8 +419,13 @@ def main():
     ap.add_argument("--plain", action="store_true",
                     help="GO without WHERE / DISTINCT (configs[1]: RMAT-22 3 steps, configs[4]: RMAT-28 2 steps)")
     ap.add_argument("--max-steps", type=int, default=8)
+    ap.add_argument("--launch-check", action="store_true",
+                    help="only bring the ranks up (gloo init, barrier, all-reduce) and print one JSON line")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no external launcher: spawn one process per GPU here, before anything touches the GPU
+        return spawn_ranks(args.gpus)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -378,6 +434,8 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.launch_check:
+        return launch_check(dist, rank, world, local)
 
     from nebula_amd import GraphSpace
     from nebula_amd import expr as X
@@ -516,7 +574,22 @@ def main():
             "bottom_up_hops": bu_steps,
             "hops": hop_stats,
         }
-    r = None  # release the last result before the parity query
+    r = None  # release the last result before the end-to-end and parity queries
+    # end to end: the same query with its result copied to the host (what a graphd caller pays);
+    # untimed by the contract's clock, reported beside the device-resident ms_per_step
+    e2e = []
+    for _ in range(3):
+        barrier()
+        t1 = time.perf_counter()
+        r = one(False)
+        e2e.append((time.perf_counter() - t1) * 1e3)
+        r = None
+    e2e_ms = float(np.median(e2e))
+    if dist is not None:
+        import torch
+        te2 = torch.tensor([e2e_ms], dtype=torch.float64)
+        dist.all_reduce(te2, op=dist.ReduceOp.MAX)
+        e2e_ms = float(te2.item())
     parity = {"status": "skipped"}
     if not args.no_parity:
         key = (f"go{args.hops}_plain_s{args.scale}" if args.plain else
@@ -560,6 +633,11 @@ def main():
                 "edges_after_collapse": info["local_out_edges"] if world == 1 else None,
                 "edges_scanned_per_query": edges // K,
                 "result_rows": rows,
+                # the timed queries leave their result in HBM (ms_per_step); with the result
+                # copied to host memory a query takes query_end_to_end_ms (median of 3), the
+                # difference being the device->host copy of the rows
+                "query_end_to_end_ms": round(e2e_ms, 4),
+                "result_d2h_ms": round(e2e_ms - dt / args.steps * 1e3, 4),
                 "snapshot_build_s": round(build_s, 2),
                 "parallelism": f"part%{world} sharding, RCCL frontier exchange" if world > 1 else "1 GPU",
                 "hub_seeds": hubs or None,
@@ -584,4 +662,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

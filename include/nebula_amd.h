@@ -83,6 +83,16 @@ int32_t nbg_comm_init_local(nbg_ctx* ctx, int64_t group_key);
  * 1 RCCL, 2 LocalComm.  Lets a multi-GPU bench line show the rank count RCCL really formed.  */
 int32_t nbg_comm_info(nbg_ctx* ctx, int32_t* ranks, int32_t* transport);
 
+/* ABI version of this header's structs and signatures.  Caller-allocated structs (nbg_timing,
+ * nbg_hop_stat, nbg_snapshot_info, nbg_go_spec, nbg_rows) change layout between versions: an
+ * integration compares nbg_abi_version() with the NBG_ABI_VERSION it was built against and
+ * refuses to run on a mismatch (INTEGRATION.md "ABI versioning").                          */
+#define NBG_ABI_VERSION 3
+int32_t nbg_abi_version(void);
+/* sizeof of the caller-allocated structs as the library was built: 0 nbg_timing, 1
+ * nbg_hop_stat, 2 nbg_snapshot_info, 3 nbg_go_spec, 4 nbg_rows, 5 nbg_prop_def; -1 otherwise */
+int64_t nbg_struct_size(int32_t which);
+
 /* pure arithmetic helpers (host, no GPU needed) */
 int32_t nbg_part_of(int64_t vid, int32_t num_parts);          /* StorageClient.cpp:238-243 */
 int32_t nbg_rank_of_part(int32_t part, int32_t world_size);   /* CreateSpaceProcessor.cpp:77-90 */

@@ -22,9 +22,11 @@ ERRORS = {
 }
 T_BOOL, T_INT, T_VID, T_FLOAT, T_DOUBLE, T_STRING, T_TIMESTAMP = 1, 2, 3, 4, 5, 6, 21
 OWNER_SOURCE, OWNER_DEST, OWNER_EDGE = 1, 2, 3
+ABI_VERSION = 3  # NBG_ABI_VERSION of include/nebula_amd.h
 
 # every symbol the header declares (tests/test_capi.py checks the .so exports them all)
 EXPORTS = [
+    "nbg_abi_version", "nbg_struct_size",
     "nbg_ctx_create", "nbg_ctx_destroy", "nbg_last_error", "nbg_comm_unique_id", "nbg_comm_init",
     "nbg_comm_init_local", "nbg_comm_info",
     "nbg_part_of", "nbg_rank_of_part", "nbg_schema_set_edge", "nbg_schema_set_tag", "nbg_snapshot_load_part",
@@ -106,6 +108,8 @@ def load(path: str | os.PathLike | None = None):
     L = C.CDLL(str(p))
     vp, i32, i64, u64, sz = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_size_t
     sig = {
+        "nbg_abi_version": (i32, []),
+        "nbg_struct_size": (i64, [i32]),
         "nbg_ctx_create": (vp, [i32, i32, i32, i32]),
         "nbg_ctx_destroy": (None, [vp]),
         "nbg_last_error": (C.c_char_p, [vp]),
@@ -136,5 +140,11 @@ def load(path: str | os.PathLike | None = None):
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    # the ctypes mirrors below must match the library's struct layouts (include/nebula_amd.h)
+    if L.nbg_abi_version() != ABI_VERSION:
+        raise ImportError(f"{p}: ABI version {L.nbg_abi_version()}, this binding expects {ABI_VERSION}")
+    for which, st in enumerate((Timing, HopStat, SnapshotInfo, GoSpec, Rows, PropDef)):
+        if L.nbg_struct_size(which) != C.sizeof(st):
+            raise ImportError(f"{p}: sizeof({st.__name__}) {C.sizeof(st)} != the library's {L.nbg_struct_size(which)}")
     _lib = L
     return L

@@ -1,4 +1,6 @@
 // capi.cpp -- extern "C" entry points declared in include/nebula_amd.h.
+#include <map>
+#include <mutex>
 #include <algorithm>
 #include <cstring>
 
@@ -52,7 +54,22 @@ static int32_t guarded(nbg_ctx* ctx, F f) {
   }
 }
 
+namespace nbg {
+static std::mutex g_dev_mu;
+static std::map<int, int> g_dev_ctx;
+int ctx_count_on_device(int device) {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  auto it = g_dev_ctx.find(device);
+  return it == g_dev_ctx.end() ? 0 : it->second;
+}
+static void ctx_count_add(int device, int d) {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  g_dev_ctx[device] += d;
+}
+}  // namespace nbg
+
 extern "C" {
+
 
 nbg_ctx* nbg_ctx_create(int32_t device, int32_t num_parts, int32_t rank, int32_t world_size) {
   if (num_parts <= 0 || world_size <= 0 || rank < 0 || rank >= world_size) return nullptr;
@@ -79,12 +96,16 @@ nbg_ctx* nbg_ctx_create(int32_t device, int32_t num_parts, int32_t rank, int32_t
   // from pageable memory go through a driver bounce buffer and block the calling thread
   if (hipHostMalloc(&ctx->c.host_stage, nbg::kHostStageBytes, hipHostMallocDefault) != hipSuccess)
     ctx->c.host_stage = nullptr;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) == hipSuccess) ctx->c.hbm_total = tot;
+  nbg::ctx_count_add(device, 1);
   return ctx;
 }
 
 void nbg_ctx_destroy(nbg_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->c.device);
+  nbg::ctx_count_add(ctx->c.device, -1);
   (void)hipStreamSynchronize(ctx->c.stream);
   nbg::comm_destroy(ctx->c);
   for (auto& e : ctx->c.ev) (void)hipEventDestroy(e);
@@ -119,6 +140,19 @@ int32_t nbg_comm_info(nbg_ctx* ctx, int32_t* ranks, int32_t* transport) {
     nbg::comm_info(c, ranks, transport);
     return NBG_OK;
   });
+}
+
+int32_t nbg_abi_version(void) { return NBG_ABI_VERSION; }
+int64_t nbg_struct_size(int32_t which) {
+  switch (which) {
+    case 0: return int64_t(sizeof(nbg_timing));
+    case 1: return int64_t(sizeof(nbg_hop_stat));
+    case 2: return int64_t(sizeof(nbg_snapshot_info));
+    case 3: return int64_t(sizeof(nbg_go_spec));
+    case 4: return int64_t(sizeof(nbg_rows));
+    case 5: return int64_t(sizeof(nbg_prop_def));
+    default: return -1;
+  }
 }
 
 int32_t nbg_part_of(int64_t vid, int32_t num_parts) {

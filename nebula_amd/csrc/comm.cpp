@@ -181,6 +181,7 @@ void comm_init(Ctx& c, const uint8_t id_bytes[128]) {
   memcpy(&id, id_bytes, 128);
   NBG_HIP(hipSetDevice(c.device));
   auto* r = new RcclComm();
+  pool_trim_all();  // RCCL's buffers come from the driver, which never trims the block caches
   ncclResult_t rc = ncclCommInitRank(&r->comm, c.world, id, c.rank);
   if (rc != ncclSuccess) {
     r->comm = nullptr;

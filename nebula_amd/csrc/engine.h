@@ -456,6 +456,7 @@ struct Ctx {
     }
   }
   std::map<std::string, int64_t> options;
+  size_t hbm_total = 0;  // the device's memory (hipMemGetInfo at create)
 
   int64_t owned_lo() const { return base.empty() ? 0 : base[size_t(rank)]; }
   int64_t owned_hi() const { return base.empty() ? n_global : base[size_t(rank) + 1]; }
@@ -465,9 +466,22 @@ struct Ctx {
   }
 };
 
-// the context's query block cache, its cap read from option query_pool_gb (default 64 GiB)
+// live contexts per device (nbg_ctx_create / nbg_ctx_destroy): in-process rank groups put
+// several contexts on one GPU, and each caches query blocks of its own
+int ctx_count_on_device(int device);
+// the context's query block cache.  Cap: option query_pool_gb, else a quarter of the device's
+// HBM shared among the contexts on it, at most 64 GiB (one MI355X context: 64 GiB; eight
+// LocalComm ranks on one GPU: 8.9 GiB each), so the cache never holds what RCCL or the driver
+// allocate outside DevBuf (those never trigger its trim)
 inline std::shared_ptr<BufPool>& query_pool(Ctx& c) {
-  c.pool->limit = size_t(std::max<int64_t>(0, c.opt("query_pool_gb", 64))) << 30;
+  const int64_t gb = c.opt("query_pool_gb", -1);
+  size_t cap = size_t(64) << 30;
+  if (gb >= 0) {
+    cap = size_t(gb) << 30;
+  } else if (c.hbm_total) {
+    cap = std::min(cap, c.hbm_total / 4 / size_t(std::max(1, ctx_count_on_device(c.device))));
+  }
+  c.pool->limit = cap;
   return c.pool;
 }
 
