@@ -1044,16 +1044,17 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
   block_store_partials(acc64, 8, lds, partials);
 }
 
-// Second pass of a lean bottom-up hop (bu_kernel = 2): the rows k_bu_lean left pending.  A wave
-// owns 64 consecutive pending-bit words (4096 rows) and ranks their pending rows (wave prefix
-// sum of the words' popcounts); 64 pending rows at a time, a lane scans its row's entries
-// [row_ptr + rest_from, row_ptr + 1) in chunks of kLeanChunk: all chunk loads issued, then all
+// Second pass of a bottom-up hop: the rows k_bu_lean left pending.  A wave owns 64 pending-bit
+// words spread over the row range (one per lane, nwaves apart, so every wave samples the dense
+// hub end and the sparse tail alike) and ranks their pending rows (wave prefix sum of the words'
+// popcounts); 64 pending rows at a time, a lane scans its row's entries [row_ptr + rest_from,
+// row_ptr + 1) in aligned 8-entry chunks (two 16-byte loads): all chunk loads issued, then all
 // probes (buffer loads out of bounds for non-candidates, LDS for hub words), then the tests, as
-// in k_bu_lean; a value is read only for a frontier hit in the constant's bucket.  After
-// kLeanSteps chunks the rows still pending (long in-edge lists) go to bu_rest_scan (whole wave /
-// 16-lane groups).  Found rows OR into the wave's 64 next-frontier words in LDS, merged into
-// nbits by the owning lanes (one writer per word).  Partials [0] found, [1] their out-degree
-// sum, [3] rows scanned by bu_rest_scan (counted by the first pass), [4] entries read, [5] values read.
+// in k_bu_lean; a value is read only for a frontier hit in an undecided bucket.  After `steps`
+// chunks the rows still pending (long in-edge lists) go to bu_rest_scan (whole wave / 16-lane
+// groups).  Found rows OR into the wave's 64 next-frontier words in LDS, merged into nbits by
+// the owning lanes (one writer per word).  Partials [0] found, [1] their out-degree sum, [3] rows
+// scanned by bu_rest_scan (counted by the first pass), [4] entries read, [5] values read.
 constexpr int kLeanChunk = 8;
 // The 8 entries [a, a + 8) of a transposed row's chunk, a a multiple of 4: two 16-byte loads
 // (one vector-memory instruction per 4 entries instead of one per entry -- the divergent
@@ -1102,8 +1103,11 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
   const int64_t nwords = (n + 63) / 64;
   const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  for (int64_t cbase = wave * 64; cbase < nwords; cbase += nwaves * 64) {
-    const int64_t myw = cbase + lane;
+  // a wave's 64 words are spread over the whole row range (word base + l * nwaves + wave for
+  // lane l): the pending rows are dense among the hub rows at the low end, and a wave of 64
+  // consecutive words there held 5-6 batches while most waves had one (r04h: 57 vs 12 us)
+  for (int64_t cbase = 0; cbase + wave < nwords; cbase += nwaves * 64) {
+    const int64_t myw = cbase + int64_t(lane) * nwaves + wave;
     const unsigned long long pw = myw < nwords ? pbits[myw] : 0ull;
     s_found[wv][lane] = 0ull;
     uint32_t total;
@@ -1126,7 +1130,7 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
 #pragma unroll
       for (int st = 32; st > 0; st >>= 1)
         if (uint32_t(__popcll(wbits & ((1ull << (bit + st)) - 1ull))) <= kk) bit += st;
-      const int32_t r = int32_t((cbase + wsel) * 64 + bit);
+      const int32_t r = int32_t((cbase + int64_t(wsel) * nwaves + wave) * 64 + bit);
       int64_t r0 = 0;  // the row's first entry to test; chunks start at the aligned a <= r0
       if (pend[0]) {
         r0 = trp[r] + rest_from;
@@ -1786,6 +1790,40 @@ void exchange_marks(Ctx& c, uint8_t* map) {
   NBG_HIP(hipGetLastError());
 }
 
+__global__ void k_min_segments(const int32_t* recv, int G, int64_t n, int32_t* out) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    int32_t m = INT32_MAX;
+    for (int g = 0; g < G; g++) m = min(m, recv[size_t(g) * size_t(n) + size_t(i)]);
+    out[i] = m;
+  }
+}
+
+// world > 1, $- / $var props with STEPS > 1: every rank's top-down hop took the smallest root
+// rank over ITS in-edges of each dst (one atomicMin per edge, any owner); the owner of a dst
+// needs the minimum over all ranks' edges (GoExecutor.h:174-193's VertexBackTracker, under the
+// deterministic rule of DESIGN.md divergence 6).  Each rank sends every owner its slice of the
+// root array and takes the elementwise minimum of the slices it receives.
+void exchange_roots(Ctx& c, int32_t* root_next) {
+  if (c.world == 1) return;
+  CommTimer t(c);
+  const size_t G = size_t(c.world);
+  const int64_t lo = c.owned_lo(), n_own = c.owned_hi() - lo;
+  DevBuf rbuf;
+  rbuf.alloc(std::max<size_t>(G * size_t(n_own) * 4, 4));
+  std::vector<size_t> sbytes(G), soff(G), rbytes(G), roff(G);
+  for (size_t p = 0; p < G; p++) {
+    sbytes[p] = size_t(c.base[p + 1] - c.base[p]) * 4;
+    soff[p] = size_t(c.base[p]) * 4;
+    rbytes[p] = size_t(n_own) * 4;
+    roff[p] = p * size_t(n_own) * 4;
+  }
+  comm_alltoallv_bytes(c, root_next, sbytes.data(), soff.data(), rbuf.p, rbytes.data(), roff.data());
+  c.timing.comm_bytes += uint64_t(c.n_global - n_own) * 4;
+  if (n_own)
+    k_min_segments<<<grid_cap(n_own), 256, 0, c.stream>>>(rbuf.as<int32_t>(), int(G), n_own, root_next + lo);
+  NBG_HIP(hipGetLastError());
+}
+
 __global__ void k_hist_dest(const uint32_t* dest, int64_t n, int G, unsigned long long* counts) {
   __shared__ unsigned int h[64];
   if (threadIdx.x < 64) h[threadIdx.x] = 0;
@@ -2322,8 +2360,6 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   const bool multi_root = uses_input && s.steps > 1;
   DevBuf root_buf[2], root_tab;
   int root_cur = 0;
-  if (multi_root && c.world > 1)
-    throw Error(NBG_E_UNSUPPORTED, "$- / $var props with STEPS > 1 across ranks");
   if (multi_root) {
     // rank of every start's vid among the distinct start vids
     std::vector<int64_t> u(s.starts, s.starts + ns);
@@ -2474,6 +2510,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         c.timing.expand_bytes += expand_bytes(nF, E, 0, EXP_MARK);
       }
       if (multi_root) {
+        exchange_roots(c, a.root_next);
         root_cur ^= 1;
         a.root_cur = nullptr;
         a.root_next = nullptr;

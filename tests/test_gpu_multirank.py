@@ -389,3 +389,36 @@ def test_sharded_write_misrouted_key_refused(world):
             assert union_rows(res) == ms(ref.rows())
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("steps", [2, 3])
+def test_sharded_multistep_input(world, steps):
+    """$- / $var props with STEPS > 1 across ranks (GoExecutor.h:174-193's VertexBackTracker):
+    each rank's top-down hop takes the smallest root over its own in-edges, the owners take the
+    minimum over all ranks (exchange_roots) -- the oracle's deterministic rule (DESIGN.md
+    divergence 6), many starts sharing descendants"""
+    from nebula_amd import synth
+    scale = 11
+    st = O.Store(16)
+    st.set_edge_schema(1, [("weight", O.INT)], name="e")
+    st.load_rmat(scale, 8, 3, 1)
+    g = Group(world, parts=16)
+    try:
+        for s in g.sp:
+            s.set_edge_schema(1, [("weight", O.INT)])
+        g.each(lambda r, s: s.gen_rmat(scale, 8, 3, 1))
+        g.each(lambda r, s: s.finalize())
+        starts = list(synth.seeds(scale, 8, 3, 24))
+        inputs = [("n", O.INT, [int(i * 7 % 11) for i in range(len(starts))])]
+        ys = [X.InputProp("n"), X.AliasProp("e", "weight"), X.EdgeDst("e")]
+        for w in (None, X.InputProp("n") > 4, (X.InputProp("n") + X.AliasProp("e", "weight")) > 600):
+            for distinct in (False, True):
+                res = g.go(starts, steps, 1, where=w, yields=ys, distinct=distinct, inputs=inputs)
+                ref = st.go(starts, steps, 1, where=X.encode(w), yields=[y.encode() for y in ys],
+                            distinct=distinct, inputs=inputs)
+                assert ref.code == 0, ref.error
+                assert union_rows(res) == ms(ref.rows())
+                assert sum(x.n_rows for x in res) > 0
+    finally:
+        g.close()

@@ -515,7 +515,7 @@ def test_rmat_bottom_up_shapes(rmat12, u, lds, rest_lds, rsteps, unroll, cap):
             assert g.edges_scanned == r_.edges_scanned
             ks = final_bu_kernels(sp)
             assert ks[0] == f"nbg::k_bu_lean<1, {u}, {1 if lds else 0}>", ks
-            assert ks[1].startswith("nbg::k_bu_rest_list<1, "), ks
+            assert ks[1].startswith("nbg::k_bu_rest_lean<1, "), ks
             pending += sum(h["c"][3] for h in sp.last_timing()["hops"] if h["mode"] == "bottom-up")
     assert pending > 0  # the rest pass had rows to scan
     # DISTINCT _dst without WHERE: the final-hop kernels with every bucket passing
@@ -556,4 +556,4 @@ def test_rmat_bottom_up_packed_predicate(rmat12, qpred, hub_cap):
             assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0))), (k, op)
             assert g.edges_scanned == r_.edges_scanned
             ks = final_bu_kernels(sp)
-            assert ks[0].startswith("nbg::k_bu_lean<1, ") and ks[1].startswith("nbg::k_bu_rest_list<1, "), ks
+            assert ks[0].startswith("nbg::k_bu_lean<1, ") and ks[1].startswith("nbg::k_bu_rest_lean<1, "), ks
