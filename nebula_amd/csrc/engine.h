@@ -92,6 +92,73 @@ struct BufPool {
   }
 };
 extern thread_local std::shared_ptr<BufPool> tl_pool;  // set for the duration of a query
+
+// Pinned host blocks for results copied back to the host.  A device->host copy into pageable
+// memory goes through the driver's bounce buffer (r04k: the 173 MB of C3's DISTINCT vids took
+// 64 ms, ~2.7 GB/s); into pinned memory it runs at the link's rate.  hipHostMalloc of a large
+// block is itself slow, so a context caches the blocks its released results hand back.
+struct HostPool {
+  std::mutex mu;
+  std::multimap<size_t, void*> blocks;
+  size_t cached = 0;
+  size_t limit = size_t(8) << 30;
+  ~HostPool() {
+    for (auto& b : blocks) (void)hipHostFree(b.second);
+  }
+  void* get(size_t want, size_t& got) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = blocks.lower_bound(want);
+    if (it == blocks.end() || it->first > 2 * want + (size_t(1) << 20)) return nullptr;
+    got = it->first;
+    void* p = it->second;
+    blocks.erase(it);
+    cached -= got;
+    return p;
+  }
+  void put(void* p, size_t cap) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (cached + cap <= limit) {
+        blocks.emplace(cap, p);
+        cached += cap;
+        return;
+      }
+    }
+    (void)hipHostFree(p);
+  }
+};
+struct HostBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  std::shared_ptr<HostPool> pool;
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  HostBuf(HostBuf&& o) noexcept : p(o.p), bytes(o.bytes), pool(std::move(o.pool)) {
+    o.p = nullptr;
+    o.bytes = 0;
+  }
+  ~HostBuf() {
+    if (!p) return;
+    if (pool) pool->put(p, bytes);
+    else (void)hipHostFree(p);
+  }
+  void alloc(const std::shared_ptr<HostPool>& pl, size_t b) {
+    if (p || b == 0) throw std::logic_error("HostBuf::alloc");
+    size_t got = 0;
+    if (pl && (p = pl->get(b, got))) {
+      bytes = got;
+      pool = pl;
+      return;
+    }
+    if (hipHostMalloc(&p, b, hipHostMallocDefault) != hipSuccess) {
+      p = nullptr;
+      throw Error(NBG_E_NOMEM, "hipHostMalloc(" + std::to_string(b) + ") failed");
+    }
+    bytes = b;
+    pool = pl;
+  }
+};
 // host time spent in hipMalloc / hipFree of DevBufs (the build's phase trace reports it)
 struct AllocClock {
   std::atomic<int64_t> alloc_ns{0}, free_ns{0}, allocs{0};
@@ -427,8 +494,10 @@ struct Ctx {
   // query's stream has drained, so timing never makes the host wait on a launch
   struct PendingTime {
     size_t a, b;
-    int32_t hop;  // Timing::hops index the time belongs to (-1: none)
+    int32_t hop;   // Timing::hops index the time belongs to (-1: none)
+    int32_t kind;  // 0: expand_ms + the hop's ms (+ kernel_ms of a top-down hop), 1: kernel_ms only
   };
+  bool hop_timing = true;  // option hop_timing: event pairs around the hops' kernels (0: none)
   std::vector<hipEvent_t> tev;
   size_t tev_used = 0;
   std::vector<PendingTime> tpend;
@@ -436,11 +505,16 @@ struct Ctx {
   // option query_pool_gb: a plain-rows result of RMAT-28 GO 2 STEPS is 21 GB, and re-allocating
   // it per query stalled one hipMalloc in ~9 for 5.7 s (r03 HIP API trace)
   std::shared_ptr<BufPool> pool = std::make_shared<BufPool>();
+  std::shared_ptr<HostPool> host_pool = std::make_shared<HostPool>();  // pinned result blocks
   // snapshot build / commit temporaries: freed blocks stay with the process (a fresh multi-GB
   // hipMalloc costs up to seconds: r03a trace), so the phases of a build and later commits of a
   // writable snapshot reuse them.  Trimmed after a read-only build.
   std::shared_ptr<BufPool> build_pool = std::make_shared<BufPool>();
-  unsigned long long* host_counters = nullptr;  // pinned, 64 entries
+  unsigned long long* host_counters = nullptr;  // pinned, coherent, 64 entries
+  // counters published by k_publish: host_counters + a sequence word the host spins on (a
+  // hipStreamSynchronize round trip costs ~19 us on this stack, tools/launch_gap)
+  unsigned long long* host_seq = nullptr;  // pinned, coherent
+  uint64_t pub_seq = 0;
   void* host_stage = nullptr;                   // pinned, kHostStageBytes (query inputs)
   size_t host_stage_used = 0;
   // async host->device copy of a query input through the pinned stage when it fits (the stage

@@ -13,6 +13,7 @@ struct HostRows {
   std::vector<int64_t*> str_off;
   std::vector<DevBuf> dev;       // device column storage when on_device
   std::vector<std::vector<uint8_t>> host;
+  std::vector<HostBuf> hpin;  // pinned result columns (GO rows copied to the host)
   std::vector<std::vector<int64_t>> host_off;
   std::vector<int64_t> row_vertex, vertex_ids, vertex_row_offsets;
   std::vector<int32_t> failed_parts, failed_codes;

@@ -1674,8 +1674,10 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
   es.q_gbits = es.q_bits = 0;
   es.tcol_q.release();
   if (c.opt("bu_pack", 1) && R > 0) {
+    // 2^gb > n_global: an empty slot (-1) decodes to a gidx past every vertex, whose bitmap
+    // probe is out of bounds (k_bu_lean relies on it)
     int gb = 1;
-    while ((int64_t(1) << gb) < std::max<int64_t>(c.n_global, 2)) gb++;
+    while ((int64_t(1) << gb) <= c.n_global) gb++;
     const int qb = std::min(8, 31 - gb);
     int f = -1;
     for (size_t i = 0; i < t.props.size() && f < 0; i++)

@@ -14,6 +14,7 @@
 // binary search in LDS.  Consecutive lanes read consecutive adjacency entries, so the col /
 // prop loads of a tile are coalesced whatever the degree distribution (a supernode simply
 // spans many tiles).
+#include <chrono>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_reduce.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -863,49 +864,57 @@ __device__ inline void bu_rest_scan(const bool (&pend)[R], bool (&found)[R], con
 // HUB: the block keeps the first cw words of the bitmap (the highest-out-degree vertices) in LDS
 // and answers candidates there from it; the global probe of such a slot is out of bounds.
 // Partials [6] / [7]: candidate probes sent to L2 / answered from LDS.
-template <int PK, int U, int HUB>
+template <int PK, int U, int HUB, int STATS>
 __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ lo, const uint2* __restrict__ hi,
                                                      int64_t ntiles, int64_t work_tiles,
-                                                     const uint32_t* __restrict__ fbits,
+                                                     const uint32_t* __restrict__ fbits, uint32_t fb_bytes,
                                                      unsigned long long* __restrict__ nbits,
                                                      unsigned long long* __restrict__ pbits,
                                                      const uint32_t* __restrict__ odeg, QArgs q_arg,
                                                      unsigned long long* __restrict__ partials, int cw) {
   __shared__ unsigned long long lds[kSlots * 16];
-  extern __shared__ uint32_t s_fb[];
+  extern __shared__ uint32_t s_fb[];  // [0, cw): the bitmap's hub words; [cw]: a zero word
   if (HUB) {
-    for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
+    for (int i = threadIdx.x; i <= cw; i += blockDim.x) s_fb[i] = i < cw ? fbits[i] : 0u;
     __syncthreads();
   }
   const QArgs q = q_sgpr(q_arg);
   constexpr bool FINAL = PK == PK_FAST;
-  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
+  constexpr int NS = FINAL ? 4 : 2;  // slots probed per row in the first round
+  // out-of-bounds reads of the bitmap return 0: a non-candidate's probe, and an empty slot
+  // (-1: its gidx bits are all ones, past every vertex, as the build guarantees)
+  const __amdgpu_buffer_rsrc_t fb_rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(fbits), 0, int(fb_bytes), 0x00020000);
+  const uint32_t gmask = q.gmask, ucw = uint32_t(cw);
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  uint32_t nfound = 0, npend = 0, nwords = 0, nglob = 0, nhub = 0;
+  uint32_t nglob = 0, nhub = 0;
+  unsigned long long nfound = 0, npend = 0, nwords = 0;  // wave-uniform
   unsigned long long odsum = 0;
-  // bitmap-word offset of slot word sw of a live row: out of bounds unless it is a candidate
-  // answered by L2; the LDS word index (HUB) in `hw` (-1: not a hub candidate).  Final hop: a
-  // slot whose bucket fails is no candidate; an undecided one (the constant's bucket, or every
-  // slot when the predicate column is not the packed one) is probed too and flagged in bit k of
-  // `und`, so only an undecided slot whose source IS in the frontier leaves the row pending
-  auto off = [&](int32_t sw, bool live, uint32_t& und, int k, int32_t& hw) -> uint32_t {
-    bool c = live && sw >= 0;
+  // One slot word: its probe (global byte offset, out of bounds unless an L2 candidate; LDS
+  // index, cw -- the zero word -- unless a hub candidate) and, final hop, its bucket's answer
+  // (bit k of `pm` pass, of `um` undecided).  A failing bucket is no candidate; an undecided
+  // one is probed too, so only a frontier hit there leaves the row pending.
+  auto prep = [&](uint32_t sw, int k, uint32_t& goff, uint32_t& lidx, uint32_t& pm, uint32_t& um) {
+    const uint32_t wi = (sw & gmask) >> 5;
+    bool cand = true;
     if (FINAL) {
-      const int t = q_test(sw, q);
-      und |= (c && t < 0) ? 1u << k : 0u;
-      c = c && t != 0;
+      const int st = q_test(int32_t(sw), q);  // below / above may be -1 (undecided) too
+      const bool und = st < 0, pass = st > 0;
+      cand = st != 0;
+      pm |= pass ? 1u << k : 0u;
+      um |= und ? 1u << k : 0u;
     }
-    const int32_t wi = q_gidx(sw, q) >> 5;
-    const bool hub = HUB && wi < cw;
-    hw = c && hub ? wi : -1;
-    nglob += c && !hub;
-    nhub += c && hub;
-    return c && !hub ? uint32_t(wi) * 4u : 0xfffffff0u;
+    const bool hub = HUB && wi < ucw;
+    goff = cand && !hub ? wi * 4u : 0xfffffff0u;
+    lidx = cand && hub ? wi : ucw;
+    if (STATS) {  // (diagnostic instantiation: the counters' masks cost the hot loop registers)
+      nglob += cand && !hub;
+      nhub += cand && hub;
+    }
   };
-  auto ld_ = [&](uint32_t o) -> uint32_t { return __builtin_amdgcn_raw_buffer_load_b32(fb_rs, o, 0, 0); };
-  auto hit = [](uint32_t w, int32_t sw) -> bool { return (w >> (uint32_t(sw) & 31u)) & 1u; };
+  auto bit = [](uint32_t w, uint32_t sw) -> uint32_t { return __builtin_amdgcn_ubfe(w, sw & 31u, 1u); };
   for (int64_t t0 = wave * U; t0 < work_tiles; t0 += nwaves * U) {
     uint2 a[U][2], b[U][2];
     uint32_t od[U][2];
@@ -922,63 +931,66 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    uint32_t w[U][2][4];
-    int32_t hw[U][2][4];
-    uint32_t und[U][2];
+    uint32_t goff[U][2][NS], lidx[U][2][NS], pm[U][2], um[U][2];
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        const bool live = v[u] && od[u][h] > 0;
-        und[u][h] = 0u;
-        w[u][h][0] = ld_(off(int32_t(a[u][h].x), live, und[u][h], 0, hw[u][h][0]));
-        w[u][h][1] = ld_(off(int32_t(a[u][h].y), live, und[u][h], 1, hw[u][h][1]));
+        pm[u][h] = um[u][h] = 0u;
+        prep(a[u][h].x, 0, goff[u][h][0], lidx[u][h][0], pm[u][h], um[u][h]);
+        prep(a[u][h].y, 1, goff[u][h][1], lidx[u][h][1], pm[u][h], um[u][h]);
         if (FINAL) {
-          w[u][h][2] = ld_(off(int32_t(b[u][h].x), live, und[u][h], 2, hw[u][h][2]));
-          w[u][h][3] = ld_(off(int32_t(b[u][h].y), live, und[u][h], 3, hw[u][h][3]));
+          prep(b[u][h].x, 2, goff[u][h][2], lidx[u][h][2], pm[u][h], um[u][h]);
+          prep(b[u][h].y, 3, goff[u][h][3], lidx[u][h][3], pm[u][h], um[u][h]);
         }
       }
+    // probes: the LDS reads first (answered in ~100 cycles), then the L2 ones, each into a
+    // register of its own, OR-ed afterwards (one of the two is always 0)
+    uint32_t lw[U][2][NS], gw[U][2][NS];
     if (HUB) {
 #pragma unroll
       for (int u = 0; u < U; u++)
 #pragma unroll
         for (int h = 0; h < 2; h++)
 #pragma unroll
-          for (int k = 0; k < (FINAL ? 4 : 2); k++) {
-            const uint32_t lw = s_fb[hw[u][h][k] < 0 ? 0 : hw[u][h][k]];
-            w[u][h][k] = hw[u][h][k] < 0 ? w[u][h][k] : lw;
-          }
+          for (int k = 0; k < NS; k++) lw[u][h][k] = s_fb[lidx[u][h][k]];
     }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int k = 0; k < NS; k++) gw[u][h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, goff[u][h][k], 0, 0);
     __builtin_amdgcn_sched_barrier(0);
     bool f[U][2], pend[U][2];
 #pragma unroll
     for (int u = 0; u < U; u++) {
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        bool x;
+        const uint32_t sw[4] = {a[u][h].x, a[u][h].y, b[u][h].x, b[u][h].y};
+        uint32_t hm = 0u;
+#pragma unroll
+        for (int k = 0; k < NS; k++) hm |= bit(HUB ? (lw[u][h][k] | gw[u][h][k]) : gw[u][h][k], sw[k]) << k;
         if (FINAL) {
-          // slot k in the frontier: found when its bucket passes, pending when undecided
-          const uint32_t hm = uint32_t(hit(w[u][h][0], int32_t(a[u][h].x))) |
-                              uint32_t(hit(w[u][h][1], int32_t(a[u][h].y))) << 1 |
-                              uint32_t(hit(w[u][h][2], int32_t(b[u][h].x))) << 2 |
-                              uint32_t(hit(w[u][h][3], int32_t(b[u][h].y))) << 3;
-          x = (hm & ~und[u][h]) != 0u;
-          pend[u][h] = v[u] && !x && (int32_t(b[u][h].y) >= 0 || (hm & und[u][h]) != 0u);
+          f[u][h] = (hm & pm[u][h]) != 0u;
+          // not found: pending when a frontier hit sits in an undecided bucket, or the row has
+          // a fifth entry (slot 3 present)
+          pend[u][h] = v[u] && !f[u][h] && (b[u][h].y != 0xffffffffu || (hm & um[u][h]) != 0u);
         } else {
-          x = hit(w[u][h][0], int32_t(a[u][h].x)) || hit(w[u][h][1], int32_t(a[u][h].y));
+          f[u][h] = hm != 0u && od[u][h] > 0;
           // rows with a third slot to test: live, not found, slot 1 present
-          pend[u][h] = v[u] && !x && od[u][h] > 0 && int32_t(a[u][h].y) >= 0;
+          pend[u][h] = v[u] && hm == 0u && od[u][h] > 0 && a[u][h].y != 0xffffffffu;
         }
-        f[u][h] = x;
       }
-      nwords += v[u] ? (FINAL ? 8u : 4u) : 0u;
+      nwords += v[u] ? (FINAL ? 8u : 4u) * 64u : 0u;  // every lane's two rows
     }
     if (!FINAL) {
       // second half, lazily: only lanes with a pending row load it (rarely any at all)
       bool anyp = false;
 #pragma unroll
       for (int u = 0; u < U; u++) anyp = anyp || pend[u][0] || pend[u][1];
-      if (__ballot(anyp)) {
+      const unsigned long long anyb = __ballot(anyp);
+      if (anyb) {
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
@@ -986,30 +998,44 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
             b[u][h] = make_uint2(0xffffffffu, 0xffffffffu);
             if (pend[u][h]) b[u][h] = hi[(t0 + u) * 128 + lane + 64 * h];
           }
+        uint64_t pc = 0;  // rows reading the second half: 2 words each
+#pragma unroll
+        for (int u = 0; u < U; u++) pc += uint64_t(__popcll(__ballot(pend[u][0])) + __popcll(__ballot(pend[u][1])));
+        nwords += 2 * pc;
+        uint32_t g2[U][2][2], l2[U][2][2];
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
           for (int h = 0; h < 2; h++) {
-            uint32_t dummy = 0u;
-            w[u][h][2] = ld_(off(int32_t(b[u][h].x), pend[u][h], dummy, 2, hw[u][h][2]));
-            w[u][h][3] = ld_(off(int32_t(b[u][h].y), pend[u][h], dummy, 3, hw[u][h][3]));
-            if (HUB) {
-#pragma unroll
-              for (int k = 2; k < 4; k++) {
-                const uint32_t lw = s_fb[hw[u][h][k] < 0 ? 0 : hw[u][h][k]];
-                w[u][h][k] = hw[u][h][k] < 0 ? w[u][h][k] : lw;
-              }
-            }
+            uint32_t d0 = 0u, d1 = 0u;
+            prep(b[u][h].x, 0, g2[u][h][0], l2[u][h][0], d0, d1);
+            prep(b[u][h].y, 1, g2[u][h][1], l2[u][h][1], d0, d1);
           }
+        uint32_t lv[U][2][2], gv[U][2][2];
+        if (HUB) {
+#pragma unroll
+          for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int h = 0; h < 2; h++)
+#pragma unroll
+              for (int k = 0; k < 2; k++) lv[u][h][k] = s_fb[l2[u][h][k]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+          for (int h = 0; h < 2; h++)
+#pragma unroll
+            for (int k = 0; k < 2; k++) gv[u][h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, g2[u][h][k], 0, 0);
 #pragma unroll
         for (int u = 0; u < U; u++)
 #pragma unroll
           for (int h = 0; h < 2; h++) {
-            const bool g = hit(w[u][h][2], int32_t(b[u][h].x)) || hit(w[u][h][3], int32_t(b[u][h].y));
-            nwords += pend[u][h] ? 2u : 0u;
+            const uint32_t w0 = HUB ? (lv[u][h][0] | gv[u][h][0]) : gv[u][h][0];
+            const uint32_t w1 = HUB ? (lv[u][h][1] | gv[u][h][1]) : gv[u][h][1];
+            const bool g = (bit(w0, b[u][h].x) | bit(w1, b[u][h].y)) != 0u;
             f[u][h] = f[u][h] || (pend[u][h] && g);
             // still pending: not found in the second half and a fifth entry may exist
-            pend[u][h] = pend[u][h] && !g && int32_t(b[u][h].y) >= 0;
+            pend[u][h] = pend[u][h] && !g && b[u][h].y != 0xffffffffu;
           }
       } else {
 #pragma unroll
@@ -1026,12 +1052,9 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
         nbits[2 * t + lane] = lane ? f1 : f0;
         pbits[2 * t + lane] = lane ? p1 : p0;
       }
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        nfound += f[u][h];
-        npend += pend[u][h];
-        if (!FINAL) odsum += f[u][h] ? od[u][h] : 0u;
-      }
+      nfound += uint64_t(__popcll(f0) + __popcll(f1));
+      npend += uint64_t(__popcll(p0) + __popcll(p1));
+      if (!FINAL) odsum += uint64_t(f[u][0] ? od[u][0] : 0u) + uint64_t(f[u][1] ? od[u][1] : 0u);
     }
   }
   // tiles past the live rows (non-final hops): nothing can be found there
@@ -1040,6 +1063,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
       nbits[2 * t + lane] = 0ull;
       pbits[2 * t + lane] = 0ull;
     }
+  // wave-uniform counters enter the block sums once, from lane 0
+  if (lane != 0) nfound = npend = nwords = 0;
   unsigned long long acc64[8] = {nfound, odsum, nwords, npend, 0, 0, nglob, nhub};
   block_store_partials(acc64, 8, lds, partials);
 }
@@ -1704,6 +1729,43 @@ struct Counters {
   unsigned long long* h;  // pinned host mirror (64 entries)
 };
 
+// Copies n device counters into coherent host memory, then the sequence word: each thread's
+// store is made visible system-wide before thread 0 publishes the sequence number.
+__global__ void k_publish(const unsigned long long* __restrict__ src, int n, unsigned long long* dst,
+                          unsigned long long* seq_slot, unsigned long long seq) {
+  const int i = threadIdx.x;
+  if (i < n) {
+    dst[i] = src[i];
+    __threadfence_system();
+  }
+  __syncthreads();
+  if (i == 0) {
+    __threadfence_system();
+    __hip_atomic_store(seq_slot, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// the device counters d[0, n) into host h[0, n) once every launch before has finished: a
+// one-thread-block kernel writes them and a sequence word to coherent host memory and the host
+// spins on the word (a memcpy + hipStreamSynchronize round trip cost ~19 us, tools/launch_gap);
+// past 2 s without it the stream is synchronised the ordinary way, which reports a fault
+void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h) {
+  if (n > 64) throw Error(NBG_E_INVALID_ARG, "fetch_counters: at most 64 words");
+  const uint64_t seq = ++c.pub_seq;
+  k_publish<<<1, 64, 0, c.stream>>>(d, n, h, c.host_seq, seq);
+  NBG_HIP(hipGetLastError());
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spin = 0;; spin++) {
+    if (__atomic_load_n(c.host_seq, __ATOMIC_ACQUIRE) == seq) return;
+    if ((spin & 1023u) == 1023u &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+      NBG_HIP(hipStreamSynchronize(c.stream));  // a fault surfaces here
+      if (__atomic_load_n(c.host_seq, __ATOMIC_ACQUIRE) == seq) return;
+      throw Error(NBG_E_DEVICE, "counter publication lost");
+    }
+  }
+}
+
 int64_t map_bytes(const Ctx& c) { return ((c.n_global + 63) / 64) * 64 + 64; }
 
 void ensure_workspaces(Ctx& c, int64_t nF_cap) {
@@ -1950,7 +2012,10 @@ void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* 
 }
 
 // records a pooled timing event on the query stream; returns its pool index
+constexpr size_t kNoEvent = ~size_t(0);
+// an event recorded on the engine stream for deferred hop timing (kNoEvent: hop_timing off)
 size_t timing_event(Ctx& c) {
+  if (!c.hop_timing) return kNoEvent;
   if (c.tev_used == c.tev.size()) {
     hipEvent_t e;
     NBG_HIP(hipEventCreate(&e));
@@ -1978,7 +2043,7 @@ void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Progr
   }
   NBG_HIP(hipGetLastError());
   const size_t ib = timing_event(c);
-  c.tpend.push_back(Ctx::PendingTime{ia, ib, c.timing.n_hops});  // read by timing_resolve
+  c.tpend.push_back(Ctx::PendingTime{ia, ib, c.timing.n_hops, 0});  // read by timing_resolve
   c.timing.expand_launches++;
 }
 
@@ -2045,8 +2110,8 @@ QArgs make_qargs(const EdgeSpace& es, int pk, int fcol, const FastArgs& fp) {
 // non-final hop: odeg keeps found rows with out-edges and sums their degrees) or PK_FAST (the
 // final hop's typed compare on transposed column fcol; decided from the packed buckets when fcol
 // is the packed column, else every value of a frontier hit is read by the rest pass).
-void launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
-                    const FastArgs& fp, int fcol, unsigned long long* out, hipEvent_t after_kernel) {
+size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
+                      const FastArgs& fp, int fcol, unsigned long long* out) {
   const Csr& tr = es.tr;
   if (pk != PK_NONE && pk != PK_FAST) throw Error(NBG_E_DEVICE, "bottom-up hop with a VM predicate");
   if (!es.pair_col[0].p) throw Error(NBG_E_DEVICE, "bottom-up hop without the quad slab");
@@ -2077,7 +2142,9 @@ void launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
   const int grid = int(std::max<int64_t>(
       1, std::min<int64_t>((waves + bs / 64 - 1) / (bs / 64),
                            std::min<int64_t>(cw > 0 ? 512 : c.opt("bu_lean_grid", 2048), kAggBlocks / 2))));
-  const size_t shm = size_t(std::max(cw, 1)) * 4;
+  const size_t shm = size_t(cw + 1) * 4;  // + the zero word non-hub probes read
+  const uint32_t fb_bytes = uint32_t(fb_words * 4);
+  const int probe_stats = int(c.opt("bu_probe_stats", 0));  // partials [6] / [7]
   c.ws_pend.ensure(size_t(ntiles * 2 + 2) * 8);  // the pending bits, 2 words per tile
   unsigned long long* pbits = c.ws_pend.as<unsigned long long>();
   unsigned long long* partials = c.ws_partials.as<unsigned long long>();
@@ -2088,15 +2155,17 @@ void launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
   auto go = [&](auto kern) {
     if (shm > 48 * 1024)
       lds_limit(reinterpret_cast<const void*>(kern), shm);
-    kern<<<grid, bs, shm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, od, q, partials, cw);
+    kern<<<grid, bs, shm, c.stream>>>(lo, hi, ntiles, work, fb, fb_bytes, nb, pbits, od, q, partials, cw);
   };
-  const int sel = (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
-#define NBG_LEAN(PKV)                               \
-  switch (sel) {                                    \
-    case 0: go(k_bu_lean<PKV, 1, 0>); break;        \
-    case 1: go(k_bu_lean<PKV, 2, 0>); break;        \
-    case 2: go(k_bu_lean<PKV, 1, 1>); break;        \
-    default: go(k_bu_lean<PKV, 2, 1>); break;       \
+  const int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
+#define NBG_LEAN(PKV)                                \
+  switch (sel) {                                     \
+    case 0: go(k_bu_lean<PKV, 1, 0, 0>); break;      \
+    case 1: go(k_bu_lean<PKV, 2, 0, 0>); break;      \
+    case 2: go(k_bu_lean<PKV, 1, 1, 0>); break;      \
+    case 3: go(k_bu_lean<PKV, 2, 1, 0>); break;      \
+    case 4: go(k_bu_lean<PKV, 1, 0, 1>); break;      \
+    default: go(k_bu_lean<PKV, 1, 1, 1>); break;     \
   }
   if (fast) {
     NBG_LEAN(PK_FAST)
@@ -2105,13 +2174,15 @@ void launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
   }
 #undef NBG_LEAN
   NBG_HIP(hipGetLastError());
-  NBG_HIP(hipEventRecord(c.ev[7], c.stream));  // end of the first pass
+  const size_t ev_first = timing_event(c);  // end of the first pass (the hop's kernel_ms)
   const int64_t* trp = tr.row_ptr.as<int64_t>();
   const int32_t* tc = q.gbits ? es.tcol_q.as<int32_t>() : tr.col.as<int32_t>();
   const int ru = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_unroll", 1), kRestMax)));
   const int grid2 = int(std::min<int64_t>(c.opt("bu_rest_grid", 512), kAggBlocks / 2));
   const int W = fast ? int(fp.width) : 0;
-  const int rcw = int(std::min<int64_t>(c.opt(fast ? "bu_rest_lds_kb_final" : "bu_rest_lds_kb", fast ? 64 : 0) * 256,
+  // the rest pass probes global memory only by default: its hub copy cost each block ~6 us of
+  // LDS fill (r04h/r04k sweeps: 0.637 -> 0.625 ms per C3 query without it)
+  const int rcw = int(std::min<int64_t>(c.opt(fast ? "bu_rest_lds_kb_final" : "bu_rest_lds_kb", 0) * 256,
                                         std::min<int64_t>({fb_words, int64_t(36 * 1024), hub_cap})));
   const size_t rshm = size_t(std::max(rcw, 1)) * 4;
   const int rsteps = int(std::max<int64_t>(1, c.opt("bu_rest_steps", 4)));
@@ -2144,7 +2215,6 @@ void launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
   }
 #undef NBG_REST
   NBG_HIP(hipGetLastError());
-  if (after_kernel) NBG_HIP(hipEventRecord(after_kernel, c.stream));
   k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid + grid2, out);
   NBG_HIP(hipGetLastError());
   if (dbg) {
@@ -2161,11 +2231,13 @@ void launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, 
     }
   }
   char nm[96];
-  snprintf(nm, sizeof nm, "nbg::k_bu_lean<%d, %d, %d>", pk, U, cw > 0 ? 1 : 0);
+  snprintf(nm, sizeof nm, "nbg::k_bu_lean<%d, %d, %d, %d>", pk, probe_stats ? 1 : U, cw > 0 ? 1 : 0,
+           probe_stats ? 1 : 0);
   c.bu_kernel_name = nm;
   const int wn = fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0;
   snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d>", pk, wn, rcw > 0 ? 1 : 0);
   c.bu_rest_name = nm;
+  return ev_first;
 }
 
 // byte models of a bottom-up hop's two passes from their counters.
@@ -2203,6 +2275,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   Csr& csr = es.out;
   c.timing = Timing{};
   timing_reset(c);
+  // per-hop event pairs (hop stats); bench.py's timed loop turns them off like a production
+  // caller would, its statistics loop on
+  c.hop_timing = c.opt("hop_timing", 1) != 0;
   if (c.host_stage_used) NBG_HIP(hipStreamSynchronize(c.stream));  // a failed query's copies
   c.host_stage_used = 0;
   hipEventRecord(c.ev[0], c.stream);
@@ -2301,8 +2376,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         k_starts_degree<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, K.d + 30);
     }
     NBG_HIP(hipGetLastError());
-    NBG_HIP(hipMemcpyAsync(K.h, K.d, 256, hipMemcpyDeviceToHost, c.stream));
-    NBG_HIP(hipStreamSynchronize(c.stream));
+    fetch_counters(c, K.d, 32, K.h);
     nF = int64_t(K.h[0]);
     if (!(s.steps == 1 && !s.distinct)) {
       E_known = int64_t(K.h[13]);
@@ -2437,8 +2511,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     if (list_n >= 0) {
       nF = list_n;  // counted by the compaction that wrote the bitmap: no round trip
     } else {
-      NBG_HIP(hipMemcpyAsync(K.h, K.d, 8, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
+      fetch_counters(c, K.d, 1, K.h);
       nF = int64_t(K.h[0]);
     }
     list_n = -1;
@@ -2469,20 +2542,17 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // bottom-up: frontier bitmap in, next frontier bitmap out
       const Csr& tr = es.tr;
       const uint32_t* fb = global_bits(c, bitsA);
-      hipEventRecord(c.ev[2], c.stream);
-      launch_bu_lean(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, K.d, c.ev[6]);
-      hipEventRecord(c.ev[3], c.stream);
-      NBG_HIP(hipMemcpyAsync(K.h, K.d, 64, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
-      float ms = 0, kms = 0;
-      hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
-      hipEventElapsedTime(&kms, c.ev[2], c.ev[7]);
-      c.timing.expand_ms += ms;
+      const size_t ia = timing_event(c);
+      const size_t ik = launch_bu_lean(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, K.d);
+      const size_t ib = timing_event(c);
+      c.tpend.push_back(Ctx::PendingTime{ia, ib, c.timing.n_hops, 0});
+      c.tpend.push_back(Ctx::PendingTime{ia, ik, c.timing.n_hops, 1});
+      fetch_counters(c, K.d, 8, K.h);
       c.timing.expand_launches++;
       c.timing.bu_steps++;
       const uint64_t kb = bu_first_bytes(K.h, tr.n_rows, true), hb = kb + bu_rest_bytes(K.h, 0);
       c.timing.expand_bytes += hb;
-      c.timing.hop(1, false, ms, K.h, kms, kb);
+      c.timing.hop(1, false, 0.0, K.h, 0.0, kb);
       c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name);
       std::swap(bitsA, bitsB);
       have_list = false;
@@ -2528,8 +2598,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const bool lazy = c.world == 1 && bu_ok && !multi_root && c.opt("compact_list", 0) == 0;
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
                      K.d, es.odeg.as<uint32_t>());
-      NBG_HIP(hipMemcpyAsync(K.h, K.d, 128, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
+      fetch_counters(c, K.d, 16, K.h);
       nF = lazy ? 0 : int64_t(K.h[0]);
       list_n = lazy ? int64_t(K.h[14]) : -1;
       E = int64_t(K.h[13]);
@@ -2587,18 +2656,15 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         const Csr& tr = es.tr;
         NBG_HIP(hipMemsetAsync(K.d, 0, 8, c.stream));
         const uint32_t* fb = global_bits(c, bitsA);
-        hipEventRecord(c.ev[2], c.stream);
-        launch_bu_lean(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8, c.ev[6]);
+        const size_t ia = timing_event(c);
+        const size_t ik = launch_bu_lean(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8);
         k_bits_compact<1><<<grid_cap((tr.n_rows + 31) / 32, 4096, 4096), 1024, 0, c.stream>>>(
             bitsB, tr.n_rows, lo, c.vid_of.as<int64_t>(), vids.p, K.d);
         NBG_HIP(hipGetLastError());
-        hipEventRecord(c.ev[3], c.stream);
-        NBG_HIP(hipMemcpyAsync(K.h, K.d, 128, hipMemcpyDeviceToHost, c.stream));
-        NBG_HIP(hipStreamSynchronize(c.stream));  // K.h is pinned: the copy is truly asynchronous
-        float ms = 0, kms = 0;
-        hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
-        hipEventElapsedTime(&kms, c.ev[2], c.ev[7]);
-        c.timing.expand_ms += ms;
+        const size_t ib = timing_event(c);
+        c.tpend.push_back(Ctx::PendingTime{ia, ib, c.timing.n_hops, 0});
+        c.tpend.push_back(Ctx::PendingTime{ia, ik, c.timing.n_hops, 1});
+        fetch_counters(c, K.d, 16, K.h);
         c.timing.expand_launches++;
         c.timing.bu_steps++;
         nrows = int64_t(K.h[0]);
@@ -2606,7 +2672,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         const uint64_t kb = bu_first_bytes(K.h + 8, tr.n_rows, false), hb = kb + bu_rest_bytes(K.h + 8, pw);
         // + the DISTINCT _dst output (k_bits_compact<1>): next bits once, vid_of read + vid written
         c.timing.expand_bytes += hb + uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
-        c.timing.hop(1, true, ms, K.h + 8, kms, kb);
+        c.timing.hop(1, true, 0.0, K.h + 8, 0.0, kb);
         c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name, "nbg::k_bits_compact<1>");
       } else {
         ensure_off();
@@ -2625,8 +2691,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         lst.alloc(size_t(n_own + 64) * 4);
         NBG_HIP(hipMemsetAsync(K.d, 0, 16, c.stream));  // keep the eval-error counter (K.d[4])
         launch_compact(c, map, lo, n_own, row_ptr, nullptr, 0, lst.as<int32_t>(), nullptr, K.d);
-        NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
-        NBG_HIP(hipStreamSynchronize(c.stream));
+        fetch_counters(c, K.d, 6, K.h);
         int64_t errs = int64_t(K.h[4]);
         allsum(c, &errs, 1, red);
         if (errs) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
@@ -2665,8 +2730,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       NBG_HIP(hipMemsetAsync(K.d, 0, 48, c.stream));
       const double ms0 = c.timing.expand_ms;
       if (E > 0) launch_expand<EXP_ROWS>(c, a, pk, fp, dprog.as<Program>(), env, E);
-      NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
+      fetch_counters(c, K.d, 6, K.h);
       int64_t errs = int64_t(K.h[4]);
       allsum(c, &errs, 1, red);
       if (errs) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
@@ -2707,8 +2771,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         }
         NBG_HIP(hipGetLastError());
       }
-      NBG_HIP(hipMemcpyAsync(K.h, K.d, 48, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
+      fetch_counters(c, K.d, 6, K.h);
       int64_t yerr = int64_t(K.h[5]);
       allsum(c, &yerr, 1, red);
       if (yerr) throw Error(NBG_E_EVAL, "YIELD evaluation failed");
@@ -2821,12 +2884,24 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       h->cols.push_back(h->dev[cc].p);
     } else {
       size_t w = h->types[cc] == NBG_T_BOOL ? 1 : 8;
-      h->host.emplace_back(size_t(nrows) * w + 8);
-      if (nrows) NBG_HIP(hipMemcpy(h->host.back().data(), h->dev[cc].p, size_t(nrows) * w, hipMemcpyDeviceToHost));
-      h->cols.push_back(h->host.back().data());
+      const size_t bytes = size_t(nrows) * w + 8;
+      if (bytes <= size_t(std::max<int64_t>(0, c.opt("host_pinned_mb", 4096))) << 20) {
+        h->hpin.emplace_back();
+        h->hpin.back().alloc(c.host_pool, bytes);
+        if (nrows)
+          NBG_HIP(hipMemcpyAsync(h->hpin.back().p, h->dev[cc].p, size_t(nrows) * w, hipMemcpyDeviceToHost, c.stream));
+        h->cols.push_back(h->hpin.back().p);
+      } else {  // very large results (RMAT-28's 21 GB of rows): pageable, through the driver
+        h->host.emplace_back(bytes);
+        if (nrows) NBG_HIP(hipMemcpy(h->host.back().data(), h->dev[cc].p, size_t(nrows) * w, hipMemcpyDeviceToHost));
+        h->cols.push_back(h->host.back().data());
+      }
     }
   }
-  if (!on_dev) h->dev.clear();
+  if (!on_dev) {
+    NBG_HIP(hipStreamSynchronize(c.stream));  // the pinned copies above
+    h->dev.clear();
+  }
   fill_rows(out, h, nrows, on_dev);
   out->edges_scanned = c.timing.edges_scanned;
   return NBG_OK;
@@ -2840,9 +2915,15 @@ void timing_reset(Ctx& c) {
 void timing_resolve(Ctx& c) {
   for (const auto& p : c.tpend) {
     float ms = 0;
+    if (p.a == kNoEvent || p.b == kNoEvent) continue;
     if (hipEventSynchronize(c.tev[p.b]) == hipSuccess && hipEventElapsedTime(&ms, c.tev[p.a], c.tev[p.b]) == hipSuccess) {
+      const bool in_hop = p.hop >= 0 && p.hop < c.timing.n_hops && p.hop < NBG_MAX_HOP_STATS;
+      if (p.kind == 1) {  // a bottom-up hop's first pass
+        if (in_hop) c.timing.hops[p.hop].kernel_ms += ms;
+        continue;
+      }
       c.timing.expand_ms += ms;
-      if (p.hop >= 0 && p.hop < c.timing.n_hops && p.hop < NBG_MAX_HOP_STATS) {
+      if (in_hop) {
         c.timing.hops[p.hop].ms += ms;
         if (c.timing.hops[p.hop].mode == 0) c.timing.hops[p.hop].kernel_ms += ms;  // k_expand is the hop
       }

@@ -514,7 +514,7 @@ def test_rmat_bottom_up_shapes(rmat12, u, lds, rest_lds, rsteps, unroll, cap):
             assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
             assert g.edges_scanned == r_.edges_scanned
             ks = final_bu_kernels(sp)
-            assert ks[0] == f"nbg::k_bu_lean<1, {u}, {1 if lds else 0}>", ks
+            assert ks[0] == f"nbg::k_bu_lean<1, {u}, {1 if lds else 0}, 0>", ks
             assert ks[1].startswith("nbg::k_bu_rest_lean<1, "), ks
             pending += sum(h["c"][3] for h in sp.last_timing()["hops"] if h["mode"] == "bottom-up")
     assert pending > 0  # the rest pass had rows to scan
@@ -522,12 +522,12 @@ def test_rmat_bottom_up_shapes(rmat12, u, lds, rest_lds, rsteps, unroll, cap):
     g = sp.go(starts, 3, FOLLOW, yields=[X.EdgeDst("follow")], distinct=True)
     r_ = st.go(starts, 3, FOLLOW, yields=[X.EdgeDst("follow").encode()], distinct=True)
     assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
-    assert final_bu_kernels(sp)[0] == f"nbg::k_bu_lean<1, {u}, {1 if lds else 0}>"
+    assert final_bu_kernels(sp)[0] == f"nbg::k_bu_lean<1, {u}, {1 if lds else 0}, 0>"
     g = sp.go(starts, 3, FOLLOW)
     r_ = st.go(starts, 3, FOLLOW)
     assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
     hops = [h for h in sp.last_timing()["hops"] if h["mode"] == "bottom-up"]
-    assert hops and hops[0]["kernels"][0] == f"nbg::k_bu_lean<0, {u}, {1 if lds else 0}>"
+    assert hops and hops[0]["kernels"][0] == f"nbg::k_bu_lean<0, {u}, {1 if lds else 0}, 0>"
 
 
 OPS = {">": lambda c, k: c > k, ">=": lambda c, k: c >= k, "<": lambda c, k: c < k, "<=": lambda c, k: c <= k,

@@ -105,6 +105,7 @@ def test_every_operator_default_path_rmat20(rmat20, op, hub_cap):
     wcol = X.AliasProp("follow", "weight")
     if hub_cap:
         sp.set_option("bu_hub_cap", hub_cap)
+        sp.set_option("bu_probe_stats", 1)  # the counting instantiation: c[6] / c[7]
     l2_probes = 0
     try:
         for k in (0, 15, 16, 499, 998, 999):
@@ -118,6 +119,7 @@ def test_every_operator_default_path_rmat20(rmat20, op, hub_cap):
             l2_probes += hops[-1]["c"][6]
     finally:
         sp.unset_option("bu_hub_cap")
+        sp.unset_option("bu_probe_stats")
     assert l2_probes > 0 or not hub_cap  # first-pass probes answered by L2
 
 
