@@ -507,6 +507,7 @@ static void reset_edge_derived(EdgeSpace& es) {
   es.q_gbits = es.q_bits = 0;
   for (int h = 0; h < 2; h++) es.pair_col[h].release();
   es.odeg.release();
+  es.max_odeg = -1;
 }
 
 static void reset_derived(Ctx& c) {
@@ -1532,6 +1533,7 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
   NBG_HIP(hipMemcpyAsync(&last_live, dmax.as<unsigned int>() + 2, 8, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
   es.bu_live_tiles = int64_t((last_live + 127) / 128);
+  es.max_odeg = int64_t(maxd);
   if (G > 1) maxd = UINT32_MAX;  // other ranks' degrees may exceed the local maximum
   // the transposed edge list: tdst (local row), tsrc (global), and the order props come in
   DevBuf tdst, tsrc;

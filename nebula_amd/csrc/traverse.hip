@@ -864,7 +864,7 @@ __device__ inline void bu_rest_scan(const bool (&pend)[R], bool (&found)[R], con
 // HUB: the block keeps the first cw words of the bitmap (the highest-out-degree vertices) in LDS
 // and answers candidates there from it; the global probe of such a slot is out of bounds.
 // Partials [6] / [7]: candidate probes sent to L2 / answered from LDS.
-template <int PK, int U, int HUB, int STATS>
+template <int PK, int U, int HUB, int STATS, int NT = 0>
 __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ lo, const uint2* __restrict__ hi,
                                                      int64_t ntiles, int64_t work_tiles,
                                                      const uint32_t* __restrict__ fbits, uint32_t fb_bytes,
@@ -925,9 +925,19 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
       const int64_t r = (v[u] ? t0 + u : t0) * 128 + lane;  // a past-the-end tile re-reads t0 (discarded)
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        a[u][h] = lo[r + 64 * h];
-        if (FINAL) b[u][h] = hi[r + 64 * h];
-        od[u][h] = FINAL ? 1u : odeg[r + 64 * h];
+        if (NT) {  // the slab and degrees are read once per hop: keep L2 for the bitmap probes
+          const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(lo + r + 64 * h));
+          a[u][h] = make_uint2(uint32_t(x), uint32_t(x >> 32));
+          if (FINAL) {
+            const uint64_t y = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(hi + r + 64 * h));
+            b[u][h] = make_uint2(uint32_t(y), uint32_t(y >> 32));
+          }
+          od[u][h] = FINAL ? 1u : __builtin_nontemporal_load(odeg + r + 64 * h);
+        } else {
+          a[u][h] = lo[r + 64 * h];
+          if (FINAL) b[u][h] = hi[r + 64 * h];
+          od[u][h] = FINAL ? 1u : odeg[r + 64 * h];
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -1066,6 +1076,129 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
   // wave-uniform counters enter the block sums once, from lane 0
   if (lane != 0) nfound = npend = nwords = 0;
   unsigned long long acc64[8] = {nfound, odsum, nwords, npend, 0, 0, nglob, nhub};
+  block_store_partials(acc64, 8, lds, partials);
+}
+
+// Final-hop first pass with the bucket tests as unsigned range checks on the raw slot word
+// (k_bu_lean's select chain cost ~19 vector instructions per slot; the r04d PMC pass showed its
+// waves busy issuing, 225 VALU per 128-row tile, the HBM stream at 4 TB/s).  FinArgs, host-built
+// per query (fin_args): a word is a candidate iff (w - clo) <= cr, it passes iff
+// ((w - plo) <= pr) != pinv (the bucket field sits above the gidx bits, so bucket ranges are
+// word ranges; the -1 pad word is either no candidate or probes past the bitmap).  A candidate's
+// probe byte offset is (w >> 3) & bmask, a non-candidate's kNoProbe; the global probe reads
+// through a resource based cw words into the bitmap (hub words wrap out of bounds: the hardware
+// returns 0), the LDS probe reads min(offset, 4 cw) (the zero word past the hub copy).
+struct FinArgs {
+  uint32_t clo = 0, cr = 0xffffffffu, plo = 0, pr = 0xffffffffu;
+  uint32_t pinv = 0, bmask = 0xfffffffcu;
+};
+constexpr uint32_t kNoProbe = 0x0ffffff0u;
+// CLS 1: the candidates are every word from clo up and the passing ones every word from plo up
+// (pinv 0): the "greater than" compares, the benchmark's.  A non-candidate's offset then comes
+// from the sign of w - clo (all ones: past the bitmap and clamped to the zero word) instead of
+// a compare and a select, and the pass test is one compare.
+// NT: non-temporal slab loads (the slab is read once per hop; the bitmap the probes hit stays
+// in L2): 158 -> 148 us at C3.  Measured without gain (r04f/r04g): the next tile's slab loads
+// issued behind the current tile's probes, an interleaved 16-byte slab (one load per row), two
+// tiles per wave; with no probes at all the slab alone streams at 4.7 TB/s in this loop.
+template <int CLS, int NT>
+__global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo, const uint2* __restrict__ hi,
+                                                    int64_t ntiles,
+                                                    const uint32_t* __restrict__ fbits,
+                                                    unsigned long long* __restrict__ nbits,
+                                                    unsigned long long* __restrict__ pbits, FinArgs fa_arg,
+                                                    unsigned long long* __restrict__ partials, int cw,
+                                                    uint32_t fb_rest) {
+  // dynamic LDS only, so the hub copy starts at address 0 and a probe's LDS address is its
+  // clamped byte offset as it is: [0, cw) the bitmap's hub words, [cw] a zero word, then the
+  // block's partials scratch
+  extern __shared__ uint32_t s_fb[];
+  unsigned long long* lds = reinterpret_cast<unsigned long long*>(s_fb + ((cw + 2) & ~1));
+  for (int i = threadIdx.x; i <= cw; i += blockDim.x) s_fb[i] = i < cw ? fbits[i] : 0u;
+  __syncthreads();
+  const uint32_t clo = __builtin_amdgcn_readfirstlane(fa_arg.clo), cr = __builtin_amdgcn_readfirstlane(fa_arg.cr);
+  const uint32_t plo = __builtin_amdgcn_readfirstlane(fa_arg.plo), pr = __builtin_amdgcn_readfirstlane(fa_arg.pr);
+  const bool pinv = __builtin_amdgcn_readfirstlane(fa_arg.pinv) != 0;
+  const uint32_t bmask = __builtin_amdgcn_readfirstlane(fa_arg.bmask);
+  const uint32_t cw4 = __builtin_amdgcn_readfirstlane(uint32_t(cw) * 4u);
+  // global probes: the bitmap from word cw on (fb_rest bytes); offsets below it (hub words) wrap
+  // past the end
+  const __amdgpu_buffer_rsrc_t fb_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(fbits + cw), 0, int(__builtin_amdgcn_readfirstlane(fb_rest)), 0x00020000);
+  // the hub copy is the kernel's only LDS (dynamic, no static arrays), at LDS address 0: a
+  // probe's address is its clamped byte offset (a pointer form cost an add per probe)
+  typedef const __attribute__((address_space(3))) uint32_t* lds_u32p;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  unsigned long long nfound = 0, npend = 0, nwords = 0;  // wave-uniform
+  auto ld8 = [&](const uint2* p) -> uint2 {
+    if (!NT) return *p;
+    const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
+    return make_uint2(uint32_t(x), uint32_t(x >> 32));
+  };
+  auto load = [&](int64_t t, uint32_t (&sw)[2][4]) {
+    const int64_t r = t * 128 + lane;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const uint2 a = ld8(lo + r + 64 * h), b = ld8(hi + r + 64 * h);
+      sw[h][0] = a.x, sw[h][1] = a.y, sw[h][2] = b.x, sw[h][3] = b.y;
+    }
+  };
+  for (int64_t t = wave; t < ntiles; t += nwaves) {
+    uint32_t sw[2][4];
+    load(t, sw);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t ob[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t w = sw[h][k];
+        if (CLS == 1)
+          ob[h][k] = ((w >> 3) & bmask) | uint32_t(int32_t(w - clo) >> 31);
+        else
+          ob[h][k] = w - clo <= cr ? (w >> 3) & bmask : kNoProbe;
+      }
+    uint32_t lw[2][4], gw[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+      for (int k = 0; k < 4; k++) lw[h][k] = *(lds_u32p)(size_t(min(ob[h][k], cw4)));
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+      for (int k = 0; k < 4; k++) gw[h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, ob[h][k] - cw4, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    bool f[2], pend[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      bool fh = false, ah = false;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t w = sw[h][k];
+        const bool hit = __builtin_amdgcn_ubfe(lw[h][k] | gw[h][k], w, 1u) != 0u;
+        const bool pass = CLS == 1 ? w >= plo : (w - plo <= pr) != pinv;
+        fh = fh || (hit && pass);
+        ah = ah || hit;
+      }
+      f[h] = fh;
+      // pending: no passing hit, and a hit (then in an undecided bucket) or a fifth entry
+      // (slot 3 set)
+      pend[h] = !fh && (ah || sw[h][3] != 0xffffffffu);
+    }
+    const unsigned long long f0 = __ballot(f[0]), f1 = __ballot(f[1]);
+    const unsigned long long p0 = __ballot(pend[0]), p1 = __ballot(pend[1]);
+    if (lane < 2) {
+      nbits[2 * t + lane] = lane ? f1 : f0;
+      pbits[2 * t + lane] = lane ? p1 : p0;
+    }
+    nfound += uint64_t(__popcll(f0) + __popcll(f1));
+    npend += uint64_t(__popcll(p0) + __popcll(p1));
+    nwords += 8u * 64u;
+  }
+  if (lane != 0) nfound = npend = nwords = 0;
+  unsigned long long acc64[8] = {nfound, 0, nwords, npend, 0, 0, 0, 0};
   block_store_partials(acc64, 8, lds, partials);
 }
 
@@ -1469,6 +1602,92 @@ __global__ void k_starts_bits(const int32_t* g, int64_t n, int64_t lo, int64_t h
 }
 
 // starts (gidx) -> mark owned in the byte-map (dedup path) or list them (steps == 1 path)
+// One-block start frontier for a few starts (ns <= kSmallStarts, one rank), everything the
+// first top-down hop needs in one launch instead of a lookup, three memsets, the bitmap dedup, a
+// degree pass, a scan and a counter round trip: zero the query counters Kd[0, 64), look the
+// start vids up (gidx -> g), dedup through the start words of the frontier bitmap (only those
+// words are cleared: a top-down first hop never reads the rest, k_compact rewrites it all), keep
+// starts with out-edges (row_ok) as the list F, write its exclusive degree scan to off[0, ns]
+// (entries past the list: degree 0, row 0) and the counts: Kd[40] list length, Kd[41] its
+// out-degree sum, Kd[30] the degree sum over every start with duplicates (hop-1 rows of a
+// query without DISTINCT rescan duplicate starts, QueryBaseProcessor.inl:462-505).
+constexpr int kSmallStarts = 4096;
+__global__ __launch_bounds__(1024) void k_starts_small(const int64_t* __restrict__ vids, int32_t ns, const int64_t* keys,
+                                                       const int32_t* vals, uint64_t mask, bool has_min,
+                                                       int32_t min_gidx, int32_t* __restrict__ g, int64_t lo,
+                                                       int64_t hi, const int64_t* __restrict__ row_ptr,
+                                                       const uint8_t* __restrict__ row_ok, uint32_t* bits,
+                                                       int32_t* __restrict__ F, int64_t* __restrict__ off,
+                                                       unsigned long long* __restrict__ Kd) {
+  __shared__ int32_t s_loc[kSmallStarts];
+  __shared__ unsigned long long s_w[16];
+  __shared__ unsigned long long s_carry[2];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < 64) Kd[tid] = 0ull;
+  for (int i = tid; i < ns; i += blockDim.x) {
+    const int32_t x = ht_lookup(keys, vals, mask, vids[i], has_min, min_gidx);
+    g[i] = x;
+    int32_t loc = -1;
+    if (x >= lo && x < hi && (row_ok == nullptr || row_ok[x - lo]) && row_ptr[x - lo + 1] > row_ptr[x - lo])
+      loc = int32_t(x - lo);
+    s_loc[i] = loc;
+    if (loc >= 0) bits[loc >> 5] = 0u;
+  }
+  if (tid < 2) s_carry[tid] = 0ull;
+  __syncthreads();
+  unsigned long long scanned = 0;  // every start's degree, duplicates included
+  for (int i0 = 0; i0 < ns; i0 += blockDim.x) {
+    const int i = i0 + tid;
+    const int32_t loc = i < ns ? s_loc[i] : -1;
+    const unsigned long long d = loc >= 0 ? (unsigned long long)(row_ptr[loc + 1] - row_ptr[loc]) : 0ull;
+    scanned += d;
+    bool keep = false;
+    if (loc >= 0) {
+      const uint32_t bit = 1u << (loc & 31);
+      keep = !(atomicOr(bits + (loc >> 5), bit) & bit);
+    }
+    // block prefix of (kept count, kept degree): wave inclusive scans, then the wave totals
+    unsigned long long kc = keep ? 1ull : 0ull, kd = keep ? d : 0ull;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long a = __shfl_up(kc, o), b = __shfl_up(kd, o);
+      if (lane >= o) kc += a, kd += b;
+    }
+    if (lane == 63) s_w[wv] = kc, s_w[8 + wv] = kd;  // at most 16 waves: 8 + 8 slots suffice
+    __syncthreads();
+    unsigned long long bc = s_carry[0], bd = s_carry[1], tc = 0, td = 0;
+    for (int w = 0; w < int(blockDim.x >> 6); w++) {
+      const unsigned long long wc = s_w[w], wd = s_w[8 + w];
+      if (w < wv) bc += wc, bd += wd;
+      tc += wc, td += wd;
+    }
+    if (keep) {
+      const unsigned long long pos = bc + kc - 1;
+      F[pos] = loc;
+      off[pos] = int64_t(bd + kd - d);
+    }
+    __syncthreads();
+    if (tid == 0) s_carry[0] += tc, s_carry[1] += td;
+    __syncthreads();
+  }
+  const unsigned long long nF = s_carry[0], E = s_carry[1];
+  for (int i = int(nF) + tid; i <= ns; i += blockDim.x) {
+    if (i < ns) F[i] = 0;
+    off[i] = int64_t(E);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) scanned += __shfl_xor(scanned, o);
+  if (lane == 0) s_w[wv] = scanned;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < int(blockDim.x >> 6); w++) t += s_w[w];
+    Kd[40] = nF;
+    Kd[41] = E;
+    Kd[30] = t;
+  }
+}
+
 __global__ void k_mark_gidx(const int32_t* g, int64_t n, int64_t lo, int64_t hi, uint8_t* map) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
     int32_t x = g[i];
@@ -2105,6 +2324,49 @@ QArgs make_qargs(const EdgeSpace& es, int pk, int fcol, const FastArgs& fp) {
   return q;
 }
 
+// k_bu_fin's word ranges from a query's bucket decisions (q_test: buckets below ulo answer
+// `below`, above uhi `above`, the rest are undecided).  The field above the gidx bits is the
+// bucket; every decision region is a contiguous field range, so each set is one word range.
+FinArgs fin_args(const QArgs& q) {
+  FinArgs f;
+  const int gb = q.gbits;
+  f.bmask = (q.gmask >> 3) & ~3u;
+  if (gb <= 0) {  // unpacked words: no buckets (every word undecided, or no predicate at all)
+    f.clo = 0, f.cr = 0xffffffffu;
+    const bool all_pass = q.below == 1 && q.above == 1;
+    f.plo = 0, f.pr = 0xffffffffu, f.pinv = all_pass ? 0u : 1u;
+    return f;
+  }
+  const int64_t B = (int64_t(1) << (32 - gb)) - 1;  // largest field value (the -1 pad's)
+  const int64_t lo_end = std::min<int64_t>(std::max<int64_t>(q.ulo, 0), B + 1);  // [0, lo_end): below
+  const int64_t u_end = std::min<int64_t>(std::max<int64_t>(q.uhi, lo_end - 1), B);  // [lo_end, u_end]: undecided
+  auto word_lo = [&](int64_t a) { return uint32_t(uint64_t(a) << gb); };
+  auto word_hi = [&](int64_t b) { return uint32_t(((uint64_t(b) + 1) << gb) - 1); };
+  auto set_range = [&](int64_t a, int64_t b, uint32_t& lo, uint32_t& r) {  // field range [a, b], a <= b
+    lo = word_lo(a);
+    r = word_hi(b) - lo;
+  };
+  const bool c0 = q.below != 0, c2 = q.above != 0;  // below / above regions are candidates
+  if (c0 && c2) set_range(0, B, f.clo, f.cr);
+  else if (c0) set_range(0, u_end, f.clo, f.cr);
+  else if (c2) set_range(lo_end, B, f.clo, f.cr);
+  else if (lo_end <= u_end) set_range(lo_end, u_end, f.clo, f.cr);
+  else f.clo = 0xffffffffu, f.cr = 0;  // no candidate but the pad word (whose probe is out of bounds)
+  const bool p0 = q.below == 1 && lo_end > 0, p2 = q.above == 1 && u_end < B;
+  f.pinv = 0;
+  if (p0 && p2) {
+    if (lo_end <= u_end) set_range(lo_end, u_end, f.plo, f.pr), f.pinv = 1;  // all but the undecided
+    else f.plo = 0, f.pr = 0xffffffffu;
+  } else if (p0) {
+    set_range(0, lo_end - 1, f.plo, f.pr);
+  } else if (p2) {
+    set_range(u_end + 1, B, f.plo, f.pr);
+  } else {
+    f.plo = 0, f.pr = 0xffffffffu, f.pinv = 1;  // nothing passes
+  }
+  return f;
+}
+
 // bottom-up hop: the first pass (k_bu_lean) over the quad slab and the pending rows' rests in
 // k_bu_rest_lean; counters reduced into out[0..8) (no synchronisation).  pk: PK_NONE (a
 // non-final hop: odeg keeps found rows with out-edges and sums their degrees) or PK_FAST (the
@@ -2157,9 +2419,11 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
       lds_limit(reinterpret_cast<const void*>(kern), shm);
     kern<<<grid, bs, shm, c.stream>>>(lo, hi, ntiles, work, fb, fb_bytes, nb, pbits, od, q, partials, cw);
   };
-  const int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
+  int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
+  if (sel == 2 && c.opt("bu_lean_nt", 1) != 0) sel = 6;  // non-temporal slab loads
 #define NBG_LEAN(PKV)                                \
   switch (sel) {                                     \
+    case 6: go(k_bu_lean<PKV, 1, 1, 0, 1>); break;   \
     case 0: go(k_bu_lean<PKV, 1, 0, 0>); break;      \
     case 1: go(k_bu_lean<PKV, 2, 0, 0>); break;      \
     case 2: go(k_bu_lean<PKV, 1, 1, 0>); break;      \
@@ -2167,7 +2431,28 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     case 4: go(k_bu_lean<PKV, 1, 0, 1>); break;      \
     default: go(k_bu_lean<PKV, 1, 1, 1>); break;     \
   }
-  if (fast) {
+  const bool fin = fast && !probe_stats && c.opt("bu_fin", 1) != 0;
+  char fin_nm[64] = "";
+  if (fin) {
+    const FinArgs fa = fin_args(q);
+    // CLS 1 ("greater than"): candidates and passing words are each one upper range
+    const bool cls1 = fa.pinv == 0 && fa.cr == ~fa.clo && fa.pr == ~fa.plo && fa.clo <= 0x80000000u &&
+                      fa.plo <= 0x80000000u && c.opt("bu_fin_cls", 1) != 0;
+    const size_t fshm = size_t((cw + 2) & ~1) * 4 + size_t(kSlots) * 16 * 8;
+    const uint32_t rest = fb_bytes > uint32_t(cw) * 4u ? fb_bytes - uint32_t(cw) * 4u : 0u;
+    auto gof = [&](auto kern) {
+      if (fshm > 48 * 1024) lds_limit(reinterpret_cast<const void*>(kern), fshm);
+      kern<<<grid, bs, fshm, c.stream>>>(lo, hi, ntiles, fb, nb, pbits, fa, partials, cw, rest);
+    };
+    const int nt = int(c.opt("bu_fin_nt", 1) != 0);
+    switch ((cls1 ? 1 : 0) | nt << 1) {
+      case 0: gof(k_bu_fin<0, 0>); break;
+      case 1: gof(k_bu_fin<1, 0>); break;
+      case 2: gof(k_bu_fin<0, 1>); break;
+      default: gof(k_bu_fin<1, 1>); break;
+    }
+    snprintf(fin_nm, sizeof fin_nm, "nbg::k_bu_fin<%d, %d>", cls1 ? 1 : 0, nt);
+  } else if (fast) {
     NBG_LEAN(PK_FAST)
   } else {
     NBG_LEAN(PK_NONE)
@@ -2231,8 +2516,11 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     }
   }
   char nm[96];
-  snprintf(nm, sizeof nm, "nbg::k_bu_lean<%d, %d, %d, %d>", pk, probe_stats ? 1 : U, cw > 0 ? 1 : 0,
-           probe_stats ? 1 : 0);
+  if (fin)
+    snprintf(nm, sizeof nm, "%s", fin_nm);
+  else
+    snprintf(nm, sizeof nm, "nbg::k_bu_lean<%d, %d, %d, %d%s>", pk, probe_stats ? 1 : U, cw > 0 ? 1 : 0,
+             probe_stats ? 1 : 0, sel == 6 ? ", 1" : "");
   c.bu_kernel_name = nm;
   const int wn = fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0;
   snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d>", pk, wn, rcw > 0 ? 1 : 0);
@@ -2329,6 +2617,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       yields.push_back(p);
     }
   }
+  bool uses_input = false;
+  for (int i = 0; i < where.n && has_where; i++) uses_input |= where.ins[i].op == P_INPUT;
+  for (auto& p : yields)
+    for (int i = 0; i < p.n; i++) uses_input |= p.ins[i].op == P_INPUT;
   const int64_t lo = c.owned_lo(), hi = c.owned_hi();
   const int64_t n_own = hi - lo;
   ensure_workspaces(c, std::max<int64_t>({n_own, int64_t(s.n_starts), 1}));
@@ -2347,9 +2639,18 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   c.ws_starts.ensure(size_t(std::max<int64_t>(ns, 1)) * 12 + 64);
   int64_t* d_starts = c.ws_starts.as<int64_t>();
   int32_t* d_sg = reinterpret_cast<int32_t*>(d_starts + std::max<int64_t>(ns, 1));
+  // a first hop that is certainly top-down (no transposed CSR, or even the ns largest
+  // out-degrees sum below the bottom-up threshold) from a few starts on one rank: one launch
+  // builds its frontier and degree scan (k_starts_small) and the hop runs without a round trip
+  // (the expansion reads the frontier size from the scan; the counts come back with the
+  // compaction's)
+  const bool td1_certain = !bu_ok || bu_force < 0 ||
+                           (bu_force == 0 && es.max_odeg >= 0 && ns * es.max_odeg < csr.nnz / bu_div);
+  const bool fast1 = ns > 0 && ns <= kSmallStarts && c.world == 1 && s.steps >= 2 && td1_certain &&
+                     !(uses_input && s.steps > 1) && c.opt("starts_small", 1) != 0;
   if (ns) {
     c.h2d(d_starts, s.starts, size_t(ns) * 8);
-    lookup_gidx(c, d_starts, d_sg, ns);
+    if (!fast1) lookup_gidx(c, d_starts, d_sg, ns);
   }
   int cur = 0;
   int64_t E_known = -1;  // frontier out-degree sum when a compaction already produced it
@@ -2357,8 +2658,17 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   int64_t nF = 0;
   int64_t nset_global = ns;  // "starts_ non-empty" (GoExecutor.cpp:93-97)
   int64_t hop1_scanned = -1;  // hop-1 rows with duplicate starts rescanned (k_starts_degree)
-  NBG_HIP(hipMemsetAsync(K.d, 0, 256, c.stream));
-  if (ns) {
+  if (fast1) {
+    k_starts_small<<<1, 1024, 0, c.stream>>>(d_starts, int32_t(ns), c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
+                                              uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, d_sg, lo, hi,
+                                              row_ptr, row_ok, reinterpret_cast<uint32_t*>(bits16), F,
+                                              c.ws_off.as<int64_t>(), K.d);
+    NBG_HIP(hipGetLastError());
+    nF = ns;  // an upper bound: the entries past the list have degree 0
+  } else {
+    NBG_HIP(hipMemsetAsync(K.d, 0, 256, c.stream));
+  }
+  if (ns && !fast1) {
     if (s.steps == 1 && !s.distinct) {
       k_list_starts<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, F, K.d);
     } else if (c.world == 1 && es.odeg.p && c.opt("starts_bits", 1) != 0) {
@@ -2420,10 +2730,6 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   a.mark_check = int32_t(c.opt("mark_check", 0));
   FastArgs fp{};
   EvalEnv env = make_env(c, es, csr, s.edge_type);
-  bool uses_input = false;
-  for (int i = 0; i < where.n && has_where; i++) uses_input |= where.ins[i].op == P_INPUT;
-  for (auto& p : yields)
-    for (int i = 0; i < p.n; i++) uses_input |= p.ins[i].op == P_INPUT;
   DevBuf in_keys, in_rows, in_tab;
   std::vector<DevBuf> in_cols;
   // STEPS > 1: graphd maps every dst of a non-final step back to a start (VertexBackTracker,
@@ -2531,11 +2837,50 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   auto want_bu = [&](int64_t eg) {  // (multi-step roots need every in-edge: top-down only)
     return eg > 0 && bu_ok && !multi_root && bu_force >= 0 && (bu_force > 0 || eg >= es.out_nnz_global / bu_div);
   };
-  ensure_off();
-  int64_t Eg = E;  // frontier out-degree sum over all ranks
-  allsum(c, &Eg, 1, red);
+  int64_t Eg = 0;  // frontier out-degree sum over all ranks
+  if (fast1) {
+    off_ready = true;  // k_starts_small wrote the scan; E is counted on the device
+  } else {
+    ensure_off();
+    Eg = E;
+    allsum(c, &Eg, 1, red);
+  }
   for (int32_t step = 1; step < s.steps; step++) {
     c.timing.steps_run++;
+    if (fast1 && step == 1) {
+      // the first hop top-down from k_starts_small's list (nF = ns bounds it), compaction, then
+      // one round trip for the start counts and the next frontier's together
+      a.F = F;
+      a.nF = nF;
+      a.off = c.ws_off.as<int64_t>();
+      const int64_t e_bound = std::max<int64_t>(1, es.max_odeg >= 0 ? ns * es.max_odeg : csr.nnz);
+      launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, std::min<int64_t>(e_bound, csr.nnz + 1));
+      cur ^= 1;
+      F = c.ws_front[cur].as<int32_t>();
+      const bool lazy = bu_ok && c.opt("compact_list", 0) == 0;
+      // (K.d[0, 4) are zero: k_starts_small cleared the counters)
+      launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
+                     K.d, es.odeg.as<uint32_t>());
+      fetch_counters(c, K.d, 42, K.h);
+      const int64_t nF1 = int64_t(K.h[40]), E1 = int64_t(K.h[41]);
+      if (!s.distinct) hop1_scanned = int64_t(K.h[30]);
+      c.timing.edges_scanned += uint64_t(hop1_scanned >= 0 ? hop1_scanned : E1);
+      if (E1 > 0) c.timing.expand_bytes += expand_bytes(nF1, E1, 0, EXP_MARK);
+      const unsigned long long hs[8] = {(unsigned long long)nF1, (unsigned long long)E1, 0, 0, 0, 0, 0, 0};
+      c.timing.hop(0, false, 0.0, hs);
+      if (E1 == 0) return finish_empty();  // every start lacks out-edges
+      nF = lazy ? 0 : int64_t(K.h[0]);
+      list_n = lazy ? int64_t(K.h[14]) : -1;
+      E = int64_t(K.h[13]);
+      E_known = E;
+      nset_global = int64_t(K.h[12]);
+      Eg = E;
+      have_list = !lazy;
+      if (lazy) cur ^= 1;  // ensure_list flips to the list buffer again
+      off_ready = false;
+      if (nset_global == 0) return finish_empty();  // onEmptyInputs (GoExecutor.cpp:392-395)
+      continue;
+    }
     c.timing.edges_scanned += uint64_t(step == 1 && hop1_scanned >= 0 ? hop1_scanned : E);
     if (Eg == 0) return finish_empty();  // every frontier vertex lacks out-edges
     if (want_bu(Eg)) {

@@ -350,6 +350,42 @@ def test_rmat_go_steps(rmat12, steps):
     assert g.edges_scanned == r.edges_scanned
 
 
+@pytest.mark.parametrize("small", [1, 0])
+def test_rmat_start_frontier_edge_cases(rmat12, small):
+    """the one-launch start frontier of a top-down first hop (k_starts_small, option starts_small)
+    and the multi-kernel path against the oracle: duplicate starts, vids not in the graph, starts
+    without out-edges, DISTINCT or not (hop-1 rows of a non-DISTINCT query rescan duplicate
+    starts), 4096 starts (the most the one-block kernel takes) and 4097 (the fallback path)"""
+    sp, st = rmat12
+    sp.set_option("starts_small", small)
+    s, d, _ = O.rmat_edges(12, 16, SEED)
+    no_out = sorted(set(d.tolist()) - set(s.tolist()))[:8]
+    assert no_out
+    base = seeds_from(12, 40, seed=31)
+    starts = base + base[:10] + [123456789, -5] + no_out
+    w = X.AliasProp("follow", "weight") > 499
+    y = [X.EdgeDst("follow")]
+    for steps in (2, 3):
+        g = sp.go(starts, steps, FOLLOW)
+        r = st.go(starts, steps, FOLLOW)
+        assert np.array_equal(np.sort(g.columns[0]), np.sort(r.int_col(0)))
+        assert g.edges_scanned == r.edges_scanned
+        g = sp.go(starts, steps, FOLLOW, where=w, yields=y, distinct=True)
+        r = st.go(starts, steps, FOLLOW, where=w.encode(), yields=[y[0].encode()], distinct=True)
+        assert np.array_equal(np.sort(g.columns[0]), np.sort(r.int_col(0)))
+        assert g.edges_scanned == r.edges_scanned
+    # only starts without out-edges: an empty first frontier
+    g = sp.go(no_out, 2, FOLLOW)
+    assert g.n_rows == 0 and st.go(no_out, 2, FOLLOW).nrows == 0
+    sp.set_option("bottom_up", 0)  # a top-down first hop is then certain at any start count
+    for n in (4096, 4097):
+        many = seeds_from(12, n, seed=n)
+        g = sp.go(many, 2, FOLLOW)
+        r = st.go(many, 2, FOLLOW)
+        assert np.array_equal(np.sort(g.columns[0]), np.sort(r.int_col(0)))
+        assert g.edges_scanned == r.edges_scanned
+
+
 def test_rmat_go_where_distinct(rmat12):
     sp, st = rmat12
     starts = seeds_from(12, 64)
@@ -493,17 +529,21 @@ def final_bu_kernels(sp):
     return hops[-1]["kernels"]
 
 
+@pytest.mark.parametrize("fin", [0, 1])
 @pytest.mark.parametrize("u,lds,rest_lds,rsteps,unroll,cap", [(1, 64, 64, 4, 1, 36 * 1024), (2, 64, 0, 1, 2, 36 * 1024),
                                                               (1, 0, 64, 2, 1, 36 * 1024), (2, 1, 1, 4, 2, 8)])
-def test_rmat_bottom_up_shapes(rmat12, u, lds, rest_lds, rsteps, unroll, cap):
-    """the bottom-up kernels (k_bu_lean first pass + k_bu_rest_lean) for every tile / LDS hub /
+def test_rmat_bottom_up_shapes(rmat12, u, lds, rest_lds, rsteps, unroll, cap, fin):
+    """the bottom-up kernels (k_bu_lean / k_bu_fin first pass + k_bu_rest_lean) for every tile / LDS hub /
     rest-chunk shape, non-final and final hops, thresholds that leave rows pending past the slab,
     against the oracle; the hop stats name the kernels that ran"""
     sp, st = rmat12
     for k, v in {"bu_force": 1, "bu_lean_u": u, "bu_lean_u_final": u, "bu_lean_lds_kb": lds,
                  "bu_lean_lds_kb_final": lds, "bu_rest_lds_kb": rest_lds, "bu_rest_lds_kb_final": rest_lds,
-                 "bu_rest_steps": rsteps, "bu_unroll": unroll, "bu_hub_cap": cap}.items():
+                 "bu_rest_steps": rsteps, "bu_unroll": unroll, "bu_hub_cap": cap, "bu_fin": fin}.items():
         sp.set_option(k, v)
+    # the final hop's first pass: k_bu_fin (the default) or k_bu_lean (bu_fin = 0; its
+    # non-temporal instantiation carries a fifth argument)
+    first = "nbg::k_bu_fin<" if fin else f"nbg::k_bu_lean<1, {u}, {1 if lds else 0}, 0"
     starts = sorted(set(seeds_from(12, 48, seed=23)))
     pending = 0
     for k in (0, 499, 990):
@@ -514,7 +554,7 @@ def test_rmat_bottom_up_shapes(rmat12, u, lds, rest_lds, rsteps, unroll, cap):
             assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
             assert g.edges_scanned == r_.edges_scanned
             ks = final_bu_kernels(sp)
-            assert ks[0] == f"nbg::k_bu_lean<1, {u}, {1 if lds else 0}, 0>", ks
+            assert ks[0].startswith(first), ks
             assert ks[1].startswith("nbg::k_bu_rest_lean<1, "), ks
             pending += sum(h["c"][3] for h in sp.last_timing()["hops"] if h["mode"] == "bottom-up")
     assert pending > 0  # the rest pass had rows to scan
@@ -522,32 +562,36 @@ def test_rmat_bottom_up_shapes(rmat12, u, lds, rest_lds, rsteps, unroll, cap):
     g = sp.go(starts, 3, FOLLOW, yields=[X.EdgeDst("follow")], distinct=True)
     r_ = st.go(starts, 3, FOLLOW, yields=[X.EdgeDst("follow").encode()], distinct=True)
     assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
-    assert final_bu_kernels(sp)[0] == f"nbg::k_bu_lean<1, {u}, {1 if lds else 0}, 0>"
+    assert final_bu_kernels(sp)[0].startswith(first)
     g = sp.go(starts, 3, FOLLOW)
     r_ = st.go(starts, 3, FOLLOW)
     assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
     hops = [h for h in sp.last_timing()["hops"] if h["mode"] == "bottom-up"]
-    assert hops and hops[0]["kernels"][0] == f"nbg::k_bu_lean<0, {u}, {1 if lds else 0}, 0>"
+    assert hops and hops[0]["kernels"][0].startswith(f"nbg::k_bu_lean<0, {u}, {1 if lds else 0}, 0")
 
 
 OPS = {">": lambda c, k: c > k, ">=": lambda c, k: c >= k, "<": lambda c, k: c < k, "<=": lambda c, k: c <= k,
        "==": lambda c, k: c.eq(k), "!=": lambda c, k: c.ne(k)}
 
 
+@pytest.mark.parametrize("fin", [0, 1])
 @pytest.mark.parametrize("qpred", [1, 0])
 @pytest.mark.parametrize("hub_cap", [36 * 1024, 16])
-def test_rmat_bottom_up_packed_predicate(rmat12, qpred, hub_cap):
-    """the shipped final bottom-up hop (k_bu_lean<1,..> + k_bu_rest_lean<1,..>, asserted by name)
-    with the quantised predicate (slot words carry the bucket of follow.weight): every compare op,
-    constants below, inside, on the edges of and above the value range; bu_qpred=0 reads every
-    value of a frontier hit instead (the path a predicate on an unpacked column takes); hub_cap
-    16 leaves all but the first 512 vertices to the global (L2) probe branch"""
+def test_rmat_bottom_up_packed_predicate(rmat12, qpred, hub_cap, fin):
+    """the final bottom-up hop (first pass k_bu_lean<1,..> or, bu_fin = 1, k_bu_fin<..>, then
+    k_bu_rest_lean<1,..>, asserted by name) with the quantised predicate (slot words carry the
+    bucket of follow.weight): every compare op, constants below, inside, on the edges of and above
+    the value range; bu_qpred=0 reads every value of a frontier hit instead (the path a predicate
+    on an unpacked column takes); hub_cap 16 leaves all but the first 512 vertices to the global
+    (L2) probe branch"""
     sp, st = rmat12
     starts = sorted(set(seeds_from(12, 48, seed=29)))
     wcol = X.AliasProp("follow", "weight")
     sp.set_option("bu_force", 1)
     sp.set_option("bu_qpred", qpred)
     sp.set_option("bu_hub_cap", hub_cap)
+    sp.set_option("bu_fin", fin)
+    first = "nbg::k_bu_fin<" if fin else "nbg::k_bu_lean<1, "
     for k in (-5, 0, 1, 3, 4, 255, 499, 500, 998, 999, 1000, 5000):
         for op, mk in OPS.items():
             w = mk(wcol, k)
@@ -556,4 +600,4 @@ def test_rmat_bottom_up_packed_predicate(rmat12, qpred, hub_cap):
             assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0))), (k, op)
             assert g.edges_scanned == r_.edges_scanned
             ks = final_bu_kernels(sp)
-            assert ks[0].startswith("nbg::k_bu_lean<1, ") and ks[1].startswith("nbg::k_bu_rest_lean<1, "), ks
+            assert ks[0].startswith(first) and ks[1].startswith("nbg::k_bu_rest_lean<1, "), ks

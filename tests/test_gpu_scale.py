@@ -115,12 +115,41 @@ def test_every_operator_default_path_rmat20(rmat20, op, hub_cap):
             assert r.edges_scanned == scanned
             hops = sp.last_timing()["hops"]
             assert hops[-1]["mode"] == "bottom-up" and hops[-1]["final"]
-            assert hops[-1]["kernels"][0].startswith("nbg::k_bu_lean<1, "), hops[-1]["kernels"]
+            # the default first pass is k_bu_fin; the counting instantiation is k_bu_lean's
+            first = "nbg::k_bu_lean<1, " if hub_cap else "nbg::k_bu_fin<"
+            assert hops[-1]["kernels"][0].startswith(first), hops[-1]["kernels"]
             l2_probes += hops[-1]["c"][6]
     finally:
         sp.unset_option("bu_hub_cap")
         sp.unset_option("bu_probe_stats")
     assert l2_probes > 0 or not hub_cap  # first-pass probes answered by L2
+
+
+@pytest.mark.parametrize("hub_cap", [None, 1024])
+@pytest.mark.parametrize("op", list(OPS))
+def test_every_operator_fin_rmat20(rmat20, op, hub_cap):
+    """the final-hop first pass k_bu_fin (bu_fin = 1: bucket decisions as word-range checks, probe
+    offsets clamped into the LDS hub or wrapped past the global bitmap) for every relational
+    operator at the bucket edges against the index-space oracle, also with the hub capped at 1024
+    words so most probes go to L2"""
+    sp, g = rmat20
+    starts = synth.seeds(20, 16, 1, 64)
+    wcol = X.AliasProp("follow", "weight")
+    sp.set_option("bu_fin", 1)
+    if hub_cap:
+        sp.set_option("bu_hub_cap", hub_cap)
+    try:
+        for k in (0, 15, 16, 499, 998, 999):
+            r = sp.go(starts, 3, FOLLOW, where=OPS[op](wcol, k), yields=[X.EdgeDst("follow")], distinct=True)
+            want, scanned = g.go(starts, 3, distinct=True, where=(op, k))
+            assert np.array_equal(np.sort(r.columns[0]), want), (op, k)
+            assert r.edges_scanned == scanned
+            hops = sp.last_timing()["hops"]
+            assert hops[-1]["mode"] == "bottom-up" and hops[-1]["final"]
+            assert hops[-1]["kernels"][0].startswith("nbg::k_bu_fin<"), hops[-1]["kernels"]
+    finally:
+        sp.unset_option("bu_hub_cap")
+        sp.unset_option("bu_fin")
 
 
 def test_bench_query_rmat20_faithful_oracle(rmat20):
