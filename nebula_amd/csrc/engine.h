@@ -350,6 +350,8 @@ struct EdgeSpace {
                                    // (padded with 0 to whole 128-row tiles)
   int64_t bu_live_tiles = 0;       // 128-row tiles up to the last row with out-degree > 0
   int64_t max_odeg = -1;           // largest owned out-degree (-1: unknown)
+  DevBuf odeg8;                    // uint8 [owned rows, padded as odeg]: min(out-degree, 255); 255 =
+                                   // read odeg (the non-final bottom-up pass streams 1 B per row)
   // quad slab (bottom-up first pass): the first 4 entries of every transposed row, row-major in
   // two halves (slots 0-1 -> pair_col[0], slots 2-3 -> pair_col[1], 2 x int32 per row, -1 past
   // the row's end, padded to whole 128-row tiles)

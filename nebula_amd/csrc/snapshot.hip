@@ -507,6 +507,7 @@ static void reset_edge_derived(EdgeSpace& es) {
   es.q_gbits = es.q_bits = 0;
   for (int h = 0; h < 2; h++) es.pair_col[h].release();
   es.odeg.release();
+  es.odeg8.release();
   es.max_odeg = -1;
 }
 
@@ -1415,6 +1416,10 @@ __global__ void k_last_live(const uint32_t* odeg, int64_t n, unsigned long long*
   if ((threadIdx.x & 63) == 0 && m) atomicMax(last, m);  // one atomic per wave
 }
 
+__global__ void k_odeg8(const uint32_t* deg, int64_t n, uint8_t* d8) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    d8[i] = uint8_t(min(deg[i], 255u));
+}
 __global__ void k_out_deg(const int64_t* row_ptr, const uint8_t* row_ok, int64_t n, uint32_t* deg,
                           unsigned int* maxd) {
   unsigned int m = 0;
@@ -1516,6 +1521,8 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
                                                   es.odeg.as<uint32_t>(), dmax.as<unsigned int>());
   k_last_live<<<grid_for(n_own), 256, 0, c.stream>>>(es.odeg.as<uint32_t>(), n_own,
                                                     reinterpret_cast<unsigned long long*>(dmax.as<unsigned int>() + 2));
+  es.odeg8.alloc(size_t(n_pad + 64));
+  k_odeg8<<<grid_for(n_pad + 1), 256, 0, c.stream>>>(es.odeg.as<uint32_t>(), n_pad + 1, es.odeg8.as<uint8_t>());
   const uint32_t* gdegp = es.odeg.as<uint32_t>();
   if (G > 1) {
     gdeg.alloc(size_t(c.n_global + 1) * 4);

@@ -871,7 +871,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
                                                      unsigned long long* __restrict__ nbits,
                                                      unsigned long long* __restrict__ pbits,
                                                      const uint32_t* __restrict__ odeg, QArgs q_arg,
-                                                     unsigned long long* __restrict__ partials, int cw) {
+                                                     unsigned long long* __restrict__ partials, int cw,
+                                                     const uint8_t* __restrict__ odeg8) {
   __shared__ unsigned long long lds[kSlots * 16];
   extern __shared__ uint32_t s_fb[];  // [0, cw): the bitmap's hub words; [cw]: a zero word
   if (HUB) {
@@ -932,7 +933,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
             const uint64_t y = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(hi + r + 64 * h));
             b[u][h] = make_uint2(uint32_t(y), uint32_t(y >> 32));
           }
-          od[u][h] = FINAL ? 1u : __builtin_nontemporal_load(odeg + r + 64 * h);
+          // 1 B per row; 255 stands for a larger degree, read from odeg where a row is found
+          od[u][h] = FINAL ? 1u : uint32_t(__builtin_nontemporal_load(odeg8 + r + 64 * h));
         } else {
           a[u][h] = lo[r + 64 * h];
           if (FINAL) b[u][h] = hi[r + 64 * h];
@@ -1064,7 +1066,14 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
       }
       nfound += uint64_t(__popcll(f0) + __popcll(f1));
       npend += uint64_t(__popcll(p0) + __popcll(p1));
-      if (!FINAL) odsum += uint64_t(f[u][0] ? od[u][0] : 0u) + uint64_t(f[u][1] ? od[u][1] : 0u);
+      if (!FINAL) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          uint32_t d = f[u][h] ? od[u][h] : 0u;
+          if (NT && d == 255u) d = odeg[t * 128 + lane + 64 * h];  // odeg8 saturates at 255
+          odsum += uint64_t(d);
+        }
+      }
     }
   }
   // tiles past the live rows (non-final hops): nothing can be found there
@@ -1620,7 +1629,7 @@ __global__ __launch_bounds__(1024) void k_starts_small(const int64_t* __restrict
                                                        int32_t* __restrict__ F, int64_t* __restrict__ off,
                                                        unsigned long long* __restrict__ Kd) {
   __shared__ int32_t s_loc[kSmallStarts];
-  __shared__ unsigned long long s_w[16];
+  __shared__ unsigned long long s_w[32];  // [0, 16): per-wave counts, [16, 32): per-wave degree sums
   __shared__ unsigned long long s_carry[2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < 64) Kd[tid] = 0ull;
@@ -1653,11 +1662,11 @@ __global__ __launch_bounds__(1024) void k_starts_small(const int64_t* __restrict
       const unsigned long long a = __shfl_up(kc, o), b = __shfl_up(kd, o);
       if (lane >= o) kc += a, kd += b;
     }
-    if (lane == 63) s_w[wv] = kc, s_w[8 + wv] = kd;  // at most 16 waves: 8 + 8 slots suffice
+    if (lane == 63) s_w[wv] = kc, s_w[16 + wv] = kd;
     __syncthreads();
     unsigned long long bc = s_carry[0], bd = s_carry[1], tc = 0, td = 0;
     for (int w = 0; w < int(blockDim.x >> 6); w++) {
-      const unsigned long long wc = s_w[w], wd = s_w[8 + w];
+      const unsigned long long wc = s_w[w], wd = s_w[16 + w];
       if (w < wv) bc += wc, bd += wd;
       tc += wc, td += wd;
     }
@@ -2417,10 +2426,11 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   auto go = [&](auto kern) {
     if (shm > 48 * 1024)
       lds_limit(reinterpret_cast<const void*>(kern), shm);
-    kern<<<grid, bs, shm, c.stream>>>(lo, hi, ntiles, work, fb, fb_bytes, nb, pbits, od, q, partials, cw);
+    kern<<<grid, bs, shm, c.stream>>>(lo, hi, ntiles, work, fb, fb_bytes, nb, pbits, od, q, partials, cw,
+                                      es.odeg8.as<uint8_t>());
   };
   int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
-  if (sel == 2 && c.opt("bu_lean_nt", 1) != 0) sel = 6;  // non-temporal slab loads
+  if (sel == 2 && c.opt("bu_lean_nt", 1) != 0 && (fast || es.odeg8.p)) sel = 6;  // non-temporal, 1 B degrees
 #define NBG_LEAN(PKV)                                \
   switch (sel) {                                     \
     case 6: go(k_bu_lean<PKV, 1, 1, 0, 1>); break;   \
