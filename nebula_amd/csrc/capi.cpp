@@ -87,13 +87,13 @@ nbg_ctx* nbg_ctx_create(int32_t device, int32_t num_parts, int32_t rank, int32_t
   }
   for (auto& e : ctx->c.ev) (void)hipEventCreate(&e);
   // coherent: the device publishes counters here and the host polls them (k_publish)
-  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->c.host_counters), 64 * 8 + 64, hipHostMallocCoherent) != hipSuccess) {
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->c.host_counters), 256 * 8 + 64, hipHostMallocCoherent) != hipSuccess) {
     (void)hipStreamDestroy(ctx->c.stream);
     delete ctx;
     return nullptr;
   }
-  memset(ctx->c.host_counters, 0, 64 * 8 + 64);
-  ctx->c.host_seq = ctx->c.host_counters + 64;
+  memset(ctx->c.host_counters, 0, 256 * 8 + 64);
+  ctx->c.host_seq = ctx->c.host_counters + 256;
   // pinned staging for a query's small host->device inputs (starts, compiled programs): copies
   // from pageable memory go through a driver bounce buffer and block the calling thread
   if (hipHostMalloc(&ctx->c.host_stage, nbg::kHostStageBytes, hipHostMallocDefault) != hipSuccess)

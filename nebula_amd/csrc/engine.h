@@ -348,8 +348,9 @@ struct EdgeSpace {
   uint64_t rmat_seed = 0;
   DevBuf odeg;                     // uint32 [owned rows]: out-degree, 0 where row_ok == 0
                                    // (padded with 0 to whole 128-row tiles)
-  int64_t bu_live_tiles = 0;       // 128-row tiles up to the last row with out-degree > 0
   int64_t max_odeg = -1;           // largest owned out-degree (-1: unknown)
+  int64_t bu_in_tiles = 0;         // 128-row tiles up to the last row with an in-edge (final hop)
+  int64_t bu_both_tiles = 0;       // ... with an in-edge and an out-edge (non-final hops)
   DevBuf odeg8;                    // uint8 [owned rows, padded as odeg]: min(out-degree, 255); 255 =
                                    // read odeg (the non-final bottom-up pass streams 1 B per row)
   // quad slab (bottom-up first pass): the first 4 entries of every transposed row, row-major in
@@ -513,7 +514,7 @@ struct Ctx {
   // hipMalloc costs up to seconds: r03a trace), so the phases of a build and later commits of a
   // writable snapshot reuse them.  Trimmed after a read-only build.
   std::shared_ptr<BufPool> build_pool = std::make_shared<BufPool>();
-  unsigned long long* host_counters = nullptr;  // pinned, coherent, 64 entries
+  unsigned long long* host_counters = nullptr;  // pinned, coherent, 256 entries
   // counters published by k_publish: host_counters + a sequence word the host spins on (a
   // hipStreamSynchronize round trip costs ~19 us on this stack, tools/launch_gap)
   unsigned long long* host_seq = nullptr;  // pinned, coherent

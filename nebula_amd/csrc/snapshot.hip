@@ -1407,15 +1407,25 @@ static bool copy_prop(const PropCol& p) {
   return intlike && !p.present.p;
 }
 
-// 1 + the last row with a non-zero out-degree (atomic max; rows past it never extend a frontier)
-__global__ void k_last_live(const uint32_t* odeg, int64_t n, unsigned long long* last) {
-  unsigned long long m = 0;
-  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
-    if (odeg[i]) m = (unsigned long long)(i + 1);
-  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor((long long)m, o));
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(last, m);  // one atomic per wave
-}
 
+// out[0] = 1 + the last row with an in-edge (transposed row), out[1] = 1 + the last row with
+// an in-edge and an out-edge
+__global__ void k_live_bounds(const int64_t* trp, const uint32_t* odeg, int64_t n, unsigned long long* out) {
+  unsigned long long a = 0, b = 0;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    if (trp[i + 1] > trp[i]) {
+      a = (unsigned long long)(i + 1);
+      if (odeg[i]) b = (unsigned long long)(i + 1);
+    }
+  for (int o = 32; o > 0; o >>= 1) {
+    a = max(a, (unsigned long long)__shfl_xor((long long)a, o));
+    b = max(b, (unsigned long long)__shfl_xor((long long)b, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (a) atomicMax(out, a);
+    if (b) atomicMax(out + 1, b);
+  }
+}
 __global__ void k_odeg8(const uint32_t* deg, int64_t n, uint8_t* d8) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
     d8[i] = uint8_t(min(deg[i], 255u));
@@ -1519,8 +1529,6 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
   NBG_HIP(hipMemsetAsync(dmax.p, 0, 16, c.stream));
   k_out_deg<<<grid_for(n_own), 256, 0, c.stream>>>(o.row_ptr.as<int64_t>(), o.row_ok.as<uint8_t>(), n_own,
                                                   es.odeg.as<uint32_t>(), dmax.as<unsigned int>());
-  k_last_live<<<grid_for(n_own), 256, 0, c.stream>>>(es.odeg.as<uint32_t>(), n_own,
-                                                    reinterpret_cast<unsigned long long*>(dmax.as<unsigned int>() + 2));
   es.odeg8.alloc(size_t(n_pad + 64));
   k_odeg8<<<grid_for(n_pad + 1), 256, 0, c.stream>>>(es.odeg.as<uint32_t>(), n_pad + 1, es.odeg8.as<uint8_t>());
   const uint32_t* gdegp = es.odeg.as<uint32_t>();
@@ -1535,11 +1543,8 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
     gdegp = gdeg.as<uint32_t>();
   }
   uint32_t maxd = 0;
-  unsigned long long last_live = 0;  // 1 + the last row with out-edges
   NBG_HIP(hipMemcpyAsync(&maxd, dmax.p, 4, hipMemcpyDeviceToHost, c.stream));
-  NBG_HIP(hipMemcpyAsync(&last_live, dmax.as<unsigned int>() + 2, 8, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
-  es.bu_live_tiles = int64_t((last_live + 127) / 128);
   es.max_odeg = int64_t(maxd);
   if (G > 1) maxd = UINT32_MAX;  // other ranks' degrees may exceed the local maximum
   // the transposed edge list: tdst (local row), tsrc (global), and the order props come in
@@ -1726,6 +1731,22 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
                                                                    es.pair_col[0].as<int32_t>(),
                                                                    es.pair_col[1].as<int32_t>(), -1);
   }
+  {
+    // exact row bounds of the bottom-up hops: past the last row with an in-edge nothing can be
+    // found (final hop), past the last one with an in-edge and an out-edge nothing can extend
+    // the next frontier (non-final hops); the class-ordered numbering makes both short prefixes
+    DevBuf lb;
+    lb.alloc(16);
+    NBG_HIP(hipMemsetAsync(lb.p, 0, 16, c.stream));
+    if (n_own)
+      k_live_bounds<<<grid_for(n_own), 256, 0, c.stream>>>(t.row_ptr.as<int64_t>(), es.odeg.as<uint32_t>(), n_own,
+                                                           lb.as<unsigned long long>());
+    unsigned long long h[2] = {0, 0};
+    NBG_HIP(hipMemcpyAsync(h, lb.p, 16, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    es.bu_in_tiles = int64_t((h[0] + 127) / 128);
+    es.bu_both_tiles = int64_t((h[1] + 127) / 128);
+  }
   NBG_HIP(hipStreamSynchronize(c.stream));
   NBG_HIP(hipGetLastError());
   es.has_tr = true;
@@ -1746,13 +1767,29 @@ __global__ void k_count_deg(const int64_t* src, int64_t n, const int64_t* keys, 
     if (g >= 0) atomicAdd(deg + g, 1u);
   }
 }
-__global__ void k_not_u32(const unsigned int* in, int64_t n, uint32_t* out) {
-  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
-    out[i] = ~in[i];
+// Vertex numbering key (sorted ascending, stable over vids ascending): the degree class above
+// the complemented out-degree.  Classes: 0 both in- and out-edges, 1 in-edges only, 2 out-edges
+// only, 3 none (ideg null: every vertex class 0, plain descending out-degree).  A bottom-up hop
+// then works on a prefix of the rows: a non-final hop on class 0 (a row needs an in-edge to be
+// found and an out-edge to matter), the final hop on classes 0-1 (snapshot: bu_both_tiles,
+// bu_in_tiles, exact bounds whatever the order).  idx (streamed RMAT build): counts are indexed
+// through it.
+__global__ void k_class_key(const unsigned int* odeg, const unsigned int* ideg, const uint32_t* idx, int64_t n,
+                            uint64_t* key) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t u = idx ? int64_t(idx[i]) : i;
+    const uint32_t od = odeg[u];
+    uint64_t cls = 0;
+    if (ideg) {
+      const uint32_t id = ideg[u];
+      cls = id ? (od ? 0 : 1) : (od ? 2 : 3);
+    }
+    key[i] = (cls << 32) | uint64_t(~od);
+  }
 }
 
 // Degree-ordered vertex numbering: a rank's owned gidx range lists its vertices by descending
-// out-degree (ties by vid).  The hubs -- the sources a bottom-up hop finds first (hub-first
+// out-degree (ties by vid), one rank: within the degree classes of k_class_key.  The hubs -- the sources a bottom-up hop finds first (hub-first
 // transposed rows) -- then share a few cache lines of every frontier bitmap instead of being
 // scattered over all of it.  `owned` holds sign-flipped vids, sorted ascending on entry.
 static void order_by_degree(Ctx& c, DevBuf& owned, int64_t n_owned) {
@@ -1775,22 +1812,35 @@ static void order_by_degree(Ctx& c, DevBuf& owned, int64_t n_owned) {
   int32_t min_idx = -1;
   NBG_HIP(hipMemcpyAsync(&min_idx, dmin.p, 4, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
+  // one rank: in-degrees too (every in-edge of an owned vertex is in the local stage), for the
+  // degree classes of class_key
+  const bool classes = c.world == 1 && c.opt("class_order", 1) != 0;
+  DevBuf ideg;
+  if (classes) {
+    ideg.alloc(size_t(n_owned) * 4);
+    NBG_HIP(hipMemsetAsync(ideg.p, 0, size_t(n_owned) * 4, c.stream));
+  }
   for (auto& kv : c.edges) {
     const Staging& st = kv.second.out_stage;
-    if (st.n)
-      k_count_deg<<<grid_for(st.n), 256, 0, c.stream>>>(st.src.as<int64_t>(), st.n, keys.as<int64_t>(),
+    if (!st.n) continue;
+    k_count_deg<<<grid_for(st.n), 256, 0, c.stream>>>(st.src.as<int64_t>(), st.n, keys.as<int64_t>(),
+                                                     vals.as<int32_t>(), uint64_t(cap - 1), min_idx >= 0, min_idx,
+                                                     deg.as<unsigned int>());
+    if (classes)
+      k_count_deg<<<grid_for(st.n), 256, 0, c.stream>>>(st.dst.as<int64_t>(), st.n, keys.as<int64_t>(),
                                                        vals.as<int32_t>(), uint64_t(cap - 1), min_idx >= 0, min_idx,
-                                                       deg.as<unsigned int>());
+                                                       ideg.as<unsigned int>());
   }
   keys.release();
   vals.release();
   DevBuf key, keyS, sorted;
-  key.alloc(size_t(n_owned) * 4);
-  keyS.alloc(size_t(n_owned) * 4);
+  key.alloc(size_t(n_owned) * 8);
+  keyS.alloc(size_t(n_owned) * 8);
   sorted.alloc(size_t(n_owned) * 8);
-  k_not_u32<<<grid_for(n_owned), 256, 0, c.stream>>>(deg.as<unsigned int>(), n_owned, key.as<uint32_t>());
-  radix_pairs<uint32_t, uint64_t>(c, key.as<uint32_t>(), keyS.as<uint32_t>(), owned.as<uint64_t>(),
-                                 sorted.as<uint64_t>(), n_owned, 32);
+  k_class_key<<<grid_for(n_owned), 256, 0, c.stream>>>(deg.as<unsigned int>(), classes ? ideg.as<unsigned int>() : nullptr,
+                                                       nullptr, n_owned, key.as<uint64_t>());
+  radix_pairs<uint64_t, uint64_t>(c, key.as<uint64_t>(), keyS.as<uint64_t>(), owned.as<uint64_t>(),
+                                 sorted.as<uint64_t>(), n_owned, classes ? 34 : 32);
   NBG_HIP(hipMemcpyAsync(owned.p, sorted.p, size_t(n_owned) * 8, hipMemcpyDeviceToDevice, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
   NBG_HIP(hipGetLastError());
@@ -2074,10 +2124,6 @@ __global__ void k_rmat_vkeys(const uint32_t* idx, int64_t n, uint64_t smix, uint
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
     key[i] = uint64_t(rmat_vid(idx[i], smix)) ^ (1ull << 63);
 }
-__global__ void k_rmat_degkey(const uint32_t* idx, int64_t n, const uint32_t* odeg_u, uint32_t* key) {
-  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
-    key[i] = ~odeg_u[idx[i]];
-}
 // gidx g <-> index u; vid_of; per-gidx sample counts of both directions
 __global__ void k_rmat_number(const uint32_t* idx, int64_t n, uint64_t smix, const uint32_t* odeg_u,
                               const uint32_t* ideg_u, int32_t* gidx_of_u, int64_t* vid_of, int64_t* ocnt,
@@ -2206,12 +2252,15 @@ static void finalize_rmat_stream(Ctx& c, EdgeSpace& es) {
   }
   uint32_t* order = idxB.as<uint32_t>();
   if (c.opt("degree_order", 1)) {
+    // the staged build's key (k_class_key; this builder runs on one rank)
+    const bool classes = c.opt("class_order", 1) != 0;
     DevBuf d1, d2;
-    d1.alloc(size_t(n) * 4);
-    d2.alloc(size_t(n) * 4);
-    k_rmat_degkey<<<grid_for(n), 256, 0, c.stream>>>(idxB.as<uint32_t>(), n, odeg_u.as<uint32_t>(), d1.as<uint32_t>());
-    radix_pairs<uint32_t, uint32_t>(c, d1.as<uint32_t>(), d2.as<uint32_t>(), idxB.as<uint32_t>(), idxA.as<uint32_t>(),
-                                    n, 32);
+    d1.alloc(size_t(n) * 8);
+    d2.alloc(size_t(n) * 8);
+    k_class_key<<<grid_for(n), 256, 0, c.stream>>>(odeg_u.as<unsigned int>(), classes ? ideg_u.as<unsigned int>() : nullptr,
+                                                   idxB.as<uint32_t>(), n, d1.as<uint64_t>());
+    radix_pairs<uint64_t, uint32_t>(c, d1.as<uint64_t>(), d2.as<uint64_t>(), idxB.as<uint32_t>(), idxA.as<uint32_t>(),
+                                    n, classes ? 34 : 32);
     order = idxA.as<uint32_t>();
   }
   // 3. vertex map (one rank: base = [0, n padded to 64])

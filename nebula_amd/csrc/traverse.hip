@@ -687,8 +687,11 @@ __device__ inline void block_store_partials(const unsigned long long* v, int k, 
 // sums the [kSlots][kAggBlocks] partials into out[0..kSlots) (one block of 1024 threads; all
 // kSlots loads of an iteration are independent, so the block has 8 loads in flight per lane
 // instead of one dependent chain per slot)
+// gate (speculative hops, go_run): when *gate == 0 the kernel does nothing
 __global__ __launch_bounds__(1024) void k_reduce_partials(const unsigned long long* partials, int nblocks,
-                                                          unsigned long long* out) {
+                                                          unsigned long long* out,
+                                                          const unsigned long long* gate = nullptr) {
+  if (gate && *gate == 0ull) return;
   __shared__ unsigned long long s[kSlots][16];
   unsigned long long a[kSlots];
 #pragma unroll
@@ -851,9 +854,8 @@ __device__ inline void bu_rest_scan(const bool (&pend)[R], bool (&found)[R], con
 //    hardware returns 0: no branch);
 //  * a non-final hop (PK_NONE) reads the second half only for rows still pending after the
 //    first (almost none: hub-first slot 0 is nearly always in a dense frontier), and only the
-//    tiles below es.bu_live_tiles (vertices are numbered by descending out-degree, so the rows
-//    with no out-edges - which never extend the frontier - form the tail); dead tiles get zero
-//    words;
+//    tiles below es.bu_both_tiles (the last row with an in- and an out-edge: one rank numbers
+//    such vertices first, snapshot k_class_key); the tiles past it get zero words;
 //  * the final hop (PK_FAST) decides each slot by two scalar compares of its packed bucket
 //    (QArgs); a frontier hit in an undecided bucket and rows with more than 4 entries are left
 //    pending for k_bu_rest_lean (rest_from 0).  A predicate on a column that is not the packed
@@ -872,7 +874,9 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
                                                      unsigned long long* __restrict__ pbits,
                                                      const uint32_t* __restrict__ odeg, QArgs q_arg,
                                                      unsigned long long* __restrict__ partials, int cw,
-                                                     const uint8_t* __restrict__ odeg8) {
+                                                     const uint8_t* __restrict__ odeg8,
+                                                     const unsigned long long* __restrict__ gate) {
+  if (gate && *gate == 0ull) return;  // a speculative hop that the direction choice did not take
   __shared__ unsigned long long lds[kSlots * 16];
   extern __shared__ uint32_t s_fb[];  // [0, cw): the bitmap's hub words; [cw]: a zero word
   if (HUB) {
@@ -1112,12 +1116,13 @@ constexpr uint32_t kNoProbe = 0x0ffffff0u;
 // tiles per wave; with no probes at all the slab alone streams at 4.7 TB/s in this loop.
 template <int CLS, int NT>
 __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo, const uint2* __restrict__ hi,
-                                                    int64_t ntiles,
+                                                    int64_t ntiles, int64_t work_tiles,
                                                     const uint32_t* __restrict__ fbits,
                                                     unsigned long long* __restrict__ nbits,
                                                     unsigned long long* __restrict__ pbits, FinArgs fa_arg,
                                                     unsigned long long* __restrict__ partials, int cw,
-                                                    uint32_t fb_rest) {
+                                                    uint32_t fb_rest, const unsigned long long* __restrict__ gate) {
+  if (gate && *gate == 0ull) return;  // a speculative hop that the direction choice did not take
   // dynamic LDS only, so the hub copy starts at address 0 and a probe's LDS address is its
   // clamped byte offset as it is: [0, cw) the bitmap's hub words, [cw] a zero word, then the
   // block's partials scratch
@@ -1154,7 +1159,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
       sw[h][0] = a.x, sw[h][1] = a.y, sw[h][2] = b.x, sw[h][3] = b.y;
     }
   };
-  for (int64_t t = wave; t < ntiles; t += nwaves) {
+  for (int64_t t = wave; t < work_tiles; t += nwaves) {
     uint32_t sw[2][4];
     load(t, sw);
     __builtin_amdgcn_sched_barrier(0);
@@ -1206,6 +1211,12 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
     npend += uint64_t(__popcll(p0) + __popcll(p1));
     nwords += 8u * 64u;
   }
+  // tiles past the last row with an in-edge: nothing to find
+  for (int64_t t = work_tiles + wave; t < ntiles; t += nwaves)
+    if (lane < 2) {
+      nbits[2 * t + lane] = 0ull;
+      pbits[2 * t + lane] = 0ull;
+    }
   if (lane != 0) nfound = npend = nwords = 0;
   unsigned long long acc64[8] = {nfound, 0, nwords, npend, 0, 0, 0, 0};
   block_store_partials(acc64, 8, lds, partials);
@@ -1243,7 +1254,9 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
                                                           const uint32_t* __restrict__ fbits, unsigned long long* nbits,
                                                           const uint32_t* __restrict__ odeg, FastArgs fp, QArgs q_arg,
                                                           unsigned long long* partials, int cw, int ru, int rest_from,
-                                                          int steps, unsigned long long* dbg) {
+                                                          int steps, unsigned long long* dbg,
+                                                          const unsigned long long* __restrict__ gate) {
+  if (gate && *gate == 0ull) return;
   const QArgs q = q_sgpr(q_arg);
   __shared__ unsigned long long lds[kSlots * 16];
   __shared__ unsigned long long s_found[16][64];
@@ -1400,8 +1413,13 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
 template <int MODE>
 __global__ __launch_bounds__(1024) void k_bits_compact(const uint32_t* __restrict__ bits, int64_t n, int64_t lo,
                                                        const int64_t* __restrict__ vid_of, void* out,
-                                                       unsigned long long* n_out) {
-  constexpr int kTileWords = 4096;  // 1024 threads x 4 words: one counter atomic per 128 K vertices
+                                                       unsigned long long* n_out,
+                                                       const unsigned long long* gate = nullptr) {
+  if (gate && *gate == 0ull) return;
+  // one word per thread: a 1024-thread block owns 1024 words (32 K vertices) per iteration, so
+  // a 32.8 M-vertex bitmap is ~1000 blocks (4096-word tiles gave ~250: one block per CU, half
+  // the resident waves this latency-bound gather needs); one counter atomic per tile
+  constexpr int kTileWords = 1024;
   __shared__ uint32_t sw[kTileWords];
   __shared__ uint32_t so[kTileWords];
   __shared__ uint32_t lds[16];
@@ -1411,32 +1429,14 @@ __global__ __launch_bounds__(1024) void k_bits_compact(const uint32_t* __restric
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int64_t w0 = t * kTileWords + int64_t(threadIdx.x) * 4;
-    uint32_t x[4];
-    if (w0 + 4 <= nwords) {
-      const uint4 v = *reinterpret_cast<const uint4*>(bits + w0);
-      x[0] = v.x, x[1] = v.y, x[2] = v.z, x[3] = v.w;
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; q++) x[q] = w0 + q < nwords ? bits[w0 + q] : 0u;
-    }
+    const int64_t w0 = t * kTileWords + int64_t(threadIdx.x);
+    uint32_t x = w0 < nwords ? bits[w0] : 0u;
     // bits at or past n (a bitmap's unused tail may hold stale bits) are never listed
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-      if ((w0 + q + 1) * 32 > n && w0 + q < nwords) x[q] &= (1u << uint32_t(n - (w0 + q) * 32)) - 1u;
-    uint32_t o[4], cnt = 0;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      o[q] = cnt;
-      cnt += __popc(x[q]);
-    }
+    if ((w0 + 1) * 32 > n && w0 < nwords) x &= (1u << uint32_t(n - w0 * 32)) - 1u;
     uint32_t total;
-    const uint32_t pre = block_excl_scan_u32(cnt, total, lds);
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      sw[threadIdx.x * 4 + q] = x[q];
-      so[threadIdx.x * 4 + q] = pre + o[q];
-    }
+    const uint32_t pre = block_excl_scan_u32(__popc(x), total, lds);
+    sw[threadIdx.x] = x;
+    so[threadIdx.x] = pre;
     if (threadIdx.x == 0) s_base = total ? atomicAdd(n_out, (unsigned long long)total) : 0ull;
     __syncthreads();
     if (total) {
@@ -1613,7 +1613,7 @@ __global__ void k_starts_bits(const int32_t* g, int64_t n, int64_t lo, int64_t h
 // starts (gidx) -> mark owned in the byte-map (dedup path) or list them (steps == 1 path)
 // One-block start frontier for a few starts (ns <= kSmallStarts, one rank), everything the
 // first top-down hop needs in one launch instead of a lookup, three memsets, the bitmap dedup, a
-// degree pass, a scan and a counter round trip: zero the query counters Kd[0, 64), look the
+// degree pass, a scan and a counter round trip: zero the query counters Kd[0, 256), look the
 // start vids up (gidx -> g), dedup through the start words of the frontier bitmap (only those
 // words are cleared: a top-down first hop never reads the rest, k_compact rewrites it all), keep
 // starts with out-edges (row_ok) as the list F, write its exclusive degree scan to off[0, ns]
@@ -1632,7 +1632,7 @@ __global__ __launch_bounds__(1024) void k_starts_small(const int64_t* __restrict
   __shared__ unsigned long long s_w[32];  // [0, 16): per-wave counts, [16, 32): per-wave degree sums
   __shared__ unsigned long long s_carry[2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid < 64) Kd[tid] = 0ull;
+  if (tid < 256) Kd[tid] = 0ull;
   for (int i = tid; i < ns; i += blockDim.x) {
     const int32_t x = ht_lookup(keys, vals, mask, vids[i], has_min, min_gidx);
     g[i] = x;
@@ -1973,14 +1973,23 @@ __global__ void k_publish(const unsigned long long* __restrict__ src, int n, uns
   }
 }
 
+// Speculative bottom-up hops (go_run): *gate = 1 iff the previous hop ran (prev_gate, when
+// given), its next frontier is non-empty (*n > 0) and its out-degree sum reaches the bottom-up
+// threshold (*e >= thr >= 1) -- the host's direction choice (want_bu) on the same counters.
+__global__ void k_gate(const unsigned long long* e, const unsigned long long* n, const unsigned long long* prev_gate,
+                       unsigned long long thr, unsigned long long* gate) {
+  if (threadIdx.x == 0)
+    *gate = (prev_gate == nullptr || *prev_gate != 0ull) && *n > 0ull && *e >= thr ? 1ull : 0ull;
+}
+
 // the device counters d[0, n) into host h[0, n) once every launch before has finished: a
 // one-thread-block kernel writes them and a sequence word to coherent host memory and the host
 // spins on the word (a memcpy + hipStreamSynchronize round trip cost ~19 us, tools/launch_gap);
 // past 2 s without it the stream is synchronised the ordinary way, which reports a fault
 void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h) {
-  if (n > 64) throw Error(NBG_E_INVALID_ARG, "fetch_counters: at most 64 words");
+  if (n > 256) throw Error(NBG_E_INVALID_ARG, "fetch_counters: at most 256 words");
   const uint64_t seq = ++c.pub_seq;
-  k_publish<<<1, 64, 0, c.stream>>>(d, n, h, c.host_seq, seq);
+  k_publish<<<1, 256, 0, c.stream>>>(d, n, h, c.host_seq, seq);
   NBG_HIP(hipGetLastError());
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 0;; spin++) {
@@ -2005,7 +2014,7 @@ void ensure_workspaces(Ctx& c, int64_t nF_cap) {
   c.ws_front[0].ensure(size_t(nF_cap + 64) * 4);
   c.ws_front[1].ensure(size_t(nF_cap + 64) * 4);
   c.ws_off.ensure(size_t(nF_cap + 2) * 8);
-  c.ws_counters.ensure(512);
+  c.ws_counters.ensure(256 * 8);  // [0, 64) hop counters, [64, 256) speculative hop blocks
   c.ws_partials.ensure(size_t(kAggBlocks) * kSlots * 8);
   c.ws_bits_send.ensure(size_t(mb / 8 + 64));
   c.ws_bits_recv.ensure(size_t(mb / 8 + 64));
@@ -2382,7 +2391,8 @@ FinArgs fin_args(const QArgs& q) {
 // final hop's typed compare on transposed column fcol; decided from the packed buckets when fcol
 // is the packed column, else every value of a frontier hit is read by the rest pass).
 size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
-                      const FastArgs& fp, int fcol, unsigned long long* out) {
+                      const FastArgs& fp, int fcol, unsigned long long* out,
+                      const unsigned long long* gate = nullptr) {
   const Csr& tr = es.tr;
   if (pk != PK_NONE && pk != PK_FAST) throw Error(NBG_E_DEVICE, "bottom-up hop with a VM predicate");
   if (!es.pair_col[0].p) throw Error(NBG_E_DEVICE, "bottom-up hop without the quad slab");
@@ -2400,7 +2410,9 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   const int rest_from = pk == PK_FAST ? 0 : 4;
   pk = fast ? PK_FAST : PK_NONE;
   const int64_t ntiles = (tr.n_rows + 127) / 128;
-  const int64_t work = fast ? ntiles : std::min(ntiles, es.bu_live_tiles);
+  // rows past the last one that can be found (final) or extend the next frontier (non-final)
+  // get zero words without being read (exact bounds, snapshot build_transpose)
+  const int64_t work = std::min(ntiles, fast ? es.bu_in_tiles : es.bu_both_tiles);
   const int U = c.opt(fast ? "bu_lean_u_final" : "bu_lean_u", 1) == 1 ? 1 : 2;
   const int64_t waves = std::max<int64_t>(1, (work + U - 1) / U);
   // hub words in LDS (bu_lean_lds_kb KiB, 0 = off): 1024-thread blocks, two per CU
@@ -2427,7 +2439,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     if (shm > 48 * 1024)
       lds_limit(reinterpret_cast<const void*>(kern), shm);
     kern<<<grid, bs, shm, c.stream>>>(lo, hi, ntiles, work, fb, fb_bytes, nb, pbits, od, q, partials, cw,
-                                      es.odeg8.as<uint8_t>());
+                                      es.odeg8.as<uint8_t>(), gate);
   };
   int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
   if (sel == 2 && c.opt("bu_lean_nt", 1) != 0 && (fast || es.odeg8.p)) sel = 6;  // non-temporal, 1 B degrees
@@ -2452,7 +2464,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     const uint32_t rest = fb_bytes > uint32_t(cw) * 4u ? fb_bytes - uint32_t(cw) * 4u : 0u;
     auto gof = [&](auto kern) {
       if (fshm > 48 * 1024) lds_limit(reinterpret_cast<const void*>(kern), fshm);
-      kern<<<grid, bs, fshm, c.stream>>>(lo, hi, ntiles, fb, nb, pbits, fa, partials, cw, rest);
+      kern<<<grid, bs, fshm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, fa, partials, cw, rest, gate);
     };
     const int nt = int(c.opt("bu_fin_nt", 1) != 0);
     switch ((cls1 ? 1 : 0) | nt << 1) {
@@ -2493,7 +2505,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     if (rshm > 48 * 1024)
       lds_limit(reinterpret_cast<const void*>(kern), rshm);
     kern<<<grid2, 1024, rshm, c.stream>>>(pbits, tr.n_rows, trp, tc, fb, nb, odeg, fp, q, partials + grid, rcw, ru,
-                                          rest_from, rsteps, dbg);
+                                          rest_from, rsteps, dbg, gate);
   };
 #define NBG_REST(PKV, WV)                        \
   if (rcw > 0) rest(k_bu_rest_lean<PKV, WV, 1>); \
@@ -2510,7 +2522,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   }
 #undef NBG_REST
   NBG_HIP(hipGetLastError());
-  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid + grid2, out);
+  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid + grid2, out, gate);
   NBG_HIP(hipGetLastError());
   if (dbg) {
     std::vector<unsigned long long> h(size_t(grid2) * 16 * 8);
@@ -2676,7 +2688,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     NBG_HIP(hipGetLastError());
     nF = ns;  // an upper bound: the entries past the list have degree 0
   } else {
-    NBG_HIP(hipMemsetAsync(K.d, 0, 256, c.stream));
+    NBG_HIP(hipMemsetAsync(K.d, 0, 256 * 8, c.stream));
   }
   if (ns && !fast1) {
     if (s.steps == 1 && !s.distinct) {
@@ -2822,7 +2834,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     cur ^= 1;
     F = c.ws_front[cur].as<int32_t>();
     NBG_HIP(hipMemsetAsync(K.d, 0, 8, c.stream));
-    k_bits_compact<0><<<grid_cap((n_own + 31) / 32, 4096, 4096), 1024, 0, c.stream>>>(bitsA, n_own, lo, nullptr, F,
+    k_bits_compact<0><<<grid_cap((n_own + 31) / 32, 1024, 4096), 1024, 0, c.stream>>>(bitsA, n_own, lo, nullptr, F,
                                                                                      K.d);
     if (list_n >= 0) {
       nF = list_n;  // counted by the compaction that wrote the bitmap: no round trip
@@ -2848,6 +2860,128 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     return eg > 0 && bu_ok && !multi_root && bu_force >= 0 && (bu_force > 0 || eg >= es.out_nnz_global / bu_div);
   };
   int64_t Eg = 0;  // frontier out-degree sum over all ranks
+  // Speculative bottom-up hops (one rank).  A direction choice needs the previous hop's counters
+  // on the host, one round trip per hop; instead, right after a top-down hop's compaction, the
+  // remaining hops are enqueued as bottom-up hops gated on the device (k_gate: the same rule as
+  // want_bu, on the same counters) before the one counter fetch.  A hop whose gate is 0 does
+  // nothing (every kernel returns at once), and the host continues from there as before: the
+  // direction never changes a hop's result, only its cost.  The final step is speculated only
+  // as the DISTINCT _dst bottom-up hop (a predicate that cannot error, no deferred compile
+  // error).  Blocks of 16 words from K.d[64]: [0, 8) the hop's counters, [8] its gate, [9] the
+  // DISTINCT output count.
+  struct Spec {
+    int32_t hop;  // Timing::hops index it will take
+    bool final;
+    std::string k0, k1;
+  };
+  std::vector<Spec> spec;
+  DevBuf spec_vids;
+  FastPred fpk0{};
+  FastArgs fp0{};
+  bool fin_spec = false;
+  if (deferred == NBG_OK) {
+    fpk0 = has_where ? classify_pred(where, es.fields) : FastPred{};
+    if (fpk0.kind == PK_FAST) {
+      const PropCol& pc = csr.props[size_t(fpk0.col)];
+      fp0 = FastArgs{pc.data.p, pc.present.as<uint8_t>(), pc.width, fpk0.op, fpk0.k};
+    }
+    const bool ddst = s.distinct && yields.size() == 1 && yields[0].n == 1 && yields[0].ins[0].op == P_DST;
+    const bool pbu = fpk0.kind == PK_NONE ||
+                     (fpk0.kind == PK_FAST && fp0.present == nullptr && es.tr.props.size() > size_t(fpk0.col) &&
+                      es.tr.props[size_t(fpk0.col)].data.p);
+    fin_spec = ddst && pbu;
+  }
+  const bool spec_ok = c.world == 1 && bu_ok && !multi_root && bu_force >= 0 && c.opt("bu_spec", 1) != 0;
+  const unsigned long long spec_thr =
+      bu_force > 0 ? 1ull : (unsigned long long)std::max<int64_t>(1, es.out_nnz_global / bu_div);
+  unsigned long long* const SPd = K.d + 64;
+  // enqueue the gated hops from step `first` on; the compaction behind them left its counts at
+  // (e, n) and its bitmap in bitsA; hop0 = the Timing::hops index of the first one
+  auto spec_enqueue = [&](int32_t first, const unsigned long long* e, const unsigned long long* n, int32_t hop0) {
+    spec.clear();
+    if (!spec_ok) return;
+    const uint32_t* in = bitsA;
+    uint32_t* outb = bitsB;
+    const unsigned long long* pg = nullptr;
+    for (int32_t st = first; st <= s.steps && spec.size() < 12; st++) {
+      const bool fin = st == s.steps;
+      if (fin && !fin_spec) break;
+      unsigned long long* blk = SPd + 16 * spec.size();
+      k_gate<<<1, 64, 0, c.stream>>>(e, n, pg, spec_thr, blk + 8);
+      const int32_t hop = hop0 + int32_t(spec.size());
+      const size_t ia = timing_event(c);
+      size_t ik;
+      if (!fin) {
+        ik = launch_bu_lean(c, es, in, outb, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, blk, blk + 8);
+      } else {
+        FastArgs tfp = fp0;
+        if (fpk0.kind == PK_FAST) tfp.data = es.tr.props[size_t(fpk0.col)].data.p;
+        ik = launch_bu_lean(c, es, in, outb, nullptr, fpk0.kind, tfp, fpk0.kind == PK_FAST ? fpk0.col : -1, blk,
+                            blk + 8);
+        spec_vids.alloc(size_t(c.n_global + 64) * 8);
+        k_bits_compact<1><<<grid_cap((es.tr.n_rows + 31) / 32, 1024, 4096), 1024, 0, c.stream>>>(
+            outb, es.tr.n_rows, lo, c.vid_of.as<int64_t>(), spec_vids.p, blk + 9, blk + 8);
+      }
+      NBG_HIP(hipGetLastError());
+      const size_t ib = timing_event(c);
+      c.tpend.push_back(Ctx::PendingTime{ia, ib, hop, 0});
+      c.tpend.push_back(Ctx::PendingTime{ia, ik, hop, 1});
+      spec.push_back(Spec{hop, fin, c.bu_kernel_name, c.bu_rest_name});
+      e = blk + 1;
+      n = blk + 0;
+      pg = blk + 8;
+      const uint32_t* t = in;
+      in = outb;
+      outb = const_cast<uint32_t*>(t);
+    }
+  };
+  auto spec_words = [&](int base) { return spec.empty() ? base : 64 + 16 * int(spec.size()); };
+  // after the fetch: record the hops that ran, as the bottom-up branch below does; stops at the
+  // first gate that was 0 (its timings dropped).  Returns the steps consumed; *fin_done when the
+  // final step ran (its counters copied to fin_h)
+  unsigned long long fin_h[16] = {};
+  std::string fin_k0, fin_k1;
+  bool fin_done = false;
+  auto spec_replay = [&]() -> int32_t {
+    int32_t used = 0;
+    for (size_t j = 0; j < spec.size(); j++) {
+      const unsigned long long* hh = K.h + 64 + 16 * j;
+      if (hh[8] == 0) {
+        const int32_t cut = spec[j].hop;
+        c.tpend.erase(std::remove_if(c.tpend.begin(), c.tpend.end(),
+                                     [cut](const Ctx::PendingTime& p) { return p.hop >= cut; }),
+                      c.tpend.end());
+        break;
+      }
+      if (spec[j].final) {
+        std::copy(hh, hh + 16, fin_h);
+        fin_k0 = spec[j].k0;
+        fin_k1 = spec[j].k1;
+        fin_done = true;
+        break;
+      }
+      c.timing.steps_run++;
+      c.timing.edges_scanned += uint64_t(E);
+      c.timing.expand_launches++;
+      c.timing.bu_steps++;
+      const uint64_t kb = bu_first_bytes(hh, es.tr.n_rows, true), hb = kb + bu_rest_bytes(hh, 0);
+      c.timing.expand_bytes += hb;
+      c.timing.hop(1, false, 0.0, hh, 0.0, kb);
+      c.timing.name_last_hop(spec[j].k0, spec[j].k1);
+      std::swap(bitsA, bitsB);
+      have_list = false;
+      list_n = -1;
+      off_ready = false;
+      E = int64_t(hh[1]);
+      E_known = E;
+      nset_global = int64_t(hh[0]);
+      Eg = E;
+      used++;
+      if (nset_global == 0) break;  // the caller returns the empty result
+    }
+    spec.clear();
+    return used;
+  };
   if (fast1) {
     off_ready = true;  // k_starts_small wrote the scan; E is counted on the device
   } else {
@@ -2871,7 +3005,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // (K.d[0, 4) are zero: k_starts_small cleared the counters)
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
                      K.d, es.odeg.as<uint32_t>());
-      fetch_counters(c, K.d, 42, K.h);
+      spec_enqueue(2, K.d + 13, K.d + 12, c.timing.n_hops + 1);  // (hop 1 is recorded below)
+      fetch_counters(c, K.d, spec_words(42), K.h);
       const int64_t nF1 = int64_t(K.h[40]), E1 = int64_t(K.h[41]);
       if (!s.distinct) hop1_scanned = int64_t(K.h[30]);
       c.timing.edges_scanned += uint64_t(hop1_scanned >= 0 ? hop1_scanned : E1);
@@ -2889,6 +3024,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       if (lazy) cur ^= 1;  // ensure_list flips to the list buffer again
       off_ready = false;
       if (nset_global == 0) return finish_empty();  // onEmptyInputs (GoExecutor.cpp:392-395)
+      step += spec_replay();
+      if (nset_global == 0) return finish_empty();
+      if (fin_done) break;
       continue;
     }
     c.timing.edges_scanned += uint64_t(step == 1 && hop1_scanned >= 0 ? hop1_scanned : E);
@@ -2953,7 +3091,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const bool lazy = c.world == 1 && bu_ok && !multi_root && c.opt("compact_list", 0) == 0;
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
                      K.d, es.odeg.as<uint32_t>());
-      fetch_counters(c, K.d, 16, K.h);
+      if (lazy) spec_enqueue(step + 1, K.d + 13, K.d + 12, c.timing.n_hops);
+      fetch_counters(c, K.d, spec_words(16), K.h);
       nF = lazy ? 0 : int64_t(K.h[0]);
       list_n = lazy ? int64_t(K.h[14]) : -1;
       E = int64_t(K.h[13]);
@@ -2967,6 +3106,11 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       off_ready = false;
     }
     if (nset_global == 0) return finish_empty();  // onEmptyInputs (GoExecutor.cpp:392-395)
+    if (!spec.empty()) {
+      step += spec_replay();
+      if (nset_global == 0) return finish_empty();
+      if (fin_done) break;
+    }
   }
   // ---- final step ----
   c.timing.steps_run++;
@@ -3004,8 +3148,22 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
                                        es.tr.props.size() > size_t(fpk.col) && es.tr.props[size_t(fpk.col)].data.p);
       bool bu = pred_bu && want_bu(Eg);
       DevBuf vids;
-      vids.alloc(size_t(c.n_global + 64) * 8);
-      if (bu) {
+      if (fin_done) {
+        // the speculated final hop ran (spec_replay): its counters, rows and kernel names
+        vids = std::move(spec_vids);
+        c.timing.expand_launches++;
+        c.timing.bu_steps++;
+        nrows = int64_t(fin_h[9]);
+        const int pw = pk == PK_FAST ? fp.width : 0;
+        const uint64_t kb = bu_first_bytes(fin_h, es.tr.n_rows, false), hb = kb + bu_rest_bytes(fin_h, pw);
+        c.timing.expand_bytes += hb + uint64_t(es.tr.n_rows) / 8 + uint64_t(nrows) * 16;
+        c.timing.hop(1, true, 0.0, fin_h, 0.0, kb);
+        c.timing.name_last_hop(fin_k0, fin_k1, "nbg::k_bits_compact<1>");
+      } else {
+        vids.alloc(size_t(c.n_global + 64) * 8);
+      }
+      if (fin_done) {
+      } else if (bu) {
         FastArgs tfp = fp;
         if (pk == PK_FAST) tfp.data = es.tr.props[size_t(fpk.col)].data.p;
         const Csr& tr = es.tr;
@@ -3013,7 +3171,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         const uint32_t* fb = global_bits(c, bitsA);
         const size_t ia = timing_event(c);
         const size_t ik = launch_bu_lean(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8);
-        k_bits_compact<1><<<grid_cap((tr.n_rows + 31) / 32, 4096, 4096), 1024, 0, c.stream>>>(
+        k_bits_compact<1><<<grid_cap((tr.n_rows + 31) / 32, 1024, 4096), 1024, 0, c.stream>>>(
             bitsB, tr.n_rows, lo, c.vid_of.as<int64_t>(), vids.p, K.d);
         NBG_HIP(hipGetLastError());
         const size_t ib = timing_event(c);

@@ -386,6 +386,33 @@ def test_rmat_start_frontier_edge_cases(rmat12, small):
         assert g.edges_scanned == r.edges_scanned
 
 
+@pytest.mark.parametrize("bu_div", [1, 2, 4, 16, 256])
+def test_rmat_speculative_hops(rmat12, bu_div):
+    """speculative bottom-up hops (bu_spec: the hops after a top-down compaction enqueued as gated
+    bottom-up hops before one counter fetch) take exactly the directions the host's choice takes
+    without speculation -- same hop modes and counters -- and return the oracle's rows, at
+    thresholds where the gate passes everywhere, only for some hops, or nowhere"""
+    sp, st = rmat12
+    sp.set_option("bu_div", bu_div)
+    starts = sorted(set(seeds_from(12, 24, seed=41)))
+    w = X.AliasProp("follow", "weight") > 499
+    y = [X.EdgeDst("follow")]
+    for steps in (2, 3, 4):
+        for where, distinct in ((w, True), (None, True), (None, False)):
+            runs = []
+            for spec in (1, 0):
+                sp.set_option("bu_spec", spec)
+                g = sp.go(starts, steps, FOLLOW, where=where, yields=y if distinct else (), distinct=distinct)
+                hops = sp.last_timing()["hops"]
+                runs.append((np.sort(g.columns[0]), g.edges_scanned, [(h["mode"], h["c"]) for h in hops]))
+            assert np.array_equal(runs[0][0], runs[1][0]) and runs[0][1] == runs[1][1]
+            assert runs[0][2] == runs[1][2], (steps, distinct)
+            r = st.go(starts, steps, FOLLOW, where=w.encode() if where is not None else b"",
+                      yields=[y[0].encode()] if distinct else (), distinct=distinct)
+            assert np.array_equal(runs[0][0], np.sort(r.int_col(0)))
+            assert runs[0][1] == r.edges_scanned
+
+
 def test_rmat_go_where_distinct(rmat12):
     sp, st = rmat12
     starts = seeds_from(12, 64)
