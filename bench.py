@@ -280,6 +280,9 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
     names = {2: "expand", 3: "probe", 4: "sweep"}
     launches = [{"kind": names.get(h["mode_id"], h["mode"]), "ms": round(h["ms"], 4), "x": h["c"][0], "entries": h["c"][1],
                  "claims": h["c"][2], "iter": h["c"][4]} for h in tm["hops"]]
+    for rec, h in zip(launches, tm["hops"]):
+        if h["c"][6] or h["c"][7]:  # option sp_sweep_stats: distinct scanned vertices, their degrees
+            rec.update(distinct_x=h["c"][6], distinct_entries=h["c"][7])
     # parity: the last result (host copy) against the committed digest
     hops, paths, srcs = r.hops, r.paths, r.src
     if dist is not None:

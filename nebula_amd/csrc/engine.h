@@ -573,6 +573,9 @@ void snapshot_write_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t
                          const uint8_t* vb, const uint64_t* voff, size_t n);
 void snapshot_commit(Ctx& c);
 void lookup_gidx(Ctx& c, const int64_t* d_vids, int32_t* d_gidx, int64_t n);
+// the device counters d[0, n) (n <= 256) into pinned host h[0, n) once every launch before has
+// finished on the context's stream (a one-block publish kernel + a host spin, traverse.hip)
+void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h);
 // traverse.hip
 int32_t go_run(Ctx& c, const nbg_go_spec& spec, nbg_rows* out);
 int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* vids, size_t n,

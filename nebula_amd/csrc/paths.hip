@@ -31,6 +31,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <unordered_map>
 #include <climits>
 #include <cmath>
 
@@ -141,6 +142,14 @@ __device__ inline bool claim_byte(uint8_t* base, uint64_t idx, uint32_t val) {
     old = prev;
   }
   return false;
+}
+
+// zero the counter slots in `mask` (bit i = cnt[i]; one launch instead of a memset per slot run)
+// and, when xdeg is given, the X degree sentinel xdeg[0] the scan reads past the list
+__global__ void k_cnt_zero(unsigned long long* cnt, uint32_t mask, int64_t* xdeg) {
+  const int i = threadIdx.x;
+  if (i < 32 && ((mask >> i) & 1u)) cnt[i] = 0ull;
+  if (i == 32 && xdeg) *xdeg = 0;
 }
 
 // seed both frontiers; trivial pairs (src == dst, unknown vertex, max_steps < 1) finish here
@@ -1016,9 +1025,11 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       bf.sweep_next = sweep_next ? sweep_next->as<uint64_t>() : nullptr;
       bf.cap_sweep = sweep_next ? cap_sweep_next : 0;
     };
-    auto sync_counters = [&]() {
-      NBG_HIP(hipMemcpyAsync(hc, cnt, C_N * 8, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
+    // the counters on the host (publish kernel + spin, traverse.hip: a memcpy + stream sync
+    // round trip cost ~20 us per call, ~15 calls per batch)
+    auto sync_counters = [&]() { fetch_counters(c, cnt, C_N, hc); };
+    auto zero = [&](uint32_t mask, int64_t* xdeg = nullptr) {
+      k_cnt_zero<<<1, 64, 0, c.stream>>>(cnt, mask, xdeg);
     };
     auto set_counter = [&](int which, int64_t v) {
       hc[32] = (unsigned long long)v;
@@ -1036,7 +1047,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     };
     auto launch_scan = [&](int64_t nX) {
       size_t tb = 0;
-      NBG_HIP(hipMemsetAsync(W.Xdeg.as<int64_t>() + nX, 0, 8, c.stream));
+      zero(0u, W.Xdeg.as<int64_t>() + nX);
       NBG_HIP(rocprim::exclusive_scan(nullptr, tb, W.Xdeg.as<int64_t>(), W.Xoff.as<int64_t>(), int64_t(0),
                                       size_t(nX + 1), rocprim::plus<int64_t>(), c.stream));
       c.ws_tmp.ensure(tb);
@@ -1082,9 +1093,11 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     };
     // per-launch record in the hop stats: mode 2 = BFS expansion, 3 = meet probe, 4 = sweep;
     // c[] = {X tuples, adjacency entries, claims, meets (total so far), iteration, active pairs}
+    unsigned long long diag[2] = {0, 0};  // option sp_sweep_stats: distinct X vertices, their degree sum
     auto sp_hop = [&](int32_t mode, double ms, int64_t nX, int64_t E, int64_t claims, int64_t it, int64_t act) {
       const unsigned long long c8[8] = {(unsigned long long)nX, (unsigned long long)E, (unsigned long long)claims,
-                                        hc[C_MEET], (unsigned long long)it, (unsigned long long)act, 0, 0};
+                                        hc[C_MEET], (unsigned long long)it, (unsigned long long)act, diag[0], diag[1]};
+      diag[0] = diag[1] = 0;
       c.timing.hop(mode, false, ms, c8);
       c.timing.name_last_hop(mode == 3 ? "nbg::(anonymous namespace)::k_sp_probe" : "nbg::(anonymous namespace)::k_sp_expand");
     };
@@ -1131,9 +1144,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       ensure_x(n_live[0] + n_live[1]);
       for (int s = 0; s < 2; s++) reserve(c, W.live_next[s], W.cap_next[s], n_live[s] + 64, 0);
       refresh(nullptr, 0);
-      NBG_HIP(hipMemsetAsync(cnt + C_LIVE0, 0, 16, c.stream));
-      NBG_HIP(hipMemsetAsync(cnt + C_X, 0, 24, c.stream));  // C_X, C_ACTIVE, C_OVF
-      NBG_HIP(hipMemsetAsync(cnt + C_XE, 0, 8, c.stream));
+      zero(1u << C_LIVE0 | 1u << C_LIVE1 | 1u << C_X | 1u << C_ACTIVE | 1u << C_OVF | 1u << C_XE);
       for (int s = 0; s < 2; s++)
         if (n_live[s])
           k_sp_select<<<grid_n(n_live[s]), 256, 0, c.stream>>>(W.live[s].as<uint64_t>(), n_live[s], 0, st, gout, gin,
@@ -1156,7 +1167,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         choff.alloc(size_t(nX + 1) * 8);
         slot.alloc(size_t(max_chunks) * 8);
         NBG_HIP(hipMemsetAsync(slot.p, 0xFF, size_t(max_chunks) * 8, c.stream));
-        NBG_HIP(hipMemsetAsync(cnt + C_PE, 0, 8, c.stream));
+        zero(1u << C_PE);
         k_sp_chunks<<<grid_n(nX + 1), 256, 0, c.stream>>>(W.Xdeg.as<int64_t>(), nX, ch.as<int64_t>());
         size_t tb = 0;
         NBG_HIP(rocprim::exclusive_scan(nullptr, tb, ch.as<int64_t>(), choff.as<int64_t>(), int64_t(0),
@@ -1257,8 +1268,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     for (int32_t j = 1; n_sw > 0; j++) {
       const bool push_now = push_ok && !arena_lost;  // an arena overflow mid-sweep: pull only
       ensure_x(n_sw + (push_now ? n_arena : 0));
-      NBG_HIP(hipMemsetAsync(cnt + C_X, 0, 24, c.stream));
-      NBG_HIP(hipMemsetAsync(cnt + C_SWEEP, 0, 16, c.stream));  // C_SWEEP, C_XE
+      zero(1u << C_X | 1u << C_ACTIVE | 1u << C_OVF | 1u << C_SWEEP | 1u << C_XE);
       refresh(nullptr, 0);
       if (push_now) {
         NBG_HIP(hipMemsetAsync(pullc, 0, size_t(nb) * 16, c.stream));
@@ -1279,6 +1289,19 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       sync_counters();
       const int64_t nX = int64_t(hc[C_X]), E = int64_t(hc[C_XE]);
       if (nX == 0 || E == 0) break;
+      if (c.opt("sp_sweep_stats", 0) && nX <= (int64_t(1) << 26)) {
+        // diagnostics: how many distinct vertices the step's adjacency scans come from (pairs
+        // sharing a meet vertex scan its row once each)
+        std::vector<uint64_t> hx(static_cast<size_t>(nX));
+        std::vector<int64_t> hd(static_cast<size_t>(nX));
+        NBG_HIP(hipMemcpyAsync(hx.data(), W.X.p, size_t(nX) * 8, hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipMemcpyAsync(hd.data(), W.Xdeg.p, size_t(nX) * 8, hipMemcpyDeviceToHost, c.stream));
+        NBG_HIP(hipStreamSynchronize(c.stream));
+        std::unordered_map<uint64_t, int64_t> seen;
+        for (int64_t i = 0; i < nX; i++) seen[(hx[size_t(i)] >> 63) << 32 | uint32_t(hx[size_t(i)])] = hd[size_t(i)];
+        diag[0] = seen.size();
+        for (auto& kv : seen) diag[1] += uint64_t(kv.second);
+      }
       c.timing.edges_scanned += uint64_t(E);
       const int64_t want = std::min<int64_t>(E, soft) + 64;
       reserve(c, W.sweep[nxt], W.cap_sweep[nxt], want, 0);
@@ -1322,7 +1345,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       doff.alloc(size_t(nb + 1) * 8);
       dpath.alloc(size_t(plen) * 8);
       NBG_HIP(hipMemcpyAsync(doff.p, boff.data(), size_t(nb + 1) * 8, hipMemcpyHostToDevice, c.stream));
-      NBG_HIP(hipMemsetAsync(cnt + C_WALKERR, 0, 8, c.stream));
+      zero(1u << C_WALKERR);
       int32_t maxL = 0;
       for (int64_t p = 0; p < nb; p++)
         if (hstate[size_t(p)] == SP_MET) maxL = std::max(maxL, hres_b[size_t(p)]);

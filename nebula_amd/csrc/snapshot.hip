@@ -509,6 +509,7 @@ static void reset_edge_derived(EdgeSpace& es) {
   es.odeg.release();
   es.odeg8.release();
   es.max_odeg = -1;
+  es.bu_in_tiles = es.bu_both_tiles = 0;
 }
 
 static void reset_derived(Ctx& c) {
@@ -2036,10 +2037,141 @@ __global__ void k_count_unknown(const int64_t* src, const int64_t* dst, int64_t 
   if ((threadIdx.x & 63) == 0 && u) atomicAdd(cnt, u);
 }
 
+// vids of a batch's endpoints that are not in the vertex map (sign-flipped for an unsigned sort)
+__global__ void k_collect_unknown(const int64_t* src, const int64_t* dst, int64_t n, const int64_t* keys_ht,
+                                  const int32_t* vals_ht, uint64_t mask, bool has_min, int32_t min_gidx,
+                                  uint64_t* out, unsigned long long* cnt) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int64_t rounds = (n + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    int64_t a = 0, b = 0;
+    bool ua = false, ub = false;
+    if (i < n) {
+      a = src[i];
+      b = dst[i];
+      ua = ht_lookup(keys_ht, vals_ht, mask, a, has_min, min_gidx) < 0;
+      ub = ht_lookup(keys_ht, vals_ht, mask, b, has_min, min_gidx) < 0;
+    }
+    const int64_t sa = wave_append(cnt, ua);
+    if (ua) out[sa] = uint64_t(a) ^ (1ull << 63);
+    const int64_t sb = wave_append(cnt, ub);
+    if (ub) out[sb] = uint64_t(b) ^ (1ull << 63);
+  }
+}
+// committed sort keys under new bytewise ranks: the src half stays, the dst rank is re-read
+__global__ void k_rekey(uint64_t* skey, const int32_t* dstg, int64_t n, const uint32_t* brank) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    skey[i] = (skey[i] & 0xffffffff00000000ull) | uint64_t(brank[dstg[i]]);
+}
+
+// bytewise order rank of every gidx (RocksDB key order of the dst bytes; holes sort anywhere)
+static DevBuf bytewise_ranks(Ctx& c) {
+  DevBuf brank;
+  const int64_t ng = std::max<int64_t>(c.n_global, 1);
+  DevBuf k1, k2, i1, i2;
+  k1.alloc(size_t(ng) * 8);
+  k2.alloc(size_t(ng) * 8);
+  i1.alloc(size_t(ng) * 4);
+  i2.alloc(size_t(ng) * 4);
+  brank.alloc(size_t(ng) * 4);
+  if (c.n_global) {
+    k_bswap_keys<<<grid_for(c.n_global), 256, 0, c.stream>>>(c.vid_of.as<int64_t>(), k1.as<uint64_t>(), i1.as<uint32_t>(),
+                                                             c.n_global);
+    radix_pairs<uint64_t, uint32_t>(c, k1.as<uint64_t>(), k2.as<uint64_t>(), i1.as<uint32_t>(), i2.as<uint32_t>(),
+                                    c.n_global, 64);
+    k_scatter_rank<<<grid_for(c.n_global), 256, 0, c.stream>>>(i2.as<uint32_t>(), brank.as<uint32_t>(), c.n_global);
+  }
+  return brank;
+}
+
+// Merge commit with new vertices (one rank): the batch's unknown endpoint vids, sorted, take
+// the gidx after the committed ones (the padding first, then a grown range), the vertex map and
+// hash table grow in place (the table is rebuilt when it would pass half full), the bytewise
+// ranks are recomputed and the committed sort keys re-read their dst rank -- the committed
+// order itself stays sorted, since inserting vids into the bytewise order moves no committed
+// vid past another.  Existing gidx never change, so every committed tuple keeps its place.
+static void extend_vertex_map(Ctx& c, int64_t unknown_bound) {
+  DevBuf raw, cnt;
+  raw.alloc(size_t(std::max<int64_t>(unknown_bound, 1)) * 8);
+  cnt.alloc(8);
+  NBG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
+  for (auto& kv : c.edges) {
+    EdgeSpace& es = kv.second;
+    for (int d = 0; d < 2; d++) {
+      const Staging& st = d ? es.in_stage : es.out_stage;
+      const int64_t n0 = es.ord[d].n;
+      if (st.n > n0)
+        k_collect_unknown<<<grid_for(st.n - n0), 256, 0, c.stream>>>(
+            st.src.as<int64_t>() + n0, st.dst.as<int64_t>() + n0, st.n - n0, c.ht_keys.as<int64_t>(),
+            c.ht_vals.as<int32_t>(), uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, raw.as<uint64_t>(),
+            cnt.as<unsigned long long>());
+    }
+  }
+  unsigned long long nraw = 0;
+  NBG_HIP(hipMemcpyAsync(&nraw, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  if (int64_t(nraw) > unknown_bound) throw Error(NBG_E_UNKNOWN, "merge commit: unknown-vertex count changed");
+  DevBuf sorted, uniq;
+  sorted.alloc(size_t(std::max<uint64_t>(nraw, 1)) * 8);
+  uniq.alloc(size_t(std::max<uint64_t>(nraw, 1)) * 8);
+  radix_keys<uint64_t>(c, raw.as<uint64_t>(), sorted.as<uint64_t>(), int64_t(nraw), 64);
+  const int64_t k = nraw ? unique_sorted<uint64_t>(c, sorted.as<uint64_t>(), uniq.as<uint64_t>(), int64_t(nraw)) : 0;
+  const int64_t n0 = c.n_vertices, n1 = n0 + k;
+  const int64_t ng1 = (n1 + 63) / 64 * 64;
+  if (ng1 >= (int64_t(1) << 31)) throw Error(NBG_E_UNSUPPORTED, "more than 2^31 vertices");
+  if (ng1 > c.n_global) {
+    DevBuf nv;
+    nv.alloc(size_t(ng1) * 8);
+    fill<int64_t>(c, nv.as<int64_t>(), INT64_MIN, ng1);
+    NBG_HIP(hipMemcpyAsync(nv.p, c.vid_of.p, size_t(c.n_global) * 8, hipMemcpyDeviceToDevice, c.stream));
+    c.vid_of = std::move(nv);
+  }
+  if (k) k_unflip<<<grid_for(k), 256, 0, c.stream>>>(uniq.as<uint64_t>(), c.vid_of.as<int64_t>() + n0, k);
+  DevBuf dmin;
+  dmin.alloc(4);
+  int32_t neg = -1;
+  NBG_HIP(hipMemcpyAsync(dmin.p, &neg, 4, hipMemcpyHostToDevice, c.stream));
+  if (2 * ng1 > c.ht_cap) {  // past half full: a table of the grown size, every vertex inserted
+    int64_t cap = 1024;
+    while (cap < 2 * ng1) cap <<= 1;
+    c.ht_cap = cap;
+    c.ht_keys.alloc(size_t(cap) * 8);
+    c.ht_vals.alloc(size_t(cap) * 4);
+    fill<int64_t>(c, c.ht_keys.as<int64_t>(), INT64_MIN, cap);
+    k_ht_insert<<<grid_for(n1), 256, 0, c.stream>>>(c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
+                                                   uint64_t(cap - 1), c.vid_of.as<int64_t>(), n1, 0, dmin.as<int32_t>());
+  } else if (k) {
+    k_ht_insert<<<grid_for(k), 256, 0, c.stream>>>(c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
+                                                  uint64_t(c.ht_cap - 1), c.vid_of.as<int64_t>() + n0, k, n0,
+                                                  dmin.as<int32_t>());
+  }
+  int32_t mg = -1;
+  NBG_HIP(hipMemcpyAsync(&mg, dmin.p, 4, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  if (mg >= 0) {
+    c.ht_has_min = true;
+    c.ht_min_gidx = mg;
+  }
+  c.n_vertices = n1;
+  c.counts.assign(1, n1);
+  c.base.assign(2, 0);
+  c.base[1] = ng1;
+  c.n_global = ng1;
+  c.brank = bytewise_ranks(c);
+  for (auto& kv : c.edges)
+    for (auto& o : kv.second.ord)
+      if (o.n > 0 && o.skey.p)
+        k_rekey<<<grid_for(o.n), 256, 0, c.stream>>>(o.skey.as<uint64_t>(), o.dstg.as<int32_t>(), o.n,
+                                                    c.brank.as<uint32_t>());
+  NBG_HIP(hipGetLastError());
+}
+
 static bool commit_merge(Ctx& c) {
   if (c.world != 1 || c.opt("merge_commit", 1) == 0 || !c.brank.p) return false;
-  for (auto& kv : c.tags)
-    if (kv.second.stage.n != kv.second.committed_n) return false;  // tag writes: full rebuild
+  bool tag_writes = false;
+  for (auto& kv : c.tags) tag_writes |= kv.second.stage.n != kv.second.committed_n;
+  if (tag_writes && c.opt("merge_tags", 1) == 0) return false;
   DevBuf cnt;
   cnt.alloc(8);
   NBG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
@@ -2059,7 +2191,15 @@ static bool commit_merge(Ctx& c) {
   unsigned long long unknown = 0;
   NBG_HIP(hipMemcpyAsync(&unknown, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
-  if (unknown) return false;  // new vertices: the vertex numbering changes
+  if (unknown) {
+    // new vertices extend the numbering (extend_vertex_map); every CSR direction then needs
+    // rows for them, which the merge builds only where the batch has tuples: other batches
+    // (and the off switch) take the full rebuild
+    if (c.opt("merge_new_vertices", 1) == 0) return false;
+    for (auto& kv : c.edges)
+      for (int d = 0; d < 2; d++)
+        if ((d ? kv.second.in_stage.n : kv.second.out_stage.n) == kv.second.ord[d].n) return false;
+  }
   PoolScope build_scope(build_pool(c));
   c.finalized = false;  // a merge that throws leaves the next commit a full rebuild
   const double t0 = now_s();
@@ -2076,6 +2216,21 @@ static bool commit_merge(Ctx& c) {
     tmark = t;
   };
   phase("checks");
+  if (unknown) {
+    extend_vertex_map(c, int64_t(unknown));
+    phase("vertex map (new vertices)");
+  }
+  if (unknown || tag_writes) {
+    // tag columns span the gidx space and pick winners over every staged row: rebuilt
+    c.tag_table.release();
+    for (auto& kv : c.tags) {
+      kv.second.cols.clear();
+      kv.second.part.release();
+    }
+    build_tag_columns(c);
+    for (auto& kv : c.tags) kv.second.committed_n = kv.second.stage.n;
+    phase("tag columns");
+  }
   for (auto& kv : c.edges) {
     EdgeSpace& es = kv.second;
     const bool out_changed = es.out_stage.n != es.ord[0].n, in_changed = es.in_stage.n != es.ord[1].n;
@@ -2635,21 +2790,7 @@ void snapshot_finalize(Ctx& c) {
   build_tag_columns(c);
   phase("tag columns");
   // 5. bytewise order rank of every vertex (for CSR row order = RocksDB key order)
-  DevBuf brank;
-  {
-    int64_t ng = std::max<int64_t>(c.n_global, 1);
-    DevBuf k1, k2, i1, i2;
-    k1.alloc(size_t(ng) * 8);
-    k2.alloc(size_t(ng) * 8);
-    i1.alloc(size_t(ng) * 4);
-    i2.alloc(size_t(ng) * 4);
-    brank.alloc(size_t(ng) * 4);
-    if (c.n_global) {
-      k_bswap_keys<<<grid_for(c.n_global), 256, 0, c.stream>>>(c.vid_of.as<int64_t>(), k1.as<uint64_t>(), i1.as<uint32_t>(), c.n_global);
-      radix_pairs<uint64_t, uint32_t>(c, k1.as<uint64_t>(), k2.as<uint64_t>(), i1.as<uint32_t>(), i2.as<uint32_t>(), c.n_global, 64);
-      k_scatter_rank<<<grid_for(c.n_global), 256, 0, c.stream>>>(i2.as<uint32_t>(), brank.as<uint32_t>(), c.n_global);
-    }
-  }
+  DevBuf brank = bytewise_ranks(c);
   phase("bytewise ranks");
   // 6. CSRs
   for (auto& kv : c.edges) {

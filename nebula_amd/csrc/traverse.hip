@@ -1957,6 +1957,8 @@ struct Counters {
   unsigned long long* h;  // pinned host mirror (64 entries)
 };
 
+}  // namespace
+
 // Copies n device counters into coherent host memory, then the sequence word: each thread's
 // store is made visible system-wide before thread 0 publishes the sequence number.
 __global__ void k_publish(const unsigned long long* __restrict__ src, int n, unsigned long long* dst,
@@ -2002,6 +2004,8 @@ void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long lo
     }
   }
 }
+
+namespace {
 
 int64_t map_bytes(const Ctx& c) { return ((c.n_global + 63) / 64) * 64 + 64; }
 

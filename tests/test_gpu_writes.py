@@ -99,12 +99,17 @@ def check_bound(sp, st, vids):
     assert ms(g.rows()) == ms(r.rows())
 
 
-def test_writes_commit_and_snapshot_view():
+@pytest.mark.parametrize("merge", [1, 0])
+def test_writes_commit_and_snapshot_view(merge):
+    """three commit rounds of AddEdges + AddVertices batches with brand-new vertices, newer
+    versions, identical-key rewrites and tag rows against the oracle; merge = 1: each commit
+    merges (new vertices extend the numbering, tag columns rebuilt), merge = 0: full rebuilds"""
     rng = random.Random(11)
     base, vids = random_space_kv(21)
     sp = GraphSpace(PARTS)
     try:
         sp.set_option("writable", 1)
+        sp.set_option("merge_commit", merge)
         sp.set_edge_schema(ET, [("weight", O.INT)])
         sp.set_tag_schema(PERSON, "person", FIELDS)
         for p, kv in base.items():
@@ -134,8 +139,10 @@ def test_writes_commit_and_snapshot_view():
             check_go(sp, st, starts + new_vids[:5])
             check_bound(sp, st, vids + new_vids)
             vids = vids + new_vids
+        assert sp.info(ET)["merge_commits"] == (3 if merge else 0)
         sp.commit()  # empty commit: same snapshot
         check_go(sp, st, starts)
+        check_bound(sp, st, vids)
     finally:
         sp.close()
 

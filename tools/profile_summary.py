@@ -20,7 +20,7 @@ BUILD = ("k_gen_rmat", "rocprim", "k_edge_keys", "k_dedup", "k_kept_src", "k_gat
          "k_row_part", "k_hub_key", "k_build_slab", "k_out_deg", "k_sorted_bounds", "k_src_global", "k_sub_lo",
          "k_count_deg", "k_row_counts", "k_not_u32", "k_col_vid", "k_pack_col", "k_minmax_w", "k_last_live",
          "k_build_pair", "k_build_slab", "k_gen_", "k_rmat_", "k_old_version", "k_ov_edges", "k_iota_off",
-         "k_count_unknown", "k_hash_part")
+         "k_count_unknown", "k_hash_part", "k_odeg8", "k_live_bounds", "k_class_key")
 
 
 def short(name: str) -> str:

@@ -67,6 +67,8 @@ def main():
     ap.add_argument("--edges", type=int, default=1 << 20)
     ap.add_argument("--trace", action="store_true", help="per-phase build / commit times on stderr")
     ap.add_argument("--commits", type=int, default=1, help="successive write batch + commit rounds")
+    ap.add_argument("--new-frac", type=float, default=0.0,
+                    help="fraction of the batch's edges whose dst is a brand-new vertex (AddEdges to new vids)")
     a = ap.parse_args()
     sp = GraphSpace(PARTS)
     sp.set_option("writable", 1)
@@ -86,6 +88,10 @@ def main():
         s, _ = synth.pairs(a.scale, 16, SEED, a.edges, pick_seed=5 + 2 * k)
         _, d = synth.pairs(a.scale, 16, SEED, a.edges, pick_seed=6 + 2 * k)
         w = rng.integers(1000, 2000, a.edges)
+        d = np.asarray(d, np.int64).copy()
+        if a.new_frac > 0:
+            sel = rng.random(a.edges) < a.new_frac
+            d[sel] = rng.integers(1, 2**62, int(sel.sum()))
         bs = batches(np.asarray(s, np.int64), np.asarray(d, np.int64), w, 2**63 - 3 - k)
         t1 = time.perf_counter()
         for p, lst in bs.items():
@@ -99,7 +105,9 @@ def main():
     info1 = sp.info(FOLLOW)
     go_after = go3(sp, starts)
     print(json.dumps({
-        "workload": f"rmat{a.scale} + {a.commits} x AddEdges batch of {a.edges} edges (out + in keys)",
+        "workload": f"rmat{a.scale} + {a.commits} x AddEdges batch of {a.edges} edges (out + in keys)"
+                    + (f", {a.new_frac:.0%} to new vertices" if a.new_frac > 0 else ""),
+        "vertices_before": info0.get("num_vertices"), "vertices_after": info1.get("num_vertices"),
         "initial_build_s": round(build_s, 3), "write_part_s": round(write_s, 3), "commit_s": round(commit_s, 3),
         "commit_s_each": commit_times, "write_part_s_each": write_times,
         "merge_commits": info1.get("merge_commits"),
