@@ -348,6 +348,7 @@ int32_t nbg_shortest_path(nbg_ctx* ctx, int32_t edge_type, const int64_t* src, c
 int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out) {
   return guarded(ctx, [&](Ctx& c) {
     if (!out) throw Error(NBG_E_INVALID_ARG, "null out");
+    nbg::resolve_total(c);
     out->total_ms = c.timing.total_ms;
     out->expand_ms = c.timing.expand_ms;
     out->expand_launches = c.timing.expand_launches;

@@ -502,6 +502,7 @@ struct Ctx {
     int32_t kind;  // 0: expand_ms + the hop's ms (+ kernel_ms of a top-down hop), 1: kernel_ms only
   };
   bool hop_timing = true;  // option hop_timing: event pairs around the hops' kernels (0: none)
+  bool total_pending = false;  // ev[1] recorded, total_ms not read yet (resolve_total)
   std::vector<hipEvent_t> tev;
   size_t tev_used = 0;
   std::vector<PendingTime> tpend;
@@ -575,7 +576,10 @@ void snapshot_commit(Ctx& c);
 void lookup_gidx(Ctx& c, const int64_t* d_vids, int32_t* d_gidx, int64_t n);
 // the device counters d[0, n) (n <= 256) into pinned host h[0, n) once every launch before has
 // finished on the context's stream (a one-block publish kernel + a host spin, traverse.hip)
-void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h);
+// `before` (optional): an event recorded just ahead of the publish kernel
+void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h, hipEvent_t before = nullptr);
+// a query's total_ms (ev[0] -> ev[1]) once asked for (go_run records ev[1] without waiting)
+void resolve_total(Ctx& c);
 // traverse.hip
 int32_t go_run(Ctx& c, const nbg_go_spec& spec, nbg_rows* out);
 int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* vids, size_t n,

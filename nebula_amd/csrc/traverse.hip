@@ -1988,8 +1988,9 @@ __global__ void k_gate(const unsigned long long* e, const unsigned long long* n,
 // one-thread-block kernel writes them and a sequence word to coherent host memory and the host
 // spins on the word (a memcpy + hipStreamSynchronize round trip cost ~19 us, tools/launch_gap);
 // past 2 s without it the stream is synchronised the ordinary way, which reports a fault
-void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h) {
+void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h, hipEvent_t before) {
   if (n > 256) throw Error(NBG_E_INVALID_ARG, "fetch_counters: at most 256 words");
+  if (before) NBG_HIP(hipEventRecord(before, c.stream));
   const uint64_t seq = ++c.pub_seq;
   k_publish<<<1, 256, 0, c.stream>>>(d, n, h, c.host_seq, seq);
   NBG_HIP(hipGetLastError());
@@ -2003,6 +2004,15 @@ void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long lo
       throw Error(NBG_E_DEVICE, "counter publication lost");
     }
   }
+}
+
+// the query's device time (ev[0] -> ev[1]) once it is asked for: go_run does not wait for ev[1]
+void resolve_total(Ctx& c) {
+  if (!c.total_pending) return;
+  c.total_pending = false;
+  float ms = 0;
+  if (hipEventSynchronize(c.ev[1]) == hipSuccess && hipEventElapsedTime(&ms, c.ev[0], c.ev[1]) == hipSuccess)
+    c.timing.total_ms = ms;
 }
 
 namespace {
@@ -2594,6 +2604,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   c.hop_timing = c.opt("hop_timing", 1) != 0;
   if (c.host_stage_used) NBG_HIP(hipStreamSynchronize(c.stream));  // a failed query's copies
   c.host_stage_used = 0;
+  c.total_pending = false;
   hipEventRecord(c.ev[0], c.stream);
 
   // compile WHERE / YIELD (errors are deferred to the final step, as the reference only
@@ -2940,6 +2951,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     }
   };
   auto spec_words = [&](int base) { return spec.empty() ? base : 64 + 16 * int(spec.size()); };
+  auto spec_final = [&]() { return !spec.empty() && spec.back().final; };
   // after the fetch: record the hops that ran, as the bottom-up branch below does; stops at the
   // first gate that was 0 (its timings dropped).  Returns the steps consumed; *fin_done when the
   // final step ran (its counters copied to fin_h)
@@ -3010,7 +3022,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
                      K.d, es.odeg.as<uint32_t>());
       spec_enqueue(2, K.d + 13, K.d + 12, c.timing.n_hops + 1);  // (hop 1 is recorded below)
-      fetch_counters(c, K.d, spec_words(42), K.h);
+      // (the device work ends here when the speculated final hop runs: ev[1] ahead of the fetch)
+      fetch_counters(c, K.d, spec_words(42), K.h, spec_final() ? c.ev[1] : nullptr);
       const int64_t nF1 = int64_t(K.h[40]), E1 = int64_t(K.h[41]);
       if (!s.distinct) hop1_scanned = int64_t(K.h[30]);
       c.timing.edges_scanned += uint64_t(hop1_scanned >= 0 ? hop1_scanned : E1);
@@ -3096,7 +3109,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
                      K.d, es.odeg.as<uint32_t>());
       if (lazy) spec_enqueue(step + 1, K.d + 13, K.d + 12, c.timing.n_hops);
-      fetch_counters(c, K.d, spec_words(16), K.h);
+      fetch_counters(c, K.d, spec_words(16), K.h, spec_final() ? c.ev[1] : nullptr);
       nF = lazy ? 0 : int64_t(K.h[0]);
       list_n = lazy ? int64_t(K.h[14]) : -1;
       E = int64_t(K.h[13]);
@@ -3345,11 +3358,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     delete h;
     throw;
   }
-  hipEventRecord(c.ev[1], c.stream);
-  NBG_HIP(hipEventSynchronize(c.ev[1]));
-  float ms = 0;
-  hipEventElapsedTime(&ms, c.ev[0], c.ev[1]);
-  c.timing.total_ms = ms;
+  // ev[1] ends the device time; not waited for here (resolve_total reads it when asked): a
+  // speculated final hop recorded it ahead of its counter fetch, after which nothing was enqueued
+  if (!fin_done) hipEventRecord(c.ev[1], c.stream);
+  c.total_pending = true;
   // STRING columns: (address, length) rows -> packed bytes + n+1 offsets
   const size_t ncols_out = h->types.size();
   std::vector<int64_t> soff_dev_idx(ncols_out, -1);
@@ -3372,7 +3384,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       soff_dev_idx[cc] = int64_t(h->dev.size());
       h->dev.push_back(std::move(off));
     }
-    NBG_HIP(hipStreamSynchronize(c.stream));
+    // the result is complete before it is handed out (a drained stream costs no wait)
+    if (hipStreamQuery(c.stream) != hipSuccess) NBG_HIP(hipStreamSynchronize(c.stream));
+    c.host_stage_used = 0;  // the query's input copies have completed
   } catch (...) {
     delete h;
     throw;
