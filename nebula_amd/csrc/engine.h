@@ -366,7 +366,15 @@ struct EdgeSpace {
   int64_t q_min = 0;
   uint64_t q_range = 1;
   DevBuf tcol_q;
+  // rest records (bottom-up rest pass): one 64-byte line per transposed row below brec_rows (the
+  // rows a bottom-up hop can leave pending): words 0-1 the row's start in tr (bits 0-47) and
+  // min(in-degree, 65535) (bits 48-63), words 2-15 its first kRecEntries entries as in tcol_q /
+  // tr.col (-1 past the row).  A pending row then costs one line instead of a row_ptr line and
+  // one or two column lines.
+  DevBuf brec;
+  int64_t brec_rows = 0;
 };
+constexpr int kRecEntries = 14;
 
 // Vertex tag props: per tag, one row per vertex = the bytewise-first version under
 // the vertex key prefix (part, vid, tag) of the vid's own part -- what collectVertexProps reads
@@ -494,6 +502,7 @@ struct Ctx {
   hipEvent_t ev[8] = {};
   DevBuf ws_tile_rows;  // k_expand: frontier entry of each tile's first slot
   std::string bu_kernel_name, bu_rest_name;  // rocprof names of the last bottom-up launch
+  bool bu_rest_rec = false;                  // ... whose rest pass read the rest records
   // deferred kernel timing: event pairs recorded around expansion launches and read once the
   // query's stream has drained, so timing never makes the host wait on a launch
   struct PendingTime {

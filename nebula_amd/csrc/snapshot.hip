@@ -491,10 +491,8 @@ void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
 // transposes and tag columns from the log on the device -- nothing is re-uploaded -- and until
 // then queries keep reading the previous commit (a RocksDB snapshot's view).
 // ------------------------------------------------------------------------------------------
-// drop everything snapshot_finalize derives from the staged tuples
-static void reset_edge_derived(EdgeSpace& es) {
-  es.out = Csr();
-  es.in = Csr();
+// drop what build_transpose derives from the out CSRs of every rank
+static void reset_transpose_derived(EdgeSpace& es) {
   es.rep_out = Csr();
   es.rep_in = Csr();
   es.has_rep = false;
@@ -510,6 +508,15 @@ static void reset_edge_derived(EdgeSpace& es) {
   es.odeg8.release();
   es.max_odeg = -1;
   es.bu_in_tiles = es.bu_both_tiles = 0;
+  es.brec.release();
+  es.brec_rows = 0;
+}
+
+// drop everything snapshot_finalize derives from the staged tuples
+static void reset_edge_derived(EdgeSpace& es) {
+  es.out = Csr();
+  es.in = Csr();
+  reset_transpose_derived(es);
 }
 
 static void reset_derived(Ctx& c) {
@@ -540,10 +547,12 @@ static void reset_derived(Ctx& c) {
   c.sp = Ctx::SpWork();
 }
 
-// Merge commit (one rank, edge writes only, no new vertex): the vertex numbering, vertex map
-// and tag columns stay; each edge CSR merges its sorted batch into the committed order
-// (build_csr merge mode) and the transposed CSR is rebuilt from the new out CSR.  Returns false
-// when the batch needs the full rebuild (new vertices, tag writes, several ranks).
+// Merge commit: each edge CSR merges its sorted batch into the committed order (build_csr merge
+// mode) and the transposed CSR is rebuilt from the new out CSRs.  One rank: new vertices extend
+// the numbering (appended gidx) and tag writes rebuild the tag columns.  Several ranks: batches
+// of edges and tag rows merge on every rank together; a batch with a new vertex anywhere takes
+// the full rebuild (appending to one rank's gidx range would move every later rank's).  Returns
+// false when the batch needs the full rebuild.
 static bool commit_merge(Ctx& c);
 
 void snapshot_write_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t* koff,
@@ -875,12 +884,45 @@ __global__ void k_dedup_flags(const uint64_t* skey, const uint32_t* perm, const 
 }
 
 // row_ptr from row keys sorted ascending (no atomics): row_ptr[v] = first i with key[i] >= v
-__global__ void k_rowptr_sorted(const uint32_t* keys, int64_t m, int64_t n, int64_t* row_ptr) {
+// row_ptr[0, n] from the sorted row keys of m entries: entry i (i = m: the end) opens the rows
+// (keys[i - 1], keys[i]].  A run of more than kRowRun rows (rows without entries: with the
+// class-ordered numbering the in-only class of an out CSR is one run of millions) goes to a list
+// filled by k_rowptr_runs, one block per run -- one thread storing it row by row took 10 ms at
+// RMAT-22 and most of a merge commit at RMAT-26.
+constexpr int64_t kRowRun = 64;
+__global__ void k_rowptr_sorted(const uint32_t* keys, int64_t m, int64_t n, int64_t* row_ptr, int64_t* runs,
+                                unsigned long long* nruns, int64_t cap) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= m; i += int64_t(gridDim.x) * blockDim.x) {
-    int64_t prev = i == 0 ? -1 : int64_t(keys[i - 1]);
-    int64_t cur = i == m ? n : int64_t(keys[i]);
+    const int64_t prev = i == 0 ? -1 : int64_t(keys[i - 1]);
+    const int64_t cur = i == m ? n : int64_t(keys[i]);
+    if (cur - prev > kRowRun) {
+      const unsigned long long slot = atomicAdd(nruns, 1ull);
+      if (int64_t(slot) < cap) {
+        runs[3 * slot] = prev + 1, runs[3 * slot + 1] = cur, runs[3 * slot + 2] = i;
+        continue;
+      }
+    }
     for (int64_t v = prev + 1; v <= cur; v++) row_ptr[v] = i;
   }
+}
+__global__ void k_rowptr_runs(const int64_t* runs, const unsigned long long* nruns, int64_t cap, int64_t* row_ptr) {
+  const int64_t nr = int64_t(*nruns) < cap ? int64_t(*nruns) : cap;
+  for (int64_t r = blockIdx.x; r < nr; r += gridDim.x) {
+    const int64_t a = runs[3 * r], b = runs[3 * r + 1], val = runs[3 * r + 2];
+    for (int64_t v = a + threadIdx.x; v <= b; v += blockDim.x) row_ptr[v] = val;
+  }
+}
+static void rowptr_from_sorted(Ctx& c, const uint32_t* keys, int64_t m, int64_t n, int64_t* row_ptr) {
+  // every listed run holds more than kRowRun of the n + 1 rows
+  const int64_t cap = (n + 1) / kRowRun + 1;
+  DevBuf runs, cnt;
+  runs.alloc(size_t(cap) * 24);
+  cnt.alloc(8);
+  NBG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
+  k_rowptr_sorted<<<grid_for(m + 1), 256, 0, c.stream>>>(keys, m, n, row_ptr, runs.as<int64_t>(),
+                                                        cnt.as<unsigned long long>(), cap);
+  k_rowptr_runs<<<1024, 256, 0, c.stream>>>(runs.as<int64_t>(), cnt.as<unsigned long long>(), cap, row_ptr);
+  NBG_HIP(hipGetLastError());
 }
 __global__ void k_kept_src(const uint64_t* skey, const uint32_t* kept, int64_t m, uint32_t* out) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x)
@@ -1284,8 +1326,7 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
     DevBuf ks;
     ks.alloc(size_t(m + 1) * 4);
     k_kept_src<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(skey_keep.as<uint64_t>(), kp, int64_t(m), ks.as<uint32_t>());
-    k_rowptr_sorted<<<grid_for(int64_t(m) + 1), 256, 0, c.stream>>>(ks.as<uint32_t>(), int64_t(m), out.n_rows,
-                                                                   out.row_ptr.as<int64_t>());
+    rowptr_from_sorted(c, ks.as<uint32_t>(), int64_t(m), out.n_rows, out.row_ptr.as<int64_t>());
     NBG_HIP(hipStreamSynchronize(c.stream));
   }
   // row_part: hash rule by default, the key's part where the staging recorded it
@@ -1499,6 +1540,22 @@ __global__ void k_build_pair(const int64_t* trp, const T* src, int64_t n, T* lo,
   }
 }
 
+// rest records (EdgeSpace::brec): row d's start and clamped in-degree, then its first
+// kRecEntries entries of src, as one 64-byte line (four 16-byte stores)
+__global__ void k_build_rec(const int64_t* trp, const int32_t* src, int64_t n, uint4* rec) {
+  for (int64_t d = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; d < n; d += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t b = trp[d], e = trp[d + 1];
+    const uint64_t deg = uint64_t(e - b) < 65535u ? uint64_t(e - b) : 65535u;
+    uint32_t w[16];
+    w[0] = uint32_t(uint64_t(b));
+    w[1] = uint32_t(uint64_t(b) >> 32) | uint32_t(deg << 16);
+#pragma unroll
+    for (int k = 0; k < kRecEntries; k++) w[2 + k] = b + k < e ? uint32_t(src[b + k]) : 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < 4; j++) rec[size_t(d) * 4 + j] = make_uint4(w[4 * j], w[4 * j + 1], w[4 * j + 2], w[4 * j + 3]);
+  }
+}
+
 // Transpose of the out CSR for bottom-up hops: rows = owned dst, entries = global src index,
 // plus copies of the INT-like props in transpose order.  With several ranks every out-edge is
 // shipped to the owner of its dst (one build-time all-to-all), so each rank can run bottom-up
@@ -1662,7 +1719,7 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
     radix_pairs<uint32_t, uint32_t>(c, key.as<uint32_t>(), keyS.as<uint32_t>(), perm1.as<uint32_t>(),
                                    perm.as<uint32_t>(), R, nbits(n_own));
     k_gather_w<int32_t><<<grid_for(R), 256, 0, c.stream>>>(tsrc.as<int32_t>(), perm.as<uint32_t>(), t.col.as<int32_t>(), R);
-    k_rowptr_sorted<<<grid_for(R + 1), 256, 0, c.stream>>>(keyS.as<uint32_t>(), R, t.n_rows, t.row_ptr.as<int64_t>());
+    rowptr_from_sorted(c, keyS.as<uint32_t>(), R, t.n_rows, t.row_ptr.as<int64_t>());
   } else {
     NBG_HIP(hipMemsetAsync(t.row_ptr.p, 0, size_t(t.n_rows + 1) * 8, c.stream));
   }
@@ -1747,6 +1804,21 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
     NBG_HIP(hipStreamSynchronize(c.stream));
     es.bu_in_tiles = int64_t((h[0] + 127) / 128);
     es.bu_both_tiles = int64_t((h[1] + 127) / 128);
+  }
+  es.brec.release();
+  es.brec_rows = 0;
+  {
+    // rest records for the rows a bottom-up hop reads (bu_rec_mb: at most that many MiB, else
+    // the rest pass reads row_ptr and the columns)
+    const int64_t rows = std::min(n_own, es.bu_in_tiles * 128);
+    const int64_t cap_mb = c.opt("bu_rec_mb", 8192);
+    if (rows > 0 && c.opt("bu_rec", 1) != 0 && rows * 64 <= (cap_mb << 20)) {
+      es.brec.alloc(size_t(rows) * 64);
+      const int32_t* src_col = es.q_field >= 0 ? es.tcol_q.as<int32_t>() : t.col.as<int32_t>();
+      k_build_rec<<<grid_for(rows), 256, 0, c.stream>>>(t.row_ptr.as<int64_t>(), src_col, rows, es.brec.as<uint4>());
+      NBG_HIP(hipGetLastError());
+      es.brec_rows = rows;
+    }
   }
   NBG_HIP(hipStreamSynchronize(c.stream));
   NBG_HIP(hipGetLastError());
@@ -2168,21 +2240,26 @@ static void extend_vertex_map(Ctx& c, int64_t unknown_bound) {
 }
 
 static bool commit_merge(Ctx& c) {
-  if (c.world != 1 || c.opt("merge_commit", 1) == 0 || !c.brank.p) return false;
+  // several ranks: the choice is collective (every rank merges or every rank rebuilds), agreed by
+  // one sum over the ranks' flags below; the option and c.brank (writable) agree on every rank
+  if (c.opt("merge_commit", 1) == 0 || !c.brank.p) return false;
   bool tag_writes = false;
   for (auto& kv : c.tags) tag_writes |= kv.second.stage.n != kv.second.committed_n;
-  if (tag_writes && c.opt("merge_tags", 1) == 0) return false;
+  bool refuse = tag_writes && c.opt("merge_tags", 1) == 0;
   DevBuf cnt;
   cnt.alloc(8);
   NBG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
   for (auto& kv : c.edges) {
     EdgeSpace& es = kv.second;
-    if (es.rmat_stream) return false;
-    for (int d = 0; d < 2; d++) {
+    if (es.rmat_stream) refuse = true;
+    for (int d = 0; d < 2 && !refuse; d++) {
       const Staging& st = d ? es.in_stage : es.out_stage;
       const int64_t n0 = es.ord[d].n;
       if (st.n == n0) continue;
-      if (n0 <= 0 || !es.ord[d].perm.p || st.n < n0 || st.seq.bytes < size_t(st.n) * 8) return false;
+      if (n0 <= 0 || !es.ord[d].perm.p || st.n < n0 || st.seq.bytes < size_t(st.n) * 8) {
+        refuse = true;
+        break;
+      }
       k_count_unknown<<<grid_for(st.n - n0), 256, 0, c.stream>>>(
           st.src.as<int64_t>() + n0, st.dst.as<int64_t>() + n0, st.n - n0, c.ht_keys.as<int64_t>(),
           c.ht_vals.as<int32_t>(), uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, cnt.as<unsigned long long>());
@@ -2191,15 +2268,39 @@ static bool commit_merge(Ctx& c) {
   unsigned long long unknown = 0;
   NBG_HIP(hipMemcpyAsync(&unknown, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
-  if (unknown) {
+  if (!refuse && unknown) {
     // new vertices extend the numbering (extend_vertex_map); every CSR direction then needs
     // rows for them, which the merge builds only where the batch has tuples: other batches
     // (and the off switch) take the full rebuild
-    if (c.opt("merge_new_vertices", 1) == 0) return false;
+    if (c.opt("merge_new_vertices", 1) == 0) refuse = true;
     for (auto& kv : c.edges)
       for (int d = 0; d < 2; d++)
-        if ((d ? kv.second.in_stage.n : kv.second.out_stage.n) == kv.second.ord[d].n) return false;
+        if ((d ? kv.second.in_stage.n : kv.second.out_stage.n) == kv.second.ord[d].n) refuse = true;
   }
+  // per edge space: did this rank's out / in CSR change (a rank without writes of its own still
+  // rebuilds its transposed rows when another rank's out-edges changed)
+  const size_t ne = c.edges.size();
+  std::vector<int64_t> flags(3 + 2 * ne, 0);
+  {
+    size_t i = 3;
+    for (auto& kv : c.edges) {
+      flags[i++] = kv.second.out_stage.n != kv.second.ord[0].n;
+      flags[i++] = kv.second.in_stage.n != kv.second.ord[1].n;
+    }
+  }
+  flags[0] = refuse, flags[1] = int64_t(unknown), flags[2] = tag_writes;
+  if (c.world > 1) {
+    DevBuf f;
+    f.alloc(flags.size() * 8);
+    NBG_HIP(hipMemcpyAsync(f.p, flags.data(), flags.size() * 8, hipMemcpyHostToDevice, c.stream));
+    comm_allreduce_sum_i64(c, f.as<int64_t>(), flags.size());
+    NBG_HIP(hipMemcpyAsync(flags.data(), f.p, flags.size() * 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    // new vertices would move every later rank's gidx range: the full rebuild renumbers
+    if (flags[1] > 0) flags[0] = 1;
+  }
+  if (flags[0]) return false;
+  const bool any_tags = flags[2] > 0;
   PoolScope build_scope(build_pool(c));
   c.finalized = false;  // a merge that throws leaves the next commit a full rebuild
   const double t0 = now_s();
@@ -2220,8 +2321,9 @@ static bool commit_merge(Ctx& c) {
     extend_vertex_map(c, int64_t(unknown));
     phase("vertex map (new vertices)");
   }
-  if (unknown || tag_writes) {
-    // tag columns span the gidx space and pick winners over every staged row: rebuilt
+  if (unknown || any_tags) {
+    // tag columns span the gidx space and pick winners over every staged row: rebuilt (on every
+    // rank when any has tag writes: the owned slices are allgathered)
     c.tag_table.release();
     for (auto& kv : c.tags) {
       kv.second.cols.clear();
@@ -2231,19 +2333,30 @@ static bool commit_merge(Ctx& c) {
     for (auto& kv : c.tags) kv.second.committed_n = kv.second.stage.n;
     phase("tag columns");
   }
+  size_t fi = 3;
   for (auto& kv : c.edges) {
     EdgeSpace& es = kv.second;
     const bool out_changed = es.out_stage.n != es.ord[0].n, in_changed = es.in_stage.n != es.ord[1].n;
+    const bool out_any = flags[fi] > 0, in_any = flags[fi + 1] > 0;  // on some rank
+    fi += 2;
     if (out_changed) {
       Csr keep_in = std::move(es.in);  // an unchanged in CSR survives the reset
       reset_edge_derived(es);          // out CSR and everything derived from it (transpose, slabs)
       es.in = std::move(keep_in);
       build_csr(c, es.out_stage, es.fields, true, es.out, c.brank.as<uint32_t>(), false, &es.ord[0], true);
       phase("out CSR (merge)");
+    } else if (out_any) {
+      reset_transpose_derived(es);  // another rank's out-edges land in this rank's transposed rows
     }
     if (in_changed) build_csr(c, es.in_stage, es.fields, false, es.in, c.brank.as<uint32_t>(), false, &es.ord[1], true);
     phase("in CSR (merge)");
-    if (out_changed && c.opt("bottom_up", 1)) build_transpose(c, es);
+    if (out_any || in_any) {
+      // replicated CSRs (FIND SHORTEST PATH on several ranks) are rebuilt on first use
+      es.rep_out = Csr();
+      es.rep_in = Csr();
+      es.has_rep = false;
+    }
+    if (out_any && c.opt("bottom_up", 1)) build_transpose(c, es);  // collective on several ranks
     phase("transpose + slabs");
   }
   c.ws_tmp.release();

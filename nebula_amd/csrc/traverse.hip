@@ -1247,7 +1247,9 @@ __device__ inline void load_chunk8(const int32_t* __restrict__ tcol, int64_t a, 
   sv[0] = x.x, sv[1] = x.y, sv[2] = x.z, sv[3] = x.w;
   sv[4] = y.x, sv[5] = y.y, sv[6] = y.z, sv[7] = y.w;
 }
-template <int PK, int W, int HUB>
+// REC: a pending row's start, in-degree and first kRecEntries entries come from its rest record
+// (EdgeSpace::brec, one 64-byte line); rows longer than that continue in tcol from there.
+template <int PK, int W, int HUB, int REC>
 __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long long* __restrict__ pbits, int64_t n,
                                                           const int64_t* __restrict__ trp,
                                                           const int32_t* __restrict__ tcol,
@@ -1255,7 +1257,8 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
                                                           const uint32_t* __restrict__ odeg, FastArgs fp, QArgs q_arg,
                                                           unsigned long long* partials, int cw, int ru, int rest_from,
                                                           int steps, unsigned long long* dbg,
-                                                          const unsigned long long* __restrict__ gate) {
+                                                          const unsigned long long* __restrict__ gate,
+                                                          const uint4* __restrict__ rec) {
   if (gate && *gate == 0ull) return;
   const QArgs q = q_sgpr(q_arg);
   __shared__ unsigned long long lds[kSlots * 16];
@@ -1311,27 +1314,16 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
       for (int st = 32; st > 0; st >>= 1)
         if (uint32_t(__popcll(wbits & ((1ull << (bit + st)) - 1ull))) <= kk) bit += st;
       const int32_t r = int32_t((cbase + int64_t(wsel) * nwaves + wave) * 64 + bit);
-      int64_t r0 = 0;  // the row's first entry to test; chunks start at the aligned a <= r0
-      if (pend[0]) {
-        r0 = trp[r] + rest_from;
-        re[0] = trp[r + 1];
-        rb[0] = r0 & ~int64_t(3);
-        pend[0] = r0 < re[0];
-      }
-      d_batches++;
-      d_rows += p < total;
-      for (int step = 0; step < steps; step++) {
-        if (__ballot(pend[0]) == 0) break;
-        d_steps++;
-        int32_t sv[kLeanChunk];
-        load_chunk8(tcol, rb[0], re[0], pend[0], sv);
-        __builtin_amdgcn_sched_barrier(0);
+      // the entries [base, base + 8) (those in [lo_e, hi_e) are valid): bitmap probes, then the
+      // tests; a frontier hit in the constant's bucket reads its value.  Wave-uniform call.
+      auto test_chunk = [&](const int32_t(&sv)[kLeanChunk], int64_t base, int64_t lo_e, int64_t hi_e, bool act,
+                            bool count) __attribute__((always_inline)) -> bool {
         uint32_t w[kLeanChunk];
         int tq[kLeanChunk];
 #pragma unroll
         for (int k = 0; k < kLeanChunk; k++) {
-          const bool valid = pend[0] && rb[0] + k >= r0 && rb[0] + k < re[0];
-          acc[4] += valid;
+          const bool valid = act && base + k >= lo_e && base + k < hi_e;
+          if (count) acc[4] += valid;  // column entries (a record's are in its line)
           tq[k] = PK == PK_FAST ? q_test(sv[k], q) : 1;
           const bool cand = valid && tq[k] != 0;
           const int32_t wi = q_gidx(sv[k], q) >> 5;
@@ -1364,10 +1356,54 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
             for (int k = 0; k < kLeanChunk; k++)
               if ((und >> k) & 1u) {
                 acc[5]++;
-                h = h || fast_cmp(fp.op, load_w<W>(fp.data, fp.width, rb[0] + k), fp.k);
+                h = h || fast_cmp(fp.op, load_w<W>(fp.data, fp.width, base + k), fp.k);
               }
           }
         }
+        return h;
+      };
+      int64_t r0 = 0;  // the row's first entry to test; chunks start at the aligned a <= r0
+      if (REC) {
+        // the rest record: entries [0, 8) and [8, kRecEntries), then tcol past kRecEntries
+        uint4 x0 = make_uint4(0u, 0u, 0u, 0u), x1 = x0, x2 = x0, x3 = x0;
+        if (pend[0]) {
+          const uint4* rp = rec + size_t(r) * 4;
+          x0 = rp[0], x1 = rp[1], x2 = rp[2], x3 = rp[3];
+        }
+        const int64_t start = int64_t(x0.x) | (int64_t(x0.y & 0xffffu) << 32);
+        const uint32_t deg = x0.y >> 16;
+        const int64_t rend = start + int64_t(deg < uint32_t(kRecEntries) ? deg : uint32_t(kRecEntries));
+        r0 = start + rest_from;
+        const int32_t sa[kLeanChunk] = {int32_t(x0.z), int32_t(x0.w), int32_t(x1.x), int32_t(x1.y),
+                                        int32_t(x1.z), int32_t(x1.w), int32_t(x2.x), int32_t(x2.y)};
+        bool h = test_chunk(sa, start, r0, rend, pend[0], false);
+        if (__ballot(pend[0] && !h && deg > 8u)) {
+          const int32_t sb[kLeanChunk] = {int32_t(x2.z), int32_t(x2.w), int32_t(x3.x), int32_t(x3.y),
+                                          int32_t(x3.z), int32_t(x3.w), -1, -1};
+          h = test_chunk(sb, start + 8, r0, rend, pend[0] && !h, false) || h;
+        }
+        if (h) found[0] = true;
+        pend[0] = pend[0] && !h && deg > uint32_t(kRecEntries);
+        if (pend[0]) {
+          re[0] = deg < 65535u ? start + deg : trp[r + 1];
+          r0 = start + kRecEntries;
+          rb[0] = r0 & ~int64_t(3);
+        }
+      } else if (pend[0]) {
+        r0 = trp[r] + rest_from;
+        re[0] = trp[r + 1];
+        rb[0] = r0 & ~int64_t(3);
+        pend[0] = r0 < re[0];
+      }
+      d_batches++;
+      d_rows += p < total;
+      for (int step = 0; step < steps; step++) {
+        if (__ballot(pend[0]) == 0) break;
+        d_steps++;
+        int32_t sv[kLeanChunk];
+        load_chunk8(tcol, rb[0], re[0], pend[0], sv);
+        __builtin_amdgcn_sched_barrier(0);
+        const bool h = test_chunk(sv, rb[0], r0, re[0], pend[0], true);
         if (h) found[0] = true;
         rb[0] += kLeanChunk;
         pend[0] = pend[0] && !h && rb[0] < re[0];
@@ -2515,15 +2551,25 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     NBG_HIP(hipMemsetAsync(dbg_buf.p, 0, size_t(grid2) * 16 * 64, c.stream));
     dbg = dbg_buf.as<unsigned long long>();
   }
+  // pending bits exist only below the work tiles (the first pass zeroes the words past them)
+  const int64_t rest_rows = std::min(tr.n_rows, work * 128);
+  // rest records cover every row the first pass can leave pending (rows below work tiles)
+  const bool use_rec = es.brec.p && es.brec_rows >= std::min(tr.n_rows, work * 128) && c.opt("bu_rec", 1) != 0;
+  const uint4* rec = use_rec ? es.brec.as<uint4>() : nullptr;
   auto rest = [&](auto kern) {
     if (rshm > 48 * 1024)
       lds_limit(reinterpret_cast<const void*>(kern), rshm);
-    kern<<<grid2, 1024, rshm, c.stream>>>(pbits, tr.n_rows, trp, tc, fb, nb, odeg, fp, q, partials + grid, rcw, ru,
-                                          rest_from, rsteps, dbg, gate);
+    kern<<<grid2, 1024, rshm, c.stream>>>(pbits, rest_rows, trp, tc, fb, nb, odeg, fp, q, partials + grid, rcw, ru,
+                                          rest_from, rsteps, dbg, gate, rec);
   };
-#define NBG_REST(PKV, WV)                        \
-  if (rcw > 0) rest(k_bu_rest_lean<PKV, WV, 1>); \
-  else rest(k_bu_rest_lean<PKV, WV, 0>)
+#define NBG_REST(PKV, WV)                                                 \
+  if (rcw > 0) {                                                          \
+    if (use_rec) rest(k_bu_rest_lean<PKV, WV, 1, 1>);                     \
+    else rest(k_bu_rest_lean<PKV, WV, 1, 0>);                             \
+  } else {                                                                \
+    if (use_rec) rest(k_bu_rest_lean<PKV, WV, 0, 1>);                     \
+    else rest(k_bu_rest_lean<PKV, WV, 0, 0>);                             \
+  }
   if (fast) {
     switch (W) {
       case 1: NBG_REST(PK_FAST, 1); break;
@@ -2559,7 +2605,8 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
              probe_stats ? 1 : 0, sel == 6 ? ", 1" : "");
   c.bu_kernel_name = nm;
   const int wn = fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0;
-  snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d>", pk, wn, rcw > 0 ? 1 : 0);
+  snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d, %d>", pk, wn, rcw > 0 ? 1 : 0, use_rec ? 1 : 0);
+  c.bu_rest_rec = use_rec;
   c.bu_rest_name = nm;
   return ev_first;
 }
@@ -2571,8 +2618,8 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
 uint64_t bu_first_bytes(const unsigned long long* h, int64_t n_rows, bool with_odeg) {
   return h[2] * 4 + 3 * (uint64_t(n_rows) / 8) + (with_odeg ? uint64_t(n_rows) * 4 : 0);
 }
-uint64_t bu_rest_bytes(const unsigned long long* h, int pred_width) {
-  return h[3] * 16 + h[4] * 4 + h[5] * uint64_t(pred_width);
+uint64_t bu_rest_bytes(const unsigned long long* h, int pred_width, bool rec) {
+  return h[3] * (rec ? 64 : 16) + h[4] * 4 + h[5] * uint64_t(pred_width);
 }
 // algorithmic bytes of one expansion (DESIGN.md "byte model"): frontier id 4 B + row_ptr pair
 // 16 B + off 8 B per frontier entry; per edge: col 4 B (+ predicate column width) + the
@@ -2980,7 +3027,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       c.timing.edges_scanned += uint64_t(E);
       c.timing.expand_launches++;
       c.timing.bu_steps++;
-      const uint64_t kb = bu_first_bytes(hh, es.tr.n_rows, true), hb = kb + bu_rest_bytes(hh, 0);
+      const uint64_t kb = bu_first_bytes(hh, es.tr.n_rows, true), hb = kb + bu_rest_bytes(hh, 0, c.bu_rest_rec);
       c.timing.expand_bytes += hb;
       c.timing.hop(1, false, 0.0, hh, 0.0, kb);
       c.timing.name_last_hop(spec[j].k0, spec[j].k1);
@@ -3060,7 +3107,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       fetch_counters(c, K.d, 8, K.h);
       c.timing.expand_launches++;
       c.timing.bu_steps++;
-      const uint64_t kb = bu_first_bytes(K.h, tr.n_rows, true), hb = kb + bu_rest_bytes(K.h, 0);
+      const uint64_t kb = bu_first_bytes(K.h, tr.n_rows, true), hb = kb + bu_rest_bytes(K.h, 0, c.bu_rest_rec);
       c.timing.expand_bytes += hb;
       c.timing.hop(1, false, 0.0, K.h, 0.0, kb);
       c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name);
@@ -3172,7 +3219,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         c.timing.bu_steps++;
         nrows = int64_t(fin_h[9]);
         const int pw = pk == PK_FAST ? fp.width : 0;
-        const uint64_t kb = bu_first_bytes(fin_h, es.tr.n_rows, false), hb = kb + bu_rest_bytes(fin_h, pw);
+        const uint64_t kb = bu_first_bytes(fin_h, es.tr.n_rows, false), hb = kb + bu_rest_bytes(fin_h, pw, c.bu_rest_rec);
         c.timing.expand_bytes += hb + uint64_t(es.tr.n_rows) / 8 + uint64_t(nrows) * 16;
         c.timing.hop(1, true, 0.0, fin_h, 0.0, kb);
         c.timing.name_last_hop(fin_k0, fin_k1, "nbg::k_bits_compact<1>");
@@ -3199,7 +3246,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         c.timing.bu_steps++;
         nrows = int64_t(K.h[0]);
         const int pw = pk == PK_FAST ? tfp.width : 0;
-        const uint64_t kb = bu_first_bytes(K.h + 8, tr.n_rows, false), hb = kb + bu_rest_bytes(K.h + 8, pw);
+        const uint64_t kb = bu_first_bytes(K.h + 8, tr.n_rows, false), hb = kb + bu_rest_bytes(K.h + 8, pw, c.bu_rest_rec);
         // + the DISTINCT _dst output (k_bits_compact<1>): next bits once, vid_of read + vid written
         c.timing.expand_bytes += hb + uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
         c.timing.hop(1, true, 0.0, K.h + 8, 0.0, kb);

@@ -294,8 +294,10 @@ def test_sharded_tag_props(world):
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_writes_commit(world):
     """Write path with sharded ownership: each rank takes the write batches of its
-    own parts (StorageClient routes an AddEdges part to its leader); commit is collective and
-    rebuilds the vertex map / CSRs / tag slices on every rank, new vertices included."""
+    own parts (StorageClient routes an AddEdges part to its leader); commit is collective.  A batch
+    with new vertices rebuilds the vertex map / CSRs / tag slices on every rank; batches of edges
+    and tag rows of known vertices merge on every rank (merge_commits), also when only one rank
+    has writes of its own."""
     import random
 
     import test_gpu_tags as T
@@ -303,7 +305,11 @@ def test_sharded_writes_commit(world):
     base, vids = T.random_space_kv(8)
     rng = random.Random(2)
     new_vids = [rng.randrange(-2**62, 2**62) for _ in range(25)]
-    batch = W.write_batch(rng, vids, new_vids, W.BASE_VER - 10)
+    ends = set()
+    batch = W.write_batch(rng, vids, new_vids, W.BASE_VER - 10, ends=ends)
+    # vertices with an edge after batch 1 (a new vid with only a tag row has no gidx: an edge to
+    # it later is a new vertex again)
+    known = vids + [v for v in new_vids if v in ends]
     g = Group(world, parts=T.PARTS)
     try:
         def load(r, s):
@@ -317,7 +323,7 @@ def test_sharded_writes_commit(world):
 
         # round 1: every rank writes its parts; round 2: only rank 0's parts get writes, the
         # other ranks still join the collective commit
-        batch2 = W.write_batch(rng, vids + new_vids, [], W.BASE_VER - 20)
+        batch2 = W.write_batch(rng, known, [], W.BASE_VER - 20)
         batch2 = {p: kv for p, kv in batch2.items() if p % world == 0}
 
         def write(b):
@@ -327,17 +333,38 @@ def test_sharded_writes_commit(world):
                         s.write_part(p, kv)
                 s.commit()
             return run
+        # round 3: edges only, on every rank
+        batch3 = W.write_batch(rng, known, [], W.BASE_VER - 30, tags=False)
+        starts = vids[::19] + new_vids[:4]
+
+        def check(history):
+            st = W.fresh_oracle(history)
+            for steps, where, ys, distinct in W.QUERIES:
+                res = g.go(starts, steps, T.ET, where=where, yields=ys, distinct=distinct)
+                ref = st.go(starts, steps, T.ET, where=X.encode(where), yields=[y.encode() for y in ys],
+                            distinct=distinct)
+                assert ref.code == 0, ref.error
+                assert union_rows(res) == ms(ref.rows())
+            # FIND SHORTEST PATH reads the replicated CSRs, rebuilt after each commit
+            src = np.array(starts[:8], dtype=np.int64)
+            dst = np.array(starts[-8:], dtype=np.int64)
+            got = Counter()
+            for pr in g.each(lambda r, s: s.shortest_path(src, dst, T.ET, 6)):
+                got.update(pr.rows())
+            want = Counter()
+            for row in st.shortest_path(src, dst, T.ET, 6).rows():
+                row = [x for x in row if x is not None]
+                want[(row[0], row[1], row[2], tuple(row[3:]))] += 1
+            assert got == want
+
         g.each(load)
         g.each(write(batch))
         g.each(write(batch2))
-        st = W.fresh_oracle([base, batch, batch2])
-        starts = vids[::19] + new_vids[:4]
-        for steps, where, ys, distinct in W.QUERIES:
-            res = g.go(starts, steps, T.ET, where=where, yields=ys, distinct=distinct)
-            ref = st.go(starts, steps, T.ET, where=X.encode(where), yields=[y.encode() for y in ys],
-                        distinct=distinct)
-            assert ref.code == 0, ref.error
-            assert union_rows(res) == ms(ref.rows())
+        check([base, batch, batch2])
+        g.each(write(batch3))
+        check([base, batch, batch2, batch3])
+        merges = g.each(lambda r, s: s.info(T.ET)["merge_commits"])
+        assert merges == [2] * world  # batch 1 has new vertices: the full rebuild
     finally:
         g.close()
 

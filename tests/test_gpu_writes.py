@@ -30,20 +30,23 @@ def ms(rows):
     return Counter(tuple(r) for r in rows)
 
 
-def write_batch(rng, vids, new_vids, ver):
+def write_batch(rng, vids, new_vids, ver, tags=True, ends=None):
     """One AddEdges + AddVertices round: new edges (also to brand-new vertices), newer versions
-    of existing edges, identical-key rewrites, new / updated tag rows."""
+    of existing edges, identical-key rewrites, new / updated tag rows (tags=False: edges only).
+    ends: a set collecting the edges' endpoints (the vertices the snapshot numbers)."""
     part = lambda v: O.part_of(v, PARTS)  # noqa: E731
     batch = {p: [] for p in range(1, PARTS + 1)}
     every = vids + new_vids
     for _ in range(600):
         s, t = rng.choice(every), rng.choice(every)
+        if ends is not None:
+            ends.update((s, t))
         kind = rng.random()
         v = BASE_VER if kind < 0.2 else ver  # 20%: identical key of a base edge -> overwrite
         w = rng.randrange(1000, 2000)
         batch[part(s)].append((O.edge_key(part(s), s, ET, 0, t, v), O.encode_row([w])))
         batch[part(t)].append((O.edge_key(part(t), t, -ET, 0, s, v), b""))
-    for v in new_vids + rng.sample(vids, 40):
+    for v in (new_vids + rng.sample(vids, 40)) if tags else []:
         p = part(v)
         batch[p].append((O.vertex_key(p, v, PERSON, ver), O.encode_row([f"w{abs(v) % 13}", rng.randrange(100), 1.5])))
     return batch
