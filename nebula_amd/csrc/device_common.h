@@ -44,6 +44,51 @@ __device__ inline int32_t ht_lookup(const int64_t* __restrict__ keys, const int3
   }
 }
 
+// The LDS hub copy of a bottom-up kernel: words [0, cw) of the frontier bitmap into s_fb, plus
+// a zero word at [cw] when `zero_word`.  Every thread issues all its 16-byte loads before its
+// LDS stores, so a block waits one global latency, not one per blockDim words (the element loop
+// compiled to load / vmcnt(0) / ds_write per iteration: 16 dependent L2 round trips for a 64 KiB
+// hub at 1024 threads).  Ends with the block barrier.
+__device__ inline void hub_fill(uint32_t* s_fb, const uint32_t* __restrict__ fbits, int cw, bool zero_word) {
+  constexpr int kB = 4;  // 16-byte loads in flight per thread per round
+  const int nt = int(blockDim.x), tid = int(threadIdx.x);
+  int done = 0;
+  if (((reinterpret_cast<uintptr_t>(fbits) | reinterpret_cast<uintptr_t>(s_fb)) & 15u) == 0u) {
+    const int nv = cw >> 2;
+    const uint4* src = reinterpret_cast<const uint4*>(fbits);
+    uint4* dst = reinterpret_cast<uint4*>(s_fb);
+    for (int base = 0; base < nv; base += kB * nt) {
+      uint4 v[kB];
+#pragma unroll
+      for (int k = 0; k < kB; k++) {
+        const int i = base + k * nt + tid;
+        v[k] = i < nv ? src[i] : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int k = 0; k < kB; k++) {
+        const int i = base + k * nt + tid;
+        if (i < nv) dst[i] = v[k];
+      }
+    }
+    done = nv << 2;
+  }
+  for (int base = done; base < cw; base += kB * nt) {
+    uint32_t v[kB];
+#pragma unroll
+    for (int k = 0; k < kB; k++) {
+      const int i = base + k * nt + tid;
+      v[k] = i < cw ? fbits[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kB; k++) {
+      const int i = base + k * nt + tid;
+      if (i < cw) s_fb[i] = v[k];
+    }
+  }
+  if (zero_word && tid == 0) s_fb[cw] = 0u;
+  __syncthreads();
+}
+
 // wave-aggregated append: returns this lane's slot in `*counter` space (lanes with !pred get -1)
 __device__ inline int64_t wave_append(unsigned long long* counter, bool pred) {
   uint64_t mask = __ballot(pred);

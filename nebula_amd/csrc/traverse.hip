@@ -879,10 +879,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
   if (gate && *gate == 0ull) return;  // a speculative hop that the direction choice did not take
   __shared__ unsigned long long lds[kSlots * 16];
   extern __shared__ uint32_t s_fb[];  // [0, cw): the bitmap's hub words; [cw]: a zero word
-  if (HUB) {
-    for (int i = threadIdx.x; i <= cw; i += blockDim.x) s_fb[i] = i < cw ? fbits[i] : 0u;
-    __syncthreads();
-  }
+  if (HUB) hub_fill(s_fb, fbits, cw, true);
   const QArgs q = q_sgpr(q_arg);
   constexpr bool FINAL = PK == PK_FAST;
   constexpr int NS = FINAL ? 4 : 2;  // slots probed per row in the first round
@@ -1128,8 +1125,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
   // block's partials scratch
   extern __shared__ uint32_t s_fb[];
   unsigned long long* lds = reinterpret_cast<unsigned long long*>(s_fb + ((cw + 2) & ~1));
-  for (int i = threadIdx.x; i <= cw; i += blockDim.x) s_fb[i] = i < cw ? fbits[i] : 0u;
-  __syncthreads();
+  hub_fill(s_fb, fbits, cw, true);
   const uint32_t clo = __builtin_amdgcn_readfirstlane(fa_arg.clo), cr = __builtin_amdgcn_readfirstlane(fa_arg.cr);
   const uint32_t plo = __builtin_amdgcn_readfirstlane(fa_arg.plo), pr = __builtin_amdgcn_readfirstlane(fa_arg.pr);
   const bool pinv = __builtin_amdgcn_readfirstlane(fa_arg.pinv) != 0;
@@ -1265,10 +1261,7 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
   __shared__ unsigned long long s_found[16][64];
   extern __shared__ uint32_t s_fb[];
   const unsigned long long t_in = wall_clock64();
-  if (HUB) {
-    for (int i = threadIdx.x; i < cw; i += blockDim.x) s_fb[i] = fbits[i];
-    __syncthreads();
-  }
+  if (HUB) hub_fill(s_fb, fbits, cw, false);
   const unsigned long long t_hub = wall_clock64();
   uint32_t d_rows = 0, d_batches = 0, d_steps = 0, d_scan = 0;
   unsigned long long t_scan = 0;
