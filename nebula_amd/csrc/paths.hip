@@ -81,7 +81,25 @@ struct SpState {  // per-pair arrays, B entries each
   unsigned long long* deg;  // [2][B] frontier sum of (degree + 1)
   int32_t B;
   int32_t vmajor;           // distance bytes vertex-major [v][pair] (else pair-major [pair][v])
+  // level filter (null: off): bit v of lvbits[(side * kLv + l) * lvw] is set when some pair of
+  // the batch claimed vertex v at depth l on that side (1 <= l < kLv).  A superset of every
+  // pair's level-l set, held in L2 (n/8 bytes a level): a test that needs "dist[side][p][v] ==
+  // l" first reads the bit, and only a set bit reads the pair's distance byte (a random line in
+  // the 2 * B * n byte arrays)
+  uint32_t* lvbits;
+  int64_t lvw;
 };
+constexpr int kLv = 8;
+
+__device__ inline void lv_mark(const SpState& st, uint32_t side, uint32_t l, uint32_t v) {
+  if (st.lvbits && l >= 1 && l < uint32_t(kLv))
+    atomicOr(st.lvbits + (int64_t(side) * kLv + l) * st.lvw + (v >> 5), 1u << (v & 31u));
+}
+// false only when no pair holds v at depth l on the side
+__device__ inline bool lv_maybe(const SpState& st, uint32_t side, int32_t l, uint32_t v) {
+  if (!st.lvbits || l < 1 || l >= kLv) return true;
+  return (st.lvbits[(int64_t(side) * kLv + l) * st.lvw + (v >> 5)] >> (v & 31u)) & 1u;
+}
 
 // byte index of (pair p, vertex v) in a distance array.  Vertex-major keeps the bytes of all
 // pairs of one vertex in one cache line run, so hub neighbourhoods expanded by many pairs share
@@ -408,12 +426,22 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
   __shared__ uint64_t s_tup[kTileE];
   __shared__ int64_t s_hdr[2];
   __shared__ int32_t s_scan[kT / 64];
+  __shared__ uint32_t s_n[3];           // tile appends staged: side-0 claims, side-1 claims, meets
+  __shared__ unsigned long long s_base[4];
+  // Appends are staged per tile in LDS (claims in s_rs's words: side 0 from the front, side 1
+  // from the back; meets in s_tup's) and reserved with one global atomic per list and tile: the
+  // lists' returning counter atomics (one per wave, slot round and list) serialise at ~90 per us
+  // on one address, which held a 748 K-claim BFS level at ~0.3 ms and the 67 K-claim sweep
+  // behind a 72 M-entry scan.
+  uint64_t* const stage = reinterpret_cast<uint64_t*>(s_rs);
+  uint64_t* const mstage = s_tup;
   const int64_t nX = a.nX;
   const int64_t E = a.off[nX];
   const int64_t ntiles = (E + kTileE - 1) / kTileE;
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int64_t e0 = t * kTileE;
     const int64_t e1 = min(e0 + int64_t(kTileE), E);
+    if (threadIdx.x < 3) s_n[threadIdx.x] = 0u;
     if (threadIdx.x == 0 && a.tile_row) {
       int64_t i0, cnt;
       tile_entries(a.tile_row, a.off, nX, t, e1, E, i0, cnt);
@@ -452,15 +480,22 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
     }
     __syncthreads();
     if (!big) tile_owner_map<kTileE, kT>(s_off, cnt_k, s_scan);  // s_off[j] = owner of slot j
+    // The slots' memory reads in phases, each phase's loads of all kIt slots in flight before
+    // the first is used (slot by slot, a tile waited on kIt chains of col -> res -> filter ->
+    // distance byte: the latency-bound sweep ran at ~45 G entries/s): owners and column
+    // entries, then the pairs' depths, then the level filter bits, then the distance bytes
+    // the tests read; the claims (CAS loops) and appends follow.
+    uint64_t tus[kIt];
+    int64_t gi[kIt];  // column index of the slot's entry, -1: past the tile
+#pragma unroll
     for (int r = 0; r < kIt; r++) {
       const int j = threadIdx.x + r * kT;
       const int64_t e = e0 + j;
       const bool valid = e < e1;
-      int k = 0;
       uint64_t tu = 0;
       int64_t rsk = 0;
       if (valid && !big) {
-        k = s_off[j];
+        const int k = s_off[j];
         tu = s_tup[k];
         rsk = s_rs[k];
       } else if (valid) {
@@ -472,33 +507,65 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
         tu = a.X[lo];
         rsk = a.g[t_side(tu)].row_ptr[t_row(tu)] - a.off[lo];
       }
+      tus[r] = tu;
+      gi[r] = valid ? rsk + e : -1;
+    }
+    __syncthreads();  // s_tup / s_rs are staging buffers from here on
+    uint32_t ws[kIt];
+#pragma unroll
+    for (int r = 0; r < kIt; r++)
+      ws[r] = gi[r] >= 0 ? uint32_t(int64_t(a.g[t_side(tus[r])].col[gi[r]]) - a.lo) : 0u;
+    // the depth a sweep test needs: pull, the in-neighbour's forward depth; push, the
+    // out-neighbour's backward depth (both L - l - 1)
+    int32_t need[kIt];
+#pragma unroll
+    for (int r = 0; r < kIt; r++)
+      need[r] = a.sweep && gi[r] >= 0 ? st.res[t_pair(tus[r])] - int32_t(t_lvl(tus[r])) - 1 : -1;
+    bool lv[kIt];
+#pragma unroll
+    for (int r = 0; r < kIt; r++)
+      lv[r] = gi[r] >= 0 && (!a.sweep || (need[r] >= 0 && lv_maybe(st, t_side(tus[r]) ^ 1u, need[r], ws[r])));
+    // the byte each test reads: BFS, the slot's own side (0xFF: unseen); sweep, the other side
+    uint32_t bt[kIt];
+#pragma unroll
+    for (int r = 0; r < kIt; r++) {
+      const uint32_t side = t_side(tus[r]);
+      const uint8_t* d = a.sweep ? a.dist[side ^ 1u] : a.dist[side];
+      bt[r] = lv[r] ? uint32_t(d[didx(st, t_pair(tus[r]), ws[r], a.n)]) : 0x1FFu;
+    }
+#pragma unroll
+    for (int r = 0; r < kIt; r++) {
+      const uint64_t tu = tus[r];
+      const bool valid = gi[r] >= 0;
       const uint32_t side = t_side(tu), p = t_pair(tu), l = t_lvl(tu);
-      uint32_t w = 0;
+      const uint32_t w = ws[r];
       bool claimed = false;
       if (valid) {
-        w = uint32_t(int64_t(a.g[side].col[rsk + e]) - a.lo);
         const uint64_t idx = didx(st, p, w, a.n);
         if (!a.sweep) {
-          claimed = claim_byte(a.dist[side], idx, l + 1);
+          claimed = bt[r] == 0xFFu && claim_byte(a.dist[side], idx, l + 1);
+          if (claimed) lv_mark(st, side, l + 1, w);
         } else if (side == 1) {  // pull: in-neighbour w of a level-(k+1) vertex, forward depth k
-          const int32_t need = st.res[p] - int32_t(l) - 1;
-          if (need >= 0 && a.dist[0][idx] == uint8_t(need)) claimed = claim_byte(a.dist[1], idx, l + 1);
+          if (bt[r] == uint32_t(need[r])) {
+            claimed = claim_byte(a.dist[1], idx, l + 1);
+            if (claimed) lv_mark(st, 1, l + 1, w);
+          }
         } else {  // push: the tuple's own vertex u (forward depth l) if out-neighbour w is on a path
-          const int32_t need = st.res[p] - int32_t(l) - 1;
           const uint32_t u = t_row(tu);
-          if (a.dist[1][idx] == uint8_t(need)) claimed = claim_byte(a.dist[1], didx(st, p, u, a.n), uint32_t(need + 1));
+          if (bt[r] == uint32_t(need[r])) {
+            claimed = claim_byte(a.dist[1], didx(st, p, u, a.n), uint32_t(need[r] + 1));
+            if (claimed) lv_mark(st, 1, uint32_t(need[r] + 1), u);
+          }
         }
       }
       // a push claim records u with dist_B = L - l; every other claim the neighbour at depth l + 1
       const bool push_t = a.sweep && side == 0;
-      const uint64_t nt = push_t ? mk_tup(1, p, uint32_t(st.res[p]) - l, t_row(tu)) : mk_tup(side, p, l + 1, w);
-      put(bf.arena, bf.cap_arena, cnt, C_ARENA, claimed, nt);
-      if (a.sweep) {
-        put(bf.sweep_next, bf.cap_sweep, cnt, C_SWEEP, claimed, nt);
-        continue;
+      const uint64_t nt = push_t ? mk_tup(1, p, uint32_t(need[r] + 1), t_row(tu)) : mk_tup(side, p, l + 1, w);
+      if (claimed) {  // arena + (sweep list | the side's live list); a sweep stages at the front
+        if (a.sweep || side == 0) stage[atomicAdd(&s_n[0], 1u)] = nt;
+        else stage[kTileE - 1 - int(atomicAdd(&s_n[1], 1u))] = nt;
       }
-      put(bf.live_next[0], bf.cap_live[0], cnt, C_LIVE0, claimed && side == 0, nt);
-      put(bf.live_next[1], bf.cap_live[1], cnt, C_LIVE1, claimed && side == 1, nt);
+      if (a.sweep) continue;
       const unsigned long long dv = claimed ? (unsigned long long)sp_deg(a.g[side], w) + 1 : 0ull;
       wave_add_keyed(st.deg, side * uint32_t(st.B) + p, dv, claimed);
       bool meet = false;
@@ -511,8 +578,29 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
           st.met[p] = 1;
         }
       }
-      put(bf.meet, bf.cap_meet, cnt, C_MEET, meet, mk_tup(1, p, dt, w));
+      if (meet) mstage[atomicAdd(&s_n[2], 1u)] = mk_tup(1, p, dt, w);
     }
+    __syncthreads();
+    const uint32_t n0 = s_n[0], n1 = s_n[1], nm = s_n[2];
+    if (threadIdx.x == 0) {
+      s_base[0] = n0 + n1 ? atomicAdd(cnt + C_ARENA, (unsigned long long)(n0 + n1)) : 0ull;
+      s_base[1] = n0 ? atomicAdd(cnt + (a.sweep ? C_SWEEP : C_LIVE0), (unsigned long long)n0) : 0ull;
+      s_base[2] = n1 ? atomicAdd(cnt + C_LIVE1, (unsigned long long)n1) : 0ull;
+      s_base[3] = nm ? atomicAdd(cnt + C_MEET, (unsigned long long)nm) : 0ull;
+    }
+    __syncthreads();
+    auto store = [&](uint64_t* list, int64_t cap, unsigned long long at, uint64_t v) {
+      if (int64_t(at) < cap) list[at] = v;
+      else atomicOr(cnt + C_OVF, 1ull);
+    };
+    for (uint32_t q = threadIdx.x; q < n0 + n1; q += kT) {
+      const bool front = q < n0;
+      const uint64_t v = front ? stage[q] : stage[kTileE - 1 - int(q - n0)];
+      store(bf.arena, bf.cap_arena, s_base[0] + q, v);
+      if (front) store(a.sweep ? bf.sweep_next : bf.live_next[0], a.sweep ? bf.cap_sweep : bf.cap_live[0], s_base[1] + q, v);
+      else store(bf.live_next[1], bf.cap_live[1], s_base[2] + (q - n0), v);
+    }
+    for (uint32_t q = threadIdx.x; q < nm; q += kT) store(bf.meet, bf.cap_meet, s_base[3] + q, mstage[q]);
     __syncthreads();
   }
 }
@@ -526,6 +614,7 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
 // hubs included).  A failed probe leaves everything as it was: the expansion then finds no meet
 // either (a meet at f + b + 1 is exactly such an edge), so detection stays complete.
 constexpr int kProbeCh = 1024;  // adjacency entries per probe chunk (one wave each)
+constexpr int kProbeU = 4;      // entries per lane and step
 
 // ch[i] = number of probe chunks of X[i]; ch[nX] = 0
 __global__ void k_sp_chunks(const int64_t* Xdeg, int64_t nX, int64_t* ch) {
@@ -563,16 +652,29 @@ __global__ __launch_bounds__(256) void k_sp_probe(const uint64_t* __restrict__ X
     const uint32_t need = uint32_t(st.lvl[other * uint32_t(st.B) + p]);
     uint8_t* od = other ? d1 : d0;
     const uint64_t ci = didx(st, p, row, n);
-    for (int64_t x = x0; x < x1; x += 64) {
+    // kProbeU entries per lane a step: their column loads, then their filter bits, then their
+    // distance bytes, each group in flight together (one entry per lane a step waited on three
+    // dependent loads per 64 entries)
+    for (int64_t x = x0; x < x1; x += 64 * kProbeU) {
       if (*reinterpret_cast<volatile const uint8_t*>(od + ci) != 0xFF) break;
-      const int64_t ex = x + lane;
+      uint32_t w[kProbeU];
+#pragma unroll
+      for (int u = 0; u < kProbeU; u++) {
+        const int64_t ex = x + u * 64 + lane;
+        w[u] = ex < x1 ? uint32_t(int64_t(col[ex]) - lo) : 0xFFFFFFFFu;
+      }
+      bool f[kProbeU];
+#pragma unroll
+      for (int u = 0; u < kProbeU; u++) f[u] = w[u] != 0xFFFFFFFFu && lv_maybe(st, other, int32_t(need), w[u]);
       bool hit = false;
-      if (ex < x1) {
-        examined++;
-        hit = od[didx(st, p, uint32_t(int64_t(col[ex]) - lo), n)] == uint8_t(need);
+#pragma unroll
+      for (int u = 0; u < kProbeU; u++) {
+        examined += w[u] != 0xFFFFFFFFu ? 1 : 0;
+        hit = (f[u] && od[didx(st, p, w[u], n)] == uint8_t(need)) || hit;
       }
       if (__ballot(hit)) {
         if (lane == 0 && claim_byte(od, ci, need + 1)) {
+          lv_mark(st, other, need + 1, row);
           st.met[p] = 1;
           slot[c] = mk_tup(other, p, need + 1, row);
         }
@@ -771,25 +873,34 @@ __global__ __launch_bounds__(kT) void k_sp_walk_scan(SpState st, int32_t i, cons
     }
     __syncthreads();
     tile_owner_map<kTileE, kT>(s_off, cnt_k, s_scan);
+    // the slots' reads in phases, each phase's loads of all kIt slots in flight (as k_sp_expand):
+    // column entries and depths, backward level filter bits, distance bytes, then the vids of hits
+    uint32_t ps[kIt], ws[kIt];
+    int32_t need[kIt];
+#pragma unroll
     for (int r = 0; r < kIt; r++) {
       const int j = threadIdx.x + r * kT;
       const int64_t e = e0 + j;
-      const bool valid = e < e1;
-      uint32_t p = 0;
-      long long cand = LLONG_MAX;
-      bool hit = false;
-      if (valid) {
+      ps[r] = 0;
+      ws[r] = 0xFFFFFFFFu;
+      need[r] = -1;
+      if (e < e1) {
         const int k = s_off[j];
-        p = uint32_t(s_pair[k]);
-        const uint32_t w = uint32_t(int64_t(gout.col[s_rs[k] + e]) - lo);
-        const uint8_t need = uint8_t(st.res[p] - i - 1);
-        if (dist_b[didx(st, p, w, n)] == need) {
-          hit = true;
-          cand = vid_of[lo + w];
-        }
+        ps[r] = uint32_t(s_pair[k]);
+        ws[r] = uint32_t(int64_t(gout.col[s_rs[k] + e]) - lo);
+        need[r] = st.res[ps[r]] - i - 1;
       }
-      wave_min_keyed(best, p, cand, hit);
     }
+    bool hit[kIt];
+#pragma unroll
+    for (int r = 0; r < kIt; r++) hit[r] = ws[r] != 0xFFFFFFFFu && lv_maybe(st, 1, need[r], ws[r]);
+#pragma unroll
+    for (int r = 0; r < kIt; r++) hit[r] = hit[r] && dist_b[didx(st, ps[r], ws[r], n)] == uint8_t(need[r]);
+    long long cand[kIt];
+#pragma unroll
+    for (int r = 0; r < kIt; r++) cand[r] = hit[r] ? vid_of[lo + ws[r]] : LLONG_MAX;
+#pragma unroll
+    for (int r = 0; r < kIt; r++) wave_min_keyed(best, ps[r], cand[r], hit[r]);
     __syncthreads();
   }
 }
@@ -1004,6 +1115,17 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     st.pside = st.side + nb;
     st.met = st.pside + nb;
     st.vmajor = int32_t(c.opt("sp_vmajor", 0));
+    if (c.opt("sp_lvbits", 1) != 0) {  // level filter: 2 * kLv bitmaps of n bits, cleared per batch
+      const int64_t lvw = (n + 31) / 32;
+      const size_t lvb = size_t(2 * kLv) * size_t(lvw) * 4;
+      if (W.lvbits.bytes < lvb) {
+        PoolScope none(nullptr);
+        W.lvbits.alloc(lvb);
+      }
+      NBG_HIP(hipMemsetAsync(W.lvbits.p, 0, lvb, c.stream));
+      st.lvbits = W.lvbits.as<uint32_t>();
+      st.lvw = lvw;
+    }
     NBG_HIP(hipMemcpyAsync(dsv, src + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
     NBG_HIP(hipMemcpyAsync(dtv, dst + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
     lookup_gidx(c, dsv, dgs, nb);
