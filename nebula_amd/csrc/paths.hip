@@ -605,6 +605,117 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
   }
 }
 
+// ---- chunked scans (meet probe, sweep) --------------------------------------------------------
+// chunk_x[c] = the X entry holding chunk c (choff = exclusive scan of the entries' chunk counts):
+// one coalesced pass instead of a binary search of choff (~15 dependent loads) per chunk
+__global__ void k_chunk_x(const int64_t* __restrict__ choff, int64_t nX, int32_t* __restrict__ chunk_x) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < nX; i += int64_t(gridDim.x) * blockDim.x)
+    for (int64_t c = choff[i]; c < choff[i + 1]; c++) chunk_x[c] = int32_t(i);
+}
+
+// One sweep step over the X tuples' adjacency, one wave per chunk of kSwCh entries (the meet
+// vertices' in-rows average ~10 K entries: the edge-balanced tile scheme paid a tile header,
+// an LDS owner map and four barriers per 2048 entries).  Pull (side 1, in-row of w at dt = l):
+// an in-neighbour u with ds(u) = L - l - 1 gets dt = l + 1.  Push (side 0, out-row of u at
+// ds = l): u gets dt = L - l once an out-neighbour has dt = L - l - 1 (the scan stops there).
+// kProbeU entries per lane a step, their column loads, filter bits and distance bytes each in
+// flight together.  Claims are staged per wave in LDS and appended to the arena and the next
+// sweep list with one counter atomic per list and flush.
+constexpr int kProbeU = 4;  // entries per lane and step of the chunked scans
+constexpr int kSwCh = 1024;
+constexpr int kSwStage = 256;
+__global__ __launch_bounds__(256) void k_sp_sweep(const uint64_t* __restrict__ X, const int64_t* __restrict__ choff,
+                                                  const int32_t* __restrict__ chunk_x, int64_t nX, SpCsr gout,
+                                                  SpCsr gin, uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo,
+                                                  SpState st, SpBufs bf, unsigned long long* cnt) {
+  __shared__ uint64_t s_stage[4][kSwStage];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t* stg = s_stage[wid];
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  uint32_t ns = 0;  // wave-uniform: claims staged
+  const int64_t total = choff[nX];
+  auto flush = [&]() {
+    if (ns == 0) return;
+    __builtin_amdgcn_wave_barrier();
+    unsigned long long ba = 0, bs = 0;
+    if (lane == 0) {
+      ba = atomicAdd(cnt + C_ARENA, (unsigned long long)ns);
+      bs = atomicAdd(cnt + C_SWEEP, (unsigned long long)ns);
+    }
+    ba = __shfl(ba, 0);
+    bs = __shfl(bs, 0);
+    for (uint32_t q = uint32_t(lane); q < ns; q += 64) {
+      const uint64_t v = stg[q];
+      if (int64_t(ba + q) < bf.cap_arena) bf.arena[ba + q] = v;
+      else atomicOr(cnt + C_OVF, 1ull);
+      if (int64_t(bs + q) < bf.cap_sweep) bf.sweep_next[bs + q] = v;
+      else atomicOr(cnt + C_OVF, 1ull);
+    }
+    __builtin_amdgcn_wave_barrier();
+    ns = 0;
+  };
+  auto stage = [&](bool claimed, uint64_t v) {  // wave-uniform call
+    const uint64_t m = __ballot(claimed);
+    if (m == 0) return;
+    if (ns + uint32_t(__popcll(m)) > uint32_t(kSwStage)) flush();
+    if (claimed) stg[ns + uint32_t(__popcll(m & ((1ull << lane) - 1ull)))] = v;
+    ns += uint32_t(__popcll(m));
+  };
+  for (int64_t c = wave; c < total; c += nwaves) {
+    const int32_t a = chunk_x[c];
+    const uint64_t t = X[a];
+    const uint32_t side = t_side(t), p = t_pair(t), l = t_lvl(t), row = t_row(t);
+    const int64_t* rp = side ? gin.row_ptr : gout.row_ptr;
+    const int32_t* col = side ? gin.col : gout.col;
+    const int64_t x0 = rp[row] + (c - choff[a]) * kSwCh;
+    const int64_t x1 = min(x0 + int64_t(kSwCh), rp[row + 1]);
+    const int32_t need = st.res[p] - int32_t(l) - 1;  // the other side's depth a neighbour needs
+    const uint64_t ui = didx(st, p, row, n);
+    for (int64_t x = x0; x < x1; x += 64 * kProbeU) {
+      if (side == 0 && *reinterpret_cast<volatile const uint8_t*>(d1 + ui) != 0xFF) break;  // u claimed
+      uint32_t w[kProbeU];
+#pragma unroll
+      for (int u = 0; u < kProbeU; u++) {
+        const int64_t ex = x + u * 64 + lane;
+        w[u] = ex < x1 ? uint32_t(int64_t(col[ex]) - lo) : 0xFFFFFFFFu;
+      }
+      bool f[kProbeU];
+#pragma unroll
+      for (int u = 0; u < kProbeU; u++)
+        f[u] = w[u] != 0xFFFFFFFFu && need >= 0 && lv_maybe(st, side ^ 1u, need, w[u]);
+      uint32_t b[kProbeU];
+#pragma unroll
+      for (int u = 0; u < kProbeU; u++) b[u] = f[u] ? uint32_t((side ? d0 : d1)[didx(st, p, w[u], n)]) : 0x1FFu;
+      if (side == 1) {
+#pragma unroll
+        for (int u = 0; u < kProbeU; u++) {
+          bool claimed = false;
+          if (b[u] == uint32_t(need)) {
+            claimed = claim_byte(d1, didx(st, p, w[u], n), l + 1);
+            if (claimed) lv_mark(st, 1, l + 1, w[u]);
+          }
+          stage(claimed, mk_tup(1, p, l + 1, w[u]));
+        }
+      } else {
+        bool hit = false;
+#pragma unroll
+        for (int u = 0; u < kProbeU; u++) hit = hit || b[u] == uint32_t(need);
+        if (__ballot(hit)) {
+          bool claimed = false;
+          if (lane == 0) {
+            claimed = claim_byte(d1, ui, uint32_t(need + 1));
+            if (claimed) lv_mark(st, 1, uint32_t(need + 1), row);
+          }
+          stage(claimed, mk_tup(1, p, uint32_t(need + 1), row));
+          break;
+        }
+      }
+    }
+  }
+  flush();
+}
+
 // ---- meet probe -----------------------------------------------------------------------------
 // Before a pair expands its cheaper side s (frontier at depth l, the other side at depth l_o),
 // probe whether the two frontiers are already one edge apart: a tuple's vertex r is a meet vertex
@@ -614,8 +725,12 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
 // hubs included).  A failed probe leaves everything as it was: the expansion then finds no meet
 // either (a meet at f + b + 1 is exactly such an edge), so detection stays complete.
 constexpr int kProbeCh = 1024;  // adjacency entries per probe chunk (one wave each)
-constexpr int kProbeU = 4;      // entries per lane and step
 
+// ch[i] = number of chunks of `size` entries of X[i]; ch[nX] = 0
+__global__ void k_sp_chunks_n(const int64_t* Xdeg, int64_t nX, int64_t* ch, int64_t size) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= nX; i += int64_t(gridDim.x) * blockDim.x)
+    ch[i] = i == nX ? 0 : (Xdeg[i] + size - 1) / size;
+}
 // ch[i] = number of probe chunks of X[i]; ch[nX] = 0
 __global__ void k_sp_chunks(const int64_t* Xdeg, int64_t nX, int64_t* ch) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= nX; i += int64_t(gridDim.x) * blockDim.x)
@@ -628,7 +743,8 @@ __global__ void k_sp_chunks(const int64_t* Xdeg, int64_t nX, int64_t* ch) {
 // side) and records that claim in slot[c] (an arena tuple); k_sp_gather_meets turns the slots into
 // the meet list without a global atomic per meet.
 __global__ __launch_bounds__(256) void k_sp_probe(const uint64_t* __restrict__ X, int64_t nX,
-                                                  const int64_t* __restrict__ choff, SpCsr g0, SpCsr g1, uint8_t* d0,
+                                                  const int64_t* __restrict__ choff,
+                                                  const int32_t* __restrict__ chunk_x, SpCsr g0, SpCsr g1, uint8_t* d0,
                                                   uint8_t* d1, int64_t n, int64_t lo, SpState st, uint64_t* slot,
                                                   unsigned long long* cnt) {
   const int lane = threadIdx.x & 63;
@@ -637,11 +753,7 @@ __global__ __launch_bounds__(256) void k_sp_probe(const uint64_t* __restrict__ X
   const int64_t total = choff[nX];
   unsigned long long examined = 0;
   for (int64_t c = wave; c < total; c += nwaves) {
-    int64_t a = 0, b = nX;  // last tuple with choff[a] <= c
-    while (b - a > 1) {
-      const int64_t mid = (a + b) >> 1;
-      if (choff[mid] <= c) a = mid; else b = mid;
-    }
+    const int64_t a = chunk_x[c];  // the tuple holding chunk c
     const uint64_t t = X[a];
     const uint32_t side = t_side(t), p = t_pair(t), row = t_row(t);
     const int64_t* rp = side ? g1.row_ptr : g0.row_ptr;
@@ -1300,8 +1412,11 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         hipEventRecord(c.ev[4], c.stream);
         const int pgrid =
             int(std::max<int64_t>(1, std::min<int64_t>((max_chunks + 3) / 4, c.opt("sp_probe_grid", 4096))));
-        k_sp_probe<<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), gout, gin, d0, d1, n, lo,
-                                                st, slot.as<uint64_t>(), cnt);
+        DevBuf chx;
+        chx.alloc(size_t(max_chunks) * 4);
+        k_chunk_x<<<grid_n(nX), 256, 0, c.stream>>>(choff.as<int64_t>(), nX, chx.as<int32_t>());
+        k_sp_probe<<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), chx.as<int32_t>(), gout,
+                                                gin, d0, d1, n, lo, st, slot.as<uint64_t>(), cnt);
         k_sp_gather_meets<<<grid_n(max_chunks), 256, 0, c.stream>>>(slot.as<uint64_t>(), max_chunks, st, bf, cnt);
         k_sp_probe_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, iter);
         k_sp_drop<<<grid_n(nX), 256, 0, c.stream>>>(W.X.as<uint64_t>(), W.Xdeg.as<int64_t>(), nX, st, cnt);
@@ -1429,8 +1544,31 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       reserve(c, W.sweep[nxt], W.cap_sweep[nxt], want, 0);
       if (!arena_lost) reserve(c, W.arena, W.cap_arena, n_arena + want, n_arena);
       refresh(&W.sweep[nxt], W.cap_sweep[nxt]);
-      launch_scan(nX);
-      launch_expand(nX, E, 1);
+      if (c.opt("sp_sweep_chunks", 1) != 0) {
+        // chunk counts -> their scan -> chunk table -> one wave per chunk
+        DevBuf ch, choff, chx;
+        ch.alloc(size_t(nX + 1) * 8);
+        choff.alloc(size_t(nX + 1) * 8);
+        k_sp_chunks_n<<<grid_n(nX + 1), 256, 0, c.stream>>>(W.Xdeg.as<int64_t>(), nX, ch.as<int64_t>(), kSwCh);
+        size_t tb = 0;
+        NBG_HIP(rocprim::exclusive_scan(nullptr, tb, ch.as<int64_t>(), choff.as<int64_t>(), int64_t(0),
+                                        size_t(nX + 1), rocprim::plus<int64_t>(), c.stream));
+        c.ws_tmp.ensure(tb);
+        NBG_HIP(rocprim::exclusive_scan(c.ws_tmp.p, tb, ch.as<int64_t>(), choff.as<int64_t>(), int64_t(0),
+                                        size_t(nX + 1), rocprim::plus<int64_t>(), c.stream));
+        const int64_t max_ch = nX + E / kSwCh + 1;
+        chx.alloc(size_t(max_ch) * 4);
+        hipEventRecord(c.ev[2], c.stream);
+        k_chunk_x<<<grid_n(nX), 256, 0, c.stream>>>(choff.as<int64_t>(), nX, chx.as<int32_t>());
+        const int sgrid = int(std::max<int64_t>(1, std::min<int64_t>((max_ch + 3) / 4, c.opt("sp_sweep_grid", 8192))));
+        k_sp_sweep<<<sgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), choff.as<int64_t>(), chx.as<int32_t>(),
+                                                 nX, gout, gin, d0, d1, n, lo, st, bf, cnt);
+        NBG_HIP(hipGetLastError());
+        hipEventRecord(c.ev[3], c.stream);
+      } else {
+        launch_scan(nX);
+        launch_expand(nX, E, 1);
+      }
       sync_counters();
       const double sms = expand_time();
       c.timing.expand_bytes += uint64_t(nX) * 32 + uint64_t(E) * 6 + hc[C_SWEEP] * 18;
