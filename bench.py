@@ -310,6 +310,24 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
             h.update(np.asarray(p, dtype="<i8").tobytes())
         parity["status"] = "digest ok" if h.hexdigest() == golden[key]["sha256"] else "mismatch"
     achieved = exp_bytes / (exp_ms / 1e3) / 1e9 if exp_ms > 0 else 0.0
+    # dominant launch kind of one query (its rocprof kernel, the engine's byte models:
+    # paths.hip timing.expand_bytes): expand / probe / sweep
+    kern = {"expand": "nbg::k_sp_expand", "probe": "nbg::k_sp_probe", "sweep": "nbg::k_sp_sweep"}
+    model = {"expand": lambda l: l["x"] * 32 + l["entries"] * 5 + l["claims"] * 26,
+             "probe": lambda l: l["x"] * 24 + l["entries"] * 5,
+             "sweep": lambda l: l["x"] * 32 + l["entries"] * 6 + l["claims"] * 18}
+    by_kind = {}
+    for l in launches:
+        k = by_kind.setdefault(l["kind"], {"ms": 0.0, "bytes": 0.0, "launches": 0})
+        k["ms"] += l["ms"]
+        k["bytes"] += model.get(l["kind"], lambda _: 0)(l)
+        k["launches"] += 1
+    dom = max(by_kind, key=lambda k: by_kind[k]["ms"]) if by_kind else "expand"
+    dk = by_kind.get(dom, {"ms": 0.0, "bytes": 0.0, "launches": 1})
+    dom_ach = dk["bytes"] / (dk["ms"] / 1e3) / 1e9 if dk["ms"] > 0 else 0.0
+    workload = (f"FIND SHORTEST PATH {args.pairs} pairs UPTO {args.max_steps} STEPS OVER follow; "
+                f"RMAT-{args.scale} ef{args.edge_factor}")
+    tr = pmc_traffic(workload, [kern.get(dom, "nbg::k_sp_expand")])
     out = {
         "metric": "FIND SHORTEST PATH pairs/s (batched bidirectional BFS) on RMAT-26",
         "value": args.pairs * args.steps / dt,
@@ -326,8 +344,7 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
         "config": {
             "parallelism": f"pairs sharded i % {world} over the ranks, replicated CSRs" if world > 1 else "1 GPU",
             "communicator": sp.comm_info() if world > 1 else None,
-            "workload": f"FIND SHORTEST PATH {args.pairs} pairs UPTO {args.max_steps} STEPS OVER follow; "
-                        f"RMAT-{args.scale} ef{args.edge_factor}",
+            "workload": workload,
             "vertices": info["num_vertices"],
             "edges_examined_per_query": edges // max(args.steps, 1),
             "gteps": edges / dt / 1e9,
@@ -339,8 +356,14 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
         },
         "parity": parity,
         "roofline": {
-            "bound": "hbm", "kernel": "k_sp_expand", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "bound": "hbm", "kernel": kern.get(dom, dom), "achieved": dom_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": dom_ach / HBM_PEAK_GBS,
+            # PMC HBM bytes of the dominant kernel per query (all its launches of one query)
+            "traffic": tr["bytes"] * dk["launches"] if tr else None,
+            "traffic_source": tr["source"] + " (FETCH_SIZE x2 + WRITE_SIZE per launch x launches per query)"
+            if tr else None,
+            "algorithmic_bytes_per_query": dk["bytes"], "kernel_ms_per_query": dk["ms"],
+            "all_scan_kernels": {"achieved": achieved, "frac": achieved / HBM_PEAK_GBS},
             "expand_ms_per_query": exp_ms / max(args.steps, 1), "device_ms_per_query": dev_ms / max(args.steps, 1),
         },
         "cpu_baseline": None,
