@@ -204,3 +204,25 @@ def test_sweep_direction_and_walk_variants(rmat, push, walk_wg, sweep_src):
         sp.set_option("sp_sweep_push", 1)
         sp.set_option("sp_walk_wg", 0)
         sp.set_option("sp_sweep_src", 0)
+
+
+@pytest.mark.parametrize("chunks,lvbits,push", [(1, 1, 1), (1, 1, 0), (0, 1, 1), (1, 0, 1), (0, 0, 0)])
+def test_sweep_kernels_and_level_filter(rmat, chunks, lvbits, push):
+    """the chunked sweep (k_sp_sweep, one wave per 1024 entries of a row) and the edge-balanced
+    tile sweep (k_sp_expand, sweep mode), with and without the per-side level bitmaps that filter
+    the sweep / probe / walk distance reads, in pull-only and push/pull mode: the oracle's paths"""
+    scale, sp, st = rmat
+    sp.set_option("sp_sweep_chunks", chunks)
+    sp.set_option("sp_lvbits", lvbits)
+    sp.set_option("sp_sweep_push", push)
+    try:
+        s, t = synth.pairs(scale, 16, 1, 300, pick_seed=29)
+        es, et_ = edge_case_pairs(scale)
+        src, dst = np.concatenate([s, es]), np.concatenate([t, et_])
+        for max_steps in (3, 8):
+            got = sp.shortest_path(src, dst, FOLLOW, max_steps).rows()
+            assert got == oracle_paths(st, src, dst, FOLLOW, max_steps)
+    finally:
+        sp.set_option("sp_sweep_chunks", 1)
+        sp.set_option("sp_lvbits", 1)
+        sp.set_option("sp_sweep_push", 1)
