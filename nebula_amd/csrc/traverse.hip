@@ -1439,7 +1439,7 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
 // exclusive offsets go to LDS, one returning atomic reserves the tile's output range, then each
 // wave expands two words per step with one lane per bit, so consecutive set bits write
 // consecutive output slots (coalesced stores, coalesced vid_of reads).
-template <int MODE>
+template <int MODE, int U = 4>
 __global__ __launch_bounds__(1024) void k_bits_compact(const uint32_t* __restrict__ bits, int64_t n, int64_t lo,
                                                        const int64_t* __restrict__ vid_of, void* out,
                                                        unsigned long long* n_out,
@@ -1471,7 +1471,6 @@ __global__ __launch_bounds__(1024) void k_bits_compact(const uint32_t* __restric
     if (total) {
       // U word pairs per step: the step's U vid_of loads are issued before any of its stores,
       // so each lane keeps U HBM requests in flight instead of one load -> store chain per pair
-      constexpr int U = 4;
       const unsigned long long base = s_base;
       const int half = lane >> 5, bit = lane & 31;
       const int per_wave = kTileWords / int(blockDim.x >> 6);
@@ -2385,6 +2384,17 @@ QArgs make_qargs(const EdgeSpace& es, int pk, int fcol, const FastArgs& fp) {
   return q;
 }
 
+// DISTINCT _dst output: the vids of a bitmap's set rows (option bits_u: word pairs per lane
+// and step, 8 or 4; r05 sweep: 8 takes the C3 final hop 266 -> 258 us)
+static void launch_bits_vids(Ctx& c, const uint32_t* bits, int64_t rows, int64_t lo, void* out,
+                             unsigned long long* n_out, const unsigned long long* gate) {
+  const int grid = grid_cap((rows + 31) / 32, 1024, 4096);
+  if (c.opt("bits_u", 8) == 8)
+    k_bits_compact<1, 8><<<grid, 1024, 0, c.stream>>>(bits, rows, lo, c.vid_of.as<int64_t>(), out, n_out, gate);
+  else
+    k_bits_compact<1, 4><<<grid, 1024, 0, c.stream>>>(bits, rows, lo, c.vid_of.as<int64_t>(), out, n_out, gate);
+}
+
 // k_bu_fin's word ranges from a query's bucket decisions (q_test: buckets below ulo answer
 // `below`, above uhi `above`, the rest are undecided).  The field above the gidx bits is the
 // bucket; every decision region is a contiguous field range, so each set is one word range.
@@ -2974,8 +2984,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         ik = launch_bu_lean(c, es, in, outb, nullptr, fpk0.kind, tfp, fpk0.kind == PK_FAST ? fpk0.col : -1, blk,
                             blk + 8);
         spec_vids.alloc(size_t(c.n_global + 64) * 8);
-        k_bits_compact<1><<<grid_cap((es.tr.n_rows + 31) / 32, 1024, 4096), 1024, 0, c.stream>>>(
-            outb, es.tr.n_rows, lo, c.vid_of.as<int64_t>(), spec_vids.p, blk + 9, blk + 8);
+        launch_bits_vids(c, outb, es.tr.n_rows, lo, spec_vids.p, blk + 9, blk + 8);
       }
       NBG_HIP(hipGetLastError());
       const size_t ib = timing_event(c);
@@ -3215,7 +3224,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         const uint64_t kb = bu_first_bytes(fin_h, es.tr.n_rows, false), hb = kb + bu_rest_bytes(fin_h, pw, c.bu_rest_rec);
         c.timing.expand_bytes += hb + uint64_t(es.tr.n_rows) / 8 + uint64_t(nrows) * 16;
         c.timing.hop(1, true, 0.0, fin_h, 0.0, kb);
-        c.timing.name_last_hop(fin_k0, fin_k1, "nbg::k_bits_compact<1>");
+        c.timing.name_last_hop(fin_k0, fin_k1, c.opt("bits_u", 8) == 8 ? "nbg::k_bits_compact<1, 8>" : "nbg::k_bits_compact<1, 4>");
       } else {
         vids.alloc(size_t(c.n_global + 64) * 8);
       }
@@ -3228,8 +3237,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         const uint32_t* fb = global_bits(c, bitsA);
         const size_t ia = timing_event(c);
         const size_t ik = launch_bu_lean(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8);
-        k_bits_compact<1><<<grid_cap((tr.n_rows + 31) / 32, 1024, 4096), 1024, 0, c.stream>>>(
-            bitsB, tr.n_rows, lo, c.vid_of.as<int64_t>(), vids.p, K.d);
+        launch_bits_vids(c, bitsB, tr.n_rows, lo, vids.p, K.d, nullptr);
         NBG_HIP(hipGetLastError());
         const size_t ib = timing_event(c);
         c.tpend.push_back(Ctx::PendingTime{ia, ib, c.timing.n_hops, 0});
@@ -3243,7 +3251,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         // + the DISTINCT _dst output (k_bits_compact<1>): next bits once, vid_of read + vid written
         c.timing.expand_bytes += hb + uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
         c.timing.hop(1, true, 0.0, K.h + 8, 0.0, kb);
-        c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name, "nbg::k_bits_compact<1>");
+        c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name, c.opt("bits_u", 8) == 8 ? "nbg::k_bits_compact<1, 8>" : "nbg::k_bits_compact<1, 4>");
       } else {
         ensure_off();
         a.F = F;
