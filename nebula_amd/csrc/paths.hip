@@ -81,24 +81,27 @@ struct SpState {  // per-pair arrays, B entries each
   unsigned long long* deg;  // [2][B] frontier sum of (degree + 1)
   int32_t B;
   int32_t vmajor;           // distance bytes vertex-major [v][pair] (else pair-major [pair][v])
-  // level filter (null: off): bit v of lvbits[(side * kLv + l) * lvw] is set when some pair of
-  // the batch claimed vertex v at depth l on that side (1 <= l < kLv).  A superset of every
-  // pair's level-l set, held in L2 (n/8 bytes a level): a test that needs "dist[side][p][v] ==
-  // l" first reads the bit, and only a set bit reads the pair's distance byte (a random line in
-  // the 2 * B * n byte arrays)
+  // level filter (null: off): bit (v & lvmask) of level (side, l)'s lvw words is set when some
+  // pair of the batch claimed vertex v at depth l on that side (1 <= l < kLv): a one-hash Bloom
+  // filter of every pair's level-l set, at most 2^23 bits (1 MiB) a level so the level a launch
+  // tests stays in an XCD's 4 MiB L2 (a full n-bit map at RMAT-26 is 4 MiB and its probes
+  // went to the fabric: the chunked sweep fetched ~40 B per entry).  A test that needs
+  // "dist[side][p][v] == l" first reads the bit; only a set bit reads the pair's distance byte
+  // (a random line in the 2 * B * n byte arrays)
   uint32_t* lvbits;
   int64_t lvw;
+  uint32_t lvmask;
 };
 constexpr int kLv = 8;
 
 __device__ inline void lv_mark(const SpState& st, uint32_t side, uint32_t l, uint32_t v) {
   if (st.lvbits && l >= 1 && l < uint32_t(kLv))
-    atomicOr(st.lvbits + (int64_t(side) * kLv + l) * st.lvw + (v >> 5), 1u << (v & 31u));
+    atomicOr(st.lvbits + (int64_t(side) * kLv + l) * st.lvw + ((v & st.lvmask) >> 5), 1u << (v & 31u));
 }
 // false only when no pair holds v at depth l on the side
 __device__ inline bool lv_maybe(const SpState& st, uint32_t side, int32_t l, uint32_t v) {
   if (!st.lvbits || l < 1 || l >= kLv) return true;
-  return (st.lvbits[(int64_t(side) * kLv + l) * st.lvw + (v >> 5)] >> (v & 31u)) & 1u;
+  return (st.lvbits[(int64_t(side) * kLv + l) * st.lvw + ((v & st.lvmask) >> 5)] >> (v & 31u)) & 1u;
 }
 
 // byte index of (pair p, vertex v) in a distance array.  Vertex-major keeps the bytes of all
@@ -1227,8 +1230,13 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     st.pside = st.side + nb;
     st.met = st.pside + nb;
     st.vmajor = int32_t(c.opt("sp_vmajor", 0));
-    if (c.opt("sp_lvbits", 1) != 0) {  // level filter: 2 * kLv bitmaps of n bits, cleared per batch
-      const int64_t lvw = (n + 31) / 32;
+    if (c.opt("sp_lvbits", 1) != 0) {  // level filter: 2 * kLv maps, cleared per batch
+      // bits per level: the power of two >= n, capped (option sp_lvbits_log2, default 23)
+      const int cap = int(std::min<int64_t>(std::max<int64_t>(c.opt("sp_lvbits_log2", 23), 5), 31));
+      int lg = 5;
+      while (lg < cap && (int64_t(1) << lg) < n) lg++;
+      const int64_t lvw = (int64_t(1) << lg) / 32;
+      st.lvmask = uint32_t((uint64_t(1) << lg) - 1);
       const size_t lvb = size_t(2 * kLv) * size_t(lvw) * 4;
       if (W.lvbits.bytes < lvb) {
         PoolScope none(nullptr);
