@@ -87,7 +87,7 @@ int32_t nbg_comm_info(nbg_ctx* ctx, int32_t* ranks, int32_t* transport);
  * nbg_hop_stat, nbg_snapshot_info, nbg_go_spec, nbg_rows) change layout between versions: an
  * integration compares nbg_abi_version() with the NBG_ABI_VERSION it was built against and
  * refuses to run on a mismatch (INTEGRATION.md "ABI versioning").                          */
-#define NBG_ABI_VERSION 3
+#define NBG_ABI_VERSION 4
 int32_t nbg_abi_version(void);
 /* sizeof of the caller-allocated structs as the library was built: 0 nbg_timing, 1
  * nbg_hop_stat, 2 nbg_snapshot_info, 3 nbg_go_spec, 4 nbg_rows, 5 nbg_prop_def; -1 otherwise */
@@ -250,8 +250,10 @@ typedef struct {
    * variable input rows, one per starts[i] (the FROM column).  A start vid's props come from its
    * LAST row (InterimResult::buildIndex, InterimResult.cpp:146-160).  Column types NBG_T_VID /
    * NBG_T_INT / NBG_T_DOUBLE (int64 / double arrays), NBG_T_BOOL (uint8) or NBG_T_STRING (bytes
-   * + n_starts+1 int64 offsets).  Only with steps == 1: a multi-step GO resolves them through a
-   * VertexBackTracker whose result depends on response order (GoExecutor.h:174-193).
+   * + n_starts+1 int64 offsets).  With steps > 1 the final step reads the input row of each
+   * dst's root start, as graphd's VertexBackTracker (GoExecutor.h:174-193) does; a dst reached
+   * from several starts takes the smallest root vid among its in-edge srcs (the reference's
+   * answer there depends on RPC response order; DESIGN.md divergence 6).
    * n_inputs = 0: no input table (zero-initialised specs stay valid).                        */
   size_t n_inputs;
   const char* const* input_names;
@@ -306,6 +308,10 @@ typedef struct {
   uint64_t comm_bytes;    /* bytes this rank sent to other ranks                            */
   int32_t n_hops;         /* entries of hops[] filled (nbg_go, nbg_shortest_path)            */
   nbg_hop_stat hops[NBG_MAX_HOP_STATS];
+  int32_t host_waits;     /* times the engine waited on the host for the device in the last
+                             call (counter fetches, stream synchronisations; waits inside the
+                             LocalComm / RCCL transport not included)                          */
+  int32_t spec_hops;      /* nbg_go hops that ran speculatively behind a device gate (k_gate)  */
 } nbg_timing;
 int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out);
 /* engine option key = value (tuning knobs); value INT64_MIN removes the key, so the

@@ -1,4 +1,5 @@
 // capi.cpp -- extern "C" entry points declared in include/nebula_amd.h.
+#include <unistd.h>
 #include <map>
 #include <mutex>
 #include <algorithm>
@@ -62,6 +63,10 @@ int ctx_count_on_device(int device) {
   auto it = g_dev_ctx.find(device);
   return it == g_dev_ctx.end() ? 0 : it->second;
 }
+size_t host_ram_bytes() {
+  const long pages = sysconf(_SC_PHYS_PAGES), psz = sysconf(_SC_PAGESIZE);
+  return pages > 0 && psz > 0 ? size_t(pages) * size_t(psz) : 0;
+}
 static void ctx_count_add(int device, int d) {
   std::lock_guard<std::mutex> lk(g_dev_mu);
   g_dev_ctx[device] += d;
@@ -110,6 +115,7 @@ void nbg_ctx_destroy(nbg_ctx* ctx) {
   nbg::ctx_count_add(ctx->c.device, -1);
   (void)hipStreamSynchronize(ctx->c.stream);
   nbg::comm_destroy(ctx->c);
+  ctx->c.host_pool->trim();  // results still held return their blocks to the (then ownerless) pool
   for (auto& e : ctx->c.ev) (void)hipEventDestroy(e);
   for (auto& e : ctx->c.tev) (void)hipEventDestroy(e);
   if (ctx->c.host_counters) (void)hipHostFree(ctx->c.host_counters);
@@ -360,6 +366,8 @@ int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out) {
     out->comm_bytes = c.timing.comm_bytes;
     out->n_hops = c.timing.n_hops;
     memcpy(out->hops, c.timing.hops, sizeof(out->hops));
+    out->host_waits = c.timing.host_waits;
+    out->spec_hops = c.timing.spec_hops;
     return NBG_OK;
   });
 }

@@ -85,6 +85,16 @@ struct RcclComm : CommImpl {
 };
 
 // ------------------------------------------------------------------------------------------
+// In-process rank group, stream-ordered like RCCL: no collective waits for the GPU on the host.
+// Each collective is three steps:
+//   1. every rank records `ready` on its stream (its send buffer is complete) and publishes the
+//      buffer pointers; host barrier A (only the enqueue order is synchronised, not the GPU);
+//   2. every rank makes its stream wait for every peer's `ready`, enqueues its receive copies
+//      from the peers' buffers and records `done`; host barrier B;
+//   3. every rank makes its stream wait for every peer's `done` (nobody overwrites a send buffer
+//      a peer still reads).
+// A rank re-records `ready` / `done` only after the next collective's barrier A, which every
+// rank reaches after step 3 of this one, so one event pair per rank suffices.
 struct LocalGroup {
   int world = 0;
   std::mutex mu;
@@ -94,7 +104,7 @@ struct LocalGroup {
   std::vector<const void*> ptr;
   std::vector<const size_t*> sizes, offs;
   std::vector<size_t> scalar;
-  std::vector<std::vector<int64_t>> vals;
+  std::vector<hipEvent_t> ready, done;
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
     uint64_t g = gen;
@@ -110,53 +120,89 @@ struct LocalGroup {
 static std::mutex g_groups_mu;
 static std::map<int64_t, std::shared_ptr<LocalGroup>> g_groups;
 
+__global__ void k_sum_slices(const int64_t* in, int world, size_t n, int64_t* out) {
+  for (size_t i = threadIdx.x; i < n; i += blockDim.x) {
+    int64_t s = 0;
+    for (int p = 0; p < world; p++) s += in[size_t(p) * n + i];
+    out[i] = s;
+  }
+}
+
 struct LocalComm : CommImpl {
   int32_t transport() const override { return 2; }
   int32_t ranks() const override { return g ? int32_t(g->world) : -1; }
   std::shared_ptr<LocalGroup> g;
+  hipEvent_t ready = nullptr, done = nullptr;
+  DevBuf scratch;  // allreduce: every rank's slice, then the sums
+  ~LocalComm() override {
+    if (ready) (void)hipEventDestroy(ready);
+    if (done) (void)hipEventDestroy(done);
+  }
+  // step 1 + barrier A
+  void publish(Ctx& c) {
+    NBG_HIP(hipEventRecord(ready, c.stream));
+    g->barrier();
+  }
+  // (after the receive copies) step 2's `done` + barrier B + step 3
+  void finish(Ctx& c) {
+    NBG_HIP(hipEventRecord(done, c.stream));
+    g->barrier();
+    for (int p = 0; p < c.world; p++)
+      if (p != c.rank) NBG_HIP(hipStreamWaitEvent(c.stream, g->done[size_t(p)], 0));
+  }
+  void wait_ready(Ctx& c, int p) {
+    if (p != c.rank) NBG_HIP(hipStreamWaitEvent(c.stream, g->ready[size_t(p)], 0));
+  }
   void allgatherv(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
                   const size_t* recv_off) override {
-    NBG_HIP(hipStreamSynchronize(c.stream));
     g->ptr[size_t(c.rank)] = send;
     g->scalar[size_t(c.rank)] = send_bytes;
-    g->barrier();
+    publish(c);
     for (int p = 0; p < c.world; p++) {
       size_t b = std::min(g->scalar[size_t(p)], recv_bytes[p]);
-      if (b) NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[p], g->ptr[size_t(p)], b,
-                                    hipMemcpyDeviceToDevice, c.stream));
+      if (!b || g->ptr[size_t(p)] == static_cast<uint8_t*>(recv) + recv_off[p]) continue;
+      wait_ready(c, p);
+      NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[p], g->ptr[size_t(p)], b,
+                             hipMemcpyDeviceToDevice, c.stream));
     }
-    NBG_HIP(hipStreamSynchronize(c.stream));
-    g->barrier();
+    finish(c);
   }
   void alltoallv(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
                  const size_t* recv_bytes, const size_t* recv_off) override {
-    NBG_HIP(hipStreamSynchronize(c.stream));
     g->ptr[size_t(c.rank)] = send;
     g->sizes[size_t(c.rank)] = send_bytes;
     g->offs[size_t(c.rank)] = send_off;
-    g->barrier();
+    publish(c);
     for (int p = 0; p < c.world; p++) {
       size_t b = std::min(g->sizes[size_t(p)][c.rank], recv_bytes[p]);
-      if (b)
-        NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[p],
-                               static_cast<const uint8_t*>(g->ptr[size_t(p)]) + g->offs[size_t(p)][c.rank], b,
-                               hipMemcpyDeviceToDevice, c.stream));
+      if (!b) continue;
+      wait_ready(c, p);
+      NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[p],
+                             static_cast<const uint8_t*>(g->ptr[size_t(p)]) + g->offs[size_t(p)][c.rank], b,
+                             hipMemcpyDeviceToDevice, c.stream));
     }
-    NBG_HIP(hipStreamSynchronize(c.stream));
-    g->barrier();
+    finish(c);
   }
+  // in place, as ncclAllReduce: gather the slices, sum them, and write the sums back only after
+  // every peer has read this rank's slice
   void allreduce_sum_i64(Ctx& c, int64_t* d, size_t n) override {
-    std::vector<int64_t> h(n);
-    NBG_HIP(hipMemcpyAsync(h.data(), d, n * 8, hipMemcpyDeviceToHost, c.stream));
-    NBG_HIP(hipStreamSynchronize(c.stream));
-    g->vals[size_t(c.rank)] = h;
-    g->barrier();
-    std::vector<int64_t> s(n, 0);
-    for (int p = 0; p < c.world; p++)
-      for (size_t i = 0; i < n; i++) s[i] += g->vals[size_t(p)][i];
-    g->barrier();
-    NBG_HIP(hipMemcpyAsync(d, s.data(), n * 8, hipMemcpyHostToDevice, c.stream));
-    NBG_HIP(hipStreamSynchronize(c.stream));
+    if (n == 0) return;
+    const size_t G = size_t(c.world);
+    {
+      PoolScope none(nullptr);  // owned by the communicator, outside the query pools
+      scratch.ensure((G + 1) * n * 8);
+    }
+    int64_t* sl = scratch.as<int64_t>();
+    g->ptr[size_t(c.rank)] = d;
+    publish(c);
+    for (int p = 0; p < c.world; p++) {
+      wait_ready(c, p);
+      NBG_HIP(hipMemcpyAsync(sl + size_t(p) * n, g->ptr[size_t(p)], n * 8, hipMemcpyDeviceToDevice, c.stream));
+    }
+    k_sum_slices<<<1, 256, 0, c.stream>>>(sl, c.world, n, sl + G * n);
+    NBG_HIP(hipGetLastError());
+    finish(c);
+    NBG_HIP(hipMemcpyAsync(d, sl + G * n, n * 8, hipMemcpyDeviceToDevice, c.stream));
   }
 };
 
@@ -205,13 +251,24 @@ void comm_init_local(Ctx& c, int64_t key) {
       slot->sizes.resize(size_t(c.world));
       slot->offs.resize(size_t(c.world));
       slot->scalar.resize(size_t(c.world));
-      slot->vals.resize(size_t(c.world));
+      slot->ready.resize(size_t(c.world));
+      slot->done.resize(size_t(c.world));
     }
     g = slot;
   }
   if (g->world != c.world) throw Error(NBG_E_INVALID_ARG, "local group world size mismatch");
   auto* l = new LocalComm();
   l->g = g;
+  if (hipEventCreateWithFlags(&l->ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&l->done, hipEventDisableTiming) != hipSuccess) {
+    delete l;
+    throw Error(NBG_E_DEVICE, "hipEventCreate (LocalComm)");
+  }
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->ready[size_t(c.rank)] = l->ready;
+    g->done[size_t(c.rank)] = l->done;
+  }
   c.comm = l;
 }
 

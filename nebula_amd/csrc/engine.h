@@ -97,13 +97,20 @@ extern thread_local std::shared_ptr<BufPool> tl_pool;  // set for the duration o
 // memory goes through the driver's bounce buffer (r04k: the 173 MB of C3's DISTINCT vids took
 // 64 ms, ~2.7 GB/s); into pinned memory it runs at the link's rate.  hipHostMalloc of a large
 // block is itself slow, so a context caches the blocks its released results hand back.
+// Cap (set per query, host_pool_cap): option host_pool_gb, else 1/16 of the host's RAM shared
+// among the contexts on the device, at most 8 GiB (eight in-process LocalComm ranks on a 1.5 TB
+// host: 8 GiB each; on a 64 GiB host: 512 MiB each).  Trimmed when the context is destroyed.
 struct HostPool {
   std::mutex mu;
   std::multimap<size_t, void*> blocks;
   size_t cached = 0;
   size_t limit = size_t(8) << 30;
-  ~HostPool() {
+  ~HostPool() { trim(); }
+  void trim() {
+    std::lock_guard<std::mutex> lk(mu);
     for (auto& b : blocks) (void)hipHostFree(b.second);
+    blocks.clear();
+    cached = 0;
   }
   void* get(size_t want, size_t& got) {
     std::lock_guard<std::mutex> lk(mu);
@@ -349,6 +356,11 @@ struct EdgeSpace {
   DevBuf odeg;                     // uint32 [owned rows]: out-degree, 0 where row_ok == 0
                                    // (padded with 0 to whole 128-row tiles)
   int64_t max_odeg = -1;           // largest owned out-degree (-1: unknown)
+  int64_t max_odeg_global = -1;    // largest out-degree over all ranks (with out_nnz_global)
+  // prefix sums of the kTopDeg largest out-degrees over all ranks (top_deg[k] = sum of the k
+  // largest): bounds the start frontier's out-degree sum of a GO from k starts (with
+  // out_nnz_global; empty: unknown)
+  std::vector<int64_t> top_deg;
   int64_t bu_in_tiles = 0;         // 128-row tiles up to the last row with an in-edge (final hop)
   int64_t bu_both_tiles = 0;       // ... with an in-edge and an out-edge (non-final hops)
   DevBuf odeg8;                    // uint8 [owned rows, padded as odeg]: min(out-degree, 255); 255 =
@@ -407,6 +419,8 @@ struct Timing {
   uint64_t comm_bytes = 0;
   int32_t n_hops = 0;
   nbg_hop_stat hops[NBG_MAX_HOP_STATS] = {};
+  int32_t host_waits = 0;  // engine-level host waits on the device (fetches, stream syncs)
+  int32_t spec_hops = 0;   // hops that ran behind a device gate
   uint64_t hop_bytes_mark = 0;  // expand_bytes at the previous hop record
   // kernel_ms < 0: the hop is one kernel (its time and bytes are the hop's; a top-down hop's
   // time is filled in later by timing_resolve)
@@ -509,7 +523,7 @@ struct Ctx {
   struct PendingTime {
     size_t a, b;
     int32_t hop;   // Timing::hops index the time belongs to (-1: none)
-    int32_t kind;  // 0: expand_ms + the hop's ms (+ kernel_ms of a top-down hop), 1: kernel_ms only
+    int32_t kind;  // 0: expand_ms + the hop's ms (+ kernel_ms of a top-down hop), 1: kernel_ms only, 2: comm_ms
   };
   bool hop_timing = true;  // option hop_timing: event pairs around the hops' kernels (0: none)
   bool total_pending = false;  // ev[1] recorded, total_ms not read yet (resolve_total)
@@ -558,6 +572,19 @@ struct Ctx {
 // live contexts per device (nbg_ctx_create / nbg_ctx_destroy): in-process rank groups put
 // several contexts on one GPU, and each caches query blocks of its own
 int ctx_count_on_device(int device);
+// the cap of the context's pinned result cache (HostPool)
+size_t host_ram_bytes();
+inline void host_pool_cap(Ctx& c) {
+  const int64_t gb = c.opt("host_pool_gb", -1);
+  size_t cap = size_t(8) << 30;
+  if (gb >= 0) {
+    cap = size_t(gb) << 30;
+  } else if (const size_t ram = host_ram_bytes()) {
+    cap = std::min(cap, ram / 16 / size_t(std::max(1, ctx_count_on_device(c.device))));
+  }
+  std::lock_guard<std::mutex> lk(c.host_pool->mu);
+  c.host_pool->limit = cap;
+}
 // the context's query block cache.  Cap: option query_pool_gb, else a quarter of the device's
 // HBM shared among the contexts on it, at most 64 GiB (one MI355X context: 64 GiB; eight
 // LocalComm ranks on one GPU: 8.9 GiB each), so the cache never holds what RCCL or the driver

@@ -507,6 +507,8 @@ static void reset_transpose_derived(EdgeSpace& es) {
   es.odeg.release();
   es.odeg8.release();
   es.max_odeg = -1;
+  es.max_odeg_global = -1;
+  es.top_deg.clear();
   es.bu_in_tiles = es.bu_both_tiles = 0;
   es.brec.release();
   es.brec_rows = 0;

@@ -25,6 +25,8 @@
 #include <algorithm>
 #include <cmath>
 #include <unordered_map>
+#include <thread>
+#include <initializer_list>
 
 #include "device_common.h"
 #include "engine.h"
@@ -2022,14 +2024,22 @@ void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long lo
   const uint64_t seq = ++c.pub_seq;
   k_publish<<<1, 256, 0, c.stream>>>(d, n, h, c.host_seq, seq);
   NBG_HIP(hipGetLastError());
+  c.timing.host_waits++;
+  if (c.opt("wait_trace", 0)) fprintf(stderr, "[nbg wait] rank %d: counter fetch of %d words\n", c.rank, n);
+  // pure spin for the first ~100 us (most waits: a hop of tens of us), then yield the core
+  // between polls (a long hop, or several in-process LocalComm ranks waiting at once)
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 0;; spin++) {
     if (__atomic_load_n(c.host_seq, __ATOMIC_ACQUIRE) == seq) return;
-    if ((spin & 1023u) == 1023u &&
-        std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-      NBG_HIP(hipStreamSynchronize(c.stream));  // a fault surfaces here
-      if (__atomic_load_n(c.host_seq, __ATOMIC_ACQUIRE) == seq) return;
-      throw Error(NBG_E_DEVICE, "counter publication lost");
+    __builtin_ia32_pause();
+    if ((spin & 255u) == 255u) {
+      const auto dt = std::chrono::steady_clock::now() - t0;
+      if (dt > std::chrono::microseconds(100)) std::this_thread::yield();
+      if (dt > std::chrono::seconds(2)) {
+        NBG_HIP(hipStreamSynchronize(c.stream));  // a fault surfaces here
+        if (__atomic_load_n(c.host_seq, __ATOMIC_ACQUIRE) == seq) return;
+        throw Error(NBG_E_DEVICE, "counter publication lost");
+      }
     }
   }
 }
@@ -2067,27 +2077,53 @@ void ensure_workspaces(Ctx& c, int64_t nF_cap) {
 }
 
 // ---- cross-rank helpers (no-ops with one rank) ---------------------------------------------
+// a host wait of the engine on the device (Timing::host_waits counts them; waits inside the
+// transport are not the engine's)
+void host_sync_at(Ctx& c, int line) {
+  c.timing.host_waits++;
+  if (c.opt("wait_trace", 0)) fprintf(stderr, "[nbg wait] rank %d: stream sync at traverse.hip:%d\n", c.rank, line);
+  NBG_HIP(hipStreamSynchronize(c.stream));
+}
+#define host_sync(c) host_sync_at((c), __LINE__)
+size_t timing_event(Ctx& c);
+// time of the exchanges between ranks: an event pair around each, read after the query (a host
+// wait per collective here would serialise the stream-ordered transport)
 struct CommTimer {
   Ctx& c;
-  explicit CommTimer(Ctx& cc) : c(cc) { hipEventRecord(c.ev[4], c.stream); }
+  size_t a;
+  explicit CommTimer(Ctx& cc) : c(cc), a(timing_event(cc)) {}
   ~CommTimer() {
-    hipEventRecord(c.ev[5], c.stream);
-    if (hipEventSynchronize(c.ev[5]) == hipSuccess) {
-      float ms = 0;
-      hipEventElapsedTime(&ms, c.ev[4], c.ev[5]);
-      c.timing.comm_ms += ms;
-    }
+    const size_t b = timing_event(c);
+    if (a != ~size_t(0) && b != ~size_t(0)) c.tpend.push_back(Ctx::PendingTime{a, b, -1, 2});
   }
 };
 
 // element-wise sum of a few host counters over ranks
 void allsum(Ctx& c, int64_t* v, int n, unsigned long long* dscratch) {
   if (c.world == 1) return;
+  {
+    CommTimer t(c);
+    NBG_HIP(hipMemcpyAsync(dscratch, v, size_t(n) * 8, hipMemcpyHostToDevice, c.stream));
+    comm_allreduce_sum_i64(c, reinterpret_cast<int64_t*>(dscratch), size_t(n));
+    NBG_HIP(hipMemcpyAsync(v, dscratch, size_t(n) * 8, hipMemcpyDeviceToHost, c.stream));
+  }
+  host_sync(c);
+}
+
+// device counters summed over ranks into dst (stream-ordered: a gate kernel reads the sums)
+// srcs: up to 8 counter indices of K.d; dst: n consecutive words
+__global__ void k_pick_counters(const unsigned long long* K, uint64_t idx, int n, unsigned long long* dst) {
+  if (threadIdx.x < unsigned(n)) dst[threadIdx.x] = K[(idx >> (8 * threadIdx.x)) & 0xffu];
+}
+void dev_allsum(Ctx& c, const unsigned long long* K, std::initializer_list<int> idx, unsigned long long* dst) {
+  uint64_t packed = 0;
+  int n = 0;
+  for (int i : idx) packed |= uint64_t(uint8_t(i)) << (8 * n++);
+  k_pick_counters<<<1, 64, 0, c.stream>>>(K, packed, n, dst);
+  NBG_HIP(hipGetLastError());
+  if (c.world == 1) return;
   CommTimer t(c);
-  NBG_HIP(hipMemcpyAsync(dscratch, v, size_t(n) * 8, hipMemcpyHostToDevice, c.stream));
-  comm_allreduce_sum_i64(c, reinterpret_cast<int64_t*>(dscratch), size_t(n));
-  NBG_HIP(hipMemcpyAsync(v, dscratch, size_t(n) * 8, hipMemcpyDeviceToHost, c.stream));
-  NBG_HIP(hipStreamSynchronize(c.stream));
+  comm_allreduce_sum_i64(c, reinterpret_cast<int64_t*>(dst), size_t(n));
 }
 
 // owned frontier bitmap -> bitmap over the whole gidx space (bottom-up hops read sources of
@@ -2196,7 +2232,7 @@ int64_t shuffle_rows(Ctx& c, YieldArgs& ya, std::vector<DevBuf>& cols, int64_t n
   dall.alloc(G * G * 8);
   comm_allgather_bytes(c, dcounts.p, G * 8, dall.p);
   NBG_HIP(hipMemcpyAsync(all.data(), dall.p, G * G * 8, hipMemcpyDeviceToHost, c.stream));
-  NBG_HIP(hipStreamSynchronize(c.stream));
+  host_sync(c);
   const size_t me = size_t(c.rank);
   std::vector<int64_t> soff(G + 1, 0), roff(G + 1, 0);
   for (size_t p = 0; p < G; p++) {
@@ -2244,7 +2280,7 @@ int64_t shuffle_rows(Ctx& c, YieldArgs& ya, std::vector<DevBuf>& cols, int64_t n
     comm_alltoallv_bytes(c, send[cc].p, sb.data(), so.data(), recv[cc].p, rb.data(), ro.data());
     c.timing.comm_bytes += uint64_t(n - (soff[me + 1] - soff[me])) * w;
   }
-  NBG_HIP(hipStreamSynchronize(c.stream));
+  host_sync(c);
   for (size_t cc = 0; cc < cols.size(); cc++) {
     cols[cc] = std::move(recv[cc]);
     ya.cols[cc].data = cols[cc].p;
@@ -2261,7 +2297,7 @@ int64_t degree_scan(Ctx& c, const int32_t* F, int64_t nF, const Csr& csr, DevBuf
   if (known >= 0) return known;
   int64_t E = 0;
   NBG_HIP(hipMemcpyAsync(&E, c.ws_off.as<int64_t>() + nF, 8, hipMemcpyDeviceToHost, c.stream));
-  NBG_HIP(hipStreamSynchronize(c.stream));
+  host_sync(c);
   return E;
 }
 
@@ -2635,6 +2671,60 @@ uint64_t expand_bytes(int64_t nF, int64_t E, int pred_width, int mode) {
 
 }  // namespace
 
+// once per snapshot (collective): the out-edges summed over ranks, the largest out-degree and
+// the prefix sums of the kTopDeg largest out-degrees over ranks, so that every rank takes the
+// same direction decisions and a GO from a few starts knows its first hop's direction before
+// it runs
+constexpr int64_t kTopDeg = 4096;
+void global_degree_stats(Ctx& c, EdgeSpace& es) {
+  const Csr& csr = es.out;
+  const size_t G = size_t(c.world);
+  const int64_t n_own = c.owned_hi() - c.owned_lo();
+  // this rank's kTopDeg largest out-degrees (0-padded), descending
+  DevBuf top;
+  top.alloc(size_t(kTopDeg) * 4 + 16);
+  NBG_HIP(hipMemsetAsync(top.p, 0, size_t(kTopDeg) * 4, c.stream));
+  if (es.odeg.p && n_own > 0) {
+    DevBuf srt;
+    srt.alloc(size_t(n_own) * 4);
+    size_t tb = 0;
+    NBG_HIP(rocprim::radix_sort_keys_desc(nullptr, tb, es.odeg.as<uint32_t>(), srt.as<uint32_t>(), size_t(n_own), 0, 32,
+                                          c.stream));
+    c.ws_tmp.ensure(tb);
+    NBG_HIP(rocprim::radix_sort_keys_desc(c.ws_tmp.p, tb, es.odeg.as<uint32_t>(), srt.as<uint32_t>(), size_t(n_own), 0,
+                                          32, c.stream));
+    NBG_HIP(hipMemcpyAsync(top.p, srt.p, size_t(std::min(n_own, kTopDeg)) * 4, hipMemcpyDeviceToDevice, c.stream));
+  }
+  const size_t row = size_t(kTopDeg) * 4 + 16;  // the degrees, then (nnz, max out-degree)
+  std::vector<int64_t> mine = {csr.nnz, es.max_odeg};
+  NBG_HIP(hipMemcpyAsync(top.as<uint8_t>() + size_t(kTopDeg) * 4, mine.data(), 16, hipMemcpyHostToDevice, c.stream));
+  std::vector<uint8_t> all(row * G);
+  DevBuf da;
+  da.alloc(row * G);
+  comm_allgather_bytes(c, top.p, row, da.p);
+  NBG_HIP(hipMemcpyAsync(all.data(), da.p, row * G, hipMemcpyDeviceToHost, c.stream));
+  host_sync(c);
+  int64_t nnz = 0, mx = 0;
+  std::vector<uint32_t> degs;
+  for (size_t r = 0; r < G; r++) {
+    const uint8_t* b = all.data() + r * row;
+    int64_t v[2];
+    memcpy(v, b + size_t(kTopDeg) * 4, 16);
+    nnz += v[0];
+    mx = v[1] < 0 || mx < 0 ? -1 : std::max(mx, v[1]);
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(b);
+    degs.insert(degs.end(), d, d + kTopDeg);
+  }
+  std::sort(degs.begin(), degs.end(), std::greater<uint32_t>());
+  es.top_deg.assign(size_t(kTopDeg) + 1, 0);
+  if (es.odeg.p)
+    for (int64_t k = 0; k < kTopDeg; k++) es.top_deg[size_t(k) + 1] = es.top_deg[size_t(k)] + int64_t(degs[size_t(k)]);
+  else
+    es.top_deg.clear();  // no degree array: unknown
+  es.out_nnz_global = nnz;
+  es.max_odeg_global = mx;
+}
+
 // ------------------------------------------------------------------------------------------
 // GO N STEPS
 // ------------------------------------------------------------------------------------------
@@ -2652,7 +2742,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   // per-hop event pairs (hop stats); bench.py's timed loop turns them off like a production
   // caller would, its statistics loop on
   c.hop_timing = c.opt("hop_timing", 1) != 0;
-  if (c.host_stage_used) NBG_HIP(hipStreamSynchronize(c.stream));  // a failed query's copies
+  if (c.host_stage_used) host_sync(c);  // a failed query's copies
   c.host_stage_used = 0;
   c.total_pending = false;
   hipEventRecord(c.ev[0], c.stream);
@@ -2731,10 +2821,20 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   // builds its frontier and degree scan (k_starts_small) and the hop runs without a round trip
   // (the expansion reads the frontier size from the scan; the counts come back with the
   // compaction's)
-  const bool td1_certain = !bu_ok || bu_force < 0 ||
-                           (bu_force == 0 && es.max_odeg >= 0 && ns * es.max_odeg < csr.nnz / bu_div);
-  const bool fast1 = ns > 0 && ns <= kSmallStarts && c.world == 1 && s.steps >= 2 && td1_certain &&
-                     !(uses_input && s.steps > 1) && c.opt("starts_small", 1) != 0;
+  if (es.out_nnz_global < 0) global_degree_stats(c, es);
+  // a first hop from ns starts is certainly top-down when even the ns largest out-degrees sum
+  // below the bottom-up threshold
+  const int64_t deg_bound = ns < int64_t(es.top_deg.size()) ? es.top_deg[size_t(ns)]
+                            : es.max_odeg_global >= 0       ? ns * es.max_odeg_global
+                                                            : INT64_MAX;
+  const bool td1_certain =
+      !bu_ok || bu_force < 0 || (bu_force == 0 && deg_bound < es.out_nnz_global / bu_div);
+  // (with several ranks each rank's k_starts_small keeps its own starts; the hop-1 marks are
+  // exchanged before the compaction)
+  const bool fast1 = ns > 0 && ns <= kSmallStarts && s.steps >= 2 && td1_certain && !(uses_input && s.steps > 1) &&
+                     c.opt("starts_small", 1) != 0;
+  // counters summed over ranks on the device (dev_allsum) land at K.d[48, 52)
+  const bool multi = c.world > 1;
   if (ns) {
     c.h2d(d_starts, s.starts, size_t(ns) * 8);
     if (!fast1) lookup_gidx(c, d_starts, d_sg, ns);
@@ -2745,6 +2845,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   int64_t nF = 0;
   int64_t nset_global = ns;  // "starts_ non-empty" (GoExecutor.cpp:93-97)
   int64_t hop1_scanned = -1;  // hop-1 rows with duplicate starts rescanned (k_starts_degree)
+  int64_t Eg_known = -1;      // several ranks: the start frontier's out-degree sum over ranks
   if (fast1) {
     k_starts_small<<<1, 1024, 0, c.stream>>>(d_starts, int32_t(ns), c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
                                               uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, d_sg, lo, hi,
@@ -2773,19 +2874,17 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         k_starts_degree<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, K.d + 30);
     }
     NBG_HIP(hipGetLastError());
-    fetch_counters(c, K.d, 32, K.h);
+    const bool counted = !(s.steps == 1 && !s.distinct);
+    if (multi && counted) dev_allsum(c, K.d, {13}, K.d + 48);
+    fetch_counters(c, K.d, multi && counted ? 52 : 32, K.h);
     nF = int64_t(K.h[0]);
-    if (!(s.steps == 1 && !s.distinct)) {
+    if (counted) {
       E_known = int64_t(K.h[13]);
+      if (multi) Eg_known = int64_t(K.h[48]);
       if (!s.distinct) hop1_scanned = int64_t(K.h[30]);
     }
   }
   unsigned long long* red = K.d + 24;  // scratch of the cross-rank sums
-  if (es.out_nnz_global < 0) {
-    int64_t v = csr.nnz;
-    allsum(c, &v, 1, red);
-    es.out_nnz_global = v;
-  }
   auto finish_empty = [&]() -> int32_t {
     auto* h = new HostRows();
     for (auto& p : yields) {
@@ -2845,7 +2944,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     root_tab.alloc(std::max<size_t>(u.size(), 1) * 4);
     if (ns) k_root_init<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, drk.as<int32_t>(), ns, root_buf[0].as<int32_t>(),
                                                            root_tab.as<int32_t>());
-    NBG_HIP(hipStreamSynchronize(c.stream));  // rk is pageable host memory
+    host_sync(c);  // rk is pageable host memory
   }
   if (uses_input) {
     uint32_t cap = 64;
@@ -2880,7 +2979,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     }
     in_tab.alloc(sizeof(PropDev) * tab.size());
     NBG_HIP(hipMemcpyAsync(in_tab.p, tab.data(), sizeof(PropDev) * tab.size(), hipMemcpyHostToDevice, c.stream));
-    NBG_HIP(hipStreamSynchronize(c.stream));  // `tab` is pageable host memory
+    host_sync(c);  // `tab` is pageable host memory
     env.in_keys = in_keys.as<int32_t>();
     env.in_rows = in_rows.as<int32_t>();
     env.in_mask = cap - 1;
@@ -2933,7 +3032,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   // direction never changes a hop's result, only its cost.  The final step is speculated only
   // as the DISTINCT _dst bottom-up hop (a predicate that cannot error, no deferred compile
   // error).  Blocks of 16 words from K.d[64]: [0, 8) the hop's counters, [8] its gate, [9] the
-  // DISTINCT output count.
+  // DISTINCT output count, [10, 12) found / next out-degree sum over ranks (several ranks).
   struct Spec {
     int32_t hop;  // Timing::hops index it will take
     bool final;
@@ -2956,7 +3055,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
                       es.tr.props[size_t(fpk0.col)].data.p);
     fin_spec = ddst && pbu;
   }
-  const bool spec_ok = c.world == 1 && bu_ok && !multi_root && bu_force >= 0 && c.opt("bu_spec", 1) != 0;
+  // (several ranks: each gate reads counters summed over ranks on the device, dev_allsum, and
+  // every rank enqueues the same chain of collectives, so every rank takes the same branches)
+  const bool spec_ok = bu_ok && !multi_root && bu_force >= 0 && c.opt("bu_spec", 1) != 0;
   const unsigned long long spec_thr =
       bu_force > 0 ? 1ull : (unsigned long long)std::max<int64_t>(1, es.out_nnz_global / bu_div);
   unsigned long long* const SPd = K.d + 64;
@@ -2974,14 +3075,17 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       unsigned long long* blk = SPd + 16 * spec.size();
       k_gate<<<1, 64, 0, c.stream>>>(e, n, pg, spec_thr, blk + 8);
       const int32_t hop = hop0 + int32_t(spec.size());
+      // several ranks: the frontier bitmaps of every rank (the exchange runs whatever the gate
+      // says: every rank enqueued it)
+      const uint32_t* fb = global_bits(c, in);
       const size_t ia = timing_event(c);
       size_t ik;
       if (!fin) {
-        ik = launch_bu_lean(c, es, in, outb, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, blk, blk + 8);
+        ik = launch_bu_lean(c, es, fb, outb, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, blk, blk + 8);
       } else {
         FastArgs tfp = fp0;
         if (fpk0.kind == PK_FAST) tfp.data = es.tr.props[size_t(fpk0.col)].data.p;
-        ik = launch_bu_lean(c, es, in, outb, nullptr, fpk0.kind, tfp, fpk0.kind == PK_FAST ? fpk0.col : -1, blk,
+        ik = launch_bu_lean(c, es, fb, outb, nullptr, fpk0.kind, tfp, fpk0.kind == PK_FAST ? fpk0.col : -1, blk,
                             blk + 8);
         spec_vids.alloc(size_t(c.n_global + 64) * 8);
         launch_bits_vids(c, outb, es.tr.n_rows, lo, spec_vids.p, blk + 9, blk + 8);
@@ -2993,6 +3097,11 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       spec.push_back(Spec{hop, fin, c.bu_kernel_name, c.bu_rest_name});
       e = blk + 1;
       n = blk + 0;
+      if (multi && !fin) {
+        dev_allsum(c, blk, {0, 1}, blk + 10);
+        e = blk + 11;
+        n = blk + 10;
+      }
       pg = blk + 8;
       const uint32_t* t = in;
       in = outb;
@@ -3018,6 +3127,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
                       c.tpend.end());
         break;
       }
+      c.timing.spec_hops++;
       if (spec[j].final) {
         std::copy(hh, hh + 16, fin_h);
         fin_k0 = spec[j].k0;
@@ -3039,8 +3149,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       off_ready = false;
       E = int64_t(hh[1]);
       E_known = E;
-      nset_global = int64_t(hh[0]);
-      Eg = E;
+      nset_global = int64_t(multi ? hh[10] : hh[0]);
+      Eg = multi ? int64_t(hh[11]) : E;
       used++;
       if (nset_global == 0) break;  // the caller returns the empty result
     }
@@ -3052,7 +3162,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   } else {
     ensure_off();
     Eg = E;
-    allsum(c, &Eg, 1, red);
+    if (Eg_known >= 0) Eg = Eg_known;
+    else allsum(c, &Eg, 1, red);
   }
   for (int32_t step = 1; step < s.steps; step++) {
     c.timing.steps_run++;
@@ -3064,28 +3175,31 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       a.off = c.ws_off.as<int64_t>();
       const int64_t e_bound = std::max<int64_t>(1, es.max_odeg >= 0 ? ns * es.max_odeg : csr.nnz);
       launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, std::min<int64_t>(e_bound, csr.nnz + 1));
+      exchange_marks(c, map);  // several ranks: every owner receives the marks of its vertices
       cur ^= 1;
       F = c.ws_front[cur].as<int32_t>();
       const bool lazy = bu_ok && c.opt("compact_list", 0) == 0;
       // (K.d[0, 4) are zero: k_starts_small cleared the counters)
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
                      K.d, es.odeg.as<uint32_t>());
-      spec_enqueue(2, K.d + 13, K.d + 12, c.timing.n_hops + 1);  // (hop 1 is recorded below)
+      // several ranks: found, next out-degree sum and hop-1 entries summed over ranks -> K.d[48, 51)
+      if (multi) dev_allsum(c, K.d, {12, 13, 41}, K.d + 48);
+      spec_enqueue(2, K.d + (multi ? 49 : 13), K.d + (multi ? 48 : 12), c.timing.n_hops + 1);  // (hop 1: below)
       // (the device work ends here when the speculated final hop runs: ev[1] ahead of the fetch)
-      fetch_counters(c, K.d, spec_words(42), K.h, spec_final() ? c.ev[1] : nullptr);
+      fetch_counters(c, K.d, spec_words(multi ? 52 : 42), K.h, spec_final() ? c.ev[1] : nullptr);
       const int64_t nF1 = int64_t(K.h[40]), E1 = int64_t(K.h[41]);
       if (!s.distinct) hop1_scanned = int64_t(K.h[30]);
       c.timing.edges_scanned += uint64_t(hop1_scanned >= 0 ? hop1_scanned : E1);
       if (E1 > 0) c.timing.expand_bytes += expand_bytes(nF1, E1, 0, EXP_MARK);
       const unsigned long long hs[8] = {(unsigned long long)nF1, (unsigned long long)E1, 0, 0, 0, 0, 0, 0};
       c.timing.hop(0, false, 0.0, hs);
-      if (E1 == 0) return finish_empty();  // every start lacks out-edges
+      if ((multi ? int64_t(K.h[50]) : E1) == 0) return finish_empty();  // every start lacks out-edges
       nF = lazy ? 0 : int64_t(K.h[0]);
       list_n = lazy ? int64_t(K.h[14]) : -1;
       E = int64_t(K.h[13]);
       E_known = E;
-      nset_global = int64_t(K.h[12]);
-      Eg = E;
+      nset_global = int64_t(K.h[multi ? 48 : 12]);
+      Eg = multi ? int64_t(K.h[49]) : E;
       have_list = !lazy;
       if (lazy) cur ^= 1;  // ensure_list flips to the list buffer again
       off_ready = false;
@@ -3106,7 +3220,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const size_t ib = timing_event(c);
       c.tpend.push_back(Ctx::PendingTime{ia, ib, c.timing.n_hops, 0});
       c.tpend.push_back(Ctx::PendingTime{ia, ik, c.timing.n_hops, 1});
-      fetch_counters(c, K.d, 8, K.h);
+      if (multi) dev_allsum(c, K.d, {0, 1}, K.d + 48);
+      fetch_counters(c, K.d, multi ? 50 : 8, K.h);
       c.timing.expand_launches++;
       c.timing.bu_steps++;
       const uint64_t kb = bu_first_bytes(K.h, tr.n_rows, true), hb = kb + bu_rest_bytes(K.h, 0, c.bu_rest_rec);
@@ -3119,10 +3234,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       off_ready = false;
       E = int64_t(K.h[1]);
       E_known = E;
-      int64_t g2[2] = {int64_t(K.h[0]), E};
-      allsum(c, g2, 2, red);
-      nset_global = g2[0];
-      Eg = g2[1];
+      nset_global = multi ? int64_t(K.h[48]) : int64_t(K.h[0]);
+      Eg = multi ? int64_t(K.h[49]) : E;
     } else {
       ensure_off();
       a.F = F;
@@ -3154,19 +3267,18 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // when the next hop may go bottom-up it reads the bitmap alone: the list is left to
       // ensure_list (option compact_list = 1 always writes it here).  One rank only: this
       // bitmap is slice-relative, ensure_list's input is the bottom-up's global-indexed one
-      const bool lazy = c.world == 1 && bu_ok && !multi_root && c.opt("compact_list", 0) == 0;
+      const bool lazy = bu_ok && !multi_root && c.opt("compact_list", 0) == 0;
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
                      K.d, es.odeg.as<uint32_t>());
-      if (lazy) spec_enqueue(step + 1, K.d + 13, K.d + 12, c.timing.n_hops);
-      fetch_counters(c, K.d, spec_words(16), K.h, spec_final() ? c.ev[1] : nullptr);
+      if (multi) dev_allsum(c, K.d, {12, 13}, K.d + 48);
+      if (lazy) spec_enqueue(step + 1, K.d + (multi ? 49 : 13), K.d + (multi ? 48 : 12), c.timing.n_hops);
+      fetch_counters(c, K.d, spec_words(multi ? 50 : 16), K.h, spec_final() ? c.ev[1] : nullptr);
       nF = lazy ? 0 : int64_t(K.h[0]);
       list_n = lazy ? int64_t(K.h[14]) : -1;
       E = int64_t(K.h[13]);
       E_known = E;
-      int64_t g2[2] = {int64_t(K.h[12]), E};
-      allsum(c, g2, 2, red);
-      nset_global = g2[0];
-      Eg = g2[1];
+      nset_global = multi ? int64_t(K.h[48]) : int64_t(K.h[12]);
+      Eg = multi ? int64_t(K.h[49]) : E;
       have_list = !lazy;
       if (lazy) cur ^= 1;  // ensure_list flips to the list buffer again
       off_ready = false;
@@ -3269,9 +3381,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         lst.alloc(size_t(n_own + 64) * 4);
         NBG_HIP(hipMemsetAsync(K.d, 0, 16, c.stream));  // keep the eval-error counter (K.d[4])
         launch_compact(c, map, lo, n_own, row_ptr, nullptr, 0, lst.as<int32_t>(), nullptr, K.d);
-        fetch_counters(c, K.d, 6, K.h);
-        int64_t errs = int64_t(K.h[4]);
-        allsum(c, &errs, 1, red);
+        if (multi) dev_allsum(c, K.d, {4}, K.d + 48);
+        fetch_counters(c, K.d, multi ? 49 : 6, K.h);
+        const int64_t errs = int64_t(K.h[multi ? 48 : 4]);
         if (errs) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
         nrows = int64_t(K.h[0]);
         if (nrows)
@@ -3308,9 +3420,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       NBG_HIP(hipMemsetAsync(K.d, 0, 48, c.stream));
       const double ms0 = c.timing.expand_ms;
       if (E > 0) launch_expand<EXP_ROWS>(c, a, pk, fp, dprog.as<Program>(), env, E);
-      fetch_counters(c, K.d, 6, K.h);
-      int64_t errs = int64_t(K.h[4]);
-      allsum(c, &errs, 1, red);
+      if (multi) dev_allsum(c, K.d, {4}, K.d + 48);
+      fetch_counters(c, K.d, multi ? 49 : 6, K.h);
+      const int64_t errs = int64_t(K.h[multi ? 48 : 4]);
       if (errs) throw Error(NBG_E_EVAL, "WHERE evaluation failed");
       const bool direct = dst_only && pk == PK_NONE;  // every edge is a row, written at its index
       nrows = direct ? E : int64_t(K.h[2]);
@@ -3349,9 +3461,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         }
         NBG_HIP(hipGetLastError());
       }
-      fetch_counters(c, K.d, 6, K.h);
-      int64_t yerr = int64_t(K.h[5]);
-      allsum(c, &yerr, 1, red);
+      if (multi) dev_allsum(c, K.d, {5}, K.d + 48);
+      fetch_counters(c, K.d, multi ? 49 : 6, K.h);
+      const int64_t yerr = int64_t(K.h[multi ? 48 : 5]);
       if (yerr) throw Error(NBG_E_EVAL, "YIELD evaluation failed");
       if (s.distinct && c.world > 1) nrows = shuffle_rows(c, ya, h->dev, nrows);
       if (s.distinct && nrows) {
@@ -3395,7 +3507,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
           }
           uint64_t kc = 0;
           NBG_HIP(hipMemcpyAsync(&kc, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
-          NBG_HIP(hipStreamSynchronize(c.stream));
+          host_sync(c);
           kept = int64_t(kc);
           h->dev[cc] = std::move(nb);
         }
@@ -3422,7 +3534,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       exclusive_scan_dev<int64_t>(c, slen[cc].as<int64_t>(), off.as<int64_t>(), nrows + 1);
       int64_t total = 0;
       NBG_HIP(hipMemcpyAsync(&total, off.as<int64_t>() + nrows, 8, hipMemcpyDeviceToHost, c.stream));
-      NBG_HIP(hipStreamSynchronize(c.stream));
+      host_sync(c);
       bytes.alloc(size_t(total) + 8);
       if (nrows && total)
         k_str_pack<<<grid_cap(nrows), 256, 0, c.stream>>>(h->dev[cc].as<int64_t>(), off.as<int64_t>(), nrows,
@@ -3432,15 +3544,26 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       soff_dev_idx[cc] = int64_t(h->dev.size());
       h->dev.push_back(std::move(off));
     }
-    // the result is complete before it is handed out (a drained stream costs no wait)
-    if (hipStreamQuery(c.stream) != hipSuccess) NBG_HIP(hipStreamSynchronize(c.stream));
-    c.host_stage_used = 0;  // the query's input copies have completed
+    // the result is complete before it is handed out: a host copy waits for its own copies
+    // (below); device columns need the stream drained, which the counter fetch of a speculated
+    // final hop already saw (nothing was enqueued after it)
+    // (STRING columns and very large ones are copied with the blocking hipMemcpy, which does not
+    // order behind the engine stream: drained first)
+    bool drain = s.keep_on_device ? !fin_done : false;
+    for (size_t cc = 0; cc < ncols_out && !s.keep_on_device; cc++) {
+      const size_t w = h->types[cc] == NBG_T_BOOL ? 1 : 8;
+      drain |= soff_dev_idx[cc] >= 0 ||
+               size_t(nrows) * w + 8 > size_t(std::max<int64_t>(0, c.opt("host_pinned_mb", 4096))) << 20;
+    }
+    if (drain && hipStreamQuery(c.stream) != hipSuccess) host_sync(c);
+    if (s.keep_on_device || drain) c.host_stage_used = 0;  // the query's input copies have completed
   } catch (...) {
     delete h;
     throw;
   }
-  // hand the columns out
+  // hand the columns out (a failed pinned allocation or copy frees the rows and rethrows)
   bool on_dev = s.keep_on_device != 0;
+  try {
   for (size_t cc = 0; cc < ncols_out; cc++) {
     if (soff_dev_idx[cc] >= 0) {  // STRING
       DevBuf& off = h->dev[size_t(soff_dev_idx[cc])];
@@ -3466,6 +3589,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const size_t bytes = size_t(nrows) * w + 8;
       if (bytes <= size_t(std::max<int64_t>(0, c.opt("host_pinned_mb", 4096))) << 20) {
         h->hpin.emplace_back();
+        if (h->hpin.size() == 1) host_pool_cap(c);
         h->hpin.back().alloc(c.host_pool, bytes);
         if (nrows)
           NBG_HIP(hipMemcpyAsync(h->hpin.back().p, h->dev[cc].p, size_t(nrows) * w, hipMemcpyDeviceToHost, c.stream));
@@ -3478,8 +3602,14 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     }
   }
   if (!on_dev) {
-    NBG_HIP(hipStreamSynchronize(c.stream));  // the pinned copies above
+    host_sync(c);  // the pinned copies above (and with them the whole query)
+    c.host_stage_used = 0;
     h->dev.clear();
+  }
+  } catch (...) {
+    (void)hipStreamSynchronize(c.stream);  // no copy may still target a block freed here
+    delete h;
+    throw;
   }
   fill_rows(out, h, nrows, on_dev);
   out->edges_scanned = c.timing.edges_scanned;
@@ -3499,6 +3629,10 @@ void timing_resolve(Ctx& c) {
       const bool in_hop = p.hop >= 0 && p.hop < c.timing.n_hops && p.hop < NBG_MAX_HOP_STATS;
       if (p.kind == 1) {  // a bottom-up hop's first pass
         if (in_hop) c.timing.hops[p.hop].kernel_ms += ms;
+        continue;
+      }
+      if (p.kind == 2) {  // an exchange between ranks
+        c.timing.comm_ms += ms;
         continue;
       }
       c.timing.expand_ms += ms;

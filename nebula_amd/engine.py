@@ -48,10 +48,32 @@ def pack_kv(pairs):
     return kb, koff, vb, voff
 
 
-class RowSet:
-    """Typed columnar result (copied to host unless ``on_device``)."""
+class _RowsHandle:
+    """Owns an nbg_rows until the last array viewing its host columns is gone (nbg_rows_free then
+    returns the pinned blocks to the context's cache)."""
 
-    def __init__(self, rows: _lib.Rows, keep_device: bool = False):
+    def __init__(self, L, rows: _lib.Rows):
+        self.L, self.rows = L, rows
+
+    def __del__(self):
+        rows, self.rows = self.rows, None
+        if rows is not None:
+            self.L.nbg_rows_free(C.byref(rows))
+
+
+def _view(ptr, n, ctype, dtype, holder):
+    """numpy view of n host values at ptr (no copy), keeping `holder` alive with it"""
+    ct = (ctype * n).from_address(ptr)
+    ct._holder = holder
+    return np.frombuffer(ct, dtype=dtype)
+
+
+class RowSet:
+    """Typed columnar result (copied to host unless ``on_device``).  With ``holder`` (nbg_go) the
+    INT / VID / DOUBLE columns are views of the engine's pinned result blocks, not copies; the
+    rows are freed when the RowSet and every such column are gone."""
+
+    def __init__(self, rows: _lib.Rows, keep_device: bool = False, holder: _RowsHandle | None = None):
         self.n_rows = int(rows.n_rows)
         self.types = [rows.col_types[i] for i in range(rows.n_cols)]
         self.edges_scanned = int(rows.edges_scanned)
@@ -76,9 +98,11 @@ class RowSet:
             elif t == _lib.T_BOOL:
                 self.columns.append(np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_uint8)), shape=(self.n_rows,)).astype(bool))
             elif t == _lib.T_DOUBLE:
-                self.columns.append(np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_double)), shape=(self.n_rows,)).copy())
+                self.columns.append(_view(ptr, self.n_rows, C.c_double, np.float64, holder) if holder else
+                                    np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_double)), shape=(self.n_rows,)).copy())
             else:
-                self.columns.append(np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_int64)), shape=(self.n_rows,)).copy())
+                self.columns.append(_view(ptr, self.n_rows, C.c_int64, np.int64, holder) if holder else
+                                    np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_int64)), shape=(self.n_rows,)).copy())
         self.row_vertex = (np.ctypeslib.as_array(rows.row_vertex, shape=(self.n_rows,)).copy()
                            if rows.row_vertex and self.n_rows else np.zeros(0, dtype=np.int64))
         nv = int(rows.n_vertices)
@@ -348,10 +372,13 @@ class GraphSpace:
             spec.input_cols, spec.input_str_offsets = cols, offs
         rows = _lib.Rows()
         self._check(self.L.nbg_go(self.h, C.byref(spec), C.byref(rows)))
-        try:
-            return RowSet(rows)
-        finally:
-            self.L.nbg_rows_free(C.byref(rows))
+        if keep_on_device:
+            try:
+                return RowSet(rows)
+            finally:
+                self.L.nbg_rows_free(C.byref(rows))
+        # host result: zero-copy views of the pinned blocks, held until the columns are dropped
+        return RowSet(rows, holder=_RowsHandle(self.L, rows))
 
 
     def shortest_path(self, src, dst, edge_type: int, max_steps: int = 5) -> "PathResult":

@@ -56,6 +56,18 @@ def test_bench_query_rmat20_sharded(force):
                 assert all(x["bu_steps"] > 0 for x in t)
             if force == -1:
                 assert all(x["bu_steps"] == 0 for x in t)
+            if force == 0:
+                # the sharded query runs from its start frontier to the result behind device
+                # gates fed by stream-ordered reductions: one counter fetch, then the result's
+                # copy to the host (GoExecutor.cpp:334-399's per-step round trips are gone).  The
+                # first query also gathers the snapshot's degree statistics once: the second
+                res = g.go(synth.seeds(20, 16, 1, 64), 3, FOLLOW, where=W499, yields=[X.EdgeDst("follow")],
+                           distinct=True)
+                col = np.sort(np.concatenate([x.columns[0] for x in res]))
+                check_gold("go3_where499_distinct_s20", col, sum(x.edges_scanned for x in res))
+                t = g.each(lambda r, s: s.last_timing())
+                assert all(x["host_waits"] <= 2 and x["spec_hops"] >= 2 for x in t), \
+                    [(x["host_waits"], x["spec_hops"]) for x in t]
         finally:
             g.close()
 

@@ -403,7 +403,16 @@ def test_rmat_speculative_hops(rmat12, bu_div):
             for spec in (1, 0):
                 sp.set_option("bu_spec", spec)
                 g = sp.go(starts, steps, FOLLOW, where=where, yields=y if distinct else (), distinct=distinct)
-                hops = sp.last_timing()["hops"]
+                t = sp.last_timing()
+                hops = t["hops"]
+                if spec:
+                    # a bottom-up hop right after a top-down hop ran behind its device gate
+                    # (the final DISTINCT hop included), never re-run by the host
+                    tr = [i for i in range(1, len(hops))
+                          if hops[i - 1]["mode"] == "top-down" and hops[i]["mode"] == "bottom-up"]
+                    assert t["spec_hops"] >= len(tr), (steps, distinct, t["spec_hops"], tr)
+                else:
+                    assert t["spec_hops"] == 0
                 runs.append((np.sort(g.columns[0]), g.edges_scanned, [(h["mode"], h["c"]) for h in hops]))
             assert np.array_equal(runs[0][0], runs[1][0]) and runs[0][1] == runs[1][1]
             assert runs[0][2] == runs[1][2], (steps, distinct)
@@ -411,6 +420,33 @@ def test_rmat_speculative_hops(rmat12, bu_div):
                       yields=[y[0].encode()] if distinct else (), distinct=distinct)
             assert np.array_equal(runs[0][0], np.sort(r.int_col(0)))
             assert runs[0][1] == r.edges_scanned
+    sp.set_option("bu_spec", 1)
+    sp.set_option("bu_div", 4)
+
+
+def test_rmat_speculative_hops_ran(rmat12):
+    """the gated path itself is exercised: over the thresholds above, some non-final and some
+    final (DISTINCT _dst) hops ran behind their gates (nbg_timing.spec_hops)"""
+    sp, _ = rmat12
+    starts = sorted(set(seeds_from(12, 24, seed=41)))
+    w = X.AliasProp("follow", "weight") > 499
+    nonfinal = final = 0
+    try:
+        for bu_div in (1, 2, 4, 16, 256):
+            sp.set_option("bu_div", bu_div)
+            for steps in (2, 3, 4):
+                sp.go(starts, steps, FOLLOW, where=w, yields=[X.EdgeDst("follow")], distinct=True)
+                t = sp.last_timing()
+                hops = t["hops"]
+                if t["spec_hops"] and hops[-1]["final"] and hops[-1]["mode"] == "bottom-up":
+                    # speculated hops are the last ones of the query
+                    final += 1
+                    nonfinal += t["spec_hops"] - 1
+                else:
+                    nonfinal += t["spec_hops"]
+    finally:
+        sp.set_option("bu_div", 4)
+    assert nonfinal > 0 and final > 0, (nonfinal, final)
 
 
 def test_rmat_go_where_distinct(rmat12):
