@@ -868,7 +868,7 @@ __device__ inline void bu_rest_scan(const bool (&pend)[R], bool (&found)[R], con
 // HUB: the block keeps the first cw words of the bitmap (the highest-out-degree vertices) in LDS
 // and answers candidates there from it; the global probe of such a slot is out of bounds.
 // Partials [6] / [7]: candidate probes sent to L2 / answered from LDS.
-template <int PK, int U, int HUB, int STATS, int NT = 0>
+template <int PK, int U, int HUB, int STATS, int NT = 0, int SKIP = 0>
 __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ lo, const uint2* __restrict__ hi,
                                                      int64_t ntiles, int64_t work_tiles,
                                                      const uint32_t* __restrict__ fbits, uint32_t fb_bytes,
@@ -961,6 +961,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
       }
     // probes: the LDS reads first (answered in ~100 cycles), then the L2 ones, each into a
     // register of its own, OR-ed afterwards (one of the two is always 0)
+    // SKIP: a probe instruction only when some lane of the wave has a candidate for it (most
+    // slot registers of a tile need few or no L2 probes: the hub copy answers the hub sources)
     uint32_t lw[U][2][NS], gw[U][2][NS];
     if (HUB) {
 #pragma unroll
@@ -968,14 +970,29 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
 #pragma unroll
         for (int h = 0; h < 2; h++)
 #pragma unroll
-          for (int k = 0; k < NS; k++) lw[u][h][k] = s_fb[lidx[u][h][k]];
+          for (int k = 0; k < NS; k++) {
+            if (SKIP) {
+              lw[u][h][k] = 0u;
+              if (__ballot(lidx[u][h][k] != ucw)) lw[u][h][k] = s_fb[lidx[u][h][k]];
+            } else {
+              lw[u][h][k] = s_fb[lidx[u][h][k]];
+            }
+          }
     }
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
       for (int h = 0; h < 2; h++)
 #pragma unroll
-        for (int k = 0; k < NS; k++) gw[u][h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, goff[u][h][k], 0, 0);
+        for (int k = 0; k < NS; k++) {
+          if (SKIP) {
+            gw[u][h][k] = 0u;
+            if (__ballot(goff[u][h][k] != 0xfffffff0u))
+              gw[u][h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, goff[u][h][k], 0, 0);
+          } else {
+            gw[u][h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, goff[u][h][k], 0, 0);
+          }
+        }
     __builtin_amdgcn_sched_barrier(0);
     bool f[U][2], pend[U][2];
 #pragma unroll
@@ -1113,7 +1130,10 @@ constexpr uint32_t kNoProbe = 0x0ffffff0u;
 // in L2): 158 -> 148 us at C3.  Measured without gain (r04f/r04g): the next tile's slab loads
 // issued behind the current tile's probes, an interleaved 16-byte slab (one load per row), two
 // tiles per wave; with no probes at all the slab alone streams at 4.7 TB/s in this loop.
-template <int CLS, int NT>
+// VAR (measurement variants): bit 0 -- a probe instruction is issued only when some lane of the
+// wave has an L2 candidate in that slot; bit 1 -- each wave takes a contiguous range of tiles;
+// bit 2 -- the same skip for the LDS hub reads
+template <int CLS, int NT, int VAR = 0>
 __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo, const uint2* __restrict__ hi,
                                                     int64_t ntiles, int64_t work_tiles,
                                                     const uint32_t* __restrict__ fbits,
@@ -1150,6 +1170,17 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
     return make_uint2(uint32_t(x), uint32_t(x >> 32));
   };
   auto load = [&](int64_t t, uint32_t (&sw)[2][4]) {
+    if (VAR & 8) {
+      // 16-byte lanes: lane l holds rows 2l (h 0) and 2l + 1 (h 1) of the tile, one load per half
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4* l4 = reinterpret_cast<const u32x4*>(lo) + t * 64 + lane;
+      const u32x4* h4 = reinterpret_cast<const u32x4*>(hi) + t * 64 + lane;
+      const u32x4 a = NT ? __builtin_nontemporal_load(l4) : *l4;
+      const u32x4 b = NT ? __builtin_nontemporal_load(h4) : *h4;
+      sw[0][0] = a.x, sw[0][1] = a.y, sw[0][2] = b.x, sw[0][3] = b.y;
+      sw[1][0] = a.z, sw[1][1] = a.w, sw[1][2] = b.z, sw[1][3] = b.w;
+      return;
+    }
     const int64_t r = t * 128 + lane;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -1157,7 +1188,25 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
       sw[h][0] = a.x, sw[h][1] = a.y, sw[h][2] = b.x, sw[h][3] = b.y;
     }
   };
-  for (int64_t t = wave; t < work_tiles; t += nwaves) {
+  // VAR bit 3: ballots of the even (e) and odd (o) rows -> the tile's two row-order words
+  auto spread = [](uint64_t x) -> uint64_t {  // bit i -> bit 2i (32 -> 64 bits)
+    x &= 0xffffffffull;
+    x = (x | (x << 16)) & 0x0000ffff0000ffffull;
+    x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
+    x = (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    return (x | (x << 1)) & 0x5555555555555555ull;
+  };
+  auto rows_order = [&](unsigned long long& e, unsigned long long& o) {
+    const unsigned long long w0 = spread(e) | (spread(o) << 1), w1 = spread(e >> 32) | (spread(o >> 32) << 1);
+    e = w0, o = w1;
+  };
+  const uint32_t rest_b = __builtin_amdgcn_readfirstlane(fb_rest);
+  const int64_t per = (work_tiles + nwaves - 1) / nwaves;  // VAR bit 1: this wave's tile range
+  const int64_t t_beg = (VAR & 2) ? wave * per : wave;
+  const int64_t t_end = (VAR & 2) ? min(work_tiles, t_beg + per) : work_tiles;
+  const int64_t t_step = (VAR & 2) ? 1 : nwaves;
+  for (int64_t t = t_beg; t < t_end; t += t_step) {
     uint32_t sw[2][4];
     load(t, sw);
     __builtin_amdgcn_sched_barrier(0);
@@ -1176,11 +1225,39 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
-      for (int k = 0; k < 4; k++) lw[h][k] = *(lds_u32p)(size_t(min(ob[h][k], cw4)));
+      for (int k = 0; k < 4; k++) {
+        if (VAR & 4) {
+          lw[h][k] = 0u;
+          if (__ballot(ob[h][k] < cw4)) lw[h][k] = *(lds_u32p)(size_t(min(ob[h][k], cw4)));
+        } else {
+          lw[h][k] = *(lds_u32p)(size_t(min(ob[h][k], cw4)));
+        }
+      }
+    // VAR bit 5: rows already found through a hub word send no L2 probe (most found rows have
+    // a hub in-neighbour in the frontier: their slots' L2 probes were wasted instructions)
+    bool hubf[2] = {false, false};
+    if (VAR & 32) {
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t w = sw[h][k];
+          const bool pass = CLS == 1 ? w >= plo : (w - plo <= pr) != pinv;
+          hubf[h] = hubf[h] || (__builtin_amdgcn_ubfe(lw[h][k], w, 1u) != 0u && pass);
+        }
+    }
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
-      for (int k = 0; k < 4; k++) gw[h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, ob[h][k] - cw4, 0, 0);
+      for (int k = 0; k < 4; k++) {
+        if (VAR & 1) {
+          gw[h][k] = 0u;
+          if (__ballot(ob[h][k] - cw4 < rest_b && !hubf[h]))
+            gw[h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, hubf[h] ? 0xfffffff0u : ob[h][k] - cw4, 0, 0);
+        } else {
+          gw[h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, ob[h][k] - cw4, 0, 0);
+        }
+      }
     __builtin_amdgcn_sched_barrier(0);
     bool f[2], pend[2];
 #pragma unroll
@@ -1199,9 +1276,22 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
       // (slot 3 set)
       pend[h] = !fh && (ah || sw[h][3] != 0xffffffffu);
     }
-    const unsigned long long f0 = __ballot(f[0]), f1 = __ballot(f[1]);
-    const unsigned long long p0 = __ballot(pend[0]), p1 = __ballot(pend[1]);
-    if (lane < 2) {
+    unsigned long long f0 = __ballot(f[0]), f1 = __ballot(f[1]);
+    unsigned long long p0 = __ballot(pend[0]), p1 = __ballot(pend[1]);
+    if (VAR & 8) {
+      rows_order(f0, f1);
+      rows_order(p0, p1);
+    }
+    if (VAR & 16) {
+      // one store instruction: lane 0 the two next-frontier words, lane 1 the two pending words
+      if (lane < 2) {
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        u64x2 v;
+        v.x = lane ? p0 : f0;
+        v.y = lane ? p1 : f1;
+        *reinterpret_cast<u64x2*>((lane ? pbits : nbits) + 2 * t) = v;
+      }
+    } else if (lane < 2) {
       nbits[2 * t + lane] = lane ? f1 : f0;
       pbits[2 * t + lane] = lane ? p1 : p0;
     }
@@ -1251,7 +1341,8 @@ template <int PK, int W, int HUB, int REC>
 __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long long* __restrict__ pbits, int64_t n,
                                                           const int64_t* __restrict__ trp,
                                                           const int32_t* __restrict__ tcol,
-                                                          const uint32_t* __restrict__ fbits, unsigned long long* nbits,
+                                                          const uint32_t* __restrict__ fbits, uint32_t fb_bytes,
+                                                          unsigned long long* nbits,
                                                           const uint32_t* __restrict__ odeg, FastArgs fp, QArgs q_arg,
                                                           unsigned long long* partials, int cw, int ru, int rest_from,
                                                           int steps, unsigned long long* dbg,
@@ -1267,7 +1358,8 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
   const unsigned long long t_hub = wall_clock64();
   uint32_t d_rows = 0, d_batches = 0, d_steps = 0, d_scan = 0;
   unsigned long long t_scan = 0;
-  const __amdgpu_buffer_rsrc_t fb_rs = raw_rsrc(fbits);
+  const __amdgpu_buffer_rsrc_t fb_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(fbits), 0, int(__builtin_amdgcn_readfirstlane(fb_bytes)), 0x00020000);
   auto in_front = [&](int32_t g) -> bool {
     const int32_t wi = g >> 5;
     uint32_t w;
@@ -2479,8 +2571,13 @@ FinArgs fin_args(const QArgs& q) {
 // non-final hop: odeg keeps found rows with out-edges and sums their degrees) or PK_FAST (the
 // final hop's typed compare on transposed column fcol; decided from the packed buckets when fcol
 // is the packed column, else every value of a frontier hit is read by the rest pass).
+// hop_front: the frontier came out of a hop (not the starts), so on one rank with the
+// class-ordered numbering (snapshot k_class_key) its bits lie below row bu_both_tiles * 128: a
+// frontier vertex has an in-edge (it was found) and an out-edge (the hops keep only those).
+// Probes past that bound are out of bounds of their buffer resource (the hardware answers 0
+// without a memory access).
 size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
-                      const FastArgs& fp, int fcol, unsigned long long* out,
+                      const FastArgs& fp, int fcol, unsigned long long* out, bool hop_front,
                       const unsigned long long* gate = nullptr) {
   const Csr& tr = es.tr;
   if (pk != PK_NONE && pk != PK_FAST) throw Error(NBG_E_DEVICE, "bottom-up hop with a VM predicate");
@@ -2515,7 +2612,9 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
       1, std::min<int64_t>((waves + bs / 64 - 1) / (bs / 64),
                            std::min<int64_t>(cw > 0 ? 512 : c.opt("bu_lean_grid", 2048), kAggBlocks / 2))));
   const size_t shm = size_t(cw + 1) * 4;  // + the zero word non-hub probes read
-  const uint32_t fb_bytes = uint32_t(fb_words * 4);
+  uint32_t fb_bytes = uint32_t(fb_words * 4);
+  if (hop_front && c.world == 1 && es.bu_both_tiles > 0 && c.opt("bu_fb_bound", 1) != 0)
+    fb_bytes = uint32_t(std::min<int64_t>(fb_bytes, (es.bu_both_tiles * 128 + 31) / 32 * 4));
   const int probe_stats = int(c.opt("bu_probe_stats", 0));  // partials [6] / [7]
   c.ws_pend.ensure(size_t(ntiles * 2 + 2) * 8);  // the pending bits, 2 words per tile
   unsigned long long* pbits = c.ws_pend.as<unsigned long long>();
@@ -2532,8 +2631,10 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   };
   int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
   if (sel == 2 && c.opt("bu_lean_nt", 1) != 0 && (fast || es.odeg8.p)) sel = 6;  // non-temporal, 1 B degrees
+  if (sel == 6 && c.opt("bu_lean_skip", 0) != 0) sel = 7;                        // + probe skip
 #define NBG_LEAN(PKV)                                \
   switch (sel) {                                     \
+    case 7: go(k_bu_lean<PKV, 1, 1, 0, 1, 1>); break; \
     case 6: go(k_bu_lean<PKV, 1, 1, 0, 1>); break;   \
     case 0: go(k_bu_lean<PKV, 1, 0, 0>); break;      \
     case 1: go(k_bu_lean<PKV, 2, 0, 0>); break;      \
@@ -2556,13 +2657,25 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
       kern<<<grid, bs, fshm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, fa, partials, cw, rest, gate);
     };
     const int nt = int(c.opt("bu_fin_nt", 1) != 0);
-    switch ((cls1 ? 1 : 0) | nt << 1) {
+    const int var = cls1 && nt ? int(c.opt("bu_fin_var", 0) & 63) : 0;
+    switch ((cls1 ? 1 : 0) | nt << 1 | var << 2) {
       case 0: gof(k_bu_fin<0, 0>); break;
       case 1: gof(k_bu_fin<1, 0>); break;
       case 2: gof(k_bu_fin<0, 1>); break;
-      default: gof(k_bu_fin<1, 1>); break;
+      case 3: gof(k_bu_fin<1, 1>); break;
+      case 3 | 4: gof(k_bu_fin<1, 1, 1>); break;
+      case 3 | 8: gof(k_bu_fin<1, 1, 2>); break;
+      case 3 | 12: gof(k_bu_fin<1, 1, 3>); break;
+      case 3 | 16: gof(k_bu_fin<1, 1, 4>); break;
+      case 3 | 20: gof(k_bu_fin<1, 1, 5>); break;
+      case 3 | 36: gof(k_bu_fin<1, 1, 9>); break;
+      case 3 | 32: gof(k_bu_fin<1, 1, 8>); break;
+      case 3 | 68: gof(k_bu_fin<1, 1, 17>); break;
+      case 3 | 132: gof(k_bu_fin<1, 1, 33>); break;
+      case 3 | 196: gof(k_bu_fin<1, 1, 49>); break;
+      default: gof(k_bu_fin<1, 1, 7>); break;
     }
-    snprintf(fin_nm, sizeof fin_nm, "nbg::k_bu_fin<%d, %d>", cls1 ? 1 : 0, nt);
+    snprintf(fin_nm, sizeof fin_nm, "nbg::k_bu_fin<%d, %d, %d>", cls1 ? 1 : 0, nt, var);
   } else if (fast) {
     NBG_LEAN(PK_FAST)
   } else {
@@ -2598,8 +2711,8 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   auto rest = [&](auto kern) {
     if (rshm > 48 * 1024)
       lds_limit(reinterpret_cast<const void*>(kern), rshm);
-    kern<<<grid2, 1024, rshm, c.stream>>>(pbits, rest_rows, trp, tc, fb, nb, odeg, fp, q, partials + grid, rcw, ru,
-                                          rest_from, rsteps, dbg, gate, rec);
+    kern<<<grid2, 1024, rshm, c.stream>>>(pbits, rest_rows, trp, tc, fb, fb_bytes, nb, odeg, fp, q, partials + grid,
+                                          rcw, ru, rest_from, rsteps, dbg, gate, rec);
   };
 #define NBG_REST(PKV, WV)                                                 \
   if (rcw > 0) {                                                          \
@@ -2641,7 +2754,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     snprintf(nm, sizeof nm, "%s", fin_nm);
   else
     snprintf(nm, sizeof nm, "nbg::k_bu_lean<%d, %d, %d, %d%s>", pk, probe_stats ? 1 : U, cw > 0 ? 1 : 0,
-             probe_stats ? 1 : 0, sel == 6 ? ", 1" : "");
+             probe_stats ? 1 : 0, sel == 7 ? ", 1, 1" : sel == 6 ? ", 1, 0" : ", 0, 0");
   c.bu_kernel_name = nm;
   const int wn = fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0;
   snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d, %d>", pk, wn, rcw > 0 ? 1 : 0, use_rec ? 1 : 0);
@@ -3081,11 +3194,11 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const size_t ia = timing_event(c);
       size_t ik;
       if (!fin) {
-        ik = launch_bu_lean(c, es, fb, outb, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, blk, blk + 8);
+        ik = launch_bu_lean(c, es, fb, outb, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, blk, true, blk + 8);
       } else {
         FastArgs tfp = fp0;
         if (fpk0.kind == PK_FAST) tfp.data = es.tr.props[size_t(fpk0.col)].data.p;
-        ik = launch_bu_lean(c, es, fb, outb, nullptr, fpk0.kind, tfp, fpk0.kind == PK_FAST ? fpk0.col : -1, blk,
+        ik = launch_bu_lean(c, es, fb, outb, nullptr, fpk0.kind, tfp, fpk0.kind == PK_FAST ? fpk0.col : -1, blk, true,
                             blk + 8);
         spec_vids.alloc(size_t(c.n_global + 64) * 8);
         launch_bits_vids(c, outb, es.tr.n_rows, lo, spec_vids.p, blk + 9, blk + 8);
@@ -3216,7 +3329,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const Csr& tr = es.tr;
       const uint32_t* fb = global_bits(c, bitsA);
       const size_t ia = timing_event(c);
-      const size_t ik = launch_bu_lean(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, K.d);
+      const size_t ik = launch_bu_lean(c, es, fb, bitsB, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, K.d, step > 1);
       const size_t ib = timing_event(c);
       c.tpend.push_back(Ctx::PendingTime{ia, ib, c.timing.n_hops, 0});
       c.tpend.push_back(Ctx::PendingTime{ia, ik, c.timing.n_hops, 1});
@@ -3348,7 +3461,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         NBG_HIP(hipMemsetAsync(K.d, 0, 8, c.stream));
         const uint32_t* fb = global_bits(c, bitsA);
         const size_t ia = timing_event(c);
-        const size_t ik = launch_bu_lean(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8);
+        const size_t ik =
+            launch_bu_lean(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8, s.steps > 1);
         launch_bits_vids(c, bitsB, tr.n_rows, lo, vids.p, K.d, nullptr);
         NBG_HIP(hipGetLastError());
         const size_t ib = timing_event(c);
