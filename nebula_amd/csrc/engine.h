@@ -510,6 +510,8 @@ struct Ctx {
     DevBuf live[2], live_next[2], arena, meet, sweep[2], X, Xdeg, Xoff, state, cnt, vids, gidx, plist;
     DevBuf tile_rows;  // k_sp_expand: X entry of each tile's first slot
     DevBuf lvbits;     // per side and depth, the vertices some pair of the batch holds there
+    DevBuf htab[2];    // option sp_hash: per side (pair, vertex) -> depth maps (paths.hip)
+    int64_t hcap = 0;
     int64_t cap_live[2] = {0, 0}, cap_next[2] = {0, 0}, cap_arena = 0, cap_meet = 0, cap_sweep[2] = {0, 0};
     int64_t cap_x = 0, cap_state = 0, cap_plist = 0;
   } sp;

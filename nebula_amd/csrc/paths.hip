@@ -91,8 +91,23 @@ struct SpState {  // per-pair arrays, B entries each
   uint32_t* lvbits;
   int64_t lvw;
   uint32_t lvmask;
+  // sparse distance maps (option sp_hash, null: the dense byte arrays): per side, open-addressing
+  // (pair, vertex) -> depth over 64-bit words, hmask + 1 slots, sized to the batch's claims (a
+  // few million per side at RMAT-26, tens of MB that stay in the Infinity Cache and in a handful
+  // of TLB pages; the dense arrays are 2 * B * n bytes read at random lines)
+  uint64_t* htab[2];
+  uint64_t hmask;
 };
 constexpr int kLv = 8;
+
+// hash map words: bits [0, 31) vertex, [31, 54) pair, [54, 62) depth; all ones = empty
+constexpr uint64_t kHEmpty = ~0ull;
+constexpr uint64_t kHKey = (1ull << 54) - 1;
+__device__ inline uint64_t hkey(uint32_t p, uint32_t v) { return (uint64_t(p) << 31) | uint64_t(v); }
+__device__ inline uint64_t hslot(uint64_t key, uint64_t mask) {
+  uint64_t x = key * 0x9E3779B97F4A7C15ull;
+  return (x ^ (x >> 29)) & mask;
+}
 
 __device__ inline void lv_mark(const SpState& st, uint32_t side, uint32_t l, uint32_t v) {
   if (st.lvbits && l >= 1 && l < uint32_t(kLv))
@@ -165,6 +180,37 @@ __device__ inline bool claim_byte(uint8_t* base, uint64_t idx, uint32_t val) {
   return false;
 }
 
+// the depth of vertex v for pair p on a side (0xFF: unseen), from the dense bytes or the map
+__device__ inline uint32_t dist_get(const SpState& st, const uint8_t* dense, uint32_t side, uint32_t p, uint32_t v,
+                                    int64_t n, bool fresh = false) {
+  if (!st.htab[0]) {
+    const uint8_t* a = dense + didx(st, p, v, n);
+    return fresh ? uint32_t(*reinterpret_cast<volatile const uint8_t*>(a)) : uint32_t(*a);
+  }
+  const uint64_t* T = st.htab[side];
+  const uint64_t key = hkey(p, v);
+  for (uint64_t h = hslot(key, st.hmask);; h = (h + 1) & st.hmask) {
+    const uint64_t e = fresh ? __hip_atomic_load(T + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : T[h];
+    if (e == kHEmpty) return 0xFFu;
+    if ((e & kHKey) == key) return uint32_t(e >> 54) & 0xFFu;
+  }
+}
+// claim the unseen (p, v) on a side with depth val: true for exactly one caller
+__device__ inline bool dist_claim(const SpState& st, uint8_t* dense, uint32_t side, uint32_t p, uint32_t v, int64_t n,
+                                  uint32_t val) {
+  if (!st.htab[0]) return claim_byte(dense, didx(st, p, v, n), val);
+  uint64_t* T = st.htab[side];
+  const uint64_t key = hkey(p, v), word = key | (uint64_t(val & 0xFFu) << 54);
+  for (uint64_t h = hslot(key, st.hmask);; h = (h + 1) & st.hmask) {
+    uint64_t e = T[h];
+    if (e == kHEmpty) {
+      e = atomicCAS(reinterpret_cast<unsigned long long*>(T + h), (unsigned long long)kHEmpty, (unsigned long long)word);
+      if (e == kHEmpty) return true;
+    }
+    if ((e & kHKey) == key) return false;
+  }
+}
+
 // zero the counter slots in `mask` (bit i = cnt[i]; one launch instead of a memset per slot run)
 // and, when xdeg is given, the X degree sentinel xdeg[0] the scan reads past the list
 __global__ void k_cnt_zero(unsigned long long* cnt, uint32_t mask, int64_t* xdeg) {
@@ -190,8 +236,8 @@ __global__ void k_sp_init(const int64_t* svid, const int64_t* tvid, const int32_
     st.state[p] = go ? SP_ACTIVE : SP_DONE;
     st.deg[p] = st.deg[B + p] = 0;
     if (go) {
-      d0[didx(st, uint32_t(p), uint32_t(a), n)] = 0;
-      d1[didx(st, uint32_t(p), uint32_t(b), n)] = 0;
+      dist_claim(st, d0, 0, uint32_t(p), uint32_t(a), n, 0);
+      dist_claim(st, d1, 1, uint32_t(p), uint32_t(b), n, 0);
       st.deg[p] = (unsigned long long)sp_deg(gout, uint32_t(a)) + 1;
       st.deg[B + p] = (unsigned long long)sp_deg(gin, uint32_t(b)) + 1;
     }
@@ -532,9 +578,8 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
     uint32_t bt[kIt];
 #pragma unroll
     for (int r = 0; r < kIt; r++) {
-      const uint32_t side = t_side(tus[r]);
-      const uint8_t* d = a.sweep ? a.dist[side ^ 1u] : a.dist[side];
-      bt[r] = lv[r] ? uint32_t(d[didx(st, t_pair(tus[r]), ws[r], a.n)]) : 0x1FFu;
+      const uint32_t side = t_side(tus[r]), ds = a.sweep ? side ^ 1u : side;
+      bt[r] = lv[r] ? dist_get(st, a.dist[ds], ds, t_pair(tus[r]), ws[r], a.n) : 0x1FFu;
     }
 #pragma unroll
     for (int r = 0; r < kIt; r++) {
@@ -544,19 +589,18 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
       const uint32_t w = ws[r];
       bool claimed = false;
       if (valid) {
-        const uint64_t idx = didx(st, p, w, a.n);
         if (!a.sweep) {
-          claimed = bt[r] == 0xFFu && claim_byte(a.dist[side], idx, l + 1);
+          claimed = bt[r] == 0xFFu && dist_claim(st, a.dist[side], side, p, w, a.n, l + 1);
           if (claimed) lv_mark(st, side, l + 1, w);
         } else if (side == 1) {  // pull: in-neighbour w of a level-(k+1) vertex, forward depth k
           if (bt[r] == uint32_t(need[r])) {
-            claimed = claim_byte(a.dist[1], idx, l + 1);
+            claimed = dist_claim(st, a.dist[1], 1, p, w, a.n, l + 1);
             if (claimed) lv_mark(st, 1, l + 1, w);
           }
         } else {  // push: the tuple's own vertex u (forward depth l) if out-neighbour w is on a path
           const uint32_t u = t_row(tu);
           if (bt[r] == uint32_t(need[r])) {
-            claimed = claim_byte(a.dist[1], didx(st, p, u, a.n), uint32_t(need[r] + 1));
+            claimed = dist_claim(st, a.dist[1], 1, p, u, a.n, uint32_t(need[r] + 1));
             if (claimed) lv_mark(st, 1, uint32_t(need[r] + 1), u);
           }
         }
@@ -574,8 +618,8 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
       bool meet = false;
       uint32_t dt = 0;
       if (claimed) {
-        const uint8_t o = a.dist[side ^ 1][didx(st, p, w, a.n)];
-        if (o != 0xFF) {
+        const uint32_t o = dist_get(st, a.dist[side ^ 1], side ^ 1u, p, w, a.n);
+        if (o != 0xFFu) {
           meet = true;
           dt = side ? l + 1 : uint32_t(o);
           st.met[p] = 1;
@@ -674,9 +718,8 @@ __global__ __launch_bounds__(256) void k_sp_sweep(const uint64_t* __restrict__ X
     const int64_t x0 = rp[row] + (c - choff[a]) * kSwCh;
     const int64_t x1 = min(x0 + int64_t(kSwCh), rp[row + 1]);
     const int32_t need = st.res[p] - int32_t(l) - 1;  // the other side's depth a neighbour needs
-    const uint64_t ui = didx(st, p, row, n);
     for (int64_t x = x0; x < x1; x += 64 * kProbeU) {
-      if (side == 0 && *reinterpret_cast<volatile const uint8_t*>(d1 + ui) != 0xFF) break;  // u claimed
+      if (side == 0 && dist_get(st, d1, 1, p, row, n, true) != 0xFFu) break;  // u claimed
       uint32_t w[kProbeU];
 #pragma unroll
       for (int u = 0; u < kProbeU; u++) {
@@ -689,13 +732,13 @@ __global__ __launch_bounds__(256) void k_sp_sweep(const uint64_t* __restrict__ X
         f[u] = w[u] != 0xFFFFFFFFu && need >= 0 && lv_maybe(st, side ^ 1u, need, w[u]);
       uint32_t b[kProbeU];
 #pragma unroll
-      for (int u = 0; u < kProbeU; u++) b[u] = f[u] ? uint32_t((side ? d0 : d1)[didx(st, p, w[u], n)]) : 0x1FFu;
+      for (int u = 0; u < kProbeU; u++) b[u] = f[u] ? dist_get(st, side ? d0 : d1, side ^ 1u, p, w[u], n) : 0x1FFu;
       if (side == 1) {
 #pragma unroll
         for (int u = 0; u < kProbeU; u++) {
           bool claimed = false;
           if (b[u] == uint32_t(need)) {
-            claimed = claim_byte(d1, didx(st, p, w[u], n), l + 1);
+            claimed = dist_claim(st, d1, 1, p, w[u], n, l + 1);
             if (claimed) lv_mark(st, 1, l + 1, w[u]);
           }
           stage(claimed, mk_tup(1, p, l + 1, w[u]));
@@ -707,7 +750,7 @@ __global__ __launch_bounds__(256) void k_sp_sweep(const uint64_t* __restrict__ X
         if (__ballot(hit)) {
           bool claimed = false;
           if (lane == 0) {
-            claimed = claim_byte(d1, ui, uint32_t(need + 1));
+            claimed = dist_claim(st, d1, 1, p, row, n, uint32_t(need + 1));
             if (claimed) lv_mark(st, 1, uint32_t(need + 1), row);
           }
           stage(claimed, mk_tup(1, p, uint32_t(need + 1), row));
@@ -766,12 +809,11 @@ __global__ __launch_bounds__(256) void k_sp_probe(const uint64_t* __restrict__ X
     const uint32_t other = side ^ 1u;
     const uint32_t need = uint32_t(st.lvl[other * uint32_t(st.B) + p]);
     uint8_t* od = other ? d1 : d0;
-    const uint64_t ci = didx(st, p, row, n);
     // kProbeU entries per lane a step: their column loads, then their filter bits, then their
     // distance bytes, each group in flight together (one entry per lane a step waited on three
     // dependent loads per 64 entries)
     for (int64_t x = x0; x < x1; x += 64 * kProbeU) {
-      if (*reinterpret_cast<volatile const uint8_t*>(od + ci) != 0xFF) break;
+      if (dist_get(st, od, other, p, row, n, true) != 0xFFu) break;
       uint32_t w[kProbeU];
 #pragma unroll
       for (int u = 0; u < kProbeU; u++) {
@@ -785,10 +827,10 @@ __global__ __launch_bounds__(256) void k_sp_probe(const uint64_t* __restrict__ X
 #pragma unroll
       for (int u = 0; u < kProbeU; u++) {
         examined += w[u] != 0xFFFFFFFFu ? 1 : 0;
-        hit = (f[u] && od[didx(st, p, w[u], n)] == uint8_t(need)) || hit;
+        hit = (f[u] && dist_get(st, od, other, p, w[u], n) == need) || hit;
       }
       if (__ballot(hit)) {
-        if (lane == 0 && claim_byte(od, ci, need + 1)) {
+        if (lane == 0 && dist_claim(st, od, other, p, row, n, need + 1)) {
           lv_mark(st, other, need + 1, row);
           st.met[p] = 1;
           slot[c] = mk_tup(other, p, need + 1, row);
@@ -877,7 +919,7 @@ __global__ __launch_bounds__(kWalkT) void k_sp_walk(SpState st, const int32_t* g
       const int64_t e1 = gout.row_ptr[v + 1];
       for (int64_t e = gout.row_ptr[v] + threadIdx.x; e < e1; e += kWalkT) {
         const int64_t w = int64_t(gout.col[e]) - lo;
-        if (db[didx(st, uint32_t(p), uint64_t(w), n)] == need) {
+        if (dist_get(st, db, 1, uint32_t(p), uint32_t(w), n) == need) {
           const int64_t vv = vid_of[lo + w];
           if (vv < best) {
             best = vv;
@@ -1010,7 +1052,7 @@ __global__ __launch_bounds__(kT) void k_sp_walk_scan(SpState st, int32_t i, cons
 #pragma unroll
     for (int r = 0; r < kIt; r++) hit[r] = ws[r] != 0xFFFFFFFFu && lv_maybe(st, 1, need[r], ws[r]);
 #pragma unroll
-    for (int r = 0; r < kIt; r++) hit[r] = hit[r] && dist_b[didx(st, ps[r], ws[r], n)] == uint8_t(need[r]);
+    for (int r = 0; r < kIt; r++) hit[r] = hit[r] && dist_get(st, dist_b, 1, ps[r], ws[r], n) == uint32_t(need[r]);
     long long cand[kIt];
 #pragma unroll
     for (int r = 0; r < kIt; r++) cand[r] = hit[r] ? vid_of[lo + ws[r]] : LLONG_MAX;
@@ -1034,6 +1076,51 @@ __global__ void k_sp_walk_pick(SpState st, int32_t i, int32_t* cur, const long l
   }
   path[path_off[p] + i + 1] = int64_t(b);
   cur[p] = ht_lookup(ht_keys, ht_vals, ht_mask, int64_t(b), ht_has_min, ht_min_gidx) - int32_t(lo);
+}
+
+// sparse maps: RG_* list rebuilds from the map words of the listed pairs (pflag[p] = 1)
+__global__ void k_sp_regen_hash(int mode, int side, int32_t j, const uint8_t* pflag, SpState st, int64_t n,
+                                uint64_t* out, int64_t cap, unsigned long long* cnt, int which) {
+  const int32_t B = st.B;
+  const uint64_t* T = st.htab[mode == RG_LIVE ? side : 1];
+  const int64_t slots = int64_t(st.hmask) + 1;
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int64_t rounds = (slots + stride - 1) / stride;
+  for (int64_t r = 0; r < rounds; r++) {
+    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    bool hit = false;
+    uint32_t p = 0, v = 0, d = 0;
+    if (i < slots) {
+      const uint64_t e = T[i];
+      if (e != kHEmpty) {
+        p = uint32_t(e >> 31) & 0x7FFFFFu;
+        v = uint32_t(e & 0x7FFFFFFFu);
+        d = uint32_t(e >> 54) & 0xFFu;
+        if (int32_t(p) < B && pflag[p]) {
+          if (mode == RG_LIVE) hit = d == uint32_t(st.lvl[side * B + p]);
+          else if (mode == RG_MEET)
+            hit = d == uint32_t(st.lvl[B + p]) && dist_get(st, nullptr, 0, p, v, n) == uint32_t(st.lvl[p]);
+          else hit = d == uint32_t(st.lvl[B + p] + j);
+        }
+      }
+    }
+    put(out, cap, cnt, which, hit, mk_tup(mode == RG_LIVE ? uint32_t(side) : 1u, p, d, v));
+  }
+}
+__global__ void k_set_flags(const int32_t* plist, int32_t np, uint8_t* flag) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < np) flag[plist[i]] = 1;
+}
+// grow a map: every word of the old table inserted into the new one (same key -> slot rule)
+__global__ void k_hash_rehash(const uint64_t* old, int64_t nold, uint64_t* nt, uint64_t nmask) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < nold; i += int64_t(gridDim.x) * blockDim.x) {
+    const uint64_t e = old[i];
+    if (e == kHEmpty) continue;
+    for (uint64_t h = hslot(e & kHKey, nmask);; h = (h + 1) & nmask)
+      if (atomicCAS(reinterpret_cast<unsigned long long*>(nt + h), (unsigned long long)kHEmpty, (unsigned long long)e) ==
+          kHEmpty)
+        break;
+  }
 }
 
 // reset every claimed distance byte of the batch
@@ -1173,7 +1260,10 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(int64_t(npairs), 1)));
   B = std::min<int64_t>(B, 0x7FFFFF);
   const size_t dist_bytes = ((size_t(B) * size_t(n) + 3) & ~size_t(3)) + 64;
-  {
+  // option sp_hash: sparse (pair, vertex) -> depth maps sized to the claims instead of the dense
+  // 2 * B * n byte arrays
+  const bool hash = c.opt("sp_hash", 0) != 0;
+  if (!hash) {
     PoolScope none(nullptr);  // the distance arrays live outside the query pool
     if (c.sp_dist_bytes < dist_bytes) {
       for (auto& d : c.sp_dist) d.release();
@@ -1200,8 +1290,34 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   c.timing = Timing{};
   hipEventRecord(c.ev[0], c.stream);
 
-  uint8_t* d0 = c.sp_dist[0].as<uint8_t>();
-  uint8_t* d1 = c.sp_dist[1].as<uint8_t>();
+  uint8_t* d0 = hash ? nullptr : c.sp_dist[0].as<uint8_t>();
+  uint8_t* d1 = hash ? nullptr : c.sp_dist[1].as<uint8_t>();
+  // the maps: at most half full (linear probing); grown (rehashed) before a launch whose claims
+  // could pass that, from a bound on them -- the claims so far plus the launch's entries
+  // (expansion), chunks (meet probe) or the claims so far again (a sweep claims only vertices the
+  // forward search holds)
+  auto hash_fit = [&](SpState& st, int64_t claims) {
+    if (!hash) return;
+    int64_t cap = std::max<int64_t>(W.hcap, int64_t(1) << std::min<int64_t>(30, std::max<int64_t>(10, c.opt("sp_hash_log2", 22))));
+    while (cap < 2 * claims + 64) cap <<= 1;
+    if (cap != W.hcap || !W.htab[0].p) {
+      PoolScope none(nullptr);
+      for (int sd = 0; sd < 2; sd++) {
+        DevBuf nt;
+        nt.alloc(size_t(cap) * 8);
+        NBG_HIP(hipMemsetAsync(nt.p, 0xFF, size_t(cap) * 8, c.stream));
+        if (W.htab[sd].p && W.hcap > 0)
+          k_hash_rehash<<<grid_n(W.hcap), 256, 0, c.stream>>>(W.htab[sd].as<uint64_t>(), W.hcap, nt.as<uint64_t>(),
+                                                               uint64_t(cap - 1));
+        NBG_HIP(hipGetLastError());
+        W.htab[sd] = std::move(nt);
+      }
+      W.hcap = cap;
+    }
+    st.htab[0] = W.htab[0].as<uint64_t>();
+    st.htab[1] = W.htab[1].as<uint64_t>();
+    st.hmask = uint64_t(W.hcap - 1);
+  };
   SpCsr gout{cout->row_ptr.as<int64_t>(), cout->col.as<int32_t>(), cout->row_ok.as<uint8_t>()};
   SpCsr gin{cin->row_ptr.as<int64_t>(), cin->col.as<int32_t>(), cin->row_ok.as<uint8_t>()};
   const int64_t* vid_of = c.vid_of.as<int64_t>();
@@ -1217,11 +1333,14 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   std::vector<int64_t> hres(npairs), hoff(1, 0), hpath;
   std::vector<int32_t> hstate(static_cast<size_t>(B)), hres_b(static_cast<size_t>(B)),
       hside(static_cast<size_t>(B)), hmet(static_cast<size_t>(B));
+  if (hash && c.sp_dirty && W.hcap > 0)  // a failed call's claims
+    for (auto& t : W.htab) NBG_HIP(hipMemsetAsync(t.p, 0xFF, size_t(W.hcap) * 8, c.stream));
   c.sp_dirty = true;  // until the batch's bytes are reset
   for (size_t b0 = 0; b0 < npairs; b0 += size_t(B)) {
     const int64_t nb = std::min<int64_t>(B, int64_t(npairs - b0));
     SpState st{};
     st.B = int32_t(nb);
+    hash_fit(st, 2 * nb);
     st.deg = W.state.as<unsigned long long>();
     st.state = reinterpret_cast<int32_t*>(st.deg + 2 * nb);
     st.res = st.state + nb;
@@ -1358,6 +1477,16 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     };
     auto regen = [&](int mode, int side, int32_t j, int32_t np, uint64_t* outl, int64_t cap, int which) {
       if (np == 0) return;
+      if (hash) {
+        DevBuf flag;
+        flag.alloc(size_t(nb) + 64);
+        NBG_HIP(hipMemsetAsync(flag.p, 0, size_t(nb) + 64, c.stream));
+        k_set_flags<<<grid_n(np), 256, 0, c.stream>>>(W.plist.as<int32_t>(), np, flag.as<uint8_t>());
+        k_sp_regen_hash<<<grid_n(W.hcap), 256, 0, c.stream>>>(mode, side, j, flag.as<uint8_t>(), st, n, outl, cap, cnt,
+                                                              which);
+        NBG_HIP(hipGetLastError());
+        return;
+      }
       dim3 grid(unsigned(std::min<int64_t>((n + 255) / 256, 1024)), unsigned(std::min<int32_t>(np, 65535)));
       k_sp_regen<<<grid, 256, 0, c.stream>>>(mode, side, j, W.plist.as<int32_t>(), np, st, d0, d1, n, outl, cap, cnt,
                                              which);
@@ -1401,6 +1530,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       if (E > 0 && probe) {
         // meet probe: pairs one edge short of meeting skip this iteration's expansion
         const int64_t max_chunks = nX + E / kProbeCh + 64;
+        hash_fit(st, int64_t(hc[C_ARENA]) + max_chunks);
         reserve(c, W.meet, W.cap_meet, n_meet + max_chunks, n_meet);
         if (!arena_lost) reserve(c, W.arena, W.cap_arena, n_arena + max_chunks, n_arena);
         refresh(nullptr, 0);
@@ -1451,6 +1581,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         if (!arena_lost) reserve(c, W.arena, W.cap_arena, n_arena + want, n_arena);
         reserve(c, W.meet, W.cap_meet, n_meet + std::min<int64_t>(E, soft) + 64, n_meet);
         refresh(nullptr, 0);
+        hash_fit(st, int64_t(hc[C_ARENA]) + E);
         launch_scan(nX);
         launch_expand(nX, E, 0);
       }
@@ -1548,6 +1679,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         for (auto& kv : seen) diag[1] += uint64_t(kv.second);
       }
       c.timing.edges_scanned += uint64_t(E);
+      hash_fit(st, 2 * int64_t(hc[C_ARENA]));
       const int64_t want = std::min<int64_t>(E, soft) + 64;
       reserve(c, W.sweep[nxt], W.cap_sweep[nxt], want, 0);
       if (!arena_lost) reserve(c, W.arena, W.cap_arena, n_arena + want, n_arena);
@@ -1667,7 +1799,9 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     }
     for (int64_t p = 0; p < nb; p++) hoff.push_back(hoff.back() + boff[size_t(p) + 1] - boff[size_t(p)]);
     // reset the batch's distance bytes
-    if (arena_lost) {
+    if (hash) {
+      for (auto& t : W.htab) NBG_HIP(hipMemsetAsync(t.p, 0xFF, size_t(W.hcap) * 8, c.stream));
+    } else if (arena_lost) {
       const size_t used = ((size_t(nb) * size_t(n) + 3) & ~size_t(3)) + 64;
       for (auto& d : c.sp_dist) NBG_HIP(hipMemsetAsync(d.p, 0xFF, std::min(used, c.sp_dist_bytes), c.stream));
     } else if (n_arena) {

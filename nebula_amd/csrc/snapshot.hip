@@ -2241,6 +2241,121 @@ static void extend_vertex_map(Ctx& c, int64_t unknown_bound) {
   NBG_HIP(hipGetLastError());
 }
 
+// Merge commit with new vertices on several ranks.  Every rank sends the unknown endpoint vids
+// of its batch (sorted, unique) to all; the union, sorted, is the same on every rank, and each
+// owner's new vertices (vid % parts + 1 on rank part % world, pickHosts) take the next gidx of
+// its growth room in vid order -- every rank computes every assignment itself, so the
+// replicated vertex map and hash table stay identical without a second exchange.  Returns false
+// (on every rank alike) when some owner's room is too small: the caller then rebuilds fully.
+struct NewVertexPlan {
+  std::vector<int64_t> vids;  // the union, sorted
+  std::vector<std::vector<int64_t>> per_owner;
+};
+static bool plan_new_vertices_ranks(Ctx& c, int64_t unknown_bound, NewVertexPlan& plan) {
+  DevBuf raw, cnt;
+  raw.alloc(size_t(std::max<int64_t>(unknown_bound, 1)) * 8);
+  cnt.alloc(8);
+  NBG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
+  for (auto& kv : c.edges) {
+    EdgeSpace& es = kv.second;
+    for (int d = 0; d < 2; d++) {
+      const Staging& st = d ? es.in_stage : es.out_stage;
+      const int64_t n0 = es.ord[d].n;
+      if (st.n > n0)
+        k_collect_unknown<<<grid_for(st.n - n0), 256, 0, c.stream>>>(
+            st.src.as<int64_t>() + n0, st.dst.as<int64_t>() + n0, st.n - n0, c.ht_keys.as<int64_t>(),
+            c.ht_vals.as<int32_t>(), uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, raw.as<uint64_t>(),
+            cnt.as<unsigned long long>());
+    }
+  }
+  unsigned long long nraw = 0;
+  NBG_HIP(hipMemcpyAsync(&nraw, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  if (int64_t(nraw) > unknown_bound) throw Error(NBG_E_UNKNOWN, "merge commit: unknown-vertex count changed");
+  int64_t k = 0;
+  DevBuf sorted, uniq;
+  sorted.alloc(size_t(std::max<uint64_t>(nraw, 1)) * 8);
+  uniq.alloc(size_t(std::max<uint64_t>(nraw, 1)) * 8);
+  if (nraw) {
+    radix_keys<uint64_t>(c, raw.as<uint64_t>(), sorted.as<uint64_t>(), int64_t(nraw), 64);
+    k = unique_sorted<uint64_t>(c, sorted.as<uint64_t>(), uniq.as<uint64_t>(), int64_t(nraw));
+  }
+  // every rank's list to every rank
+  const size_t G = size_t(c.world);
+  DevBuf dk, dall;
+  dk.alloc(8);
+  dall.alloc(8 * G);
+  NBG_HIP(hipMemcpyAsync(dk.p, &k, 8, hipMemcpyHostToDevice, c.stream));
+  comm_allgather_bytes(c, dk.p, 8, dall.p);
+  std::vector<int64_t> ks(G);
+  NBG_HIP(hipMemcpyAsync(ks.data(), dall.p, 8 * G, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  std::vector<size_t> rb(G), ro(G);
+  size_t tot = 0;
+  for (size_t r = 0; r < G; r++) {
+    rb[r] = size_t(ks[r]) * 8;
+    ro[r] = tot;
+    tot += rb[r];
+  }
+  DevBuf recv;
+  recv.alloc(std::max<size_t>(tot, 8));
+  comm_allgatherv_bytes(c, uniq.p, size_t(k) * 8, recv.p, rb.data(), ro.data());
+  std::vector<uint64_t> flipped(tot / 8);
+  if (tot) NBG_HIP(hipMemcpyAsync(flipped.data(), recv.p, tot, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));
+  std::sort(flipped.begin(), flipped.end());
+  flipped.erase(std::unique(flipped.begin(), flipped.end()), flipped.end());
+  plan.vids.resize(flipped.size());
+  plan.per_owner.assign(G, {});
+  for (size_t i = 0; i < flipped.size(); i++) {  // sign-flipped order = signed vid order
+    const int64_t v = int64_t(flipped[i] ^ (1ull << 63));
+    plan.vids[i] = v;
+    plan.per_owner[size_t(dev_owner(v, c.num_parts, c.world))].push_back(v);
+  }
+  for (size_t q = 0; q < G; q++)
+    if (c.counts[q] + int64_t(plan.per_owner[q].size()) > c.base[q + 1] - c.base[q]) return false;
+  return true;
+}
+
+// applies a plan: each owner's new vertices at base + counts onward, in the replicated vertex map
+// and hash table; bytewise ranks recomputed and the committed sort keys re-read their dst rank
+static void extend_vertex_map_ranks(Ctx& c, const NewVertexPlan& plan) {
+  DevBuf dmin, dv;
+  dmin.alloc(4);
+  int32_t neg = -1;
+  NBG_HIP(hipMemcpyAsync(dmin.p, &neg, 4, hipMemcpyHostToDevice, c.stream));
+  dv.alloc(std::max<size_t>(plan.vids.size(), 1) * 8);
+  size_t off = 0;
+  for (size_t q = 0; q < plan.per_owner.size(); q++) {
+    const auto& l = plan.per_owner[q];
+    if (l.empty()) continue;
+    const int64_t g0 = c.base[q] + c.counts[q];
+    NBG_HIP(hipMemcpyAsync(dv.as<int64_t>() + off, l.data(), l.size() * 8, hipMemcpyHostToDevice, c.stream));
+    NBG_HIP(hipMemcpyAsync(c.vid_of.as<int64_t>() + g0, dv.as<int64_t>() + off, l.size() * 8, hipMemcpyDeviceToDevice,
+                           c.stream));
+    k_ht_insert<<<grid_for(int64_t(l.size())), 256, 0, c.stream>>>(c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
+                                                                   uint64_t(c.ht_cap - 1), dv.as<int64_t>() + off,
+                                                                   int64_t(l.size()), g0, dmin.as<int32_t>());
+    off += l.size();
+  }
+  int32_t mg = -1;
+  NBG_HIP(hipMemcpyAsync(&mg, dmin.p, 4, hipMemcpyDeviceToHost, c.stream));
+  NBG_HIP(hipStreamSynchronize(c.stream));  // (the host lists are pageable)
+  if (mg >= 0) {
+    c.ht_has_min = true;
+    c.ht_min_gidx = mg;
+  }
+  for (size_t q = 0; q < plan.per_owner.size(); q++) c.counts[q] += int64_t(plan.per_owner[q].size());
+  c.n_vertices += int64_t(plan.vids.size());
+  c.brank = bytewise_ranks(c);
+  for (auto& kv : c.edges)
+    for (auto& o : kv.second.ord)
+      if (o.n > 0 && o.skey.p)
+        k_rekey<<<grid_for(o.n), 256, 0, c.stream>>>(o.skey.as<uint64_t>(), o.dstg.as<int32_t>(), o.n,
+                                                    c.brank.as<uint32_t>());
+  NBG_HIP(hipGetLastError());
+}
+
 static bool commit_merge(Ctx& c) {
   // several ranks: the choice is collective (every rank merges or every rank rebuilds), agreed by
   // one sum over the ranks' flags below; the option and c.brank (writable) agree on every rank
@@ -2274,9 +2389,10 @@ static bool commit_merge(Ctx& c) {
     // new vertices extend the numbering (extend_vertex_map); every CSR direction then needs
     // rows for them, which the merge builds only where the batch has tuples: other batches
     // (and the off switch) take the full rebuild
+    // (several ranks: the new vertices land in rows every CSR already has, the growth room)
     if (c.opt("merge_new_vertices", 1) == 0) refuse = true;
     for (auto& kv : c.edges)
-      for (int d = 0; d < 2; d++)
+      for (int d = 0; d < 2 && c.world == 1; d++)
         if ((d ? kv.second.in_stage.n : kv.second.out_stage.n) == kv.second.ord[d].n) refuse = true;
   }
   // per edge space: did this rank's out / in CSR change (a rank without writes of its own still
@@ -2298,9 +2414,13 @@ static bool commit_merge(Ctx& c) {
     comm_allreduce_sum_i64(c, f.as<int64_t>(), flags.size());
     NBG_HIP(hipMemcpyAsync(flags.data(), f.p, flags.size() * 8, hipMemcpyDeviceToHost, c.stream));
     NBG_HIP(hipStreamSynchronize(c.stream));
-    // new vertices would move every later rank's gidx range: the full rebuild renumbers
-    if (flags[1] > 0) flags[0] = 1;
   }
+  // several ranks with new vertices: placed in the owners' growth rooms when they fit on every
+  // rank (collective: the same union and decision everywhere), else the full rebuild
+  NewVertexPlan plan;
+  if (c.world > 1 && !flags[0] && flags[1] > 0 &&
+      (c.opt("merge_new_vertices", 1) == 0 || !plan_new_vertices_ranks(c, int64_t(unknown), plan)))
+    flags[0] = 1;
   if (flags[0]) return false;
   const bool any_tags = flags[2] > 0;
   PoolScope build_scope(build_pool(c));
@@ -2319,11 +2439,15 @@ static bool commit_merge(Ctx& c) {
     tmark = t;
   };
   phase("checks");
-  if (unknown) {
+  const bool new_vertices = c.world > 1 ? !plan.vids.empty() : unknown > 0;
+  if (c.world > 1 && new_vertices) {
+    extend_vertex_map_ranks(c, plan);
+    phase("vertex map (new vertices)");
+  } else if (new_vertices) {
     extend_vertex_map(c, int64_t(unknown));
     phase("vertex map (new vertices)");
   }
-  if (unknown || any_tags) {
+  if (new_vertices || any_tags) {
     // tag columns span the gidx space and pick winners over every staged row: rebuilt (on every
     // rank when any has tag writes: the owned slices are allgathered)
     c.tag_table.release();
@@ -2857,9 +2981,17 @@ void snapshot_finalize(Ctx& c) {
   }
   // owner ranges padded to 64 vertices: every rank's slice of a frontier bitmap starts on a
   // 64-bit word, so bitmap slices are exchanged without shifting (holes have no edges)
+  // A writable snapshot on several ranks also reserves growth room in every owner range (option
+  // grow_room_pct of the rank's vertices, at least 1024): a merge commit places new vertices
+  // there without moving any rank's range (extend_vertex_map_ranks); a batch that overflows
+  // some rank's room takes the full rebuild, which reserves room again.
+  const int64_t room_pct = keep && c.world > 1 ? std::max<int64_t>(0, c.opt("grow_room_pct", 10)) : 0;
   c.base.assign(size_t(c.world) + 1, 0);
   c.counts = counts;
-  for (int r = 0; r < c.world; r++) c.base[size_t(r) + 1] = c.base[size_t(r)] + ((counts[size_t(r)] + 63) / 64) * 64;
+  for (int r = 0; r < c.world; r++) {
+    const int64_t room = room_pct ? std::max<int64_t>(1024, counts[size_t(r)] * room_pct / 100) : 0;
+    c.base[size_t(r) + 1] = c.base[size_t(r)] + ((counts[size_t(r)] + room + 63) / 64) * 64;
+  }
   c.n_global = c.base[size_t(c.world)];
   c.n_vertices = 0;
   for (auto x : counts) c.n_vertices += x;

@@ -2605,7 +2605,8 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   const int64_t fb_words = (c.n_global + 31) / 32;
   // bu_hub_cap (tests): at most that many hub words, so small graphs exercise the L2 probes too
   const int64_t hub_cap = std::max<int64_t>(0, c.opt("bu_hub_cap", 36 * 1024));
-  const int cw = int(std::min<int64_t>(c.opt(fast ? "bu_lean_lds_kb_final" : "bu_lean_lds_kb", 64) * 256,
+  // (final hop 72 KiB, two blocks per CU still fit: r06g/r06h 1 % faster than 64)
+  const int cw = int(std::min<int64_t>(c.opt(fast ? "bu_lean_lds_kb_final" : "bu_lean_lds_kb", fast ? 72 : 64) * 256,
                                        std::min<int64_t>({fb_words, int64_t(36 * 1024), hub_cap})));
   const int bs = cw > 0 ? 1024 : 256;
   const int grid = int(std::max<int64_t>(
@@ -2631,7 +2632,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   };
   int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
   if (sel == 2 && c.opt("bu_lean_nt", 1) != 0 && (fast || es.odeg8.p)) sel = 6;  // non-temporal, 1 B degrees
-  if (sel == 6 && c.opt("bu_lean_skip", 0) != 0) sel = 7;                        // + probe skip
+  if (sel == 6 && c.opt("bu_lean_skip", 1) != 0) sel = 7;  // + probe skip (r06e: 100.4 -> 96.8 us)
 #define NBG_LEAN(PKV)                                \
   switch (sel) {                                     \
     case 7: go(k_bu_lean<PKV, 1, 1, 0, 1, 1>); break; \
@@ -2657,7 +2658,9 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
       kern<<<grid, bs, fshm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, fa, partials, cw, rest, gate);
     };
     const int nt = int(c.opt("bu_fin_nt", 1) != 0);
-    const int var = cls1 && nt ? int(c.opt("bu_fin_var", 0) & 63) : 0;
+    // default 49: the probe skip, one store per tile, hub-first L2 probes (r06h sweep:
+    // k_bu_fin 124.9 -> 108.1 us; the 16-byte-lane and blocked-tile variants measured no gain)
+    const int var = cls1 && nt ? int(c.opt("bu_fin_var", 49) & 63) : 0;
     switch ((cls1 ? 1 : 0) | nt << 1 | var << 2) {
       case 0: gof(k_bu_fin<0, 0>); break;
       case 1: gof(k_bu_fin<1, 0>); break;

@@ -291,13 +291,15 @@ def test_sharded_tag_props(world):
         g.close()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_writes_commit(world):
+@pytest.mark.parametrize("world,room", [(2, 10), (3, 10), (2, 0), (3, 0)])
+def test_sharded_writes_commit(world, room):
     """Write path with sharded ownership: each rank takes the write batches of its
     own parts (StorageClient routes an AddEdges part to its leader); commit is collective.  A batch
-    with new vertices rebuilds the vertex map / CSRs / tag slices on every rank; batches of edges
-    and tag rows of known vertices merge on every rank (merge_commits), also when only one rank
-    has writes of its own."""
+    with new vertices (INSERT EDGE to unseen vids, AddEdgesProcessor.cpp:15-31) merges on every
+    rank: the new vertices take gidx in their owners' growth room (grow_room_pct), the same
+    numbering on every rank; without room (grow_room_pct = 0) it rebuilds fully.  Batches of
+    edges and tag rows of known vertices merge on every rank (merge_commits), also when only one
+    rank has writes of its own."""
     import random
 
     import test_gpu_tags as T
@@ -314,6 +316,7 @@ def test_sharded_writes_commit(world):
     try:
         def load(r, s):
             s.set_option("writable", 1)
+            s.set_option("grow_room_pct", room)
             s.set_edge_schema(T.ET, [("weight", O.INT)])
             s.set_tag_schema(T.PERSON, "person", W.FIELDS)
             for p, kv in base.items():
@@ -357,14 +360,25 @@ def test_sharded_writes_commit(world):
                 want[(row[0], row[1], row[2], tuple(row[3:]))] += 1
             assert got == want
 
+        # round 4: edges to brand-new vertices again, on every rank
+        new4 = [rng.randrange(-2**62, 2**62) for _ in range(20)]
+        batch4 = W.write_batch(rng, known, new4, W.BASE_VER - 40)
         g.each(load)
         g.each(write(batch))
+        check([base, batch])
         g.each(write(batch2))
         check([base, batch, batch2])
         g.each(write(batch3))
         check([base, batch, batch2, batch3])
+        g.each(write(batch4))
+        check([base, batch, batch2, batch3, batch4])
         merges = g.each(lambda r, s: s.info(T.ET)["merge_commits"])
-        assert merges == [2] * world  # batch 1 has new vertices: the full rebuild
+        # batches 1 and 4 have new vertices: merged into the growth room; without reserved room
+        # only when the owners' 64-vertex padding happens to hold them, else rebuilt
+        assert len(set(merges)) == 1
+        assert merges[0] == 4 if room else 2 <= merges[0] <= 4
+        nv = g.each(lambda r, s: s.info(T.ET)["num_vertices"])
+        assert len(set(nv)) == 1
     finally:
         g.close()
 

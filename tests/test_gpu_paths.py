@@ -226,3 +226,25 @@ def test_sweep_kernels_and_level_filter(rmat, chunks, lvbits, push):
         sp.set_option("sp_sweep_chunks", 1)
         sp.set_option("sp_lvbits", 1)
         sp.set_option("sp_sweep_push", 1)
+
+
+@pytest.mark.parametrize("log2,soft,batch", [(22, 16 << 20, 1024), (10, 16 << 20, 1024), (10, 1, 1024), (12, 16 << 20, 7)])
+def test_sparse_distance_maps(rmat, log2, soft, batch):
+    """option sp_hash: the (pair, vertex) -> depth maps replace the dense distance bytes; a map
+    starting at 2^10 slots grows (rehash) mid-batch, sp_list_soft = 1 forces every list to
+    overflow and be rebuilt from the maps (regen), small batches reuse cleared maps"""
+    scale, sp, st = rmat
+    s, t = synth.pairs(scale, 16, 1, 200, pick_seed=17)
+    es, et_ = edge_case_pairs(scale)
+    src = np.concatenate([s, es])
+    dst = np.concatenate([t, et_])
+    for k, v in (("sp_hash", 1), ("sp_hash_log2", log2), ("sp_list_soft", soft), ("sp_batch", batch)):
+        sp.set_option(k, v)
+    try:
+        got = sp.shortest_path(src, dst, FOLLOW, 8).rows()
+        again = sp.shortest_path(src, dst, FOLLOW, 8).rows()
+    finally:
+        for k in ("sp_hash", "sp_hash_log2", "sp_list_soft", "sp_batch"):
+            sp.unset_option(k)
+    assert got == again
+    assert got == oracle_paths(st, src, dst, FOLLOW, 8)

@@ -404,3 +404,93 @@ def test_merge_commit_matches_full_rebuild_and_oracle(merge):
         assert v_new in set(int(x) for x in sp.go([vids[0]], 1, ET).columns[0])
     finally:
         sp.close()
+
+
+def sst_files(rng, vids, new_vids, n_files=3):
+    """SST-shaped ingest input (RocksEngine::ingest, RocksEngine.cpp:361-363: IngestExternalFile of
+    prebuilt files): each file holds unique keys in key order -- edges with several versions of
+    one (src, rank, dst), non-zero ranks, identical keys of base edges (the ingest overwrites
+    them), in-edge keys, tag rows; a later file may repeat an earlier file's key (the later file
+    wins, as a later put).  Returns the files as lists of (key, value) sorted by key bytes."""
+    part = lambda v: O.part_of(v, PARTS)  # noqa: E731
+    every = vids + new_vids
+    files = []
+    for f in range(n_files):
+        kv = {}
+        for _ in range(300):
+            s, t = rng.choice(every), rng.choice(every)
+            rank = rng.choice([0, 0, 0, 7, -3])
+            vers = [BASE_VER] if rng.random() < 0.15 else rng.sample(range(BASE_VER - 500, BASE_VER - 100), 3)
+            for ver in vers:  # several versions of the edge in one file
+                w = rng.randrange(0, 3000)
+                kv[O.edge_key(part(s), s, ET, rank, t, ver)] = O.encode_row([w])
+                kv[O.edge_key(part(t), t, -ET, rank, s, ver)] = b""
+        for v in rng.sample(every, 25):
+            p = part(v)
+            for ver in rng.sample(range(BASE_VER - 500, BASE_VER - 100), 2):
+                kv[O.vertex_key(p, v, PERSON, ver)] = O.encode_row([f"s{f}_{abs(v) % 7}", rng.randrange(100), 0.5 * f])
+        for v in new_vids:  # every new vertex gets a tag row (QUERIES read $$ props)
+            p = part(v)
+            kv[O.vertex_key(p, v, PERSON, BASE_VER - 50 - f)] = O.encode_row([f"n{abs(v) % 5}", f, 1.0])
+        files.append(sorted(kv.items()))
+    return files
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_sst_ingest_after_finalize(world):
+    """SST ingest mapped onto the write path: the files' pairs are read
+    in key order, grouped by part (the key's first 4 bytes, NebulaKeyUtils.h:14-21) and passed to
+    nbg_snapshot_write_part, then one nbg_snapshot_commit -- the same as puts of the same pairs in
+    file order.  Multi-version edges, ranks, overwritten base keys, tag rows and new vertices;
+    one rank and two LocalComm ranks (the commit merges on both: merge_commits)."""
+    import struct
+
+    from test_gpu_multirank import Group, union_rows
+    rng = random.Random(5)
+    base, vids = random_space_kv(13)
+    seen = set(vids)
+    new_vids = []
+    while len(new_vids) < 24:
+        v = rng.randrange(-2**62, 2**62)
+        if v not in seen:
+            seen.add(v)
+            new_vids.append(v)
+    files = sst_files(rng, vids, new_vids)
+    # ingest order: file by file, each in key order, grouped by part
+    ingest = []
+    for kvs in files:
+        by_part = {}
+        for k, v in kvs:
+            by_part.setdefault(struct.unpack("<i", k[:4])[0], []).append((k, v))
+        ingest.append(by_part)
+    st = fresh_oracle([base] + ingest)
+    starts = vids[::11] + new_vids[:4]
+    g = Group(world, parts=PARTS)
+    try:
+        def load(r, s):
+            s.set_option("writable", 1)
+            s.set_edge_schema(ET, [("weight", O.INT)])
+            s.set_tag_schema(PERSON, "person", FIELDS)
+            for p, kv in base.items():
+                if kv and p % world == r:
+                    s.load_part(p, kv)
+            s.finalize()
+
+        def ingest_all(r, s):
+            for by_part in ingest:
+                for p, kv in sorted(by_part.items()):
+                    if p % world == r:
+                        s.write_part(p, kv)
+            s.commit()
+        g.each(load)
+        g.each(ingest_all)
+        for steps, where, ys, distinct in QUERIES:
+            res = g.go(starts, steps, ET, where=where, yields=ys, distinct=distinct)
+            ref = st.go(starts, steps, ET, where=X.encode(where), yields=[y.encode() for y in ys], distinct=distinct)
+            assert ref.code == 0, ref.error
+            assert union_rows(res) == ms(ref.rows())
+        if world == 1:
+            check_bound(g.sp[0], st, vids + new_vids)
+        assert g.each(lambda r, s: s.info(ET)["merge_commits"]) == [1] * world
+    finally:
+        g.close()
