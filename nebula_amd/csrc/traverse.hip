@@ -868,6 +868,24 @@ __device__ inline void bu_rest_scan(const bool (&pend)[R], bool (&found)[R], con
 // HUB: the block keeps the first cw words of the bitmap (the highest-out-degree vertices) in LDS
 // and answers candidates there from it; the global probe of such a slot is out of bounds.
 // Partials [6] / [7]: candidate probes sent to L2 / answered from LDS.
+// Speculative hops (go_run): the first pass of a gated hop evaluates the host's direction rule
+// itself on the previous hop's device counters -- open iff the previous hop ran (pg), its next
+// frontier is non-empty (*n > 0) and its out-degree sum reaches the threshold (*e >= thr) -- and
+// block 0 publishes the answer at `gate` for the hop's later kernels and the host (a separate
+// one-thread k_gate launch cost ~4.6 us a hop).  e == nullptr: not gated.
+struct GateIn {
+  const unsigned long long* e = nullptr;
+  const unsigned long long* n = nullptr;
+  const unsigned long long* pg = nullptr;
+  unsigned long long thr = 0;
+};
+__device__ inline bool gate_open(const GateIn& gi, unsigned long long* gate) {
+  if (gi.e == nullptr) return gate == nullptr || *gate != 0ull;
+  const bool open = (gi.pg == nullptr || *gi.pg != 0ull) && *gi.n > 0ull && *gi.e >= gi.thr;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *gate = open ? 1ull : 0ull;
+  return open;
+}
+
 template <int PK, int U, int HUB, int STATS, int NT = 0, int SKIP = 0>
 __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ lo, const uint2* __restrict__ hi,
                                                      int64_t ntiles, int64_t work_tiles,
@@ -877,8 +895,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
                                                      const uint32_t* __restrict__ odeg, QArgs q_arg,
                                                      unsigned long long* __restrict__ partials, int cw,
                                                      const uint8_t* __restrict__ odeg8,
-                                                     const unsigned long long* __restrict__ gate) {
-  if (gate && *gate == 0ull) return;  // a speculative hop that the direction choice did not take
+                                                     unsigned long long* gate, GateIn gi) {
+  if (!gate_open(gi, gate)) return;  // a speculative hop that the direction choice did not take
   __shared__ unsigned long long lds[kSlots * 16];
   extern __shared__ uint32_t s_fb[];  // [0, cw): the bitmap's hub words; [cw]: a zero word
   if (HUB) hub_fill(s_fb, fbits, cw, true);
@@ -919,6 +937,21 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
     }
   };
   auto bit = [](uint32_t w, uint32_t sw) -> uint32_t { return __builtin_amdgcn_ubfe(w, sw & 31u, 1u); };
+  // SKIP bit 2 (WIDE, non-final hops): lane l holds rows 2l (h 0) and 2l + 1 (h 1) of a tile,
+  // so the slab's first half is one 16-byte load per lane and the 1-byte degrees one 2-byte load
+  // (the 8-byte and 1-byte loads of the row-per-lane layout made this pass instruction-bound:
+  // two slab and two degree loads per 128 rows for 1.1 KB); the ballots of the even and odd rows
+  // are interleaved back into the tile's row-order words, stored with one instruction
+  constexpr bool WIDE = (SKIP & 4) && !FINAL && U == 1 && NT;
+  auto row_of = [&](int64_t t, int h) -> int64_t { return WIDE ? t * 128 + 2 * lane + h : t * 128 + lane + 64 * h; };
+  auto spread = [](uint64_t x) -> uint64_t {  // bit i -> bit 2i (32 -> 64 bits)
+    x &= 0xffffffffull;
+    x = (x | (x << 16)) & 0x0000ffff0000ffffull;
+    x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
+    x = (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    return (x | (x << 1)) & 0x5555555555555555ull;
+  };
   for (int64_t t0 = wave * U; t0 < work_tiles; t0 += nwaves * U) {
     uint2 a[U][2], b[U][2];
     uint32_t od[U][2];
@@ -927,6 +960,17 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
     for (int u = 0; u < U; u++) {
       v[u] = t0 + u < work_tiles;
       const int64_t r = (v[u] ? t0 + u : t0) * 128 + lane;  // a past-the-end tile re-reads t0 (discarded)
+      if (WIDE) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const int64_t tt = v[u] ? t0 + u : t0;
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(lo) + tt * 64 + lane);
+        a[u][0] = make_uint2(x.x, x.y);
+        a[u][1] = make_uint2(x.z, x.w);
+        const uint32_t o2 = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(odeg8 + tt * 128) + lane);
+        od[u][0] = o2 & 0xffu;
+        od[u][1] = o2 >> 8;
+        continue;
+      }
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         if (NT) {  // the slab and degrees are read once per hop: keep L2 for the bitmap probes
@@ -979,6 +1023,22 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
             }
           }
     }
+    // SKIP bit 1 (non-final hops): rows already found through a hub word, and rows without
+    // out-edges (they cannot extend the next frontier), send no L2 probe
+    bool noprobe[U][2];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        noprobe[u][h] = false;
+        if ((SKIP & 2) && HUB && !FINAL) {
+          const uint32_t sw[2] = {a[u][h].x, a[u][h].y};
+          bool hf = false;
+#pragma unroll
+          for (int k = 0; k < NS; k++) hf = hf || bit(lw[u][h][k], sw[k]) != 0u;
+          noprobe[u][h] = hf || od[u][h] == 0u;
+        }
+      }
 #pragma unroll
     for (int u = 0; u < U; u++)
 #pragma unroll
@@ -987,8 +1047,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
         for (int k = 0; k < NS; k++) {
           if (SKIP) {
             gw[u][h][k] = 0u;
-            if (__ballot(goff[u][h][k] != 0xfffffff0u))
-              gw[u][h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, goff[u][h][k], 0, 0);
+            const uint32_t go = noprobe[u][h] ? 0xfffffff0u : goff[u][h][k];
+            if (__ballot(go != 0xfffffff0u)) gw[u][h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, go, 0, 0);
           } else {
             gw[u][h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, goff[u][h][k], 0, 0);
           }
@@ -1028,7 +1088,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
 #pragma unroll
           for (int h = 0; h < 2; h++) {
             b[u][h] = make_uint2(0xffffffffu, 0xffffffffu);
-            if (pend[u][h]) b[u][h] = hi[(t0 + u) * 128 + lane + 64 * h];
+            if (pend[u][h]) b[u][h] = hi[row_of(t0 + u, h)];
           }
         uint64_t pc = 0;  // rows reading the second half: 2 words each
 #pragma unroll
@@ -1078,9 +1138,20 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
     for (int u = 0; u < U; u++) {
       if (!v[u]) continue;  // wave-uniform
       const int64_t t = t0 + u;
-      const unsigned long long f0 = __ballot(f[u][0]), f1 = __ballot(f[u][1]);
-      const unsigned long long p0 = __ballot(pend[u][0]), p1 = __ballot(pend[u][1]);
-      if (lane < 2) {
+      unsigned long long f0 = __ballot(f[u][0]), f1 = __ballot(f[u][1]);
+      unsigned long long p0 = __ballot(pend[u][0]), p1 = __ballot(pend[u][1]);
+      if (WIDE) {
+        const unsigned long long w0 = spread(f0) | (spread(f1) << 1), w1 = spread(f0 >> 32) | (spread(f1 >> 32) << 1);
+        const unsigned long long q0 = spread(p0) | (spread(p1) << 1), q1 = spread(p0 >> 32) | (spread(p1 >> 32) << 1);
+        f0 = w0, f1 = w1, p0 = q0, p1 = q1;
+        if (lane < 2) {  // lane 0 the two next-frontier words, lane 1 the two pending words
+          typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+          u64x2 vv;
+          vv.x = lane ? p0 : f0;
+          vv.y = lane ? p1 : f1;
+          *reinterpret_cast<u64x2*>((lane ? pbits : nbits) + 2 * t) = vv;
+        }
+      } else if (lane < 2) {
         nbits[2 * t + lane] = lane ? f1 : f0;
         pbits[2 * t + lane] = lane ? p1 : p0;
       }
@@ -1090,7 +1161,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           uint32_t d = f[u][h] ? od[u][h] : 0u;
-          if (NT && d == 255u) d = odeg[t * 128 + lane + 64 * h];  // odeg8 saturates at 255
+          if (NT && d == 255u) d = odeg[row_of(t, h)];  // odeg8 saturates at 255
           odsum += uint64_t(d);
         }
       }
@@ -1140,8 +1211,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
                                                     unsigned long long* __restrict__ nbits,
                                                     unsigned long long* __restrict__ pbits, FinArgs fa_arg,
                                                     unsigned long long* __restrict__ partials, int cw,
-                                                    uint32_t fb_rest, const unsigned long long* __restrict__ gate) {
-  if (gate && *gate == 0ull) return;  // a speculative hop that the direction choice did not take
+                                                    uint32_t fb_rest, unsigned long long* gate, GateIn gi) {
+  if (!gate_open(gi, gate)) return;  // a speculative hop that the direction choice did not take
   // dynamic LDS only, so the hub copy starts at address 0 and a probe's LDS address is its
   // clamped byte offset as it is: [0, cw) the bitmap's hub words, [cw] a zero word, then the
   // block's partials scratch
@@ -2097,15 +2168,6 @@ __global__ void k_publish(const unsigned long long* __restrict__ src, int n, uns
   }
 }
 
-// Speculative bottom-up hops (go_run): *gate = 1 iff the previous hop ran (prev_gate, when
-// given), its next frontier is non-empty (*n > 0) and its out-degree sum reaches the bottom-up
-// threshold (*e >= thr >= 1) -- the host's direction choice (want_bu) on the same counters.
-__global__ void k_gate(const unsigned long long* e, const unsigned long long* n, const unsigned long long* prev_gate,
-                       unsigned long long thr, unsigned long long* gate) {
-  if (threadIdx.x == 0)
-    *gate = (prev_gate == nullptr || *prev_gate != 0ull) && *n > 0ull && *e >= thr ? 1ull : 0ull;
-}
-
 // the device counters d[0, n) into host h[0, n) once every launch before has finished: a
 // one-thread-block kernel writes them and a sequence word to coherent host memory and the host
 // spins on the word (a memcpy + hipStreamSynchronize round trip cost ~19 us, tools/launch_gap);
@@ -2578,7 +2640,7 @@ FinArgs fin_args(const QArgs& q) {
 // without a memory access).
 size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
                       const FastArgs& fp, int fcol, unsigned long long* out, bool hop_front,
-                      const unsigned long long* gate = nullptr) {
+                      unsigned long long* gate = nullptr, GateIn gi = GateIn{}) {
   const Csr& tr = es.tr;
   if (pk != PK_NONE && pk != PK_FAST) throw Error(NBG_E_DEVICE, "bottom-up hop with a VM predicate");
   if (!es.pair_col[0].p) throw Error(NBG_E_DEVICE, "bottom-up hop without the quad slab");
@@ -2628,13 +2690,17 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     if (shm > 48 * 1024)
       lds_limit(reinterpret_cast<const void*>(kern), shm);
     kern<<<grid, bs, shm, c.stream>>>(lo, hi, ntiles, work, fb, fb_bytes, nb, pbits, od, q, partials, cw,
-                                      es.odeg8.as<uint8_t>(), gate);
+                                      es.odeg8.as<uint8_t>(), gate, gi);
   };
   int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
   if (sel == 2 && c.opt("bu_lean_nt", 1) != 0 && (fast || es.odeg8.p)) sel = 6;  // non-temporal, 1 B degrees
-  if (sel == 6 && c.opt("bu_lean_skip", 1) != 0) sel = 7;  // + probe skip (r06e: 100.4 -> 96.8 us)
+  const int64_t lskip = c.opt("bu_lean_skip", 1);
+  if (sel == 6 && lskip != 0) sel = lskip == 3 ? 8 : lskip == 7 ? 9 : lskip == 5 ? 10 : 7;  // + probe skip
 #define NBG_LEAN(PKV)                                \
   switch (sel) {                                     \
+    case 10: go(k_bu_lean<PKV, 1, 1, 0, 1, 5>); break; \
+    case 9: go(k_bu_lean<PKV, 1, 1, 0, 1, 7>); break; \
+    case 8: go(k_bu_lean<PKV, 1, 1, 0, 1, 3>); break; \
     case 7: go(k_bu_lean<PKV, 1, 1, 0, 1, 1>); break; \
     case 6: go(k_bu_lean<PKV, 1, 1, 0, 1>); break;   \
     case 0: go(k_bu_lean<PKV, 1, 0, 0>); break;      \
@@ -2655,7 +2721,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     const uint32_t rest = fb_bytes > uint32_t(cw) * 4u ? fb_bytes - uint32_t(cw) * 4u : 0u;
     auto gof = [&](auto kern) {
       if (fshm > 48 * 1024) lds_limit(reinterpret_cast<const void*>(kern), fshm);
-      kern<<<grid, bs, fshm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, fa, partials, cw, rest, gate);
+      kern<<<grid, bs, fshm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, fa, partials, cw, rest, gate, gi);
     };
     const int nt = int(c.opt("bu_fin_nt", 1) != 0);
     // default 49: the probe skip, one store per tile, hub-first L2 probes (r06h sweep:
@@ -2757,7 +2823,8 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     snprintf(nm, sizeof nm, "%s", fin_nm);
   else
     snprintf(nm, sizeof nm, "nbg::k_bu_lean<%d, %d, %d, %d%s>", pk, probe_stats ? 1 : U, cw > 0 ? 1 : 0,
-             probe_stats ? 1 : 0, sel == 7 ? ", 1, 1" : sel == 6 ? ", 1, 0" : ", 0, 0");
+             probe_stats ? 1 : 0,
+             sel == 10 ? ", 1, 5" : sel == 9 ? ", 1, 7" : sel == 8 ? ", 1, 3" : sel == 7 ? ", 1, 1" : sel == 6 ? ", 1, 0" : ", 0, 0");
   c.bu_kernel_name = nm;
   const int wn = fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0;
   snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d, %d>", pk, wn, rcw > 0 ? 1 : 0, use_rec ? 1 : 0);
@@ -3142,7 +3209,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   int64_t Eg = 0;  // frontier out-degree sum over all ranks
   // Speculative bottom-up hops (one rank).  A direction choice needs the previous hop's counters
   // on the host, one round trip per hop; instead, right after a top-down hop's compaction, the
-  // remaining hops are enqueued as bottom-up hops gated on the device (k_gate: the same rule as
+  // remaining hops are enqueued as bottom-up hops gated on the device (GateIn: the same rule as
   // want_bu, on the same counters) before the one counter fetch.  A hop whose gate is 0 does
   // nothing (every kernel returns at once), and the host continues from there as before: the
   // direction never changes a hop's result, only its cost.  The final step is speculated only
@@ -3189,7 +3256,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const bool fin = st == s.steps;
       if (fin && !fin_spec) break;
       unsigned long long* blk = SPd + 16 * spec.size();
-      k_gate<<<1, 64, 0, c.stream>>>(e, n, pg, spec_thr, blk + 8);
+      // the hop's first pass evaluates its gate (GateIn) and publishes it at blk[8]
+      GateIn gi;
+      gi.e = e, gi.n = n, gi.pg = pg, gi.thr = spec_thr;
       const int32_t hop = hop0 + int32_t(spec.size());
       // several ranks: the frontier bitmaps of every rank (the exchange runs whatever the gate
       // says: every rank enqueued it)
@@ -3197,12 +3266,12 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const size_t ia = timing_event(c);
       size_t ik;
       if (!fin) {
-        ik = launch_bu_lean(c, es, fb, outb, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, blk, true, blk + 8);
+        ik = launch_bu_lean(c, es, fb, outb, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, blk, true, blk + 8, gi);
       } else {
         FastArgs tfp = fp0;
         if (fpk0.kind == PK_FAST) tfp.data = es.tr.props[size_t(fpk0.col)].data.p;
         ik = launch_bu_lean(c, es, fb, outb, nullptr, fpk0.kind, tfp, fpk0.kind == PK_FAST ? fpk0.col : -1, blk, true,
-                            blk + 8);
+                            blk + 8, gi);
         spec_vids.alloc(size_t(c.n_global + 64) * 8);
         launch_bits_vids(c, outb, es.tr.n_rows, lo, spec_vids.p, blk + 9, blk + 8);
       }
