@@ -145,10 +145,25 @@ struct HostBuf {
     o.p = nullptr;
     o.bytes = 0;
   }
-  ~HostBuf() {
+  HostBuf& operator=(HostBuf&& o) noexcept {
+    if (this != &o) {
+      release();
+      p = o.p;
+      bytes = o.bytes;
+      pool = std::move(o.pool);
+      o.p = nullptr;
+      o.bytes = 0;
+    }
+    return *this;
+  }
+  ~HostBuf() { release(); }
+  void release() {
     if (!p) return;
     if (pool) pool->put(p, bytes);
     else (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    pool.reset();
   }
   void alloc(const std::shared_ptr<HostPool>& pl, size_t b) {
     if (p || b == 0) throw std::logic_error("HostBuf::alloc");

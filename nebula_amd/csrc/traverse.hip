@@ -3223,6 +3223,20 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   };
   std::vector<Spec> spec;
   DevBuf spec_vids;
+  // option host_direct: a DISTINCT _dst result that goes to the host is written by the bottom-up
+  // output kernel straight into pinned host memory (mapped into the device's address space), so
+  // the hand-out copies nothing
+  const bool host_direct = !s.keep_on_device && c.opt("host_direct", 0) != 0;
+  HostBuf spec_hvids;
+  auto vid_block = [&](DevBuf& d, HostBuf& hb) -> void* {
+    if (host_direct) {
+      host_pool_cap(c);
+      hb.alloc(c.host_pool, size_t(c.n_global + 64) * 8);
+      return hb.p;
+    }
+    d.alloc(size_t(c.n_global + 64) * 8);
+    return d.p;
+  };
   FastPred fpk0{};
   FastArgs fp0{};
   bool fin_spec = false;
@@ -3272,8 +3286,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         if (fpk0.kind == PK_FAST) tfp.data = es.tr.props[size_t(fpk0.col)].data.p;
         ik = launch_bu_lean(c, es, fb, outb, nullptr, fpk0.kind, tfp, fpk0.kind == PK_FAST ? fpk0.col : -1, blk, true,
                             blk + 8, gi);
-        spec_vids.alloc(size_t(c.n_global + 64) * 8);
-        launch_bits_vids(c, outb, es.tr.n_rows, lo, spec_vids.p, blk + 9, blk + 8);
+        void* vout = vid_block(spec_vids, spec_hvids);
+        launch_bits_vids(c, outb, es.tr.n_rows, lo, vout, blk + 9, blk + 8);
       }
       NBG_HIP(hipGetLastError());
       const size_t ib = timing_event(c);
@@ -3502,6 +3516,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   auto* h = new HostRows();
   int64_t nrows = 0;
   std::vector<DevBuf> slen(yields.size());  // STRING yield columns: byte length per row
+  std::map<size_t, bool> host_cols;         // columns already in pinned host memory (host_direct)
   try {
     if (distinct_dst) {
       // DISTINCT e._dst: mark surviving dsts, compact the whole vertex space (no deg filter).
@@ -3511,9 +3526,12 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
                                        es.tr.props.size() > size_t(fpk.col) && es.tr.props[size_t(fpk.col)].data.p);
       bool bu = pred_bu && want_bu(Eg);
       DevBuf vids;
+      HostBuf hvids;
+      void* vout = nullptr;
       if (fin_done) {
         // the speculated final hop ran (spec_replay): its counters, rows and kernel names
         vids = std::move(spec_vids);
+        hvids = std::move(spec_hvids);
         c.timing.expand_launches++;
         c.timing.bu_steps++;
         nrows = int64_t(fin_h[9]);
@@ -3523,7 +3541,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         c.timing.hop(1, true, 0.0, fin_h, 0.0, kb);
         c.timing.name_last_hop(fin_k0, fin_k1, c.opt("bits_u", 8) == 8 ? "nbg::k_bits_compact<1, 8>" : "nbg::k_bits_compact<1, 4>");
       } else {
-        vids.alloc(size_t(c.n_global + 64) * 8);
+        vout = nullptr;
       }
       if (fin_done) {
       } else if (bu) {
@@ -3535,7 +3553,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         const size_t ia = timing_event(c);
         const size_t ik =
             launch_bu_lean(c, es, fb, bitsB, nullptr, pk, tfp, pk == PK_FAST ? fpk.col : -1, K.d + 8, s.steps > 1);
-        launch_bits_vids(c, bitsB, tr.n_rows, lo, vids.p, K.d, nullptr);
+        vout = vid_block(vids, hvids);
+        launch_bits_vids(c, bitsB, tr.n_rows, lo, vout, K.d, nullptr);
         NBG_HIP(hipGetLastError());
         const size_t ib = timing_event(c);
         c.tpend.push_back(Ctx::PendingTime{ia, ib, c.timing.n_hops, 0});
@@ -3551,6 +3570,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         c.timing.hop(1, true, 0.0, K.h + 8, 0.0, kb);
         c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name, c.opt("bits_u", 8) == 8 ? "nbg::k_bits_compact<1, 8>" : "nbg::k_bits_compact<1, 4>");
       } else {
+        vids.alloc(size_t(c.n_global + 64) * 8);
         ensure_off();
         a.F = F;
         a.nF = nF;
@@ -3577,6 +3597,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
                                                                vids.as<int64_t>());
       }
       h->types.push_back(NBG_T_VID);
+      if (hvids.p) {  // already on the host (host_direct)
+        host_cols[h->dev.size()] = true;
+        h->hpin.push_back(std::move(hvids));
+      }
       h->dev.push_back(std::move(vids));
     } else {
       // rows (src, edge) passing WHERE; a lone YIELD _dst (the default) is written directly as
@@ -3768,7 +3792,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       continue;
     }
     h->str_off.push_back(nullptr);
-    if (on_dev) {
+    if (host_cols.count(cc)) {  // written into pinned host memory by the output kernel
+      h->cols.push_back(h->hpin.back().p);
+    } else if (on_dev) {
       h->cols.push_back(h->dev[cc].p);
     } else {
       size_t w = h->types[cc] == NBG_T_BOOL ? 1 : 8;

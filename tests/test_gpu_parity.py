@@ -664,3 +664,29 @@ def test_rmat_bottom_up_packed_predicate(rmat12, qpred, hub_cap, fin):
             assert g.edges_scanned == r_.edges_scanned
             ks = final_bu_kernels(sp)
             assert ks[0].startswith(first) and ks[1].startswith("nbg::k_bu_rest_lean<1, "), ks
+
+
+@pytest.mark.parametrize("spec,force", [(1, 0), (0, 0), (1, 1), (1, -1)])
+def test_host_direct_distinct_output(rmat12, spec, force):
+    """option host_direct: the DISTINCT _dst output kernel writes the vids straight into pinned
+    host memory (no device->host copy); same rows as the default path and the oracle, on the
+    speculated final hop, the host-driven bottom-up hop and the top-down hop (device column)"""
+    sp, st = rmat12
+    starts = seeds_from(12, 64)
+    w = X.AliasProp("follow", "weight") > 499
+    y = [X.EdgeDst("follow")]
+    r = st.go(starts, 3, FOLLOW, where=w.encode(), yields=[y[0].encode()], distinct=True)
+    want = np.sort(r.int_col(0))
+    sp.set_option("bu_spec", spec)
+    sp.set_option("bu_force", force)
+    sp.set_option("bu_div", 16)
+    try:
+        for hd in (1, 0, 1):
+            sp.set_option("host_direct", hd)
+            g = sp.go(starts, 3, FOLLOW, where=w, yields=y, distinct=True)
+            col = np.array(g.columns[0])
+            del g  # the pinned block returns to the cache while `col` keeps its copy
+            assert np.array_equal(np.sort(col), want)
+    finally:
+        for k in ("bu_spec", "bu_force", "bu_div", "host_direct"):
+            sp.unset_option(k)
