@@ -398,7 +398,28 @@ def spawn_ranks(n: int) -> int:
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env,
                                       stdout=None if r == 0 else subprocess.DEVNULL))
-    rcs = [p.wait() for p in procs]
+    # poll every child: when one fails, the others (possibly blocked in the rendezvous or a
+    # collective waiting for it) are ended at once instead of waiting out their timeouts
+    import time as _t
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        failed = [rc for rc in rcs if rc not in (None, 0)]
+        if failed:
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.terminate()
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = p.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        p.kill()
+                        rcs[i] = p.wait()
+            break
+        _t.sleep(0.2)
     bad = [c for c in rcs if c != 0]
     if bad:
         print(f"bench.py: rank exit codes {rcs}", file=sys.stderr)
@@ -459,7 +480,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import datetime
+        # a rank that dies before the rendezvous fails the others within minutes, not 30
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(minutes=5))
     if args.launch_check:
         return launch_check(dist, rank, world, local)
 
