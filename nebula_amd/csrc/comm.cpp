@@ -34,6 +34,10 @@ struct CommImpl {
   virtual void alltoallv(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
                          const size_t* recv_bytes, const size_t* recv_off) = 0;
   virtual void allreduce_sum_i64(Ctx& c, int64_t* d, size_t n) = 0;
+  // allgatherv plus a small fixed-size allgather in the same exchange (one grouped launch):
+  // every rank's send2 (bytes2) lands at recv2 + r * bytes2 of every rank
+  virtual void allgatherv2(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
+                           const size_t* recv_off, const void* send2, size_t bytes2, void* recv2) = 0;
   virtual int32_t ranks() const = 0;     // the communicator's own rank count
   virtual int32_t transport() const = 0;  // 1 = RCCL, 2 = in-process LocalComm
 };
@@ -82,6 +86,24 @@ struct RcclComm : CommImpl {
   void allreduce_sum_i64(Ctx& c, int64_t* d, size_t n) override {
     NBG_NCCL(ncclAllReduce(d, d, n, ncclInt64, ncclSum, comm, c.stream));
   }
+  void allgatherv2(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
+                   const size_t* recv_off, const void* send2, size_t bytes2, void* recv2) override {
+    NBG_NCCL(ncclGroupStart());
+    for (int p = 0; p < c.world; p++) {
+      if (p == c.rank) continue;
+      if (send_bytes) NBG_NCCL(ncclSend(send, send_bytes, ncclUint8, p, comm, c.stream));
+      if (recv_bytes[p])
+        NBG_NCCL(ncclRecv(static_cast<uint8_t*>(recv) + recv_off[p], recv_bytes[p], ncclUint8, p, comm, c.stream));
+      NBG_NCCL(ncclSend(send2, bytes2, ncclUint8, p, comm, c.stream));
+      NBG_NCCL(ncclRecv(static_cast<uint8_t*>(recv2) + size_t(p) * bytes2, bytes2, ncclUint8, p, comm, c.stream));
+    }
+    NBG_NCCL(ncclGroupEnd());
+    if (send_bytes && static_cast<uint8_t*>(recv) + recv_off[c.rank] != send)
+      NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[c.rank], send, send_bytes,
+                             hipMemcpyDeviceToDevice, c.stream));
+    NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv2) + size_t(c.rank) * bytes2, send2, bytes2,
+                           hipMemcpyDeviceToDevice, c.stream));
+  }
 };
 
 // ------------------------------------------------------------------------------------------
@@ -101,7 +123,7 @@ struct LocalGroup {
   std::condition_variable cv;
   int arrived = 0;
   uint64_t gen = 0;
-  std::vector<const void*> ptr;
+  std::vector<const void*> ptr, ptr2;
   std::vector<const size_t*> sizes, offs;
   std::vector<size_t> scalar;
   std::vector<hipEvent_t> ready, done;
@@ -183,6 +205,23 @@ struct LocalComm : CommImpl {
     }
     finish(c);
   }
+  void allgatherv2(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
+                   const size_t* recv_off, const void* send2, size_t bytes2, void* recv2) override {
+    g->ptr[size_t(c.rank)] = send;
+    g->scalar[size_t(c.rank)] = send_bytes;
+    g->ptr2[size_t(c.rank)] = send2;
+    publish(c);
+    for (int p = 0; p < c.world; p++) {
+      wait_ready(c, p);
+      size_t b = std::min(g->scalar[size_t(p)], recv_bytes[p]);
+      if (b && g->ptr[size_t(p)] != static_cast<uint8_t*>(recv) + recv_off[p])
+        NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[p], g->ptr[size_t(p)], b,
+                               hipMemcpyDeviceToDevice, c.stream));
+      NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv2) + size_t(p) * bytes2, g->ptr2[size_t(p)], bytes2,
+                             hipMemcpyDeviceToDevice, c.stream));
+    }
+    finish(c);
+  }
   // in place, as ncclAllReduce: gather the slices, sum them, and write the sums back only after
   // every peer has read this rank's slice
   void allreduce_sum_i64(Ctx& c, int64_t* d, size_t n) override {
@@ -248,6 +287,7 @@ void comm_init_local(Ctx& c, int64_t key) {
       slot = std::make_shared<LocalGroup>();
       slot->world = c.world;
       slot->ptr.resize(size_t(c.world));
+      slot->ptr2.resize(size_t(c.world));
       slot->sizes.resize(size_t(c.world));
       slot->offs.resize(size_t(c.world));
       slot->scalar.resize(size_t(c.world));
@@ -315,6 +355,18 @@ void comm_alltoallv_bytes(Ctx& c, const void* send, const size_t* send_bytes, co
     return;
   }
   impl(c)->alltoallv(c, send, send_bytes, send_off, recv, recv_bytes, recv_off);
+}
+
+void comm_allgatherv2_bytes(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
+                            const size_t* recv_off, const void* send2, size_t bytes2, void* recv2) {
+  if (c.world == 1) {
+    if (send_bytes && static_cast<uint8_t*>(recv) + recv_off[0] != send)
+      NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[0], send, send_bytes, hipMemcpyDeviceToDevice,
+                             c.stream));
+    NBG_HIP(hipMemcpyAsync(recv2, send2, bytes2, hipMemcpyDeviceToDevice, c.stream));
+    return;
+  }
+  impl(c)->allgatherv2(c, send, send_bytes, recv, recv_bytes, recv_off, send2, bytes2, recv2);
 }
 
 void comm_allreduce_sum_i64(Ctx& c, int64_t* d_vals, size_t n) {

@@ -513,6 +513,7 @@ struct Ctx {
   DevBuf ws_bits_send, ws_bits_recv;
   DevBuf ws_bits_glob;  // world > 1: allgathered frontier bitmap / per-owner mark bitmap
   DevBuf ws_bits_xchg;  // world > 1: received mark segments [world][owned/32]
+  DevBuf ws_piggy;      // world > 1: every rank's (n, e) counters per speculated hop
   DevBuf ws_starts;
   DevBuf ws_partials;  // per-block partial sums of the aggregated kernels
   DevBuf ws_pend;      // deferred bottom-up rows: pending bits + compacted list
@@ -648,6 +649,8 @@ void comm_alltoallv_bytes(Ctx& c, const void* send, const size_t* send_bytes, co
                           void* recv, const size_t* recv_bytes, const size_t* recv_off);
 void comm_allgather_bytes(Ctx& c, const void* send, size_t bytes_each, void* recv);
 void comm_allreduce_sum_i64(Ctx& c, int64_t* d_vals, size_t n);
+void comm_allgatherv2_bytes(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
+                            const size_t* recv_off, const void* send2, size_t bytes2, void* recv2);
 void comm_allgatherv_bytes(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
                            const size_t* recv_off);
 void comm_init_local(Ctx& c, int64_t key);

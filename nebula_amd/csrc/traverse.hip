@@ -873,16 +873,32 @@ __device__ inline void bu_rest_scan(const bool (&pend)[R], bool (&found)[R], con
 // frontier is non-empty (*n > 0) and its out-degree sum reaches the threshold (*e >= thr) -- and
 // block 0 publishes the answer at `gate` for the hop's later kernels and the host (a separate
 // one-thread k_gate launch cost ~4.6 us a hop).  e == nullptr: not gated.
+// Several ranks (all != nullptr): the previous hop's (n, e) of every rank arrived with this
+// hop's frontier allgather (all[2r], all[2r + 1]); the gate sums them and block 0 also publishes
+// the sums at gate[2], gate[3] (the host's global counts of the previous hop).
 struct GateIn {
   const unsigned long long* e = nullptr;
   const unsigned long long* n = nullptr;
   const unsigned long long* pg = nullptr;
   unsigned long long thr = 0;
+  const unsigned long long* all = nullptr;
+  int world = 1;
 };
 __device__ inline bool gate_open(const GateIn& gi, unsigned long long* gate) {
-  if (gi.e == nullptr) return gate == nullptr || *gate != 0ull;
-  const bool open = (gi.pg == nullptr || *gi.pg != 0ull) && *gi.n > 0ull && *gi.e >= gi.thr;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *gate = open ? 1ull : 0ull;
+  if (gi.e == nullptr && gi.all == nullptr) return gate == nullptr || *gate != 0ull;
+  unsigned long long n, e;
+  if (gi.all) {
+    n = e = 0ull;
+    for (int r = 0; r < gi.world; r++) n += gi.all[2 * r], e += gi.all[2 * r + 1];
+  } else {
+    n = *gi.n;
+    e = *gi.e;
+  }
+  const bool open = (gi.pg == nullptr || *gi.pg != 0ull) && n > 0ull && e >= gi.thr;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *gate = open ? 1ull : 0ull;
+    if (gi.all) gate[2] = n, gate[3] = e;
+  }
   return open;
 }
 
@@ -2225,6 +2241,7 @@ void ensure_workspaces(Ctx& c, int64_t nF_cap) {
   c.ws_bits_send.ensure(size_t(mb / 8 + 64));
   c.ws_bits_recv.ensure(size_t(mb / 8 + 64));
   if (c.world > 1) {
+    c.ws_piggy.ensure(size_t(12) * size_t(c.world) * 16 + 64);  // spec hops' counters of every rank
     c.ws_bits_glob.ensure(size_t(mb / 8 + 64));
     c.ws_bits_xchg.ensure(size_t(c.world) * size_t((c.owned_hi() - c.owned_lo()) / 8) + 64);
   }
@@ -2293,6 +2310,20 @@ const uint32_t* global_bits(Ctx& c, const uint32_t* owned) {
   }
   comm_allgatherv_bytes(c, owned, rb[size_t(c.rank)], c.ws_bits_glob.p, rb.data(), ro.data());
   c.timing.comm_bytes += uint64_t(rb[size_t(c.rank)]) * (G - 1);
+  return c.ws_bits_glob.as<uint32_t>();
+}
+
+// global_bits + every rank's two counters (n, e) at cnt into all[2r, 2r + 2), one exchange
+const uint32_t* global_bits_cnt(Ctx& c, const uint32_t* owned, const unsigned long long* cnt, unsigned long long* all) {
+  CommTimer t(c);
+  const size_t G = size_t(c.world);
+  std::vector<size_t> rb(G), ro(G);
+  for (size_t p = 0; p < G; p++) {
+    rb[p] = size_t(c.base[p + 1] - c.base[p]) / 8;
+    ro[p] = size_t(c.base[p]) / 8;
+  }
+  comm_allgatherv2_bytes(c, owned, rb[size_t(c.rank)], c.ws_bits_glob.p, rb.data(), ro.data(), cnt, 16, all);
+  c.timing.comm_bytes += uint64_t(rb[size_t(c.rank)] + 16) * (G - 1);
   return c.ws_bits_glob.as<uint32_t>();
 }
 
@@ -3260,12 +3291,17 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   unsigned long long* const SPd = K.d + 64;
   // enqueue the gated hops from step `first` on; the compaction behind them left its counts at
   // (e, n) and its bitmap in bitsA; hop0 = the Timing::hops index of the first one
-  auto spec_enqueue = [&](int32_t first, const unsigned long long* e, const unsigned long long* n, int32_t hop0) {
+  // several ranks (piggy): instead of (e, n), cnt = this rank's (n, e) of the compaction behind
+  // the first hop; every hop's frontier allgather carries the previous hop's (n, e) of every rank
+  // to its gate (GateIn::all), one exchange per hop instead of an allgather and an all-reduce
+  auto spec_enqueue = [&](int32_t first, const unsigned long long* e, const unsigned long long* n, int32_t hop0,
+                          const unsigned long long* cnt = nullptr) {
     spec.clear();
     if (!spec_ok) return;
     const uint32_t* in = bitsA;
     uint32_t* outb = bitsB;
     const unsigned long long* pg = nullptr;
+    unsigned long long* last_blk = nullptr;
     for (int32_t st = first; st <= s.steps && spec.size() < 12; st++) {
       const bool fin = st == s.steps;
       if (fin && !fin_spec) break;
@@ -3276,7 +3312,16 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const int32_t hop = hop0 + int32_t(spec.size());
       // several ranks: the frontier bitmaps of every rank (the exchange runs whatever the gate
       // says: every rank enqueued it)
-      const uint32_t* fb = global_bits(c, in);
+      const uint32_t* fb;
+      if (cnt) {
+        unsigned long long* all = c.ws_piggy.as<unsigned long long>() + spec.size() * size_t(c.world) * 2;
+        fb = global_bits_cnt(c, in, cnt, all);
+        gi.e = gi.n = nullptr;
+        gi.all = all;
+        gi.world = c.world;
+      } else {
+        fb = global_bits(c, in);
+      }
       const size_t ia = timing_event(c);
       size_t ik;
       if (!fin) {
@@ -3296,7 +3341,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       spec.push_back(Spec{hop, fin, c.bu_kernel_name, c.bu_rest_name});
       e = blk + 1;
       n = blk + 0;
-      if (multi && !fin) {
+      last_blk = fin ? nullptr : blk;
+      if (cnt) {
+        cnt = blk;  // the next hop's exchange carries this hop's (n, e)
+      } else if (multi && !fin) {
         dev_allsum(c, blk, {0, 1}, blk + 10);
         e = blk + 11;
         n = blk + 10;
@@ -3306,7 +3354,22 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       in = outb;
       outb = const_cast<uint32_t*>(t);
     }
+    // (piggy) a chain ending on a non-final hop: its global counts for the host, at blk[12, 14)
+    if (cnt && last_blk) dev_allsum(c, last_blk, {0, 1}, last_blk + 12);
   };
+  // several ranks: the global (n, e) of speculated hop j after the fetch -- piggy: published by
+  // hop j + 1's gate (its block's [10, 12)) or, for the chain's last hop, at [12, 14); else [10, 12)
+  auto spec_global = [&](size_t j, bool piggy, unsigned long long& ng, unsigned long long& eg) {
+    const unsigned long long* hh = K.h + 64 + 16 * j;
+    if (!piggy) {
+      ng = hh[10], eg = hh[11];
+    } else if (j + 1 < spec.size()) {
+      ng = hh[16 + 10], eg = hh[16 + 11];
+    } else {
+      ng = hh[12], eg = hh[13];
+    }
+  };
+  bool piggy_used = false;
   auto spec_words = [&](int base) { return spec.empty() ? base : 64 + 16 * int(spec.size()); };
   auto spec_final = [&]() { return !spec.empty() && spec.back().final; };
   // after the fetch: record the hops that ran, as the bottom-up branch below does; stops at the
@@ -3348,8 +3411,14 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       off_ready = false;
       E = int64_t(hh[1]);
       E_known = E;
-      nset_global = int64_t(multi ? hh[10] : hh[0]);
-      Eg = multi ? int64_t(hh[11]) : E;
+      nset_global = int64_t(hh[0]);
+      Eg = E;
+      if (multi) {
+        unsigned long long ng, eg;
+        spec_global(j, piggy_used, ng, eg);
+        nset_global = int64_t(ng);
+        Eg = int64_t(eg);
+      }
       used++;
       if (nset_global == 0) break;  // the caller returns the empty result
     }
@@ -3381,9 +3450,17 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // (K.d[0, 4) are zero: k_starts_small cleared the counters)
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
                      K.d, es.odeg.as<uint32_t>());
-      // several ranks: found, next out-degree sum and hop-1 entries summed over ranks -> K.d[48, 51)
-      if (multi) dev_allsum(c, K.d, {12, 13, 41}, K.d + 48);
-      spec_enqueue(2, K.d + (multi ? 49 : 13), K.d + (multi ? 48 : 12), c.timing.n_hops + 1);  // (hop 1: below)
+      // several ranks: the counts over ranks -- piggy: carried by the first speculated hop's
+      // frontier exchange (its gate publishes them); else found, next out-degree sum and hop-1
+      // entries summed into K.d[48, 51)
+      piggy_used = multi && spec_ok && c.opt("comm_piggy", 1) != 0;
+      if (multi && !piggy_used) dev_allsum(c, K.d, {12, 13, 41}, K.d + 48);
+      spec_enqueue(2, K.d + (multi ? 49 : 13), K.d + (multi ? 48 : 12), c.timing.n_hops + 1,
+                   piggy_used ? K.d + 12 : nullptr);  // (hop 1: below)
+      if (piggy_used && spec.empty()) {  // nothing speculated (steps == 2 without the final): sum here
+        piggy_used = false;
+        dev_allsum(c, K.d, {12, 13, 41}, K.d + 48);
+      }
       // (the device work ends here when the speculated final hop runs: ev[1] ahead of the fetch)
       fetch_counters(c, K.d, spec_words(multi ? 52 : 42), K.h, spec_final() ? c.ev[1] : nullptr);
       const int64_t nF1 = int64_t(K.h[40]), E1 = int64_t(K.h[41]);
@@ -3392,13 +3469,23 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       if (E1 > 0) c.timing.expand_bytes += expand_bytes(nF1, E1, 0, EXP_MARK);
       const unsigned long long hs[8] = {(unsigned long long)nF1, (unsigned long long)E1, 0, 0, 0, 0, 0, 0};
       c.timing.hop(0, false, 0.0, hs);
-      if ((multi ? int64_t(K.h[50]) : E1) == 0) return finish_empty();  // every start lacks out-edges
+      int64_t n1g = int64_t(K.h[12]), e1g = int64_t(K.h[13]), E1g = E1;
+      if (multi && piggy_used) {  // the first speculated hop's gate published hop 1's sums
+        n1g = int64_t(K.h[64 + 10]);
+        e1g = int64_t(K.h[64 + 11]);
+        E1g = n1g;  // (no marks anywhere iff no start has out-edges: the empty result either way)
+      } else if (multi) {
+        n1g = int64_t(K.h[48]);
+        e1g = int64_t(K.h[49]);
+        E1g = int64_t(K.h[50]);
+      }
+      if (E1g == 0) return finish_empty();  // every start lacks out-edges
       nF = lazy ? 0 : int64_t(K.h[0]);
       list_n = lazy ? int64_t(K.h[14]) : -1;
       E = int64_t(K.h[13]);
       E_known = E;
-      nset_global = int64_t(K.h[multi ? 48 : 12]);
-      Eg = multi ? int64_t(K.h[49]) : E;
+      nset_global = n1g;
+      Eg = e1g;
       have_list = !lazy;
       if (lazy) cur ^= 1;  // ensure_list flips to the list buffer again
       off_ready = false;
@@ -3469,15 +3556,26 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const bool lazy = bu_ok && !multi_root && c.opt("compact_list", 0) == 0;
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
                      K.d, es.odeg.as<uint32_t>());
-      if (multi) dev_allsum(c, K.d, {12, 13}, K.d + 48);
-      if (lazy) spec_enqueue(step + 1, K.d + (multi ? 49 : 13), K.d + (multi ? 48 : 12), c.timing.n_hops);
+      piggy_used = multi && lazy && spec_ok && c.opt("comm_piggy", 1) != 0;
+      if (multi && !piggy_used) dev_allsum(c, K.d, {12, 13}, K.d + 48);
+      if (lazy)
+        spec_enqueue(step + 1, K.d + (multi ? 49 : 13), K.d + (multi ? 48 : 12), c.timing.n_hops,
+                     piggy_used ? K.d + 12 : nullptr);
+      if (piggy_used && spec.empty()) {
+        piggy_used = false;
+        dev_allsum(c, K.d, {12, 13}, K.d + 48);
+      }
       fetch_counters(c, K.d, spec_words(multi ? 50 : 16), K.h, spec_final() ? c.ev[1] : nullptr);
       nF = lazy ? 0 : int64_t(K.h[0]);
       list_n = lazy ? int64_t(K.h[14]) : -1;
       E = int64_t(K.h[13]);
       E_known = E;
-      nset_global = multi ? int64_t(K.h[48]) : int64_t(K.h[12]);
-      Eg = multi ? int64_t(K.h[49]) : E;
+      nset_global = int64_t(K.h[12]);
+      Eg = E;
+      if (multi) {
+        nset_global = int64_t(piggy_used ? K.h[64 + 10] : K.h[48]);
+        Eg = int64_t(piggy_used ? K.h[64 + 11] : K.h[49]);
+      }
       have_list = !lazy;
       if (lazy) cur ^= 1;  // ensure_list flips to the list buffer again
       off_ready = false;
