@@ -686,6 +686,23 @@ __device__ inline void block_store_partials(const unsigned long long* v, int k, 
     partials[size_t(threadIdx.x) * kAggBlocks + blockIdx.x] = s;  // slot-major: coalesced reduce
   }
 }
+// the block's sums straight into out[0, k) with no-return atomics (option bu_atomic_sums: the
+// bottom-up passes then need no k_reduce_partials launch; out starts at zero)
+__device__ inline void block_add_sums(const unsigned long long* v, int k, unsigned long long* lds,
+                                      unsigned long long* out) {
+  const int w = threadIdx.x >> 6;
+  const int nw = int(blockDim.x >> 6);
+  for (int i = 0; i < k; i++) {
+    unsigned long long s = wave_sum_u64(v[i]);
+    if ((threadIdx.x & 63) == 0) lds[i * 16 + w] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < unsigned(k)) {
+    unsigned long long s = 0;
+    for (int j = 0; j < nw; j++) s += lds[threadIdx.x * 16 + j];
+    if (s) __hip_atomic_fetch_add(out + threadIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 // sums the [kSlots][kAggBlocks] partials into out[0..kSlots) (one block of 1024 threads; all
 // kSlots loads of an iteration are independent, so the block has 8 loads in flight per lane
 // instead of one dependent chain per slot)
@@ -911,7 +928,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
                                                      const uint32_t* __restrict__ odeg, QArgs q_arg,
                                                      unsigned long long* __restrict__ partials, int cw,
                                                      const uint8_t* __restrict__ odeg8,
-                                                     unsigned long long* gate, GateIn gi) {
+                                                     unsigned long long* gate, GateIn gi, int atomic_sums) {
   if (!gate_open(gi, gate)) return;  // a speculative hop that the direction choice did not take
   __shared__ unsigned long long lds[kSlots * 16];
   extern __shared__ uint32_t s_fb[];  // [0, cw): the bitmap's hub words; [cw]: a zero word
@@ -1192,7 +1209,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
   // wave-uniform counters enter the block sums once, from lane 0
   if (lane != 0) nfound = npend = nwords = 0;
   unsigned long long acc64[8] = {nfound, odsum, nwords, npend, 0, 0, nglob, nhub};
-  block_store_partials(acc64, 8, lds, partials);
+  if (atomic_sums) block_add_sums(acc64, 8, lds, partials);
+  else block_store_partials(acc64, 8, lds, partials);
 }
 
 // Final-hop first pass with the bucket tests as unsigned range checks on the raw slot word
@@ -1227,7 +1245,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
                                                     unsigned long long* __restrict__ nbits,
                                                     unsigned long long* __restrict__ pbits, FinArgs fa_arg,
                                                     unsigned long long* __restrict__ partials, int cw,
-                                                    uint32_t fb_rest, unsigned long long* gate, GateIn gi) {
+                                                    uint32_t fb_rest, unsigned long long* gate, GateIn gi,
+                                                    int atomic_sums) {
   if (!gate_open(gi, gate)) return;  // a speculative hop that the direction choice did not take
   // dynamic LDS only, so the hub copy starts at address 0 and a probe's LDS address is its
   // clamped byte offset as it is: [0, cw) the bitmap's hub words, [cw] a zero word, then the
@@ -1394,7 +1413,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
     }
   if (lane != 0) nfound = npend = nwords = 0;
   unsigned long long acc64[8] = {nfound, 0, nwords, npend, 0, 0, 0, 0};
-  block_store_partials(acc64, 8, lds, partials);
+  if (atomic_sums) block_add_sums(acc64, 8, lds, partials);
+  else block_store_partials(acc64, 8, lds, partials);
 }
 
 // Second pass of a bottom-up hop: the rows k_bu_lean left pending.  A wave owns 64 pending-bit
@@ -1434,7 +1454,7 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
                                                           unsigned long long* partials, int cw, int ru, int rest_from,
                                                           int steps, unsigned long long* dbg,
                                                           const unsigned long long* __restrict__ gate,
-                                                          const uint4* __restrict__ rec) {
+                                                          const uint4* __restrict__ rec, int atomic_sums) {
   if (gate && *gate == 0ull) return;
   const QArgs q = q_sgpr(q_arg);
   __shared__ unsigned long long lds[kSlots * 16];
@@ -1611,7 +1631,8 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
     }
   }
   unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
-  block_store_partials(acc64, 6, lds, partials);
+  if (atomic_sums) block_add_sums(acc64, 6, lds, partials);
+  else block_store_partials(acc64, 6, lds, partials);
 }
 
 // bitmap -> compacted list.  mode 0: local rows (a top-down hop's frontier; the bitmaps this
@@ -2671,7 +2692,7 @@ FinArgs fin_args(const QArgs& q) {
 // without a memory access).
 size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
                       const FastArgs& fp, int fcol, unsigned long long* out, bool hop_front,
-                      unsigned long long* gate = nullptr, GateIn gi = GateIn{}) {
+                      unsigned long long* gate = nullptr, GateIn gi = GateIn{}, bool out_zero = false) {
   const Csr& tr = es.tr;
   if (pk != PK_NONE && pk != PK_FAST) throw Error(NBG_E_DEVICE, "bottom-up hop with a VM predicate");
   if (!es.pair_col[0].p) throw Error(NBG_E_DEVICE, "bottom-up hop without the quad slab");
@@ -2712,7 +2733,11 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   const int probe_stats = int(c.opt("bu_probe_stats", 0));  // partials [6] / [7]
   c.ws_pend.ensure(size_t(ntiles * 2 + 2) * 8);  // the pending bits, 2 words per tile
   unsigned long long* pbits = c.ws_pend.as<unsigned long long>();
-  unsigned long long* partials = c.ws_partials.as<unsigned long long>();
+  // option bu_atomic_sums: both passes add their block sums into `out` (zeroed first unless the
+  // caller's block is known zero) and no k_reduce_partials launch follows
+  const int atomic_sums = int(c.opt("bu_atomic_sums", 0) != 0 && c.opt("bu_rest_dbg", 0) == 0);
+  unsigned long long* partials = atomic_sums ? out : c.ws_partials.as<unsigned long long>();
+  if (atomic_sums && !out_zero) NBG_HIP(hipMemsetAsync(out, 0, 8 * 8, c.stream));
   auto* nb = reinterpret_cast<unsigned long long*>(nbits);
   const uint2* lo = es.pair_col[0].as<uint2>();
   const uint2* hi = es.pair_col[1].as<uint2>();
@@ -2721,7 +2746,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     if (shm > 48 * 1024)
       lds_limit(reinterpret_cast<const void*>(kern), shm);
     kern<<<grid, bs, shm, c.stream>>>(lo, hi, ntiles, work, fb, fb_bytes, nb, pbits, od, q, partials, cw,
-                                      es.odeg8.as<uint8_t>(), gate, gi);
+                                      es.odeg8.as<uint8_t>(), gate, gi, atomic_sums);
   };
   int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
   if (sel == 2 && c.opt("bu_lean_nt", 1) != 0 && (fast || es.odeg8.p)) sel = 6;  // non-temporal, 1 B degrees
@@ -2752,7 +2777,8 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     const uint32_t rest = fb_bytes > uint32_t(cw) * 4u ? fb_bytes - uint32_t(cw) * 4u : 0u;
     auto gof = [&](auto kern) {
       if (fshm > 48 * 1024) lds_limit(reinterpret_cast<const void*>(kern), fshm);
-      kern<<<grid, bs, fshm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, fa, partials, cw, rest, gate, gi);
+      kern<<<grid, bs, fshm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, fa, partials, cw, rest, gate, gi,
+                                         atomic_sums);
     };
     const int nt = int(c.opt("bu_fin_nt", 1) != 0);
     // default 49: the probe skip, one store per tile, hub-first L2 probes (r06h sweep:
@@ -2811,8 +2837,9 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   auto rest = [&](auto kern) {
     if (rshm > 48 * 1024)
       lds_limit(reinterpret_cast<const void*>(kern), rshm);
-    kern<<<grid2, 1024, rshm, c.stream>>>(pbits, rest_rows, trp, tc, fb, fb_bytes, nb, odeg, fp, q, partials + grid,
-                                          rcw, ru, rest_from, rsteps, dbg, gate, rec);
+    kern<<<grid2, 1024, rshm, c.stream>>>(pbits, rest_rows, trp, tc, fb, fb_bytes, nb, odeg, fp, q,
+                                          atomic_sums ? partials : partials + grid, rcw, ru, rest_from, rsteps, dbg,
+                                          gate, rec, atomic_sums);
   };
 #define NBG_REST(PKV, WV)                                                 \
   if (rcw > 0) {                                                          \
@@ -2834,7 +2861,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   }
 #undef NBG_REST
   NBG_HIP(hipGetLastError());
-  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid + grid2, out, gate);
+  if (!atomic_sums) k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid + grid2, out, gate);
   NBG_HIP(hipGetLastError());
   if (dbg) {
     std::vector<unsigned long long> h(size_t(grid2) * 16 * 8);
@@ -3294,10 +3321,14 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   // several ranks (piggy): instead of (e, n), cnt = this rank's (n, e) of the compaction behind
   // the first hop; every hop's frontier allgather carries the previous hop's (n, e) of every rank
   // to its gate (GateIn::all), one exchange per hop instead of an allgather and an all-reduce
+  bool spec_blocks_used = false;
   auto spec_enqueue = [&](int32_t first, const unsigned long long* e, const unsigned long long* n, int32_t hop0,
                           const unsigned long long* cnt = nullptr) {
     spec.clear();
     if (!spec_ok) return;
+    // the blocks start at zero (query start); a second chain in one query reuses them
+    if (spec_blocks_used) NBG_HIP(hipMemsetAsync(SPd, 0, 16 * 12 * 8, c.stream));
+    spec_blocks_used = true;
     const uint32_t* in = bitsA;
     uint32_t* outb = bitsB;
     const unsigned long long* pg = nullptr;
@@ -3325,12 +3356,12 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const size_t ia = timing_event(c);
       size_t ik;
       if (!fin) {
-        ik = launch_bu_lean(c, es, fb, outb, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, blk, true, blk + 8, gi);
+        ik = launch_bu_lean(c, es, fb, outb, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, blk, true, blk + 8, gi, true);
       } else {
         FastArgs tfp = fp0;
         if (fpk0.kind == PK_FAST) tfp.data = es.tr.props[size_t(fpk0.col)].data.p;
         ik = launch_bu_lean(c, es, fb, outb, nullptr, fpk0.kind, tfp, fpk0.kind == PK_FAST ? fpk0.col : -1, blk, true,
-                            blk + 8, gi);
+                            blk + 8, gi, true);
         void* vout = vid_block(spec_vids, spec_hvids);
         launch_bits_vids(c, outb, es.tr.n_rows, lo, vout, blk + 9, blk + 8);
       }

@@ -690,3 +690,28 @@ def test_host_direct_distinct_output(rmat12, spec, force):
     finally:
         for k in ("bu_spec", "bu_force", "bu_div", "host_direct"):
             sp.unset_option(k)
+
+
+@pytest.mark.parametrize("bu_div", [2, 16])
+def test_atomic_hop_sums_match(rmat12, bu_div):
+    """option bu_atomic_sums: the bottom-up passes add their block sums into the hop counters
+    with no-return atomics instead of partials + k_reduce_partials; same rows and the same hop
+    counters (found, out-degree sum, slab words, pending rows), speculated hops included"""
+    sp, st = rmat12
+    starts = sorted(set(seeds_from(12, 24, seed=43)))
+    w = X.AliasProp("follow", "weight") > 499
+    y = [X.EdgeDst("follow")]
+    sp.set_option("bu_div", bu_div)
+    try:
+        for steps in (2, 3, 4):
+            runs = []
+            for atomic in (0, 1):
+                sp.set_option("bu_atomic_sums", atomic)
+                g = sp.go(starts, steps, FOLLOW, where=w, yields=y, distinct=True)
+                hops = sp.last_timing()["hops"]
+                runs.append((np.sort(g.columns[0]), [(h["mode"], h["c"][:4]) for h in hops]))
+            assert np.array_equal(runs[0][0], runs[1][0])
+            assert runs[0][1] == runs[1][1], steps
+    finally:
+        sp.unset_option("bu_atomic_sums")
+        sp.set_option("bu_div", 4)
