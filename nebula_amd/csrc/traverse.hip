@@ -1227,6 +1227,7 @@ struct FinArgs {
   uint32_t pinv = 0, bmask = 0xfffffffcu;
 };
 constexpr uint32_t kNoProbe = 0x0ffffff0u;
+constexpr int kProbeCap = 128;  // k_bu_fin VAR bit 6: packed L2 probes per wave and tile
 // CLS 1: the candidates are every word from clo up and the passing ones every word from plo up
 // (pinv 0): the "greater than" compares, the benchmark's.  A non-candidate's offset then comes
 // from the sign of w - clo (all ones: past the bitmap and clamped to the zero word) instead of
@@ -1253,6 +1254,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
   // block's partials scratch
   extern __shared__ uint32_t s_fb[];
   unsigned long long* lds = reinterpret_cast<unsigned long long*>(s_fb + ((cw + 2) & ~1));
+  // VAR bit 6: kProbeCap words of probe scratch per wave, after the partials scratch
+  uint32_t* wscr = reinterpret_cast<uint32_t*>(lds + kSlots * 16) + (threadIdx.x >> 6) * kProbeCap;
   hub_fill(s_fb, fbits, cw, true);
   const uint32_t clo = __builtin_amdgcn_readfirstlane(fa_arg.clo), cr = __builtin_amdgcn_readfirstlane(fa_arg.cr);
   const uint32_t plo = __builtin_amdgcn_readfirstlane(fa_arg.plo), pr = __builtin_amdgcn_readfirstlane(fa_arg.pr);
@@ -1352,6 +1355,45 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
           hubf[h] = hubf[h] || (__builtin_amdgcn_ubfe(lw[h][k], w, 1u) != 0u && pass);
         }
     }
+    if (VAR & 64) {
+      // VAR bit 6: the tile's L2 probes packed into as few instructions as lanes allow -- each
+      // lane's candidates (offsets) go to the wave's LDS scratch at their rank among the tile's
+      // candidates, ceil(count / 64) full-width probe loads answer them, each lane reads its
+      // answers back (8 partly-empty probe instructions a tile became ~2)
+      uint32_t pos[2][4];
+      uint32_t T = 0;  // wave-uniform
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const bool cnd = ob[h][k] - cw4 < rest_b && !hubf[h];
+          const unsigned long long m = __ballot(cnd);
+          const uint32_t p = T + uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
+          pos[h][k] = cnd ? p : 0xffffffffu;
+          if (cnd && p < uint32_t(kProbeCap)) wscr[p] = ob[h][k] - cw4;
+          T += uint32_t(__popcll(m));
+        }
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t Tc = min(T, uint32_t(kProbeCap));
+      for (uint32_t b0 = 0; b0 < Tc; b0 += 64) {
+        const uint32_t i = b0 + uint32_t(lane);
+        const uint32_t off = i < Tc ? wscr[i] : 0xfffffff0u;
+        const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, off, 0, 0);
+        if (i < Tc) wscr[i] = w;
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const uint32_t p = pos[h][k];
+          gw[h][k] = 0u;
+          if (p < uint32_t(kProbeCap)) gw[h][k] = wscr[p];
+          else if (__ballot(p != 0xffffffffu))  // past the scratch (a rare dense tile): direct
+            gw[h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, p != 0xffffffffu ? ob[h][k] - cw4 : 0xfffffff0u, 0, 0);
+        }
+      __builtin_amdgcn_wave_barrier();
+    } else {
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
@@ -1364,6 +1406,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
           gw[h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, ob[h][k] - cw4, 0, 0);
         }
       }
+    }
     __builtin_amdgcn_sched_barrier(0);
     bool f[2], pend[2];
 #pragma unroll
@@ -2773,7 +2816,9 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     // CLS 1 ("greater than"): candidates and passing words are each one upper range
     const bool cls1 = fa.pinv == 0 && fa.cr == ~fa.clo && fa.pr == ~fa.plo && fa.clo <= 0x80000000u &&
                       fa.plo <= 0x80000000u && c.opt("bu_fin_cls", 1) != 0;
-    const size_t fshm = size_t((cw + 2) & ~1) * 4 + size_t(kSlots) * 16 * 8;
+    const int var0 = cls1 && c.opt("bu_fin_nt", 1) != 0 ? int(c.opt("bu_fin_var", 49) & 127) : 0;
+    const size_t fshm = size_t((cw + 2) & ~1) * 4 + size_t(kSlots) * 16 * 8 +
+                        ((var0 & 64) ? size_t(bs / 64) * kProbeCap * 4 : 0);
     const uint32_t rest = fb_bytes > uint32_t(cw) * 4u ? fb_bytes - uint32_t(cw) * 4u : 0u;
     auto gof = [&](auto kern) {
       if (fshm > 48 * 1024) lds_limit(reinterpret_cast<const void*>(kern), fshm);
@@ -2783,7 +2828,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     const int nt = int(c.opt("bu_fin_nt", 1) != 0);
     // default 49: the probe skip, one store per tile, hub-first L2 probes (r06h sweep:
     // k_bu_fin 124.9 -> 108.1 us; the 16-byte-lane and blocked-tile variants measured no gain)
-    const int var = cls1 && nt ? int(c.opt("bu_fin_var", 49) & 63) : 0;
+    const int var = cls1 && nt ? int(c.opt("bu_fin_var", 49) & 127) : 0;
     switch ((cls1 ? 1 : 0) | nt << 1 | var << 2) {
       case 0: gof(k_bu_fin<0, 0>); break;
       case 1: gof(k_bu_fin<1, 0>); break;
@@ -2799,6 +2844,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
       case 3 | 68: gof(k_bu_fin<1, 1, 17>); break;
       case 3 | 132: gof(k_bu_fin<1, 1, 33>); break;
       case 3 | 196: gof(k_bu_fin<1, 1, 49>); break;
+      case 3 | ((113) << 2): gof(k_bu_fin<1, 1, 113>); break;
       default: gof(k_bu_fin<1, 1, 7>); break;
     }
     snprintf(fin_nm, sizeof fin_nm, "nbg::k_bu_fin<%d, %d, %d>", cls1 ? 1 : 0, nt, var);
