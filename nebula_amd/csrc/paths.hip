@@ -671,7 +671,8 @@ __global__ void k_chunk_x(const int64_t* __restrict__ choff, int64_t nX, int32_t
 constexpr int kProbeU = 4;  // entries per lane and step of the chunked scans
 constexpr int kSwCh = 1024;
 constexpr int kSwStage = 256;
-__global__ __launch_bounds__(256) void k_sp_sweep(const uint64_t* __restrict__ X, const int64_t* __restrict__ choff,
+template <int OCC>  // waves per SIMD the register budget allows (option sp_sweep_occ: 5 or 8)
+__global__ __launch_bounds__(256, OCC) void k_sp_sweep(const uint64_t* __restrict__ X, const int64_t* __restrict__ choff,
                                                   const int32_t* __restrict__ chunk_x, int64_t nX, SpCsr gout,
                                                   SpCsr gin, uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo,
                                                   SpState st, SpBufs bf, unsigned long long* cnt) {
@@ -788,7 +789,8 @@ __global__ void k_sp_chunks(const int64_t* Xdeg, int64_t nX, int64_t* ch) {
 // side (depth l_o + 1: the vertex is then seen by both sides, as after an expansion of the other
 // side) and records that claim in slot[c] (an arena tuple); k_sp_gather_meets turns the slots into
 // the meet list without a global atomic per meet.
-__global__ __launch_bounds__(256) void k_sp_probe(const uint64_t* __restrict__ X, int64_t nX,
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void k_sp_probe(const uint64_t* __restrict__ X, int64_t nX,
                                                   const int64_t* __restrict__ choff,
                                                   const int32_t* __restrict__ chunk_x, SpCsr g0, SpCsr g1, uint8_t* d0,
                                                   uint8_t* d1, int64_t n, int64_t lo, SpState st, uint64_t* slot,
@@ -1553,8 +1555,12 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         DevBuf chx;
         chx.alloc(size_t(max_chunks) * 4);
         k_chunk_x<<<grid_n(nX), 256, 0, c.stream>>>(choff.as<int64_t>(), nX, chx.as<int32_t>());
-        k_sp_probe<<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), chx.as<int32_t>(), gout,
-                                                gin, d0, d1, n, lo, st, slot.as<uint64_t>(), cnt);
+        if (c.opt("sp_probe_occ", 7) >= 8)
+          k_sp_probe<8><<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), chx.as<int32_t>(),
+                                                     gout, gin, d0, d1, n, lo, st, slot.as<uint64_t>(), cnt);
+        else
+          k_sp_probe<1><<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), chx.as<int32_t>(),
+                                                     gout, gin, d0, d1, n, lo, st, slot.as<uint64_t>(), cnt);
         k_sp_gather_meets<<<grid_n(max_chunks), 256, 0, c.stream>>>(slot.as<uint64_t>(), max_chunks, st, bf, cnt);
         k_sp_probe_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, iter);
         k_sp_drop<<<grid_n(nX), 256, 0, c.stream>>>(W.X.as<uint64_t>(), W.Xdeg.as<int64_t>(), nX, st, cnt);
@@ -1701,8 +1707,16 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         hipEventRecord(c.ev[2], c.stream);
         k_chunk_x<<<grid_n(nX), 256, 0, c.stream>>>(choff.as<int64_t>(), nX, chx.as<int32_t>());
         const int sgrid = int(std::max<int64_t>(1, std::min<int64_t>((max_ch + 3) / 4, c.opt("sp_sweep_grid", 8192))));
-        k_sp_sweep<<<sgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), choff.as<int64_t>(), chx.as<int32_t>(),
-                                                 nX, gout, gin, d0, d1, n, lo, st, bf, cnt);
+        const int64_t socc = c.opt("sp_sweep_occ", 5);
+        if (socc >= 8)
+          k_sp_sweep<8><<<sgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), choff.as<int64_t>(), chx.as<int32_t>(), nX,
+                                                      gout, gin, d0, d1, n, lo, st, bf, cnt);
+        else if (socc >= 6)
+          k_sp_sweep<6><<<sgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), choff.as<int64_t>(), chx.as<int32_t>(), nX,
+                                                      gout, gin, d0, d1, n, lo, st, bf, cnt);
+        else
+          k_sp_sweep<1><<<sgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), choff.as<int64_t>(), chx.as<int32_t>(), nX,
+                                                      gout, gin, d0, d1, n, lo, st, bf, cnt);
         NBG_HIP(hipGetLastError());
         hipEventRecord(c.ev[3], c.stream);
       } else {

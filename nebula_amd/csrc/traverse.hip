@@ -2778,7 +2778,8 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   unsigned long long* pbits = c.ws_pend.as<unsigned long long>();
   // option bu_atomic_sums: both passes add their block sums into `out` (zeroed first unless the
   // caller's block is known zero) and no k_reduce_partials launch follows
-  const int atomic_sums = int(c.opt("bu_atomic_sums", 0) != 0 && c.opt("bu_rest_dbg", 0) == 0);
+  // (r06j: 0.4796 -> 0.4663 ms per C3 query, the two k_reduce_partials launches gone)
+  const int atomic_sums = int(c.opt("bu_atomic_sums", 1) != 0 && c.opt("bu_rest_dbg", 0) == 0);
   unsigned long long* partials = atomic_sums ? out : c.ws_partials.as<unsigned long long>();
   if (atomic_sums && !out_zero) NBG_HIP(hipMemsetAsync(out, 0, 8 * 8, c.stream));
   auto* nb = reinterpret_cast<unsigned long long*>(nbits);
@@ -2793,7 +2794,9 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   };
   int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
   if (sel == 2 && c.opt("bu_lean_nt", 1) != 0 && (fast || es.odeg8.p)) sel = 6;  // non-temporal, 1 B degrees
-  const int64_t lskip = c.opt("bu_lean_skip", 1);
+  // default 3: the probe skip and hub-first L2 probes (r06j: 100.7 -> 91.6 us at C3 hop 2; the
+  // wide-lane layouts 5 / 7 measured 104.7-105 us)
+  const int64_t lskip = c.opt("bu_lean_skip", 3);
   if (sel == 6 && lskip != 0) sel = lskip == 3 ? 8 : lskip == 7 ? 9 : lskip == 5 ? 10 : 7;  // + probe skip
 #define NBG_LEAN(PKV)                                \
   switch (sel) {                                     \
@@ -3330,7 +3333,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   // option host_direct: a DISTINCT _dst result that goes to the host is written by the bottom-up
   // output kernel straight into pinned host memory (mapped into the device's address space), so
   // the hand-out copies nothing
-  const bool host_direct = !s.keep_on_device && c.opt("host_direct", 0) != 0;
+  // (r06j: stores from the device reach 54.6 GB/s into pinned host memory, hipMemcpyAsync 29.7:
+  // C3's 173 MB hand-out 7.4 -> 3.8 ms end to end)
+  const bool host_direct = !s.keep_on_device && c.opt("host_direct", 1) != 0;
   HostBuf spec_hvids;
   auto vid_block = [&](DevBuf& d, HostBuf& hb) -> void* {
     if (host_direct) {
