@@ -3340,6 +3340,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   auto vid_block = [&](DevBuf& d, HostBuf& hb) -> void* {
     if (host_direct) {
       host_pool_cap(c);
+      hb.release();  // (a second speculation chain in one query replaces the first's block)
       hb.alloc(c.host_pool, size_t(c.n_global + 64) * 8);
       return hb.p;
     }
