@@ -316,48 +316,112 @@ __global__ void k_sp_regen(int mode, int side, int32_t j, const int32_t* plist, 
   }
 }
 
+// Block-wide reservation in two lists at once (256-thread blocks, block-uniform call): a thread
+// asks for na slots of list A and nb of list B (each < 2^16 per block); returns its first slot
+// in each.  One returning atomic per list and block: a counter takes ~90 returning atomics per us
+// on one address, so the per-wave appends of a 748 K-tuple select (two lists, ~23 K atomics)
+// had held it at ~75 us.
+constexpr int kBlk = 256;
+__device__ inline void blk_reserve2(unsigned long long* ca, unsigned long long* cb, uint32_t na, uint32_t nb,
+                                    unsigned long long& oa, unsigned long long& ob) {
+  __shared__ uint32_t s_w[kBlk / 64];
+  __shared__ unsigned long long s_base[2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t x = na | (nb << 16);
+  uint32_t v = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(v, o);
+    if (lane >= o) v += y;
+  }
+  if (lane == 63) s_w[w] = v;
+  __syncthreads();
+  uint32_t pre = v - x, tot = 0;
+#pragma unroll
+  for (int i = 0; i < kBlk / 64; i++) {
+    if (i < w) pre += s_w[i];
+    tot += s_w[i];
+  }
+  if (threadIdx.x == 0) {
+    s_base[0] = (tot & 0xFFFFu) ? atomicAdd(ca, (unsigned long long)(tot & 0xFFFFu)) : 0ull;
+    s_base[1] = (tot >> 16) ? atomicAdd(cb, (unsigned long long)(tot >> 16)) : 0ull;
+  }
+  __syncthreads();
+  oa = s_base[0] + (pre & 0xFFFFu);
+  ob = s_base[1] + (pre >> 16);
+  __syncthreads();  // s_w / s_base are reused by the next call
+}
+
 // split a live list: tuples of the side their pair expands now -> X (with degrees), the rest
 // of still-active pairs -> carried into the next live list.  sweep = 1: the list holds sweep
-// tuples; those of MET pairs short of src go to X.
-__global__ void k_sp_select(const uint64_t* __restrict__ live, int64_t nl, int32_t sweep, SpState st, SpCsr gout,
-                            SpCsr gin, uint64_t* X, int64_t* Xdeg, int64_t cap_x, SpBufs bf,
-                            unsigned long long* cnt, const int32_t* push_pair = nullptr) {
-  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-  const int64_t rounds = (nl + stride - 1) / stride;
-  for (int64_t r = 0; r < rounds; r++) {
-    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-    bool go = false, stay = false;
-    uint64_t t = 0;
-    uint32_t side = 0;
-    int64_t d = 0;
-    if (i < nl) {
-      t = live[i];
-      const uint32_t p = t_pair(t);
-      side = t_side(t);
-      const int32_t s = st.state[p];
+// tuples; those of MET pairs short of src go to X.  kSelIt tuples per thread (their loads in
+// flight together), one reservation per block and round.
+constexpr int kSelIt = 8;
+int grid_sel(int64_t n) { return int(std::max<int64_t>(1, std::min<int64_t>((n + kBlk * kSelIt - 1) / (kBlk * kSelIt), 4096))); }
+__global__ __launch_bounds__(kBlk) void k_sp_select(const uint64_t* __restrict__ live, int64_t nl, int32_t sweep,
+                                                    SpState st, SpCsr gout, SpCsr gin, uint64_t* X, int64_t* Xdeg,
+                                                    int64_t cap_x, SpBufs bf, unsigned long long* cnt,
+                                                    const int32_t* push_pair = nullptr) {
+  constexpr int64_t per = int64_t(kBlk) * kSelIt;
+  const int64_t rounds = (nl + per - 1) / per;
+  // carried tuples: every tuple of one launch has the same side (one list per side)
+  const uint32_t side = nl > 0 ? t_side(live[0]) : 0u;
+  uint64_t* const carry = bf.live_next[side];
+  const int64_t cap_carry = bf.cap_live[side];
+  const SpCsr& g = side ? gin : gout;
+  for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
+    const int64_t i0 = r * per + threadIdx.x;
+    uint64_t t[kSelIt];
+    int32_t s[kSelIt];
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) t[u] = i0 + u * kBlk < nl ? live[i0 + u * kBlk] : ~0ull;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) s[u] = t[u] != ~0ull ? st.state[t_pair(t[u])] : SP_DONE;
+    uint32_t gm = 0, sm = 0;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      if (t[u] == ~0ull) continue;
+      const uint32_t p = t_pair(t[u]);
       if (sweep) {
         // sweep = 2: stop one level short of src (the walk from src never reads dist_B(src),
         // and the in-lists of src's shortest-path out-neighbours are typically hub rows)
-        go = s == SP_MET && int32_t(t_lvl(t)) < st.res[p] - (sweep - 1) && !(push_pair && push_pair[p]);
-      } else if (s == SP_ACTIVE) {
-        go = uint32_t(st.side[p]) == side;
-        stay = !go;
-      }
-      if (go) d = sp_deg(side ? gin : gout, t_row(t));
-    }
-    const int64_t xs = wave_append(cnt + C_X, go);
-    if (go) {
-      if (xs < cap_x) {
-        X[xs] = t;
-        Xdeg[xs] = d;
-      } else {
-        atomicOr(cnt + C_OVF, 2ull);
+        if (s[u] == SP_MET && int32_t(t_lvl(t[u])) < st.res[p] - (sweep - 1) && !(push_pair && push_pair[p]))
+          gm |= 1u << u;
+      } else if (s[u] == SP_ACTIVE) {
+        if (uint32_t(st.side[p]) == side) gm |= 1u << u;
+        else sm |= 1u << u;
       }
     }
-    const unsigned long long e = wsum((unsigned long long)d);
+    int64_t d[kSelIt];
+    unsigned long long dsum = 0;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      d[u] = (gm >> u) & 1u ? sp_deg(g, t_row(t[u])) : 0;
+      dsum += (unsigned long long)d[u];
+    }
+    unsigned long long ox, oc;
+    blk_reserve2(cnt + C_X, cnt + (side ? C_LIVE1 : C_LIVE0), uint32_t(__popc(gm)), uint32_t(__popc(sm)), ox, oc);
+    bool ovf_x = false, ovf_c = false;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      if ((gm >> u) & 1u) {
+        if (int64_t(ox) < cap_x) {
+          X[ox] = t[u];
+          Xdeg[ox] = d[u];
+        } else {
+          ovf_x = true;
+        }
+        ox++;
+      } else if ((sm >> u) & 1u) {
+        if (int64_t(oc) < cap_carry) carry[oc] = t[u];
+        else ovf_c = true;
+        oc++;
+      }
+    }
+    if (ovf_x) atomicOr(cnt + C_OVF, 2ull);
+    if (ovf_c) atomicOr(cnt + C_OVF, 1ull);
+    const unsigned long long e = wsum(dsum);
     if ((threadIdx.x & 63) == 0 && e) atomicAdd(cnt + C_XE, e);
-    // carried tuples: every tuple of one launch has the same side (one list per side)
-    put(bf.live_next[side], bf.cap_live[side], cnt, side ? C_LIVE1 : C_LIVE0, stay, t);
   }
 }
 
@@ -847,23 +911,38 @@ __global__ __launch_bounds__(256, OCC) void k_sp_probe(const uint64_t* __restric
 
 // slots -> meet list (1, p, dt, r) + arena (the claimed byte).  Runs before k_sp_probe_step, so
 // lvl still holds the depths the probe compared against.
-__global__ void k_sp_gather_meets(const uint64_t* slot, int64_t m, SpState st, SpBufs bf, unsigned long long* cnt) {
-  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-  const int64_t rounds = (m + stride - 1) / stride;
-  for (int64_t r = 0; r < rounds; r++) {
-    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-    const uint64_t t = i < m ? slot[i] : ~0ull;
-    const bool ok = t != ~0ull;
-    uint64_t mt = 0;
-    if (ok) {
-      const uint32_t p = t_pair(t);
+__global__ __launch_bounds__(kBlk) void k_sp_gather_meets(const uint64_t* slot, int64_t m, SpState st, SpBufs bf,
+                                                          unsigned long long* cnt) {
+  constexpr int64_t per = int64_t(kBlk) * kSelIt;
+  const int64_t rounds = (m + per - 1) / per;
+  for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
+    const int64_t i0 = r * per + threadIdx.x;
+    uint64_t t[kSelIt];
+    uint32_t k = 0;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      t[u] = i0 + u * kBlk < m ? slot[i0 + u * kBlk] : ~0ull;
+      k += t[u] != ~0ull ? 1u : 0u;
+    }
+    unsigned long long om, oa;
+    blk_reserve2(cnt + C_MEET, cnt + C_ARENA, k, k, om, oa);
+    bool ovf = false;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      if (t[u] == ~0ull) continue;
+      const uint32_t p = t_pair(t[u]);
       // claimed backward byte: r has dt = its new depth; claimed forward byte: r is on the
       // backward frontier (dt = the backward depth)
-      mt = t_side(t) ? mk_tup(1, p, t_lvl(t), t_row(t))
-                     : mk_tup(1, p, uint32_t(st.lvl[uint32_t(st.B) + p]), t_row(t));
+      const uint64_t mt = t_side(t[u]) ? mk_tup(1, p, t_lvl(t[u]), t_row(t[u]))
+                                       : mk_tup(1, p, uint32_t(st.lvl[uint32_t(st.B) + p]), t_row(t[u]));
+      if (int64_t(om) < bf.cap_meet) bf.meet[om] = mt;
+      else ovf = true;
+      if (int64_t(oa) < bf.cap_arena) bf.arena[oa] = t[u];
+      else ovf = true;
+      om++;
+      oa++;
     }
-    put(bf.meet, bf.cap_meet, cnt, C_MEET, ok, mt);
-    put(bf.arena, bf.cap_arena, cnt, C_ARENA, ok, t);
+    if (ovf) atomicOr(cnt + C_OVF, 1ull);
   }
 }
 
@@ -1462,7 +1541,9 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
                                         hc[C_MEET], (unsigned long long)it, (unsigned long long)act, diag[0], diag[1]};
       diag[0] = diag[1] = 0;
       c.timing.hop(mode, false, ms, c8);
-      c.timing.name_last_hop(mode == 3 ? "nbg::(anonymous namespace)::k_sp_probe" : "nbg::(anonymous namespace)::k_sp_expand");
+      c.timing.name_last_hop(mode == 3   ? "nbg::(anonymous namespace)::k_sp_probe"
+                             : mode == 4 && c.opt("sp_sweep_chunks", 1) != 0 ? "nbg::(anonymous namespace)::k_sp_sweep"
+                                                                             : "nbg::(anonymous namespace)::k_sp_expand");
     };
     // pairs (of this batch) matching a host predicate over (state, pside, met) -> W.plist
     auto pair_list = [&](auto pred) -> int32_t {
@@ -1520,7 +1601,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       zero(1u << C_LIVE0 | 1u << C_LIVE1 | 1u << C_X | 1u << C_ACTIVE | 1u << C_OVF | 1u << C_XE);
       for (int s = 0; s < 2; s++)
         if (n_live[s])
-          k_sp_select<<<grid_n(n_live[s]), 256, 0, c.stream>>>(W.live[s].as<uint64_t>(), n_live[s], 0, st, gout, gin,
+          k_sp_select<<<grid_sel(n_live[s]), kBlk, 0, c.stream>>>(W.live[s].as<uint64_t>(), n_live[s], 0, st, gout, gin,
                                                                  W.X.as<uint64_t>(), W.Xdeg.as<int64_t>(), W.cap_x, bf,
                                                                  cnt);
       NBG_HIP(hipGetLastError());
@@ -1529,14 +1610,20 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       const int64_t nX = int64_t(hc[C_X]);
       int64_t E = int64_t(hc[C_XE]);
       const int64_t carried[2] = {int64_t(hc[C_LIVE0]), int64_t(hc[C_LIVE1])};
-      if (E > 0 && probe) {
+      // The probe's results (meets, claims, the dropped pairs' degrees) are read with the
+      // iteration's last counter fetch: the expansion is sized by the pre-probe E (an upper
+      // bound; it reads its own E from the scan on the device) and the lists keep room for
+      // every probe claim, so no round trip separates the probe from the expansion.
+      DevBuf ch, choff, slot, chx;  // live until the fetch below (stream-ordered reuse aside)
+      int64_t max_chunks = 0;
+      const bool probed = E > 0 && probe;
+      if (probed) {
         // meet probe: pairs one edge short of meeting skip this iteration's expansion
-        const int64_t max_chunks = nX + E / kProbeCh + 64;
+        max_chunks = nX + E / kProbeCh + 64;
         hash_fit(st, int64_t(hc[C_ARENA]) + max_chunks);
         reserve(c, W.meet, W.cap_meet, n_meet + max_chunks, n_meet);
         if (!arena_lost) reserve(c, W.arena, W.cap_arena, n_arena + max_chunks, n_arena);
         refresh(nullptr, 0);
-        DevBuf ch, choff, slot;
         ch.alloc(size_t(nX + 1) * 8);
         choff.alloc(size_t(nX + 1) * 8);
         slot.alloc(size_t(max_chunks) * 8);
@@ -1552,7 +1639,6 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         hipEventRecord(c.ev[4], c.stream);
         const int pgrid =
             int(std::max<int64_t>(1, std::min<int64_t>((max_chunks + 3) / 4, c.opt("sp_probe_grid", 4096))));
-        DevBuf chx;
         chx.alloc(size_t(max_chunks) * 4);
         k_chunk_x<<<grid_n(nX), 256, 0, c.stream>>>(choff.as<int64_t>(), nX, chx.as<int32_t>());
         if (c.opt("sp_probe_occ", 7) >= 8)
@@ -1561,12 +1647,30 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         else
           k_sp_probe<1><<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), chx.as<int32_t>(),
                                                      gout, gin, d0, d1, n, lo, st, slot.as<uint64_t>(), cnt);
-        k_sp_gather_meets<<<grid_n(max_chunks), 256, 0, c.stream>>>(slot.as<uint64_t>(), max_chunks, st, bf, cnt);
+        k_sp_gather_meets<<<grid_sel(max_chunks), kBlk, 0, c.stream>>>(slot.as<uint64_t>(), max_chunks, st, bf, cnt);
         k_sp_probe_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, iter);
         k_sp_drop<<<grid_n(nX), 256, 0, c.stream>>>(W.X.as<uint64_t>(), W.Xdeg.as<int64_t>(), nX, st, cnt);
         NBG_HIP(hipGetLastError());
         hipEventRecord(c.ev[5], c.stream);
-        sync_counters();
+      }
+      // the probe's meets and claims are at most one per chunk
+      const int64_t meet_keep = n_meet + max_chunks, arena_keep = n_arena + max_chunks;
+      if (E > 0) {
+        // lists sized for min(every edge claims, a soft bound); an overflow is rebuilt below
+        const int64_t want = std::min<int64_t>(E, std::max<int64_t>(soft, 2 * last_claims)) + 64;
+        for (int s = 0; s < 2; s++) reserve(c, W.live_next[s], W.cap_next[s], carried[s] + want, carried[s]);
+        if (!arena_lost)
+          reserve(c, W.arena, W.cap_arena, arena_keep + want, std::min<int64_t>(arena_keep, W.cap_arena));
+        reserve(c, W.meet, W.cap_meet, meet_keep + std::min<int64_t>(E, soft) + 64, std::min<int64_t>(meet_keep, W.cap_meet));
+        refresh(nullptr, 0);
+        hash_fit(st, int64_t(hc[C_ARENA]) + max_chunks + E);
+        launch_scan(nX);
+        launch_expand(nX, E, 0);
+      }
+      k_sp_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, max_steps, 0, iter, cnt);
+      NBG_HIP(hipGetLastError());
+      sync_counters();
+      if (probed) {
         float pms = 0;
         hipEventElapsedTime(&pms, c.ev[4], c.ev[5]);
         c.timing.expand_ms += pms;
@@ -1574,27 +1678,11 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         c.timing.edges_scanned += hc[C_PE];
         c.timing.expand_bytes += uint64_t(nX) * 24 + hc[C_PE] * 5;
         sp_hop(3, pms, nX, int64_t(hc[C_PE]), 0, iter, active);
-        E = int64_t(hc[C_XE]);
-        n_meet = int64_t(hc[C_MEET]);
-        if (int64_t(hc[C_ARENA]) > W.cap_arena) arena_lost = true;
-        n_arena = std::min<int64_t>(int64_t(hc[C_ARENA]), W.cap_arena);
       }
+      const bool launched = E > 0;
+      E = int64_t(hc[C_XE]);  // after the probe's drops: the expansion's own E
       c.timing.edges_scanned += uint64_t(E);
-      if (E > 0) {
-        // lists sized for min(every edge claims, a soft bound); an overflow is rebuilt below
-        const int64_t want = std::min<int64_t>(E, std::max<int64_t>(soft, 2 * last_claims)) + 64;
-        for (int s = 0; s < 2; s++) reserve(c, W.live_next[s], W.cap_next[s], carried[s] + want, carried[s]);
-        if (!arena_lost) reserve(c, W.arena, W.cap_arena, n_arena + want, n_arena);
-        reserve(c, W.meet, W.cap_meet, n_meet + std::min<int64_t>(E, soft) + 64, n_meet);
-        refresh(nullptr, 0);
-        hash_fit(st, int64_t(hc[C_ARENA]) + E);
-        launch_scan(nX);
-        launch_expand(nX, E, 0);
-      }
-      k_sp_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, max_steps, 0, iter, cnt);
-      NBG_HIP(hipGetLastError());
-      sync_counters();
-      const double ems = E > 0 ? expand_time() : 0.0;
+      const double ems = launched && E > 0 ? expand_time() : 0.0;
       const int64_t cl = int64_t(hc[C_LIVE0] + hc[C_LIVE1]) - carried[0] - carried[1];
       last_claims = cl;
       c.timing.expand_bytes += uint64_t(nX) * 32 + uint64_t(E) * 5 + uint64_t(cl) * 26;
@@ -1660,7 +1748,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
                                                                     pushc);
         k_sweep_choose<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(pullc, pushc, int32_t(nb), push_pair);
       }
-      k_sp_select<<<grid_n(n_sw), 256, 0, c.stream>>>(cur->as<uint64_t>(), n_sw, sweep_mode, st, gout, gin, W.X.as<uint64_t>(),
+      k_sp_select<<<grid_sel(n_sw), kBlk, 0, c.stream>>>(cur->as<uint64_t>(), n_sw, sweep_mode, st, gout, gin, W.X.as<uint64_t>(),
                                                        W.Xdeg.as<int64_t>(), W.cap_x, bf, cnt,
                                                        push_now ? push_pair : nullptr);
       if (push_now && n_arena)

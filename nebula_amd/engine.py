@@ -397,23 +397,31 @@ class GraphSpace:
             off = np.ctypeslib.as_array(rows.path_offsets, shape=(n + 1,)).copy() if n else np.zeros(1, np.int64)
             tot = int(off[-1])
             vids = (np.ctypeslib.as_array(rows.path_vids, shape=(tot,)).copy() if tot else np.zeros(0, np.int64))
-            paths = [vids[off[i]:off[i + 1]] for i in range(n)]
             # with world_size > 1 this rank answers pairs rank, rank + world, ... (columns 0 / 1)
             rs = np.ctypeslib.as_array(C.cast(rows.cols[0], C.POINTER(C.c_int64)), shape=(n,)).copy() if n else src[:0]
             rd = np.ctypeslib.as_array(C.cast(rows.cols[1], C.POINTER(C.c_int64)), shape=(n,)).copy() if n else dst[:0]
-            return PathResult(rs, rd, hops, paths, int(rows.edges_scanned))
+            return PathResult(rs, rd, hops, vids, off, int(rows.edges_scanned))
         finally:
             self.L.nbg_rows_free(C.byref(rows))
 
 
 @dataclass
 class PathResult:
-    """FIND SHORTEST PATH result: per pair the hop count (-1 = unreachable) and the path."""
+    """FIND SHORTEST PATH result: per pair the hop count (-1 = unreachable) and the path (pair
+    i's vids are path_vids[path_offsets[i]:path_offsets[i + 1]]; `paths` slices them on first use)."""
     src: np.ndarray
     dst: np.ndarray
     hops: np.ndarray
-    paths: list
+    path_vids: np.ndarray
+    path_offsets: np.ndarray
     edges_scanned: int = 0
+
+    @property
+    def paths(self):
+        if not hasattr(self, "_paths"):
+            v, o = self.path_vids, self.path_offsets
+            self._paths = [v[o[i]:o[i + 1]] for i in range(len(self.hops))]
+        return self._paths
 
     def rows(self):
         return [(int(s), int(d), int(h), tuple(int(v) for v in p))

@@ -11,7 +11,7 @@ def main():
     for path in sys.argv[1:]:
         with open(path) as f:
             for r in csv.DictReader(f):
-                k = r["Kernel_Name"].split("(")[0][:60]
+                k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:60]
                 acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[k].add(r["Dispatch_Id"])
     rows = sorted(acc.items(), key=lambda kv: -max(kv[1].values()))
