@@ -1843,7 +1843,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     const size_t base = hpath.size();
     hpath.resize(base + size_t(plen));
     if (plen > 0) {
-      DevBuf doff, dpath;
+      DevBuf doff, dpath, wk;  // (wk: the walk state, drained by the path copy's fetch below)
       doff.alloc(size_t(nb + 1) * 8);
       dpath.alloc(size_t(plen) * 8);
       NBG_HIP(hipMemcpyAsync(doff.p, boff.data(), size_t(nb + 1) * 8, hipMemcpyHostToDevice, c.stream));
@@ -1859,7 +1859,6 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         const int64_t max_tiles = (cout->nnz + kTileE - 1) / kTileE + nb + 2;
         const size_t wbytes = size_t(nb) * 4 + 64 + size_t(nb) * 8 + 64 + 2 * (size_t(nb + 1) * 8 + 64) +
                               size_t(max_tiles) * 4 + 64;
-        DevBuf wk;
         wk.alloc(wbytes);
         char* q = static_cast<char*>(wk.p);
         auto take = [&](size_t b) { char* r = q; q += (b + 63) & ~size_t(63); return r; };
@@ -1885,7 +1884,6 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
               c.ht_vals.as<int32_t>(), uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, lo, cnt);
           NBG_HIP(hipGetLastError());
         }
-        sync_counters();  // wk is released at scope end: the walk must have drained
       }
       NBG_HIP(hipGetLastError());
       NBG_HIP(hipMemcpyAsync(hpath.data() + base, dpath.p, size_t(plen) * 8, hipMemcpyDeviceToHost, c.stream));

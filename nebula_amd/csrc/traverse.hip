@@ -970,21 +970,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
     }
   };
   auto bit = [](uint32_t w, uint32_t sw) -> uint32_t { return __builtin_amdgcn_ubfe(w, sw & 31u, 1u); };
-  // SKIP bit 2 (WIDE, non-final hops): lane l holds rows 2l (h 0) and 2l + 1 (h 1) of a tile,
-  // so the slab's first half is one 16-byte load per lane and the 1-byte degrees one 2-byte load
-  // (the 8-byte and 1-byte loads of the row-per-lane layout made this pass instruction-bound:
-  // two slab and two degree loads per 128 rows for 1.1 KB); the ballots of the even and odd rows
-  // are interleaved back into the tile's row-order words, stored with one instruction
-  constexpr bool WIDE = (SKIP & 4) && !FINAL && U == 1 && NT;
-  auto row_of = [&](int64_t t, int h) -> int64_t { return WIDE ? t * 128 + 2 * lane + h : t * 128 + lane + 64 * h; };
-  auto spread = [](uint64_t x) -> uint64_t {  // bit i -> bit 2i (32 -> 64 bits)
-    x &= 0xffffffffull;
-    x = (x | (x << 16)) & 0x0000ffff0000ffffull;
-    x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
-    x = (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
-    x = (x | (x << 2)) & 0x3333333333333333ull;
-    return (x | (x << 1)) & 0x5555555555555555ull;
-  };
+  // (a 16-byte-lane layout, lane l holding rows 2l and 2l + 1, measured 104.7 us against 91.6)
+  auto row_of = [&](int64_t t, int h) -> int64_t { return t * 128 + lane + 64 * h; };
   for (int64_t t0 = wave * U; t0 < work_tiles; t0 += nwaves * U) {
     uint2 a[U][2], b[U][2];
     uint32_t od[U][2];
@@ -993,17 +980,6 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
     for (int u = 0; u < U; u++) {
       v[u] = t0 + u < work_tiles;
       const int64_t r = (v[u] ? t0 + u : t0) * 128 + lane;  // a past-the-end tile re-reads t0 (discarded)
-      if (WIDE) {
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const int64_t tt = v[u] ? t0 + u : t0;
-        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(lo) + tt * 64 + lane);
-        a[u][0] = make_uint2(x.x, x.y);
-        a[u][1] = make_uint2(x.z, x.w);
-        const uint32_t o2 = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(odeg8 + tt * 128) + lane);
-        od[u][0] = o2 & 0xffu;
-        od[u][1] = o2 >> 8;
-        continue;
-      }
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         if (NT) {  // the slab and degrees are read once per hop: keep L2 for the bitmap probes
@@ -1173,11 +1149,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
       const int64_t t = t0 + u;
       unsigned long long f0 = __ballot(f[u][0]), f1 = __ballot(f[u][1]);
       unsigned long long p0 = __ballot(pend[u][0]), p1 = __ballot(pend[u][1]);
-      if (WIDE) {
-        const unsigned long long w0 = spread(f0) | (spread(f1) << 1), w1 = spread(f0 >> 32) | (spread(f1 >> 32) << 1);
-        const unsigned long long q0 = spread(p0) | (spread(p1) << 1), q1 = spread(p0 >> 32) | (spread(p1 >> 32) << 1);
-        f0 = w0, f1 = w1, p0 = q0, p1 = q1;
-        if (lane < 2) {  // lane 0 the two next-frontier words, lane 1 the two pending words
+      if (SKIP & 4) {  // one store: lane 0 the tile's two next-frontier words, lane 1 the pending ones
+        if (lane < 2) {
           typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
           u64x2 vv;
           vv.x = lane ? p0 : f0;
@@ -1227,7 +1200,6 @@ struct FinArgs {
   uint32_t pinv = 0, bmask = 0xfffffffcu;
 };
 constexpr uint32_t kNoProbe = 0x0ffffff0u;
-constexpr int kProbeCap = 128;  // k_bu_fin VAR bit 6: packed L2 probes per wave and tile
 // CLS 1: the candidates are every word from clo up and the passing ones every word from plo up
 // (pinv 0): the "greater than" compares, the benchmark's.  A non-candidate's offset then comes
 // from the sign of w - clo (all ones: past the bitmap and clamped to the zero word) instead of
@@ -1236,9 +1208,11 @@ constexpr int kProbeCap = 128;  // k_bu_fin VAR bit 6: packed L2 probes per wave
 // in L2): 158 -> 148 us at C3.  Measured without gain (r04f/r04g): the next tile's slab loads
 // issued behind the current tile's probes, an interleaved 16-byte slab (one load per row), two
 // tiles per wave; with no probes at all the slab alone streams at 4.7 TB/s in this loop.
-// VAR (measurement variants): bit 0 -- a probe instruction is issued only when some lane of the
-// wave has an L2 candidate in that slot; bit 1 -- each wave takes a contiguous range of tiles;
-// bit 2 -- the same skip for the LDS hub reads
+// VAR: bit 0 -- a probe instruction is issued only when some lane of the wave has an L2
+// candidate in that slot; bit 4 -- one 16-byte store of the tile's next / pending words; bit 5 --
+// rows a hub word already found send no L2 probe.  Measured without gain and removed (r06e-r06h):
+// contiguous tile ranges per wave, the same skip for the LDS reads, 16-byte lanes (rows 2l and
+// 2l + 1 per lane), the tile's L2 probes packed into the fewest lanes through an LDS scratch.
 template <int CLS, int NT, int VAR = 0>
 __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo, const uint2* __restrict__ hi,
                                                     int64_t ntiles, int64_t work_tiles,
@@ -1254,8 +1228,6 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
   // block's partials scratch
   extern __shared__ uint32_t s_fb[];
   unsigned long long* lds = reinterpret_cast<unsigned long long*>(s_fb + ((cw + 2) & ~1));
-  // VAR bit 6: kProbeCap words of probe scratch per wave, after the partials scratch
-  uint32_t* wscr = reinterpret_cast<uint32_t*>(lds + kSlots * 16) + (threadIdx.x >> 6) * kProbeCap;
   hub_fill(s_fb, fbits, cw, true);
   const uint32_t clo = __builtin_amdgcn_readfirstlane(fa_arg.clo), cr = __builtin_amdgcn_readfirstlane(fa_arg.cr);
   const uint32_t plo = __builtin_amdgcn_readfirstlane(fa_arg.plo), pr = __builtin_amdgcn_readfirstlane(fa_arg.pr);
@@ -1279,17 +1251,6 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
     return make_uint2(uint32_t(x), uint32_t(x >> 32));
   };
   auto load = [&](int64_t t, uint32_t (&sw)[2][4]) {
-    if (VAR & 8) {
-      // 16-byte lanes: lane l holds rows 2l (h 0) and 2l + 1 (h 1) of the tile, one load per half
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      const u32x4* l4 = reinterpret_cast<const u32x4*>(lo) + t * 64 + lane;
-      const u32x4* h4 = reinterpret_cast<const u32x4*>(hi) + t * 64 + lane;
-      const u32x4 a = NT ? __builtin_nontemporal_load(l4) : *l4;
-      const u32x4 b = NT ? __builtin_nontemporal_load(h4) : *h4;
-      sw[0][0] = a.x, sw[0][1] = a.y, sw[0][2] = b.x, sw[0][3] = b.y;
-      sw[1][0] = a.z, sw[1][1] = a.w, sw[1][2] = b.z, sw[1][3] = b.w;
-      return;
-    }
     const int64_t r = t * 128 + lane;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -1297,25 +1258,8 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
       sw[h][0] = a.x, sw[h][1] = a.y, sw[h][2] = b.x, sw[h][3] = b.y;
     }
   };
-  // VAR bit 3: ballots of the even (e) and odd (o) rows -> the tile's two row-order words
-  auto spread = [](uint64_t x) -> uint64_t {  // bit i -> bit 2i (32 -> 64 bits)
-    x &= 0xffffffffull;
-    x = (x | (x << 16)) & 0x0000ffff0000ffffull;
-    x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
-    x = (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
-    x = (x | (x << 2)) & 0x3333333333333333ull;
-    return (x | (x << 1)) & 0x5555555555555555ull;
-  };
-  auto rows_order = [&](unsigned long long& e, unsigned long long& o) {
-    const unsigned long long w0 = spread(e) | (spread(o) << 1), w1 = spread(e >> 32) | (spread(o >> 32) << 1);
-    e = w0, o = w1;
-  };
   const uint32_t rest_b = __builtin_amdgcn_readfirstlane(fb_rest);
-  const int64_t per = (work_tiles + nwaves - 1) / nwaves;  // VAR bit 1: this wave's tile range
-  const int64_t t_beg = (VAR & 2) ? wave * per : wave;
-  const int64_t t_end = (VAR & 2) ? min(work_tiles, t_beg + per) : work_tiles;
-  const int64_t t_step = (VAR & 2) ? 1 : nwaves;
-  for (int64_t t = t_beg; t < t_end; t += t_step) {
+  for (int64_t t = wave; t < work_tiles; t += nwaves) {
     uint32_t sw[2][4];
     load(t, sw);
     __builtin_amdgcn_sched_barrier(0);
@@ -1334,14 +1278,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
-        if (VAR & 4) {
-          lw[h][k] = 0u;
-          if (__ballot(ob[h][k] < cw4)) lw[h][k] = *(lds_u32p)(size_t(min(ob[h][k], cw4)));
-        } else {
-          lw[h][k] = *(lds_u32p)(size_t(min(ob[h][k], cw4)));
-        }
-      }
+      for (int k = 0; k < 4; k++) lw[h][k] = *(lds_u32p)(size_t(min(ob[h][k], cw4)));
     // VAR bit 5: rows already found through a hub word send no L2 probe (most found rows have
     // a hub in-neighbour in the frontier: their slots' L2 probes were wasted instructions)
     bool hubf[2] = {false, false};
@@ -1355,45 +1292,6 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
           hubf[h] = hubf[h] || (__builtin_amdgcn_ubfe(lw[h][k], w, 1u) != 0u && pass);
         }
     }
-    if (VAR & 64) {
-      // VAR bit 6: the tile's L2 probes packed into as few instructions as lanes allow -- each
-      // lane's candidates (offsets) go to the wave's LDS scratch at their rank among the tile's
-      // candidates, ceil(count / 64) full-width probe loads answer them, each lane reads its
-      // answers back (8 partly-empty probe instructions a tile became ~2)
-      uint32_t pos[2][4];
-      uint32_t T = 0;  // wave-uniform
-#pragma unroll
-      for (int h = 0; h < 2; h++)
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const bool cnd = ob[h][k] - cw4 < rest_b && !hubf[h];
-          const unsigned long long m = __ballot(cnd);
-          const uint32_t p = T + uint32_t(__builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u)));
-          pos[h][k] = cnd ? p : 0xffffffffu;
-          if (cnd && p < uint32_t(kProbeCap)) wscr[p] = ob[h][k] - cw4;
-          T += uint32_t(__popcll(m));
-        }
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t Tc = min(T, uint32_t(kProbeCap));
-      for (uint32_t b0 = 0; b0 < Tc; b0 += 64) {
-        const uint32_t i = b0 + uint32_t(lane);
-        const uint32_t off = i < Tc ? wscr[i] : 0xfffffff0u;
-        const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, off, 0, 0);
-        if (i < Tc) wscr[i] = w;
-      }
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int h = 0; h < 2; h++)
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const uint32_t p = pos[h][k];
-          gw[h][k] = 0u;
-          if (p < uint32_t(kProbeCap)) gw[h][k] = wscr[p];
-          else if (__ballot(p != 0xffffffffu))  // past the scratch (a rare dense tile): direct
-            gw[h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, p != 0xffffffffu ? ob[h][k] - cw4 : 0xfffffff0u, 0, 0);
-        }
-      __builtin_amdgcn_wave_barrier();
-    } else {
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
@@ -1406,7 +1304,6 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
           gw[h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, ob[h][k] - cw4, 0, 0);
         }
       }
-    }
     __builtin_amdgcn_sched_barrier(0);
     bool f[2], pend[2];
 #pragma unroll
@@ -1427,10 +1324,6 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
     }
     unsigned long long f0 = __ballot(f[0]), f1 = __ballot(f[1]);
     unsigned long long p0 = __ballot(pend[0]), p1 = __ballot(pend[1]);
-    if (VAR & 8) {
-      rows_order(f0, f1);
-      rows_order(p0, p1);
-    }
     if (VAR & 16) {
       // one store instruction: lane 0 the two next-frontier words, lane 1 the two pending words
       if (lane < 2) {
@@ -2794,13 +2687,12 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   };
   int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
   if (sel == 2 && c.opt("bu_lean_nt", 1) != 0 && (fast || es.odeg8.p)) sel = 6;  // non-temporal, 1 B degrees
-  // default 3: the probe skip and hub-first L2 probes (r06j: 100.7 -> 91.6 us at C3 hop 2; the
-  // wide-lane layouts 5 / 7 measured 104.7-105 us)
+  // default 3: the probe skip and hub-first L2 probes (r06j: 100.7 -> 91.6 us at C3 hop 2); 7 adds
+  // one store per tile
   const int64_t lskip = c.opt("bu_lean_skip", 3);
-  if (sel == 6 && lskip != 0) sel = lskip == 3 ? 8 : lskip == 7 ? 9 : lskip == 5 ? 10 : 7;  // + probe skip
+  if (sel == 6 && lskip != 0) sel = lskip == 3 ? 8 : lskip == 7 ? 9 : 7;  // + probe skip
 #define NBG_LEAN(PKV)                                \
   switch (sel) {                                     \
-    case 10: go(k_bu_lean<PKV, 1, 1, 0, 1, 5>); break; \
     case 9: go(k_bu_lean<PKV, 1, 1, 0, 1, 7>); break; \
     case 8: go(k_bu_lean<PKV, 1, 1, 0, 1, 3>); break; \
     case 7: go(k_bu_lean<PKV, 1, 1, 0, 1, 1>); break; \
@@ -2819,9 +2711,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     // CLS 1 ("greater than"): candidates and passing words are each one upper range
     const bool cls1 = fa.pinv == 0 && fa.cr == ~fa.clo && fa.pr == ~fa.plo && fa.clo <= 0x80000000u &&
                       fa.plo <= 0x80000000u && c.opt("bu_fin_cls", 1) != 0;
-    const int var0 = cls1 && c.opt("bu_fin_nt", 1) != 0 ? int(c.opt("bu_fin_var", 49) & 127) : 0;
-    const size_t fshm = size_t((cw + 2) & ~1) * 4 + size_t(kSlots) * 16 * 8 +
-                        ((var0 & 64) ? size_t(bs / 64) * kProbeCap * 4 : 0);
+    const size_t fshm = size_t((cw + 2) & ~1) * 4 + size_t(kSlots) * 16 * 8;
     const uint32_t rest = fb_bytes > uint32_t(cw) * 4u ? fb_bytes - uint32_t(cw) * 4u : 0u;
     auto gof = [&](auto kern) {
       if (fshm > 48 * 1024) lds_limit(reinterpret_cast<const void*>(kern), fshm);
@@ -2831,24 +2721,19 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     const int nt = int(c.opt("bu_fin_nt", 1) != 0);
     // default 49: the probe skip, one store per tile, hub-first L2 probes (r06h sweep:
     // k_bu_fin 124.9 -> 108.1 us; the 16-byte-lane and blocked-tile variants measured no gain)
-    const int var = cls1 && nt ? int(c.opt("bu_fin_var", 49) & 127) : 0;
+    const int var = cls1 && nt ? int(c.opt("bu_fin_var", 49) & (1 | 16 | 32)) : 0;
     switch ((cls1 ? 1 : 0) | nt << 1 | var << 2) {
       case 0: gof(k_bu_fin<0, 0>); break;
       case 1: gof(k_bu_fin<1, 0>); break;
       case 2: gof(k_bu_fin<0, 1>); break;
       case 3: gof(k_bu_fin<1, 1>); break;
-      case 3 | 4: gof(k_bu_fin<1, 1, 1>); break;
-      case 3 | 8: gof(k_bu_fin<1, 1, 2>); break;
-      case 3 | 12: gof(k_bu_fin<1, 1, 3>); break;
-      case 3 | 16: gof(k_bu_fin<1, 1, 4>); break;
-      case 3 | 20: gof(k_bu_fin<1, 1, 5>); break;
-      case 3 | 36: gof(k_bu_fin<1, 1, 9>); break;
-      case 3 | 32: gof(k_bu_fin<1, 1, 8>); break;
-      case 3 | 68: gof(k_bu_fin<1, 1, 17>); break;
-      case 3 | 132: gof(k_bu_fin<1, 1, 33>); break;
-      case 3 | 196: gof(k_bu_fin<1, 1, 49>); break;
-      case 3 | ((113) << 2): gof(k_bu_fin<1, 1, 113>); break;
-      default: gof(k_bu_fin<1, 1, 7>); break;
+      case 3 | (1 << 2): gof(k_bu_fin<1, 1, 1>); break;
+      case 3 | (16 << 2): gof(k_bu_fin<1, 1, 16>); break;
+      case 3 | (17 << 2): gof(k_bu_fin<1, 1, 17>); break;
+      case 3 | (32 << 2): gof(k_bu_fin<1, 1, 32>); break;
+      case 3 | (33 << 2): gof(k_bu_fin<1, 1, 33>); break;
+      case 3 | (48 << 2): gof(k_bu_fin<1, 1, 48>); break;
+      default: gof(k_bu_fin<1, 1, 49>); break;
     }
     snprintf(fin_nm, sizeof fin_nm, "nbg::k_bu_fin<%d, %d, %d>", cls1 ? 1 : 0, nt, var);
   } else if (fast) {
@@ -2931,7 +2816,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   else
     snprintf(nm, sizeof nm, "nbg::k_bu_lean<%d, %d, %d, %d%s>", pk, probe_stats ? 1 : U, cw > 0 ? 1 : 0,
              probe_stats ? 1 : 0,
-             sel == 10 ? ", 1, 5" : sel == 9 ? ", 1, 7" : sel == 8 ? ", 1, 3" : sel == 7 ? ", 1, 1" : sel == 6 ? ", 1, 0" : ", 0, 0");
+             sel == 9 ? ", 1, 7" : sel == 8 ? ", 1, 3" : sel == 7 ? ", 1, 1" : sel == 6 ? ", 1, 0" : ", 0, 0");
   c.bu_kernel_name = nm;
   const int wn = fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0;
   snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d, %d>", pk, wn, rcw > 0 ? 1 : 0, use_rec ? 1 : 0);

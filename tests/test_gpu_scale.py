@@ -267,25 +267,22 @@ def test_configs2_rmat26_bench_query_digest():
         sp.close()
 
 
-@pytest.mark.parametrize("var,hub_cap", [(0, None), (1, None), (49, None), (49, 1024), (113, None), (113, 1024),
-                                         (17, None), (9, None)])
+@pytest.mark.parametrize("var,hub_cap", [(0, None), (1, None), (49, None), (49, 1024), (17, None), (33, 1024)])
 def test_bu_fin_variants_rmat20(rmat20, var, hub_cap):
-    """every measured k_bu_fin variant (bu_fin_var bits: probe-instruction skip, blocked tiles,
-    16-byte lanes, one store per tile, hub-first L2 probes, packed L2 probes) and the non-final
-    pass's (bu_lean_skip 1 / 3 / 5 / 7) against the committed digest, with the hub capped too"""
+    """the k_bu_fin variants (bu_fin_var bits: probe-instruction skip, one store per tile, no L2
+    probe for rows a hub word found) and the non-final pass's (bu_lean_skip 1 / 3 / 7: probe skip,
+    hub-first, one store) against the committed digest, with the hub capped too"""
     sp, g = rmat20
     sp.set_option("bu_fin_var", var)
     if hub_cap:
         sp.set_option("bu_hub_cap", hub_cap)
-    if var & 64:
-        sp.set_option("bu_lean_lds_kb_final", 64)
     try:
-        for lskip in (1, 3, 5, 7, 0):
+        for lskip in (1, 3, 7, 0):
             sp.set_option("bu_lean_skip", lskip)
             r = bench_query(sp, 20)
             check_gold("go3_where499_distinct_s20", r.columns[0], r.edges_scanned)
             hops = sp.last_timing()["hops"]
             assert hops[-1]["kernels"][0] == f"nbg::k_bu_fin<1, 1, {var}>", hops[-1]["kernels"]
     finally:
-        for k in ("bu_fin_var", "bu_hub_cap", "bu_lean_lds_kb_final", "bu_lean_skip"):
+        for k in ("bu_fin_var", "bu_hub_cap", "bu_lean_skip"):
             sp.unset_option(k)
