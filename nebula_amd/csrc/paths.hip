@@ -480,10 +480,12 @@ __global__ void k_sweep_push_cost(const uint64_t* __restrict__ arena, int64_t na
     wave_add_keyed(push, p, d, go);
   }
 }
+// bias (option sp_push_bias, in 1/16): push when its entries are below pull's x bias / 16 (a push
+// row scan stops at its first hit, so its full degree sum overstates it)
 __global__ void k_sweep_choose(const unsigned long long* pull, const unsigned long long* push, int32_t B,
-                               int32_t* push_pair) {
+                               int32_t* push_pair, unsigned long long bias16) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < B) push_pair[p] = pull[p] > 0 && push[p] < pull[p];
+  if (p < B) push_pair[p] = pull[p] > 0 && push[p] * 16ull < pull[p] * bias16;
 }
 // X += the forward level-k tuples of push pairs (their out-rows are the step's adjacency)
 __global__ void k_sweep_push_select(const uint64_t* __restrict__ arena, int64_t na, int32_t j, SpState st,
@@ -1746,7 +1748,8 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         if (n_arena)
           k_sweep_push_cost<<<grid_n(n_arena), 256, 0, c.stream>>>(W.arena.as<uint64_t>(), n_arena, j, st, gout, pullc,
                                                                     pushc);
-        k_sweep_choose<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(pullc, pushc, int32_t(nb), push_pair);
+        k_sweep_choose<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(
+            pullc, pushc, int32_t(nb), push_pair, (unsigned long long)std::max<int64_t>(0, c.opt("sp_push_bias", 16)));
       }
       k_sp_select<<<grid_sel(n_sw), kBlk, 0, c.stream>>>(cur->as<uint64_t>(), n_sw, sweep_mode, st, gout, gin, W.X.as<uint64_t>(),
                                                        W.Xdeg.as<int64_t>(), W.cap_x, bf, cnt,
