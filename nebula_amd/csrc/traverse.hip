@@ -3484,7 +3484,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name);
       std::swap(bitsA, bitsB);
       have_list = false;
-      list_n = -1;  // the new bitmap's population is read back by ensure_list
+      // one rank: the found rows the two passes counted are the new bitmap's population (every
+      // found row sets one bit; pending rows are disjoint from the first pass's found rows), so
+      // ensure_list needs no round trip; several ranks: the local population is read back
+      list_n = multi ? -1 : int64_t(K.h[0]);
       off_ready = false;
       E = int64_t(K.h[1]);
       E_known = E;
@@ -3737,10 +3740,12 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         }
         NBG_HIP(hipGetLastError());
       }
-      if (multi) dev_allsum(c, K.d, {5}, K.d + 48);
-      fetch_counters(c, K.d, multi ? 49 : 6, K.h);
-      const int64_t yerr = int64_t(K.h[multi ? 48 : 5]);
-      if (yerr) throw Error(NBG_E_EVAL, "YIELD evaluation failed");
+      if (!dst_only) {  // (the fused _dst rows evaluate nothing: no error count to read)
+        if (multi) dev_allsum(c, K.d, {5}, K.d + 48);
+        fetch_counters(c, K.d, multi ? 49 : 6, K.h);
+        const int64_t yerr = int64_t(K.h[multi ? 48 : 5]);
+        if (yerr) throw Error(NBG_E_EVAL, "YIELD evaluation failed");
+      }
       if (s.distinct && c.world > 1) nrows = shuffle_rows(c, ya, h->dev, nrows);
       if (s.distinct && nrows) {
         uint64_t cap = 1024;
