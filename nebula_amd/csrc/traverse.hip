@@ -1656,7 +1656,8 @@ __global__ void k_degrees(const int32_t* F, int64_t nF, const int64_t* row_ptr, 
 __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64_t n, const int64_t* row_ptr,
                                                  const uint8_t* row_ok, int require_deg, int32_t* out,
                                                  unsigned long long* n_out, unsigned long long* partials,
-                                                 uint16_t* bits, const uint32_t* __restrict__ odeg) {
+                                                 uint16_t* bits, const uint32_t* __restrict__ odeg,
+                                                 unsigned long long* sums = nullptr) {
   // tile = 256 threads x 4 chunks of 16 bytes = 16384 vertices; one returning atomic per tile
   // (1024-thread tiles, a quarter of the atomics, measured slower: 40 -> 47 us at hop 1);
   // n_set (partials[0]), the kept out-degree sum (partials[1]) and the kept count (partials[2])
@@ -1743,7 +1744,9 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
     }
     __syncthreads();
   }
-  block_store_partials(acc, 3, lds64, partials);
+  // sums (zeroed by the caller): the block sums added there, no k_reduce_partials launch
+  if (sums) block_add_sums(acc, 3, lds64, sums);
+  else block_store_partials(acc, 3, lds64, partials);
 }
 
 // starts (gidx) -> deduplicated frontier: bitmap bits (set once, by a returning atomicOr) and
@@ -1793,7 +1796,8 @@ __global__ __launch_bounds__(1024) void k_starts_small(const int64_t* __restrict
                                                        int64_t hi, const int64_t* __restrict__ row_ptr,
                                                        const uint8_t* __restrict__ row_ok, uint32_t* bits,
                                                        int32_t* __restrict__ F, int64_t* __restrict__ off,
-                                                       unsigned long long* __restrict__ Kd) {
+                                                       unsigned long long* __restrict__ Kd,
+                                                       int32_t* __restrict__ tile_row = nullptr) {
   __shared__ int32_t s_loc[kSmallStarts];
   __shared__ unsigned long long s_w[32];  // [0, 16): per-wave counts, [16, 32): per-wave degree sums
   __shared__ unsigned long long s_carry[2];
@@ -1861,6 +1865,13 @@ __global__ __launch_bounds__(1024) void k_starts_small(const int64_t* __restrict
     Kd[41] = E;
     Kd[30] = t;
   }
+  // the hop-1 expansion's tile-row table (k_tile_rows' rule) from the offsets just written: one
+  // launch and its gap less before the first hop
+  if (tile_row)
+    for (int k = tid; k < int(nF); k += blockDim.x) {
+      const int64_t b = off[k], e = off[k + 1];
+      for (int64_t t = (b + kTile - 1) / kTile; t * kTile < e; t++) tile_row[t] = k;
+    }
 }
 
 __global__ void k_mark_gidx(const int32_t* g, int64_t n, int64_t lo, int64_t hi, uint8_t* map) {
@@ -2457,14 +2468,17 @@ static void lds_limit(const void* kern, size_t shm) {
 
 void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* row_ptr, const uint8_t* row_ok,
                     int require_deg, int32_t* out, uint16_t* bits, unsigned long long* Kd,
-                    const uint32_t* odeg = nullptr) {
+                    const uint32_t* odeg = nullptr, bool sums_zero = false) {
   // counters: Kd[0] list length (atomic), Kd[12] vertices set, Kd[13] kept out-degree sum,
-  // Kd[14] kept vertices (= the list length, also when out == nullptr writes no list)
+  // Kd[14] kept vertices (= the list length, also when out == nullptr writes no list).
+  // sums_zero: Kd[12, 15) are already zero, so the blocks add into them (bu_atomic_sums)
   unsigned long long* partials = c.ws_partials.as<unsigned long long>();
   int64_t ntiles = ((n + 15) / 16 + 1023) / 1024;
   int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, kAggBlocks)));
-  k_compact<<<grid, 256, 0, c.stream>>>(map, lo, n, row_ptr, row_ok, require_deg, out, Kd, partials, bits, odeg);
-  k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, Kd + 12);
+  const bool atomic = sums_zero && c.opt("bu_atomic_sums", 1) != 0;
+  k_compact<<<grid, 256, 0, c.stream>>>(map, lo, n, row_ptr, row_ok, require_deg, out, Kd, partials, bits, odeg,
+                                        atomic ? Kd + 12 : nullptr);
+  if (!atomic) k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, Kd + 12);
   NBG_HIP(hipGetLastError());
 }
 
@@ -2484,11 +2498,13 @@ size_t timing_event(Ctx& c) {
 
 template <int MODE>
 void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Program* dprog, const EvalEnv& env,
-                   int64_t E) {
+                   int64_t E, bool tile_rows_ready = false) {
   int64_t ntiles = (E + kTile - 1) / kTile;
   int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, int64_t(c.opt("expand_grid", 256 * 8)))));
   const size_t ia = timing_event(c);
-  if (c.opt("expand_tile_rows", 1) && a.nF < (int64_t(1) << 31)) {
+  if (tile_rows_ready) {  // k_starts_small wrote the table
+    a.tile_row = c.ws_tile_rows.as<int32_t>();
+  } else if (c.opt("expand_tile_rows", 1) && a.nF < (int64_t(1) << 31)) {
     c.ws_tile_rows.ensure(size_t(ntiles + 2) * 4);
     a.tile_row = c.ws_tile_rows.as<int32_t>();
     k_tile_rows<kTile><<<grid_cap(a.nF), 256, 0, c.stream>>>(a.off, a.nF, c.ws_tile_rows.as<int32_t>());
@@ -3021,11 +3037,18 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   int64_t nset_global = ns;  // "starts_ non-empty" (GoExecutor.cpp:93-97)
   int64_t hop1_scanned = -1;  // hop-1 rows with duplicate starts rescanned (k_starts_degree)
   int64_t Eg_known = -1;      // several ranks: the start frontier's out-degree sum over ranks
+  // the hop-1 expansion's tile-row table is written by k_starts_small (sized for the degree bound)
+  const bool starts_tiles = fast1 && c.opt("expand_tile_rows", 1) != 0 && c.opt("starts_tile_rows", 1) != 0;
+  if (starts_tiles) {
+    const int64_t eb = std::max<int64_t>(1, es.max_odeg >= 0 ? int64_t(ns) * es.max_odeg : csr.nnz);
+    c.ws_tile_rows.ensure(size_t(std::min<int64_t>(eb, csr.nnz + 1) / kTile + 4) * 4);
+  }
   if (fast1) {
     k_starts_small<<<1, 1024, 0, c.stream>>>(d_starts, int32_t(ns), c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
                                               uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, d_sg, lo, hi,
                                               row_ptr, row_ok, reinterpret_cast<uint32_t*>(bits16), F,
-                                              c.ws_off.as<int64_t>(), K.d);
+                                              c.ws_off.as<int64_t>(), K.d,
+                                              starts_tiles ? c.ws_tile_rows.as<int32_t>() : nullptr);
     NBG_HIP(hipGetLastError());
     nF = ns;  // an upper bound: the entries past the list have degree 0
   } else {
@@ -3410,14 +3433,14 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       a.nF = nF;
       a.off = c.ws_off.as<int64_t>();
       const int64_t e_bound = std::max<int64_t>(1, es.max_odeg >= 0 ? ns * es.max_odeg : csr.nnz);
-      launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, std::min<int64_t>(e_bound, csr.nnz + 1));
+      launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, std::min<int64_t>(e_bound, csr.nnz + 1), starts_tiles);
       exchange_marks(c, map);  // several ranks: every owner receives the marks of its vertices
       cur ^= 1;
       F = c.ws_front[cur].as<int32_t>();
       const bool lazy = bu_ok && c.opt("compact_list", 0) == 0;
-      // (K.d[0, 4) are zero: k_starts_small cleared the counters)
+      // (K.d[0, 256) are zero: k_starts_small cleared the counters)
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
-                     K.d, es.odeg.as<uint32_t>());
+                     K.d, es.odeg.as<uint32_t>(), true);
       // several ranks: the counts over ranks -- piggy: carried by the first speculated hop's
       // frontier exchange (its gate publishes them); else found, next out-degree sum and hop-1
       // entries summed into K.d[48, 51)
