@@ -213,10 +213,13 @@ __device__ inline bool dist_claim(const SpState& st, uint8_t* dense, uint32_t si
 
 // zero the counter slots in `mask` (bit i = cnt[i]; one launch instead of a memset per slot run)
 // and, when xdeg is given, the X degree sentinel xdeg[0] the scan reads past the list
-__global__ void k_cnt_zero(unsigned long long* cnt, uint32_t mask, int64_t* xdeg) {
+// (z, zn: an extra array zeroed by the same launch -- the sweep's per-pair cost sums)
+__global__ void k_cnt_zero(unsigned long long* cnt, uint32_t mask, int64_t* xdeg, unsigned long long* z = nullptr,
+                           int64_t zn = 0) {
   const int i = threadIdx.x;
   if (i < 32 && ((mask >> i) & 1u)) cnt[i] = 0ull;
   if (i == 32 && xdeg) *xdeg = 0;
+  for (int64_t k = i; k < zn; k += blockDim.x) z[k] = 0ull;
 }
 
 // seed both frontiers; trivial pairs (src == dst, unknown vertex, max_steps < 1) finish here
@@ -721,9 +724,14 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
 // ---- chunked scans (meet probe, sweep) --------------------------------------------------------
 // chunk_x[c] = the X entry holding chunk c (choff = exclusive scan of the entries' chunk counts):
 // one coalesced pass instead of a binary search of choff (~15 dependent loads) per chunk
-__global__ void k_chunk_x(const int64_t* __restrict__ choff, int64_t nX, int32_t* __restrict__ chunk_x) {
+// slot (the meet probe): its per-chunk result slots are emptied here too (no memset launch)
+__global__ void k_chunk_x(const int64_t* __restrict__ choff, int64_t nX, int32_t* __restrict__ chunk_x,
+                          uint64_t* __restrict__ slot = nullptr) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < nX; i += int64_t(gridDim.x) * blockDim.x)
-    for (int64_t c = choff[i]; c < choff[i + 1]; c++) chunk_x[c] = int32_t(i);
+    for (int64_t c = choff[i]; c < choff[i + 1]; c++) {
+      chunk_x[c] = int32_t(i);
+      if (slot) slot[c] = ~0ull;
+    }
 }
 
 // One sweep step over the X tuples' adjacency, one wave per chunk of kSwCh entries (the meet
@@ -844,8 +852,9 @@ __global__ void k_sp_chunks_n(const int64_t* Xdeg, int64_t nX, int64_t* ch, int6
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= nX; i += int64_t(gridDim.x) * blockDim.x)
     ch[i] = i == nX ? 0 : (Xdeg[i] + size - 1) / size;
 }
-// ch[i] = number of probe chunks of X[i]; ch[nX] = 0
-__global__ void k_sp_chunks(const int64_t* Xdeg, int64_t nX, int64_t* ch) {
+// ch[i] = number of probe chunks of X[i]; ch[nX] = 0; the probe's examined-entry counter cleared
+__global__ void k_sp_chunks(const int64_t* Xdeg, int64_t nX, int64_t* ch, unsigned long long* cnt) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[C_PE] = 0ull;
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i <= nX; i += int64_t(gridDim.x) * blockDim.x)
     ch[i] = i == nX ? 0 : (Xdeg[i] + kProbeCh - 1) / kProbeCh;
 }
@@ -911,10 +920,11 @@ __global__ __launch_bounds__(256, OCC) void k_sp_probe(const uint64_t* __restric
   if (lane == 0 && ev) atomicAdd(cnt + C_PE, ev);
 }
 
-// slots -> meet list (1, p, dt, r) + arena (the claimed byte).  Runs before k_sp_probe_step, so
+// slots -> meet list (1, p, dt, r) + arena (the claimed byte).  Runs before k_sp_probe_end, so
 // lvl still holds the depths the probe compared against.
 __global__ __launch_bounds__(kBlk) void k_sp_gather_meets(const uint64_t* slot, int64_t m, SpState st, SpBufs bf,
-                                                          unsigned long long* cnt) {
+                                                          unsigned long long* cnt, const int64_t* m_dev = nullptr) {
+  if (m_dev) m = min(m, *m_dev);  // the probe's chunk count (slots past it are not emptied)
   constexpr int64_t per = int64_t(kBlk) * kSelIt;
   const int64_t rounds = (m + per - 1) / per;
   for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
@@ -948,27 +958,31 @@ __global__ __launch_bounds__(kBlk) void k_sp_gather_meets(const uint64_t* slot, 
   }
 }
 
-// pairs whose probe met: finish as if the other side had expanded (its depth + 1)
-__global__ void k_sp_probe_step(SpState st, int32_t iter) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= st.B || st.state[p] != SP_ACTIVE || st.met[p] != 1) return;
-  const int B = st.B;
-  const int adv = st.side[p] ^ 1;
-  st.lvl[adv * B + p] += 1;
-  st.res[p] = st.lvl[p] + st.lvl[B + p];
-  st.state[p] = SP_MET;
-  st.met[p] = 2 + iter;
-  st.pside[p] = adv;
-}
-
-// X tuples of pairs that are no longer active: degree 0 (the expansion skips them)
-__global__ void k_sp_drop(const uint64_t* X, int64_t* Xdeg, int64_t nX, SpState st, unsigned long long* cnt) {
+// After a meet probe, one launch: thread i finishes pair i (i < B) as if the other side had
+// expanded (its depth + 1) when the probe met, and drops X tuple i (i < nX) of a pair that met
+// (degree 0: the expansion skips it).  An X tuple's pair was active when selected, so it met in
+// this probe iff its met flag is set (1 before the pair's update, 2 + iter after: either order
+// is seen as met).  Also clears the X degree sentinel Xdeg[nX] the expansion's scan reads.
+__global__ void k_sp_probe_end(SpState st, int32_t iter, const uint64_t* X, int64_t* Xdeg, int64_t nX,
+                               unsigned long long* cnt) {
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-  const int64_t rounds = (nX + stride - 1) / stride;
+  const int64_t m = max(int64_t(st.B), nX);
+  const int64_t rounds = (m + stride - 1) / stride;
+  if (blockIdx.x == 0 && threadIdx.x == 0) Xdeg[nX] = 0;
   for (int64_t r = 0; r < rounds; r++) {
     const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+    if (i < st.B && st.state[i] == SP_ACTIVE && st.met[i] == 1) {
+      const int B = st.B;
+      const int p = int(i);
+      const int adv = st.side[p] ^ 1;
+      st.lvl[adv * B + p] += 1;
+      st.res[p] = st.lvl[p] + st.lvl[B + p];
+      st.state[p] = SP_MET;
+      st.met[p] = 2 + iter;
+      st.pside[p] = adv;
+    }
     unsigned long long d = 0;
-    if (i < nX && st.state[t_pair(X[i])] != SP_ACTIVE) {
+    if (i < nX && st.met[t_pair(X[i])] != 0) {
       d = (unsigned long long)Xdeg[i];
       Xdeg[i] = 0;
     }
@@ -976,6 +990,7 @@ __global__ void k_sp_drop(const uint64_t* X, int64_t* Xdeg, int64_t nX, SpState 
     if ((threadIdx.x & 63) == 0 && sd) atomicAdd(cnt + C_XE, 0ull - sd);
   }
 }
+
 
 // one workgroup per pair that met: greedy walk from src (dist_B now exact on every shortest
 // path).  Each step scans the current vertex's out-edges with the whole workgroup (hub rows on a
@@ -1489,9 +1504,9 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         W.Xoff.alloc(size_t(W.cap_x + 1) * 8);
       }
     };
-    auto launch_scan = [&](int64_t nX) {
+    auto launch_scan = [&](int64_t nX, bool sentinel_zero = false) {
       size_t tb = 0;
-      zero(0u, W.Xdeg.as<int64_t>() + nX);
+      if (!sentinel_zero) zero(0u, W.Xdeg.as<int64_t>() + nX);
       NBG_HIP(rocprim::exclusive_scan(nullptr, tb, W.Xdeg.as<int64_t>(), W.Xoff.as<int64_t>(), int64_t(0),
                                       size_t(nX + 1), rocprim::plus<int64_t>(), c.stream));
       c.ws_tmp.ensure(tb);
@@ -1629,9 +1644,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         ch.alloc(size_t(nX + 1) * 8);
         choff.alloc(size_t(nX + 1) * 8);
         slot.alloc(size_t(max_chunks) * 8);
-        NBG_HIP(hipMemsetAsync(slot.p, 0xFF, size_t(max_chunks) * 8, c.stream));
-        zero(1u << C_PE);
-        k_sp_chunks<<<grid_n(nX + 1), 256, 0, c.stream>>>(W.Xdeg.as<int64_t>(), nX, ch.as<int64_t>());
+        k_sp_chunks<<<grid_n(nX + 1), 256, 0, c.stream>>>(W.Xdeg.as<int64_t>(), nX, ch.as<int64_t>(), cnt);
         size_t tb = 0;
         NBG_HIP(rocprim::exclusive_scan(nullptr, tb, ch.as<int64_t>(), choff.as<int64_t>(), int64_t(0),
                                         size_t(nX + 1), rocprim::plus<int64_t>(), c.stream));
@@ -1642,16 +1655,17 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         const int pgrid =
             int(std::max<int64_t>(1, std::min<int64_t>((max_chunks + 3) / 4, c.opt("sp_probe_grid", 4096))));
         chx.alloc(size_t(max_chunks) * 4);
-        k_chunk_x<<<grid_n(nX), 256, 0, c.stream>>>(choff.as<int64_t>(), nX, chx.as<int32_t>());
+        k_chunk_x<<<grid_n(nX), 256, 0, c.stream>>>(choff.as<int64_t>(), nX, chx.as<int32_t>(), slot.as<uint64_t>());
         if (c.opt("sp_probe_occ", 7) >= 8)
           k_sp_probe<8><<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), chx.as<int32_t>(),
                                                      gout, gin, d0, d1, n, lo, st, slot.as<uint64_t>(), cnt);
         else
           k_sp_probe<1><<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), chx.as<int32_t>(),
                                                      gout, gin, d0, d1, n, lo, st, slot.as<uint64_t>(), cnt);
-        k_sp_gather_meets<<<grid_sel(max_chunks), kBlk, 0, c.stream>>>(slot.as<uint64_t>(), max_chunks, st, bf, cnt);
-        k_sp_probe_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, iter);
-        k_sp_drop<<<grid_n(nX), 256, 0, c.stream>>>(W.X.as<uint64_t>(), W.Xdeg.as<int64_t>(), nX, st, cnt);
+        k_sp_gather_meets<<<grid_sel(max_chunks), kBlk, 0, c.stream>>>(slot.as<uint64_t>(), max_chunks, st, bf, cnt,
+                                                                       choff.as<int64_t>() + nX);
+        k_sp_probe_end<<<grid_n(std::max<int64_t>(nb, nX)), 256, 0, c.stream>>>(st, iter, W.X.as<uint64_t>(),
+                                                                                W.Xdeg.as<int64_t>(), nX, cnt);
         NBG_HIP(hipGetLastError());
         hipEventRecord(c.ev[5], c.stream);
       }
@@ -1666,7 +1680,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         reserve(c, W.meet, W.cap_meet, meet_keep + std::min<int64_t>(E, soft) + 64, std::min<int64_t>(meet_keep, W.cap_meet));
         refresh(nullptr, 0);
         hash_fit(st, int64_t(hc[C_ARENA]) + max_chunks + E);
-        launch_scan(nX);
+        launch_scan(nX, probed);  // (k_sp_probe_end cleared the sentinel)
         launch_expand(nX, E, 0);
       }
       k_sp_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(st, max_steps, 0, iter, cnt);
@@ -1740,10 +1754,10 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     for (int32_t j = 1; n_sw > 0; j++) {
       const bool push_now = push_ok && !arena_lost;  // an arena overflow mid-sweep: pull only
       ensure_x(n_sw + (push_now ? n_arena : 0));
-      zero(1u << C_X | 1u << C_ACTIVE | 1u << C_OVF | 1u << C_SWEEP | 1u << C_XE);
+      k_cnt_zero<<<1, 256, 0, c.stream>>>(cnt, 1u << C_X | 1u << C_ACTIVE | 1u << C_OVF | 1u << C_SWEEP | 1u << C_XE,
+                                          nullptr, push_now ? pullc : nullptr, push_now ? 2 * nb : 0);
       refresh(nullptr, 0);
       if (push_now) {
-        NBG_HIP(hipMemsetAsync(pullc, 0, size_t(nb) * 16, c.stream));
         k_sweep_pull_cost<<<grid_n(n_sw), 256, 0, c.stream>>>(cur->as<uint64_t>(), n_sw, sweep_mode, st, gin, pullc);
         if (n_arena)
           k_sweep_push_cost<<<grid_n(n_arena), 256, 0, c.stream>>>(W.arena.as<uint64_t>(), n_arena, j, st, gout, pullc,
