@@ -150,8 +150,25 @@ __global__ void k_sum_slices(const int64_t* in, int world, size_t n, int64_t* ou
   }
 }
 
+// The in-process transport also holds every exchange to RCCL's pairing rule: a grouped
+// ncclSend / ncclRecv pair must agree on the byte count, and a side that skips a zero-byte
+// transfer must face a peer that skips it too (otherwise RCCL hangs or truncates).  A mismatch is
+// recorded while the collective completes (every rank still reaches both barriers) and thrown
+// after it, so the multi-rank tests that run on LocalComm prove the RCCL exchange sizes as well.
 struct LocalComm : CommImpl {
   int32_t transport() const override { return 2; }
+  std::string mismatch;
+  void pair_check(Ctx& c, int p, size_t peer_sends, size_t i_recv, const char* what) {
+    if (p == c.rank || peer_sends == i_recv || !mismatch.empty()) return;
+    mismatch = std::string(what) + ": rank " + std::to_string(p) + " sends " + std::to_string(peer_sends) +
+               " bytes, rank " + std::to_string(c.rank) + " receives " + std::to_string(i_recv);
+  }
+  void raise_mismatch() {
+    if (mismatch.empty()) return;
+    std::string m;
+    m.swap(mismatch);
+    throw Error(NBG_E_COMM, "exchange sizes would not pair under RCCL: " + m);
+  }
   int32_t ranks() const override { return g ? int32_t(g->world) : -1; }
   std::shared_ptr<LocalGroup> g;
   hipEvent_t ready = nullptr, done = nullptr;
@@ -181,6 +198,7 @@ struct LocalComm : CommImpl {
     g->scalar[size_t(c.rank)] = send_bytes;
     publish(c);
     for (int p = 0; p < c.world; p++) {
+      pair_check(c, p, g->scalar[size_t(p)], recv_bytes[p], "allgatherv");
       size_t b = std::min(g->scalar[size_t(p)], recv_bytes[p]);
       if (!b || g->ptr[size_t(p)] == static_cast<uint8_t*>(recv) + recv_off[p]) continue;
       wait_ready(c, p);
@@ -188,6 +206,7 @@ struct LocalComm : CommImpl {
                              hipMemcpyDeviceToDevice, c.stream));
     }
     finish(c);
+    raise_mismatch();
   }
   void alltoallv(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
                  const size_t* recv_bytes, const size_t* recv_off) override {
@@ -196,6 +215,7 @@ struct LocalComm : CommImpl {
     g->offs[size_t(c.rank)] = send_off;
     publish(c);
     for (int p = 0; p < c.world; p++) {
+      pair_check(c, p, g->sizes[size_t(p)][c.rank], recv_bytes[p], "alltoallv");
       size_t b = std::min(g->sizes[size_t(p)][c.rank], recv_bytes[p]);
       if (!b) continue;
       wait_ready(c, p);
@@ -204,6 +224,7 @@ struct LocalComm : CommImpl {
                              hipMemcpyDeviceToDevice, c.stream));
     }
     finish(c);
+    raise_mismatch();
   }
   void allgatherv2(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
                    const size_t* recv_off, const void* send2, size_t bytes2, void* recv2) override {
@@ -212,6 +233,7 @@ struct LocalComm : CommImpl {
     g->ptr2[size_t(c.rank)] = send2;
     publish(c);
     for (int p = 0; p < c.world; p++) {
+      pair_check(c, p, g->scalar[size_t(p)], recv_bytes[p], "allgatherv2");
       wait_ready(c, p);
       size_t b = std::min(g->scalar[size_t(p)], recv_bytes[p]);
       if (b && g->ptr[size_t(p)] != static_cast<uint8_t*>(recv) + recv_off[p])
@@ -221,6 +243,7 @@ struct LocalComm : CommImpl {
                              hipMemcpyDeviceToDevice, c.stream));
     }
     finish(c);
+    raise_mismatch();
   }
   // in place, as ncclAllReduce: gather the slices, sum them, and write the sums back only after
   // every peer has read this rank's slice
