@@ -126,6 +126,7 @@ struct LocalGroup {
   std::vector<const void*> ptr, ptr2;
   std::vector<const size_t*> sizes, offs;
   std::vector<size_t> scalar;
+  std::vector<uint64_t> op;  // per rank: the collective it entered (kind | fixed size << 8)
   std::vector<hipEvent_t> ready, done;
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
@@ -177,10 +178,16 @@ struct LocalComm : CommImpl {
     if (ready) (void)hipEventDestroy(ready);
     if (done) (void)hipEventDestroy(done);
   }
-  // step 1 + barrier A
-  void publish(Ctx& c) {
+  // step 1 + barrier A; every rank must have entered the same collective (RCCL matches
+  // collectives by issue order, so a rank in another one would hang or mix the buffers there)
+  void publish(Ctx& c, uint64_t op) {
+    g->op[size_t(c.rank)] = op;
     NBG_HIP(hipEventRecord(ready, c.stream));
     g->barrier();
+    for (int p = 0; p < c.world; p++)
+      if (g->op[size_t(p)] != op && mismatch.empty())
+        mismatch = "rank " + std::to_string(p) + " entered collective " + std::to_string(g->op[size_t(p)]) +
+                   " while rank " + std::to_string(c.rank) + " entered " + std::to_string(op);
   }
   // (after the receive copies) step 2's `done` + barrier B + step 3
   void finish(Ctx& c) {
@@ -196,7 +203,7 @@ struct LocalComm : CommImpl {
                   const size_t* recv_off) override {
     g->ptr[size_t(c.rank)] = send;
     g->scalar[size_t(c.rank)] = send_bytes;
-    publish(c);
+    publish(c, 1);
     for (int p = 0; p < c.world; p++) {
       pair_check(c, p, g->scalar[size_t(p)], recv_bytes[p], "allgatherv");
       size_t b = std::min(g->scalar[size_t(p)], recv_bytes[p]);
@@ -213,7 +220,7 @@ struct LocalComm : CommImpl {
     g->ptr[size_t(c.rank)] = send;
     g->sizes[size_t(c.rank)] = send_bytes;
     g->offs[size_t(c.rank)] = send_off;
-    publish(c);
+    publish(c, 2);
     for (int p = 0; p < c.world; p++) {
       pair_check(c, p, g->sizes[size_t(p)][c.rank], recv_bytes[p], "alltoallv");
       size_t b = std::min(g->sizes[size_t(p)][c.rank], recv_bytes[p]);
@@ -231,7 +238,7 @@ struct LocalComm : CommImpl {
     g->ptr[size_t(c.rank)] = send;
     g->scalar[size_t(c.rank)] = send_bytes;
     g->ptr2[size_t(c.rank)] = send2;
-    publish(c);
+    publish(c, 3ull | uint64_t(bytes2) << 8);
     for (int p = 0; p < c.world; p++) {
       pair_check(c, p, g->scalar[size_t(p)], recv_bytes[p], "allgatherv2");
       wait_ready(c, p);
@@ -256,7 +263,7 @@ struct LocalComm : CommImpl {
     }
     int64_t* sl = scratch.as<int64_t>();
     g->ptr[size_t(c.rank)] = d;
-    publish(c);
+    publish(c, 4ull | uint64_t(n) << 8);
     for (int p = 0; p < c.world; p++) {
       wait_ready(c, p);
       NBG_HIP(hipMemcpyAsync(sl + size_t(p) * n, g->ptr[size_t(p)], n * 8, hipMemcpyDeviceToDevice, c.stream));
@@ -265,6 +272,7 @@ struct LocalComm : CommImpl {
     NBG_HIP(hipGetLastError());
     finish(c);
     NBG_HIP(hipMemcpyAsync(d, sl + G * n, n * 8, hipMemcpyDeviceToDevice, c.stream));
+    raise_mismatch();
   }
 };
 
@@ -314,6 +322,7 @@ void comm_init_local(Ctx& c, int64_t key) {
       slot->sizes.resize(size_t(c.world));
       slot->offs.resize(size_t(c.world));
       slot->scalar.resize(size_t(c.world));
+      slot->op.resize(size_t(c.world));
       slot->ready.resize(size_t(c.world));
       slot->done.resize(size_t(c.world));
     }
