@@ -1602,35 +1602,44 @@ __global__ __launch_bounds__(1024) void k_bits_compact(const uint32_t* __restric
     if ((w0 + 1) * 32 > n && w0 < nwords) x &= (1u << uint32_t(n - w0 * 32)) - 1u;
     uint32_t total;
     const uint32_t pre = block_excl_scan_u32(__popc(x), total, lds);
+    // the tile's output range: the returning atomic (serialised with every other tile's on the
+    // one counter) is issued here and read only after the first step's vid_of loads are out, so
+    // its wait overlaps them instead of preceding every load of the tile
+    unsigned long long my_base = 0;
+    if (threadIdx.x == 0 && total) my_base = atomicAdd(n_out, (unsigned long long)total);
     sw[threadIdx.x] = x;
     so[threadIdx.x] = pre;
-    if (threadIdx.x == 0) s_base = total ? atomicAdd(n_out, (unsigned long long)total) : 0ull;
     __syncthreads();
-    if (total) {
+    if (total) {  // block-uniform
       // U word pairs per step: the step's U vid_of loads are issued before any of its stores,
       // so each lane keeps U HBM requests in flight instead of one load -> store chain per pair
-      const unsigned long long base = s_base;
+      unsigned long long base = 0;
       const int half = lane >> 5, bit = lane & 31;
       const int per_wave = kTileWords / int(blockDim.x >> 6);
       for (int j = wv * per_wave; j < (wv + 1) * per_wave; j += 2 * U) {
         bool has[U];
-        unsigned long long p[U];
+        uint32_t rel[U];
         int64_t val[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
           const int wi = j + 2 * u + half;
           const uint32_t xw = sw[wi];
           has[u] = (xw >> bit) & 1u;
-          p[u] = base + so[wi] + __popc(xw & ((1u << bit) - 1u));
+          rel[u] = so[wi] + __popc(xw & ((1u << bit) - 1u));
           const int64_t v = (t * kTileWords + wi) * 32 + bit;
           val[u] = v;
           if (MODE == 1 && has[u]) val[u] = vid_of[lo + v];
         }
+        if (j == wv * per_wave) {  // every wave's first step (same trip count in every wave)
+          if (threadIdx.x == 0) s_base = my_base;
+          __syncthreads();
+          base = s_base;
+        }
 #pragma unroll
         for (int u = 0; u < U; u++) {
           if (!has[u]) continue;
-          if (MODE == 0) static_cast<int32_t*>(out)[p[u]] = int32_t(val[u]);
-          else static_cast<int64_t*>(out)[p[u]] = val[u];
+          if (MODE == 0) static_cast<int32_t*>(out)[base + rel[u]] = int32_t(val[u]);
+          else static_cast<int64_t*>(out)[base + rel[u]] = val[u];
         }
       }
     }
@@ -1799,6 +1808,7 @@ __global__ __launch_bounds__(1024) void k_starts_small(const int64_t* __restrict
                                                        unsigned long long* __restrict__ Kd,
                                                        int32_t* __restrict__ tile_row = nullptr) {
   __shared__ int32_t s_loc[kSmallStarts];
+  __shared__ int64_t s_off[kSmallStarts];  // the kept starts' exclusive degree offsets
   __shared__ unsigned long long s_w[32];  // [0, 16): per-wave counts, [16, 32): per-wave degree sums
   __shared__ unsigned long long s_carry[2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1844,6 +1854,7 @@ __global__ __launch_bounds__(1024) void k_starts_small(const int64_t* __restrict
       const unsigned long long pos = bc + kc - 1;
       F[pos] = loc;
       off[pos] = int64_t(bd + kd - d);
+      s_off[pos] = int64_t(bd + kd - d);
     }
     __syncthreads();
     if (tid == 0) s_carry[0] += tc, s_carry[1] += td;
@@ -1866,12 +1877,20 @@ __global__ __launch_bounds__(1024) void k_starts_small(const int64_t* __restrict
     Kd[30] = t;
   }
   // the hop-1 expansion's tile-row table (k_tile_rows' rule) from the offsets just written: one
-  // launch and its gap less before the first hop
-  if (tile_row)
-    for (int k = tid; k < int(nF); k += blockDim.x) {
-      const int64_t b = off[k], e = off[k + 1];
-      for (int64_t t = (b + kTile - 1) / kTile; t * kTile < e; t++) tile_row[t] = k;
+  // launch and its gap less before the first hop.  Tile t's row is the last kept start whose
+  // range begins at or before t * kTile (every kept start has out-edges, so the ranges tile
+  // [0, E)): one thread per tile, a binary search of the offsets in LDS (a thread per start
+  // walked a hub seed's hundreds of tiles alone)
+  if (tile_row && nF > 0) {
+    const int64_t nT = (int64_t(E) + kTile - 1) / kTile;
+    for (int64_t t = tid; t < nT; t += blockDim.x) {
+      const int64_t e0 = t * kTile;
+      int k = 0;
+      for (int st = kSmallStarts / 2; st > 0; st >>= 1)
+        if (k + st < int(nF) && s_off[k + st] <= e0) k += st;
+      tile_row[t] = k;
     }
+  }
 }
 
 __global__ void k_mark_gidx(const int32_t* g, int64_t n, int64_t lo, int64_t hi, uint8_t* map) {
@@ -2474,7 +2493,7 @@ void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* 
   // sums_zero: Kd[12, 15) are already zero, so the blocks add into them (bu_atomic_sums)
   unsigned long long* partials = c.ws_partials.as<unsigned long long>();
   int64_t ntiles = ((n + 15) / 16 + 1023) / 1024;
-  int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, kAggBlocks)));
+  int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, std::min<int64_t>(kAggBlocks, c.opt("compact_grid", 1024)))));
   const bool atomic = sums_zero && c.opt("bu_atomic_sums", 1) != 0;
   k_compact<<<grid, 256, 0, c.stream>>>(map, lo, n, row_ptr, row_ok, require_deg, out, Kd, partials, bits, odeg,
                                         atomic ? Kd + 12 : nullptr);
