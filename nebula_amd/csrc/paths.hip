@@ -372,6 +372,7 @@ __global__ __launch_bounds__(kBlk) void k_sp_select(const uint64_t* __restrict__
   uint64_t* const carry = bf.live_next[side];
   const int64_t cap_carry = bf.cap_live[side];
   const SpCsr& g = side ? gin : gout;
+  unsigned long long esum = 0;  // X's degree sum: one counter add per block at the end
   for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
     const int64_t i0 = r * per + threadIdx.x;
     uint64_t t[kSelIt];
@@ -423,8 +424,17 @@ __global__ __launch_bounds__(kBlk) void k_sp_select(const uint64_t* __restrict__
     }
     if (ovf_x) atomicOr(cnt + C_OVF, 2ull);
     if (ovf_c) atomicOr(cnt + C_OVF, 1ull);
-    const unsigned long long e = wsum(dsum);
-    if ((threadIdx.x & 63) == 0 && e) atomicAdd(cnt + C_XE, e);
+    esum += dsum;
+  }
+  __shared__ unsigned long long s_e[kBlk / 64];
+  const unsigned long long e = wsum(esum);
+  if ((threadIdx.x & 63) == 0) s_e[threadIdx.x >> 6] = e;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long bt = 0;
+#pragma unroll
+    for (int i = 0; i < kBlk / 64; i++) bt += s_e[i];
+    if (bt) atomicAdd(cnt + C_XE, bt);
   }
 }
 
@@ -834,7 +844,29 @@ __global__ __launch_bounds__(256, OCC) void k_sp_sweep(const uint64_t* __restric
       }
     }
   }
-  flush();
+  // the final flush per block, not per wave: one pair of counter atomics for the block's four
+  // stages (the waves of the grid end together, and their returning atomics on the two
+  // counters queued behind each other at the kernel's tail)
+  __shared__ uint32_t s_ns[4];
+  __shared__ unsigned long long s_b[2];
+  if (lane == 0) s_ns[wid] = ns;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long tot = s_ns[0] + s_ns[1] + s_ns[2] + s_ns[3];
+    s_b[0] = tot ? atomicAdd(cnt + C_ARENA, tot) : 0ull;
+    s_b[1] = tot ? atomicAdd(cnt + C_SWEEP, tot) : 0ull;
+  }
+  __syncthreads();
+  uint32_t pre = 0;
+  for (int k = 0; k < wid; k++) pre += s_ns[k];
+  const unsigned long long ba = s_b[0] + pre, bs = s_b[1] + pre;
+  for (uint32_t q = uint32_t(lane); q < ns; q += 64) {
+    const uint64_t v = stg[q];
+    if (int64_t(ba + q) < bf.cap_arena) bf.arena[ba + q] = v;
+    else atomicOr(cnt + C_OVF, 1ull);
+    if (int64_t(bs + q) < bf.cap_sweep) bf.sweep_next[bs + q] = v;
+    else atomicOr(cnt + C_OVF, 1ull);
+  }
 }
 
 // ---- meet probe -----------------------------------------------------------------------------
@@ -916,8 +948,16 @@ __global__ __launch_bounds__(256, OCC) void k_sp_probe(const uint64_t* __restric
       }
     }
   }
+  // one counter atomic per block: the grid's waves (up to 16 K) end together, and one add each
+  // on the same counter queued behind each other at the kernel's tail
+  __shared__ unsigned long long s_ev[4];
   const unsigned long long ev = wsum(examined);
-  if (lane == 0 && ev) atomicAdd(cnt + C_PE, ev);
+  if (lane == 0) s_ev[threadIdx.x >> 6] = ev;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long bt = s_ev[0] + s_ev[1] + s_ev[2] + s_ev[3];
+    if (bt) atomicAdd(cnt + C_PE, bt);
+  }
 }
 
 // slots -> meet list (1, p, dt, r) + arena (the claimed byte).  Runs before k_sp_probe_end, so
