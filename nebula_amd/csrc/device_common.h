@@ -108,13 +108,36 @@ __device__ inline int64_t wave_append(unsigned long long* counter, bool pred) {
 // entry k writes the tiles whose first slot falls in [off[k], off[k + 1]) (each tile start lies
 // in exactly one non-empty entry).  One coalesced pass over off[] instead of two dependent binary
 // searches of off[] by one thread at the head of every tile.
+// Every wave takes 64 consecutive entries (one per lane) and fills their item ranges [i0, i1)
+// together, entry by entry, 64 items a step: a hub entry's thousands of tiles / chunks are no
+// longer one thread's serial loop (~20 us for the C4 probe's largest rows).  Wave-uniform;
+// blockDim a multiple of 64.  range(k, i0, i1) gives entry k's items; fill(item, k) writes one.
+template <typename Range, typename Fill>
+__device__ inline void wave_fill_ranges(int64_t nk, Range range, Fill fill) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  for (int64_t k0 = wave * 64; k0 < nk; k0 += nwaves * 64) {
+    int64_t i0 = 0, i1 = 0;
+    if (k0 + lane < nk) range(k0 + lane, i0, i1);
+    uint64_t m = __ballot(i1 > i0);
+    while (m) {
+      const int j = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int64_t a = __shfl(i0, j), z = __shfl(i1, j);
+      for (int64_t i = a + lane; i < z; i += 64) fill(i, k0 + j);
+    }
+  }
+}
 template <int TILE>
 __global__ void k_tile_rows(const int64_t* __restrict__ off, int64_t nF, int32_t* __restrict__ tile_row) {
-  for (int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; k < nF; k += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t b = off[k], e = off[k + 1];
-    if (b == e) continue;
-    for (int64_t t = (b + TILE - 1) / TILE; t * TILE < e; t++) tile_row[t] = int32_t(k);
-  }
+  wave_fill_ranges(
+      nF,
+      [&](int64_t k, int64_t& t0, int64_t& t1) {
+        const int64_t b = off[k], e = off[k + 1];
+        if (b < e) t0 = (b + TILE - 1) / TILE, t1 = (e + TILE - 1) / TILE;  // tiles with t * TILE in [b, e)
+      },
+      [&](int64_t t, int64_t k) { tile_row[t] = int32_t(k); });
 }
 // The entries [i0, i0 + cnt) staged for tile t (slots [e0, e1) of E): i0 holds e0; the last one
 // holds e1 - 1, i.e. the entry before the one holding e1 when that one starts at e1 (entries of

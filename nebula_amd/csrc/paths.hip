@@ -737,11 +737,12 @@ __global__ __launch_bounds__(kT) void k_sp_expand(SpExpand a, SpState st, SpBufs
 // slot (the meet probe): its per-chunk result slots are emptied here too (no memset launch)
 __global__ void k_chunk_x(const int64_t* __restrict__ choff, int64_t nX, int32_t* __restrict__ chunk_x,
                           uint64_t* __restrict__ slot = nullptr) {
-  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < nX; i += int64_t(gridDim.x) * blockDim.x)
-    for (int64_t c = choff[i]; c < choff[i + 1]; c++) {
-      chunk_x[c] = int32_t(i);
-      if (slot) slot[c] = ~0ull;
-    }
+  wave_fill_ranges(
+      nX, [&](int64_t i, int64_t& c0, int64_t& c1) { c0 = choff[i], c1 = choff[i + 1]; },
+      [&](int64_t c, int64_t i) {
+        chunk_x[c] = int32_t(i);
+        if (slot) slot[c] = ~0ull;
+      });
 }
 
 // One sweep step over the X tuples' adjacency, one wave per chunk of kSwCh entries (the meet
