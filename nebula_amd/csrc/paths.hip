@@ -50,7 +50,7 @@ enum : int32_t { SP_ACTIVE = 0, SP_MET = 1, SP_DONE = 2 };
 // device counters (one array): live list F / B, arena, meets, X list, active pairs, overflow,
 // sweep list, X edges
 enum : int { C_LIVE0 = 0, C_LIVE1 = 1, C_ARENA = 2, C_MEET = 3, C_X = 4, C_ACTIVE = 5, C_OVF = 6, C_SWEEP = 7,
-             C_XE = 8, C_WALKERR = 9, C_PE = 10, C_N = 16 };
+             C_XE = 8, C_WALKERR = 9, C_PE = 10, C_PLEN = 11, C_MAXL = 12, C_N = 16 };
 
 __host__ __device__ inline uint64_t mk_tup(uint32_t side, uint32_t pair, uint32_t lvl, uint32_t row) {
   return (uint64_t(side) << 63) | (uint64_t(pair & 0x7FFFFFu) << 40) | (uint64_t(lvl & 0xFFu) << 32) | uint64_t(row);
@@ -1296,6 +1296,61 @@ void reserve(Ctx& c, DevBuf& b, int64_t& cap, int64_t need, int64_t keep) {
 // i % world) and every rank answers its own pairs against a replica of the whole graph's out / in
 // CSRs.  The replicas are assembled once with allgathers of every rank's rows (the rows of rank r
 // are the gidx range [base[r], base[r+1])); the traversal itself exchanges nothing.
+// the batch's path offsets on the device (one block): pair p's path holds L + 1 vids when it met
+// at length L (an ACTIVE pair has none); doff = their exclusive scan, cnt[C_PLEN] the total,
+// cnt[C_MAXL] the longest L, cnt[C_WALKERR] cleared.  The host reads the two counters with one
+// counter fetch instead of copying state and res back and scanning them itself.
+__global__ __launch_bounds__(1024) void k_sp_path_offsets(SpState st, int64_t nb, int64_t* doff,
+                                                          unsigned long long* cnt) {
+  __shared__ int64_t s_w[16];
+  __shared__ int32_t s_m[16];
+  __shared__ int64_t s_carry;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_carry = 0;
+  int32_t mx = 0;
+  __syncthreads();
+  for (int64_t p0 = 0; p0 < nb; p0 += blockDim.x) {
+    const int64_t p = p0 + threadIdx.x;
+    int64_t len = 0;
+    if (p < nb && st.state[p] != SP_ACTIVE) {
+      const int32_t L = st.res[p];
+      if (L >= 0) {
+        len = L + 1;
+        mx = max(mx, st.state[p] == SP_MET ? L : 0);
+      }
+    }
+    int64_t v = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(v, o);
+      if (lane >= o) v += y;
+    }
+    if (lane == 63) s_w[wv] = v;
+    __syncthreads();
+    int64_t pre = s_carry, tot = 0;
+    for (int w = 0; w < int(blockDim.x >> 6); w++) {
+      if (w < wv) pre += s_w[w];
+      tot += s_w[w];
+    }
+    if (p < nb) doff[p] = pre + v - len;
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry += tot;
+    __syncthreads();
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+  if (lane == 0) s_m[wv] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t m = 0;
+    for (int w = 0; w < int(blockDim.x >> 6); w++) m = max(m, s_m[w]);
+    doff[nb] = s_carry;
+    cnt[C_PLEN] = (unsigned long long)s_carry;
+    cnt[C_MAXL] = (unsigned long long)m;
+    cnt[C_WALKERR] = 0ull;
+  }
+}
+
 __global__ void k_add_i64(int64_t* a, int64_t n, int64_t v) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
     a[i] += v;
@@ -1470,8 +1525,8 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   const bool probe = c.opt("sp_probe", 1) != 0;
 
   std::vector<int64_t> hres(npairs), hoff(1, 0), hpath;
-  std::vector<int32_t> hstate(static_cast<size_t>(B)), hres_b(static_cast<size_t>(B)),
-      hside(static_cast<size_t>(B)), hmet(static_cast<size_t>(B));
+  std::vector<int32_t> hstate(static_cast<size_t>(2 * B)), hside(static_cast<size_t>(B)),
+      hmet(static_cast<size_t>(B));
   if (hash && c.sp_dirty && W.hcap > 0)  // a failed call's claims
     for (auto& t : W.htab) NBG_HIP(hipMemsetAsync(t.p, 0xFF, size_t(W.hcap) * 8, c.stream));
   c.sp_dirty = true;  // until the batch's bytes are reset
@@ -1504,8 +1559,18 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       st.lvbits = W.lvbits.as<uint32_t>();
       st.lvw = lvw;
     }
-    NBG_HIP(hipMemcpyAsync(dsv, src + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
-    NBG_HIP(hipMemcpyAsync(dtv, dst + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
+    if (c.host_stage && c.host_stage_used == 0 && size_t(nb) * 16 <= kHostStageBytes) {
+      // through the pinned stage: a pageable source makes the copy wait on the host (the stage's
+      // previous contents, the last batch's results, were read back before this point)
+      int64_t* hs = static_cast<int64_t*>(c.host_stage);
+      memcpy(hs, src + b0, size_t(nb) * 8);
+      memcpy(hs + nb, dst + b0, size_t(nb) * 8);
+      NBG_HIP(hipMemcpyAsync(dsv, hs, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
+      NBG_HIP(hipMemcpyAsync(dtv, hs + nb, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
+    } else {
+      NBG_HIP(hipMemcpyAsync(dsv, src + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
+      NBG_HIP(hipMemcpyAsync(dtv, dst + b0, size_t(nb) * 8, hipMemcpyHostToDevice, c.stream));
+    }
     lookup_gidx(c, dsv, dgs, nb);
     lookup_gidx(c, dtv, dgt, nb);
     NBG_HIP(hipMemsetAsync(cnt, 0, C_N * 8, c.stream));
@@ -1887,28 +1952,19 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       nxt ^= 1;
     }
 
-    // results + paths
-    NBG_HIP(hipMemcpyAsync(hstate.data(), st.state, size_t(nb) * 4, hipMemcpyDeviceToHost, c.stream));
-    NBG_HIP(hipMemcpyAsync(hres_b.data(), st.res, size_t(nb) * 4, hipMemcpyDeviceToHost, c.stream));
-    NBG_HIP(hipStreamSynchronize(c.stream));
-    std::vector<int64_t> boff(size_t(nb) + 1, 0);
-    for (int64_t p = 0; p < nb; p++) {
-      const int32_t L = hstate[size_t(p)] == SP_ACTIVE ? -1 : hres_b[size_t(p)];
-      hres[b0 + size_t(p)] = L;
-      boff[size_t(p) + 1] = boff[size_t(p)] + (L >= 0 ? L + 1 : 0);
-    }
-    const int64_t plen = boff[size_t(nb)];
-    const size_t base = hpath.size();
-    hpath.resize(base + size_t(plen));
+    // results + paths: the path offsets, their total and the longest path on the device (one
+    // counter fetch); state, res, offsets and the walked paths come back with the batch's last
+    // fetch, through the pinned stage when they fit (pageable copies and a stream synchronisation
+    // here cost ~0.1 ms a batch)
+    DevBuf doff, dpath, wk;  // (wk: the walk state, drained by the batch's last fetch)
+    doff.alloc(size_t(nb + 1) * 8);
+    k_sp_path_offsets<<<1, 1024, 0, c.stream>>>(st, nb, doff.as<int64_t>(), cnt);
+    NBG_HIP(hipGetLastError());
+    sync_counters();
+    const int64_t plen = int64_t(hc[C_PLEN]);
+    const int32_t maxL = int32_t(hc[C_MAXL]);
     if (plen > 0) {
-      DevBuf doff, dpath, wk;  // (wk: the walk state, drained by the path copy's fetch below)
-      doff.alloc(size_t(nb + 1) * 8);
       dpath.alloc(size_t(plen) * 8);
-      NBG_HIP(hipMemcpyAsync(doff.p, boff.data(), size_t(nb + 1) * 8, hipMemcpyHostToDevice, c.stream));
-      zero(1u << C_WALKERR);
-      int32_t maxL = 0;
-      for (int64_t p = 0; p < nb; p++)
-        if (hstate[size_t(p)] == SP_MET) maxL = std::max(maxL, hres_b[size_t(p)]);
       if (c.opt("sp_walk_wg", 0) || nb >= kTileE) {  // a tile stages at most kTileE pair entries
         k_sp_walk<<<int(nb), kWalkT, 0, c.stream>>>(st, dgs, doff.as<int64_t>(), dpath.as<int64_t>(), gout, d1,
                                                     vid_of, n, lo, cnt);
@@ -1944,18 +2000,45 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         }
       }
       NBG_HIP(hipGetLastError());
-      NBG_HIP(hipMemcpyAsync(hpath.data() + base, dpath.p, size_t(plen) * 8, hipMemcpyDeviceToHost, c.stream));
-      sync_counters();
-      if (hc[C_WALKERR])
-        throw Error(NBG_E_UNKNOWN, "shortest path: in-edge keys without mirrored out-edges on a shortest path");
-      for (int64_t p = 0; p < nb; p++) {  // the ends: src (also the whole path of src == dst) and dst
-        const int64_t L = hres[b0 + size_t(p)];
-        if (L < 0) continue;
-        hpath[base + size_t(boff[size_t(p)])] = src[b0 + size_t(p)];
-        if (L > 0) hpath[base + size_t(boff[size_t(p)] + L)] = dst[b0 + size_t(p)];
-      }
     }
-    for (int64_t p = 0; p < nb; p++) hoff.push_back(hoff.back() + boff[size_t(p) + 1] - boff[size_t(p)]);
+    const size_t sb = (size_t(nb) * 8 + 63) & ~size_t(63);  // state + res (adjacent in W.state)
+    const size_t ob = (size_t(nb + 1) * 8 + 63) & ~size_t(63);
+    const bool staged = c.host_stage && c.host_stage_used == 0 && sb + ob + size_t(plen) * 8 <= kHostStageBytes;
+    std::vector<int64_t> hoff_b, hpath_b;
+    int32_t* h_sr = hstate.data();  // [state nb][res nb]
+    int64_t* h_off = nullptr;
+    int64_t* h_path = nullptr;
+    if (staged) {
+      char* hs = static_cast<char*>(c.host_stage);
+      h_sr = reinterpret_cast<int32_t*>(hs);
+      h_off = reinterpret_cast<int64_t*>(hs + sb);
+      h_path = reinterpret_cast<int64_t*>(hs + sb + ob);
+    } else {
+      hstate.resize(size_t(2 * nb));
+      h_sr = hstate.data();
+      hoff_b.resize(size_t(nb + 1));
+      hpath_b.resize(size_t(std::max<int64_t>(plen, 1)));
+      h_off = hoff_b.data();
+      h_path = hpath_b.data();
+    }
+    NBG_HIP(hipMemcpyAsync(h_sr, st.state, size_t(nb) * 8, hipMemcpyDeviceToHost, c.stream));
+    NBG_HIP(hipMemcpyAsync(h_off, doff.p, size_t(nb + 1) * 8, hipMemcpyDeviceToHost, c.stream));
+    if (plen > 0) NBG_HIP(hipMemcpyAsync(h_path, dpath.p, size_t(plen) * 8, hipMemcpyDeviceToHost, c.stream));
+    sync_counters();  // every copy above has landed (stream order) and C_WALKERR is current
+    if (plen > 0 && hc[C_WALKERR])
+      throw Error(NBG_E_UNKNOWN, "shortest path: in-edge keys without mirrored out-edges on a shortest path");
+    const size_t base = hpath.size();
+    hpath.resize(base + size_t(plen));
+    if (plen > 0) memcpy(hpath.data() + base, h_path, size_t(plen) * 8);
+    for (int64_t p = 0; p < nb; p++) {
+      const int32_t L = h_sr[p] == SP_ACTIVE ? -1 : h_sr[nb + p];
+      hres[b0 + size_t(p)] = L;
+      if (L >= 0) {  // the ends: src (also the whole path of src == dst) and dst
+        hpath[base + size_t(h_off[p])] = src[b0 + size_t(p)];
+        if (L > 0) hpath[base + size_t(h_off[p] + L)] = dst[b0 + size_t(p)];
+      }
+      hoff.push_back(hoff.back() + h_off[p + 1] - h_off[p]);
+    }
     // reset the batch's distance bytes
     if (hash) {
       for (auto& t : W.htab) NBG_HIP(hipMemsetAsync(t.p, 0xFF, size_t(W.hcap) * 8, c.stream));
