@@ -108,8 +108,8 @@ __device__ inline int64_t wave_append(unsigned long long* counter, bool pred) {
 // entry k writes the tiles whose first slot falls in [off[k], off[k + 1]) (each tile start lies
 // in exactly one non-empty entry).  One coalesced pass over off[] instead of two dependent binary
 // searches of off[] by one thread at the head of every tile.
-// Every wave takes 64 consecutive entries (one per lane) and fills their item ranges [i0, i1)
-// together, entry by entry, 64 items a step: a hub entry's thousands of tiles / chunks are no
+// Every wave takes 64 consecutive entries (one per lane); a lane fills a range of up to 4 items
+// itself, longer ranges [i0, i1) are filled by the whole wave, entry by entry, 64 items a step: a hub entry's thousands of tiles / chunks are no
 // longer one thread's serial loop (~20 us for the C4 probe's largest rows).  Wave-uniform;
 // blockDim a multiple of 64.  range(k, i0, i1) gives entry k's items; fill(item, k) writes one.
 template <typename Range, typename Fill>
@@ -120,6 +120,11 @@ __device__ inline void wave_fill_ranges(int64_t nk, Range range, Fill fill) {
   for (int64_t k0 = wave * 64; k0 < nk; k0 += nwaves * 64) {
     int64_t i0 = 0, i1 = 0;
     if (k0 + lane < nk) range(k0 + lane, i0, i1);
+    // short ranges (most entries: one or two items) by their own lane, the rest together
+    if (i1 - i0 <= 4) {
+      for (int64_t i = i0; i < i1; i++) fill(i, k0 + lane);
+      i1 = i0;
+    }
     uint64_t m = __ballot(i1 > i0);
     while (m) {
       const int j = __ffsll((long long)m) - 1;

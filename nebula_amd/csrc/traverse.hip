@@ -2157,18 +2157,15 @@ struct Counters {
 
 // Copies n device counters into coherent host memory, then the sequence word: each thread's
 // store is made visible system-wide before thread 0 publishes the sequence number.
-__global__ void k_publish(const unsigned long long* __restrict__ src, int n, unsigned long long* dst,
+// One wave copies the words (a lane per word, loads in flight together), and lane 0 publishes
+// the sequence with one system-scope release store: one system fence (an L2 write-back) instead
+// of one per word.  A single wave, so the release's wait on the wave's outstanding stores covers
+// every copy.  (One thread copying every word waited on each load in turn: ~10 us more.)
+__global__ void k_publish(const unsigned long long* __restrict__ src, int n, unsigned long long* __restrict__ dst,
                           unsigned long long* seq_slot, unsigned long long seq) {
-  const int i = threadIdx.x;
-  if (i < n) {
-    dst[i] = src[i];
-    __threadfence_system();
-  }
+  for (int i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
   __syncthreads();
-  if (i == 0) {
-    __threadfence_system();
-    __hip_atomic_store(seq_slot, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  if (threadIdx.x == 0) __hip_atomic_store(seq_slot, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // the device counters d[0, n) into host h[0, n) once every launch before has finished: a
@@ -2179,7 +2176,7 @@ void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long lo
   if (n > 256) throw Error(NBG_E_INVALID_ARG, "fetch_counters: at most 256 words");
   if (before) NBG_HIP(hipEventRecord(before, c.stream));
   const uint64_t seq = ++c.pub_seq;
-  k_publish<<<1, 256, 0, c.stream>>>(d, n, h, c.host_seq, seq);
+  k_publish<<<1, 64, 0, c.stream>>>(d, n, h, c.host_seq, seq);
   NBG_HIP(hipGetLastError());
   c.timing.host_waits++;
   if (c.opt("wait_trace", 0)) fprintf(stderr, "[nbg wait] rank %d: counter fetch of %d words\n", c.rank, n);
