@@ -311,7 +311,9 @@ typedef struct {
   int32_t host_waits;     /* times the engine waited on the host for the device in the last
                              call (counter fetches, stream synchronisations; waits inside the
                              LocalComm / RCCL transport not included)                          */
-  int32_t spec_hops;      /* nbg_go hops that ran speculatively behind a device gate (k_gate)  */
+  int32_t spec_hops;      /* nbg_go: hops that ran speculatively behind a device gate;
+                             nbg_shortest_path: batches that ran device-driven (the others ran
+                             host-driven: option sp_dev = 0, or a list overflow re-ran them)   */
 } nbg_timing;
 int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out);
 /* engine option key = value (tuning knobs); value INT64_MIN removes the key, so the

@@ -120,6 +120,7 @@ void nbg_ctx_destroy(nbg_ctx* ctx) {
   for (auto& e : ctx->c.tev) (void)hipEventDestroy(e);
   if (ctx->c.host_counters) (void)hipHostFree(ctx->c.host_counters);
   if (ctx->c.host_stage) (void)hipHostFree(ctx->c.host_stage);
+  if (ctx->c.sp_host) (void)hipHostFree(ctx->c.sp_host);
   (void)hipStreamDestroy(ctx->c.stream);
   delete ctx;
 }

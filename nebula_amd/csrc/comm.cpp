@@ -124,7 +124,7 @@ struct LocalGroup {
   int arrived = 0;
   uint64_t gen = 0;
   std::vector<const void*> ptr, ptr2;
-  std::vector<const size_t*> sizes, offs;
+  std::vector<const size_t*> sizes, offs, rsizes;
   std::vector<size_t> scalar;
   std::vector<uint64_t> op;  // per rank: the collective it entered (kind | fixed size << 8)
   std::vector<hipEvent_t> ready, done;
@@ -153,23 +153,14 @@ __global__ void k_sum_slices(const int64_t* in, int world, size_t n, int64_t* ou
 
 // The in-process transport also holds every exchange to RCCL's pairing rule: a grouped
 // ncclSend / ncclRecv pair must agree on the byte count, and a side that skips a zero-byte
-// transfer must face a peer that skips it too (otherwise RCCL hangs or truncates).  A mismatch is
-// recorded while the collective completes (every rank still reaches both barriers) and thrown
-// after it, so the multi-rank tests that run on LocalComm prove the RCCL exchange sizes as well.
+// transfer must face a peer that skips it too (otherwise RCCL hangs or truncates); and every rank
+// must be in the same collective (RCCL matches them by issue order).  Each rank publishes its
+// collective, send sizes and receive sizes before barrier A; after it every rank checks every
+// pair from the same published arrays, so all ranks reach the same verdict before any data moves.
+// On a mismatch no rank copies anything (a peer's pointers may belong to another collective),
+// every rank still passes barrier B so the group stays in step, and every rank throws.
 struct LocalComm : CommImpl {
   int32_t transport() const override { return 2; }
-  std::string mismatch;
-  void pair_check(Ctx& c, int p, size_t peer_sends, size_t i_recv, const char* what) {
-    if (p == c.rank || peer_sends == i_recv || !mismatch.empty()) return;
-    mismatch = std::string(what) + ": rank " + std::to_string(p) + " sends " + std::to_string(peer_sends) +
-               " bytes, rank " + std::to_string(c.rank) + " receives " + std::to_string(i_recv);
-  }
-  void raise_mismatch() {
-    if (mismatch.empty()) return;
-    std::string m;
-    m.swap(mismatch);
-    throw Error(NBG_E_COMM, "exchange sizes would not pair under RCCL: " + m);
-  }
   int32_t ranks() const override { return g ? int32_t(g->world) : -1; }
   std::shared_ptr<LocalGroup> g;
   hipEvent_t ready = nullptr, done = nullptr;
@@ -178,23 +169,39 @@ struct LocalComm : CommImpl {
     if (ready) (void)hipEventDestroy(ready);
     if (done) (void)hipEventDestroy(done);
   }
-  // step 1 + barrier A; every rank must have entered the same collective (RCCL matches
-  // collectives by issue order, so a rank in another one would hang or mix the buffers there)
-  void publish(Ctx& c, uint64_t op) {
+  // what rank p sends to rank q (kinds 1 and 3: the same to everyone; 2: its row of send sizes)
+  size_t sent(int kind, int p, int q) const { return kind == 2 ? g->sizes[size_t(p)][q] : g->scalar[size_t(p)]; }
+  // step 1 + barrier A, then the group's verdict (empty: every rank entered collective `op` and
+  // every send pairs with its receive), the same string on every rank
+  std::string publish(Ctx& c, uint64_t op, const size_t* recv_bytes) {
     g->op[size_t(c.rank)] = op;
+    g->rsizes[size_t(c.rank)] = recv_bytes;
     NBG_HIP(hipEventRecord(ready, c.stream));
     g->barrier();
     for (int p = 0; p < c.world; p++)
-      if (g->op[size_t(p)] != op && mismatch.empty())
-        mismatch = "rank " + std::to_string(p) + " entered collective " + std::to_string(g->op[size_t(p)]) +
-                   " while rank " + std::to_string(c.rank) + " entered " + std::to_string(op);
+      if (g->op[size_t(p)] != g->op[0])
+        return "rank " + std::to_string(p) + " entered collective " + std::to_string(g->op[size_t(p)]) +
+               " while rank 0 entered " + std::to_string(g->op[0]);
+    const int kind = int(op & 0xFF);
+    if (kind == 4) return std::string();  // allreduce: its size is part of op
+    const char* what = kind == 1 ? "allgatherv" : kind == 2 ? "alltoallv" : "allgatherv2";
+    for (int q = 0; q < c.world; q++)
+      for (int p = 0; p < c.world; p++) {
+        if (p == q) continue;
+        const size_t sb = sent(kind, p, q), rb = g->rsizes[size_t(q)][p];
+        if (sb != rb)
+          return std::string(what) + ": rank " + std::to_string(p) + " sends " + std::to_string(sb) +
+                 " bytes, rank " + std::to_string(q) + " receives " + std::to_string(rb);
+      }
+    return std::string();
   }
-  // (after the receive copies) step 2's `done` + barrier B + step 3
-  void finish(Ctx& c) {
+  // (after the receive copies, or none) step 2's `done` + barrier B + step 3, then the verdict
+  void finish(Ctx& c, const std::string& mismatch) {
     NBG_HIP(hipEventRecord(done, c.stream));
     g->barrier();
     for (int p = 0; p < c.world; p++)
       if (p != c.rank) NBG_HIP(hipStreamWaitEvent(c.stream, g->done[size_t(p)], 0));
+    if (!mismatch.empty()) throw Error(NBG_E_COMM, "exchange sizes would not pair under RCCL: " + mismatch);
   }
   void wait_ready(Ctx& c, int p) {
     if (p != c.rank) NBG_HIP(hipStreamWaitEvent(c.stream, g->ready[size_t(p)], 0));
@@ -203,26 +210,23 @@ struct LocalComm : CommImpl {
                   const size_t* recv_off) override {
     g->ptr[size_t(c.rank)] = send;
     g->scalar[size_t(c.rank)] = send_bytes;
-    publish(c, 1);
-    for (int p = 0; p < c.world; p++) {
-      pair_check(c, p, g->scalar[size_t(p)], recv_bytes[p], "allgatherv");
+    const std::string bad = publish(c, 1, recv_bytes);
+    for (int p = 0; p < c.world && bad.empty(); p++) {
       size_t b = std::min(g->scalar[size_t(p)], recv_bytes[p]);
       if (!b || g->ptr[size_t(p)] == static_cast<uint8_t*>(recv) + recv_off[p]) continue;
       wait_ready(c, p);
       NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[p], g->ptr[size_t(p)], b,
                              hipMemcpyDeviceToDevice, c.stream));
     }
-    finish(c);
-    raise_mismatch();
+    finish(c, bad);
   }
   void alltoallv(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
                  const size_t* recv_bytes, const size_t* recv_off) override {
     g->ptr[size_t(c.rank)] = send;
     g->sizes[size_t(c.rank)] = send_bytes;
     g->offs[size_t(c.rank)] = send_off;
-    publish(c, 2);
-    for (int p = 0; p < c.world; p++) {
-      pair_check(c, p, g->sizes[size_t(p)][c.rank], recv_bytes[p], "alltoallv");
+    const std::string bad = publish(c, 2, recv_bytes);
+    for (int p = 0; p < c.world && bad.empty(); p++) {
       size_t b = std::min(g->sizes[size_t(p)][c.rank], recv_bytes[p]);
       if (!b) continue;
       wait_ready(c, p);
@@ -230,17 +234,15 @@ struct LocalComm : CommImpl {
                              static_cast<const uint8_t*>(g->ptr[size_t(p)]) + g->offs[size_t(p)][c.rank], b,
                              hipMemcpyDeviceToDevice, c.stream));
     }
-    finish(c);
-    raise_mismatch();
+    finish(c, bad);
   }
   void allgatherv2(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
                    const size_t* recv_off, const void* send2, size_t bytes2, void* recv2) override {
     g->ptr[size_t(c.rank)] = send;
     g->scalar[size_t(c.rank)] = send_bytes;
     g->ptr2[size_t(c.rank)] = send2;
-    publish(c, 3ull | uint64_t(bytes2) << 8);
-    for (int p = 0; p < c.world; p++) {
-      pair_check(c, p, g->scalar[size_t(p)], recv_bytes[p], "allgatherv2");
+    const std::string bad = publish(c, 3ull | uint64_t(bytes2) << 8, recv_bytes);
+    for (int p = 0; p < c.world && bad.empty(); p++) {
       wait_ready(c, p);
       size_t b = std::min(g->scalar[size_t(p)], recv_bytes[p]);
       if (b && g->ptr[size_t(p)] != static_cast<uint8_t*>(recv) + recv_off[p])
@@ -249,8 +251,7 @@ struct LocalComm : CommImpl {
       NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv2) + size_t(p) * bytes2, g->ptr2[size_t(p)], bytes2,
                              hipMemcpyDeviceToDevice, c.stream));
     }
-    finish(c);
-    raise_mismatch();
+    finish(c, bad);
   }
   // in place, as ncclAllReduce: gather the slices, sum them, and write the sums back only after
   // every peer has read this rank's slice
@@ -263,16 +264,17 @@ struct LocalComm : CommImpl {
     }
     int64_t* sl = scratch.as<int64_t>();
     g->ptr[size_t(c.rank)] = d;
-    publish(c, 4ull | uint64_t(n) << 8);
-    for (int p = 0; p < c.world; p++) {
-      wait_ready(c, p);
-      NBG_HIP(hipMemcpyAsync(sl + size_t(p) * n, g->ptr[size_t(p)], n * 8, hipMemcpyDeviceToDevice, c.stream));
+    const std::string bad = publish(c, 4ull | uint64_t(n) << 8, nullptr);
+    if (bad.empty()) {
+      for (int p = 0; p < c.world; p++) {
+        wait_ready(c, p);
+        NBG_HIP(hipMemcpyAsync(sl + size_t(p) * n, g->ptr[size_t(p)], n * 8, hipMemcpyDeviceToDevice, c.stream));
+      }
+      k_sum_slices<<<1, 256, 0, c.stream>>>(sl, c.world, n, sl + G * n);
+      NBG_HIP(hipGetLastError());
     }
-    k_sum_slices<<<1, 256, 0, c.stream>>>(sl, c.world, n, sl + G * n);
-    NBG_HIP(hipGetLastError());
-    finish(c);
+    finish(c, bad);
     NBG_HIP(hipMemcpyAsync(d, sl + G * n, n * 8, hipMemcpyDeviceToDevice, c.stream));
-    raise_mismatch();
   }
 };
 
@@ -321,6 +323,7 @@ void comm_init_local(Ctx& c, int64_t key) {
       slot->ptr2.resize(size_t(c.world));
       slot->sizes.resize(size_t(c.world));
       slot->offs.resize(size_t(c.world));
+      slot->rsizes.resize(size_t(c.world));
       slot->scalar.resize(size_t(c.world));
       slot->op.resize(size_t(c.world));
       slot->ready.resize(size_t(c.world));

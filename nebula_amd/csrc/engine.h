@@ -526,11 +526,19 @@ struct Ctx {
     DevBuf live[2], live_next[2], arena, meet, sweep[2], X, Xdeg, Xoff, state, cnt, vids, gidx, plist;
     DevBuf tile_rows;  // k_sp_expand: X entry of each tile's first slot
     DevBuf lvbits;     // per side and depth, the vertices some pair of the batch holds there
-    DevBuf htab[2];    // option sp_hash: per side (pair, vertex) -> depth maps (paths.hip)
-    int64_t hcap = 0;
     int64_t cap_live[2] = {0, 0}, cap_next[2] = {0, 0}, cap_arena = 0, cap_meet = 0, cap_sweep[2] = {0, 0};
     int64_t cap_x = 0, cap_state = 0, cap_plist = 0;
+    // device-driven batches (paths.hip, option sp_dev): fixed-capacity lists, chunk tables, the
+    // per-pair arrays, the pair and global level filters and the counter blocks
+    DevBuf dv_cnt, dv_live[4], dv_arena, dv_meet, dv_sw[2], dv_X, dv_Xcb, dv_chx, dv_slot, dv_wchx, dv_pair, dv_path,
+        dv_pf, dv_gf;
+    int64_t dv_B = 0, dv_cap = 0, dv_cap_ch = 0, dv_cap_wch = 0, dv_gf_log2 = -1;
+    bool dv_pf_on = false;
+    bool dv_clean = false;  // filter words and counters all zero
   } sp;
+  // coherent pinned host block of the device-driven batches: publish slots, the pairs, results
+  void* sp_host = nullptr;
+  size_t sp_host_bytes = 0;
   Timing timing;
   hipEvent_t ev[8] = {};
   DevBuf ws_tile_rows;  // k_expand: frontier entry of each tile's first slot
@@ -633,6 +641,8 @@ void lookup_gidx(Ctx& c, const int64_t* d_vids, int32_t* d_gidx, int64_t n);
 // finished on the context's stream (a one-block publish kernel + a host spin, traverse.hip)
 // `before` (optional): an event recorded just ahead of the publish kernel
 void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h, hipEvent_t before = nullptr);
+// one host wait (counted in Timing::host_waits) until the device publishes `seq` in `word`
+void wait_host_word(Ctx& c, const unsigned long long* word, uint64_t seq);
 // a query's total_ms (ev[0] -> ev[1]) once asked for (go_run records ev[1] without waiting)
 void resolve_total(Ctx& c);
 // traverse.hip

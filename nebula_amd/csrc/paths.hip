@@ -31,6 +31,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <array>
 #include <unordered_map>
 #include <climits>
 #include <cmath>
@@ -91,23 +92,8 @@ struct SpState {  // per-pair arrays, B entries each
   uint32_t* lvbits;
   int64_t lvw;
   uint32_t lvmask;
-  // sparse distance maps (option sp_hash, null: the dense byte arrays): per side, open-addressing
-  // (pair, vertex) -> depth over 64-bit words, hmask + 1 slots, sized to the batch's claims (a
-  // few million per side at RMAT-26, tens of MB that stay in the Infinity Cache and in a handful
-  // of TLB pages; the dense arrays are 2 * B * n bytes read at random lines)
-  uint64_t* htab[2];
-  uint64_t hmask;
 };
 constexpr int kLv = 8;
-
-// hash map words: bits [0, 31) vertex, [31, 54) pair, [54, 62) depth; all ones = empty
-constexpr uint64_t kHEmpty = ~0ull;
-constexpr uint64_t kHKey = (1ull << 54) - 1;
-__device__ inline uint64_t hkey(uint32_t p, uint32_t v) { return (uint64_t(p) << 31) | uint64_t(v); }
-__device__ inline uint64_t hslot(uint64_t key, uint64_t mask) {
-  uint64_t x = key * 0x9E3779B97F4A7C15ull;
-  return (x ^ (x >> 29)) & mask;
-}
 
 __device__ inline void lv_mark(const SpState& st, uint32_t side, uint32_t l, uint32_t v) {
   if (st.lvbits && l >= 1 && l < uint32_t(kLv))
@@ -180,35 +166,18 @@ __device__ inline bool claim_byte(uint8_t* base, uint64_t idx, uint32_t val) {
   return false;
 }
 
-// the depth of vertex v for pair p on a side (0xFF: unseen), from the dense bytes or the map
+// the depth of vertex v for pair p on a side (0xFF: unseen)
 __device__ inline uint32_t dist_get(const SpState& st, const uint8_t* dense, uint32_t side, uint32_t p, uint32_t v,
                                     int64_t n, bool fresh = false) {
-  if (!st.htab[0]) {
-    const uint8_t* a = dense + didx(st, p, v, n);
-    return fresh ? uint32_t(*reinterpret_cast<volatile const uint8_t*>(a)) : uint32_t(*a);
-  }
-  const uint64_t* T = st.htab[side];
-  const uint64_t key = hkey(p, v);
-  for (uint64_t h = hslot(key, st.hmask);; h = (h + 1) & st.hmask) {
-    const uint64_t e = fresh ? __hip_atomic_load(T + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : T[h];
-    if (e == kHEmpty) return 0xFFu;
-    if ((e & kHKey) == key) return uint32_t(e >> 54) & 0xFFu;
-  }
+  (void)side;
+  const uint8_t* a = dense + didx(st, p, v, n);
+  return fresh ? uint32_t(*reinterpret_cast<volatile const uint8_t*>(a)) : uint32_t(*a);
 }
 // claim the unseen (p, v) on a side with depth val: true for exactly one caller
 __device__ inline bool dist_claim(const SpState& st, uint8_t* dense, uint32_t side, uint32_t p, uint32_t v, int64_t n,
                                   uint32_t val) {
-  if (!st.htab[0]) return claim_byte(dense, didx(st, p, v, n), val);
-  uint64_t* T = st.htab[side];
-  const uint64_t key = hkey(p, v), word = key | (uint64_t(val & 0xFFu) << 54);
-  for (uint64_t h = hslot(key, st.hmask);; h = (h + 1) & st.hmask) {
-    uint64_t e = T[h];
-    if (e == kHEmpty) {
-      e = atomicCAS(reinterpret_cast<unsigned long long*>(T + h), (unsigned long long)kHEmpty, (unsigned long long)word);
-      if (e == kHEmpty) return true;
-    }
-    if ((e & kHKey) == key) return false;
-  }
+  (void)side;
+  return claim_byte(dense, didx(st, p, v, n), val);
 }
 
 // zero the counter slots in `mask` (bit i = cnt[i]; one launch instead of a memset per slot run)
@@ -1217,51 +1186,6 @@ __global__ void k_sp_walk_pick(SpState st, int32_t i, int32_t* cur, const long l
   cur[p] = ht_lookup(ht_keys, ht_vals, ht_mask, int64_t(b), ht_has_min, ht_min_gidx) - int32_t(lo);
 }
 
-// sparse maps: RG_* list rebuilds from the map words of the listed pairs (pflag[p] = 1)
-__global__ void k_sp_regen_hash(int mode, int side, int32_t j, const uint8_t* pflag, SpState st, int64_t n,
-                                uint64_t* out, int64_t cap, unsigned long long* cnt, int which) {
-  const int32_t B = st.B;
-  const uint64_t* T = st.htab[mode == RG_LIVE ? side : 1];
-  const int64_t slots = int64_t(st.hmask) + 1;
-  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-  const int64_t rounds = (slots + stride - 1) / stride;
-  for (int64_t r = 0; r < rounds; r++) {
-    const int64_t i = r * stride + blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-    bool hit = false;
-    uint32_t p = 0, v = 0, d = 0;
-    if (i < slots) {
-      const uint64_t e = T[i];
-      if (e != kHEmpty) {
-        p = uint32_t(e >> 31) & 0x7FFFFFu;
-        v = uint32_t(e & 0x7FFFFFFFu);
-        d = uint32_t(e >> 54) & 0xFFu;
-        if (int32_t(p) < B && pflag[p]) {
-          if (mode == RG_LIVE) hit = d == uint32_t(st.lvl[side * B + p]);
-          else if (mode == RG_MEET)
-            hit = d == uint32_t(st.lvl[B + p]) && dist_get(st, nullptr, 0, p, v, n) == uint32_t(st.lvl[p]);
-          else hit = d == uint32_t(st.lvl[B + p] + j);
-        }
-      }
-    }
-    put(out, cap, cnt, which, hit, mk_tup(mode == RG_LIVE ? uint32_t(side) : 1u, p, d, v));
-  }
-}
-__global__ void k_set_flags(const int32_t* plist, int32_t np, uint8_t* flag) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < np) flag[plist[i]] = 1;
-}
-// grow a map: every word of the old table inserted into the new one (same key -> slot rule)
-__global__ void k_hash_rehash(const uint64_t* old, int64_t nold, uint64_t* nt, uint64_t nmask) {
-  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < nold; i += int64_t(gridDim.x) * blockDim.x) {
-    const uint64_t e = old[i];
-    if (e == kHEmpty) continue;
-    for (uint64_t h = hslot(e & kHKey, nmask);; h = (h + 1) & nmask)
-      if (atomicCAS(reinterpret_cast<unsigned long long*>(nt + h), (unsigned long long)kHEmpty, (unsigned long long)e) ==
-          kHEmpty)
-        break;
-  }
-}
-
 // reset every claimed distance byte of the batch
 __global__ void k_sp_clear(const uint64_t* arena, int64_t m, uint8_t* d0, uint8_t* d1, int64_t n, SpState st) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < m; i += int64_t(gridDim.x) * blockDim.x) {
@@ -1288,6 +1212,1119 @@ void reserve(Ctx& c, DevBuf& b, int64_t& cap, int64_t need, int64_t keep) {
   }
   b = std::move(nb);
   cap = nc;
+}
+
+// ==== device-driven batches (option sp_dev, default 1) ===========================================
+// A batch as one fixed chain of launches.  Every kernel reads its list lengths and chunk counts
+// from device counters, the producers fill the chunk tables through block-reserved ranges (no
+// scans, no host-sized grids), and the last block of each BFS step publishes that iteration's
+// counters to coherent host memory (no publish launch).  The host enqueues iteration i + 1 before
+// it reads iteration i's counters, so the device never idles on a round trip inside the BFS; the
+// sweep and the walk are enqueued in one go once the longest path is known.  Launches per batch:
+// begin, 4 per BFS iteration (select, meet probe, expansion + the probe's meets, step), a post
+// pass, 2 per sweep step, 2 per walk step, the result pass and the finish publish.  A list that
+// overflows its fixed capacity makes the host restore the clean state and re-run the batch on the
+// host-driven path (which grows its lists and regenerates lost appends).
+//
+// Level filters: a test "dist[side][p][v] == l" (meet probe, sweep, walk) first asks
+//  * the pair's own filter of (side, l): 4096 bits per (side, level, pair), set at every claim; a
+//    scanning wave holds its chunk's pair row in registers (8 bytes a lane) and tests an entry with
+//    two cross-lane reads (ds_bpermute): no memory access;
+//  * then a blocked Bloom filter over (side, level, pair, vertex) keys, 3 bits in one 32-bit word
+//    (option sp_gf_log2, default 2^24 bits = 2 MiB, L2-resident);
+// and only an entry that passes both reads the pair's distance byte (a random line of the 2 * B * n
+// byte arrays).  The host-driven path's batch-wide level bitmaps (the union over all pairs) pass
+// most entries of the large steps, and each passed entry fetched a whole line for one byte (PMC:
+// sweep 5.1x, probe 6.7x their byte models).  Depth 0 is tested exactly (the pair's src / dst).
+enum : int { D_ARENA = 0, D_MEET = 1, D_OVF = 2, D_WALKERR = 3, D_MAXL = 4, D_MAXF = 5, D_TICKET = 6, D_CLEAR = 7,
+             D_G = 16 };
+enum : int { Q_LIVE0 = 0, Q_LIVE1 = 1, Q_X = 2, Q_NCH = 3, Q_XE = 4, Q_PE = 5, Q_ACTIVE = 6, Q_CLAIMS = 7, Q_EE = 8,
+             Q_W = 16 };
+constexpr int kMaxQ = 32;                 // BFS iterations, sweep steps, walk steps (each)
+constexpr int kSwQ = kMaxQ, kWkQ = 2 * kMaxQ, kNQ = 3 * kMaxQ;
+constexpr int kDevCnt = D_G + kNQ * Q_W;  // counter words
+constexpr int kCh = 1024;                 // adjacency entries per chunk (one wave)
+constexpr int kPubW = 64;                 // words per host publish slot (the sequence word last)
+constexpr int kDvStage = 256;             // claims staged per wave and list
+__device__ inline unsigned long long* qblk(unsigned long long* cnt, int q) { return cnt + D_G + q * Q_W; }
+
+struct SpFilt {
+  uint32_t* pf;     // [2 * kLv][B][128] pair filters (null: off)
+  uint32_t* gf;     // blocked Bloom filter words (null: off)
+  uint32_t gshift;  // 64 - log2(gf words)
+  int32_t B;
+  int32_t k2;       // pair filters with two bits per vertex (option sp_pf_k = 2)
+};
+__device__ inline uint32_t pf_bit(uint32_t v) { return (v * 0x9E3779B1u) >> 20; }
+__device__ inline uint32_t pf_bit2(uint32_t v) { return ((v * 0x9E3779B1u) >> 8) & 4095u; }
+__device__ inline uint64_t gf_hash(uint32_t sl, uint32_t p, uint32_t v) {
+  uint64_t h = (uint64_t(v) * 0xD6E8FEB86659FD93ull) ^ (uint64_t(p) * 0xA0761D6478BD642Full) ^
+               (uint64_t(sl + 1) * 0xE7037ED1A0B428DBull);
+  h ^= h >> 31;
+  return h * 0x9E3779B97F4A7C15ull;
+}
+__device__ inline uint32_t gf_mask(uint64_t h) {
+  return (1u << (h & 31u)) | (1u << ((h >> 5) & 31u)) | (1u << ((h >> 10) & 31u));
+}
+__device__ inline void filt_mark(const SpFilt& f, uint32_t side, uint32_t l, uint32_t p, uint32_t v) {
+  if (l < 1 || l >= uint32_t(kLv)) return;
+  const uint32_t sl = side * kLv + l;
+  if (f.pf) {
+    uint32_t* row = f.pf + (size_t(sl) * uint32_t(f.B) + p) * 128;
+    const uint32_t b = pf_bit(v);
+    atomicOr(row + (b >> 5), 1u << (b & 31u));
+    if (f.k2) {
+      const uint32_t b2 = pf_bit2(v);
+      atomicOr(row + (b2 >> 5), 1u << (b2 & 31u));
+    }
+  }
+  if (f.gf) {
+    const uint64_t h = gf_hash(sl, p, v);
+    atomicOr(f.gf + (h >> f.gshift), gf_mask(h));
+  }
+}
+// the chunk's pair row of the pair filter (side, l) in registers: lane i holds words 2i, 2i + 1
+__device__ inline uint2 pf_load(const SpFilt& f, uint32_t side, int32_t l, uint32_t p, bool& on) {
+  on = f.pf && l >= 1 && l < kLv;
+  if (!on) return make_uint2(~0u, ~0u);
+  const uint2* r = reinterpret_cast<const uint2*>(f.pf + (size_t(side * kLv + uint32_t(l)) * uint32_t(f.B) + p) * 128);
+  return r[threadIdx.x & 63];
+}
+// bit b of the row: wave-uniform call (cross-lane reads of every lane's row words)
+__device__ inline bool pf_bit_set(uint2 row, uint32_t b) {
+  const uint32_t wd = b >> 5;
+  const int src = int((wd >> 1) << 2);
+  const uint32_t lo = uint32_t(__builtin_amdgcn_ds_bpermute(src, int(row.x)));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_ds_bpermute(src, int(row.y)));
+  return ((((wd & 1u) ? hi : lo) >> (b & 31u)) & 1u) != 0u;
+}
+// (both cross-lane reads run on every active lane: a lane left out of a ds_bpermute reads as 0 to
+// the lanes that ask it, so the second read must not depend on the first's answer)
+__device__ inline bool pf_test(uint2 row, uint32_t v, bool k2) {
+  const bool a = pf_bit_set(row, pf_bit(v));
+  if (!k2) return a;  // wave-uniform
+  const bool b = pf_bit_set(row, pf_bit2(v));
+  return a && b;
+}
+__device__ inline bool gf_test(const SpFilt& f, uint32_t side, int32_t l, uint32_t p, uint32_t v) {
+  if (!f.gf || l < 1 || l >= kLv) return true;
+  const uint64_t h = gf_hash(side * kLv + uint32_t(l), p, v);
+  const uint32_t m = gf_mask(h);
+  return (f.gf[h >> f.gshift] & m) == m;
+}
+
+// the overflow flag as the block sees it at its start (block-uniform: the kernels below end with
+// block-wide reductions, and this launch may raise the flag while its blocks run)
+__device__ inline bool dv_ovf_block(const unsigned long long* cnt) {
+  __shared__ int s_ovf;
+  if (threadIdx.x == 0) s_ovf = __hip_atomic_load(cnt + D_OVF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  __syncthreads();
+  return s_ovf != 0;
+}
+
+struct SpDev {
+  unsigned long long* cnt;   // kDevCnt counters
+  uint64_t* live[2][2];      // [iteration parity][side]
+  int64_t cap_live;
+  uint64_t* arena;
+  int64_t cap_arena;
+  uint64_t* meet;
+  int64_t cap_meet;
+  uint64_t* sw[2];           // sweep lists by step parity
+  int64_t cap_sw;
+  uint64_t* X;
+  int64_t* Xcb;              // first chunk of each X entry
+  int64_t cap_x;
+  int32_t* chx;              // chunk -> X entry
+  uint64_t* slot;            // meet probe: chunk -> the claim it made (~0: none)
+  int64_t cap_ch;
+  int32_t* wchx;             // walk: chunk -> pair
+  int64_t cap_wch;
+  int64_t* wcb;              // walk: first chunk of each pair
+  int32_t* gs;               // [2B] src gidx, dst gidx
+  int32_t* cur;              // walk: current vertex of each pair
+  long long* best;           // walk: smallest candidate vid of each pair
+  unsigned long long* pull;  // [kMaxQ][B] sweep step j's pull entries (in-degree + 1 sums)
+  unsigned long long* push;  // [kMaxQ][B] forward level k's out-degree + 1 sums
+  int64_t* doff;             // [B + 1] path offsets
+  int64_t* path;
+  const int64_t* h_pairs;    // coherent host: [B] src vids, [B] dst vids
+  int32_t* h_sr;             // coherent host: [B] state, [B] res
+  int64_t* h_off;            // coherent host: [B + 1]
+  int64_t* h_path;           // coherent host
+};
+
+__device__ inline void dput(uint64_t* list, int64_t cap, unsigned long long* ctr, unsigned long long* cnt, bool pred,
+                            uint64_t v) {
+  const int64_t s = wave_append(ctr, pred);
+  if (pred) {
+    if (s < cap) list[s] = v;
+    else atomicOr(cnt + D_OVF, 1ull);
+  }
+}
+
+// block-wide reservation in K counters (kBlk threads, block-uniform call): thread asks n[k] slots
+// of counter k, gets its first slot o[k]; one returning atomic per counter and block
+template <int K>
+__device__ inline void blk_reserve_n(unsigned long long* const* ctr, const uint32_t* n, unsigned long long* o) {
+  __shared__ uint32_t s_w[K][kBlk / 64];
+  __shared__ unsigned long long s_base[K];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t v[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    v[k] = n[k];
+#pragma unroll
+    for (int of = 1; of < 64; of <<= 1) {
+      const uint32_t y = __shfl_up(v[k], of);
+      if (lane >= of) v[k] += y;
+    }
+    if (lane == 63) s_w[k][w] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    uint32_t pre = v[k] - n[k], tot = 0;
+#pragma unroll
+    for (int i = 0; i < kBlk / 64; i++) {
+      if (i < w) pre += s_w[k][i];
+      tot += s_w[k][i];
+    }
+    v[k] = pre;
+    if (threadIdx.x == 0) s_base[k] = tot ? atomicAdd(ctr[k], (unsigned long long)tot) : 0ull;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; k++) o[k] = s_base[k] + v[k];
+  __syncthreads();
+}
+
+// one add per block of a per-thread value (kBlk threads, block-uniform call)
+__device__ inline void blk_add(unsigned long long* ctr, unsigned long long v) {
+  __shared__ unsigned long long s_a[kBlk / 64];
+  v = wsum(v);
+  if ((threadIdx.x & 63) == 0) s_a[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+#pragma unroll
+    for (int i = 0; i < kBlk / 64; i++) t += s_a[i];
+    if (t) atomicAdd(ctr, t);
+  }
+  __syncthreads();
+}
+
+// items [c0, c0 + nc) of every lane get fill(item, val): short ranges by their lane, long ones
+// (a hub row's thousands of chunks) by the whole wave.  Wave-uniform call.
+template <typename Fill>
+__device__ inline void wave_fill_val(int64_t c0, int64_t nc, int64_t val, Fill fill) {
+  const int lane = threadIdx.x & 63;
+  if (nc <= 4) {
+    for (int64_t k = 0; k < nc; k++) fill(c0 + k, val);
+    nc = 0;
+  }
+  uint64_t m = __ballot(nc > 0);
+  while (m) {
+    const int j = __ffsll((long long)m) - 1;
+    m &= m - 1;
+    const int64_t a = __shfl(c0, j), z = a + __shfl(nc, j), v = __shfl(val, j);
+    for (int64_t c = a + lane; c < z; c += 64) fill(c, v);
+  }
+}
+
+// Publication by the last block of a kernel: every block takes a ticket after its work; the
+// last one copies the global counters and counter block q to the host slot (one wave: lane 0's
+// system-scope release covers the wave's stores) and then the sequence word the host spins on.
+__device__ inline void dv_publish_last(unsigned long long* cnt, int q, unsigned long long* hslot, uint64_t seq) {
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    s_last = atomicAdd(cnt + D_TICKET, 1ull) == (unsigned long long)(gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!s_last || threadIdx.x >= 64) return;
+  __threadfence();
+  const int i = threadIdx.x;
+  if (i < D_G + Q_W) {
+    const unsigned long long* src = i < D_G ? cnt + i : qblk(cnt, q) + (i - D_G);
+    hslot[i] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (i == 0) __hip_atomic_store(cnt + D_TICKET, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_wave_barrier();
+  if (i == 0) __hip_atomic_store(hslot + kPubW - 1, (unsigned long long)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// batch start: pairs from host memory, vid -> gidx, both frontiers seeded, the first side choice
+// (trivial pairs finish here); the sweep cost sums cleared
+__global__ __launch_bounds__(256) void k_dv_begin(SpDev d, SpState st, SpCsr gout, SpCsr gin, uint8_t* d0, uint8_t* d1,
+                                                  int64_t n, int32_t max_steps, const int64_t* ht_keys,
+                                                  const int32_t* ht_vals, uint64_t ht_mask, bool ht_has_min,
+                                                  int32_t ht_min_gidx) {
+  const int32_t B = st.B;
+  const int64_t gt = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, gn = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = gt; i < int64_t(2) * kMaxQ * B; i += gn) d.pull[i] = 0ull;  // pull and push adjacent
+  bool go = false;
+  int32_t a = -1, b = -1;
+  if (gt < B) {
+    const int p = int(gt);
+    const int64_t sv = d.h_pairs[p], tv = d.h_pairs[B + p];
+    a = ht_lookup(ht_keys, ht_vals, ht_mask, sv, ht_has_min, ht_min_gidx);
+    b = ht_lookup(ht_keys, ht_vals, ht_mask, tv, ht_has_min, ht_min_gidx);
+    d.gs[p] = a;
+    d.gs[B + p] = b;
+    st.res[p] = sv == tv ? 0 : -1;
+    st.lvl[p] = st.lvl[B + p] = 0;
+    st.met[p] = 0;
+    st.pside[p] = 0;
+    st.side[p] = 0;
+    st.deg[p] = st.deg[B + p] = 0;
+    go = sv != tv && a >= 0 && b >= 0 && max_steps >= 1;
+    if (go) {
+      claim_byte(d0, didx(st, uint32_t(p), uint32_t(a), n), 0);
+      claim_byte(d1, didx(st, uint32_t(p), uint32_t(b), n), 0);
+      const unsigned long long df = (unsigned long long)sp_deg(gout, uint32_t(a)) + 1;
+      const unsigned long long db = (unsigned long long)sp_deg(gin, uint32_t(b)) + 1;
+      const int s = df <= db ? 0 : 1;
+      st.side[p] = s;
+      st.deg[p] = s == 0 ? 0ull : df;  // the expanding side's sum restarts (the expansion adds)
+      st.deg[B + p] = s == 1 ? 0ull : db;
+    }
+    st.state[p] = go ? SP_ACTIVE : SP_DONE;
+  }
+  const uint32_t pp = uint32_t(gt);
+  unsigned long long* q0 = qblk(d.cnt, 0);
+  dput(d.live[0][0], d.cap_live, q0 + Q_LIVE0, d.cnt, go, mk_tup(0, pp, 0, uint32_t(a)));
+  dput(d.live[0][1], d.cap_live, q0 + Q_LIVE1, d.cnt, go, mk_tup(1, pp, 0, uint32_t(b)));
+  dput(d.arena, d.cap_arena, d.cnt + D_ARENA, d.cnt, go, mk_tup(0, pp, 0, uint32_t(a)));
+  dput(d.arena, d.cap_arena, d.cnt + D_ARENA, d.cnt, go, mk_tup(1, pp, 0, uint32_t(b)));
+  (void)wave_append(q0 + Q_ACTIVE, go);
+}
+
+// BFS iteration it, first launch: the live lists of iteration it - 1 -> X (tuples of the side
+// their pair expands, with their chunk ranges in the chunk table) + the tuples carried into
+// iteration it's lists.  kSelIt tuples per thread, one reservation per block and round.
+__global__ __launch_bounds__(kBlk) void k_dv_select(SpDev d, SpState st, SpCsr gout, SpCsr gin, int32_t it) {
+  unsigned long long* qp = qblk(d.cnt, it - 1);
+  unsigned long long* q = qblk(d.cnt, it);
+  const int64_t n0 = min(int64_t(qp[Q_LIVE0]), d.cap_live), n1 = min(int64_t(qp[Q_LIVE1]), d.cap_live);
+  const int64_t nl = n0 + n1;
+  const uint64_t* in0 = d.live[(it - 1) & 1][0];
+  const uint64_t* in1 = d.live[(it - 1) & 1][1];
+  uint64_t* out0 = d.live[it & 1][0];
+  uint64_t* out1 = d.live[it & 1][1];
+  constexpr int64_t per = int64_t(kBlk) * kSelIt;
+  const int64_t rounds = (nl + per - 1) / per;
+  unsigned long long esum = 0;
+  unsigned long long* ctr[4] = {q + Q_X, q + Q_LIVE0, q + Q_LIVE1, q + Q_NCH};
+  for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
+    const int64_t i0 = r * per + threadIdx.x;
+    uint64_t t[kSelIt];
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      const int64_t i = i0 + u * kBlk;
+      t[u] = i < n0 ? in0[i] : i < nl ? in1[i - n0] : ~0ull;
+    }
+    int32_t s[kSelIt], sd[kSelIt];
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) s[u] = t[u] != ~0ull ? st.state[t_pair(t[u])] : SP_DONE;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) sd[u] = s[u] == SP_ACTIVE ? st.side[t_pair(t[u])] : 0;
+    uint32_t xm = 0, cm0 = 0, cm1 = 0;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      if (s[u] != SP_ACTIVE) continue;
+      const uint32_t ts = t_side(t[u]);
+      if (uint32_t(sd[u]) == ts) xm |= 1u << u;
+      else if (ts) cm1 |= 1u << u;
+      else cm0 |= 1u << u;
+    }
+    int64_t dg[kSelIt];
+    uint32_t nch = 0;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      dg[u] = (xm >> u) & 1u ? sp_deg(t_side(t[u]) ? gin : gout, t_row(t[u])) : 0;
+      if (dg[u] == 0) xm &= ~(1u << u);  // nothing to scan
+      nch += uint32_t((dg[u] + kCh - 1) / kCh);
+      esum += (unsigned long long)dg[u];
+    }
+    const uint32_t nn[4] = {uint32_t(__popc(xm)), uint32_t(__popc(cm0)), uint32_t(__popc(cm1)), nch};
+    unsigned long long o[4];
+    blk_reserve_n<4>(ctr, nn, o);
+    bool ovf = false;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      const bool x = (xm >> u) & 1u;
+      const int64_t nc = x ? (dg[u] + kCh - 1) / kCh : 0;
+      const int64_t xa = int64_t(o[0]), ca = int64_t(o[3]);
+      if (x) {
+        if (xa < d.cap_x && ca + nc <= d.cap_ch) {
+          d.X[xa] = t[u];
+          d.Xcb[xa] = ca;
+        } else {
+          ovf = true;
+        }
+        o[0]++;
+        o[3] += uint64_t(nc);
+      }
+      const bool fill = x && xa < d.cap_x && ca + nc <= d.cap_ch;
+      wave_fill_val(ca, fill ? nc : 0, xa, [&](int64_t c, int64_t v) {
+        d.chx[c] = int32_t(v);
+        d.slot[c] = ~0ull;
+      });
+      if ((cm0 >> u) & 1u) {
+        if (int64_t(o[1]) < d.cap_live) out0[o[1]] = t[u];
+        else ovf = true;
+        o[1]++;
+      } else if ((cm1 >> u) & 1u) {
+        if (int64_t(o[2]) < d.cap_live) out1[o[2]] = t[u];
+        else ovf = true;
+        o[2]++;
+      }
+    }
+    if (ovf) atomicOr(d.cnt + D_OVF, 2ull);
+  }
+  blk_add(q + Q_XE, esum);
+}
+
+// Chunk groups.  A wave takes G virtual chunks, nwaves apart (the grid-stride order: at any time
+// neighbouring waves scan neighbouring chunks, often of one row), and its first G lanes load their
+// descriptors together (chunk table -> tuple -> row bounds: a chain of dependent loads paid once
+// per group, not once per chunk); the wave then scans the live ones one by one with the
+// descriptor read from its lane into scalar registers.  G (a power of two <= 64) is the share of
+// chunks per wave of the grid, so small steps still spread over every wave.
+struct ChunkRec {
+  uint64_t t;
+  int64_t x0, x1;
+  int32_t a0, a1;
+};
+__device__ inline int64_t rl64(int64_t v, int j) {
+  const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(v))), j));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(v) >> 32)), j));
+  return int64_t((uint64_t(hi) << 32) | lo);
+}
+template <typename Desc, typename Body>
+__device__ inline void chunk_groups(int64_t vtotal, Desc desc, Body body) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  int lg = 0;
+  while (lg < 6 && (nwaves << (lg + 1)) <= vtotal) lg++;
+  for (int64_t base = wave; base < vtotal; base += nwaves << lg) {
+    ChunkRec r{0, 0, 0, 0, 0};
+    bool live = false;
+    const int64_t mine = base + int64_t(lane) * nwaves;
+    if (lane < (1 << lg) && mine < vtotal) live = desc(mine, r);
+    uint64_t m = __ballot(live);
+    while (m) {
+      const int j = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      ChunkRec u;
+      u.t = uint64_t(rl64(int64_t(r.t), j));
+      u.x0 = rl64(r.x0, j);
+      u.x1 = rl64(r.x1, j);
+      u.a0 = __builtin_amdgcn_readlane(r.a0, j);
+      u.a1 = __builtin_amdgcn_readlane(r.a1, j);
+      body(u, base + int64_t(j) * nwaves);
+    }
+  }
+}
+// the X chunk c's row slice [x0, x1) (sub-chunk s of 2^lg_sub)
+__device__ inline bool x_chunk(const SpDev& d, const SpCsr& g0, const SpCsr& g1, int64_t c, int32_t lg_sub, int64_t s,
+                               ChunkRec& r) {
+  const int32_t a = d.chx[c];
+  r.t = d.X[a];
+  const SpCsr& g = t_side(r.t) ? g1 : g0;
+  const uint32_t row = t_row(r.t);
+  const int64_t re = g.row_ptr[row + 1];
+  r.x0 = g.row_ptr[row] + (c - d.Xcb[a]) * kCh + s * (int64_t(kCh) >> lg_sub);
+  r.x1 = min(r.x0 + (int64_t(kCh) >> lg_sub), re);
+  return r.x0 < r.x1;
+}
+
+// BFS iteration it, meet probe: one wave per chunk of an X tuple's row, stopping at the first
+// neighbour at the other side's depth (or once another chunk claimed the vertex); the winner
+// claims the vertex on the other side, marks the pair (met = -1) and records the claim in its
+// chunk's slot
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void k_dv_probe(SpDev d, SpState st, SpFilt f, SpCsr g0, SpCsr g1,
+                                                       uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo, int32_t it) {
+  if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
+  const int lane = threadIdx.x & 63;
+  unsigned long long* q = qblk(d.cnt, it);
+  const int64_t total = min(int64_t(q[Q_NCH]), d.cap_ch);
+  const uint32_t B = uint32_t(st.B);
+  unsigned long long examined = 0;
+  chunk_groups(
+      total,
+      [&](int64_t c, ChunkRec& r) {
+        if (!x_chunk(d, g0, g1, c, 0, 0, r)) return false;
+        const uint32_t o = t_side(r.t) ^ 1u, p = t_pair(r.t);
+        r.a0 = st.lvl[o * B + p];  // the other side's depth
+        r.a1 = d.gs[o * B + p];    // its root (depth 0)
+        return true;
+      },
+      [&](const ChunkRec& r, int64_t c) {
+        const uint32_t side = t_side(r.t), p = t_pair(r.t), row = t_row(r.t), o = side ^ 1u;
+        const int32_t* col = side ? g1.col : g0.col;
+        const int32_t need = r.a0;
+        uint8_t* const odp = (o ? d1 : d0) + uint64_t(p) * uint64_t(n);  // the pair's bytes (pair-major)
+        bool pf_on;
+        const uint2 prow = pf_load(f, o, need, p, pf_on);
+        for (int64_t x = r.x0; x < r.x1; x += 64 * kProbeU) {
+          const int32_t rem = int32_t(min(r.x1 - x, int64_t(64 * kProbeU)));
+          if (uint32_t(*reinterpret_cast<volatile const uint8_t*>(odp + row)) != 0xFFu) break;  // another chunk claimed r
+          const int32_t* cp = col + x;
+          uint32_t w[kProbeU];
+#pragma unroll
+          for (int u = 0; u < kProbeU; u++) {
+            const int32_t e = u * 64 + lane;
+            w[u] = e < rem ? uint32_t(int64_t(cp[e]) - lo) : 0xFFFFFFFFu;
+          }
+          bool hit = false;
+          if (need == 0) {
+#pragma unroll
+            for (int u = 0; u < kProbeU; u++) hit = hit || w[u] == uint32_t(r.a1);
+          } else {
+            uint32_t fm = 0;
+#pragma unroll
+            for (int u = 0; u < kProbeU; u++) {
+              const bool pv = pf_on ? pf_test(prow, w[u], f.k2 != 0) : true;
+              fm |= (w[u] != 0xFFFFFFFFu && pv && gf_test(f, o, need, p, w[u])) ? 1u << u : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kProbeU; u++) hit = (((fm >> u) & 1u) && uint32_t(odp[w[u]]) == uint32_t(need)) || hit;
+          }
+          examined += uint64_t(min(int64_t(64 * kProbeU), r.x1 - x)) * (lane == 0);
+          if (__ballot(hit)) {
+            if (lane == 0 && claim_byte(odp, row, uint32_t(need + 1))) {
+              filt_mark(f, o, uint32_t(need + 1), p, row);
+              st.met[p] = -1;
+              d.slot[c] = mk_tup(o, p, uint32_t(need + 1), row);
+            }
+            break;
+          }
+        }
+      });
+  blk_add(q + Q_PE, examined);
+}
+
+// stage a wave-uniform batch of claims (lanes with `claimed`) into the wave's LDS buffer, flushing
+// it to the arena and `list` when full (two counter atomics per flush)
+struct DvStage {
+  uint64_t* buf;
+  uint32_t n;  // wave-uniform
+};
+__device__ inline void dv_flush(DvStage& s, unsigned long long* cnt, unsigned long long* lctr, uint64_t* list,
+                                int64_t cap_list, uint64_t* arena, int64_t cap_arena) {
+  if (s.n == 0) return;
+  const int lane = threadIdx.x & 63;
+  __builtin_amdgcn_wave_barrier();
+  unsigned long long ba = 0, bl = 0;
+  if (lane == 0) {
+    ba = atomicAdd(cnt + D_ARENA, (unsigned long long)s.n);
+    bl = atomicAdd(lctr, (unsigned long long)s.n);
+  }
+  ba = __shfl(ba, 0);
+  bl = __shfl(bl, 0);
+  bool ovf = false;
+  for (uint32_t k = uint32_t(lane); k < s.n; k += 64) {
+    const uint64_t v = s.buf[k];
+    if (int64_t(ba + k) < cap_arena) arena[ba + k] = v;
+    else ovf = true;
+    if (int64_t(bl + k) < cap_list) list[bl + k] = v;
+    else ovf = true;
+  }
+  if (ovf) atomicOr(cnt + D_OVF, 1ull);
+  __builtin_amdgcn_wave_barrier();
+  s.n = 0;
+}
+__device__ inline void dv_stage(DvStage& s, bool claimed, uint64_t v, unsigned long long* cnt,
+                                unsigned long long* lctr, uint64_t* list, int64_t cap_list, uint64_t* arena,
+                                int64_t cap_arena) {
+  const uint64_t m = __ballot(claimed);
+  if (m == 0) return;
+  const uint32_t k = uint32_t(__popcll(m));
+  if (s.n + k > uint32_t(kDvStage)) dv_flush(s, cnt, lctr, list, cap_list, arena, cap_arena);
+  const int lane = threadIdx.x & 63;
+  if (claimed) s.buf[s.n + uint32_t(__popcll(m & ((1ull << lane) - 1ull)))] = v;
+  s.n += k;
+}
+// the block's final stages (one per wave) appended with one pair of counter atomics for the block
+// (the grid's waves end together: one atomic each queued at the kernel's tail).  Block-uniform.
+__device__ inline void dv_flush_block(DvStage& s, unsigned long long* cnt, unsigned long long* lctr, uint64_t* list,
+                                      int64_t cap_list, uint64_t* arena, int64_t cap_arena) {
+  __shared__ uint32_t s_ns[4];
+  __shared__ unsigned long long s_b[2];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) s_ns[wid] = s.n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long tot = s_ns[0] + s_ns[1] + s_ns[2] + s_ns[3];
+    s_b[0] = tot ? atomicAdd(cnt + D_ARENA, tot) : 0ull;
+    s_b[1] = tot ? atomicAdd(lctr, tot) : 0ull;
+  }
+  __syncthreads();
+  uint32_t pre = 0;
+  for (int k = 0; k < wid; k++) pre += s_ns[k];
+  const unsigned long long ba = s_b[0] + pre, bl = s_b[1] + pre;
+  bool ovf = false;
+  for (uint32_t k = uint32_t(lane); k < s.n; k += 64) {
+    const uint64_t v = s.buf[k];
+    if (int64_t(ba + k) < cap_arena) arena[ba + k] = v;
+    else ovf = true;
+    if (int64_t(bl + k) < cap_list) list[bl + k] = v;
+    else ovf = true;
+  }
+  if (ovf) atomicOr(cnt + D_OVF, 1ull);
+  s.n = 0;
+  __syncthreads();
+}
+
+// BFS iteration it, expansion: 2^lg_sub waves per chunk of the X tuples of pairs the probe did not
+// finish (a BFS level's claims are CAS and atomic round trips: more waves in flight, not longer
+// streams, set its pace); a claim (CAS on the pair's distance byte) sets the filters, joins the
+// side's next list and the arena (staged per wave), adds (degree + 1) to the pair's frontier sum
+// (one atomic per chunk: a chunk is one pair's) and is a meet when the other side has seen the
+// vertex.  Then the probe's slots become meet tuples and arena entries.
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpFilt f, SpCsr g0, SpCsr g1,
+                                                        uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo, int32_t it,
+                                                        int32_t lg_sub) {
+  __shared__ uint64_t s_stage[4][2][kDvStage];
+  if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
+  unsigned long long* q = qblk(d.cnt, it);
+  const int64_t total = min(int64_t(q[Q_NCH]), d.cap_ch);
+  const uint32_t B = uint32_t(st.B);
+  uint64_t* const out0 = d.live[it & 1][0];
+  uint64_t* const out1 = d.live[it & 1][1];
+  DvStage sg0{s_stage[wid][0], 0u}, sg1{s_stage[wid][1], 0u};
+  unsigned long long claims = 0, entries = 0;
+  chunk_groups(
+      total << lg_sub,
+      [&](int64_t vc, ChunkRec& r) {
+        if (!x_chunk(d, g0, g1, vc >> lg_sub, lg_sub, vc & ((int64_t(1) << lg_sub) - 1), r)) return false;
+        return st.met[t_pair(r.t)] != -1;  // the probe finished the pair
+      },
+      [&](const ChunkRec& r, int64_t) {
+        const uint32_t side = t_side(r.t), p = t_pair(r.t), l = t_lvl(r.t);
+        const SpCsr& g = side ? g1 : g0;
+        uint8_t* const sdp = (side ? d1 : d0) + uint64_t(p) * uint64_t(n);  // the pair's bytes (pair-major)
+        const uint8_t* const odp = (side ? d0 : d1) + uint64_t(p) * uint64_t(n);
+        entries += uint64_t(r.x1 - r.x0) * (lane == 0);
+        unsigned long long dsum = 0;
+        for (int64_t x = r.x0; x < r.x1; x += 64 * kProbeU) {
+          const int32_t rem = int32_t(min(r.x1 - x, int64_t(64 * kProbeU)));
+          const int32_t* cp = g.col + x;
+          uint32_t w[kProbeU];
+#pragma unroll
+          for (int u = 0; u < kProbeU; u++) {
+            const int32_t e = u * 64 + lane;
+            w[u] = e < rem ? uint32_t(int64_t(cp[e]) - lo) : 0xFFFFFFFFu;
+          }
+          uint32_t bt[kProbeU];
+#pragma unroll
+          for (int u = 0; u < kProbeU; u++) bt[u] = w[u] != 0xFFFFFFFFu ? uint32_t(sdp[w[u]]) : 0x1FFu;
+#pragma unroll
+          for (int u = 0; u < kProbeU; u++) {
+            const bool cl = bt[u] == 0xFFu && claim_byte(sdp, w[u], l + 1);
+            bool meet = false;
+            uint32_t dt = 0;
+            if (cl) {
+              filt_mark(f, side, l + 1, p, w[u]);
+              dsum += (unsigned long long)sp_deg(g, w[u]) + 1;
+              const uint32_t ob = odp[w[u]];
+              if (ob != 0xFFu) {
+                meet = true;
+                dt = side ? l + 1 : ob;
+                st.met[p] = 1;
+              }
+            }
+            const uint64_t cm = __ballot(cl);
+            if (cm == 0) continue;
+            claims += uint64_t(__popcll(cm)) * (lane == 0);
+            if (side)
+              dv_stage(sg1, cl, mk_tup(1, p, l + 1, w[u]), d.cnt, q + Q_LIVE1, out1, d.cap_live, d.arena, d.cap_arena);
+            else
+              dv_stage(sg0, cl, mk_tup(0, p, l + 1, w[u]), d.cnt, q + Q_LIVE0, out0, d.cap_live, d.arena, d.cap_arena);
+            dput(d.meet, d.cap_meet, d.cnt + D_MEET, d.cnt, meet, mk_tup(1, p, dt, w[u]));
+          }
+        }
+        dsum = wsum(dsum);
+        if (lane == 0 && dsum) {
+          atomicAdd(st.deg + side * B + p, dsum);
+          // a forward level's (degree + 1) sum is also the sweep's push entries for that level
+          if (side == 0 && l + 1 < uint32_t(kMaxQ)) atomicAdd(d.push + int64_t(l + 1) * B + p, dsum);
+        }
+      });
+  // the probe's claims: meet tuples (the vertex at the backward depth) + arena entries
+  for (int64_t c0 = wave * 64; c0 < total; c0 += nwaves * 64) {
+    const int64_t c = c0 + lane;
+    const uint64_t v = c < total ? d.slot[c] : ~0ull;
+    const bool hit = v != ~0ull;
+    uint64_t mt = 0;
+    if (hit) {
+      const uint32_t o = t_side(v), lv = t_lvl(v);
+      mt = mk_tup(1, t_pair(v), o ? lv : t_lvl(d.X[d.chx[c]]), t_row(v));
+    }
+    if (__ballot(hit) == 0) continue;
+    dput(d.arena, d.cap_arena, d.cnt + D_ARENA, d.cnt, hit, v);
+    dput(d.meet, d.cap_meet, d.cnt + D_MEET, d.cnt, hit, mt);
+  }
+  dv_flush_block(sg0, d.cnt, q + Q_LIVE0, out0, d.cap_live, d.arena, d.cap_arena);
+  dv_flush_block(sg1, d.cnt, q + Q_LIVE1, out1, d.cap_live, d.arena, d.cap_arena);
+  blk_add(q + Q_CLAIMS, claims);
+  blk_add(q + Q_EE, entries);
+}
+
+// BFS iteration it, last launch: per pair, the end of the iteration (depth, meet, done) and the
+// next side choice; the last block publishes the iteration's counters to host slot `hslot`
+__global__ __launch_bounds__(256) void k_dv_step(SpDev d, SpState st, int32_t max_steps, int32_t it,
+                                                 unsigned long long* hslot, uint64_t seq) {
+  const int32_t B = st.B;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  bool active = false;
+  if (p < B && st.state[p] == SP_ACTIVE) {
+    const int32_t m = st.met[p];
+    if (m == -1) {  // the probe met: the other side advanced by one
+      const int o = st.side[p] ^ 1;
+      st.lvl[o * B + p] += 1;
+      st.res[p] = st.lvl[p] + st.lvl[B + p];
+      st.state[p] = SP_MET;
+      st.met[p] = 2 + it;
+      st.pside[p] = o;
+    } else {
+      const int s = st.side[p];
+      st.pside[p] = s;
+      st.lvl[s * B + p] += 1;
+      const int32_t L = st.lvl[p] + st.lvl[B + p];
+      if (m == 1) {
+        st.res[p] = L;
+        st.state[p] = SP_MET;
+        st.met[p] = 2 + it;
+      } else if (st.deg[s * B + p] == 0 || L >= max_steps) {
+        st.state[p] = SP_DONE;
+      }
+    }
+    if (st.state[p] == SP_MET) {
+      atomicMax(d.cnt + D_MAXL, (unsigned long long)st.res[p]);
+      atomicMax(d.cnt + D_MAXF, (unsigned long long)st.lvl[p]);
+    } else if (st.state[p] == SP_ACTIVE) {
+      const int s = st.deg[p] <= st.deg[B + p] ? 0 : 1;
+      st.side[p] = s;
+      st.deg[s * B + p] = 0;
+      active = true;
+    }
+  }
+  (void)wave_append(qblk(d.cnt, it) + Q_ACTIVE, active);
+  dv_publish_last(d.cnt, it, hslot, seq);
+}
+
+// path offsets of the batch by one block: pair p's path holds L + 1 vids when it finished at
+// length L (an ACTIVE pair has none); doff[B] the total
+__device__ inline void dv_path_offsets(const SpState& st, int64_t nb, int64_t* doff) {
+  __shared__ int64_t s_w[kBlk / 64];
+  __shared__ int64_t s_carry;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (int64_t p0 = 0; p0 < nb; p0 += kBlk) {
+    const int64_t p = p0 + threadIdx.x;
+    int64_t len = 0;
+    if (p < nb && st.state[p] != SP_ACTIVE && st.res[p] >= 0) len = st.res[p] + 1;
+    int64_t v = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(v, o);
+      if (lane >= o) v += y;
+    }
+    if (lane == 63) s_w[wv] = v;
+    __syncthreads();
+    int64_t pre = s_carry, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kBlk / 64; w++) {
+      if (w < wv) pre += s_w[w];
+      tot += s_w[w];
+    }
+    if (p < nb) doff[p] = pre + v - len;
+    __syncthreads();
+    if (threadIdx.x == 0) s_carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) doff[nb] = s_carry;
+}
+
+// walk step i's front (block-uniform): the pick of step i - 1 (path vid, next vertex through the
+// vertex hash), then the chunks of the current vertex's out-row for step i
+__device__ inline void dv_walk_front(SpDev& d, const SpState& st, const SpCsr& gout, int32_t i, int64_t lo,
+                                     const int64_t* ht_keys, const int32_t* ht_vals, uint64_t ht_mask,
+                                     bool ht_has_min, int32_t ht_min_gidx) {
+  const int32_t B = st.B;
+  unsigned long long* q = qblk(d.cnt, kWkQ + i);
+  unsigned long long* ctr[1] = {q + Q_NCH};
+  const int64_t rounds = (int64_t(B) + kBlk - 1) / kBlk;
+  for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
+    const int64_t p = r * kBlk + threadIdx.x;
+    int64_t dg = 0;
+    if (p < B && st.state[p] == SP_MET) {
+      const int32_t L = st.res[p];
+      if (i == 0) {
+        d.cur[p] = d.gs[p];
+      } else if (L - 1 > i - 1 && d.cur[p] >= 0) {
+        const long long b = d.best[p];
+        if (b == LLONG_MAX) {  // in-edge keys without the mirrored out-edge: the definition does not hold
+          atomicAdd(d.cnt + D_WALKERR, 1ull);
+          d.cur[p] = -1;
+        } else {
+          d.path[d.doff[p] + i] = int64_t(b);
+          d.cur[p] = ht_lookup(ht_keys, ht_vals, ht_mask, int64_t(b), ht_has_min, ht_min_gidx) - int32_t(lo);
+        }
+      }
+      if (L - 1 > i && d.cur[p] >= 0) dg = sp_deg(gout, uint32_t(d.cur[p]));
+      d.best[p] = LLONG_MAX;
+    }
+    const uint32_t nc = uint32_t((dg + kCh - 1) / kCh);
+    unsigned long long o[1];
+    blk_reserve_n<1>(ctr, &nc, o);
+    const bool ok = int64_t(o[0]) + int64_t(nc) <= d.cap_wch;
+    if (nc && !ok) atomicOr(d.cnt + D_OVF, 4ull);
+    if (p < B && nc) d.wcb[p] = int64_t(o[0]);
+    wave_fill_val(int64_t(o[0]), ok ? int64_t(nc) : 0, p, [&](int64_t c, int64_t v) { d.wchx[c] = int32_t(v); });
+  }
+}
+
+// after the BFS: path offsets (block 0), the walk's first front and sweep step 1's pull entries
+// per pair (in-rows of the meet vertices short of src).  The push entries of every forward level
+// were summed by the expansions that claimed it.
+__global__ __launch_bounds__(kBlk) void k_dv_post(SpDev d, SpState st, SpCsr gout, SpCsr gin, int64_t lo,
+                                                  const int64_t* ht_keys, const int32_t* ht_vals, uint64_t ht_mask,
+                                                  bool ht_has_min, int32_t ht_min_gidx) {
+  const int32_t B = st.B;
+  if (blockIdx.x == 0) dv_path_offsets(st, B, d.doff);
+  dv_walk_front(d, st, gout, 0, lo, ht_keys, ht_vals, ht_mask, ht_has_min, ht_min_gidx);
+  const int64_t gn = int64_t(gridDim.x) * blockDim.x;
+  const int64_t nm = min(int64_t(d.cnt[D_MEET]), d.cap_meet);
+  const int64_t rm = (nm + gn - 1) / gn;
+  for (int64_t r = 0; r < rm; r++) {
+    const int64_t i = r * gn + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    bool go = false;
+    uint32_t p = 0;
+    unsigned long long dg = 0;
+    if (i < nm) {
+      const uint64_t t = d.meet[i];
+      p = t_pair(t);
+      go = st.state[p] == SP_MET && int32_t(t_lvl(t)) < st.res[p] - 1;
+      if (go) dg = (unsigned long long)sp_deg(gin, t_row(t)) + 1;
+    }
+    wave_add_keyed(d.pull + B, p, dg, go);  // step 1
+  }
+}
+
+// sweep step j: pull (in-rows of the level above, from the current sweep list) or push (out-rows
+// of the forward level k = f - j, from the arena), per pair the side with fewer entries (option
+// sp_push_bias in 1/16: push when its entries are below pull's x bias / 16)
+__device__ inline bool dv_push_pair(const SpDev& d, const SpState& st, uint32_t p, int32_t j,
+                                    unsigned long long bias16) {
+  const int32_t B = st.B;
+  const unsigned long long pl = d.pull[int64_t(j) * B + p];
+  const int32_t k = st.lvl[p] - j;
+  if (pl == 0 || k < 1 || k >= kMaxQ) return false;
+  return d.push[int64_t(k) * B + p] * 16ull < pl * bias16;
+}
+__global__ __launch_bounds__(kBlk) void k_dv_sweep_select(SpDev d, SpState st, SpCsr gout, SpCsr gin, int32_t j,
+                                                          unsigned long long bias16) {
+  unsigned long long* q = qblk(d.cnt, kSwQ + j);
+  const uint64_t* cur = j == 1 ? d.meet : d.sw[(j - 1) & 1];
+  const int64_t ncur = j == 1 ? min(int64_t(d.cnt[D_MEET]), d.cap_meet)
+                              : min(int64_t(qblk(d.cnt, kSwQ + j - 1)[Q_CLAIMS]), d.cap_sw);
+  // the arena's forward tuples are scanned only when some pair pushes at this step (each block
+  // asks every pair: a few loads per thread instead of 1 M+ arena tuples per step)
+  int anyp = 0;
+  for (int p = threadIdx.x; p < st.B; p += blockDim.x) anyp |= dv_push_pair(d, st, uint32_t(p), j, bias16) ? 1 : 0;
+  const int64_t na = __syncthreads_or(anyp) ? min(int64_t(d.cnt[D_ARENA]), d.cap_arena) : 0;
+  const int64_t nt = ncur + na;
+  constexpr int64_t per = int64_t(kBlk) * kSelIt;
+  const int64_t rounds = (nt + per - 1) / per;
+  unsigned long long esum = 0;
+  unsigned long long* ctr[2] = {q + Q_X, q + Q_NCH};
+  for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
+    const int64_t i0 = r * per + threadIdx.x;
+    uint64_t t[kSelIt];
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      const int64_t i = i0 + u * kBlk;
+      t[u] = i < ncur ? cur[i] : i < nt ? d.arena[i - ncur] : ~0ull;
+    }
+    int32_t s[kSelIt];
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) s[u] = t[u] != ~0ull ? st.state[t_pair(t[u])] : SP_DONE;
+    uint32_t xm = 0;
+    int64_t dg[kSelIt];
+    uint32_t nch = 0;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      dg[u] = 0;
+      if (s[u] != SP_MET) continue;
+      const uint32_t p = t_pair(t[u]);
+      const bool pulled = i0 + u * kBlk < ncur;
+      bool go;
+      if (pulled) {
+        go = int32_t(t_lvl(t[u])) < st.res[p] - 1 && !dv_push_pair(d, st, p, j, bias16);
+      } else {
+        const int32_t k = st.lvl[p] - j;
+        go = t_side(t[u]) == 0 && k >= 1 && int32_t(t_lvl(t[u])) == k && dv_push_pair(d, st, p, j, bias16);
+      }
+      if (!go) continue;
+      dg[u] = sp_deg(pulled ? gin : gout, t_row(t[u]));
+      if (dg[u] == 0) continue;
+      xm |= 1u << u;
+      nch += uint32_t((dg[u] + kCh - 1) / kCh);
+      esum += (unsigned long long)dg[u];
+    }
+    const uint32_t nn[2] = {uint32_t(__popc(xm)), nch};
+    unsigned long long o[2];
+    blk_reserve_n<2>(ctr, nn, o);
+    bool ovf = false;
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) {
+      const bool x = (xm >> u) & 1u;
+      const int64_t nc = x ? (dg[u] + kCh - 1) / kCh : 0;
+      const int64_t xa = int64_t(o[0]), ca = int64_t(o[1]);
+      const bool fit = xa < d.cap_x && ca + nc <= d.cap_ch;
+      if (x) {
+        if (fit) {
+          d.X[xa] = t[u];
+          d.Xcb[xa] = ca;
+        } else {
+          ovf = true;
+        }
+        o[0]++;
+        o[1] += uint64_t(nc);
+      }
+      wave_fill_val(ca, x && fit ? nc : 0, xa, [&](int64_t c, int64_t v) { d.chx[c] = int32_t(v); });
+    }
+    if (ovf) atomicOr(d.cnt + D_OVF, 2ull);
+  }
+  blk_add(q + Q_XE, esum);
+}
+
+// sweep step j: one wave per chunk.  Pull (side 1, in-row of w at dt = l): an in-neighbour u with
+// ds(u) = L - l - 1 gets dt = l + 1.  Push (side 0, out-row of u at ds = l): u gets dt = L - l
+// once an out-neighbour has dt = L - l - 1 (the scan stops there).  Claims go to the arena and
+// the next sweep list, and the pull entries of the claimed vertices that the next step scans are
+// added to the pair's step j + 1 sum.
+template <int OCC>
+__global__ __launch_bounds__(256, OCC) void k_dv_sweep(SpDev d, SpState st, SpFilt f, SpCsr gout, SpCsr gin,
+                                                       uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo, int32_t j) {
+  __shared__ uint64_t s_stage[4][kDvStage];
+  if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long* q = qblk(d.cnt, kSwQ + j);
+  const int64_t total = min(int64_t(q[Q_NCH]), d.cap_ch);
+  const uint32_t B = uint32_t(st.B);
+  uint64_t* out = d.sw[j & 1];
+  unsigned long long* pull_next = j + 1 < kMaxQ ? d.pull + int64_t(j + 1) * B : nullptr;
+  DvStage sg{s_stage[wid], 0u};
+  unsigned long long entries = 0;
+  chunk_groups(
+      total,
+      [&](int64_t c, ChunkRec& r) {
+        if (!x_chunk(d, gout, gin, c, 0, 0, r)) return false;
+        const uint32_t os = t_side(r.t) ^ 1u, p = t_pair(r.t);
+        r.a0 = st.res[p];
+        r.a1 = d.gs[os * B + p];
+        return true;
+      },
+      [&](const ChunkRec& r, int64_t) {
+        const uint32_t side = t_side(r.t), p = t_pair(r.t), l = t_lvl(r.t), row = t_row(r.t), os = side ^ 1u;
+        const int32_t* col = side ? gin.col : gout.col;
+        const int32_t L = r.a0;
+        const int32_t need = L - int32_t(l) - 1;  // the other side's depth a neighbour needs
+        const uint8_t* const odp = (side ? d0 : d1) + uint64_t(p) * uint64_t(n);  // the pair's bytes (pair-major)
+        uint8_t* const d1p = d1 + uint64_t(p) * uint64_t(n);
+        bool pf_on;
+        const uint2 prow = pf_load(f, os, need, p, pf_on);
+        entries += uint64_t(r.x1 - r.x0) * (lane == 0);
+        unsigned long long pc = 0;
+        for (int64_t x = r.x0; x < r.x1; x += 64 * kProbeU) {
+          const int32_t rem = int32_t(min(r.x1 - x, int64_t(64 * kProbeU)));
+          if (side == 0 && *reinterpret_cast<volatile const uint8_t*>(d1p + row) != 0xFFu) break;  // u claimed
+          const int32_t* cp = col + x;
+          uint32_t w[kProbeU];
+#pragma unroll
+          for (int u = 0; u < kProbeU; u++) {
+            const int32_t e = u * 64 + lane;
+            w[u] = e < rem ? uint32_t(int64_t(cp[e]) - lo) : 0xFFFFFFFFu;
+          }
+          uint32_t hm = 0;  // entries whose neighbour sits at depth need on the other side
+          if (need == 0) {
+#pragma unroll
+            for (int u = 0; u < kProbeU; u++) hm |= w[u] == uint32_t(r.a1) ? 1u << u : 0u;
+          } else {
+            uint32_t fm = 0;
+#pragma unroll
+            for (int u = 0; u < kProbeU; u++) {
+              const bool pv = pf_on ? pf_test(prow, w[u], f.k2 != 0) : true;
+              fm |= (w[u] != 0xFFFFFFFFu && pv && gf_test(f, os, need, p, w[u])) ? 1u << u : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < kProbeU; u++)
+              hm |= ((fm >> u) & 1u) && uint32_t(odp[w[u]]) == uint32_t(need) ? 1u << u : 0u;
+          }
+          if (__ballot(hm != 0) == 0) continue;
+          if (side == 1) {
+#pragma unroll
+            for (int u = 0; u < kProbeU; u++) {
+              const bool cl = ((hm >> u) & 1u) && claim_byte(d1p, w[u], l + 1);
+              if (cl) {
+                filt_mark(f, 1, l + 1, p, w[u]);
+                if (int32_t(l + 1) < L - 1) pc += (unsigned long long)sp_deg(gin, w[u]) + 1;
+              }
+              dv_stage(sg, cl, mk_tup(1, p, l + 1, w[u]), d.cnt, q + Q_CLAIMS, out, d.cap_sw, d.arena, d.cap_arena);
+            }
+          } else {
+            bool cl = false;
+            if (lane == 0) {
+              cl = claim_byte(d1p, row, uint32_t(need + 1));
+              if (cl) {
+                filt_mark(f, 1, uint32_t(need + 1), p, row);
+                if (need + 1 < L - 1) pc += (unsigned long long)sp_deg(gin, row) + 1;
+              }
+            }
+            dv_stage(sg, cl, mk_tup(1, p, uint32_t(need + 1), row), d.cnt, q + Q_CLAIMS, out, d.cap_sw, d.arena,
+                     d.cap_arena);
+            break;
+          }
+        }
+        pc = wsum(pc);
+        if (lane == 0 && pc && pull_next) atomicAdd(pull_next + p, pc);
+      });
+  dv_flush_block(sg, d.cnt, q + Q_CLAIMS, out, d.cap_sw, d.arena, d.cap_arena);
+  blk_add(q + Q_EE, entries);
+}
+
+// walk step i: one wave per chunk of a walking pair's current out-row; the smallest vid w with
+// dist_B(w) = L - i - 1 (by the filters, then the byte) goes to best[p] with one atomicMin per
+// chunk.  The last step is dst itself and never scanned.
+__global__ __launch_bounds__(256) void k_dv_walk_scan(SpDev d, SpState st, SpFilt f, SpCsr gout, const uint8_t* d1,
+                                                      const int64_t* vid_of, int64_t n, int64_t lo, int32_t i) {
+  if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
+  const int lane = threadIdx.x & 63;
+  unsigned long long* q = qblk(d.cnt, kWkQ + i);
+  const int64_t total = min(int64_t(q[Q_NCH]), d.cap_wch);
+  chunk_groups(
+      total,
+      [&](int64_t c, ChunkRec& r) {
+        const uint32_t p = uint32_t(d.wchx[c]);
+        const uint32_t v = uint32_t(d.cur[p]);
+        const int64_t re = gout.row_ptr[v + 1];
+        r.t = p;
+        r.x0 = gout.row_ptr[v] + (c - d.wcb[p]) * kCh;
+        r.x1 = min(r.x0 + int64_t(kCh), re);
+        r.a0 = st.res[p] - i - 1;
+        return r.x0 < r.x1;
+      },
+      [&](const ChunkRec& r, int64_t) {
+        const uint32_t p = uint32_t(r.t);
+        const int32_t need = r.a0;
+        bool pf_on;
+        const uint2 prow = pf_load(f, 1, need, p, pf_on);
+        const uint8_t* const d1p = d1 + uint64_t(p) * uint64_t(n);  // the pair's bytes (pair-major)
+        long long bm = LLONG_MAX;
+        for (int64_t x = r.x0; x < r.x1; x += 64 * kProbeU) {
+          const int32_t rem = int32_t(min(r.x1 - x, int64_t(64 * kProbeU)));
+          const int32_t* cp = gout.col + x;
+          uint32_t w[kProbeU];
+#pragma unroll
+          for (int u = 0; u < kProbeU; u++) {
+            const int32_t e = u * 64 + lane;
+            w[u] = e < rem ? uint32_t(int64_t(cp[e]) - lo) : 0xFFFFFFFFu;
+          }
+          uint32_t fm = 0;
+#pragma unroll
+          for (int u = 0; u < kProbeU; u++) {
+            const bool pv = pf_on ? pf_test(prow, w[u], f.k2 != 0) : true;
+            fm |= (w[u] != 0xFFFFFFFFu && pv && gf_test(f, 1, need, p, w[u])) ? 1u << u : 0u;
+          }
+#pragma unroll
+          for (int u = 0; u < kProbeU; u++)
+            if (((fm >> u) & 1u) && uint32_t(d1p[w[u]]) == uint32_t(need)) {
+              const long long vv = vid_of[lo + w[u]];
+              bm = vv < bm ? vv : bm;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const long long y = __shfl_xor(bm, o);
+          bm = y < bm ? y : bm;
+        }
+        if (lane == 0 && bm != LLONG_MAX) atomicMin(d.best + p, bm);
+      });
+}
+
+__global__ __launch_bounds__(kBlk) void k_dv_walk_front(SpDev d, SpState st, SpCsr gout, int32_t i, int64_t lo,
+                                                        const int64_t* ht_keys, const int32_t* ht_vals,
+                                                        uint64_t ht_mask, bool ht_has_min, int32_t ht_min_gidx) {
+  dv_walk_front(d, st, gout, i, lo, ht_keys, ht_vals, ht_mask, ht_has_min, ht_min_gidx);
+}
+
+// the batch's results: the last walk step's pick (step ilast, pairs of the longest length), then
+// state, length, path offset and path of every pair into coherent host memory (the ends src and
+// dst are the host's)
+__global__ __launch_bounds__(256) void k_dv_out(SpDev d, SpState st, int32_t ilast) {
+  const int32_t B = st.B;
+  const int64_t gt = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, gn = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t p = gt; p < B; p += gn) {
+    const int32_t s = st.state[p], L = st.res[p];
+    const int64_t o = d.doff[p];
+    if (s == SP_MET && ilast >= 0 && L - 1 > ilast && d.cur[p] >= 0) {
+      const long long b = d.best[p];
+      if (b == LLONG_MAX) atomicAdd(d.cnt + D_WALKERR, 1ull);
+      else d.path[o + ilast + 1] = int64_t(b);
+    }
+    d.h_sr[p] = s;
+    d.h_sr[B + p] = L;
+    d.h_off[p] = o;
+    if (p == B - 1) d.h_off[B] = d.doff[B];
+    if (s != SP_ACTIVE)
+      for (int32_t k = 1; k < L; k++) d.h_path[o + k] = d.path[o + k];
+  }
+}
+
+// every claimed distance byte of the batch and its filter words reset from the arena (after the
+// finish publication: the host reads the results while this runs; D_CLEAR holds the arena length)
+__global__ __launch_bounds__(256) void k_dv_clear(SpDev d, SpState st, SpFilt f, uint8_t* d0, uint8_t* d1, int64_t n) {
+  const uint32_t B = uint32_t(st.B);
+  const int64_t gt = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, gn = int64_t(gridDim.x) * blockDim.x;
+  const int64_t na = min(int64_t(d.cnt[D_CLEAR]), d.cap_arena);
+  for (int64_t i = gt; i < na; i += gn) {
+    const uint64_t t = d.arena[i];
+    const uint32_t side = t_side(t), p = t_pair(t), l = t_lvl(t), v = t_row(t);
+    (side ? d1 : d0)[didx(st, p, v, n)] = 0xFF;
+    if (l >= 1 && l < uint32_t(kLv)) {
+      const uint32_t sl = side * kLv + l;
+      if (f.pf) {
+        uint32_t* row = f.pf + (size_t(sl) * B + p) * 128;
+        row[pf_bit(v) >> 5] = 0u;
+        if (f.k2) row[pf_bit2(v) >> 5] = 0u;
+      }
+      if (f.gf) f.gf[gf_hash(sl, p, v) >> f.gshift] = 0u;
+    }
+  }
+}
+
+// every counter of the batch into coherent host memory, then cleared for the next batch; one
+// wave, lane 0's system-scope release publishes the sequence word after the copies
+__global__ void k_dv_finish(unsigned long long* cnt, unsigned long long* h, unsigned long long* hseq, uint64_t seq) {
+  for (int i = threadIdx.x; i < kDevCnt; i += 64) {
+    h[i] = cnt[i];
+    cnt[i] = i == D_CLEAR ? cnt[D_ARENA] : 0ull;
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (threadIdx.x == 0) __hip_atomic_store(hseq, (unsigned long long)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
@@ -1454,10 +2491,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   B = std::max<int64_t>(1, std::min<int64_t>(B, std::max<int64_t>(int64_t(npairs), 1)));
   B = std::min<int64_t>(B, 0x7FFFFF);
   const size_t dist_bytes = ((size_t(B) * size_t(n) + 3) & ~size_t(3)) + 64;
-  // option sp_hash: sparse (pair, vertex) -> depth maps sized to the claims instead of the dense
-  // 2 * B * n byte arrays
-  const bool hash = c.opt("sp_hash", 0) != 0;
-  if (!hash) {
+  {
     PoolScope none(nullptr);  // the distance arrays live outside the query pool
     if (c.sp_dist_bytes < dist_bytes) {
       for (auto& d : c.sp_dist) d.release();
@@ -1466,8 +2500,10 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       c.sp_dist_bytes = dist_bytes;
       c.sp_dirty = true;
     }
-    if (c.sp_dirty)
+    if (c.sp_dirty) {
       for (auto& d : c.sp_dist) NBG_HIP(hipMemsetAsync(d.p, 0xFF, c.sp_dist_bytes, c.stream));
+      c.sp.dv_clean = false;  // a failed call may have left filter words and counters set too
+    }
     c.sp_dirty = false;
   }
   Ctx::SpWork& W = c.sp;
@@ -1482,36 +2518,12 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   }
   PoolScope pool_scope(query_pool(c));
   c.timing = Timing{};
+  c.tev_used = 0;
+  c.hop_timing = c.opt("hop_timing", 1) != 0;  // event pairs around the scan launches (0: none)
   hipEventRecord(c.ev[0], c.stream);
 
-  uint8_t* d0 = hash ? nullptr : c.sp_dist[0].as<uint8_t>();
-  uint8_t* d1 = hash ? nullptr : c.sp_dist[1].as<uint8_t>();
-  // the maps: at most half full (linear probing); grown (rehashed) before a launch whose claims
-  // could pass that, from a bound on them -- the claims so far plus the launch's entries
-  // (expansion), chunks (meet probe) or the claims so far again (a sweep claims only vertices the
-  // forward search holds)
-  auto hash_fit = [&](SpState& st, int64_t claims) {
-    if (!hash) return;
-    int64_t cap = std::max<int64_t>(W.hcap, int64_t(1) << std::min<int64_t>(30, std::max<int64_t>(10, c.opt("sp_hash_log2", 22))));
-    while (cap < 2 * claims + 64) cap <<= 1;
-    if (cap != W.hcap || !W.htab[0].p) {
-      PoolScope none(nullptr);
-      for (int sd = 0; sd < 2; sd++) {
-        DevBuf nt;
-        nt.alloc(size_t(cap) * 8);
-        NBG_HIP(hipMemsetAsync(nt.p, 0xFF, size_t(cap) * 8, c.stream));
-        if (W.htab[sd].p && W.hcap > 0)
-          k_hash_rehash<<<grid_n(W.hcap), 256, 0, c.stream>>>(W.htab[sd].as<uint64_t>(), W.hcap, nt.as<uint64_t>(),
-                                                               uint64_t(cap - 1));
-        NBG_HIP(hipGetLastError());
-        W.htab[sd] = std::move(nt);
-      }
-      W.hcap = cap;
-    }
-    st.htab[0] = W.htab[0].as<uint64_t>();
-    st.htab[1] = W.htab[1].as<uint64_t>();
-    st.hmask = uint64_t(W.hcap - 1);
-  };
+  uint8_t* d0 = c.sp_dist[0].as<uint8_t>();
+  uint8_t* d1 = c.sp_dist[1].as<uint8_t>();
   SpCsr gout{cout->row_ptr.as<int64_t>(), cout->col.as<int32_t>(), cout->row_ok.as<uint8_t>()};
   SpCsr gin{cin->row_ptr.as<int64_t>(), cin->col.as<int32_t>(), cin->row_ok.as<uint8_t>()};
   const int64_t* vid_of = c.vid_of.as<int64_t>();
@@ -1527,14 +2539,317 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   std::vector<int64_t> hres(npairs), hoff(1, 0), hpath;
   std::vector<int32_t> hstate(static_cast<size_t>(2 * B)), hside(static_cast<size_t>(B)),
       hmet(static_cast<size_t>(B));
-  if (hash && c.sp_dirty && W.hcap > 0)  // a failed call's claims
-    for (auto& t : W.htab) NBG_HIP(hipMemsetAsync(t.p, 0xFF, size_t(W.hcap) * 8, c.stream));
+  // ---- device-driven batches (k_dv_*): fixed capacities sized once per context and batch size;
+  // false = a list overflowed (the clean state is restored, the batch runs host-driven below)
+  // (pair-major distance bytes only: the kernels address a pair's bytes from one row pointer)
+  const bool dev = c.opt("sp_dev", 1) != 0 && max_steps <= kMaxQ - 2 && lo == 0 && c.opt("sp_vmajor", 0) == 0;
+  auto dv_event = [&]() -> size_t {
+    if (!c.hop_timing) return ~size_t(0);
+    if (c.tev_used == c.tev.size()) {
+      hipEvent_t e;
+      NBG_HIP(hipEventCreate(&e));
+      c.tev.push_back(e);
+    }
+    NBG_HIP(hipEventRecord(c.tev[c.tev_used], c.stream));
+    return c.tev_used++;
+  };
+  auto dv_ms = [&](size_t a, size_t b) -> double {
+    float ms = 0;
+    if (a == ~size_t(0) || b == ~size_t(0)) return 0.0;
+    if (hipEventElapsedTime(&ms, c.tev[a], c.tev[b]) != hipSuccess) return 0.0;
+    return ms;
+  };
+  // host block layout (coherent pinned): publish slots, the finish copy of every counter, the
+  // pairs, then the results
+  const int64_t dvB = std::max<int64_t>(W.dv_B, B);
+  const size_t h_pub = 0, h_fin = h_pub + size_t(kMaxQ) * kPubW * 8, h_pairs = h_fin + size_t(kDevCnt + 64) * 8,
+               h_sr = h_pairs + size_t(dvB) * 16, h_off = h_sr + ((size_t(dvB) * 8 + 63) & ~size_t(63)),
+               h_path = h_off + size_t(dvB + 8) * 8, h_end = h_path + size_t(dvB) * (kMaxQ + 1) * 8;
+  auto dv_alloc = [&]() {
+    const int64_t gf_log2 = std::min<int64_t>(std::max<int64_t>(c.opt("sp_gf_log2", 24), 0), 32);
+    const bool pf_on = c.opt("sp_pf", 1) != 0;
+    const int64_t nnz = std::max(cout->nnz, cin->nnz);
+    const int64_t soft_dv = std::max<int64_t>(c.opt("sp_dv_list", int64_t(8) << 20), 64);
+    const int64_t cap = std::min<int64_t>(soft_dv, 2 * dvB * n + 64);
+    const int64_t cap_ch = cap + nnz / kCh + 64, cap_wch = std::min<int64_t>(soft_dv, dvB * (nnz / kCh + 1)) + 64;
+    if (W.dv_B >= dvB && W.dv_cap == cap && W.dv_cap_ch == cap_ch && W.dv_gf_log2 == gf_log2 && W.dv_pf_on == pf_on &&
+        c.sp_host && c.sp_host_bytes >= h_end) {
+      if (!W.dv_clean) {  // a failed call: every filter word and counter back to zero
+        NBG_HIP(hipMemsetAsync(W.dv_cnt.p, 0, W.dv_cnt.bytes, c.stream));
+        if (W.dv_pf.p) NBG_HIP(hipMemsetAsync(W.dv_pf.p, 0, W.dv_pf.bytes, c.stream));
+        if (W.dv_gf.p) NBG_HIP(hipMemsetAsync(W.dv_gf.p, 0, W.dv_gf.bytes, c.stream));
+        W.dv_clean = true;
+      }
+      return;
+    }
+    PoolScope none(nullptr);
+    NBG_HIP(hipStreamSynchronize(c.stream));
+    if (c.sp_host) (void)hipHostFree(c.sp_host);
+    c.sp_host = nullptr;
+    c.sp_host_bytes = 0;
+    NBG_HIP(hipHostMalloc(&c.sp_host, h_end, hipHostMallocCoherent));
+    memset(c.sp_host, 0, h_end);
+    c.sp_host_bytes = h_end;
+    W.dv_cnt = DevBuf();
+    W.dv_cnt.alloc(size_t(kDevCnt) * 8);
+    for (auto& b : W.dv_live) {
+      b = DevBuf();
+      b.alloc(size_t(cap) * 8);
+    }
+    for (DevBuf* b : {&W.dv_arena, &W.dv_meet, &W.dv_sw[0], &W.dv_sw[1], &W.dv_X, &W.dv_Xcb}) *b = DevBuf();
+    W.dv_arena.alloc(size_t(2 * cap) * 8);
+    W.dv_meet.alloc(size_t(cap) * 8);
+    W.dv_sw[0].alloc(size_t(cap) * 8);
+    W.dv_sw[1].alloc(size_t(cap) * 8);
+    W.dv_X.alloc(size_t(cap) * 8);
+    W.dv_Xcb.alloc(size_t(cap) * 8);
+    for (DevBuf* b : {&W.dv_chx, &W.dv_slot, &W.dv_wchx, &W.dv_pair, &W.dv_path, &W.dv_pf, &W.dv_gf}) *b = DevBuf();
+    W.dv_chx.alloc(size_t(cap_ch) * 4);
+    W.dv_slot.alloc(size_t(cap_ch) * 8);
+    W.dv_wchx.alloc(size_t(cap_wch) * 4);
+    // per pair: gs [2B] i32, cur [B] i32, best / wcb [B] i64, doff [B + 8] i64, pull / push [kMaxQ][B] u64
+    W.dv_pair.alloc(size_t(dvB) * (8 + 4 + 16 + 16 * kMaxQ) + size_t(8 + 8) * 8 + 256);
+    W.dv_path.alloc(size_t(dvB) * (kMaxQ + 1) * 8);
+    if (pf_on) W.dv_pf.alloc(size_t(2 * kLv) * size_t(dvB) * 512);
+    if (gf_log2 >= 5) W.dv_gf.alloc(size_t(1) << (gf_log2 - 3));
+    NBG_HIP(hipMemsetAsync(W.dv_cnt.p, 0, W.dv_cnt.bytes, c.stream));
+    if (W.dv_pf.p) NBG_HIP(hipMemsetAsync(W.dv_pf.p, 0, W.dv_pf.bytes, c.stream));
+    if (W.dv_gf.p) NBG_HIP(hipMemsetAsync(W.dv_gf.p, 0, W.dv_gf.bytes, c.stream));
+    W.dv_B = dvB;
+    W.dv_cap = cap;
+    W.dv_cap_ch = cap_ch;
+    W.dv_cap_wch = cap_wch;
+    W.dv_gf_log2 = gf_log2;
+    W.dv_pf_on = pf_on;
+    W.dv_clean = true;
+  };
+  auto run_dev = [&](size_t b0, int64_t nb) -> bool {
+    dv_alloc();
+    W.dv_clean = false;  // until the batch's finish launch (or the abort below) restores it
+    char* hb = static_cast<char*>(c.sp_host);
+    SpState st{};
+    st.B = int32_t(nb);
+    st.deg = W.state.as<unsigned long long>();
+    st.state = reinterpret_cast<int32_t*>(st.deg + 2 * nb);
+    st.res = st.state + nb;
+    st.lvl = st.res + nb;
+    st.side = st.lvl + 2 * nb;
+    st.pside = st.side + nb;
+    st.met = st.pside + nb;
+    st.vmajor = int32_t(c.opt("sp_vmajor", 0));
+    SpFilt f{};
+    f.pf = W.dv_pf.as<uint32_t>();
+    f.gf = W.dv_gf.as<uint32_t>();
+    f.gshift = W.dv_gf.p ? uint32_t(64 - (W.dv_gf_log2 - 5)) : 0u;
+    f.B = int32_t(nb);
+    f.k2 = c.opt("sp_pf_k", 2) >= 2 ? 1 : 0;
+    SpDev d{};
+    d.cnt = W.dv_cnt.as<unsigned long long>();
+    for (int k = 0; k < 4; k++) d.live[k >> 1][k & 1] = W.dv_live[k].as<uint64_t>();
+    d.cap_live = W.dv_cap;
+    d.arena = W.dv_arena.as<uint64_t>();
+    d.cap_arena = 2 * W.dv_cap;
+    d.meet = W.dv_meet.as<uint64_t>();
+    d.cap_meet = W.dv_cap;
+    d.sw[0] = W.dv_sw[0].as<uint64_t>();
+    d.sw[1] = W.dv_sw[1].as<uint64_t>();
+    d.cap_sw = W.dv_cap;
+    d.X = W.dv_X.as<uint64_t>();
+    d.Xcb = W.dv_Xcb.as<int64_t>();
+    d.cap_x = W.dv_cap;
+    d.chx = W.dv_chx.as<int32_t>();
+    d.slot = W.dv_slot.as<uint64_t>();
+    d.cap_ch = W.dv_cap_ch;
+    d.wchx = W.dv_wchx.as<int32_t>();
+    d.cap_wch = W.dv_cap_wch;
+    {
+      char* q = static_cast<char*>(W.dv_pair.p);
+      auto take = [&](size_t b) { char* r = q; q += (b + 63) & ~size_t(63); return r; };
+      d.gs = reinterpret_cast<int32_t*>(take(size_t(nb) * 8));
+      d.cur = reinterpret_cast<int32_t*>(take(size_t(nb) * 4));
+      d.best = reinterpret_cast<long long*>(take(size_t(nb) * 8));
+      d.wcb = reinterpret_cast<int64_t*>(take(size_t(nb) * 8));
+      d.doff = reinterpret_cast<int64_t*>(take(size_t(nb + 8) * 8));
+      d.pull = reinterpret_cast<unsigned long long*>(take(size_t(nb) * kMaxQ * 8));
+      d.push = d.pull + size_t(nb) * kMaxQ;  // adjacent: k_dv_begin clears both in one pass
+      (void)take(size_t(nb) * kMaxQ * 8);
+    }
+    d.path = W.dv_path.as<int64_t>();
+    int64_t* hp = reinterpret_cast<int64_t*>(hb + h_pairs);
+    memcpy(hp, src + b0, size_t(nb) * 8);
+    memcpy(hp + nb, dst + b0, size_t(nb) * 8);
+    d.h_pairs = hp;
+    d.h_sr = reinterpret_cast<int32_t*>(hb + h_sr);
+    d.h_off = reinterpret_cast<int64_t*>(hb + h_off);
+    d.h_path = reinterpret_cast<int64_t*>(hb + h_path);
+    auto pub = [&](int it) { return reinterpret_cast<unsigned long long*>(hb + h_pub) + size_t(it) * kPubW; };
+    unsigned long long* fin = reinterpret_cast<unsigned long long*>(hb + h_fin);
+
+    const int grid_sel_dv = int(std::max<int64_t>(1, c.opt("sp_dv_sel_grid", 512)));
+    const int grid_scan = int(std::max<int64_t>(1, c.opt("sp_dv_grid", 2048)));
+    const int occ = int(c.opt("sp_dv_occ", 1));
+    const int32_t lg_sub = int32_t(std::min<int64_t>(std::max<int64_t>(c.opt("sp_dv_exp_sub", 2), 0), 4));
+    const int max_it = std::min<int>(max_steps, kMaxQ - 2);
+    const int64_t htm = int64_t(c.ht_cap - 1);
+    const int64_t* htk = c.ht_keys.as<int64_t>();
+    const int32_t* htv = c.ht_vals.as<int32_t>();
+    std::vector<uint64_t> seq(size_t(kMaxQ), 0);
+    std::vector<std::array<size_t, 3>> evi(size_t(kMaxQ), {~size_t(0), ~size_t(0), ~size_t(0)});
+    std::vector<std::array<size_t, 2>> evs(size_t(kMaxQ), {~size_t(0), ~size_t(0)});
+
+    // the state is restored from whatever the device reached: the claimed bytes from the arena
+    // (wholesale when it overflowed, or `wipe`), every filter word and counter cleared; the batch
+    // then runs host-driven
+    auto dv_abort = [&](bool wipe) {
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      unsigned long long na = 0;
+      NBG_HIP(hipMemcpy(&na, d.cnt + D_ARENA, 8, hipMemcpyDeviceToHost));
+      if (!wipe && int64_t(na) <= d.cap_arena) {
+        if (na) k_sp_clear<<<grid_n(int64_t(na)), 256, 0, c.stream>>>(d.arena, int64_t(na), d0, d1, n, st);
+      } else {
+        const size_t used = ((size_t(nb) * size_t(n) + 3) & ~size_t(3)) + 64;
+        for (auto& dd : c.sp_dist) NBG_HIP(hipMemsetAsync(dd.p, 0xFF, std::min(used, c.sp_dist_bytes), c.stream));
+      }
+      NBG_HIP(hipMemsetAsync(W.dv_cnt.p, 0, W.dv_cnt.bytes, c.stream));
+      if (W.dv_pf.p) NBG_HIP(hipMemsetAsync(W.dv_pf.p, 0, W.dv_pf.bytes, c.stream));
+      if (W.dv_gf.p) NBG_HIP(hipMemsetAsync(W.dv_gf.p, 0, W.dv_gf.bytes, c.stream));
+      NBG_HIP(hipGetLastError());
+      NBG_HIP(hipStreamSynchronize(c.stream));
+      W.dv_clean = true;
+      return false;
+    };
+
+    k_dv_begin<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(d, st, gout, gin, d0, d1, n, max_steps, htk, htv,
+                                                          uint64_t(htm), c.ht_has_min, c.ht_min_gidx);
+    auto enqueue = [&](int it) {
+      k_dv_select<<<grid_sel_dv, kBlk, 0, c.stream>>>(d, st, gout, gin, it);
+      evi[size_t(it)][0] = dv_event();
+      if (probe) {
+        if (occ >= 8) k_dv_probe<8><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
+        else k_dv_probe<1><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
+      }
+      evi[size_t(it)][1] = dv_event();
+      if (occ >= 8) k_dv_expand<8><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it, lg_sub);
+      else k_dv_expand<1><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it, lg_sub);
+      evi[size_t(it)][2] = dv_event();
+      seq[size_t(it)] = ++c.pub_seq;
+      k_dv_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(d, st, max_steps, it, pub(it), seq[size_t(it)]);
+      NBG_HIP(hipGetLastError());
+    };
+    enqueue(1);
+    int it = 1;
+    for (;; it++) {
+      if (it < max_it) enqueue(it + 1);  // speculative: a no-op when iteration it ends the BFS
+      wait_host_word(c, pub(it) + kPubW - 1, seq[size_t(it)]);
+      const unsigned long long* hs = pub(it);
+      if (hs[D_OVF]) return dv_abort(false);
+      if (hs[D_G + Q_ACTIVE] == 0 || it >= max_it) break;
+    }
+    const int64_t maxL = int64_t(pub(it)[D_MAXL]), maxF = int64_t(pub(it)[D_MAXF]);
+    const int iters = it;
+    k_dv_post<<<int(std::max<int64_t>(1, c.opt("sp_dv_post_grid", 512))), kBlk, 0, c.stream>>>(
+        d, st, gout, gin, lo, htk, htv, uint64_t(htm), c.ht_has_min, c.ht_min_gidx);
+    const int nsw = int(std::min<int64_t>(std::max<int64_t>(maxF - 1, 0), kMaxQ - 2));
+    const unsigned long long bias16 = (unsigned long long)std::max<int64_t>(0, c.opt("sp_push_bias", 16));
+    for (int j = 1; j <= nsw; j++) {
+      k_dv_sweep_select<<<grid_sel_dv, kBlk, 0, c.stream>>>(d, st, gout, gin, j, bias16);
+      evs[size_t(j)][0] = dv_event();
+      if (occ >= 8) k_dv_sweep<8><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
+      else k_dv_sweep<1><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
+      evs[size_t(j)][1] = dv_event();
+    }
+    const int nwalk = int(std::min<int64_t>(maxL >= 2 ? maxL - 1 : 0, kMaxQ - 2));
+    for (int i = 0; i < nwalk; i++) {
+      if (i > 0)
+        k_dv_walk_front<<<grid_n(nb, 1 << 20), kBlk, 0, c.stream>>>(d, st, gout, i, lo, htk, htv, uint64_t(htm),
+                                                                   c.ht_has_min, c.ht_min_gidx);
+      k_dv_walk_scan<<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, d1, vid_of, n, lo, i);
+    }
+    k_dv_out<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(d, st, nwalk - 1);
+    const uint64_t fseq = ++c.pub_seq;
+    k_dv_finish<<<1, 64, 0, c.stream>>>(d.cnt, fin, fin + kDevCnt + 8, fseq);
+    k_dv_clear<<<grid_scan, 256, 0, c.stream>>>(d, st, f, d0, d1, n);
+    NBG_HIP(hipGetLastError());
+    wait_host_word(c, fin + kDevCnt + 8, fseq);
+    W.dv_clean = true;  // the finish launch cleared the counters, the clear launch (queued) the bytes and filters
+    if (fin[D_OVF]) {
+      // a sweep or walk list overflowed after the BFS: the result pass reset every byte and
+      // filter word the arena holds, unless the arena itself overflowed
+      if (int64_t(fin[D_ARENA]) > d.cap_arena) return dv_abort(true);
+      return false;
+    }
+    if (fin[D_WALKERR])
+      throw Error(NBG_E_UNKNOWN, "shortest path: in-edge keys without mirrored out-edges on a shortest path");
+
+    // per-launch records (modes 3 = meet probe, 2 = BFS expansion, 4 = sweep), from the copy of
+    // every counter the finish launch made
+    auto blkq = [&](int q) { return fin + D_G + size_t(q) * Q_W; };
+    if (c.hop_timing && c.tev_used) (void)hipEventSynchronize(c.tev[c.tev_used - 1]);
+    for (int i = 1; i <= iters; i++) {
+      const unsigned long long* q = blkq(i);
+      const unsigned long long act = blkq(i - 1)[Q_ACTIVE];
+      if (act == 0) continue;
+      c.timing.steps_run++;
+      const double pms = dv_ms(evi[size_t(i)][0], evi[size_t(i)][1]), ems = dv_ms(evi[size_t(i)][1], evi[size_t(i)][2]);
+      if (probe && q[Q_X]) {
+        c.timing.expand_ms += pms;
+        c.timing.expand_launches++;
+        c.timing.edges_scanned += q[Q_PE];
+        c.timing.expand_bytes += q[Q_X] * 24 + q[Q_PE] * 5;
+        const unsigned long long c8[8] = {q[Q_X], q[Q_PE], 0, fin[D_MEET], (unsigned long long)i, act, 0, 0};
+        c.timing.hop(3, false, pms, c8);
+        c.timing.name_last_hop(occ >= 8 ? "nbg::(anonymous namespace)::k_dv_probe<8>" : "nbg::(anonymous namespace)::k_dv_probe<1>");
+      }
+      if (q[Q_EE]) {
+        c.timing.expand_ms += ems;
+        c.timing.expand_launches++;
+        c.timing.edges_scanned += q[Q_EE];
+        c.timing.expand_bytes += q[Q_X] * 32 + q[Q_EE] * 5 + q[Q_CLAIMS] * 26;
+        const unsigned long long c8[8] = {q[Q_X], q[Q_EE], q[Q_CLAIMS], fin[D_MEET], (unsigned long long)i, act, 0, 0};
+        c.timing.hop(2, false, ems, c8);
+        c.timing.name_last_hop(occ >= 8 ? "nbg::(anonymous namespace)::k_dv_expand<8>" : "nbg::(anonymous namespace)::k_dv_expand<1>");
+      }
+    }
+    for (int j = 1; j <= nsw; j++) {
+      const unsigned long long* q = blkq(kSwQ + j);
+      if (!q[Q_EE]) continue;
+      const double sms = dv_ms(evs[size_t(j)][0], evs[size_t(j)][1]);
+      c.timing.expand_ms += sms;
+      c.timing.expand_launches++;
+      c.timing.edges_scanned += q[Q_EE];
+      c.timing.expand_bytes += q[Q_X] * 32 + q[Q_EE] * 6 + q[Q_CLAIMS] * 18;
+      const unsigned long long c8[8] = {q[Q_X], q[Q_EE], q[Q_CLAIMS], fin[D_MEET], (unsigned long long)j, 0, 0, 0};
+      c.timing.hop(4, false, sms, c8);
+      c.timing.name_last_hop(occ >= 8 ? "nbg::(anonymous namespace)::k_dv_sweep<8>" : "nbg::(anonymous namespace)::k_dv_sweep<1>");
+    }
+
+    // results (the ends of each path are the host's)
+    const int32_t* hsr = d.h_sr;
+    const int64_t* hoffb = d.h_off;
+    const int64_t plen = hoffb[nb];
+    const size_t base = hpath.size();
+    hpath.resize(base + size_t(plen));
+    if (plen > 0) memcpy(hpath.data() + base, d.h_path, size_t(plen) * 8);
+    for (int64_t p = 0; p < nb; p++) {
+      const int32_t L = hsr[p] == SP_ACTIVE ? -1 : hsr[nb + p];
+      hres[b0 + size_t(p)] = L;
+      if (L >= 0) {
+        hpath[base + size_t(hoffb[p])] = src[b0 + size_t(p)];
+        if (L > 0) hpath[base + size_t(hoffb[p] + L)] = dst[b0 + size_t(p)];
+      }
+      hoff.push_back(hoff.back() + hoffb[p + 1] - hoffb[p]);
+    }
+    return true;
+  };
   c.sp_dirty = true;  // until the batch's bytes are reset
   for (size_t b0 = 0; b0 < npairs; b0 += size_t(B)) {
     const int64_t nb = std::min<int64_t>(B, int64_t(npairs - b0));
+    if (dev && run_dev(b0, nb)) {
+      c.timing.spec_hops++;  // nbg_timing.spec_hops of a shortest-path call: batches run device-driven
+      continue;
+    }
     SpState st{};
     st.B = int32_t(nb);
-    hash_fit(st, 2 * nb);
     st.deg = W.state.as<unsigned long long>();
     st.state = reinterpret_cast<int32_t*>(st.deg + 2 * nb);
     st.res = st.state + nb;
@@ -1683,16 +2998,6 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     };
     auto regen = [&](int mode, int side, int32_t j, int32_t np, uint64_t* outl, int64_t cap, int which) {
       if (np == 0) return;
-      if (hash) {
-        DevBuf flag;
-        flag.alloc(size_t(nb) + 64);
-        NBG_HIP(hipMemsetAsync(flag.p, 0, size_t(nb) + 64, c.stream));
-        k_set_flags<<<grid_n(np), 256, 0, c.stream>>>(W.plist.as<int32_t>(), np, flag.as<uint8_t>());
-        k_sp_regen_hash<<<grid_n(W.hcap), 256, 0, c.stream>>>(mode, side, j, flag.as<uint8_t>(), st, n, outl, cap, cnt,
-                                                              which);
-        NBG_HIP(hipGetLastError());
-        return;
-      }
       dim3 grid(unsigned(std::min<int64_t>((n + 255) / 256, 1024)), unsigned(std::min<int32_t>(np, 65535)));
       k_sp_regen<<<grid, 256, 0, c.stream>>>(mode, side, j, W.plist.as<int32_t>(), np, st, d0, d1, n, outl, cap, cnt,
                                              which);
@@ -1743,7 +3048,6 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       if (probed) {
         // meet probe: pairs one edge short of meeting skip this iteration's expansion
         max_chunks = nX + E / kProbeCh + 64;
-        hash_fit(st, int64_t(hc[C_ARENA]) + max_chunks);
         reserve(c, W.meet, W.cap_meet, n_meet + max_chunks, n_meet);
         if (!arena_lost) reserve(c, W.arena, W.cap_arena, n_arena + max_chunks, n_arena);
         refresh(nullptr, 0);
@@ -1785,7 +3089,6 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
           reserve(c, W.arena, W.cap_arena, arena_keep + want, std::min<int64_t>(arena_keep, W.cap_arena));
         reserve(c, W.meet, W.cap_meet, meet_keep + std::min<int64_t>(E, soft) + 64, std::min<int64_t>(meet_keep, W.cap_meet));
         refresh(nullptr, 0);
-        hash_fit(st, int64_t(hc[C_ARENA]) + max_chunks + E);
         launch_scan(nX, probed);  // (k_sp_probe_end cleared the sentinel)
         launch_expand(nX, E, 0);
       }
@@ -1896,7 +3199,6 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         for (auto& kv : seen) diag[1] += uint64_t(kv.second);
       }
       c.timing.edges_scanned += uint64_t(E);
-      hash_fit(st, 2 * int64_t(hc[C_ARENA]));
       const int64_t want = std::min<int64_t>(E, soft) + 64;
       reserve(c, W.sweep[nxt], W.cap_sweep[nxt], want, 0);
       if (!arena_lost) reserve(c, W.arena, W.cap_arena, n_arena + want, n_arena);
@@ -2040,9 +3342,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       hoff.push_back(hoff.back() + h_off[p + 1] - h_off[p]);
     }
     // reset the batch's distance bytes
-    if (hash) {
-      for (auto& t : W.htab) NBG_HIP(hipMemsetAsync(t.p, 0xFF, size_t(W.hcap) * 8, c.stream));
-    } else if (arena_lost) {
+    if (arena_lost) {
       const size_t used = ((size_t(nb) * size_t(n) + 3) & ~size_t(3)) + 64;
       for (auto& d : c.sp_dist) NBG_HIP(hipMemsetAsync(d.p, 0xFF, std::min(used, c.sp_dist_bytes), c.stream));
     } else if (n_arena) {

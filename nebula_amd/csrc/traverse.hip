@@ -2178,20 +2178,26 @@ void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long lo
   const uint64_t seq = ++c.pub_seq;
   k_publish<<<1, 64, 0, c.stream>>>(d, n, h, c.host_seq, seq);
   NBG_HIP(hipGetLastError());
-  c.timing.host_waits++;
   if (c.opt("wait_trace", 0)) fprintf(stderr, "[nbg wait] rank %d: counter fetch of %d words\n", c.rank, n);
+  wait_host_word(c, c.host_seq, seq);
+}
+
+// one host wait on a word the device publishes with a system-scope release (k_publish, the
+// paths kernels' last-block publications)
+void wait_host_word(Ctx& c, const unsigned long long* word, uint64_t seq) {
+  c.timing.host_waits++;
   // pure spin for the first ~100 us (most waits: a hop of tens of us), then yield the core
   // between polls (a long hop, or several in-process LocalComm ranks waiting at once)
   const auto t0 = std::chrono::steady_clock::now();
   for (uint32_t spin = 0;; spin++) {
-    if (__atomic_load_n(c.host_seq, __ATOMIC_ACQUIRE) == seq) return;
+    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return;
     __builtin_ia32_pause();
     if ((spin & 255u) == 255u) {
       const auto dt = std::chrono::steady_clock::now() - t0;
       if (dt > std::chrono::microseconds(100)) std::this_thread::yield();
       if (dt > std::chrono::seconds(2)) {
         NBG_HIP(hipStreamSynchronize(c.stream));  // a fault surfaces here
-        if (__atomic_load_n(c.host_seq, __ATOMIC_ACQUIRE) == seq) return;
+        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return;
         throw Error(NBG_E_DEVICE, "counter publication lost");
       }
     }

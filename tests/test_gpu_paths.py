@@ -144,8 +144,9 @@ def test_nba_like_paths():
 
 
 def test_list_overflow_recovery():
-    # tiny list bounds force every overflow path: frontier lists and meet lists rebuilt from
-    # the distance bytes, the claim arena replaced by a full reset of the batch's bytes
+    # host-driven path (sp_dev = 0): tiny list bounds force every overflow path: frontier lists and
+    # meet lists rebuilt from the distance bytes, the claim arena replaced by a full reset of the
+    # batch's bytes
     scale = 12
     sp = GraphSpace(64)
     sp.set_edge_schema(FOLLOW, [("weight", 2)])
@@ -155,6 +156,7 @@ def test_list_overflow_recovery():
     st.set_edge_schema(FOLLOW, [("weight", O.INT)], name="follow")
     st.load_rmat(scale, 16, 1, FOLLOW)
     sp.set_option("sp_list_soft", 1)
+    sp.set_option("sp_dev", 0)
     s, t = synth.pairs(scale, 16, 1, 300, pick_seed=17)
     got = sp.shortest_path(s, t, FOLLOW, 7).rows()
     assert got == oracle_paths(st, s, t, FOLLOW, 7)
@@ -171,6 +173,7 @@ def test_meet_probe_on_and_off_match_oracle(rmat, probe, vmajor):
     scale, sp, st = rmat
     sp.set_option("sp_probe", probe)
     sp.set_option("sp_vmajor", vmajor)
+    sp.set_option("sp_dev", int(probe == 1 and vmajor == 0))
     try:
         s, t = synth.pairs(scale, 16, 1, 300, pick_seed=17)
         es, et_ = edge_case_pairs(scale)
@@ -179,6 +182,7 @@ def test_meet_probe_on_and_off_match_oracle(rmat, probe, vmajor):
             got = sp.shortest_path(src, dst, FOLLOW, max_steps).rows()
             assert got == oracle_paths(st, src, dst, FOLLOW, max_steps)
     finally:
+        sp.set_option("sp_dev", 1)
         sp.set_option("sp_probe", 1)
         sp.set_option("sp_vmajor", 0)
 
@@ -191,6 +195,7 @@ def test_sweep_direction_and_walk_variants(rmat, push, walk_wg, sweep_src):
     sp.set_option("sp_sweep_push", push)
     sp.set_option("sp_walk_wg", walk_wg)
     sp.set_option("sp_sweep_src", sweep_src)
+    sp.set_option("sp_dev", 0)
     try:
         s, t = synth.pairs(scale, 16, 1, 300, pick_seed=23)
         es, et_ = edge_case_pairs(scale)
@@ -201,6 +206,7 @@ def test_sweep_direction_and_walk_variants(rmat, push, walk_wg, sweep_src):
         hops = sp.last_timing()["hops"]
         assert any(h["mode"] == "sp-sweep" for h in hops) or scale < 11
     finally:
+        sp.set_option("sp_dev", 1)
         sp.set_option("sp_sweep_push", 1)
         sp.set_option("sp_walk_wg", 0)
         sp.set_option("sp_sweep_src", 0)
@@ -215,6 +221,7 @@ def test_sweep_kernels_and_level_filter(rmat, chunks, lvbits, push):
     sp.set_option("sp_sweep_chunks", chunks)
     sp.set_option("sp_lvbits", lvbits)
     sp.set_option("sp_sweep_push", push)
+    sp.set_option("sp_dev", 0)
     try:
         s, t = synth.pairs(scale, 16, 1, 300, pick_seed=29)
         es, et_ = edge_case_pairs(scale)
@@ -223,28 +230,72 @@ def test_sweep_kernels_and_level_filter(rmat, chunks, lvbits, push):
             got = sp.shortest_path(src, dst, FOLLOW, max_steps).rows()
             assert got == oracle_paths(st, src, dst, FOLLOW, max_steps)
     finally:
+        sp.set_option("sp_dev", 1)
         sp.set_option("sp_sweep_chunks", 1)
         sp.set_option("sp_lvbits", 1)
         sp.set_option("sp_sweep_push", 1)
 
 
-@pytest.mark.parametrize("log2,soft,batch", [(22, 16 << 20, 1024), (10, 16 << 20, 1024), (10, 1, 1024), (12, 16 << 20, 7)])
-def test_sparse_distance_maps(rmat, log2, soft, batch):
-    """option sp_hash: the (pair, vertex) -> depth maps replace the dense distance bytes; a map
-    starting at 2^10 slots grows (rehash) mid-batch, sp_list_soft = 1 forces every list to
-    overflow and be rebuilt from the maps (regen), small batches reuse cleared maps"""
+@pytest.mark.parametrize("dev", [1, 0])
+@pytest.mark.parametrize("pf,gf,occ,batch", [(1, 24, 1, 1024), (0, 24, 1, 1024), (1, 0, 1, 1024), (0, 0, 8, 1024),
+                                             (1, 10, 1, 1024), (1, 24, 8, 7)])
+def test_device_driven_batches(rmat, dev, pf, gf, occ, batch):
+    """the device-driven batch (k_dv_*: one fixed launch chain per batch, counters published by
+    the step kernels' last block) with the pair filters (sp_pf), the global level filter (sp_gf_log2,
+    2^10 bits: saturated, every test reaches the byte) and neither, against the host-driven path and
+    the oracle; nbg_timing.spec_hops counts the batches that ran device-driven"""
     scale, sp, st = rmat
     s, t = synth.pairs(scale, 16, 1, 200, pick_seed=17)
     es, et_ = edge_case_pairs(scale)
     src = np.concatenate([s, es])
     dst = np.concatenate([t, et_])
-    for k, v in (("sp_hash", 1), ("sp_hash_log2", log2), ("sp_list_soft", soft), ("sp_batch", batch)):
+    opts = (("sp_dev", dev), ("sp_pf", pf), ("sp_gf_log2", gf), ("sp_dv_occ", occ), ("sp_batch", batch))
+    for k, v in opts:
         sp.set_option(k, v)
     try:
-        got = sp.shortest_path(src, dst, FOLLOW, 8).rows()
-        again = sp.shortest_path(src, dst, FOLLOW, 8).rows()
+        for max_steps in (3, 8):
+            got = sp.shortest_path(src, dst, FOLLOW, max_steps).rows()
+            tm = sp.last_timing()
+            again = sp.shortest_path(src, dst, FOLLOW, max_steps).rows()
+            assert got == again
+            assert got == oracle_paths(st, src, dst, FOLLOW, max_steps)
+            nbatch = -(-len(src) // batch)
+            assert tm["spec_hops"] == (nbatch if dev else 0), tm["spec_hops"]
+            if dev and batch >= len(src):
+                # one wait per BFS iteration (published by its step kernel) + the batch's results
+                assert tm["host_waits"] <= tm["steps_run"] + 2, (tm["host_waits"], tm["steps_run"])
     finally:
-        for k in ("sp_hash", "sp_hash_log2", "sp_list_soft", "sp_batch"):
+        for k, _ in opts:
             sp.unset_option(k)
-    assert got == again
-    assert got == oracle_paths(st, src, dst, FOLLOW, 8)
+
+
+@pytest.mark.parametrize("cap", [64, 300, 2000])
+def test_device_driven_overflow_falls_back(cap):
+    """sp_dv_list bounds every list of the device-driven batch: an overflow (BFS lists, meets,
+    sweep lists, chunk tables, arena) restores the clean state and re-runs the batch host-driven;
+    results stay the oracle's and later calls see clean distance bytes and filters"""
+    scale = 12
+    sp = GraphSpace(64)
+    sp.set_edge_schema(FOLLOW, [("weight", 2)])
+    sp.gen_rmat(scale, 16, 1, FOLLOW)
+    sp.finalize()
+    st = O.Store(64)
+    st.set_edge_schema(FOLLOW, [("weight", O.INT)], name="follow")
+    st.load_rmat(scale, 16, 1, FOLLOW)
+    try:
+        s, t = synth.pairs(scale, 16, 1, 300, pick_seed=17)
+        sp.set_option("sp_dv_list", cap)
+        sp.set_option("sp_batch", 100)
+        got = sp.shortest_path(s, t, FOLLOW, 7).rows()
+        fell_back = 3 - sp.last_timing()["spec_hops"]
+        assert got == oracle_paths(st, s, t, FOLLOW, 7)
+        again = sp.shortest_path(t, s, FOLLOW, 7).rows()
+        assert again == oracle_paths(st, t, s, FOLLOW, 7)
+        if cap == 64:
+            assert fell_back == 3
+        sp.unset_option("sp_dv_list")
+        clean = sp.shortest_path(s, t, FOLLOW, 7).rows()  # device-driven again, clean state
+        assert sp.last_timing()["spec_hops"] == 3
+        assert clean == got
+    finally:
+        sp.close()

@@ -257,12 +257,19 @@ def test_configs2_rmat26_bench_query_digest():
         check_gold("go3_where499_distinct_s26", r.columns[0], r.edges_scanned)
         if "paths1024_s26" in GOLD:
             s, t = synth.pairs(26, 16, 1, 1024)
-            p = sp.shortest_path(s, t, FOLLOW, 8)
             import hashlib
-            h = hashlib.sha256(np.asarray(p.hops, dtype="<i8").tobytes())
-            for q in p.paths:
-                h.update(np.asarray(q, dtype="<i8").tobytes())
-            assert h.hexdigest() == GOLD["paths1024_s26"]["sha256"]
+            for dev in (1, 0):  # the device-driven batch, then the host-driven one
+                sp.set_option("sp_dev", dev)
+                p = sp.shortest_path(s, t, FOLLOW, 8)
+                tm = sp.last_timing()
+                h = hashlib.sha256(np.asarray(p.hops, dtype="<i8").tobytes())
+                for q in p.paths:
+                    h.update(np.asarray(q, dtype="<i8").tobytes())
+                assert h.hexdigest() == GOLD["paths1024_s26"]["sha256"], dev
+                if dev:
+                    # one counter wait per BFS iteration + the results (round 4: 16 fetches)
+                    assert tm["spec_hops"] == 1 and tm["host_waits"] <= 6, (tm["spec_hops"], tm["host_waits"])
+            sp.set_option("sp_dev", 1)
     finally:
         sp.close()
 
