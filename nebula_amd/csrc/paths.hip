@@ -32,6 +32,8 @@
 
 #include <algorithm>
 #include <array>
+#include <map>
+#include <mutex>
 #include <unordered_map>
 #include <climits>
 #include <cmath>
@@ -1246,6 +1248,7 @@ constexpr int kDevCnt = D_G + kNQ * Q_W;  // counter words
 constexpr int kCh = 1024;                 // adjacency entries per chunk (one wave)
 constexpr int kPubW = 64;                 // words per host publish slot (the sequence word last)
 constexpr int kDvStage = 256;             // claims staged per wave and list
+constexpr int kPairLds = 4096;            // pairs per batch whose per-pair tables the selects keep in LDS
 __device__ inline unsigned long long* qblk(unsigned long long* cnt, int q) { return cnt + D_G + q * Q_W; }
 
 struct SpFilt {
@@ -1254,6 +1257,8 @@ struct SpFilt {
   uint32_t gshift;  // 64 - log2(gf words)
   int32_t B;
   int32_t k2;       // pair filters with two bits per vertex (option sp_pf_k = 2)
+  int32_t diag;     // option sp_dv_diag (timing diagnostics, wrong results): sweep bit 0 no tests,
+                    // bit 1 filter tests without the byte reads
 };
 __device__ inline uint32_t pf_bit(uint32_t v) { return (v * 0x9E3779B1u) >> 20; }
 __device__ inline uint32_t pf_bit2(uint32_t v) { return ((v * 0x9E3779B1u) >> 8) & 4095u; }
@@ -1347,6 +1352,7 @@ struct SpDev {
   unsigned long long* pull;  // [kMaxQ][B] sweep step j's pull entries (in-degree + 1 sums)
   unsigned long long* push;  // [kMaxQ][B] forward level k's out-degree + 1 sums
   int64_t* doff;             // [B + 1] path offsets
+  int32_t lg_chb, lg_chs;    // log2 entries per chunk: BFS iterations (probe / expansion), sweep steps
   int64_t* path;
   const int64_t* h_pairs;    // coherent host: [B] src vids, [B] dst vids
   int32_t* h_sr;             // coherent host: [B] state, [B] res
@@ -1517,6 +1523,14 @@ __global__ __launch_bounds__(kBlk) void k_dv_select(SpDev d, SpState st, SpCsr g
   const int64_t rounds = (nl + per - 1) / per;
   unsigned long long esum = 0;
   unsigned long long* ctr[4] = {q + Q_X, q + Q_LIVE0, q + Q_LIVE1, q + Q_NCH};
+  // per pair, the side it expands (1 + side; 0: not active), in LDS: a tuple's lookup is then no
+  // global load behind its own (one round trip less in the chain tuple -> pair -> degree)
+  __shared__ uint8_t s_ps[kPairLds];
+  if (int64_t(blockIdx.x) < rounds) {
+    for (int p = threadIdx.x; p < st.B; p += blockDim.x)
+      s_ps[p] = st.state[p] == SP_ACTIVE ? uint8_t(1 + st.side[p]) : uint8_t(0);
+  }
+  __syncthreads();
   for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
     const int64_t i0 = r * per + threadIdx.x;
     uint64_t t[kSelIt];
@@ -1525,27 +1539,27 @@ __global__ __launch_bounds__(kBlk) void k_dv_select(SpDev d, SpState st, SpCsr g
       const int64_t i = i0 + u * kBlk;
       t[u] = i < n0 ? in0[i] : i < nl ? in1[i - n0] : ~0ull;
     }
-    int32_t s[kSelIt], sd[kSelIt];
+    // every tuple's degree in flight with the table lookups (the carried ones' unused)
+    int64_t dg[kSelIt];
 #pragma unroll
-    for (int u = 0; u < kSelIt; u++) s[u] = t[u] != ~0ull ? st.state[t_pair(t[u])] : SP_DONE;
-#pragma unroll
-    for (int u = 0; u < kSelIt; u++) sd[u] = s[u] == SP_ACTIVE ? st.side[t_pair(t[u])] : 0;
+    for (int u = 0; u < kSelIt; u++) dg[u] = t[u] != ~0ull ? sp_deg(t_side(t[u]) ? gin : gout, t_row(t[u])) : 0;
     uint32_t xm = 0, cm0 = 0, cm1 = 0;
 #pragma unroll
     for (int u = 0; u < kSelIt; u++) {
-      if (s[u] != SP_ACTIVE) continue;
+      if (t[u] == ~0ull) continue;
+      const uint32_t ps = s_ps[t_pair(t[u])];
+      if (ps == 0) continue;
       const uint32_t ts = t_side(t[u]);
-      if (uint32_t(sd[u]) == ts) xm |= 1u << u;
+      if (ps - 1 == ts) xm |= 1u << u;
       else if (ts) cm1 |= 1u << u;
       else cm0 |= 1u << u;
     }
-    int64_t dg[kSelIt];
     uint32_t nch = 0;
 #pragma unroll
     for (int u = 0; u < kSelIt; u++) {
-      dg[u] = (xm >> u) & 1u ? sp_deg(t_side(t[u]) ? gin : gout, t_row(t[u])) : 0;
+      if (!((xm >> u) & 1u)) dg[u] = 0;
       if (dg[u] == 0) xm &= ~(1u << u);  // nothing to scan
-      nch += uint32_t((dg[u] + kCh - 1) / kCh);
+      nch += uint32_t((dg[u] + (int64_t(1) << d.lg_chb) - 1) >> d.lg_chb);
       esum += (unsigned long long)dg[u];
     }
     const uint32_t nn[4] = {uint32_t(__popc(xm)), uint32_t(__popc(cm0)), uint32_t(__popc(cm1)), nch};
@@ -1555,7 +1569,7 @@ __global__ __launch_bounds__(kBlk) void k_dv_select(SpDev d, SpState st, SpCsr g
 #pragma unroll
     for (int u = 0; u < kSelIt; u++) {
       const bool x = (xm >> u) & 1u;
-      const int64_t nc = x ? (dg[u] + kCh - 1) / kCh : 0;
+      const int64_t nc = x ? (dg[u] + (int64_t(1) << d.lg_chb) - 1) >> d.lg_chb : 0;
       const int64_t xa = int64_t(o[0]), ca = int64_t(o[3]);
       if (x) {
         if (xa < d.cap_x && ca + nc <= d.cap_ch) {
@@ -1629,16 +1643,37 @@ __device__ inline void chunk_groups(int64_t vtotal, Desc desc, Body body) {
     }
   }
 }
-// the X chunk c's row slice [x0, x1) (sub-chunk s of 2^lg_sub)
-__device__ inline bool x_chunk(const SpDev& d, const SpCsr& g0, const SpCsr& g1, int64_t c, int32_t lg_sub, int64_t s,
-                               ChunkRec& r) {
+// one step's column entries: 64 * U from the 16-byte aligned x (lane L holds entries x + 4L .. +3
+// of each 256-entry block: one 16-byte load per lane and block instead of four 4-byte ones);
+// entries outside the slice [x0, x1) read as ~0.  A load stays inside the column array: it starts
+// below x1, and the arrays are padded past their last entry.
+template <int U = kProbeU>
+__device__ inline void col_step(const int32_t* col, int64_t x, int64_t x0, int64_t x1, int64_t lo, uint32_t* w) {
+  static_assert(U % 4 == 0, "whole 16-byte groups");
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < U / 4; j++) {
+    const int64_t e0 = x + j * 256 + 4 * lane;
+    int4 v = make_int4(-1, -1, -1, -1);
+    if (e0 < x1) v = *reinterpret_cast<const int4*>(col + e0);
+    const int32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      w[4 * j + k] = e0 + k >= x0 && e0 + k < x1 ? uint32_t(int64_t(vv[k]) - lo) : 0xFFFFFFFFu;
+  }
+}
+__device__ inline int64_t step_start(int64_t x0) { return x0 & ~int64_t(3); }
+
+// the X chunk c's row slice [x0, x1) (2^lg_ch entries; sub-chunk s of 2^lg_sub)
+__device__ inline bool x_chunk(const SpDev& d, const SpCsr& g0, const SpCsr& g1, int64_t c, int32_t lg_ch, int32_t lg_sub,
+                               int64_t s, ChunkRec& r) {
   const int32_t a = d.chx[c];
   r.t = d.X[a];
   const SpCsr& g = t_side(r.t) ? g1 : g0;
   const uint32_t row = t_row(r.t);
   const int64_t re = g.row_ptr[row + 1];
-  r.x0 = g.row_ptr[row] + (c - d.Xcb[a]) * kCh + s * (int64_t(kCh) >> lg_sub);
-  r.x1 = min(r.x0 + (int64_t(kCh) >> lg_sub), re);
+  r.x0 = g.row_ptr[row] + ((c - d.Xcb[a]) << lg_ch) + (s << (lg_ch - lg_sub));
+  r.x1 = min(r.x0 + (int64_t(1) << (lg_ch - lg_sub)), re);
   return r.x0 < r.x1;
 }
 
@@ -1646,8 +1681,8 @@ __device__ inline bool x_chunk(const SpDev& d, const SpCsr& g0, const SpCsr& g1,
 // neighbour at the other side's depth (or once another chunk claimed the vertex); the winner
 // claims the vertex on the other side, marks the pair (met = -1) and records the claim in its
 // chunk's slot
-template <int OCC>
-__global__ __launch_bounds__(256, OCC) void k_dv_probe(SpDev d, SpState st, SpFilt f, SpCsr g0, SpCsr g1,
+template <int U>  // column entries per lane and step (4, 8, 16: a whole chunk in one step)
+__global__ __launch_bounds__(256) void k_dv_probe(SpDev d, SpState st, SpFilt f, SpCsr g0, SpCsr g1,
                                                        uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo, int32_t it) {
   if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
   const int lane = threadIdx.x & 63;
@@ -1658,7 +1693,7 @@ __global__ __launch_bounds__(256, OCC) void k_dv_probe(SpDev d, SpState st, SpFi
   chunk_groups(
       total,
       [&](int64_t c, ChunkRec& r) {
-        if (!x_chunk(d, g0, g1, c, 0, 0, r)) return false;
+        if (!x_chunk(d, g0, g1, c, d.lg_chb, 0, 0, r)) return false;
         const uint32_t o = t_side(r.t) ^ 1u, p = t_pair(r.t);
         r.a0 = st.lvl[o * B + p];  // the other side's depth
         r.a1 = d.gs[o * B + p];    // its root (depth 0)
@@ -1671,31 +1706,31 @@ __global__ __launch_bounds__(256, OCC) void k_dv_probe(SpDev d, SpState st, SpFi
         uint8_t* const odp = (o ? d1 : d0) + uint64_t(p) * uint64_t(n);  // the pair's bytes (pair-major)
         bool pf_on;
         const uint2 prow = pf_load(f, o, need, p, pf_on);
-        for (int64_t x = r.x0; x < r.x1; x += 64 * kProbeU) {
-          const int32_t rem = int32_t(min(r.x1 - x, int64_t(64 * kProbeU)));
+        // the next step's columns are loaded before this step's tests wait on their filter and
+        // byte loads (one round trip less per step of the chain)
+        uint32_t wn[U];
+        col_step<U>(col, step_start(r.x0), r.x0, r.x1, lo, wn);
+        for (int64_t x = step_start(r.x0); x < r.x1; x += 64 * U) {
           if (uint32_t(*reinterpret_cast<volatile const uint8_t*>(odp + row)) != 0xFFu) break;  // another chunk claimed r
-          const int32_t* cp = col + x;
-          uint32_t w[kProbeU];
+          uint32_t w[U];
 #pragma unroll
-          for (int u = 0; u < kProbeU; u++) {
-            const int32_t e = u * 64 + lane;
-            w[u] = e < rem ? uint32_t(int64_t(cp[e]) - lo) : 0xFFFFFFFFu;
-          }
+          for (int u = 0; u < U; u++) w[u] = wn[u];
+          if (x + 64 * U < r.x1) col_step<U>(col, x + 64 * U, r.x0, r.x1, lo, wn);
           bool hit = false;
           if (need == 0) {
 #pragma unroll
-            for (int u = 0; u < kProbeU; u++) hit = hit || w[u] == uint32_t(r.a1);
+            for (int u = 0; u < U; u++) hit = hit || w[u] == uint32_t(r.a1);
           } else {
             uint32_t fm = 0;
 #pragma unroll
-            for (int u = 0; u < kProbeU; u++) {
+            for (int u = 0; u < U; u++) {
               const bool pv = pf_on ? pf_test(prow, w[u], f.k2 != 0) : true;
               fm |= (w[u] != 0xFFFFFFFFu && pv && gf_test(f, o, need, p, w[u])) ? 1u << u : 0u;
             }
 #pragma unroll
-            for (int u = 0; u < kProbeU; u++) hit = (((fm >> u) & 1u) && uint32_t(odp[w[u]]) == uint32_t(need)) || hit;
+            for (int u = 0; u < U; u++) hit = (((fm >> u) & 1u) && uint32_t(odp[w[u]]) == uint32_t(need)) || hit;
           }
-          examined += uint64_t(min(int64_t(64 * kProbeU), r.x1 - x)) * (lane == 0);
+          examined += uint64_t(min(x + 64 * U, r.x1) - max(x, r.x0)) * (lane == 0);
           if (__ballot(hit)) {
             if (lane == 0 && claim_byte(odp, row, uint32_t(need + 1))) {
               filt_mark(f, o, uint32_t(need + 1), p, row);
@@ -1790,7 +1825,7 @@ __device__ inline void dv_flush_block(DvStage& s, unsigned long long* cnt, unsig
 template <int OCC>
 __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpFilt f, SpCsr g0, SpCsr g1,
                                                         uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo, int32_t it,
-                                                        int32_t lg_sub) {
+                                                        int32_t lg_sub, int32_t cas) {
   __shared__ uint64_t s_stage[4][2][kDvStage];
   if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1806,7 +1841,7 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
   chunk_groups(
       total << lg_sub,
       [&](int64_t vc, ChunkRec& r) {
-        if (!x_chunk(d, g0, g1, vc >> lg_sub, lg_sub, vc & ((int64_t(1) << lg_sub) - 1), r)) return false;
+        if (!x_chunk(d, g0, g1, vc >> lg_sub, d.lg_chb, lg_sub, vc & ((int64_t(1) << lg_sub) - 1), r)) return false;
         return st.met[t_pair(r.t)] != -1;  // the probe finished the pair
       },
       [&](const ChunkRec& r, int64_t) {
@@ -1816,21 +1851,18 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
         const uint8_t* const odp = (side ? d0 : d1) + uint64_t(p) * uint64_t(n);
         entries += uint64_t(r.x1 - r.x0) * (lane == 0);
         unsigned long long dsum = 0;
-        for (int64_t x = r.x0; x < r.x1; x += 64 * kProbeU) {
-          const int32_t rem = int32_t(min(r.x1 - x, int64_t(64 * kProbeU)));
-          const int32_t* cp = g.col + x;
+        for (int64_t x = step_start(r.x0); x < r.x1; x += 64 * kProbeU) {
           uint32_t w[kProbeU];
-#pragma unroll
-          for (int u = 0; u < kProbeU; u++) {
-            const int32_t e = u * 64 + lane;
-            w[u] = e < rem ? uint32_t(int64_t(cp[e]) - lo) : 0xFFFFFFFFu;
-          }
+          col_step(g.col, x, r.x0, r.x1, lo, w);
           uint32_t bt[kProbeU];
 #pragma unroll
           for (int u = 0; u < kProbeU; u++) bt[u] = w[u] != 0xFFFFFFFFu ? uint32_t(sdp[w[u]]) : 0x1FFu;
 #pragma unroll
           for (int u = 0; u < kProbeU; u++) {
-            const bool cl = bt[u] == 0xFFu && claim_byte(sdp, w[u], l + 1);
+            // a claim: the CAS (option sp_dv_cas) or a plain byte store (the default: two chunks of one
+            // pair reaching the same vertex in this level may both list it; the byte holds l + 1 either
+            // way, and a duplicate tuple only repeats work)
+            const bool cl = bt[u] == 0xFFu && (cas ? claim_byte(sdp, w[u], l + 1) : (sdp[w[u]] = uint8_t(l + 1), true));
             bool meet = false;
             uint32_t dt = 0;
             if (cl) {
@@ -2040,10 +2072,18 @@ __global__ __launch_bounds__(kBlk) void k_dv_sweep_select(SpDev d, SpState st, S
   const uint64_t* cur = j == 1 ? d.meet : d.sw[(j - 1) & 1];
   const int64_t ncur = j == 1 ? min(int64_t(d.cnt[D_MEET]), d.cap_meet)
                               : min(int64_t(qblk(d.cnt, kSwQ + j - 1)[Q_CLAIMS]), d.cap_sw);
-  // the arena's forward tuples are scanned only when some pair pushes at this step (each block
-  // asks every pair: a few loads per thread instead of 1 M+ arena tuples per step)
+  // per pair in LDS: res - 1 of a MET pair (0: not sweeping) and the forward level it pushes at this
+  // step (0: it pulls); the arena's forward tuples are scanned only when some pair pushes (every
+  // block asks every pair: a few loads per thread instead of 1 M+ arena tuples per step)
+  __shared__ uint8_t s_rm1[kPairLds], s_pk[kPairLds];
   int anyp = 0;
-  for (int p = threadIdx.x; p < st.B; p += blockDim.x) anyp |= dv_push_pair(d, st, uint32_t(p), j, bias16) ? 1 : 0;
+  for (int p = threadIdx.x; p < st.B; p += blockDim.x) {
+    const bool met = st.state[p] == SP_MET;
+    const bool push = met && dv_push_pair(d, st, uint32_t(p), j, bias16);
+    s_rm1[p] = met ? uint8_t(max(st.res[p] - 1, 0)) : uint8_t(0);
+    s_pk[p] = push ? uint8_t(st.lvl[p] - j) : uint8_t(0);
+    anyp |= push ? 1 : 0;
+  }
   const int64_t na = __syncthreads_or(anyp) ? min(int64_t(d.cnt[D_ARENA]), d.cap_arena) : 0;
   const int64_t nt = ncur + na;
   constexpr int64_t per = int64_t(kBlk) * kSelIt;
@@ -2058,30 +2098,22 @@ __global__ __launch_bounds__(kBlk) void k_dv_sweep_select(SpDev d, SpState st, S
       const int64_t i = i0 + u * kBlk;
       t[u] = i < ncur ? cur[i] : i < nt ? d.arena[i - ncur] : ~0ull;
     }
-    int32_t s[kSelIt];
-#pragma unroll
-    for (int u = 0; u < kSelIt; u++) s[u] = t[u] != ~0ull ? st.state[t_pair(t[u])] : SP_DONE;
     uint32_t xm = 0;
     int64_t dg[kSelIt];
     uint32_t nch = 0;
 #pragma unroll
     for (int u = 0; u < kSelIt; u++) {
       dg[u] = 0;
-      if (s[u] != SP_MET) continue;
-      const uint32_t p = t_pair(t[u]);
+      if (t[u] == ~0ull) continue;
+      const uint32_t p = t_pair(t[u]), lv = t_lvl(t[u]);
       const bool pulled = i0 + u * kBlk < ncur;
-      bool go;
-      if (pulled) {
-        go = int32_t(t_lvl(t[u])) < st.res[p] - 1 && !dv_push_pair(d, st, p, j, bias16);
-      } else {
-        const int32_t k = st.lvl[p] - j;
-        go = t_side(t[u]) == 0 && k >= 1 && int32_t(t_lvl(t[u])) == k && dv_push_pair(d, st, p, j, bias16);
-      }
+      const uint32_t rm1 = s_rm1[p], pk = s_pk[p];
+      const bool go = pulled ? lv < rm1 && pk == 0 : t_side(t[u]) == 0 && pk != 0 && lv == pk;
       if (!go) continue;
       dg[u] = sp_deg(pulled ? gin : gout, t_row(t[u]));
       if (dg[u] == 0) continue;
       xm |= 1u << u;
-      nch += uint32_t((dg[u] + kCh - 1) / kCh);
+      nch += uint32_t((dg[u] + (int64_t(1) << d.lg_chs) - 1) >> d.lg_chs);
       esum += (unsigned long long)dg[u];
     }
     const uint32_t nn[2] = {uint32_t(__popc(xm)), nch};
@@ -2091,7 +2123,7 @@ __global__ __launch_bounds__(kBlk) void k_dv_sweep_select(SpDev d, SpState st, S
 #pragma unroll
     for (int u = 0; u < kSelIt; u++) {
       const bool x = (xm >> u) & 1u;
-      const int64_t nc = x ? (dg[u] + kCh - 1) / kCh : 0;
+      const int64_t nc = x ? (dg[u] + (int64_t(1) << d.lg_chs) - 1) >> d.lg_chs : 0;
       const int64_t xa = int64_t(o[0]), ca = int64_t(o[1]);
       const bool fit = xa < d.cap_x && ca + nc <= d.cap_ch;
       if (x) {
@@ -2116,8 +2148,8 @@ __global__ __launch_bounds__(kBlk) void k_dv_sweep_select(SpDev d, SpState st, S
 // once an out-neighbour has dt = L - l - 1 (the scan stops there).  Claims go to the arena and
 // the next sweep list, and the pull entries of the claimed vertices that the next step scans are
 // added to the pair's step j + 1 sum.
-template <int OCC>
-__global__ __launch_bounds__(256, OCC) void k_dv_sweep(SpDev d, SpState st, SpFilt f, SpCsr gout, SpCsr gin,
+template <int U>  // column entries per lane and step (4, 8, 16: a whole chunk in one step)
+__global__ __launch_bounds__(256) void k_dv_sweep(SpDev d, SpState st, SpFilt f, SpCsr gout, SpCsr gin,
                                                        uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo, int32_t j) {
   __shared__ uint64_t s_stage[4][kDvStage];
   if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
@@ -2132,7 +2164,7 @@ __global__ __launch_bounds__(256, OCC) void k_dv_sweep(SpDev d, SpState st, SpFi
   chunk_groups(
       total,
       [&](int64_t c, ChunkRec& r) {
-        if (!x_chunk(d, gout, gin, c, 0, 0, r)) return false;
+        if (!x_chunk(d, gout, gin, c, d.lg_chs, 0, 0, r)) return false;
         const uint32_t os = t_side(r.t) ^ 1u, p = t_pair(r.t);
         r.a0 = st.res[p];
         r.a1 = d.gs[os * B + p];
@@ -2149,35 +2181,34 @@ __global__ __launch_bounds__(256, OCC) void k_dv_sweep(SpDev d, SpState st, SpFi
         const uint2 prow = pf_load(f, os, need, p, pf_on);
         entries += uint64_t(r.x1 - r.x0) * (lane == 0);
         unsigned long long pc = 0;
-        for (int64_t x = r.x0; x < r.x1; x += 64 * kProbeU) {
-          const int32_t rem = int32_t(min(r.x1 - x, int64_t(64 * kProbeU)));
+        uint32_t wn[U];  // the next step's columns (see the probe)
+        col_step<U>(col, step_start(r.x0), r.x0, r.x1, lo, wn);
+        for (int64_t x = step_start(r.x0); x < r.x1; x += 64 * U) {
           if (side == 0 && *reinterpret_cast<volatile const uint8_t*>(d1p + row) != 0xFFu) break;  // u claimed
-          const int32_t* cp = col + x;
-          uint32_t w[kProbeU];
+          uint32_t w[U];
 #pragma unroll
-          for (int u = 0; u < kProbeU; u++) {
-            const int32_t e = u * 64 + lane;
-            w[u] = e < rem ? uint32_t(int64_t(cp[e]) - lo) : 0xFFFFFFFFu;
-          }
+          for (int u = 0; u < U; u++) w[u] = wn[u];
+          if (x + 64 * U < r.x1) col_step<U>(col, x + 64 * U, r.x0, r.x1, lo, wn);
           uint32_t hm = 0;  // entries whose neighbour sits at depth need on the other side
           if (need == 0) {
 #pragma unroll
-            for (int u = 0; u < kProbeU; u++) hm |= w[u] == uint32_t(r.a1) ? 1u << u : 0u;
+            for (int u = 0; u < U; u++) hm |= w[u] == uint32_t(r.a1) ? 1u << u : 0u;
           } else {
             uint32_t fm = 0;
 #pragma unroll
-            for (int u = 0; u < kProbeU; u++) {
+            for (int u = 0; u < U; u++) {
               const bool pv = pf_on ? pf_test(prow, w[u], f.k2 != 0) : true;
               fm |= (w[u] != 0xFFFFFFFFu && pv && gf_test(f, os, need, p, w[u])) ? 1u << u : 0u;
             }
+            if (f.diag) fm = (f.diag & 1) ? 0u : (__ballot(fm != 0) ? 0u : fm);
 #pragma unroll
-            for (int u = 0; u < kProbeU; u++)
+            for (int u = 0; u < U; u++)
               hm |= ((fm >> u) & 1u) && uint32_t(odp[w[u]]) == uint32_t(need) ? 1u << u : 0u;
           }
           if (__ballot(hm != 0) == 0) continue;
           if (side == 1) {
 #pragma unroll
-            for (int u = 0; u < kProbeU; u++) {
+            for (int u = 0; u < U; u++) {
               const bool cl = ((hm >> u) & 1u) && claim_byte(d1p, w[u], l + 1);
               if (cl) {
                 filt_mark(f, 1, l + 1, p, w[u]);
@@ -2234,15 +2265,15 @@ __global__ __launch_bounds__(256) void k_dv_walk_scan(SpDev d, SpState st, SpFil
         const uint2 prow = pf_load(f, 1, need, p, pf_on);
         const uint8_t* const d1p = d1 + uint64_t(p) * uint64_t(n);  // the pair's bytes (pair-major)
         long long bm = LLONG_MAX;
-        for (int64_t x = r.x0; x < r.x1; x += 64 * kProbeU) {
-          const int32_t rem = int32_t(min(r.x1 - x, int64_t(64 * kProbeU)));
-          const int32_t* cp = gout.col + x;
+        // the next step's columns are loaded before this step's tests wait on their filter and
+        // byte loads (one round trip less per step of the chain)
+        uint32_t wn[kProbeU];
+        col_step(gout.col, step_start(r.x0), r.x0, r.x1, lo, wn);
+        for (int64_t x = step_start(r.x0); x < r.x1; x += 64 * kProbeU) {
           uint32_t w[kProbeU];
 #pragma unroll
-          for (int u = 0; u < kProbeU; u++) {
-            const int32_t e = u * 64 + lane;
-            w[u] = e < rem ? uint32_t(int64_t(cp[e]) - lo) : 0xFFFFFFFFu;
-          }
+          for (int u = 0; u < kProbeU; u++) w[u] = wn[u];
+          if (x + 64 * kProbeU < r.x1) col_step(gout.col, x + 64 * kProbeU, r.x0, r.x1, lo, wn);
           uint32_t fm = 0;
 #pragma unroll
           for (int u = 0; u < kProbeU; u++) {
@@ -2316,13 +2347,22 @@ __global__ __launch_bounds__(256) void k_dv_clear(SpDev d, SpState st, SpFilt f,
   }
 }
 
-// every counter of the batch into coherent host memory, then cleared for the next batch; one
-// wave, lane 0's system-scope release publishes the sequence word after the copies
-__global__ void k_dv_finish(unsigned long long* cnt, unsigned long long* h, unsigned long long* hseq, uint64_t seq) {
-  for (int i = threadIdx.x; i < kDevCnt; i += 64) {
-    h[i] = cnt[i];
-    cnt[i] = i == D_CLEAR ? cnt[D_ARENA] : 0ull;
-  }
+// the batch's counters into coherent host memory, then cleared for the next batch: the globals
+// and the blocks the batch used (BFS blocks [0, nbfs), sweep steps [1, nsw], walk steps
+// [0, nwalk)); one wave, lane 0's system-scope release publishes the sequence word after the
+// copies.  D_CLEAR keeps the arena length for k_dv_clear.
+__global__ void k_dv_finish(unsigned long long* cnt, unsigned long long* h, unsigned long long* hseq, uint64_t seq,
+                            int32_t nbfs, int32_t nsw, int32_t nwalk) {
+  const unsigned long long arena = cnt[D_ARENA];  // read before any lane clears it
+  auto move = [&](int a, int b) {
+    for (int i = a + int(threadIdx.x); i < b; i += 64) {
+      h[i] = cnt[i];
+      cnt[i] = i == D_CLEAR ? arena : 0ull;
+    }
+  };
+  move(0, D_G + nbfs * Q_W);
+  move(D_G + (kSwQ + 1) * Q_W, D_G + (kSwQ + 1 + nsw) * Q_W);
+  move(D_G + kWkQ * Q_W, D_G + (kWkQ + nwalk) * Q_W);
   __builtin_amdgcn_wave_barrier();
   if (threadIdx.x == 0) __hip_atomic_store(hseq, (unsigned long long)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -2450,6 +2490,32 @@ static void replicate_csr(Ctx& c, const Csr& loc, Csr& rep) {
   NBG_HIP(hipStreamSynchronize(c.stream));
 }
 
+// the grid that fills the device exactly once with blocks of `kernel` (its occupancy x CUs): a
+// grid-stride scan over the chunks of a step then has no second, partial round of blocks
+// (measured: 1024 blocks of the sweep 0.42 ms, its resident 1280 0.38 ms, 2048 0.43 ms)
+static int cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+static int resident_grid(const void* kernel, int block) {
+  static std::mutex mu;
+  static std::map<const void*, int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(kernel);
+  if (it != cache.end()) return it->second;
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess || cus <= 0 || per <= 0)
+    return cache[kernel] = 1024;
+  return cache[kernel] = cus * per;
+}
+
 int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int64_t* dst_all, size_t npairs_all,
                           int32_t max_steps, nbg_rows* out) {
   if (!c.finalized) throw Error(NBG_E_STATE, "snapshot not finalized");
@@ -2542,7 +2608,8 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   // ---- device-driven batches (k_dv_*): fixed capacities sized once per context and batch size;
   // false = a list overflowed (the clean state is restored, the batch runs host-driven below)
   // (pair-major distance bytes only: the kernels address a pair's bytes from one row pointer)
-  const bool dev = c.opt("sp_dev", 1) != 0 && max_steps <= kMaxQ - 2 && lo == 0 && c.opt("sp_vmajor", 0) == 0;
+  const bool dev = c.opt("sp_dev", 1) != 0 && max_steps <= kMaxQ - 2 && lo == 0 && c.opt("sp_vmajor", 0) == 0 &&
+                   B <= kPairLds;
   auto dv_event = [&]() -> size_t {
     if (!c.hop_timing) return ~size_t(0);
     if (c.tev_used == c.tev.size()) {
@@ -2566,12 +2633,12 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
                h_sr = h_pairs + size_t(dvB) * 16, h_off = h_sr + ((size_t(dvB) * 8 + 63) & ~size_t(63)),
                h_path = h_off + size_t(dvB + 8) * 8, h_end = h_path + size_t(dvB) * (kMaxQ + 1) * 8;
   auto dv_alloc = [&]() {
-    const int64_t gf_log2 = std::min<int64_t>(std::max<int64_t>(c.opt("sp_gf_log2", 24), 0), 32);
+    const int64_t gf_log2 = std::min<int64_t>(std::max<int64_t>(c.opt("sp_gf_log2", 0), 0), 32);
     const bool pf_on = c.opt("sp_pf", 1) != 0;
     const int64_t nnz = std::max(cout->nnz, cin->nnz);
     const int64_t soft_dv = std::max<int64_t>(c.opt("sp_dv_list", int64_t(8) << 20), 64);
     const int64_t cap = std::min<int64_t>(soft_dv, 2 * dvB * n + 64);
-    const int64_t cap_ch = cap + nnz / kCh + 64, cap_wch = std::min<int64_t>(soft_dv, dvB * (nnz / kCh + 1)) + 64;
+    const int64_t cap_ch = cap + nnz / 512 + 64, cap_wch = std::min<int64_t>(soft_dv, dvB * (nnz / kCh + 1)) + 64;
     if (W.dv_B >= dvB && W.dv_cap == cap && W.dv_cap_ch == cap_ch && W.dv_gf_log2 == gf_log2 && W.dv_pf_on == pf_on &&
         c.sp_host && c.sp_host_bytes >= h_end) {
       if (!W.dv_clean) {  // a failed call: every filter word and counter back to zero
@@ -2642,7 +2709,8 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     f.gf = W.dv_gf.as<uint32_t>();
     f.gshift = W.dv_gf.p ? uint32_t(64 - (W.dv_gf_log2 - 5)) : 0u;
     f.B = int32_t(nb);
-    f.k2 = c.opt("sp_pf_k", 2) >= 2 ? 1 : 0;
+    f.k2 = c.opt("sp_pf_k", 1) >= 2 ? 1 : 0;
+    f.diag = int32_t(c.opt("sp_dv_diag", 0));
     SpDev d{};
     d.cnt = W.dv_cnt.as<unsigned long long>();
     for (int k = 0; k < 4; k++) d.live[k >> 1][k & 1] = W.dv_live[k].as<uint64_t>();
@@ -2675,6 +2743,8 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       (void)take(size_t(nb) * kMaxQ * 8);
     }
     d.path = W.dv_path.as<int64_t>();
+    d.lg_chb = int32_t(std::min<int64_t>(std::max<int64_t>(c.opt("sp_dv_lg_ch", 10), 9), 14));
+    d.lg_chs = int32_t(std::min<int64_t>(std::max<int64_t>(c.opt("sp_dv_lg_chs", 10), 9), 14));
     int64_t* hp = reinterpret_cast<int64_t*>(hb + h_pairs);
     memcpy(hp, src + b0, size_t(nb) * 8);
     memcpy(hp + nb, dst + b0, size_t(nb) * 8);
@@ -2686,9 +2756,21 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     unsigned long long* fin = reinterpret_cast<unsigned long long*>(hb + h_fin);
 
     const int grid_sel_dv = int(std::max<int64_t>(1, c.opt("sp_dv_sel_grid", 512)));
-    const int grid_scan = int(std::max<int64_t>(1, c.opt("sp_dv_grid", 2048)));
+    // scan grids: option sp_dv_grid, else each kernel's resident grid
+    const int64_t grid_opt = c.opt("sp_dv_grid", 0);
+    auto gsz = [&](const void* k) { return grid_opt > 0 ? int(grid_opt) : resident_grid(k, 256); };
+    // the meet probe at 5 blocks per CU (its resident 8 ran the third iteration at 0.29 ms, 5: 0.22)
+    const int64_t probe_grid = c.opt("sp_dv_probe_grid", 0);
+    auto gpr = [&](const void* k) {
+      return probe_grid > 0 ? int(probe_grid) : grid_opt > 0 ? int(grid_opt) : std::min(resident_grid(k, 256), 5 * cu_count());
+    };
     const int occ = int(c.opt("sp_dv_occ", 1));
-    const int32_t lg_sub = int32_t(std::min<int64_t>(std::max<int64_t>(c.opt("sp_dv_exp_sub", 2), 0), 4));
+    // expansion waves per BFS chunk: option sp_dv_exp_sub (log2), default 256-entry sub-chunks
+    int32_t lg_sub = int32_t(std::min<int64_t>(std::max<int64_t>(c.opt("sp_dv_exp_sub", -1), -1), 6));
+    if (lg_sub < 0) lg_sub = std::max<int32_t>(0, d.lg_chb - 8);
+    lg_sub = std::min<int32_t>(lg_sub, d.lg_chb);
+    const int32_t cas = int32_t(c.opt("sp_dv_cas", 0));
+    const int64_t pu = c.opt("sp_dv_probe_u", 4), su = c.opt("sp_dv_sweep_u", 4);  // entries per lane and step
     const int max_it = std::min<int>(max_steps, kMaxQ - 2);
     const int64_t htm = int64_t(c.ht_cap - 1);
     const int64_t* htk = c.ht_keys.as<int64_t>();
@@ -2725,12 +2807,20 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       k_dv_select<<<grid_sel_dv, kBlk, 0, c.stream>>>(d, st, gout, gin, it);
       evi[size_t(it)][0] = dv_event();
       if (probe) {
-        if (occ >= 8) k_dv_probe<8><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
-        else k_dv_probe<1><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
+        if (pu >= 16)
+          k_dv_probe<16><<<gpr((const void*)k_dv_probe<16>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
+        else if (pu >= 8)
+          k_dv_probe<8><<<gpr((const void*)k_dv_probe<8>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
+        else
+          k_dv_probe<4><<<gpr((const void*)k_dv_probe<4>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
       }
       evi[size_t(it)][1] = dv_event();
-      if (occ >= 8) k_dv_expand<8><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it, lg_sub);
-      else k_dv_expand<1><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it, lg_sub);
+      if (occ >= 8)
+        k_dv_expand<8><<<gsz((const void*)k_dv_expand<8>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it,
+                                                                               lg_sub, cas);
+      else
+        k_dv_expand<1><<<gsz((const void*)k_dv_expand<1>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it,
+                                                                               lg_sub, cas);
       evi[size_t(it)][2] = dv_event();
       seq[size_t(it)] = ++c.pub_seq;
       k_dv_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(d, st, max_steps, it, pub(it), seq[size_t(it)]);
@@ -2754,8 +2844,12 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     for (int j = 1; j <= nsw; j++) {
       k_dv_sweep_select<<<grid_sel_dv, kBlk, 0, c.stream>>>(d, st, gout, gin, j, bias16);
       evs[size_t(j)][0] = dv_event();
-      if (occ >= 8) k_dv_sweep<8><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
-      else k_dv_sweep<1><<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
+      if (su >= 16)
+        k_dv_sweep<16><<<gsz((const void*)k_dv_sweep<16>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
+      else if (su >= 8)
+        k_dv_sweep<8><<<gsz((const void*)k_dv_sweep<8>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
+      else
+        k_dv_sweep<4><<<gsz((const void*)k_dv_sweep<4>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
       evs[size_t(j)][1] = dv_event();
     }
     const int nwalk = int(std::min<int64_t>(maxL >= 2 ? maxL - 1 : 0, kMaxQ - 2));
@@ -2763,12 +2857,14 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       if (i > 0)
         k_dv_walk_front<<<grid_n(nb, 1 << 20), kBlk, 0, c.stream>>>(d, st, gout, i, lo, htk, htv, uint64_t(htm),
                                                                    c.ht_has_min, c.ht_min_gidx);
-      k_dv_walk_scan<<<grid_scan, 256, 0, c.stream>>>(d, st, f, gout, d1, vid_of, n, lo, i);
+      k_dv_walk_scan<<<gsz((const void*)k_dv_walk_scan), 256, 0, c.stream>>>(d, st, f, gout, d1, vid_of, n, lo, i);
     }
     k_dv_out<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(d, st, nwalk - 1);
     const uint64_t fseq = ++c.pub_seq;
-    k_dv_finish<<<1, 64, 0, c.stream>>>(d.cnt, fin, fin + kDevCnt + 8, fseq);
-    k_dv_clear<<<grid_scan, 256, 0, c.stream>>>(d, st, f, d0, d1, n);
+    // BFS blocks written: 0 .. iters, plus the speculative iteration after the last
+    const int32_t nbfs = std::min<int32_t>(iters + (iters < max_it ? 2 : 1), kMaxQ);
+    k_dv_finish<<<1, 64, 0, c.stream>>>(d.cnt, fin, fin + kDevCnt + 8, fseq, nbfs, nsw, nwalk);
+    k_dv_clear<<<gsz((const void*)k_dv_clear), 256, 0, c.stream>>>(d, st, f, d0, d1, n);
     NBG_HIP(hipGetLastError());
     wait_host_word(c, fin + kDevCnt + 8, fseq);
     W.dv_clean = true;  // the finish launch cleared the counters, the clear launch (queued) the bytes and filters
@@ -2778,7 +2874,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       if (int64_t(fin[D_ARENA]) > d.cap_arena) return dv_abort(true);
       return false;
     }
-    if (fin[D_WALKERR])
+    if (fin[D_WALKERR] && !f.diag)
       throw Error(NBG_E_UNKNOWN, "shortest path: in-edge keys without mirrored out-edges on a shortest path");
 
     // per-launch records (modes 3 = meet probe, 2 = BFS expansion, 4 = sweep), from the copy of
@@ -2798,7 +2894,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         c.timing.expand_bytes += q[Q_X] * 24 + q[Q_PE] * 5;
         const unsigned long long c8[8] = {q[Q_X], q[Q_PE], 0, fin[D_MEET], (unsigned long long)i, act, 0, 0};
         c.timing.hop(3, false, pms, c8);
-        c.timing.name_last_hop(occ >= 8 ? "nbg::(anonymous namespace)::k_dv_probe<8>" : "nbg::(anonymous namespace)::k_dv_probe<1>");
+        c.timing.name_last_hop("nbg::(anonymous namespace)::k_dv_probe");
       }
       if (q[Q_EE]) {
         c.timing.expand_ms += ems;
@@ -2807,7 +2903,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         c.timing.expand_bytes += q[Q_X] * 32 + q[Q_EE] * 5 + q[Q_CLAIMS] * 26;
         const unsigned long long c8[8] = {q[Q_X], q[Q_EE], q[Q_CLAIMS], fin[D_MEET], (unsigned long long)i, act, 0, 0};
         c.timing.hop(2, false, ems, c8);
-        c.timing.name_last_hop(occ >= 8 ? "nbg::(anonymous namespace)::k_dv_expand<8>" : "nbg::(anonymous namespace)::k_dv_expand<1>");
+        c.timing.name_last_hop("nbg::(anonymous namespace)::k_dv_expand");
       }
     }
     for (int j = 1; j <= nsw; j++) {
@@ -2820,7 +2916,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       c.timing.expand_bytes += q[Q_X] * 32 + q[Q_EE] * 6 + q[Q_CLAIMS] * 18;
       const unsigned long long c8[8] = {q[Q_X], q[Q_EE], q[Q_CLAIMS], fin[D_MEET], (unsigned long long)j, 0, 0, 0};
       c.timing.hop(4, false, sms, c8);
-      c.timing.name_last_hop(occ >= 8 ? "nbg::(anonymous namespace)::k_dv_sweep<8>" : "nbg::(anonymous namespace)::k_dv_sweep<1>");
+      c.timing.name_last_hop("nbg::(anonymous namespace)::k_dv_sweep");
     }
 
     // results (the ends of each path are the host's)

@@ -1351,7 +1351,7 @@ static void build_csr(Ctx& c, Staging& s, const std::vector<Field>& fields, bool
     if (hb == 0) out.row_ok.release();
   }
   // col
-  out.col.alloc(size_t(m) * 4 + 4);
+  out.col.alloc(size_t(m) * 4 + 64);  // padded: aligned 16-byte loads past the last entry
   k_gather_i32<<<grid_for(int64_t(m)), 256, 0, c.stream>>>(dstg.as<int32_t>(), kp, out.col.as<int32_t>(), int64_t(m));
   // the out CSR's dst vids as a column of their own: a plain GO's rows (YIELD _dst) stream it
   // instead of gathering vid_of[col[e]] (one random line per row)
@@ -2749,7 +2749,7 @@ static void finalize_rmat_stream(Ctx& c, EdgeSpace& es) {
     // final arrays sized for every sample (trimmed nnz is known only at the end; the tail stays unused)
     out.row_ptr.alloc(size_t(n_rows + 1) * 8);
     NBG_HIP(hipMemsetAsync(out.row_ptr.p, 0, 8, c.stream));
-    out.col.alloc(size_t(E) * 4 + 4);
+    out.col.alloc(size_t(E) * 4 + 64);  // padded: aligned 16-byte loads past the last entry
     const bool with_props = dir == 0;
     DevBuf w16;
     if (with_props) {
