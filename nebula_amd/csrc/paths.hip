@@ -2633,7 +2633,9 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
                h_sr = h_pairs + size_t(dvB) * 16, h_off = h_sr + ((size_t(dvB) * 8 + 63) & ~size_t(63)),
                h_path = h_off + size_t(dvB + 8) * 8, h_end = h_path + size_t(dvB) * (kMaxQ + 1) * 8;
   auto dv_alloc = [&]() {
-    const int64_t gf_log2 = std::min<int64_t>(std::max<int64_t>(c.opt("sp_gf_log2", 0), 0), 32);
+    // the global filter (2^24 bits): off costs the expansions nothing but lets the pair filters'
+    // false positives fetch a distance line each (sweep step 1: 3.4x its byte model, 1.1x with it)
+    const int64_t gf_log2 = std::min<int64_t>(std::max<int64_t>(c.opt("sp_gf_log2", 24), 0), 32);
     const bool pf_on = c.opt("sp_pf", 1) != 0;
     const int64_t nnz = std::max(cout->nnz, cin->nnz);
     const int64_t soft_dv = std::max<int64_t>(c.opt("sp_dv_list", int64_t(8) << 20), 64);
@@ -2755,7 +2757,8 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     auto pub = [&](int it) { return reinterpret_cast<unsigned long long*>(hb + h_pub) + size_t(it) * kPubW; };
     unsigned long long* fin = reinterpret_cast<unsigned long long*>(hb + h_fin);
 
-    const int grid_sel_dv = int(std::max<int64_t>(1, c.opt("sp_dv_sel_grid", 512)));
+    const int64_t sel_opt = c.opt("sp_dv_sel_grid", 0);  // select grids (default: resident)
+    auto gsel = [&](const void* k) { return sel_opt > 0 ? int(sel_opt) : resident_grid(k, kBlk); };
     // scan grids: option sp_dv_grid, else each kernel's resident grid
     const int64_t grid_opt = c.opt("sp_dv_grid", 0);
     auto gsz = [&](const void* k) { return grid_opt > 0 ? int(grid_opt) : resident_grid(k, 256); };
@@ -2804,7 +2807,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     k_dv_begin<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(d, st, gout, gin, d0, d1, n, max_steps, htk, htv,
                                                           uint64_t(htm), c.ht_has_min, c.ht_min_gidx);
     auto enqueue = [&](int it) {
-      k_dv_select<<<grid_sel_dv, kBlk, 0, c.stream>>>(d, st, gout, gin, it);
+      k_dv_select<<<gsel((const void*)k_dv_select), kBlk, 0, c.stream>>>(d, st, gout, gin, it);
       evi[size_t(it)][0] = dv_event();
       if (probe) {
         if (pu >= 16)
@@ -2842,7 +2845,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     const int nsw = int(std::min<int64_t>(std::max<int64_t>(maxF - 1, 0), kMaxQ - 2));
     const unsigned long long bias16 = (unsigned long long)std::max<int64_t>(0, c.opt("sp_push_bias", 16));
     for (int j = 1; j <= nsw; j++) {
-      k_dv_sweep_select<<<grid_sel_dv, kBlk, 0, c.stream>>>(d, st, gout, gin, j, bias16);
+      k_dv_sweep_select<<<gsel((const void*)k_dv_sweep_select), kBlk, 0, c.stream>>>(d, st, gout, gin, j, bias16);
       evs[size_t(j)][0] = dv_event();
       if (su >= 16)
         k_dv_sweep<16><<<gsz((const void*)k_dv_sweep<16>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);

@@ -9,7 +9,7 @@ BUILD = ("k_gen_rmat", "rocprim", "k_edge_keys", "k_dedup", "k_kept_src", "k_gat
 rows = list(csv.DictReader(open(sys.argv[1])))
 show_all = "--all" in sys.argv
 for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
-    name = r["Name"].split("(")[0]
+    name = r["Name"].replace("(anonymous namespace)::", "").split("(")[0]
     if not show_all and any(b in r["Name"] for b in BUILD):
         continue
     print(f"{name[-58:]:58s} calls={int(r['Calls']):5d} avg_us={float(r['AverageNs']) / 1e3:10.1f} "
