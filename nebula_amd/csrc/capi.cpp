@@ -103,6 +103,9 @@ nbg_ctx* nbg_ctx_create(int32_t device, int32_t num_parts, int32_t rank, int32_t
   // from pageable memory go through a driver bounce buffer and block the calling thread
   if (hipHostMalloc(&ctx->c.host_stage, nbg::kHostStageBytes, hipHostMallocDefault) != hipSuccess)
     ctx->c.host_stage = nullptr;
+  // coherent: k_starts_small reads a GO's small start set straight from here
+  if (hipHostMalloc(reinterpret_cast<void**>(&ctx->c.starts_host), 4096 * 8, hipHostMallocCoherent) != hipSuccess)
+    ctx->c.starts_host = nullptr;
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) == hipSuccess) ctx->c.hbm_total = tot;
   nbg::ctx_count_add(device, 1);
@@ -121,6 +124,7 @@ void nbg_ctx_destroy(nbg_ctx* ctx) {
   if (ctx->c.host_counters) (void)hipHostFree(ctx->c.host_counters);
   if (ctx->c.host_stage) (void)hipHostFree(ctx->c.host_stage);
   if (ctx->c.sp_host) (void)hipHostFree(ctx->c.sp_host);
+  if (ctx->c.starts_host) (void)hipHostFree(ctx->c.starts_host);
   (void)hipStreamDestroy(ctx->c.stream);
   delete ctx;
 }

@@ -571,6 +571,7 @@ struct Ctx {
   unsigned long long* host_seq = nullptr;  // pinned, coherent
   uint64_t pub_seq = 0;
   void* host_stage = nullptr;                   // pinned, kHostStageBytes (query inputs)
+  int64_t* starts_host = nullptr;               // pinned, coherent: a GO's small start set (k_starts_small)
   size_t host_stage_used = 0;
   // async host->device copy of a query input through the pinned stage when it fits (the stage
   // is reset at every query start; the stream drains before a query returns)

@@ -1257,8 +1257,9 @@ struct SpFilt {
   uint32_t gshift;  // 64 - log2(gf words)
   int32_t B;
   int32_t k2;       // pair filters with two bits per vertex (option sp_pf_k = 2)
-  int32_t diag;     // option sp_dv_diag (timing diagnostics, wrong results): sweep bit 0 no tests,
-                    // bit 1 filter tests without the byte reads
+  int32_t diag;     // option sp_dv_diag (diagnostics): sweep bit 0 no tests, bit 1 filter tests
+                    // without the byte reads (timing only, wrong results); bit 2 a walk error
+                    // returns the partial result instead of failing the call
 };
 __device__ inline uint32_t pf_bit(uint32_t v) { return (v * 0x9E3779B1u) >> 20; }
 __device__ inline uint32_t pf_bit2(uint32_t v) { return ((v * 0x9E3779B1u) >> 8) & 4095u; }
@@ -2200,7 +2201,7 @@ __global__ __launch_bounds__(256) void k_dv_sweep(SpDev d, SpState st, SpFilt f,
               const bool pv = pf_on ? pf_test(prow, w[u], f.k2 != 0) : true;
               fm |= (w[u] != 0xFFFFFFFFu && pv && gf_test(f, os, need, p, w[u])) ? 1u << u : 0u;
             }
-            if (f.diag) fm = (f.diag & 1) ? 0u : (__ballot(fm != 0) ? 0u : fm);
+            if (f.diag & 3) fm = (f.diag & 1) ? 0u : (__ballot(fm != 0) ? 0u : fm);
 #pragma unroll
             for (int u = 0; u < U; u++)
               hm |= ((fm >> u) & 1u) && uint32_t(odp[w[u]]) == uint32_t(need) ? 1u << u : 0u;
@@ -2323,6 +2324,11 @@ __global__ __launch_bounds__(256) void k_dv_out(SpDev d, SpState st, int32_t ila
     if (s != SP_ACTIVE)
       for (int32_t k = 1; k < L; k++) d.h_path[o + k] = d.path[o + k];
   }
+  // the host reads these words once k_dv_finish (the next launch) publishes its sequence word:
+  // every writer's stores must have left the device first (a system-scope release per wave; the
+  // kernel boundary alone did not order them before the finish wave's store when several
+  // contexts shared the device: stale paths at 8 in-process ranks)
+  __threadfence_system();
 }
 
 // every claimed distance byte of the batch and its filter words reset from the arena (after the
@@ -2632,6 +2638,11 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   const size_t h_pub = 0, h_fin = h_pub + size_t(kMaxQ) * kPubW * 8, h_pairs = h_fin + size_t(kDevCnt + 64) * 8,
                h_sr = h_pairs + size_t(dvB) * 16, h_off = h_sr + ((size_t(dvB) * 8 + 63) & ~size_t(63)),
                h_path = h_off + size_t(dvB + 8) * 8, h_end = h_path + size_t(dvB) * (kMaxQ + 1) * 8;
+  auto dv_pair_bytes = [](int64_t nb) {
+    auto r = [](size_t b) { return (b + 63) & ~size_t(63); };
+    const size_t b = size_t(nb);
+    return r(b * 8) + r(b * 4) + r(b * 8) + r(b * 8) + r((b + 8) * 8) + 2 * r(b * kMaxQ * 8);
+  };
   auto dv_alloc = [&]() {
     // the global filter (2^24 bits): off costs the expansions nothing but lets the pair filters'
     // false positives fetch a distance line each (sweep step 1: 3.4x its byte model, 1.1x with it)
@@ -2676,8 +2687,9 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     W.dv_chx.alloc(size_t(cap_ch) * 4);
     W.dv_slot.alloc(size_t(cap_ch) * 8);
     W.dv_wchx.alloc(size_t(cap_wch) * 4);
-    // per pair: gs [2B] i32, cur [B] i32, best / wcb [B] i64, doff [B + 8] i64, pull / push [kMaxQ][B] u64
-    W.dv_pair.alloc(size_t(dvB) * (8 + 4 + 16 + 16 * kMaxQ) + size_t(8 + 8) * 8 + 256);
+    // per pair (the layout run_dev carves, each piece rounded up to 64 bytes): gs [2B] i32, cur [B]
+    // i32, best [B] i64, wcb [B] i64, doff [B + 8] i64, pull [kMaxQ][B] u64, push [kMaxQ][B] u64
+    W.dv_pair.alloc(dv_pair_bytes(dvB));
     W.dv_path.alloc(size_t(dvB) * (kMaxQ + 1) * 8);
     if (pf_on) W.dv_pf.alloc(size_t(2 * kLv) * size_t(dvB) * 512);
     if (gf_log2 >= 5) W.dv_gf.alloc(size_t(1) << (gf_log2 - 3));
@@ -2734,7 +2746,13 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     d.cap_wch = W.dv_cap_wch;
     {
       char* q = static_cast<char*>(W.dv_pair.p);
-      auto take = [&](size_t b) { char* r = q; q += (b + 63) & ~size_t(63); return r; };
+      char* const q_end = q + W.dv_pair.bytes;
+      auto take = [&](size_t b) {
+        char* r = q;
+        q += (b + 63) & ~size_t(63);
+        if (q > q_end) throw Error(NBG_E_UNKNOWN, "shortest path: per-pair workspace layout exceeds its block");
+        return r;
+      };
       d.gs = reinterpret_cast<int32_t*>(take(size_t(nb) * 8));
       d.cur = reinterpret_cast<int32_t*>(take(size_t(nb) * 4));
       d.best = reinterpret_cast<long long*>(take(size_t(nb) * 8));
@@ -2877,7 +2895,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       if (int64_t(fin[D_ARENA]) > d.cap_arena) return dv_abort(true);
       return false;
     }
-    if (fin[D_WALKERR] && !f.diag)
+    if (fin[D_WALKERR] && !(f.diag & 4))
       throw Error(NBG_E_UNKNOWN, "shortest path: in-edge keys without mirrored out-edges on a shortest path");
 
     // per-launch records (modes 3 = meet probe, 2 = BFS expansion, 4 = sweep), from the copy of

@@ -2958,7 +2958,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   if (c.host_stage_used) host_sync(c);  // a failed query's copies
   c.host_stage_used = 0;
   c.total_pending = false;
-  hipEventRecord(c.ev[0], c.stream);
+  // the query's device-time events too are instrumentation: with hop_timing off none is recorded
+  // (an event between two launches leaves ~5.5 us between them on the device)
+  const bool tot_ev = c.hop_timing;
+  if (tot_ev) hipEventRecord(c.ev[0], c.stream);
 
   // compile WHERE / YIELD (errors are deferred to the final step, as the reference only
   // reports them when the final getNeighbors request is actually sent)
@@ -3048,7 +3051,13 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
                      c.opt("starts_small", 1) != 0;
   // counters summed over ranks on the device (dev_allsum) land at K.d[48, 52)
   const bool multi = c.world > 1;
-  if (ns) {
+  // the small-start path's one block reads the starts from coherent pinned host memory (the
+  // stream's previous query finished before this one was enqueued): no copy between queries
+  const int64_t* k_starts = d_starts;
+  if (ns && fast1 && c.starts_host) {
+    memcpy(c.starts_host, s.starts, size_t(ns) * 8);
+    k_starts = c.starts_host;
+  } else if (ns) {
     c.h2d(d_starts, s.starts, size_t(ns) * 8);
     if (!fast1) lookup_gidx(c, d_starts, d_sg, ns);
   }
@@ -3066,7 +3075,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     c.ws_tile_rows.ensure(size_t(std::min<int64_t>(eb, csr.nnz + 1) / kTile + 4) * 4);
   }
   if (fast1) {
-    k_starts_small<<<1, 1024, 0, c.stream>>>(d_starts, int32_t(ns), c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
+    k_starts_small<<<1, 1024, 0, c.stream>>>(k_starts, int32_t(ns), c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
                                               uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, d_sg, lo, hi,
                                               row_ptr, row_ok, reinterpret_cast<uint32_t*>(bits16), F,
                                               c.ws_off.as<int64_t>(), K.d,
@@ -3475,7 +3484,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         dev_allsum(c, K.d, {12, 13, 41}, K.d + 48);
       }
       // (the device work ends here when the speculated final hop runs: ev[1] ahead of the fetch)
-      fetch_counters(c, K.d, spec_words(multi ? 52 : 42), K.h, spec_final() ? c.ev[1] : nullptr);
+      fetch_counters(c, K.d, spec_words(multi ? 52 : 42), K.h, spec_final() && tot_ev ? c.ev[1] : nullptr);
       const int64_t nF1 = int64_t(K.h[40]), E1 = int64_t(K.h[41]);
       if (!s.distinct) hop1_scanned = int64_t(K.h[30]);
       c.timing.edges_scanned += uint64_t(hop1_scanned >= 0 ? hop1_scanned : E1);
@@ -3581,7 +3590,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         piggy_used = false;
         dev_allsum(c, K.d, {12, 13}, K.d + 48);
       }
-      fetch_counters(c, K.d, spec_words(multi ? 50 : 16), K.h, spec_final() ? c.ev[1] : nullptr);
+      fetch_counters(c, K.d, spec_words(multi ? 50 : 16), K.h, spec_final() && tot_ev ? c.ev[1] : nullptr);
       nF = lazy ? 0 : int64_t(K.h[0]);
       list_n = lazy ? int64_t(K.h[14]) : -1;
       E = int64_t(K.h[13]);
@@ -3846,8 +3855,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   }
   // ev[1] ends the device time; not waited for here (resolve_total reads it when asked): a
   // speculated final hop recorded it ahead of its counter fetch, after which nothing was enqueued
-  if (!fin_done) hipEventRecord(c.ev[1], c.stream);
-  c.total_pending = true;
+  if (tot_ev && !fin_done) hipEventRecord(c.ev[1], c.stream);
+  c.total_pending = tot_ev;
   // STRING columns: (address, length) rows -> packed bytes + n+1 offsets
   const size_t ncols_out = h->types.size();
   std::vector<int64_t> soff_dev_idx(ncols_out, -1);

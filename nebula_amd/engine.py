@@ -154,6 +154,7 @@ class GraphSpace:
         self.L = _lib.load()
         self.num_parts, self.rank, self.world_size = num_parts, rank, world_size
         self._options: set[str] = set()
+        self._plan_views: dict = {}  # (WHERE bytes, YIELD bytes) -> their C views (go())
         self.h = self.L.nbg_ctx_create(device, num_parts, rank, world_size)
         if not self.h:
             raise RuntimeError("nbg_ctx_create failed: no MI355X visible or bad arguments "
@@ -358,11 +359,21 @@ class GraphSpace:
         as [(name, NBG_T_*, values)] (GoExecutor::getPropFromInterim)."""
         starts = np.ascontiguousarray(starts, dtype=np.int64)
         w = X.encode(where)
-        wb = np.frombuffer(w + b"\0", dtype=np.uint8)
-        ys = [X.encode(y) for y in yields]
-        ybufs = [C.create_string_buffer(y, len(y) + 1) for y in ys]
-        yp = (C.c_void_p * max(len(ys), 1))(*[C.cast(b, C.c_void_p) for b in ybufs])
-        yl = (C.c_size_t * max(len(ys), 1))(*[len(y) for y in ys])
+        ys = tuple(X.encode(y) for y in yields)
+        # the C views of the encoded WHERE / YIELD bytes, built once per distinct plan (a GO
+        # repeated with the same plan re-uses them; they live as long as the space)
+        key = (w, ys)
+        views = self._plan_views.get(key)
+        if views is None:
+            wb = np.frombuffer(w + b"\0", dtype=np.uint8)
+            ybufs = [C.create_string_buffer(y, len(y) + 1) for y in ys]
+            yp = (C.c_void_p * max(len(ys), 1))(*[C.cast(b, C.c_void_p) for b in ybufs])
+            yl = (C.c_size_t * max(len(ys), 1))(*[len(y) for y in ys])
+            views = (wb, ybufs, yp, yl)
+            if len(self._plan_views) >= 64:
+                self._plan_views.clear()
+            self._plan_views[key] = views
+        wb, _, yp, yl = views
         spec = _lib.GoSpec(edge_type, steps, _p(starts), len(starts), _p(wb), len(w), yp, yl, len(ys),
                            int(distinct), int(keep_on_device))
         if inputs:
