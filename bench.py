@@ -69,6 +69,26 @@ def pmc_traffic(workload: str, prefixes):
     return best
 
 
+def pmc_traffic_query(workload: str, kind: str):
+    """HBM bytes per query of one scan kind (all its launches of one query) from the newest
+    committed C4 PMC summary of the same workload (profiles/<tag>_c4.json, tools/c4_counters.sh +
+    tools/c4_summary.py: FETCH_SIZE x2 + WRITE_SIZE per dispatch).  None if absent."""
+    best = None
+    for f in sorted((ROOT / "profiles").glob("*_c4.json"), key=lambda p: p.name):
+        try:
+            d = json.loads(f.read_text())
+        except ValueError:
+            continue
+        if ((d.get("bench") or {}).get("config") or {}).get("workload") != workload:
+            continue
+        k = (d.get("query_kinds") or {}).get(kind)
+        if k and k.get("complete"):
+            best = {"bytes": k["fetch_bytes_x2"] + k["write_bytes"],
+                    "raw_bytes": k["fetch_bytes_x2"] / 2 + k["write_bytes"],
+                    "model_bytes": k["model_bytes"], "launches": k["launches"], "source": f"profiles/{f.name}"}
+    return best
+
+
 # ---- CPU baseline -----------------------------------------------------------------------------
 def host_cpu():
     """(usable cores of this process, cores of the machine, CPU model).  The GPU box pins a
@@ -335,7 +355,7 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
     dl = [l for l in launches if l["kind"] == dom]
     if dl:
         kern[dom] = max(dl, key=lambda l: l["ms"])["kernel"]
-    tr = pmc_traffic(workload, [kern.get(dom, "nbg::k_sp_expand")])
+    tr = pmc_traffic_query(workload, dom)
     out = {
         "metric": "FIND SHORTEST PATH pairs/s (batched bidirectional BFS) on RMAT-26",
         "value": args.pairs * args.steps / dt,
@@ -366,10 +386,12 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
         "roofline": {
             "bound": "hbm", "kernel": kern.get(dom, dom), "achieved": dom_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": dom_ach / HBM_PEAK_GBS,
-            # PMC HBM bytes of the dominant kernel per query (all its launches of one query)
-            "traffic": tr["bytes"] * dk["launches"] if tr else None,
-            "traffic_source": tr["source"] + " (FETCH_SIZE x2 + WRITE_SIZE per launch x launches per query)"
-            if tr else None,
+            # PMC HBM bytes of the dominant kind per query (all its launches of one profiled query)
+            "traffic": tr["bytes"] if tr else None,
+            "traffic_raw_fetch_plus_write": tr["raw_bytes"] if tr else None,
+            "traffic_over_model": tr["bytes"] / tr["model_bytes"] if tr and tr["model_bytes"] else None,
+            "traffic_source": tr["source"] + " (FETCH_SIZE x2 + WRITE_SIZE summed over the kind's launches "
+            "of one query)" if tr else None,
             "algorithmic_bytes_per_query": dk["bytes"], "kernel_ms_per_query": dk["ms"],
             "all_scan_kernels": {"achieved": achieved, "frac": achieved / HBM_PEAK_GBS},
             "expand_ms_per_query": exp_ms / max(args.steps, 1), "device_ms_per_query": dev_ms / max(args.steps, 1),

@@ -3443,7 +3443,10 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     NBG_HIP(hipMemcpyAsync(h_sr, st.state, size_t(nb) * 8, hipMemcpyDeviceToHost, c.stream));
     NBG_HIP(hipMemcpyAsync(h_off, doff.p, size_t(nb + 1) * 8, hipMemcpyDeviceToHost, c.stream));
     if (plen > 0) NBG_HIP(hipMemcpyAsync(h_path, dpath.p, size_t(plen) * 8, hipMemcpyDeviceToHost, c.stream));
-    sync_counters();  // every copy above has landed (stream order) and C_WALKERR is current
+    sync_counters();  // C_WALKERR is current; the staged copies above have landed (stream order)
+    // pageable destinations: hipMemcpyAsync may return before such a copy completes, so the
+    // stream is drained before the host reads them
+    if (!staged) NBG_HIP(hipStreamSynchronize(c.stream));
     if (plen > 0 && hc[C_WALKERR])
       throw Error(NBG_E_UNKNOWN, "shortest path: in-edge keys without mirrored out-edges on a shortest path");
     const size_t base = hpath.size();

@@ -1680,16 +1680,39 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
   const int64_t tile = int64_t(blockDim.x) * 4;
   const int64_t ntiles = (nchunks + tile - 1) / tile;
   unsigned long long acc[3] = {0, 0, 0};
+  // bitmap-only compaction (out == nullptr, the bottom-up path): the next tile's chunk loads are
+  // issued with this one's (its map words stay in registers for the next round), so a block waits
+  // one map latency per round of tiles, not one per tile
+  const bool pre = out == nullptr;
+  uint4 wn[4];
+  if (pre) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int64_t ch = int64_t(blockIdx.x) * tile + q * int64_t(blockDim.x) + threadIdx.x;
+      wn[q] = int64_t(blockIdx.x) < ntiles && ch < nchunks ? reinterpret_cast<const uint4*>(map + lo)[ch]
+                                                            : make_uint4(0, 0, 0, 0);
+    }
+  }
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     uint32_t keep[4];
     uint32_t cnt = 0;
     // the tile's four chunk loads issued together (the clearing stores below would otherwise
     // order each load behind the previous chunk's store)
     uint4 wq[4];
+    if (pre) {
+      const int64_t tn = t + gridDim.x;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int64_t ch = t * tile + q * int64_t(blockDim.x) + threadIdx.x;
-      wq[q] = ch < nchunks ? reinterpret_cast<const uint4*>(map + lo)[ch] : make_uint4(0, 0, 0, 0);
+      for (int q = 0; q < 4; q++) {
+        wq[q] = wn[q];
+        const int64_t ch = tn * tile + q * int64_t(blockDim.x) + threadIdx.x;
+        wn[q] = tn < ntiles && ch < nchunks ? reinterpret_cast<const uint4*>(map + lo)[ch] : make_uint4(0, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int64_t ch = t * tile + q * int64_t(blockDim.x) + threadIdx.x;
+        wq[q] = ch < nchunks ? reinterpret_cast<const uint4*>(map + lo)[ch] : make_uint4(0, 0, 0, 0);
+      }
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -3918,6 +3941,17 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     }
     h->str_off.push_back(nullptr);
     if (host_cols.count(cc)) {  // written into pinned host memory by the output kernel
+      // the block spans the vertex space (n_global vids): a result far smaller than it is copied
+      // into a right-sized pinned block, so a result the caller keeps pins about its own size (the
+      // large block returns to the context's pinned cache, whose cap bounds what stays held)
+      HostBuf& big = h->hpin.back();
+      const size_t need = size_t(nrows) * 8 + 8;
+      if (need * 4 < big.bytes && need <= (size_t(64) << 20)) {
+        HostBuf small;
+        small.alloc(c.host_pool, need);
+        if (nrows) memcpy(small.p, big.p, size_t(nrows) * 8);
+        big = std::move(small);
+      }
       h->cols.push_back(h->hpin.back().p);
     } else if (on_dev) {
       h->cols.push_back(h->dev[cc].p);

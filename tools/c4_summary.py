@@ -85,7 +85,22 @@ def main():
         wb = write[key].get("WRITE_SIZE", 0.0) * 1024 if key in write else None
         rows.append({**l, "model_bytes": m, "fetch_bytes_x2": fb, "write_bytes": wb,
                      "traffic_over_model": (fb + wb) / m if fb is not None and wb is not None and m else None})
-    summary = {"bench": {k: bench[k] for k in ("metric", "value", "unit", "ms_per_step", "parity")},
+    # per-query PMC bytes of each scan kind (every launch of the kind in the profiled query): what
+    # bench.py reports as the dominant kind's measured traffic
+    kinds = {}
+    for r in rows:
+        k = kinds.setdefault(r["kind"], {"launches": 0, "fetch_bytes_x2": 0.0, "write_bytes": 0.0,
+                                          "model_bytes": 0.0, "complete": True})
+        k["launches"] += 1
+        k["model_bytes"] += r["model_bytes"]
+        if r["fetch_bytes_x2"] is None or r["write_bytes"] is None:
+            k["complete"] = False
+        else:
+            k["fetch_bytes_x2"] += r["fetch_bytes_x2"]
+            k["write_bytes"] += r["write_bytes"]
+    summary = {"bench": {**{k: bench[k] for k in ("metric", "value", "unit", "ms_per_step", "parity")},
+                         "config": {"workload": bench["config"]["workload"]}},
+               "query_kinds": kinds,
                "device_ms_per_query": bench["roofline"]["device_ms_per_query"],
                "kernels": stats, "launches": rows, "source": str(src)}
     out.with_suffix(".json").write_text(json.dumps(summary, indent=1))
