@@ -299,7 +299,7 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
         exp_bytes += tm["expand_bytes"]
         dev_ms += tm["total_ms"]
         iters = tm["steps_run"]
-    names = {2: "expand", 3: "probe", 4: "sweep"}
+    names = {2: "expand", 3: "probe", 4: "sweep", 5: "walk"}
     launches = [{"kind": names.get(h["mode_id"], h["mode"]), "ms": round(h["ms"], 4), "x": h["c"][0], "entries": h["c"][1],
                  "claims": h["c"][2], "iter": h["c"][4],
                  "kernel": h.get("kernels", ["?"])[0].replace("(anonymous namespace)::", "")} for h in tm["hops"]]
@@ -335,10 +335,12 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
     achieved = exp_bytes / (exp_ms / 1e3) / 1e9 if exp_ms > 0 else 0.0
     # dominant launch kind of one query (its rocprof kernel, the engine's byte models:
     # paths.hip timing.expand_bytes): expand / probe / sweep
-    kern = {"expand": "nbg::k_sp_expand", "probe": "nbg::k_sp_probe", "sweep": "nbg::k_sp_sweep"}
+    kern = {"expand": "nbg::k_sp_expand", "probe": "nbg::k_sp_probe", "sweep": "nbg::k_sp_sweep",
+            "walk": "nbg::k_dv_walk_scan"}
     model = {"expand": lambda l: l["x"] * 32 + l["entries"] * 5 + l["claims"] * 26,
              "probe": lambda l: l["x"] * 24 + l["entries"] * 5,
-             "sweep": lambda l: l["x"] * 32 + l["entries"] * 6 + l["claims"] * 18}
+             "sweep": lambda l: l["x"] * 32 + l["entries"] * 6 + l["claims"] * 18,
+             "walk": lambda l: l["x"] * 24 + l["entries"] * 5}
     by_kind = {}
     for l in launches:
         k = by_kind.setdefault(l["kind"], {"ms": 0.0, "bytes": 0.0, "launches": 0})

@@ -283,7 +283,8 @@ int32_t nbg_shortest_path(nbg_ctx* ctx, int32_t edge_type, const int64_t* src,
  * answered by L2, first-pass probes answered from the LDS hub copy}.
  * nbg_shortest_path records one entry per launch instead: mode 2 = BFS expansion, 3 = meet
  * probe, 4 = sweep; c[] = {tuples, adjacency entries, claims, meets so far, iteration,
- * active pairs, 0, 0}.                                                                      */
+ * active pairs, 0, 0}; 5 = walk scan (device-driven batches), c[] = {chunks, adjacency
+ * entries, 0, meets, walk step, 0, 0, 0}.                                                   */
 typedef struct {
   int32_t mode;
   int32_t final_hop;

@@ -84,6 +84,8 @@ struct SpState {  // per-pair arrays, B entries each
   unsigned long long* deg;  // [2][B] frontier sum of (degree + 1)
   int32_t B;
   int32_t vmajor;           // distance bytes vertex-major [v][pair] (else pair-major [pair][v])
+  int32_t ilv;              // 1: the two sides' bytes of a (pair, vertex) adjacent (d1 = d0 + 1, index
+                            // x 2): a claim reads its own and the other side's byte in one load
   // level filter (null: off): bit (v & lvmask) of level (side, l)'s lvw words is set when some
   // pair of the batch claimed vertex v at depth l on that side (1 <= l < kLv): a one-hash Bloom
   // filter of every pair's level-l set, at most 2^23 bits (1 MiB) a level so the level a launch
@@ -109,9 +111,10 @@ __device__ inline bool lv_maybe(const SpState& st, uint32_t side, int32_t l, uin
 
 // byte index of (pair p, vertex v) in a distance array.  Vertex-major keeps the bytes of all
 // pairs of one vertex in one cache line run, so hub neighbourhoods expanded by many pairs share
-// lines in L2 / the Infinity cache; pair-major keeps each pair's bytes contiguous.
+// lines in L2 / the Infinity cache; pair-major keeps each pair's bytes contiguous.  Interleaved
+// (ilv), the index doubles and side 1's array starts one byte after side 0's.
 __device__ inline uint64_t didx(const SpState& st, uint32_t p, uint64_t v, int64_t n) {
-  return st.vmajor ? v * uint64_t(st.B) + p : uint64_t(p) * uint64_t(n) + v;
+  return (st.vmajor ? v * uint64_t(st.B) + p : uint64_t(p) * uint64_t(n) + v) << st.ilv;
 }
 
 struct SpBufs {
@@ -156,8 +159,10 @@ __device__ inline void put(uint64_t* list, int64_t cap, unsigned long long* cnt,
 // claim the unseen (0xFF) distance byte idx with val: true for exactly one caller
 __device__ inline bool claim_byte(uint8_t* base, uint64_t idx, uint32_t val) {
   if (base[idx] != 0xFF) return false;  // already seen (values only leave 0xFF within a batch)
-  uint32_t* w = reinterpret_cast<uint32_t*>(base + (idx & ~uint64_t(3)));
-  const uint32_t sh = uint32_t(idx & 3) * 8;
+  // the aligned word holding the byte (the base itself may be odd: the interleaved side 1)
+  const uintptr_t a = reinterpret_cast<uintptr_t>(base + idx);
+  uint32_t* w = reinterpret_cast<uint32_t*>(a & ~uintptr_t(3));
+  const uint32_t sh = uint32_t(a & 3) * 8;
   uint32_t old = *reinterpret_cast<volatile uint32_t*>(w);
   while (((old >> sh) & 0xFFu) == 0xFFu) {
     const uint32_t nw = (old & ~(0xFFu << sh)) | (val << sh);
@@ -1470,7 +1475,8 @@ __global__ __launch_bounds__(256) void k_dv_begin(SpDev d, SpState st, SpCsr gou
                                                   int32_t ht_min_gidx) {
   const int32_t B = st.B;
   const int64_t gt = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, gn = int64_t(gridDim.x) * blockDim.x;
-  for (int64_t i = gt; i < int64_t(2) * kMaxQ * B; i += gn) d.pull[i] = 0ull;  // pull and push adjacent
+  // pull and push adjacent, 64-byte aligned, 2 kMaxQ B words: 16-byte stores
+  for (int64_t i = gt; i < int64_t(kMaxQ) * B; i += gn) reinterpret_cast<uint4*>(d.pull)[i] = make_uint4(0u, 0u, 0u, 0u);
   bool go = false;
   int32_t a = -1, b = -1;
   if (gt < B) {
@@ -1499,13 +1505,30 @@ __global__ __launch_bounds__(256) void k_dv_begin(SpDev d, SpState st, SpCsr gou
     }
     st.state[p] = go ? SP_ACTIVE : SP_DONE;
   }
+  // the batch's first writer of the lists and the arena (their counters start at 0): pair k of
+  // the active ones takes slot k of both live lists and arena slots 2k, 2k + 1, so one returning
+  // atomic (the active count) places all four tuples
   const uint32_t pp = uint32_t(gt);
   unsigned long long* q0 = qblk(d.cnt, 0);
-  dput(d.live[0][0], d.cap_live, q0 + Q_LIVE0, d.cnt, go, mk_tup(0, pp, 0, uint32_t(a)));
-  dput(d.live[0][1], d.cap_live, q0 + Q_LIVE1, d.cnt, go, mk_tup(1, pp, 0, uint32_t(b)));
-  dput(d.arena, d.cap_arena, d.cnt + D_ARENA, d.cnt, go, mk_tup(0, pp, 0, uint32_t(a)));
-  dput(d.arena, d.cap_arena, d.cnt + D_ARENA, d.cnt, go, mk_tup(1, pp, 0, uint32_t(b)));
-  (void)wave_append(q0 + Q_ACTIVE, go);
+  const int64_t k = wave_append(q0 + Q_ACTIVE, go);
+  if (go) {
+    if (k < d.cap_live) {
+      d.live[0][0][k] = mk_tup(0, pp, 0, uint32_t(a));
+      d.live[0][1][k] = mk_tup(1, pp, 0, uint32_t(b));
+    }
+    if (2 * k + 1 < d.cap_arena) {
+      d.arena[2 * k] = mk_tup(0, pp, 0, uint32_t(a));
+      d.arena[2 * k + 1] = mk_tup(1, pp, 0, uint32_t(b));
+    }
+    if (k >= d.cap_live || 2 * k + 1 >= d.cap_arena) atomicOr(d.cnt + D_OVF, 1ull);
+  }
+  const uint64_t m = __ballot(go);
+  if ((threadIdx.x & 63) == 0 && m) {
+    const unsigned long long nw = (unsigned long long)__popcll(m);
+    atomicAdd(q0 + Q_LIVE0, nw);
+    atomicAdd(q0 + Q_LIVE1, nw);
+    atomicAdd(d.cnt + D_ARENA, 2 * nw);
+  }
 }
 
 // BFS iteration it, first launch: the live lists of iteration it - 1 -> X (tuples of the side
@@ -1514,6 +1537,7 @@ __global__ __launch_bounds__(256) void k_dv_begin(SpDev d, SpState st, SpCsr gou
 __global__ __launch_bounds__(kBlk) void k_dv_select(SpDev d, SpState st, SpCsr gout, SpCsr gin, int32_t it) {
   unsigned long long* qp = qblk(d.cnt, it - 1);
   unsigned long long* q = qblk(d.cnt, it);
+  if (qp[Q_ACTIVE] == 0) return;  // the BFS ended (a speculative iteration): nothing selected
   const int64_t n0 = min(int64_t(qp[Q_LIVE0]), d.cap_live), n1 = min(int64_t(qp[Q_LIVE1]), d.cap_live);
   const int64_t nl = n0 + n1;
   const uint64_t* in0 = d.live[(it - 1) & 1][0];
@@ -1540,10 +1564,6 @@ __global__ __launch_bounds__(kBlk) void k_dv_select(SpDev d, SpState st, SpCsr g
       const int64_t i = i0 + u * kBlk;
       t[u] = i < n0 ? in0[i] : i < nl ? in1[i - n0] : ~0ull;
     }
-    // every tuple's degree in flight with the table lookups (the carried ones' unused)
-    int64_t dg[kSelIt];
-#pragma unroll
-    for (int u = 0; u < kSelIt; u++) dg[u] = t[u] != ~0ull ? sp_deg(t_side(t[u]) ? gin : gout, t_row(t[u])) : 0;
     uint32_t xm = 0, cm0 = 0, cm1 = 0;
 #pragma unroll
     for (int u = 0; u < kSelIt; u++) {
@@ -1555,10 +1575,13 @@ __global__ __launch_bounds__(kBlk) void k_dv_select(SpDev d, SpState st, SpCsr g
       else if (ts) cm1 |= 1u << u;
       else cm0 |= 1u << u;
     }
+    // the degrees of the tuples that expand (a carried tuple's row is not read)
+    int64_t dg[kSelIt];
+#pragma unroll
+    for (int u = 0; u < kSelIt; u++) dg[u] = (xm >> u) & 1u ? sp_deg(t_side(t[u]) ? gin : gout, t_row(t[u])) : 0;
     uint32_t nch = 0;
 #pragma unroll
     for (int u = 0; u < kSelIt; u++) {
-      if (!((xm >> u) & 1u)) dg[u] = 0;
       if (dg[u] == 0) xm &= ~(1u << u);  // nothing to scan
       nch += uint32_t((dg[u] + (int64_t(1) << d.lg_chb) - 1) >> d.lg_chb);
       esum += (unsigned long long)dg[u];
@@ -1665,17 +1688,22 @@ __device__ inline void col_step(const int32_t* col, int64_t x, int64_t x0, int64
 }
 __device__ inline int64_t step_start(int64_t x0) { return x0 & ~int64_t(3); }
 
-// the X chunk c's row slice [x0, x1) (2^lg_ch entries; sub-chunk s of 2^lg_sub)
-__device__ inline bool x_chunk(const SpDev& d, const SpCsr& g0, const SpCsr& g1, int64_t c, int32_t lg_ch, int32_t lg_sub,
-                               int64_t s, ChunkRec& r) {
-  const int32_t a = d.chx[c];
-  r.t = d.X[a];
+// the X chunk c's row slice [x0, x1) (2^lg_ch entries; sub-chunk s of 2^lg_sub) for its X entry a
+// holding tuple t
+__device__ inline bool x_chunk_at(const SpDev& d, const SpCsr& g0, const SpCsr& g1, int64_t c, int32_t a, uint64_t t,
+                                  int32_t lg_ch, int32_t lg_sub, int64_t s, ChunkRec& r) {
+  r.t = t;
   const SpCsr& g = t_side(r.t) ? g1 : g0;
   const uint32_t row = t_row(r.t);
   const int64_t re = g.row_ptr[row + 1];
   r.x0 = g.row_ptr[row] + ((c - d.Xcb[a]) << lg_ch) + (s << (lg_ch - lg_sub));
   r.x1 = min(r.x0 + (int64_t(1) << (lg_ch - lg_sub)), re);
   return r.x0 < r.x1;
+}
+__device__ inline bool x_chunk(const SpDev& d, const SpCsr& g0, const SpCsr& g1, int64_t c, int32_t lg_ch, int32_t lg_sub,
+                               int64_t s, ChunkRec& r) {
+  const int32_t a = d.chx[c];
+  return x_chunk_at(d, g0, g1, c, a, d.X[a], lg_ch, lg_sub, s, r);
 }
 
 // BFS iteration it, meet probe: one wave per chunk of an X tuple's row, stopping at the first
@@ -1689,6 +1717,7 @@ __global__ __launch_bounds__(256) void k_dv_probe(SpDev d, SpState st, SpFilt f,
   const int lane = threadIdx.x & 63;
   unsigned long long* q = qblk(d.cnt, it);
   const int64_t total = min(int64_t(q[Q_NCH]), d.cap_ch);
+  if (total == 0) return;  // nothing selected (grid-uniform)
   const uint32_t B = uint32_t(st.B);
   unsigned long long examined = 0;
   chunk_groups(
@@ -1704,7 +1733,8 @@ __global__ __launch_bounds__(256) void k_dv_probe(SpDev d, SpState st, SpFilt f,
         const uint32_t side = t_side(r.t), p = t_pair(r.t), row = t_row(r.t), o = side ^ 1u;
         const int32_t* col = side ? g1.col : g0.col;
         const int32_t need = r.a0;
-        uint8_t* const odp = (o ? d1 : d0) + uint64_t(p) * uint64_t(n);  // the pair's bytes (pair-major)
+        const uint32_t sh = uint32_t(st.ilv);
+        uint8_t* const odp = (o ? d1 : d0) + ((uint64_t(p) * uint64_t(n)) << sh);  // the pair's bytes (pair-major)
         bool pf_on;
         const uint2 prow = pf_load(f, o, need, p, pf_on);
         // the next step's columns are loaded before this step's tests wait on their filter and
@@ -1712,7 +1742,8 @@ __global__ __launch_bounds__(256) void k_dv_probe(SpDev d, SpState st, SpFilt f,
         uint32_t wn[U];
         col_step<U>(col, step_start(r.x0), r.x0, r.x1, lo, wn);
         for (int64_t x = step_start(r.x0); x < r.x1; x += 64 * U) {
-          if (uint32_t(*reinterpret_cast<volatile const uint8_t*>(odp + row)) != 0xFFu) break;  // another chunk claimed r
+          if (uint32_t(*reinterpret_cast<volatile const uint8_t*>(odp + (uint64_t(row) << sh))) != 0xFFu)
+            break;  // another chunk claimed r
           uint32_t w[U];
 #pragma unroll
           for (int u = 0; u < U; u++) w[u] = wn[u];
@@ -1729,11 +1760,12 @@ __global__ __launch_bounds__(256) void k_dv_probe(SpDev d, SpState st, SpFilt f,
               fm |= (w[u] != 0xFFFFFFFFu && pv && gf_test(f, o, need, p, w[u])) ? 1u << u : 0u;
             }
 #pragma unroll
-            for (int u = 0; u < U; u++) hit = (((fm >> u) & 1u) && uint32_t(odp[w[u]]) == uint32_t(need)) || hit;
+            for (int u = 0; u < U; u++)
+              hit = (((fm >> u) & 1u) && uint32_t(odp[uint64_t(w[u]) << sh]) == uint32_t(need)) || hit;
           }
           examined += uint64_t(min(x + 64 * U, r.x1) - max(x, r.x0)) * (lane == 0);
           if (__ballot(hit)) {
-            if (lane == 0 && claim_byte(odp, row, uint32_t(need + 1))) {
+            if (lane == 0 && claim_byte(odp, uint64_t(row) << sh, uint32_t(need + 1))) {
               filt_mark(f, o, uint32_t(need + 1), p, row);
               st.met[p] = -1;
               d.slot[c] = mk_tup(o, p, uint32_t(need + 1), row);
@@ -1834,6 +1866,7 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
   const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
   unsigned long long* q = qblk(d.cnt, it);
   const int64_t total = min(int64_t(q[Q_NCH]), d.cap_ch);
+  if (total == 0) return;  // nothing selected (grid-uniform)
   const uint32_t B = uint32_t(st.B);
   uint64_t* const out0 = d.live[it & 1][0];
   uint64_t* const out1 = d.live[it & 1][1];
@@ -1842,34 +1875,55 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
   chunk_groups(
       total << lg_sub,
       [&](int64_t vc, ChunkRec& r) {
-        if (!x_chunk(d, g0, g1, vc >> lg_sub, d.lg_chb, lg_sub, vc & ((int64_t(1) << lg_sub) - 1), r)) return false;
-        return st.met[t_pair(r.t)] != -1;  // the probe finished the pair
+        // a pair the probe finished (met = -1) is dropped before its row bounds are loaded
+        const int64_t c = vc >> lg_sub;
+        const int32_t a = d.chx[c];
+        const uint64_t t = d.X[a];
+        if (st.met[t_pair(t)] == -1) return false;
+        return x_chunk_at(d, g0, g1, c, a, t, d.lg_chb, lg_sub, vc & ((int64_t(1) << lg_sub) - 1), r);
       },
       [&](const ChunkRec& r, int64_t) {
         const uint32_t side = t_side(r.t), p = t_pair(r.t), l = t_lvl(r.t);
         const SpCsr& g = side ? g1 : g0;
-        uint8_t* const sdp = (side ? d1 : d0) + uint64_t(p) * uint64_t(n);  // the pair's bytes (pair-major)
-        const uint8_t* const odp = (side ? d0 : d1) + uint64_t(p) * uint64_t(n);
+        const uint32_t sh = uint32_t(st.ilv);
+        uint8_t* const sdp = (side ? d1 : d0) + ((uint64_t(p) * uint64_t(n)) << sh);  // the pair's bytes (pair-major)
+        const uint8_t* const odp = (side ? d0 : d1) + ((uint64_t(p) * uint64_t(n)) << sh);
+        // interleaved: both sides' bytes of a vertex in one 2-byte load (the other side's bytes do
+        // not change during an expansion: only the expanding side of a pair is written)
+        const uint16_t* const bdp = reinterpret_cast<const uint16_t*>(d0 + ((uint64_t(p) * uint64_t(n)) << 1));
         entries += uint64_t(r.x1 - r.x0) * (lane == 0);
         unsigned long long dsum = 0;
         for (int64_t x = step_start(r.x0); x < r.x1; x += 64 * kProbeU) {
           uint32_t w[kProbeU];
           col_step(g.col, x, r.x0, r.x1, lo, w);
-          uint32_t bt[kProbeU];
+          uint32_t bt[kProbeU], obt[kProbeU];
 #pragma unroll
-          for (int u = 0; u < kProbeU; u++) bt[u] = w[u] != 0xFFFFFFFFu ? uint32_t(sdp[w[u]]) : 0x1FFu;
+          for (int u = 0; u < kProbeU; u++) {
+            bt[u] = 0x1FFu;
+            obt[u] = 0xFFu;
+            if (w[u] != 0xFFFFFFFFu) {
+              if (sh) {
+                const uint32_t both = bdp[w[u]];
+                bt[u] = side ? both >> 8 : both & 0xFFu;
+                obt[u] = side ? both & 0xFFu : both >> 8;
+              } else {
+                bt[u] = sdp[w[u]];
+              }
+            }
+          }
 #pragma unroll
           for (int u = 0; u < kProbeU; u++) {
             // a claim: the CAS (option sp_dv_cas) or a plain byte store (the default: two chunks of one
             // pair reaching the same vertex in this level may both list it; the byte holds l + 1 either
             // way, and a duplicate tuple only repeats work)
-            const bool cl = bt[u] == 0xFFu && (cas ? claim_byte(sdp, w[u], l + 1) : (sdp[w[u]] = uint8_t(l + 1), true));
+            const uint64_t wi = uint64_t(w[u]) << sh;
+            const bool cl = bt[u] == 0xFFu && (cas ? claim_byte(sdp, wi, l + 1) : (sdp[wi] = uint8_t(l + 1), true));
             bool meet = false;
             uint32_t dt = 0;
             if (cl) {
               filt_mark(f, side, l + 1, p, w[u]);
               dsum += (unsigned long long)sp_deg(g, w[u]) + 1;
-              const uint32_t ob = odp[w[u]];
+              const uint32_t ob = sh ? obt[u] : uint32_t(odp[w[u]]);
               if (ob != 0xFFu) {
                 meet = true;
                 dt = side ? l + 1 : ob;
@@ -2176,8 +2230,9 @@ __global__ __launch_bounds__(256) void k_dv_sweep(SpDev d, SpState st, SpFilt f,
         const int32_t* col = side ? gin.col : gout.col;
         const int32_t L = r.a0;
         const int32_t need = L - int32_t(l) - 1;  // the other side's depth a neighbour needs
-        const uint8_t* const odp = (side ? d0 : d1) + uint64_t(p) * uint64_t(n);  // the pair's bytes (pair-major)
-        uint8_t* const d1p = d1 + uint64_t(p) * uint64_t(n);
+        const uint32_t sh = uint32_t(st.ilv);
+        const uint8_t* const odp = (side ? d0 : d1) + ((uint64_t(p) * uint64_t(n)) << sh);  // the pair's bytes
+        uint8_t* const d1p = d1 + ((uint64_t(p) * uint64_t(n)) << sh);
         bool pf_on;
         const uint2 prow = pf_load(f, os, need, p, pf_on);
         entries += uint64_t(r.x1 - r.x0) * (lane == 0);
@@ -2185,7 +2240,8 @@ __global__ __launch_bounds__(256) void k_dv_sweep(SpDev d, SpState st, SpFilt f,
         uint32_t wn[U];  // the next step's columns (see the probe)
         col_step<U>(col, step_start(r.x0), r.x0, r.x1, lo, wn);
         for (int64_t x = step_start(r.x0); x < r.x1; x += 64 * U) {
-          if (side == 0 && *reinterpret_cast<volatile const uint8_t*>(d1p + row) != 0xFFu) break;  // u claimed
+          if (side == 0 && *reinterpret_cast<volatile const uint8_t*>(d1p + (uint64_t(row) << sh)) != 0xFFu)
+            break;  // u claimed
           uint32_t w[U];
 #pragma unroll
           for (int u = 0; u < U; u++) w[u] = wn[u];
@@ -2204,13 +2260,13 @@ __global__ __launch_bounds__(256) void k_dv_sweep(SpDev d, SpState st, SpFilt f,
             if (f.diag & 3) fm = (f.diag & 1) ? 0u : (__ballot(fm != 0) ? 0u : fm);
 #pragma unroll
             for (int u = 0; u < U; u++)
-              hm |= ((fm >> u) & 1u) && uint32_t(odp[w[u]]) == uint32_t(need) ? 1u << u : 0u;
+              hm |= ((fm >> u) & 1u) && uint32_t(odp[uint64_t(w[u]) << sh]) == uint32_t(need) ? 1u << u : 0u;
           }
           if (__ballot(hm != 0) == 0) continue;
           if (side == 1) {
 #pragma unroll
             for (int u = 0; u < U; u++) {
-              const bool cl = ((hm >> u) & 1u) && claim_byte(d1p, w[u], l + 1);
+              const bool cl = ((hm >> u) & 1u) && claim_byte(d1p, uint64_t(w[u]) << sh, l + 1);
               if (cl) {
                 filt_mark(f, 1, l + 1, p, w[u]);
                 if (int32_t(l + 1) < L - 1) pc += (unsigned long long)sp_deg(gin, w[u]) + 1;
@@ -2220,7 +2276,7 @@ __global__ __launch_bounds__(256) void k_dv_sweep(SpDev d, SpState st, SpFilt f,
           } else {
             bool cl = false;
             if (lane == 0) {
-              cl = claim_byte(d1p, row, uint32_t(need + 1));
+              cl = claim_byte(d1p, uint64_t(row) << sh, uint32_t(need + 1));
               if (cl) {
                 filt_mark(f, 1, uint32_t(need + 1), p, row);
                 if (need + 1 < L - 1) pc += (unsigned long long)sp_deg(gin, row) + 1;
@@ -2247,6 +2303,7 @@ __global__ __launch_bounds__(256) void k_dv_walk_scan(SpDev d, SpState st, SpFil
   const int lane = threadIdx.x & 63;
   unsigned long long* q = qblk(d.cnt, kWkQ + i);
   const int64_t total = min(int64_t(q[Q_NCH]), d.cap_wch);
+  unsigned long long entries = 0;
   chunk_groups(
       total,
       [&](int64_t c, ChunkRec& r) {
@@ -2262,9 +2319,11 @@ __global__ __launch_bounds__(256) void k_dv_walk_scan(SpDev d, SpState st, SpFil
       [&](const ChunkRec& r, int64_t) {
         const uint32_t p = uint32_t(r.t);
         const int32_t need = r.a0;
+        entries += uint64_t(r.x1 - r.x0) * (lane == 0);
         bool pf_on;
         const uint2 prow = pf_load(f, 1, need, p, pf_on);
-        const uint8_t* const d1p = d1 + uint64_t(p) * uint64_t(n);  // the pair's bytes (pair-major)
+        const uint32_t sh = uint32_t(st.ilv);
+        const uint8_t* const d1p = d1 + ((uint64_t(p) * uint64_t(n)) << sh);  // the pair's bytes (pair-major)
         long long bm = LLONG_MAX;
         // the next step's columns are loaded before this step's tests wait on their filter and
         // byte loads (one round trip less per step of the chain)
@@ -2283,7 +2342,7 @@ __global__ __launch_bounds__(256) void k_dv_walk_scan(SpDev d, SpState st, SpFil
           }
 #pragma unroll
           for (int u = 0; u < kProbeU; u++)
-            if (((fm >> u) & 1u) && uint32_t(d1p[w[u]]) == uint32_t(need)) {
+            if (((fm >> u) & 1u) && uint32_t(d1p[uint64_t(w[u]) << sh]) == uint32_t(need)) {
               const long long vv = vid_of[lo + w[u]];
               bm = vv < bm ? vv : bm;
             }
@@ -2295,6 +2354,7 @@ __global__ __launch_bounds__(256) void k_dv_walk_scan(SpDev d, SpState st, SpFil
         }
         if (lane == 0 && bm != LLONG_MAX) atomicMin(d.best + p, bm);
       });
+  blk_add(q + Q_EE, entries);
 }
 
 __global__ __launch_bounds__(kBlk) void k_dv_walk_front(SpDev d, SpState st, SpCsr gout, int32_t i, int64_t lo,
@@ -2331,25 +2391,21 @@ __global__ __launch_bounds__(256) void k_dv_out(SpDev d, SpState st, int32_t ila
   __threadfence_system();
 }
 
-// every claimed distance byte of the batch and its filter words reset from the arena (after the
-// finish publication: the host reads the results while this runs; D_CLEAR holds the arena length)
+// every claimed distance byte of the batch reset from the arena, and the filters zeroed whole --
+// the batch's pair rows (2 kLv B x 512 B) and the global filter are a few MB of streaming stores,
+// cheaper than a random store per claim (after the finish publication: the host reads the results
+// while this runs; D_CLEAR holds the arena length)
 __global__ __launch_bounds__(256) void k_dv_clear(SpDev d, SpState st, SpFilt f, uint8_t* d0, uint8_t* d1, int64_t n) {
-  const uint32_t B = uint32_t(st.B);
   const int64_t gt = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, gn = int64_t(gridDim.x) * blockDim.x;
+  const int64_t pf4 = f.pf ? int64_t(2 * kLv) * st.B * 32 : 0;          // uint4 groups of the pair rows
+  const int64_t gf4 = f.gf ? (int64_t(1) << (64 - f.gshift)) / 4 : 0;  // uint4 groups of the global filter
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (int64_t i = gt; i < pf4; i += gn) reinterpret_cast<uint4*>(f.pf)[i] = z;
+  for (int64_t i = gt; i < gf4; i += gn) reinterpret_cast<uint4*>(f.gf)[i] = z;
   const int64_t na = min(int64_t(d.cnt[D_CLEAR]), d.cap_arena);
   for (int64_t i = gt; i < na; i += gn) {
     const uint64_t t = d.arena[i];
-    const uint32_t side = t_side(t), p = t_pair(t), l = t_lvl(t), v = t_row(t);
-    (side ? d1 : d0)[didx(st, p, v, n)] = 0xFF;
-    if (l >= 1 && l < uint32_t(kLv)) {
-      const uint32_t sl = side * kLv + l;
-      if (f.pf) {
-        uint32_t* row = f.pf + (size_t(sl) * B + p) * 128;
-        row[pf_bit(v) >> 5] = 0u;
-        if (f.k2) row[pf_bit2(v) >> 5] = 0u;
-      }
-      if (f.gf) f.gf[gf_hash(sl, p, v) >> f.gshift] = 0u;
-    }
+    (t_side(t) ? d1 : d0)[didx(st, t_pair(t), t_row(t), n)] = 0xFF;
   }
 }
 
@@ -2564,16 +2620,19 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   B = std::min<int64_t>(B, 0x7FFFFF);
   const size_t dist_bytes = ((size_t(B) * size_t(n) + 3) & ~size_t(3)) + 64;
   {
+    // both sides' distance arrays in one block of 2 x dist_bytes: side 1 in its upper half, or
+    // (option sp_ilv, default) interleaved with side 0 byte by byte.  Either layout is all 0xFF
+    // between batches, so the option may change from call to call.
     PoolScope none(nullptr);  // the distance arrays live outside the query pool
     if (c.sp_dist_bytes < dist_bytes) {
       for (auto& d : c.sp_dist) d.release();
       c.sp_dist_bytes = 0;
-      for (auto& d : c.sp_dist) d.alloc(dist_bytes);
+      c.sp_dist[0].alloc(2 * dist_bytes);
       c.sp_dist_bytes = dist_bytes;
       c.sp_dirty = true;
     }
     if (c.sp_dirty) {
-      for (auto& d : c.sp_dist) NBG_HIP(hipMemsetAsync(d.p, 0xFF, c.sp_dist_bytes, c.stream));
+      NBG_HIP(hipMemsetAsync(c.sp_dist[0].p, 0xFF, 2 * c.sp_dist_bytes, c.stream));
       c.sp.dv_clean = false;  // a failed call may have left filter words and counters set too
     }
     c.sp_dirty = false;
@@ -2594,8 +2653,9 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   c.hop_timing = c.opt("hop_timing", 1) != 0;  // event pairs around the scan launches (0: none)
   hipEventRecord(c.ev[0], c.stream);
 
+  const int32_t ilv = c.opt("sp_ilv", 1) != 0 ? 1 : 0;
   uint8_t* d0 = c.sp_dist[0].as<uint8_t>();
-  uint8_t* d1 = c.sp_dist[1].as<uint8_t>();
+  uint8_t* d1 = ilv ? d0 + 1 : d0 + c.sp_dist_bytes;
   SpCsr gout{cout->row_ptr.as<int64_t>(), cout->col.as<int32_t>(), cout->row_ok.as<uint8_t>()};
   SpCsr gin{cin->row_ptr.as<int64_t>(), cin->col.as<int32_t>(), cin->row_ok.as<uint8_t>()};
   const int64_t* vid_of = c.vid_of.as<int64_t>();
@@ -2718,6 +2778,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     st.pside = st.side + nb;
     st.met = st.pside + nb;
     st.vmajor = int32_t(c.opt("sp_vmajor", 0));
+    st.ilv = ilv;
     SpFilt f{};
     f.pf = W.dv_pf.as<uint32_t>();
     f.gf = W.dv_gf.as<uint32_t>();
@@ -2799,6 +2860,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     std::vector<uint64_t> seq(size_t(kMaxQ), 0);
     std::vector<std::array<size_t, 3>> evi(size_t(kMaxQ), {~size_t(0), ~size_t(0), ~size_t(0)});
     std::vector<std::array<size_t, 2>> evs(size_t(kMaxQ), {~size_t(0), ~size_t(0)});
+    std::vector<std::array<size_t, 2>> evw(size_t(kMaxQ), {~size_t(0), ~size_t(0)});
 
     // the state is restored from whatever the device reached: the claimed bytes from the arena
     // (wholesale when it overflowed, or `wipe`), every filter word and counter cleared; the batch
@@ -2810,8 +2872,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       if (!wipe && int64_t(na) <= d.cap_arena) {
         if (na) k_sp_clear<<<grid_n(int64_t(na)), 256, 0, c.stream>>>(d.arena, int64_t(na), d0, d1, n, st);
       } else {
-        const size_t used = ((size_t(nb) * size_t(n) + 3) & ~size_t(3)) + 64;
-        for (auto& dd : c.sp_dist) NBG_HIP(hipMemsetAsync(dd.p, 0xFF, std::min(used, c.sp_dist_bytes), c.stream));
+        NBG_HIP(hipMemsetAsync(c.sp_dist[0].p, 0xFF, 2 * c.sp_dist_bytes, c.stream));
       }
       NBG_HIP(hipMemsetAsync(W.dv_cnt.p, 0, W.dv_cnt.bytes, c.stream));
       if (W.dv_pf.p) NBG_HIP(hipMemsetAsync(W.dv_pf.p, 0, W.dv_pf.bytes, c.stream));
@@ -2822,7 +2883,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       return false;
     };
 
-    k_dv_begin<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(d, st, gout, gin, d0, d1, n, max_steps, htk, htv,
+    k_dv_begin<<<std::max(grid_n(nb, 1 << 20), 64), 256, 0, c.stream>>>(d, st, gout, gin, d0, d1, n, max_steps, htk, htv,
                                                           uint64_t(htm), c.ht_has_min, c.ht_min_gidx);
     auto enqueue = [&](int it) {
       k_dv_select<<<gsel((const void*)k_dv_select), kBlk, 0, c.stream>>>(d, st, gout, gin, it);
@@ -2878,7 +2939,9 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       if (i > 0)
         k_dv_walk_front<<<grid_n(nb, 1 << 20), kBlk, 0, c.stream>>>(d, st, gout, i, lo, htk, htv, uint64_t(htm),
                                                                    c.ht_has_min, c.ht_min_gidx);
+      evw[size_t(i)][0] = dv_event();
       k_dv_walk_scan<<<gsz((const void*)k_dv_walk_scan), 256, 0, c.stream>>>(d, st, f, gout, d1, vid_of, n, lo, i);
+      evw[size_t(i)][1] = dv_event();
     }
     k_dv_out<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(d, st, nwalk - 1);
     const uint64_t fseq = ++c.pub_seq;
@@ -2939,6 +3002,19 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       c.timing.hop(4, false, sms, c8);
       c.timing.name_last_hop("nbg::(anonymous namespace)::k_dv_sweep");
     }
+    // walk scans (mode 5): the out-rows of every walking pair's current vertex; not counted in
+    // edges_scanned (the traversal's entries), in the scan kernels' time and bytes
+    for (int i = 0; i < nwalk; i++) {
+      const unsigned long long* q = blkq(kWkQ + i);
+      if (!q[Q_EE]) continue;
+      const double wms = dv_ms(evw[size_t(i)][0], evw[size_t(i)][1]);
+      c.timing.expand_ms += wms;
+      c.timing.expand_launches++;
+      c.timing.expand_bytes += q[Q_NCH] * 24 + q[Q_EE] * 5;
+      const unsigned long long c8[8] = {q[Q_NCH], q[Q_EE], 0, fin[D_MEET], (unsigned long long)i, 0, 0, 0};
+      c.timing.hop(5, false, wms, c8);
+      c.timing.name_last_hop("nbg::(anonymous namespace)::k_dv_walk_scan");
+    }
 
     // results (the ends of each path are the host's)
     const int32_t* hsr = d.h_sr;
@@ -2975,6 +3051,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     st.pside = st.side + nb;
     st.met = st.pside + nb;
     st.vmajor = int32_t(c.opt("sp_vmajor", 0));
+    st.ilv = ilv;
     if (c.opt("sp_lvbits", 1) != 0) {  // level filter: 2 * kLv maps, cleared per batch
       // bits per level: the power of two >= n, capped (option sp_lvbits_log2, default 23)
       const int cap = int(std::min<int64_t>(std::max<int64_t>(c.opt("sp_lvbits_log2", 23), 5), 31));
@@ -3463,8 +3540,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     }
     // reset the batch's distance bytes
     if (arena_lost) {
-      const size_t used = ((size_t(nb) * size_t(n) + 3) & ~size_t(3)) + 64;
-      for (auto& d : c.sp_dist) NBG_HIP(hipMemsetAsync(d.p, 0xFF, std::min(used, c.sp_dist_bytes), c.stream));
+      NBG_HIP(hipMemsetAsync(c.sp_dist[0].p, 0xFF, 2 * c.sp_dist_bytes, c.stream));
     } else if (n_arena) {
       k_sp_clear<<<grid_n(n_arena), 256, 0, c.stream>>>(W.arena.as<uint64_t>(), n_arena, d0, d1, n, st);
       NBG_HIP(hipGetLastError());

@@ -272,7 +272,7 @@ class GraphSpace:
         t = _lib.Timing()
         self._check(self.L.nbg_last_timing(self.h, C.byref(t)))
         d = {k: getattr(t, k) for k, _ in t._fields_ if k not in ("hops", "n_hops")}
-        modes = {0: "top-down", 1: "bottom-up", 2: "sp-expand", 3: "sp-probe", 4: "sp-sweep"}
+        modes = {0: "top-down", 1: "bottom-up", 2: "sp-expand", 3: "sp-probe", 4: "sp-sweep", 5: "sp-walk"}
         d["hops"] = [{"mode": modes.get(h.mode, h.mode), "mode_id": h.mode, "final": bool(h.final_hop), "ms": h.ms,
                       "bytes": int(h.bytes), "c": list(h.c), "kernel_ms": h.kernel_ms,
                       "kernel_bytes": int(h.kernel_bytes),

@@ -187,6 +187,31 @@ def test_meet_probe_on_and_off_match_oracle(rmat, probe, vmajor):
         sp.set_option("sp_vmajor", 0)
 
 
+@pytest.mark.parametrize("dev,ilv,vmajor", [(1, 1, 0), (1, 0, 0), (0, 1, 0), (0, 0, 0), (0, 1, 1), (0, 0, 1)])
+def test_distance_layouts_match_oracle(rmat, dev, ilv, vmajor):
+    """the distance bytes interleaved by side (sp_ilv: one 2-byte load reads both sides of a vertex)
+    or in two separate halves, pair-major or vertex-major, device-driven or host-driven: the
+    oracle's paths; the layout switched between calls leaves the bytes clean (all unseen)"""
+    scale, sp, st = rmat
+    s, t = synth.pairs(scale, 16, 1, 300, pick_seed=31)
+    es, et_ = edge_case_pairs(scale)
+    src, dst = np.concatenate([s, es]), np.concatenate([t, et_])
+    try:
+        for lay in (ilv, 1 - ilv, ilv):
+            sp.set_option("sp_dev", dev)
+            sp.set_option("sp_ilv", lay)
+            sp.set_option("sp_vmajor", vmajor)
+            for max_steps in (2, 8):
+                got = sp.shortest_path(src, dst, FOLLOW, max_steps).rows()
+                assert got == oracle_paths(st, src, dst, FOLLOW, max_steps), (lay, max_steps)
+            if dev and not vmajor:
+                assert sp.last_timing()["spec_hops"] >= 1  # the batches ran device-driven
+    finally:
+        sp.set_option("sp_dev", 1)
+        sp.set_option("sp_ilv", 1)
+        sp.set_option("sp_vmajor", 0)
+
+
 @pytest.mark.parametrize("push,walk_wg,sweep_src", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 0, 1), (1, 0, 1)])
 def test_sweep_direction_and_walk_variants(rmat, push, walk_wg, sweep_src):
     """the sweep's per-pair push/pull choice (forced off: pull only), the workgroup-per-pair walk

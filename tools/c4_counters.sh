@@ -15,7 +15,7 @@ bash tools/pmc_passes.sh $out/pmc "FETCH_SIZE" "WRITE_SIZE" \
   "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum" \
   "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TA_BUSY_avr" \
   -- bench.py --no-cpu --workload paths --steps 1 --warmup 1 "$@"
-python3 tools/pmc_summary.py --dispatch 'k_(sp|dv)_(sweep|probe|expand)' $(find $out/pmc -name "*counter_collection.csv" | sort) \
+python3 tools/pmc_summary.py --dispatch 'k_(sp|dv)_(sweep|probe|expand|walk_scan)' $(find $out/pmc -name "*counter_collection.csv" | sort) \
   > $out/pmc/dispatch.txt
 find $out/pmc -name "*.db" -delete 2>/dev/null || true
 echo done

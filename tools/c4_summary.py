@@ -17,8 +17,9 @@ from pathlib import Path
 
 MODEL = {"probe": lambda l: l["x"] * 24 + l["entries"] * 5,
          "expand": lambda l: l["x"] * 32 + l["entries"] * 5 + l["claims"] * 26,
-         "sweep": lambda l: l["x"] * 32 + l["entries"] * 6 + l["claims"] * 18}
-KIND = {"k_dv_probe": "probe", "k_dv_expand": "expand", "k_dv_sweep": "sweep",
+         "sweep": lambda l: l["x"] * 32 + l["entries"] * 6 + l["claims"] * 18,
+         "walk": lambda l: l["x"] * 24 + l["entries"] * 5}
+KIND = {"k_dv_probe": "probe", "k_dv_expand": "expand", "k_dv_sweep": "sweep", "k_dv_walk_scan": "walk",
         "k_sp_probe": "probe", "k_sp_expand": "expand", "k_sp_sweep": "sweep"}
 
 
@@ -63,7 +64,7 @@ def main():
         # then the sweep steps; a probe after a sweep starts the next query
         qs, cur = [], []
         for d in ds:
-            if d["kind"] == "probe" and cur and cur[-1]["kind"] == "sweep":
+            if d["kind"] == "probe" and cur and cur[-1]["kind"] in ("sweep", "walk"):
                 qs.append(cur)
                 cur = []
             cur.append(d)
