@@ -384,6 +384,10 @@ struct EdgeSpace {
   // two halves (slots 0-1 -> pair_col[0], slots 2-3 -> pair_col[1], 2 x int32 per row, -1 past
   // the row's end, padded to whole 128-row tiles)
   DevBuf pair_col[2];
+  // 3-slot slab (option bu_slab3 at finalize; the final-hop first pass with bu_fin_var bit 64):
+  // slot 2 of every row as one int32, bit 31 set when the row has a fourth entry (the packed
+  // words use at most 31 bits; -1 past the row's end), so slots 0-2 cost 12 B a row, not 16
+  DevBuf slab3;
   // quantised predicate packing (bottom-up hops): the words of pair_col and tcol_q carry the
   // source gidx in their low q_gbits bits and, above it, q_bits bits of the bucket of transposed
   // prop q_field's value: bucket(v) = (v - q_min) * 2^q_bits / q_range (monotone), so a
@@ -544,6 +548,7 @@ struct Ctx {
   DevBuf ws_tile_rows;  // k_expand: frontier entry of each tile's first slot
   std::string bu_kernel_name, bu_rest_name;  // rocprof names of the last bottom-up launch
   bool bu_rest_rec = false;                  // ... whose rest pass read the rest records
+  uint64_t bu_od_bytes = 0;                  // ... out-degree bytes its first pass read (non-final hop)
   // deferred kernel timing: event pairs recorded around expansion launches and read once the
   // query's stream has drained, so timing never makes the host wait on a launch
   struct PendingTime {

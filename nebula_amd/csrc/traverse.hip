@@ -1213,6 +1213,11 @@ constexpr uint32_t kNoProbe = 0x0ffffff0u;
 // rows a hub word already found send no L2 probe.  Measured without gain and removed (r06e-r06h):
 // contiguous tile ranges per wave, the same skip for the LDS reads, 16-byte lanes (rows 2l and
 // 2l + 1 per lane), the tile's L2 probes packed into the fewest lanes through an LDS scratch.
+// Bit 6 -- the 3-slot slab (EdgeSpace::slab3 as `hi`, 4 B a row: slot 2 with bit 31 flagging a
+// fourth entry): 12 B per row instead of 16; a row with a fourth entry and no passing hit in
+// slots 0-2 goes to the rest pass (which rescans the final hop's pending rows from entry 0).
+// Measured (r10e, C3): this pass 106.9 -> 90.5 us, the rest pass 43 -> 74 us, the query 0.413
+// -> 0.425 ms; kept as an option (bu_slab3 + bu_fin_var 113), not the default.
 template <int CLS, int NT, int VAR = 0>
 __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo, const uint2* __restrict__ hi,
                                                     int64_t ntiles, int64_t work_tiles,
@@ -1250,12 +1255,25 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
     const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
     return make_uint2(uint32_t(x), uint32_t(x >> 32));
   };
+  constexpr bool S3 = (VAR & 64) != 0;
+  constexpr int NS = S3 ? 3 : 4;  // slots per row
+  bool more[2] = {false, false};  // S3: the row has a fourth entry
   auto load = [&](int64_t t, uint32_t (&sw)[2][4]) {
     const int64_t r = t * 128 + lane;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-      const uint2 a = ld8(lo + r + 64 * h), b = ld8(hi + r + 64 * h);
-      sw[h][0] = a.x, sw[h][1] = a.y, sw[h][2] = b.x, sw[h][3] = b.y;
+      const uint2 a = ld8(lo + r + 64 * h);
+      sw[h][0] = a.x, sw[h][1] = a.y;
+      if (S3) {
+        const uint32_t* s3 = reinterpret_cast<const uint32_t*>(hi);
+        const uint32_t x = NT ? __builtin_nontemporal_load(s3 + r + 64 * h) : s3[r + 64 * h];
+        more[h] = x != 0xffffffffu && (x >> 31) != 0u;
+        sw[h][2] = more[h] ? x & 0x7fffffffu : x;
+        sw[h][3] = 0xffffffffu;
+      } else {
+        const uint2 b = ld8(hi + r + 64 * h);
+        sw[h][2] = b.x, sw[h][3] = b.y;
+      }
     }
   };
   const uint32_t rest_b = __builtin_amdgcn_readfirstlane(fb_rest);
@@ -1267,7 +1285,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
+      for (int k = 0; k < NS; k++) {
         const uint32_t w = sw[h][k];
         if (CLS == 1)
           ob[h][k] = ((w >> 3) & bmask) | uint32_t(int32_t(w - clo) >> 31);
@@ -1278,7 +1296,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
-      for (int k = 0; k < 4; k++) lw[h][k] = *(lds_u32p)(size_t(min(ob[h][k], cw4)));
+      for (int k = 0; k < NS; k++) lw[h][k] = *(lds_u32p)(size_t(min(ob[h][k], cw4)));
     // VAR bit 5: rows already found through a hub word send no L2 probe (most found rows have
     // a hub in-neighbour in the frontier: their slots' L2 probes were wasted instructions)
     bool hubf[2] = {false, false};
@@ -1286,7 +1304,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
 #pragma unroll
       for (int h = 0; h < 2; h++)
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < NS; k++) {
           const uint32_t w = sw[h][k];
           const bool pass = CLS == 1 ? w >= plo : (w - plo <= pr) != pinv;
           hubf[h] = hubf[h] || (__builtin_amdgcn_ubfe(lw[h][k], w, 1u) != 0u && pass);
@@ -1295,7 +1313,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
+      for (int k = 0; k < NS; k++) {
         if (VAR & 1) {
           gw[h][k] = 0u;
           if (__ballot(ob[h][k] - cw4 < rest_b && !hubf[h]))
@@ -1310,7 +1328,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
     for (int h = 0; h < 2; h++) {
       bool fh = false, ah = false;
 #pragma unroll
-      for (int k = 0; k < 4; k++) {
+      for (int k = 0; k < NS; k++) {
         const uint32_t w = sw[h][k];
         const bool hit = __builtin_amdgcn_ubfe(lw[h][k] | gw[h][k], w, 1u) != 0u;
         const bool pass = CLS == 1 ? w >= plo : (w - plo <= pr) != pinv;
@@ -1320,7 +1338,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
       f[h] = fh;
       // pending: no passing hit, and a hit (then in an undecided bucket) or a fifth entry
       // (slot 3 set)
-      pend[h] = !fh && (ah || sw[h][3] != 0xffffffffu);
+      pend[h] = !fh && (ah || (S3 ? more[h] : sw[h][3] != 0xffffffffu));
     }
     unsigned long long f0 = __ballot(f[0]), f1 = __ballot(f[1]);
     unsigned long long p0 = __ballot(pend[0]), p1 = __ballot(pend[1]);
@@ -1339,7 +1357,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
     }
     nfound += uint64_t(__popcll(f0) + __popcll(f1));
     npend += uint64_t(__popcll(p0) + __popcll(p1));
-    nwords += 8u * 64u;
+    nwords += uint64_t(2 * NS) * 64u;
   }
   // tiles past the last row with an in-edge: nothing to find
   for (int64_t t = work_tiles + wave; t < ntiles; t += nwaves)
@@ -2774,15 +2792,18 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
                       fa.plo <= 0x80000000u && c.opt("bu_fin_cls", 1) != 0;
     const size_t fshm = size_t((cw + 2) & ~1) * 4 + size_t(kSlots) * 16 * 8;
     const uint32_t rest = fb_bytes > uint32_t(cw) * 4u ? fb_bytes - uint32_t(cw) * 4u : 0u;
-    auto gof = [&](auto kern) {
-      if (fshm > 48 * 1024) lds_limit(reinterpret_cast<const void*>(kern), fshm);
-      kern<<<grid, bs, fshm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, fa, partials, cw, rest, gate, gi,
-                                         atomic_sums);
-    };
     const int nt = int(c.opt("bu_fin_nt", 1) != 0);
     // default 49: the probe skip, one store per tile, hub-first L2 probes (r06h sweep:
     // k_bu_fin 124.9 -> 108.1 us; the 16-byte-lane and blocked-tile variants measured no gain)
-    const int var = cls1 && nt ? int(c.opt("bu_fin_var", 49) & (1 | 16 | 32)) : 0;
+    int var = cls1 && nt ? int(c.opt("bu_fin_var", 49) & (1 | 16 | 32 | 64)) : 0;
+    if (!es.slab3.p) var &= ~64;  // the 3-slot slab is built at finalize only with option bu_slab3
+    if (var & 64) var = 113;      // (the one 3-slot instantiation)
+    const uint2* fhi = (var & 64) ? reinterpret_cast<const uint2*>(es.slab3.p) : hi;
+    auto gof = [&](auto kern) {
+      if (fshm > 48 * 1024) lds_limit(reinterpret_cast<const void*>(kern), fshm);
+      kern<<<grid, bs, fshm, c.stream>>>(lo, fhi, ntiles, work, fb, nb, pbits, fa, partials, cw, rest, gate, gi,
+                                         atomic_sums);
+    };
     switch ((cls1 ? 1 : 0) | nt << 1 | var << 2) {
       case 0: gof(k_bu_fin<0, 0>); break;
       case 1: gof(k_bu_fin<1, 0>); break;
@@ -2794,6 +2815,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
       case 3 | (32 << 2): gof(k_bu_fin<1, 1, 32>); break;
       case 3 | (33 << 2): gof(k_bu_fin<1, 1, 33>); break;
       case 3 | (48 << 2): gof(k_bu_fin<1, 1, 48>); break;
+      case 3 | (113 << 2): gof(k_bu_fin<1, 1, 113>); break;
       default: gof(k_bu_fin<1, 1, 49>); break;
     }
     snprintf(fin_nm, sizeof fin_nm, "nbg::k_bu_fin<%d, %d, %d>", cls1 ? 1 : 0, nt, var);
@@ -2879,6 +2901,9 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
              probe_stats ? 1 : 0,
              sel == 9 ? ", 1, 7" : sel == 8 ? ", 1, 3" : sel == 7 ? ", 1, 1" : sel == 6 ? ", 1, 0" : ", 0, 0");
   c.bu_kernel_name = nm;
+  // the non-final first pass reads one out-degree per row of its work tiles: 1 B (odeg8, the
+  // non-temporal instantiations) or 4 B (odeg)
+  if (!fast) c.bu_od_bytes = uint64_t(work) * 128u * (sel >= 6 && sel <= 9 ? 1u : 4u);
   const int wn = fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0;
   snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d, %d>", pk, wn, rcw > 0 ? 1 : 0, use_rec ? 1 : 0);
   c.bu_rest_rec = use_rec;
@@ -2888,10 +2913,11 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
 
 // byte models of a bottom-up hop's two passes from their counters.
 // First pass: 4 B per slab word read, the frontier bitmap once, the next-frontier and pending
-// bits written, the out-degree (4 B/row) at a non-final hop.  Rest pass: a row_ptr pair per
-// pending row, 4 B per entry read, predicate values read.
-uint64_t bu_first_bytes(const unsigned long long* h, int64_t n_rows, bool with_odeg) {
-  return h[2] * 4 + 3 * (uint64_t(n_rows) / 8) + (with_odeg ? uint64_t(n_rows) * 4 : 0);
+// bits written, the out-degrees a non-final hop read (od_bytes: 1 B per work row from odeg8;
+// rounds 2-4 counted 4 B for every row, 1.5x the bytes the default kernel reads).  Rest pass:
+// a row_ptr pair (or a 64 B rest record) per pending row, 4 B per entry read, predicate values read.
+uint64_t bu_first_bytes(const unsigned long long* h, int64_t n_rows, uint64_t od_bytes) {
+  return h[2] * 4 + 3 * (uint64_t(n_rows) / 8) + od_bytes;
 }
 uint64_t bu_rest_bytes(const unsigned long long* h, int pred_width, bool rec) {
   return h[3] * (rec ? 64 : 16) + h[4] * 4 + h[5] * uint64_t(pred_width);
@@ -3446,7 +3472,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       c.timing.edges_scanned += uint64_t(E);
       c.timing.expand_launches++;
       c.timing.bu_steps++;
-      const uint64_t kb = bu_first_bytes(hh, es.tr.n_rows, true), hb = kb + bu_rest_bytes(hh, 0, c.bu_rest_rec);
+      const uint64_t kb = bu_first_bytes(hh, es.tr.n_rows, c.bu_od_bytes), hb = kb + bu_rest_bytes(hh, 0, c.bu_rest_rec);
       c.timing.expand_bytes += hb;
       c.timing.hop(1, false, 0.0, hh, 0.0, kb);
       c.timing.name_last_hop(spec[j].k0, spec[j].k1);
@@ -3555,7 +3581,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       fetch_counters(c, K.d, multi ? 50 : 8, K.h);
       c.timing.expand_launches++;
       c.timing.bu_steps++;
-      const uint64_t kb = bu_first_bytes(K.h, tr.n_rows, true), hb = kb + bu_rest_bytes(K.h, 0, c.bu_rest_rec);
+      const uint64_t kb = bu_first_bytes(K.h, tr.n_rows, c.bu_od_bytes), hb = kb + bu_rest_bytes(K.h, 0, c.bu_rest_rec);
       c.timing.expand_bytes += hb;
       c.timing.hop(1, false, 0.0, K.h, 0.0, kb);
       c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name);
@@ -3682,7 +3708,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         c.timing.bu_steps++;
         nrows = int64_t(fin_h[9]);
         const int pw = pk == PK_FAST ? fp.width : 0;
-        const uint64_t kb = bu_first_bytes(fin_h, es.tr.n_rows, false), hb = kb + bu_rest_bytes(fin_h, pw, c.bu_rest_rec);
+        const uint64_t kb = bu_first_bytes(fin_h, es.tr.n_rows, 0), hb = kb + bu_rest_bytes(fin_h, pw, c.bu_rest_rec);
         c.timing.expand_bytes += hb + uint64_t(es.tr.n_rows) / 8 + uint64_t(nrows) * 16;
         c.timing.hop(1, true, 0.0, fin_h, 0.0, kb);
         c.timing.name_last_hop(fin_k0, fin_k1, c.opt("bits_u", 8) == 8 ? "nbg::k_bits_compact<1, 8>" : "nbg::k_bits_compact<1, 4>");
@@ -3710,7 +3736,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         c.timing.bu_steps++;
         nrows = int64_t(K.h[0]);
         const int pw = pk == PK_FAST ? tfp.width : 0;
-        const uint64_t kb = bu_first_bytes(K.h + 8, tr.n_rows, false), hb = kb + bu_rest_bytes(K.h + 8, pw, c.bu_rest_rec);
+        const uint64_t kb = bu_first_bytes(K.h + 8, tr.n_rows, 0), hb = kb + bu_rest_bytes(K.h + 8, pw, c.bu_rest_rec);
         // + the DISTINCT _dst output (k_bits_compact<1>): next bits once, vid_of read + vid written
         c.timing.expand_bytes += hb + uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
         c.timing.hop(1, true, 0.0, K.h + 8, 0.0, kb);

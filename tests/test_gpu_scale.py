@@ -293,3 +293,29 @@ def test_bu_fin_variants_rmat20(rmat20, var, hub_cap):
     finally:
         for k in ("bu_fin_var", "bu_hub_cap", "bu_lean_skip"):
             sp.unset_option(k)
+
+
+def test_bu_fin_three_slot_slab_rmat20():
+    """the 3-slot slab (bu_slab3 at finalize, bu_fin_var bit 64: slots 0-2 in 12 B a row, a
+    fourth entry flagged in bit 31 of slot 2) against the committed digest, with the hub copy on
+    and capped (the L2 probes then answer most rows); without the slab the option falls back"""
+    sp = rmat_space(20, bu_slab3=1)
+    try:
+        for hub_cap in (None, 1024):
+            if hub_cap:
+                sp.set_option("bu_hub_cap", hub_cap)
+            sp.set_option("bu_fin_var", 113)
+            r = bench_query(sp, 20)
+            check_gold("go3_where499_distinct_s20", r.columns[0], r.edges_scanned)
+            hops = sp.last_timing()["hops"]
+            assert hops[-1]["kernels"][0] == "nbg::k_bu_fin<1, 1, 113>", hops[-1]["kernels"]
+            # 3 slab words a row were read (the hop's counters feed the byte model)
+            sp.set_option("bu_fin_var", 49)
+            r4 = bench_query(sp, 20)
+            check_gold("go3_where499_distinct_s20", r4.columns[0], r4.edges_scanned)
+            h4 = sp.last_timing()["hops"][-1]
+            assert h4["kernels"][0] == "nbg::k_bu_fin<1, 1, 49>"
+            assert hops[-1]["c"][2] * 4 == h4["c"][2] * 3, (hops[-1]["c"][2], h4["c"][2])
+    finally:
+        sp.close()
+
