@@ -74,7 +74,7 @@ def main():
         out, seen = {}, defaultdict(int)
         for d in q:  # the n-th dispatch of a kind is iteration / step n
             seen[d["kind"]] += 1
-            out[(d["kind"], seen[d["kind"]])] = d
+            out[(d["kind"], seen[d["kind"]] - (1 if d["kind"] == "walk" else 0))] = d
         return out
 
     fetch, write = last_query(by_pass.get("p0", [])), last_query(by_pass.get("p1", []))
