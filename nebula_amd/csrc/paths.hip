@@ -1254,7 +1254,20 @@ constexpr int kCh = 1024;                 // adjacency entries per chunk (one wa
 constexpr int kPubW = 64;                 // words per host publish slot (the sequence word last)
 constexpr int kDvStage = 256;             // claims staged per wave and list
 constexpr int kPairLds = 4096;            // pairs per batch whose per-pair tables the selects keep in LDS
-__device__ inline unsigned long long* qblk(unsigned long long* cnt, int q) { return cnt + D_G + q * Q_W; }
+// every counter on a 128-byte line of its own (logical counter i at word i * kCS): blocks of a grid
+// ending together add to a line's words one atomic at a time at the memory side (~12 ns each), so
+// counters that shared a line had serialised each other's adds (round 5: 16 counters per line)
+constexpr int kCS = 16;
+__host__ __device__ inline unsigned long long* gcnt(unsigned long long* cnt, int i) { return cnt + size_t(i) * kCS; }
+__host__ __device__ inline const unsigned long long* gcnt(const unsigned long long* cnt, int i) {
+  return cnt + size_t(i) * kCS;
+}
+struct QBlk {  // counter block q: q[k] / q + k address its counter k
+  unsigned long long* p;
+  __device__ unsigned long long& operator[](int k) const { return p[size_t(k) * kCS]; }
+  __device__ unsigned long long* operator+(int k) const { return p + size_t(k) * kCS; }
+};
+__device__ inline QBlk qblk(unsigned long long* cnt, int q) { return QBlk{gcnt(cnt, D_G + q * Q_W)}; }
 
 struct SpFilt {
   uint32_t* pf;     // [2 * kLv][B][128] pair filters (null: off)
@@ -1328,7 +1341,7 @@ __device__ inline bool gf_test(const SpFilt& f, uint32_t side, int32_t l, uint32
 // block-wide reductions, and this launch may raise the flag while its blocks run)
 __device__ inline bool dv_ovf_block(const unsigned long long* cnt) {
   __shared__ int s_ovf;
-  if (threadIdx.x == 0) s_ovf = __hip_atomic_load(cnt + D_OVF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  if (threadIdx.x == 0) s_ovf = __hip_atomic_load(gcnt(cnt, D_OVF), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   __syncthreads();
   return s_ovf != 0;
 }
@@ -1371,7 +1384,7 @@ __device__ inline void dput(uint64_t* list, int64_t cap, unsigned long long* ctr
   const int64_t s = wave_append(ctr, pred);
   if (pred) {
     if (s < cap) list[s] = v;
-    else atomicOr(cnt + D_OVF, 1ull);
+    else atomicOr(gcnt(cnt, D_OVF), 1ull);
   }
 }
 
@@ -1452,17 +1465,17 @@ __device__ inline void dv_publish_last(unsigned long long* cnt, int q, unsigned 
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
-    s_last = atomicAdd(cnt + D_TICKET, 1ull) == (unsigned long long)(gridDim.x - 1);
+    s_last = atomicAdd(gcnt(cnt, D_TICKET), 1ull) == (unsigned long long)(gridDim.x - 1);
   }
   __syncthreads();
   if (!s_last || threadIdx.x >= 64) return;
   __threadfence();
   const int i = threadIdx.x;
   if (i < D_G + Q_W) {
-    const unsigned long long* src = i < D_G ? cnt + i : qblk(cnt, q) + (i - D_G);
+    const unsigned long long* src = i < D_G ? gcnt(cnt, i) : qblk(cnt, q) + (i - D_G);
     hslot[i] = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (i == 0) __hip_atomic_store(cnt + D_TICKET, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (i == 0) __hip_atomic_store(gcnt(cnt, D_TICKET), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __builtin_amdgcn_wave_barrier();
   if (i == 0) __hip_atomic_store(hslot + kPubW - 1, (unsigned long long)seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1509,7 +1522,7 @@ __global__ __launch_bounds__(256) void k_dv_begin(SpDev d, SpState st, SpCsr gou
   // the active ones takes slot k of both live lists and arena slots 2k, 2k + 1, so one returning
   // atomic (the active count) places all four tuples
   const uint32_t pp = uint32_t(gt);
-  unsigned long long* q0 = qblk(d.cnt, 0);
+  const QBlk q0 = qblk(d.cnt, 0);
   const int64_t k = wave_append(q0 + Q_ACTIVE, go);
   if (go) {
     if (k < d.cap_live) {
@@ -1520,14 +1533,14 @@ __global__ __launch_bounds__(256) void k_dv_begin(SpDev d, SpState st, SpCsr gou
       d.arena[2 * k] = mk_tup(0, pp, 0, uint32_t(a));
       d.arena[2 * k + 1] = mk_tup(1, pp, 0, uint32_t(b));
     }
-    if (k >= d.cap_live || 2 * k + 1 >= d.cap_arena) atomicOr(d.cnt + D_OVF, 1ull);
+    if (k >= d.cap_live || 2 * k + 1 >= d.cap_arena) atomicOr(gcnt(d.cnt, D_OVF), 1ull);
   }
   const uint64_t m = __ballot(go);
   if ((threadIdx.x & 63) == 0 && m) {
     const unsigned long long nw = (unsigned long long)__popcll(m);
     atomicAdd(q0 + Q_LIVE0, nw);
     atomicAdd(q0 + Q_LIVE1, nw);
-    atomicAdd(d.cnt + D_ARENA, 2 * nw);
+    atomicAdd(gcnt(d.cnt, D_ARENA), 2 * nw);
   }
 }
 
@@ -1535,8 +1548,8 @@ __global__ __launch_bounds__(256) void k_dv_begin(SpDev d, SpState st, SpCsr gou
 // their pair expands, with their chunk ranges in the chunk table) + the tuples carried into
 // iteration it's lists.  kSelIt tuples per thread, one reservation per block and round.
 __global__ __launch_bounds__(kBlk) void k_dv_select(SpDev d, SpState st, SpCsr gout, SpCsr gin, int32_t it) {
-  unsigned long long* qp = qblk(d.cnt, it - 1);
-  unsigned long long* q = qblk(d.cnt, it);
+  const QBlk qp = qblk(d.cnt, it - 1);
+  const QBlk q = qblk(d.cnt, it);
   if (qp[Q_ACTIVE] == 0) return;  // the BFS ended (a speculative iteration): nothing selected
   const int64_t n0 = min(int64_t(qp[Q_LIVE0]), d.cap_live), n1 = min(int64_t(qp[Q_LIVE1]), d.cap_live);
   const int64_t nl = n0 + n1;
@@ -1620,7 +1633,7 @@ __global__ __launch_bounds__(kBlk) void k_dv_select(SpDev d, SpState st, SpCsr g
         o[2]++;
       }
     }
-    if (ovf) atomicOr(d.cnt + D_OVF, 2ull);
+    if (ovf) atomicOr(gcnt(d.cnt, D_OVF), 2ull);
   }
   blk_add(q + Q_XE, esum);
 }
@@ -1715,7 +1728,7 @@ __global__ __launch_bounds__(256) void k_dv_probe(SpDev d, SpState st, SpFilt f,
                                                        uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo, int32_t it) {
   if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
   const int lane = threadIdx.x & 63;
-  unsigned long long* q = qblk(d.cnt, it);
+  const QBlk q = qblk(d.cnt, it);
   const int64_t total = min(int64_t(q[Q_NCH]), d.cap_ch);
   if (total == 0) return;  // nothing selected (grid-uniform)
   const uint32_t B = uint32_t(st.B);
@@ -1790,7 +1803,7 @@ __device__ inline void dv_flush(DvStage& s, unsigned long long* cnt, unsigned lo
   __builtin_amdgcn_wave_barrier();
   unsigned long long ba = 0, bl = 0;
   if (lane == 0) {
-    ba = atomicAdd(cnt + D_ARENA, (unsigned long long)s.n);
+    ba = atomicAdd(gcnt(cnt, D_ARENA), (unsigned long long)s.n);
     bl = atomicAdd(lctr, (unsigned long long)s.n);
   }
   ba = __shfl(ba, 0);
@@ -1803,7 +1816,7 @@ __device__ inline void dv_flush(DvStage& s, unsigned long long* cnt, unsigned lo
     if (int64_t(bl + k) < cap_list) list[bl + k] = v;
     else ovf = true;
   }
-  if (ovf) atomicOr(cnt + D_OVF, 1ull);
+  if (ovf) atomicOr(gcnt(cnt, D_OVF), 1ull);
   __builtin_amdgcn_wave_barrier();
   s.n = 0;
 }
@@ -1829,7 +1842,7 @@ __device__ inline void dv_flush_block(DvStage& s, unsigned long long* cnt, unsig
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned long long tot = s_ns[0] + s_ns[1] + s_ns[2] + s_ns[3];
-    s_b[0] = tot ? atomicAdd(cnt + D_ARENA, tot) : 0ull;
+    s_b[0] = tot ? atomicAdd(gcnt(cnt, D_ARENA), tot) : 0ull;
     s_b[1] = tot ? atomicAdd(lctr, tot) : 0ull;
   }
   __syncthreads();
@@ -1844,7 +1857,7 @@ __device__ inline void dv_flush_block(DvStage& s, unsigned long long* cnt, unsig
     if (int64_t(bl + k) < cap_list) list[bl + k] = v;
     else ovf = true;
   }
-  if (ovf) atomicOr(cnt + D_OVF, 1ull);
+  if (ovf) atomicOr(gcnt(cnt, D_OVF), 1ull);
   s.n = 0;
   __syncthreads();
 }
@@ -1864,7 +1877,7 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
-  unsigned long long* q = qblk(d.cnt, it);
+  const QBlk q = qblk(d.cnt, it);
   const int64_t total = min(int64_t(q[Q_NCH]), d.cap_ch);
   if (total == 0) return;  // nothing selected (grid-uniform)
   const uint32_t B = uint32_t(st.B);
@@ -1937,7 +1950,7 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
               dv_stage(sg1, cl, mk_tup(1, p, l + 1, w[u]), d.cnt, q + Q_LIVE1, out1, d.cap_live, d.arena, d.cap_arena);
             else
               dv_stage(sg0, cl, mk_tup(0, p, l + 1, w[u]), d.cnt, q + Q_LIVE0, out0, d.cap_live, d.arena, d.cap_arena);
-            dput(d.meet, d.cap_meet, d.cnt + D_MEET, d.cnt, meet, mk_tup(1, p, dt, w[u]));
+            dput(d.meet, d.cap_meet, gcnt(d.cnt, D_MEET), d.cnt, meet, mk_tup(1, p, dt, w[u]));
           }
         }
         dsum = wsum(dsum);
@@ -1958,8 +1971,8 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
       mt = mk_tup(1, t_pair(v), o ? lv : t_lvl(d.X[d.chx[c]]), t_row(v));
     }
     if (__ballot(hit) == 0) continue;
-    dput(d.arena, d.cap_arena, d.cnt + D_ARENA, d.cnt, hit, v);
-    dput(d.meet, d.cap_meet, d.cnt + D_MEET, d.cnt, hit, mt);
+    dput(d.arena, d.cap_arena, gcnt(d.cnt, D_ARENA), d.cnt, hit, v);
+    dput(d.meet, d.cap_meet, gcnt(d.cnt, D_MEET), d.cnt, hit, mt);
   }
   dv_flush_block(sg0, d.cnt, q + Q_LIVE0, out0, d.cap_live, d.arena, d.cap_arena);
   dv_flush_block(sg1, d.cnt, q + Q_LIVE1, out1, d.cap_live, d.arena, d.cap_arena);
@@ -1997,8 +2010,8 @@ __global__ __launch_bounds__(256) void k_dv_step(SpDev d, SpState st, int32_t ma
       }
     }
     if (st.state[p] == SP_MET) {
-      atomicMax(d.cnt + D_MAXL, (unsigned long long)st.res[p]);
-      atomicMax(d.cnt + D_MAXF, (unsigned long long)st.lvl[p]);
+      atomicMax(gcnt(d.cnt, D_MAXL), (unsigned long long)st.res[p]);
+      atomicMax(gcnt(d.cnt, D_MAXF), (unsigned long long)st.lvl[p]);
     } else if (st.state[p] == SP_ACTIVE) {
       const int s = st.deg[p] <= st.deg[B + p] ? 0 : 1;
       st.side[p] = s;
@@ -2050,7 +2063,7 @@ __device__ inline void dv_walk_front(SpDev& d, const SpState& st, const SpCsr& g
                                      const int64_t* ht_keys, const int32_t* ht_vals, uint64_t ht_mask,
                                      bool ht_has_min, int32_t ht_min_gidx) {
   const int32_t B = st.B;
-  unsigned long long* q = qblk(d.cnt, kWkQ + i);
+  const QBlk q = qblk(d.cnt, kWkQ + i);
   unsigned long long* ctr[1] = {q + Q_NCH};
   const int64_t rounds = (int64_t(B) + kBlk - 1) / kBlk;
   for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
@@ -2063,7 +2076,7 @@ __device__ inline void dv_walk_front(SpDev& d, const SpState& st, const SpCsr& g
       } else if (L - 1 > i - 1 && d.cur[p] >= 0) {
         const long long b = d.best[p];
         if (b == LLONG_MAX) {  // in-edge keys without the mirrored out-edge: the definition does not hold
-          atomicAdd(d.cnt + D_WALKERR, 1ull);
+          atomicAdd(gcnt(d.cnt, D_WALKERR), 1ull);
           d.cur[p] = -1;
         } else {
           d.path[d.doff[p] + i] = int64_t(b);
@@ -2077,7 +2090,7 @@ __device__ inline void dv_walk_front(SpDev& d, const SpState& st, const SpCsr& g
     unsigned long long o[1];
     blk_reserve_n<1>(ctr, &nc, o);
     const bool ok = int64_t(o[0]) + int64_t(nc) <= d.cap_wch;
-    if (nc && !ok) atomicOr(d.cnt + D_OVF, 4ull);
+    if (nc && !ok) atomicOr(gcnt(d.cnt, D_OVF), 4ull);
     if (p < B && nc) d.wcb[p] = int64_t(o[0]);
     wave_fill_val(int64_t(o[0]), ok ? int64_t(nc) : 0, p, [&](int64_t c, int64_t v) { d.wchx[c] = int32_t(v); });
   }
@@ -2093,7 +2106,7 @@ __global__ __launch_bounds__(kBlk) void k_dv_post(SpDev d, SpState st, SpCsr gou
   if (blockIdx.x == 0) dv_path_offsets(st, B, d.doff);
   dv_walk_front(d, st, gout, 0, lo, ht_keys, ht_vals, ht_mask, ht_has_min, ht_min_gidx);
   const int64_t gn = int64_t(gridDim.x) * blockDim.x;
-  const int64_t nm = min(int64_t(d.cnt[D_MEET]), d.cap_meet);
+  const int64_t nm = min(int64_t((*gcnt(d.cnt, D_MEET))), d.cap_meet);
   const int64_t rm = (nm + gn - 1) / gn;
   for (int64_t r = 0; r < rm; r++) {
     const int64_t i = r * gn + int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -2123,9 +2136,9 @@ __device__ inline bool dv_push_pair(const SpDev& d, const SpState& st, uint32_t 
 }
 __global__ __launch_bounds__(kBlk) void k_dv_sweep_select(SpDev d, SpState st, SpCsr gout, SpCsr gin, int32_t j,
                                                           unsigned long long bias16) {
-  unsigned long long* q = qblk(d.cnt, kSwQ + j);
+  const QBlk q = qblk(d.cnt, kSwQ + j);
   const uint64_t* cur = j == 1 ? d.meet : d.sw[(j - 1) & 1];
-  const int64_t ncur = j == 1 ? min(int64_t(d.cnt[D_MEET]), d.cap_meet)
+  const int64_t ncur = j == 1 ? min(int64_t((*gcnt(d.cnt, D_MEET))), d.cap_meet)
                               : min(int64_t(qblk(d.cnt, kSwQ + j - 1)[Q_CLAIMS]), d.cap_sw);
   // per pair in LDS: res - 1 of a MET pair (0: not sweeping) and the forward level it pushes at this
   // step (0: it pulls); the arena's forward tuples are scanned only when some pair pushes (every
@@ -2139,7 +2152,7 @@ __global__ __launch_bounds__(kBlk) void k_dv_sweep_select(SpDev d, SpState st, S
     s_pk[p] = push ? uint8_t(st.lvl[p] - j) : uint8_t(0);
     anyp |= push ? 1 : 0;
   }
-  const int64_t na = __syncthreads_or(anyp) ? min(int64_t(d.cnt[D_ARENA]), d.cap_arena) : 0;
+  const int64_t na = __syncthreads_or(anyp) ? min(int64_t((*gcnt(d.cnt, D_ARENA))), d.cap_arena) : 0;
   const int64_t nt = ncur + na;
   constexpr int64_t per = int64_t(kBlk) * kSelIt;
   const int64_t rounds = (nt + per - 1) / per;
@@ -2193,7 +2206,7 @@ __global__ __launch_bounds__(kBlk) void k_dv_sweep_select(SpDev d, SpState st, S
       }
       wave_fill_val(ca, x && fit ? nc : 0, xa, [&](int64_t c, int64_t v) { d.chx[c] = int32_t(v); });
     }
-    if (ovf) atomicOr(d.cnt + D_OVF, 2ull);
+    if (ovf) atomicOr(gcnt(d.cnt, D_OVF), 2ull);
   }
   blk_add(q + Q_XE, esum);
 }
@@ -2209,7 +2222,7 @@ __global__ __launch_bounds__(256) void k_dv_sweep(SpDev d, SpState st, SpFilt f,
   __shared__ uint64_t s_stage[4][kDvStage];
   if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  unsigned long long* q = qblk(d.cnt, kSwQ + j);
+  const QBlk q = qblk(d.cnt, kSwQ + j);
   const int64_t total = min(int64_t(q[Q_NCH]), d.cap_ch);
   const uint32_t B = uint32_t(st.B);
   uint64_t* out = d.sw[j & 1];
@@ -2301,7 +2314,7 @@ __global__ __launch_bounds__(256) void k_dv_walk_scan(SpDev d, SpState st, SpFil
                                                       const int64_t* vid_of, int64_t n, int64_t lo, int32_t i) {
   if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
   const int lane = threadIdx.x & 63;
-  unsigned long long* q = qblk(d.cnt, kWkQ + i);
+  const QBlk q = qblk(d.cnt, kWkQ + i);
   const int64_t total = min(int64_t(q[Q_NCH]), d.cap_wch);
   unsigned long long entries = 0;
   chunk_groups(
@@ -2374,7 +2387,7 @@ __global__ __launch_bounds__(256) void k_dv_out(SpDev d, SpState st, int32_t ila
     const int64_t o = d.doff[p];
     if (s == SP_MET && ilast >= 0 && L - 1 > ilast && d.cur[p] >= 0) {
       const long long b = d.best[p];
-      if (b == LLONG_MAX) atomicAdd(d.cnt + D_WALKERR, 1ull);
+      if (b == LLONG_MAX) atomicAdd(gcnt(d.cnt, D_WALKERR), 1ull);
       else d.path[o + ilast + 1] = int64_t(b);
     }
     d.h_sr[p] = s;
@@ -2402,7 +2415,7 @@ __global__ __launch_bounds__(256) void k_dv_clear(SpDev d, SpState st, SpFilt f,
   const uint4 z = make_uint4(0u, 0u, 0u, 0u);
   for (int64_t i = gt; i < pf4; i += gn) reinterpret_cast<uint4*>(f.pf)[i] = z;
   for (int64_t i = gt; i < gf4; i += gn) reinterpret_cast<uint4*>(f.gf)[i] = z;
-  const int64_t na = min(int64_t(d.cnt[D_CLEAR]), d.cap_arena);
+  const int64_t na = min(int64_t((*gcnt(d.cnt, D_CLEAR))), d.cap_arena);
   for (int64_t i = gt; i < na; i += gn) {
     const uint64_t t = d.arena[i];
     (t_side(t) ? d1 : d0)[didx(st, t_pair(t), t_row(t), n)] = 0xFF;
@@ -2415,11 +2428,11 @@ __global__ __launch_bounds__(256) void k_dv_clear(SpDev d, SpState st, SpFilt f,
 // copies.  D_CLEAR keeps the arena length for k_dv_clear.
 __global__ void k_dv_finish(unsigned long long* cnt, unsigned long long* h, unsigned long long* hseq, uint64_t seq,
                             int32_t nbfs, int32_t nsw, int32_t nwalk) {
-  const unsigned long long arena = cnt[D_ARENA];  // read before any lane clears it
+  const unsigned long long arena = (*gcnt(cnt, D_ARENA));  // read before any lane clears it
   auto move = [&](int a, int b) {
     for (int i = a + int(threadIdx.x); i < b; i += 64) {
-      h[i] = cnt[i];
-      cnt[i] = i == D_CLEAR ? arena : 0ull;
+      h[i] = *gcnt(cnt, i);
+      *gcnt(cnt, i) = i == D_CLEAR ? arena : 0ull;
     }
   };
   move(0, D_G + nbfs * Q_W);
@@ -2731,7 +2744,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     memset(c.sp_host, 0, h_end);
     c.sp_host_bytes = h_end;
     W.dv_cnt = DevBuf();
-    W.dv_cnt.alloc(size_t(kDevCnt) * 8);
+    W.dv_cnt.alloc(size_t(kDevCnt) * kCS * 8);
     for (auto& b : W.dv_live) {
       b = DevBuf();
       b.alloc(size_t(cap) * 8);
@@ -2868,7 +2881,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     auto dv_abort = [&](bool wipe) {
       NBG_HIP(hipStreamSynchronize(c.stream));
       unsigned long long na = 0;
-      NBG_HIP(hipMemcpy(&na, d.cnt + D_ARENA, 8, hipMemcpyDeviceToHost));
+      NBG_HIP(hipMemcpy(&na, gcnt(d.cnt, D_ARENA), 8, hipMemcpyDeviceToHost));
       if (!wipe && int64_t(na) <= d.cap_arena) {
         if (na) k_sp_clear<<<grid_n(int64_t(na)), 256, 0, c.stream>>>(d.arena, int64_t(na), d0, d1, n, st);
       } else {
