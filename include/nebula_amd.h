@@ -87,7 +87,7 @@ int32_t nbg_comm_info(nbg_ctx* ctx, int32_t* ranks, int32_t* transport);
  * nbg_hop_stat, nbg_snapshot_info, nbg_go_spec, nbg_rows) change layout between versions: an
  * integration compares nbg_abi_version() with the NBG_ABI_VERSION it was built against and
  * refuses to run on a mismatch (INTEGRATION.md "ABI versioning").                          */
-#define NBG_ABI_VERSION 4
+#define NBG_ABI_VERSION 5
 int32_t nbg_abi_version(void);
 /* sizeof of the caller-allocated structs as the library was built: 0 nbg_timing, 1
  * nbg_hop_stat, 2 nbg_snapshot_info, 3 nbg_go_spec, 4 nbg_rows, 5 nbg_prop_def; -1 otherwise */
@@ -315,6 +315,8 @@ typedef struct {
   int32_t spec_hops;      /* nbg_go: hops that ran speculatively behind a device gate;
                              nbg_shortest_path: batches that ran device-driven (the others ran
                              host-driven: option sp_dev = 0, or a list overflow re-ran them)   */
+  int32_t launches;       /* nbg_shortest_path: kernel launches of its device-driven batches
+                             (ABI 5; 0 for other calls)                                         */
 } nbg_timing;
 int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out);
 /* engine option key = value (tuning knobs); value INT64_MIN removes the key, so the

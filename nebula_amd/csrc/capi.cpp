@@ -373,6 +373,7 @@ int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out) {
     memcpy(out->hops, c.timing.hops, sizeof(out->hops));
     out->host_waits = c.timing.host_waits;
     out->spec_hops = c.timing.spec_hops;
+    out->launches = c.timing.launches;
     return NBG_OK;
   });
 }

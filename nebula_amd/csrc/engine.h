@@ -440,6 +440,7 @@ struct Timing {
   nbg_hop_stat hops[NBG_MAX_HOP_STATS] = {};
   int32_t host_waits = 0;  // engine-level host waits on the device (fetches, stream syncs)
   int32_t spec_hops = 0;   // hops that ran behind a device gate
+  int32_t launches = 0;    // kernel launches of the device-driven shortest-path batches
   uint64_t hop_bytes_mark = 0;  // expand_bytes at the previous hop record
   // kernel_ms < 0: the hop is one kernel (its time and bytes are the hop's; a top-down hop's
   // time is filled in later by timing_resolve)

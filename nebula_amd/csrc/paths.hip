@@ -2778,6 +2778,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     W.dv_clean = true;
   };
   auto run_dev = [&](size_t b0, int64_t nb) -> bool {
+    int32_t nl = 0;  // kernel launches of the batch (nbg_timing.launches)
     dv_alloc();
     W.dv_clean = false;  // until the batch's finish launch (or the abort below) restores it
     char* hb = static_cast<char*>(c.sp_host);
@@ -2896,12 +2897,15 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       return false;
     };
 
+    ++nl;
     k_dv_begin<<<std::max(grid_n(nb, 1 << 20), 64), 256, 0, c.stream>>>(d, st, gout, gin, d0, d1, n, max_steps, htk, htv,
                                                           uint64_t(htm), c.ht_has_min, c.ht_min_gidx);
     auto enqueue = [&](int it) {
+      ++nl;
       k_dv_select<<<gsel((const void*)k_dv_select), kBlk, 0, c.stream>>>(d, st, gout, gin, it);
       evi[size_t(it)][0] = dv_event();
       if (probe) {
+        ++nl;
         if (pu >= 16)
           k_dv_probe<16><<<gpr((const void*)k_dv_probe<16>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
         else if (pu >= 8)
@@ -2910,6 +2914,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
           k_dv_probe<4><<<gpr((const void*)k_dv_probe<4>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
       }
       evi[size_t(it)][1] = dv_event();
+      ++nl;
       if (occ >= 8)
         k_dv_expand<8><<<gsz((const void*)k_dv_expand<8>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it,
                                                                                lg_sub, cas);
@@ -2918,6 +2923,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
                                                                                lg_sub, cas);
       evi[size_t(it)][2] = dv_event();
       seq[size_t(it)] = ++c.pub_seq;
+      ++nl;
       k_dv_step<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(d, st, max_steps, it, pub(it), seq[size_t(it)]);
       NBG_HIP(hipGetLastError());
     };
@@ -2932,13 +2938,16 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     }
     const int64_t maxL = int64_t(pub(it)[D_MAXL]), maxF = int64_t(pub(it)[D_MAXF]);
     const int iters = it;
+    ++nl;
     k_dv_post<<<int(std::max<int64_t>(1, c.opt("sp_dv_post_grid", 512))), kBlk, 0, c.stream>>>(
         d, st, gout, gin, lo, htk, htv, uint64_t(htm), c.ht_has_min, c.ht_min_gidx);
     const int nsw = int(std::min<int64_t>(std::max<int64_t>(maxF - 1, 0), kMaxQ - 2));
     const unsigned long long bias16 = (unsigned long long)std::max<int64_t>(0, c.opt("sp_push_bias", 16));
     for (int j = 1; j <= nsw; j++) {
+      ++nl;
       k_dv_sweep_select<<<gsel((const void*)k_dv_sweep_select), kBlk, 0, c.stream>>>(d, st, gout, gin, j, bias16);
       evs[size_t(j)][0] = dv_event();
+      ++nl;
       if (su >= 16)
         k_dv_sweep<16><<<gsz((const void*)k_dv_sweep<16>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
       else if (su >= 8)
@@ -2949,18 +2958,24 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     }
     const int nwalk = int(std::min<int64_t>(maxL >= 2 ? maxL - 1 : 0, kMaxQ - 2));
     for (int i = 0; i < nwalk; i++) {
-      if (i > 0)
+      if (i > 0) {
+        ++nl;
         k_dv_walk_front<<<grid_n(nb, 1 << 20), kBlk, 0, c.stream>>>(d, st, gout, i, lo, htk, htv, uint64_t(htm),
                                                                    c.ht_has_min, c.ht_min_gidx);
+      }
       evw[size_t(i)][0] = dv_event();
+      ++nl;
       k_dv_walk_scan<<<gsz((const void*)k_dv_walk_scan), 256, 0, c.stream>>>(d, st, f, gout, d1, vid_of, n, lo, i);
       evw[size_t(i)][1] = dv_event();
     }
+    ++nl;
     k_dv_out<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(d, st, nwalk - 1);
     const uint64_t fseq = ++c.pub_seq;
     // BFS blocks written: 0 .. iters, plus the speculative iteration after the last
     const int32_t nbfs = std::min<int32_t>(iters + (iters < max_it ? 2 : 1), kMaxQ);
+    ++nl;
     k_dv_finish<<<1, 64, 0, c.stream>>>(d.cnt, fin, fin + kDevCnt + 8, fseq, nbfs, nsw, nwalk);
+    ++nl;
     k_dv_clear<<<gsz((const void*)k_dv_clear), 256, 0, c.stream>>>(d, st, f, d0, d1, n);
     NBG_HIP(hipGetLastError());
     wait_host_word(c, fin + kDevCnt + 8, fseq);
@@ -2971,6 +2986,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       if (int64_t(fin[D_ARENA]) > d.cap_arena) return dv_abort(true);
       return false;
     }
+    c.timing.launches += nl;
     if (fin[D_WALKERR] && !(f.diag & 4))
       throw Error(NBG_E_UNKNOWN, "shortest path: in-edge keys without mirrored out-edges on a shortest path");
 

@@ -269,6 +269,8 @@ def test_configs2_rmat26_bench_query_digest():
                 if dev:
                     # one counter wait per BFS iteration + the results (round 4: 16 fetches)
                     assert tm["spec_hops"] == 1 and tm["host_waits"] <= 6, (tm["spec_hops"], tm["host_waits"])
+                    # one fixed launch chain (round 4: ~70 launches with 16 counter fetches)
+                    assert 0 < tm["launches"] <= 40, tm["launches"]
             sp.set_option("sp_dev", 1)
     finally:
         sp.close()
