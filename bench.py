@@ -388,6 +388,9 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
             "reachable": int((np.asarray(hops) >= 0).sum()),
             "hops_histogram": {int(h): int((np.asarray(hops) == h).sum()) for h in sorted(set(np.asarray(hops).tolist()))},
             "bfs_iterations": iters,
+            # the last query's batch: host waits and kernel launches (the device-driven chain)
+            "host_waits": tm["host_waits"], "kernel_launches": tm.get("launches"),
+            "device_driven_batches": tm["spec_hops"],
             "launches": launches,
             "snapshot_build_s": round(build_s, 2),
         },
