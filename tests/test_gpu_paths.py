@@ -3,7 +3,8 @@
 The reference has no implementation (src/graph/FindExecutor.cpp:20-22), so the oracle
 (oracle/refcpu.cpp ora_shortest_path: backward BFS from dst over the in-edge keys + greedy
 smallest-vid walk from src) is the definition; no reference fixture pins it ("parity unpinned"
-in DESIGN.md).  Hop counts and whole paths must match bit-exactly.
+in DESIGN.md), and tests/test_oracle_paths_independent.py pins the oracle to an independent
+restatement (scipy BFS over the raw edge list).  Hop counts and whole paths must match bit-exactly.
 """
 import numpy as np
 import pytest
