@@ -311,7 +311,10 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
                  "claims": h["c"][2], "iter": h["c"][4],
                  "kernel": h.get("kernels", ["?"])[0].replace("(anonymous namespace)::", "")} for h in tm["hops"]]
     for rec, h in zip(launches, tm["hops"]):
-        if h["c"][6] or h["c"][7]:  # option sp_sweep_stats: distinct scanned vertices, their degrees
+        if rec["kind"] == "probe" and (h["c"][6] or h["c"][7]):
+            # option sp_dv_diag bit 3: the meet probe's filter statistics
+            rec.update(pair_filter_passes=h["c"][6], distance_bytes_read=h["c"][2], bytes_at_depth=h["c"][7])
+        elif h["c"][6] or h["c"][7]:  # option sp_sweep_stats: distinct scanned vertices, their degrees
             rec.update(distinct_x=h["c"][6], distinct_entries=h["c"][7])
     # parity: the last result (host copy) against the committed digest
     hops, paths, srcs = r.hops, r.paths, r.src

@@ -1733,6 +1733,10 @@ __global__ __launch_bounds__(256) void k_dv_probe(SpDev d, SpState st, SpFilt f,
   if (total == 0) return;  // nothing selected (grid-uniform)
   const uint32_t B = uint32_t(st.B);
   unsigned long long examined = 0;
+  // option sp_dv_diag bit 3 (diagnostics): entries passing the pair filter, distance bytes read
+  // (entries passing both filters), bytes at the wanted depth -- counters Q_W-3 .. Q_W-1
+  const bool stats = (f.diag & 8) != 0;
+  unsigned long long n_pf = 0, n_rd = 0, n_hit = 0;
   chunk_groups(
       total,
       [&](int64_t c, ChunkRec& r) {
@@ -1770,11 +1774,15 @@ __global__ __launch_bounds__(256) void k_dv_probe(SpDev d, SpState st, SpFilt f,
 #pragma unroll
             for (int u = 0; u < U; u++) {
               const bool pv = pf_on ? pf_test(prow, w[u], f.k2 != 0) : true;
+              if (stats) n_pf += (w[u] != 0xFFFFFFFFu && pv) ? 1u : 0u;
               fm |= (w[u] != 0xFFFFFFFFu && pv && gf_test(f, o, need, p, w[u])) ? 1u << u : 0u;
             }
 #pragma unroll
-            for (int u = 0; u < U; u++)
-              hit = (((fm >> u) & 1u) && uint32_t(odp[uint64_t(w[u]) << sh]) == uint32_t(need)) || hit;
+            for (int u = 0; u < U; u++) {
+              const bool h = ((fm >> u) & 1u) && uint32_t(odp[uint64_t(w[u]) << sh]) == uint32_t(need);
+              if (stats) n_rd += (fm >> u) & 1u, n_hit += h ? 1u : 0u;
+              hit = h || hit;
+            }
           }
           examined += uint64_t(min(x + 64 * U, r.x1) - max(x, r.x0)) * (lane == 0);
           if (__ballot(hit)) {
@@ -1788,6 +1796,11 @@ __global__ __launch_bounds__(256) void k_dv_probe(SpDev d, SpState st, SpFilt f,
         }
       });
   blk_add(q + Q_PE, examined);
+  if (stats) {
+    blk_add(q + (Q_W - 3), n_pf);
+    blk_add(q + (Q_W - 2), n_rd);
+    blk_add(q + (Q_W - 1), n_hit);
+  }
 }
 
 // stage a wave-uniform batch of claims (lanes with `claimed`) into the wave's LDS buffer, flushing
@@ -3005,7 +3018,9 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         c.timing.expand_launches++;
         c.timing.edges_scanned += q[Q_PE];
         c.timing.expand_bytes += q[Q_X] * 24 + q[Q_PE] * 5;
-        const unsigned long long c8[8] = {q[Q_X], q[Q_PE], 0, fin[D_MEET], (unsigned long long)i, act, 0, 0};
+        // (diag bit 3: c[2] distance bytes read, c[6] pair-filter passes, c[7] bytes at the depth)
+        const unsigned long long c8[8] = {q[Q_X], q[Q_PE], q[Q_W - 2], fin[D_MEET], (unsigned long long)i, act,
+                                          q[Q_W - 3], q[Q_W - 1]};
         c.timing.hop(3, false, pms, c8);
         c.timing.name_last_hop("nbg::(anonymous namespace)::k_dv_probe");
       }
