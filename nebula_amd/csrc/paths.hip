@@ -1507,8 +1507,9 @@ __global__ __launch_bounds__(256) void k_dv_begin(SpDev d, SpState st, SpCsr gou
     st.deg[p] = st.deg[B + p] = 0;
     go = sv != tv && a >= 0 && b >= 0 && max_steps >= 1;
     if (go) {
-      claim_byte(d0, didx(st, uint32_t(p), uint32_t(a), n), 0);
-      claim_byte(d1, didx(st, uint32_t(p), uint32_t(b), n), 0);
+      // the batch's bytes are all unseen here and no other thread writes these two: plain stores
+      d0[didx(st, uint32_t(p), uint32_t(a), n)] = 0;
+      d1[didx(st, uint32_t(p), uint32_t(b), n)] = 0;
       const unsigned long long df = (unsigned long long)sp_deg(gout, uint32_t(a)) + 1;
       const unsigned long long db = (unsigned long long)sp_deg(gin, uint32_t(b)) + 1;
       const int s = df <= db ? 0 : 1;
@@ -2116,7 +2117,8 @@ __global__ __launch_bounds__(kBlk) void k_dv_post(SpDev d, SpState st, SpCsr gou
                                                   const int64_t* ht_keys, const int32_t* ht_vals, uint64_t ht_mask,
                                                   bool ht_has_min, int32_t ht_min_gidx) {
   const int32_t B = st.B;
-  if (blockIdx.x == 0) dv_path_offsets(st, B, d.doff);
+  // the path offsets by the last block, beside the walk front the first blocks build
+  if (blockIdx.x == gridDim.x - 1) dv_path_offsets(st, B, d.doff);
   dv_walk_front(d, st, gout, 0, lo, ht_keys, ht_vals, ht_mask, ht_has_min, ht_min_gidx);
   const int64_t gn = int64_t(gridDim.x) * blockDim.x;
   const int64_t nm = min(int64_t((*gcnt(d.cnt, D_MEET))), d.cap_meet);
