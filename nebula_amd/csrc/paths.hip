@@ -1485,9 +1485,11 @@ __device__ inline void dv_publish_last(unsigned long long* cnt, int q, unsigned 
 __global__ __launch_bounds__(256) void k_dv_begin(SpDev d, SpState st, SpCsr gout, SpCsr gin, uint8_t* d0, uint8_t* d1,
                                                   int64_t n, int32_t max_steps, const int64_t* ht_keys,
                                                   const int32_t* ht_vals, uint64_t ht_mask, bool ht_has_min,
-                                                  int32_t ht_min_gidx) {
+                                                  int32_t ht_min_gidx, int32_t sel1) {
   const int32_t B = st.B;
   const int64_t gt = int64_t(blockIdx.x) * blockDim.x + threadIdx.x, gn = int64_t(gridDim.x) * blockDim.x;
+  int32_t s1 = 0;   // the side pair gt expands in iteration 1
+  int64_t dg1 = 0;  // its root's degree there
   // pull and push adjacent, 64-byte aligned, 2 kMaxQ B words: 16-byte stores
   for (int64_t i = gt; i < int64_t(kMaxQ) * B; i += gn) reinterpret_cast<uint4*>(d.pull)[i] = make_uint4(0u, 0u, 0u, 0u);
   bool go = false;
@@ -1513,6 +1515,8 @@ __global__ __launch_bounds__(256) void k_dv_begin(SpDev d, SpState st, SpCsr gou
       const unsigned long long df = (unsigned long long)sp_deg(gout, uint32_t(a)) + 1;
       const unsigned long long db = (unsigned long long)sp_deg(gin, uint32_t(b)) + 1;
       const int s = df <= db ? 0 : 1;
+      s1 = s;
+      dg1 = int64_t(s == 0 ? df : db) - 1;
       st.side[p] = s;
       st.deg[p] = s == 0 ? 0ull : df;  // the expanding side's sum restarts (the expansion adds)
       st.deg[B + p] = s == 1 ? 0ull : db;
@@ -1542,6 +1546,52 @@ __global__ __launch_bounds__(256) void k_dv_begin(SpDev d, SpState st, SpCsr gou
     atomicAdd(q0 + Q_LIVE0, nw);
     atomicAdd(q0 + Q_LIVE1, nw);
     atomicAdd(gcnt(d.cnt, D_ARENA), 2 * nw);
+  }
+  if (!sel1) return;  // (grid-uniform) k_dv_select builds iteration 1's tables
+  // iteration 1's tables, which k_dv_select would build from the lists above: the expanding root
+  // of active pair k is X entry k with its chunk range, the other root is carried into iteration
+  // 1's list of its side (one launch and its dependent chain less per batch)
+  const QBlk q1 = qblk(d.cnt, 1);
+  const int lane = threadIdx.x & 63;
+  const int64_t nc = go ? (dg1 + (int64_t(1) << d.lg_chb) - 1) >> d.lg_chb : 0;
+  int64_t inc = nc;  // inclusive wave scan of the chunk counts
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  const int64_t wtot = __shfl(inc, 63);
+  unsigned long long cb = 0;
+  if (lane == 0 && wtot) cb = atomicAdd(q1 + Q_NCH, (unsigned long long)wtot);
+  const int64_t ca = int64_t(__shfl(cb, 0)) + inc - nc;
+  const bool fit = go && k < d.cap_x && ca + nc <= d.cap_ch;
+  if (go) {
+    if (fit) {
+      d.X[k] = mk_tup(uint32_t(s1), pp, 0, uint32_t(s1 ? b : a));
+      d.Xcb[k] = ca;
+    } else {
+      atomicOr(gcnt(d.cnt, D_OVF), 2ull);
+    }
+  }
+  wave_fill_val(ca, fit ? nc : 0, k, [&](int64_t c, int64_t v) {
+    d.chx[c] = int32_t(v);
+    d.slot[c] = ~0ull;
+  });
+  const int64_t c0 = wave_append(q1 + Q_LIVE0, go && s1 == 1);  // side 0's root carried
+  const int64_t c1 = wave_append(q1 + Q_LIVE1, go && s1 == 0);  // side 1's root carried
+  if (go && s1 == 1) {
+    if (c0 < d.cap_live) d.live[1][0][c0] = mk_tup(0, pp, 0, uint32_t(a));
+    else atomicOr(gcnt(d.cnt, D_OVF), 2ull);
+  }
+  if (go && s1 == 0) {
+    if (c1 < d.cap_live) d.live[1][1][c1] = mk_tup(1, pp, 0, uint32_t(b));
+    else atomicOr(gcnt(d.cnt, D_OVF), 2ull);
+  }
+  unsigned long long esum = go ? (unsigned long long)dg1 : 0ull;
+  esum = wsum(esum);
+  if (lane == 0 && m) {
+    atomicAdd(q1 + Q_X, (unsigned long long)__popcll(m));
+    if (esum) atomicAdd(q1 + Q_XE, esum);
   }
 }
 
@@ -2913,11 +2963,15 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     };
 
     ++nl;
+    // iteration 1's select folded into the batch start (option sp_dv_begin_x)
+    const int32_t sel1 = c.opt("sp_dv_begin_x", 1) != 0 ? 1 : 0;
     k_dv_begin<<<std::max(grid_n(nb, 1 << 20), 64), 256, 0, c.stream>>>(d, st, gout, gin, d0, d1, n, max_steps, htk, htv,
-                                                          uint64_t(htm), c.ht_has_min, c.ht_min_gidx);
+                                                          uint64_t(htm), c.ht_has_min, c.ht_min_gidx, sel1);
     auto enqueue = [&](int it) {
-      ++nl;
-      k_dv_select<<<gsel((const void*)k_dv_select), kBlk, 0, c.stream>>>(d, st, gout, gin, it);
+      if (it > 1 || !sel1) {
+        ++nl;
+        k_dv_select<<<gsel((const void*)k_dv_select), kBlk, 0, c.stream>>>(d, st, gout, gin, it);
+      }
       evi[size_t(it)][0] = dv_event();
       if (probe) {
         ++nl;

@@ -213,6 +213,25 @@ def test_distance_layouts_match_oracle(rmat, dev, ilv, vmajor):
         sp.set_option("sp_vmajor", 0)
 
 
+@pytest.mark.parametrize("begin_x", [1, 0])
+def test_first_iteration_tables_from_batch_start(rmat, begin_x):
+    """iteration 1's X table, chunk ranges and carried roots built by the batch start kernel
+    (sp_dv_begin_x, default) or by k_dv_select from the depth-0 lists: the oracle's paths, with
+    roots of degree 0, src == dst and unknown vids among the pairs"""
+    scale, sp, st = rmat
+    s, t = synth.pairs(scale, 16, 1, 300, pick_seed=41)
+    es, et_ = edge_case_pairs(scale)
+    src, dst = np.concatenate([s, es]), np.concatenate([t, et_])
+    sp.set_option("sp_dv_begin_x", begin_x)
+    try:
+        for max_steps in (1, 3, 8):
+            got = sp.shortest_path(src, dst, FOLLOW, max_steps).rows()
+            assert got == oracle_paths(st, src, dst, FOLLOW, max_steps), max_steps
+            assert sp.last_timing()["spec_hops"] >= 1
+    finally:
+        sp.unset_option("sp_dv_begin_x")
+
+
 @pytest.mark.parametrize("push,walk_wg,sweep_src", [(0, 0, 0), (1, 0, 0), (1, 1, 0), (0, 0, 1), (1, 0, 1)])
 def test_sweep_direction_and_walk_variants(rmat, push, walk_wg, sweep_src):
     """the sweep's per-pair push/pull choice (forced off: pull only), the workgroup-per-pair walk
