@@ -41,10 +41,18 @@ def hop_kernels(h):
     return h.get("kernels") or ["nbg::k_expand"]
 
 
-def pmc_traffic(workload: str, prefixes):
+def same_model(a, b, tol=0.01):
+    """the profiled run and this run moved the same algorithmic bytes (within tol): the profile's
+    counters describe this tree's kernel on this workload, not an older one"""
+    return a is not None and b is not None and abs(float(a) - float(b)) <= tol * max(float(a), float(b), 1.0)
+
+
+def pmc_traffic(workload: str, prefixes, model_bytes=None):
     """HBM bytes per launch of the given kernels from the newest committed rocprof PMC summary of
     the same workload (profiles/<tag>_summary.json: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE,
-    separate --pmc passes, tools/gpu_profile.sh + tools/profile_summary.py).  None if absent."""
+    separate --pmc passes, tools/gpu_profile.sh + tools/profile_summary.py) whose bench line
+    recorded the same algorithmic bytes per launch as this run (model_bytes; a profile of an older
+    tree whose kernel moved other bytes is skipped).  None if absent."""
     best = None
     # newest round tag last (r01b < r01c < ... < r02a); file mtimes are meaningless in a checkout
     for f in sorted((ROOT / "profiles").glob("*_summary.json"), key=lambda p: p.name):
@@ -54,6 +62,9 @@ def pmc_traffic(workload: str, prefixes):
             continue
         b = d.get("bench") or {}
         if (b.get("config") or {}).get("workload") != workload:
+            continue
+        if model_bytes is not None and not same_model((b.get("roofline") or {}).get("algorithmic_bytes_per_launch"),
+                                                      model_bytes):
             continue
         tot, raw, hit = 0.0, 0.0, 0
         for pre in prefixes:
@@ -69,10 +80,11 @@ def pmc_traffic(workload: str, prefixes):
     return best
 
 
-def pmc_traffic_query(workload: str, kind: str):
+def pmc_traffic_query(workload: str, kind: str, model_bytes=None):
     """HBM bytes per query of one scan kind (all its launches of one query) from the newest
     committed C4 PMC summary of the same workload (profiles/<tag>_c4.json, tools/c4_counters.sh +
-    tools/c4_summary.py: FETCH_SIZE x2 + WRITE_SIZE per dispatch).  None if absent."""
+    tools/c4_summary.py: FETCH_SIZE x2 + WRITE_SIZE per dispatch) whose byte model of that kind
+    equals this run's (model_bytes, within 1 %).  None if absent."""
     best = None
     for f in sorted((ROOT / "profiles").glob("*_c4.json"), key=lambda p: p.name):
         try:
@@ -82,7 +94,7 @@ def pmc_traffic_query(workload: str, kind: str):
         if ((d.get("bench") or {}).get("config") or {}).get("workload") != workload:
             continue
         k = (d.get("query_kinds") or {}).get(kind)
-        if k and k.get("complete"):
+        if k and k.get("complete") and (model_bytes is None or same_model(k.get("model_bytes"), model_bytes)):
             best = {"bytes": k["fetch_bytes_x2"] + k["write_bytes"],
                     "raw_bytes": k["fetch_bytes_x2"] / 2 + k["write_bytes"],
                     "model_bytes": k["model_bytes"], "launches": k["launches"], "source": f"profiles/{f.name}"}
@@ -367,7 +379,7 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
     dl = [l for l in launches if l["kind"] == dom]
     if dl:
         kern[dom] = max(dl, key=lambda l: l["ms"])["kernel"]
-    tr = pmc_traffic_query(workload, dom)
+    tr = pmc_traffic_query(workload, dom, dk["bytes"])
     out = {
         "metric": "FIND SHORTEST PATH pairs/s (batched bidirectional BFS) on RMAT-26",
         "value": args.pairs * args.steps / dt,
@@ -382,8 +394,10 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
         "dtype": "int64",
         "data": "synthetic RMAT (Graph500 a/b/c=0.57/0.19/0.19, seed 1) generated on device",
         "config": {
-            "parallelism": f"pairs sharded i % {world} over the ranks, replicated CSRs" if world > 1 else "1 GPU",
-            "communicator": sp.comm_info() if world > 1 else None,
+            "parallelism": (f"pairs sharded i % {world} over the ranks, replicated CSRs" if world > 1 else
+                            "1 GPU, replicas assembled through a one-rank RCCL communicator" if args.comm_single
+                            else "1 GPU"),
+            "communicator": sp.comm_info() if world > 1 or args.comm_single else None,
             "workload": workload,
             "vertices": info["num_vertices"],
             "edges_examined_per_query": edges // max(args.steps, 1),
@@ -511,6 +525,9 @@ def main():
     ap.add_argument("--plain", action="store_true",
                     help="GO without WHERE / DISTINCT (configs[1]: RMAT-22 3 steps, configs[4]: RMAT-28 2 steps)")
     ap.add_argument("--max-steps", type=int, default=8)
+    ap.add_argument("--comm-single", action="store_true",
+                    help="one GPU through a one-rank RCCL communicator: the sharded algorithm with every "
+                         "exchange issued to RCCL (the rank's own slice sent to itself)")
     ap.add_argument("--launch-check", action="store_true",
                     help="only bring the ranks up (gloo init, barrier, all-reduce) and print one JSON line")
     args = ap.parse_args()
@@ -537,13 +554,17 @@ def main():
 
     golden = json.loads(GOLDEN.read_text()) if GOLDEN.exists() else {}
     sp = GraphSpace(64, device=local, rank=rank, world_size=world)
+    for kv in args.option:
+        k, v = kv.split("=")
+        sp.set_option(k, int(v))
+    single = args.comm_single and world == 1
     if world > 1:
         uid = [GraphSpace.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         sp.comm_init(uid[0])
-    for kv in args.option:
-        k, v = kv.split("=")
-        sp.set_option(k, int(v))
+    elif single:
+        sp.set_option("comm_single", 1)
+        sp.comm_init(GraphSpace.comm_unique_id())
     FOLLOW = 1
     sp.set_edge_schema(FOLLOW, [("weight", 2)])
     t0 = time.time()
@@ -551,7 +572,8 @@ def main():
     sp.finalize()
     build_s = time.time() - t0
     info = sp.info(FOLLOW)
-    comm_seen = sp.comm_info() if world > 1 else None  # ncclCommCount of the engine's communicator
+    sharded = world > 1 or single
+    comm_seen = sp.comm_info() if sharded else None  # ncclCommCount of the engine's communicator
     if args.workload == "paths":
         return bench_paths(args, sp, info, build_s, rank, world, golden, dist)
     starts = synth.seeds(args.scale, args.edge_factor, 1, args.seeds)
@@ -605,6 +627,7 @@ def main():
     exp_ms = 0.0
     exp_bytes = 0
     tot_ms = comm_ms = 0.0
+    comm_calls = 0
     tot_each = []
     comm_bytes = 0
     bu_steps = 0
@@ -618,6 +641,7 @@ def main():
         tot_each.append(round(t["total_ms"], 3))
         comm_ms += t["comm_ms"]
         comm_bytes += t["comm_bytes"]
+        comm_calls += t["comm_calls"]
         bu_steps = t["bu_steps"]
         hop_stats = t["hops"]
         for i, h in enumerate(hop_stats):
@@ -650,7 +674,7 @@ def main():
         dom_names = hop_kernels(dh)
         kach = k_bytes[dom] / (k_ms[dom] / 1e3) / 1e9 if k_ms[dom] > 0 else 0.0
         hach = hop_bytes[dom] / (hop_ms[dom] / 1e3) / 1e9 if hop_ms[dom] > 0 else 0.0
-        tr = pmc_traffic(workload, dom_names[:1])
+        tr = pmc_traffic(workload, dom_names[:1], k_bytes[dom] // K)
         roof = {
             "bound": "hbm",
             "kernel": dom_names[0] + f" (hop {dom + 1} of {len(hop_stats)})",
@@ -738,17 +762,20 @@ def main():
                 "query_end_to_end_ms": round(e2e_ms, 4),
                 "result_d2h_ms": round(e2e_ms - dt / args.steps * 1e3, 4),
                 "snapshot_build_s": round(build_s, 2),
-                "parallelism": f"part%{world} sharding, RCCL frontier exchange" if world > 1 else "1 GPU",
+                "parallelism": (f"part%{world} sharding, RCCL frontier exchange" if world > 1 else
+                                "1 GPU, sharded algorithm through a one-rank RCCL communicator" if single else "1 GPU"),
                 "hub_seeds": hubs or None,
             },
             "parity": parity,
             "roofline": roof,
             "cpu_baseline": None,
         }
-        if world > 1:
+        if sharded:
             out["comm"] = {"backend": "rccl (nbg_comm_init over ncclCommInitRank)", "ranks": world,
                            "communicator": comm_seen,
-                           "comm_ms_per_query_rank0": comm_ms / K, "comm_bytes_per_query_rank0": comm_bytes // K}
+                           "comm_ms_per_query_rank0": comm_ms / K, "comm_bytes_per_query_rank0": comm_bytes // K,
+                           "collectives_per_query_rank0": comm_calls / K,
+                           "ms_per_collective_rank0": comm_ms / comm_calls if comm_calls else None}
         if world == 1 and not args.no_cpu and not args.plain:
             try:
                 out["cpu_baseline"] = cpu_baseline(args.cpu_scale, args.where, golden)

@@ -87,7 +87,7 @@ int32_t nbg_comm_info(nbg_ctx* ctx, int32_t* ranks, int32_t* transport);
  * nbg_hop_stat, nbg_snapshot_info, nbg_go_spec, nbg_rows) change layout between versions: an
  * integration compares nbg_abi_version() with the NBG_ABI_VERSION it was built against and
  * refuses to run on a mismatch (INTEGRATION.md "ABI versioning").                          */
-#define NBG_ABI_VERSION 5
+#define NBG_ABI_VERSION 6
 int32_t nbg_abi_version(void);
 /* sizeof of the caller-allocated structs as the library was built: 0 nbg_timing, 1
  * nbg_hop_stat, 2 nbg_snapshot_info, 3 nbg_go_spec, 4 nbg_rows, 5 nbg_prop_def; -1 otherwise */
@@ -298,7 +298,9 @@ typedef struct {
 } nbg_hop_stat;
 #define NBG_MAX_HOP_STATS 16
 typedef struct {
-  double total_ms;        /* device time of the last nbg_go / nbg_get_bound                  */
+  double total_ms;        /* device time of the last nbg_go / nbg_get_bound (events around the
+                             whole call; 0 for nbg_go with option hop_timing = 0, which records
+                             no event at all)                                                  */
   double expand_ms;       /* summed time of the expansion kernels                            */
   int64_t expand_launches;
   uint64_t edges_scanned;
@@ -317,6 +319,9 @@ typedef struct {
                              host-driven: option sp_dev = 0, or a list overflow re-ran them)   */
   int32_t launches;       /* nbg_shortest_path: kernel launches of its device-driven batches
                              (ABI 5; 0 for other calls)                                         */
+  int32_t comm_calls;     /* collectives this rank issued through its communicator in the last
+                             call (ABI 6; comm_ms / comm_calls = the mean time of one on the
+                             engine stream, enqueue to completion)                              */
 } nbg_timing;
 int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out);
 /* engine option key = value (tuning knobs); value INT64_MIN removes the key, so the

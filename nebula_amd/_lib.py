@@ -22,7 +22,7 @@ ERRORS = {
 }
 T_BOOL, T_INT, T_VID, T_FLOAT, T_DOUBLE, T_STRING, T_TIMESTAMP = 1, 2, 3, 4, 5, 6, 21
 OWNER_SOURCE, OWNER_DEST, OWNER_EDGE = 1, 2, 3
-ABI_VERSION = 5  # NBG_ABI_VERSION of include/nebula_amd.h
+ABI_VERSION = 6  # NBG_ABI_VERSION of include/nebula_amd.h
 
 # every symbol the header declares (tests/test_capi.py checks the .so exports them all)
 EXPORTS = [
@@ -92,7 +92,8 @@ class Timing(C.Structure):
                 ("edges_scanned", C.c_uint64), ("expand_bytes", C.c_uint64), ("steps_run", C.c_int32),
                 ("bu_steps", C.c_int32), ("comm_ms", C.c_double), ("comm_bytes", C.c_uint64),
                 ("n_hops", C.c_int32), ("hops", HopStat * MAX_HOP_STATS), ("host_waits", C.c_int32),
-                ("spec_hops", C.c_int32), ("launches", C.c_int32)]
+                ("spec_hops", C.c_int32), ("launches", C.c_int32),
+                ("comm_calls", C.c_int32)]
 
 
 _lib = None

@@ -86,6 +86,7 @@ nbg_ctx* nbg_ctx_create(int32_t device, int32_t num_parts, int32_t rank, int32_t
   ctx->c.num_parts = num_parts;
   ctx->c.rank = rank;
   ctx->c.world = world_size;
+  ctx->c.sharded = world_size > 1;
   if (hipStreamCreateWithFlags(&ctx->c.stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return nullptr;
@@ -374,6 +375,7 @@ int32_t nbg_last_timing(nbg_ctx* ctx, nbg_timing* out) {
     out->host_waits = c.timing.host_waits;
     out->spec_hops = c.timing.spec_hops;
     out->launches = c.timing.launches;
+    out->comm_calls = c.timing.comm_calls;
     return NBG_OK;
   });
 }

@@ -45,6 +45,10 @@ struct CommImpl {
 // ------------------------------------------------------------------------------------------
 struct RcclComm : CommImpl {
   ncclComm_t comm = nullptr;
+  // self_p2p: the rank's own slice also goes through ncclSend / ncclRecv to itself (a one-rank
+  // communicator, option comm_single, runs every RCCL entry point on a one-GPU box); otherwise it
+  // is a device-to-device copy beside the grouped transfers
+  bool self_p2p = false;
   int32_t ranks() const override {
     int n = 0;
     return ncclCommCount(comm, &n) == ncclSuccess ? int32_t(n) : -1;
@@ -53,35 +57,48 @@ struct RcclComm : CommImpl {
   ~RcclComm() override {
     if (comm) ncclCommDestroy(comm);
   }
+  bool skip(const Ctx& c, int p) const { return p == c.rank && !self_p2p; }
+  void self_copy(Ctx& c, void* dst, const void* src, size_t bytes) {
+    if (!self_p2p && bytes && dst != src) NBG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c.stream));
+  }
+  // point-to-point transfers in pieces of at most msg bytes (option comm_chunk_mb, default 1024):
+  // both sides split a transfer identically, and RCCL pairs the pieces of one peer pair in issue
+  // order (see DESIGN.md section 4 for the measured reason)
+  size_t msg = size_t(1) << 30;
+  void p2p_send(const void* buf, size_t bytes, int peer, hipStream_t s) {
+    for (size_t o = 0; o < bytes; o += msg)
+      NBG_NCCL(ncclSend(static_cast<const uint8_t*>(buf) + o, std::min(msg, bytes - o), ncclUint8, peer, comm, s));
+  }
+  void p2p_recv(void* buf, size_t bytes, int peer, hipStream_t s) {
+    for (size_t o = 0; o < bytes; o += msg)
+      NBG_NCCL(ncclRecv(static_cast<uint8_t*>(buf) + o, std::min(msg, bytes - o), ncclUint8, peer, comm, s));
+  }
   void allgatherv(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
                   const size_t* recv_off) override {
     NBG_NCCL(ncclGroupStart());
     for (int p = 0; p < c.world; p++) {
-      if (p == c.rank) continue;
-      if (send_bytes) NBG_NCCL(ncclSend(send, send_bytes, ncclUint8, p, comm, c.stream));
-      if (recv_bytes[p])
-        NBG_NCCL(ncclRecv(static_cast<uint8_t*>(recv) + recv_off[p], recv_bytes[p], ncclUint8, p, comm, c.stream));
+      if (skip(c, p)) continue;
+      if (p == c.rank && static_cast<uint8_t*>(recv) + recv_off[p] == send) {
+        // in place: the own slice is already where it belongs
+      } else {
+        p2p_send(send, send_bytes, p, c.stream);
+        p2p_recv(static_cast<uint8_t*>(recv) + recv_off[p], recv_bytes[p], p, c.stream);
+      }
     }
     NBG_NCCL(ncclGroupEnd());
-    if (send_bytes && static_cast<uint8_t*>(recv) + recv_off[c.rank] != send)
-      NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[c.rank], send, send_bytes,
-                             hipMemcpyDeviceToDevice, c.stream));
+    self_copy(c, static_cast<uint8_t*>(recv) + recv_off[c.rank], send, send_bytes);
   }
   void alltoallv(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
                  const size_t* recv_bytes, const size_t* recv_off) override {
     NBG_NCCL(ncclGroupStart());
     for (int p = 0; p < c.world; p++) {
-      if (p == c.rank) continue;
-      if (send_bytes[p])
-        NBG_NCCL(ncclSend(static_cast<const uint8_t*>(send) + send_off[p], send_bytes[p], ncclUint8, p, comm, c.stream));
-      if (recv_bytes[p])
-        NBG_NCCL(ncclRecv(static_cast<uint8_t*>(recv) + recv_off[p], recv_bytes[p], ncclUint8, p, comm, c.stream));
+      if (skip(c, p)) continue;
+      p2p_send(static_cast<const uint8_t*>(send) + send_off[p], send_bytes[p], p, c.stream);
+      p2p_recv(static_cast<uint8_t*>(recv) + recv_off[p], recv_bytes[p], p, c.stream);
     }
     NBG_NCCL(ncclGroupEnd());
-    if (send_bytes[c.rank])
-      NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[c.rank],
-                             static_cast<const uint8_t*>(send) + send_off[c.rank], send_bytes[c.rank],
-                             hipMemcpyDeviceToDevice, c.stream));
+    self_copy(c, static_cast<uint8_t*>(recv) + recv_off[c.rank], static_cast<const uint8_t*>(send) + send_off[c.rank],
+              send_bytes[c.rank]);
   }
   void allreduce_sum_i64(Ctx& c, int64_t* d, size_t n) override {
     NBG_NCCL(ncclAllReduce(d, d, n, ncclInt64, ncclSum, comm, c.stream));
@@ -90,19 +107,19 @@ struct RcclComm : CommImpl {
                    const size_t* recv_off, const void* send2, size_t bytes2, void* recv2) override {
     NBG_NCCL(ncclGroupStart());
     for (int p = 0; p < c.world; p++) {
-      if (p == c.rank) continue;
-      if (send_bytes) NBG_NCCL(ncclSend(send, send_bytes, ncclUint8, p, comm, c.stream));
-      if (recv_bytes[p])
-        NBG_NCCL(ncclRecv(static_cast<uint8_t*>(recv) + recv_off[p], recv_bytes[p], ncclUint8, p, comm, c.stream));
-      NBG_NCCL(ncclSend(send2, bytes2, ncclUint8, p, comm, c.stream));
-      NBG_NCCL(ncclRecv(static_cast<uint8_t*>(recv2) + size_t(p) * bytes2, bytes2, ncclUint8, p, comm, c.stream));
+      if (skip(c, p)) continue;
+      if (p == c.rank && static_cast<uint8_t*>(recv) + recv_off[p] == send) {
+        // in place: the own slice is already where it belongs
+      } else {
+        p2p_send(send, send_bytes, p, c.stream);
+        p2p_recv(static_cast<uint8_t*>(recv) + recv_off[p], recv_bytes[p], p, c.stream);
+      }
+      p2p_send(send2, bytes2, p, c.stream);
+      p2p_recv(static_cast<uint8_t*>(recv2) + size_t(p) * bytes2, bytes2, p, c.stream);
     }
     NBG_NCCL(ncclGroupEnd());
-    if (send_bytes && static_cast<uint8_t*>(recv) + recv_off[c.rank] != send)
-      NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[c.rank], send, send_bytes,
-                             hipMemcpyDeviceToDevice, c.stream));
-    NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv2) + size_t(c.rank) * bytes2, send2, bytes2,
-                           hipMemcpyDeviceToDevice, c.stream));
+    self_copy(c, static_cast<uint8_t*>(recv) + recv_off[c.rank], send, send_bytes);
+    self_copy(c, static_cast<uint8_t*>(recv2) + size_t(c.rank) * bytes2, send2, bytes2);
   }
 };
 
@@ -280,6 +297,7 @@ struct LocalComm : CommImpl {
 
 static CommImpl* impl(Ctx& c) {
   if (!c.comm) throw Error(NBG_E_STATE, "multi-rank context without a communicator (nbg_comm_init)");
+  c.timing.comm_calls++;
   return static_cast<CommImpl*>(c.comm);
 }
 
@@ -292,13 +310,21 @@ int32_t comm_unique_id(uint8_t out[128]) {
   return NBG_OK;
 }
 
+// world > 1: the rank's RCCL communicator.  world == 1: nothing, unless option comm_single = 1
+// (set before the snapshot is built): then a one-rank RCCL communicator is formed and the
+// context runs the sharded algorithm through it (every exchange, its own slice sent to itself)
 void comm_init(Ctx& c, const uint8_t id_bytes[128]) {
-  if (c.world == 1) return;
+  const bool single = c.world == 1 && c.opt("comm_single", 0) != 0;
+  if (c.world == 1 && !single) return;
   if (c.comm) throw Error(NBG_E_STATE, "communicator already initialised");
+  if (single && (c.finalized || c.n_global > 0))
+    throw Error(NBG_E_STATE, "comm_single: initialise the communicator before the snapshot is built");
   ncclUniqueId id;
   memcpy(&id, id_bytes, 128);
   NBG_HIP(hipSetDevice(c.device));
   auto* r = new RcclComm();
+  r->self_p2p = single || c.opt("comm_self_p2p", 0) != 0;
+  r->msg = size_t(std::max<int64_t>(1, c.opt("comm_chunk_mb", 1024))) << 20;
   pool_trim_all();  // RCCL's buffers come from the driver, which never trims the block caches
   ncclResult_t rc = ncclCommInitRank(&r->comm, c.world, id, c.rank);
   if (rc != ncclSuccess) {
@@ -307,6 +333,7 @@ void comm_init(Ctx& c, const uint8_t id_bytes[128]) {
     throw Error(NBG_E_COMM, std::string("ncclCommInitRank: ") + ncclGetErrorString(rc));
   }
   c.comm = r;
+  c.sharded = true;
 }
 
 void comm_init_local(Ctx& c, int64_t key) {
@@ -360,7 +387,7 @@ void comm_destroy(Ctx& c) {
 }
 
 void comm_allgather_bytes(Ctx& c, const void* send, size_t bytes_each, void* recv) {
-  if (c.world == 1) {
+  if (!c.sharded) {
     NBG_HIP(hipMemcpyAsync(recv, send, bytes_each, hipMemcpyDeviceToDevice, c.stream));
     return;
   }
@@ -371,7 +398,7 @@ void comm_allgather_bytes(Ctx& c, const void* send, size_t bytes_each, void* rec
 
 void comm_allgatherv_bytes(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
                            const size_t* recv_off) {
-  if (c.world == 1) {
+  if (!c.sharded) {
     if (send_bytes && static_cast<uint8_t*>(recv) + recv_off[0] != send)
       NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[0], send, send_bytes, hipMemcpyDeviceToDevice,
                              c.stream));
@@ -382,7 +409,7 @@ void comm_allgatherv_bytes(Ctx& c, const void* send, size_t send_bytes, void* re
 
 void comm_alltoallv_bytes(Ctx& c, const void* send, const size_t* send_bytes, const size_t* send_off, void* recv,
                           const size_t* recv_bytes, const size_t* recv_off) {
-  if (c.world == 1) {
+  if (!c.sharded) {
     if (send_bytes[0])
       NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[0],
                              static_cast<const uint8_t*>(send) + send_off[0], send_bytes[0],
@@ -394,7 +421,7 @@ void comm_alltoallv_bytes(Ctx& c, const void* send, const size_t* send_bytes, co
 
 void comm_allgatherv2_bytes(Ctx& c, const void* send, size_t send_bytes, void* recv, const size_t* recv_bytes,
                             const size_t* recv_off, const void* send2, size_t bytes2, void* recv2) {
-  if (c.world == 1) {
+  if (!c.sharded) {
     if (send_bytes && static_cast<uint8_t*>(recv) + recv_off[0] != send)
       NBG_HIP(hipMemcpyAsync(static_cast<uint8_t*>(recv) + recv_off[0], send, send_bytes, hipMemcpyDeviceToDevice,
                              c.stream));
@@ -405,7 +432,7 @@ void comm_allgatherv2_bytes(Ctx& c, const void* send, size_t send_bytes, void* r
 }
 
 void comm_allreduce_sum_i64(Ctx& c, int64_t* d_vals, size_t n) {
-  if (c.world == 1) return;
+  if (!c.sharded) return;
   impl(c)->allreduce_sum_i64(c, d_vals, n);
 }
 

@@ -441,6 +441,7 @@ struct Timing {
   int32_t host_waits = 0;  // engine-level host waits on the device (fetches, stream syncs)
   int32_t spec_hops = 0;   // hops that ran behind a device gate
   int32_t launches = 0;    // kernel launches of the device-driven shortest-path batches
+  int32_t comm_calls = 0;  // collectives issued through the communicator (comm.cpp)
   uint64_t hop_bytes_mark = 0;  // expand_bytes at the previous hop record
   // kernel_ms < 0: the hop is one kernel (its time and bytes are the hop's; a top-down hop's
   // time is filled in later by timing_resolve)
@@ -473,6 +474,10 @@ constexpr size_t kHostStageBytes = size_t(1) << 20;
 
 struct Ctx {
   int32_t device = 0, num_parts = 1, rank = 0, world = 1;
+  // the sharded algorithm runs (owner slices, exchanges through the communicator): world > 1, or
+  // one rank with a real one-rank RCCL communicator (option comm_single before nbg_comm_init), so
+  // the RCCL entry points run on a one-GPU box exactly as they do at world > 1
+  bool sharded = false;
   hipStream_t stream = nullptr;
   std::mutex mu;
   std::string last_error;

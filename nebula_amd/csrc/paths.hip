@@ -1937,7 +1937,10 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
                                                         uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo, int32_t it,
                                                         int32_t lg_sub, int32_t cas) {
   __shared__ uint64_t s_stage[4][2][kDvStage];
-  if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
+  // a producer overflowed: its tables are incomplete and the host re-runs the batch, so the block
+  // expands nothing -- but the probe's claims still go to the arena below, which is the only
+  // record the host's abort resets distance bytes from (block-uniform)
+  const bool skip = dv_ovf_block(d.cnt);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t wave = (int64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = (int64_t(gridDim.x) * blockDim.x) >> 6;
@@ -1949,6 +1952,7 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
   uint64_t* const out1 = d.live[it & 1][1];
   DvStage sg0{s_stage[wid][0], 0u}, sg1{s_stage[wid][1], 0u};
   unsigned long long claims = 0, entries = 0;
+  if (!skip)
   chunk_groups(
       total << lg_sub,
       [&](int64_t vc, ChunkRec& r) {
@@ -2038,6 +2042,7 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
     dput(d.arena, d.cap_arena, gcnt(d.cnt, D_ARENA), d.cnt, hit, v);
     dput(d.meet, d.cap_meet, gcnt(d.cnt, D_MEET), d.cnt, hit, mt);
   }
+  if (skip) return;
   dv_flush_block(sg0, d.cnt, q + Q_LIVE0, out0, d.cap_live, d.arena, d.cap_arena);
   dv_flush_block(sg1, d.cnt, q + Q_LIVE1, out1, d.cap_live, d.arena, d.cap_arena);
   blk_add(q + Q_CLAIMS, claims);
@@ -2672,7 +2677,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   const int64_t* dst = dst_all;
   size_t npairs = npairs_all;
   std::vector<int64_t> my_src, my_dst;
-  if (c.world > 1) {
+  if (c.sharded) {
     if (!es.has_rep) {
       replicate_csr(c, es.out, es.rep_out);
       replicate_csr(c, es.in, es.rep_in);
@@ -2784,7 +2789,9 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   auto dv_alloc = [&]() {
     // the global filter (2^24 bits): off costs the expansions nothing but lets the pair filters'
     // false positives fetch a distance line each (sweep step 1: 3.4x its byte model, 1.1x with it)
-    const int64_t gf_log2 = std::min<int64_t>(std::max<int64_t>(c.opt("sp_gf_log2", 24), 0), 32);
+    // below 2^5 bits: off; at least 2^7 bits otherwise (k_dv_clear zeroes the words 4 at a time)
+    int64_t gf_log2 = std::min<int64_t>(std::max<int64_t>(c.opt("sp_gf_log2", 24), 0), 32);
+    if (gf_log2 >= 5) gf_log2 = std::max<int64_t>(gf_log2, 7);
     const bool pf_on = c.opt("sp_pf", 1) != 0;
     const int64_t nnz = std::max(cout->nnz, cin->nnz);
     const int64_t soft_dv = std::max<int64_t>(c.opt("sp_dv_list", int64_t(8) << 20), 64);

@@ -679,14 +679,14 @@ void snapshot_gen_rmat(Ctx& c, int32_t scale, int32_t ef, uint64_t seed, int32_t
   if (scale < 1 || scale > 31 || ef < 1) throw Error(NBG_E_INVALID_ARG, "bad RMAT scale");
   double t0 = now_s();
   int64_t E = int64_t(ef) << scale;
-  int64_t expect = c.world == 1 ? E : E / c.world + E / (4 * c.world) + (1 << 20);
+  int64_t expect = !c.sharded ? E : E / c.world + E / (4 * c.world) + (1 << 20);
   Staging& so = es.out_stage;
   Staging& si = es.in_stage;
   if (so.n != 0 || si.n != 0 || es.rmat_stream) throw Error(NBG_E_STATE, "RMAT must be the only source of this edge type");
   // streamed build: forced with rmat_stream = 1, automatic on one rank once the tuple stage
   // would pass its 2^32 cap (2^31 samples and up: two CSR directions of 40+ B tuples)
   const int64_t stream_opt = c.opt("rmat_stream", -1);
-  if (c.world == 1 && (stream_opt > 0 || (stream_opt < 0 && E >= (int64_t(1) << 31)))) {
+  if (!c.sharded && (stream_opt > 0 || (stream_opt < 0 && E >= (int64_t(1) << 31)))) {
     if (c.opt("writable", 0)) throw Error(NBG_E_UNSUPPORTED, "streamed RMAT snapshot is read-only (writable = 1)");
     es.rmat_stream = true;
     es.rmat_scale = scale;
@@ -1903,7 +1903,7 @@ static void order_by_degree(Ctx& c, DevBuf& owned, int64_t n_owned) {
   NBG_HIP(hipStreamSynchronize(c.stream));
   // one rank: in-degrees too (every in-edge of an owned vertex is in the local stage), for the
   // degree classes of class_key
-  const bool classes = c.world == 1 && c.opt("class_order", 1) != 0;
+  const bool classes = !c.sharded && c.opt("class_order", 1) != 0;
   DevBuf ideg;
   if (classes) {
     ideg.alloc(size_t(n_owned) * 4);
@@ -2013,7 +2013,7 @@ static void build_tag_columns(Ctx& c) {
       const int64_t olo = c.owned_lo(), ohi = c.owned_hi();
       for (int64_t i = 0; i < n; i++) {
         int32_t gi = g[size_t(i)];
-        if (gi < 0 || (c.world > 1 && (gi < olo || gi >= ohi))) continue;
+        if (gi < 0 || (c.sharded && (gi < olo || gi >= ohi))) continue;
         int32_t& w = win[size_t(gi)];
         if (w < 0) {
           w = int32_t(i);
@@ -2082,7 +2082,7 @@ static void build_tag_columns(Ctx& c) {
           k_tag_str_copy<<<grid_for(ng), 256, 0, c.stream>>>(dwin.as<int32_t>(), ng, c.heap.as<uint8_t>(),
                                                               ts.stage.props[f].as<int64_t>(), pc.str_off.as<int64_t>(),
                                                               pc.str_bytes.as<uint8_t>());
-        if (c.world > 1) {
+        if (c.sharded) {
           // lengths of every rank's owned slice -> global offsets; bytes by owner block
           replicate_owned(c, lens, 8);
           exclusive_scan<int64_t>(c, lens.as<int64_t>(), pc.str_off.as<int64_t>(), ng + 1);
@@ -2100,7 +2100,7 @@ static void build_tag_columns(Ctx& c) {
           pc.str_bytes = std::move(all);
         }
       }
-      if (c.world > 1) {
+      if (c.sharded) {
         replicate_owned(c, pc.data, 8);
         replicate_owned(c, pc.present, 1);
       }
@@ -2108,7 +2108,7 @@ static void build_tag_columns(Ctx& c) {
       c.tag_refs.push_back(TagFieldRef{ts.name, pc.name, pc.type});
       ts.cols.push_back(std::move(pc));
     }
-    if (c.world > 1) replicate_owned(c, ts.part, 4);
+    if (c.sharded) replicate_owned(c, ts.part, 4);
     NBG_HIP(hipStreamSynchronize(c.stream));
     if (!c.opt("writable", 0)) ts.stage = Staging{};
   }
@@ -2406,7 +2406,7 @@ static bool commit_merge(Ctx& c) {
     // (several ranks: the new vertices land in rows every CSR already has, the growth room)
     if (c.opt("merge_new_vertices", 1) == 0) refuse = true;
     for (auto& kv : c.edges)
-      for (int d = 0; d < 2 && c.world == 1; d++)
+      for (int d = 0; d < 2 && !c.sharded; d++)
         if ((d ? kv.second.in_stage.n : kv.second.out_stage.n) == kv.second.ord[d].n) refuse = true;
   }
   // per edge space: did this rank's out / in CSR change (a rank without writes of its own still
@@ -2421,7 +2421,7 @@ static bool commit_merge(Ctx& c) {
     }
   }
   flags[0] = refuse, flags[1] = int64_t(unknown), flags[2] = tag_writes;
-  if (c.world > 1) {
+  if (c.sharded) {
     DevBuf f;
     f.alloc(flags.size() * 8);
     NBG_HIP(hipMemcpyAsync(f.p, flags.data(), flags.size() * 8, hipMemcpyHostToDevice, c.stream));
@@ -2432,7 +2432,7 @@ static bool commit_merge(Ctx& c) {
   // several ranks with new vertices: placed in the owners' growth rooms when they fit on every
   // rank (collective: the same union and decision everywhere), else the full rebuild
   NewVertexPlan plan;
-  if (c.world > 1 && !flags[0] && flags[1] > 0 &&
+  if (c.sharded && !flags[0] && flags[1] > 0 &&
       (c.opt("merge_new_vertices", 1) == 0 || !plan_new_vertices_ranks(c, int64_t(unknown), plan)))
     flags[0] = 1;
   if (flags[0]) return false;
@@ -2453,8 +2453,8 @@ static bool commit_merge(Ctx& c) {
     tmark = t;
   };
   phase("checks");
-  const bool new_vertices = c.world > 1 ? !plan.vids.empty() : unknown > 0;
-  if (c.world > 1 && new_vertices) {
+  const bool new_vertices = c.sharded ? !plan.vids.empty() : unknown > 0;
+  if (c.sharded && new_vertices) {
     extend_vertex_map_ranks(c, plan);
     phase("vertex map (new vertices)");
   } else if (new_vertices) {
@@ -2605,7 +2605,7 @@ __global__ void k_i16_to_i8(const int16_t* in, int8_t* out, int64_t m) {
 }
 
 static void finalize_rmat_stream(Ctx& c, EdgeSpace& es) {
-  if (c.world != 1) throw Error(NBG_E_UNSUPPORTED, "streamed RMAT build on more than one rank");
+  if (c.sharded) throw Error(NBG_E_UNSUPPORTED, "streamed RMAT build on more than one rank");
   if (c.edges.size() != 1 || !c.tags.empty())
     throw Error(NBG_E_UNSUPPORTED, "streamed RMAT must be the snapshot's only edge type, without tags");
   const int32_t scale = es.rmat_scale;
@@ -2926,7 +2926,7 @@ void snapshot_finalize(Ctx& c) {
   std::vector<int64_t> counts(size_t(c.world), 0);
   DevBuf owned;
   int64_t n_owned = nuniq;
-  if (c.world == 1) {
+  if (!c.sharded) {
     owned = std::move(vA);
   } else {
     // every rank sends the vids it references to their owners; owners union.  (Simple form:
@@ -2982,7 +2982,7 @@ void snapshot_finalize(Ctx& c) {
   phase("degree order");
   // 3. counts -> base; allgather owned tables into vid_of (rank-major; within a rank by
   // descending out-degree, or by vid with degree_order=0)
-  if (c.world == 1) {
+  if (!c.sharded) {
     counts[0] = n_owned;
   } else {
     DevBuf dsz, dmine;
@@ -2999,7 +2999,7 @@ void snapshot_finalize(Ctx& c) {
   // grow_room_pct of the rank's vertices, at least 1024): a merge commit places new vertices
   // there without moving any rank's range (extend_vertex_map_ranks); a batch that overflows
   // some rank's room takes the full rebuild, which reserves room again.
-  const int64_t room_pct = keep && c.world > 1 ? std::max<int64_t>(0, c.opt("grow_room_pct", 10)) : 0;
+  const int64_t room_pct = keep && c.sharded ? std::max<int64_t>(0, c.opt("grow_room_pct", 10)) : 0;
   c.base.assign(size_t(c.world) + 1, 0);
   c.counts = counts;
   for (int r = 0; r < c.world; r++) {
@@ -3012,7 +3012,7 @@ void snapshot_finalize(Ctx& c) {
   if (c.n_global >= (int64_t(1) << 31)) throw Error(NBG_E_UNSUPPORTED, "more than 2^31 vertices");
   c.vid_of.alloc(size_t(std::max<int64_t>(c.n_global, 1)) * 8);
   fill<int64_t>(c, c.vid_of.as<int64_t>(), INT64_MIN, c.n_global);
-  if (c.world == 1) {
+  if (!c.sharded) {
     if (n_owned) k_unflip<<<grid_for(n_owned), 256, 0, c.stream>>>(owned.as<uint64_t>(), c.vid_of.as<int64_t>(), n_owned);
   } else {
     int64_t mx = *std::max_element(counts.begin(), counts.end());

@@ -2271,7 +2271,7 @@ void ensure_workspaces(Ctx& c, int64_t nF_cap) {
   c.ws_partials.ensure(size_t(kAggBlocks) * kSlots * 8);
   c.ws_bits_send.ensure(size_t(mb / 8 + 64));
   c.ws_bits_recv.ensure(size_t(mb / 8 + 64));
-  if (c.world > 1) {
+  if (c.sharded) {
     c.ws_piggy.ensure(size_t(12) * size_t(c.world) * 16 + 64);  // spec hops' counters of every rank
     c.ws_bits_glob.ensure(size_t(mb / 8 + 64));
     c.ws_bits_xchg.ensure(size_t(c.world) * size_t((c.owned_hi() - c.owned_lo()) / 8) + 64);
@@ -2302,7 +2302,7 @@ struct CommTimer {
 
 // element-wise sum of a few host counters over ranks
 void allsum(Ctx& c, int64_t* v, int n, unsigned long long* dscratch) {
-  if (c.world == 1) return;
+  if (!c.sharded) return;
   {
     CommTimer t(c);
     NBG_HIP(hipMemcpyAsync(dscratch, v, size_t(n) * 8, hipMemcpyHostToDevice, c.stream));
@@ -2323,7 +2323,7 @@ void dev_allsum(Ctx& c, const unsigned long long* K, std::initializer_list<int> 
   for (int i : idx) packed |= uint64_t(uint8_t(i)) << (8 * n++);
   k_pick_counters<<<1, 64, 0, c.stream>>>(K, packed, n, dst);
   NBG_HIP(hipGetLastError());
-  if (c.world == 1) return;
+  if (!c.sharded) return;
   CommTimer t(c);
   comm_allreduce_sum_i64(c, reinterpret_cast<int64_t*>(dst), size_t(n));
 }
@@ -2331,7 +2331,7 @@ void dev_allsum(Ctx& c, const unsigned long long* K, std::initializer_list<int> 
 // owned frontier bitmap -> bitmap over the whole gidx space (bottom-up hops read sources of
 // every rank).  Owner ranges are padded to 64, so every segment is whole 64-bit words.
 const uint32_t* global_bits(Ctx& c, const uint32_t* owned) {
-  if (c.world == 1) return owned;
+  if (!c.sharded) return owned;
   CommTimer t(c);
   const size_t G = size_t(c.world);
   std::vector<size_t> rb(G), ro(G);
@@ -2361,7 +2361,7 @@ const uint32_t* global_bits_cnt(Ctx& c, const uint32_t* owned, const unsigned lo
 // top-down hops mark dsts of every rank in the global byte-map: ship each owner its slice as
 // a bitmap and OR the received slices back into the owned range of the map
 void exchange_marks(Ctx& c, uint8_t* map) {
-  if (c.world == 1) return;
+  if (!c.sharded) return;
   CommTimer t(c);
   const size_t G = size_t(c.world);
   const int64_t lo = c.owned_lo(), n_own = c.owned_hi() - lo;
@@ -2397,7 +2397,7 @@ __global__ void k_min_segments(const int32_t* recv, int G, int64_t n, int32_t* o
 // deterministic rule of DESIGN.md divergence 6).  Each rank sends every owner its slice of the
 // root array and takes the elementwise minimum of the slices it receives.
 void exchange_roots(Ctx& c, int32_t* root_next) {
-  if (c.world == 1) return;
+  if (!c.sharded) return;
   CommTimer t(c);
   const size_t G = size_t(c.world);
   const int64_t lo = c.owned_lo(), n_own = c.owned_hi() - lo;
@@ -2743,7 +2743,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
                            std::min<int64_t>(cw > 0 ? 512 : c.opt("bu_lean_grid", 2048), kAggBlocks / 2))));
   const size_t shm = size_t(cw + 1) * 4;  // + the zero word non-hub probes read
   uint32_t fb_bytes = uint32_t(fb_words * 4);
-  if (hop_front && c.world == 1 && es.bu_both_tiles > 0 && c.opt("bu_fb_bound", 1) != 0)
+  if (hop_front && !c.sharded && es.bu_both_tiles > 0 && c.opt("bu_fb_bound", 1) != 0)
     fb_bytes = uint32_t(std::min<int64_t>(fb_bytes, (es.bu_both_tiles * 128 + 31) / 32 * 4));
   const int probe_stats = int(c.opt("bu_probe_stats", 0));  // partials [6] / [7]
   c.ws_pend.ensure(size_t(ntiles * 2 + 2) * 8);  // the pending bits, 2 words per tile
@@ -3054,7 +3054,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         deferred = rc;
         deferred_msg = "YIELD: " + msg;
       }
-      if (rc == NBG_OK && p.result_type == VT_STR && s.distinct && c.world > 1)
+      if (rc == NBG_OK && p.result_type == VT_STR && s.distinct && c.sharded)
         throw Error(NBG_E_UNSUPPORTED, "DISTINCT over STRING YIELD columns across ranks");
       yields.push_back(p);
     }
@@ -3099,7 +3099,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   const bool fast1 = ns > 0 && ns <= kSmallStarts && s.steps >= 2 && td1_certain && !(uses_input && s.steps > 1) &&
                      c.opt("starts_small", 1) != 0;
   // counters summed over ranks on the device (dev_allsum) land at K.d[48, 52)
-  const bool multi = c.world > 1;
+  const bool multi = c.sharded;
   // the small-start path's one block reads the starts from coherent pinned host memory (the
   // stream's previous query finished before this one was enqueued): no copy between queries
   const int64_t* k_starts = d_starts;
@@ -3137,7 +3137,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   if (ns && !fast1) {
     if (s.steps == 1 && !s.distinct) {
       k_list_starts<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, F, K.d);
-    } else if (c.world == 1 && es.odeg.p && c.opt("starts_bits", 1) != 0) {
+    } else if (!c.sharded && es.odeg.p && c.opt("starts_bits", 1) != 0) {
       // one rank: dedup the starts through the frontier bitmap itself (a few hundred atomics)
       // instead of marking the byte map and compacting the whole vertex space
       NBG_HIP(hipMemsetAsync(bits16, 0, c.ws_bits_send.bytes, c.stream));
@@ -3849,7 +3849,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         const int64_t yerr = int64_t(K.h[multi ? 48 : 5]);
         if (yerr) throw Error(NBG_E_EVAL, "YIELD evaluation failed");
       }
-      if (s.distinct && c.world > 1) nrows = shuffle_rows(c, ya, h->dev, nrows);
+      if (s.distinct && c.sharded) nrows = shuffle_rows(c, ya, h->dev, nrows);
       if (s.distinct && nrows) {
         uint64_t cap = 1024;
         while (cap < uint64_t(2 * nrows)) cap <<= 1;

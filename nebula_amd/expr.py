@@ -169,18 +169,11 @@ def prop(name: str, alias: str = "") -> AliasProp:
 
 
 def encode(e: Expr | bytes | None) -> bytes:
-    """Expression::encode bytes.  An Expr tree is encoded once and the bytes kept on its root
-    (trees are built, then only read, as the reference's parsed Expression objects are): a query
-    loop that passes the same WHERE / YIELD objects pays the encoding once."""
+    """Expression::encode bytes of a tree (or bytes passed through).  Not cached on the tree: Expr
+    nodes are mutable, and a child changed after a first encode must change the bytes sent (the
+    engine caches the C views per encoded bytes instead, GraphSpace._plan_views)."""
     if e is None:
         return b""
     if isinstance(e, (bytes, bytearray)):
         return bytes(e)
-    enc = getattr(e, "_nbg_enc", None)
-    if enc is None:
-        enc = e.encode()
-        try:
-            e._nbg_enc = enc
-        except AttributeError:  # a tree type without instance attributes
-            pass
-    return enc
+    return e.encode()

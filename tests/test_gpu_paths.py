@@ -314,11 +314,14 @@ def test_device_driven_batches(rmat, dev, pf, gf, occ, batch):
             sp.unset_option(k)
 
 
-@pytest.mark.parametrize("cap", [64, 300, 2000])
-def test_device_driven_overflow_falls_back(cap):
+@pytest.mark.parametrize("cap,grid", [(64, 0), (300, 0), (2000, 0), (300, 8192), (2000, 8192)])
+def test_device_driven_overflow_falls_back(cap, grid):
     """sp_dv_list bounds every list of the device-driven batch: an overflow (BFS lists, meets,
     sweep lists, chunk tables, arena) restores the clean state and re-runs the batch host-driven;
-    results stay the oracle's and later calls see clean distance bytes and filters"""
+    results stay the oracle's and later calls see clean distance bytes and filters.  grid: scan
+    grids of 8192 blocks, far past the resident grid, so expansion blocks start after a list
+    has overflowed (they skip their chunks but must still hand the meet probe's claims to the
+    arena the abort resets distance bytes from)"""
     scale = 12
     sp = GraphSpace(64)
     sp.set_edge_schema(FOLLOW, [("weight", 2)])
@@ -331,6 +334,8 @@ def test_device_driven_overflow_falls_back(cap):
         s, t = synth.pairs(scale, 16, 1, 300, pick_seed=17)
         sp.set_option("sp_dv_list", cap)
         sp.set_option("sp_batch", 100)
+        if grid:
+            sp.set_option("sp_dv_grid", grid)
         got = sp.shortest_path(s, t, FOLLOW, 7).rows()
         fell_back = 3 - sp.last_timing()["spec_hops"]
         assert got == oracle_paths(st, s, t, FOLLOW, 7)
@@ -339,6 +344,7 @@ def test_device_driven_overflow_falls_back(cap):
         if cap == 64:
             assert fell_back == 3
         sp.unset_option("sp_dv_list")
+        sp.unset_option("sp_dv_grid")
         clean = sp.shortest_path(s, t, FOLLOW, 7).rows()  # device-driven again, clean state
         assert sp.last_timing()["spec_hops"] == 3
         assert clean == got
