@@ -384,10 +384,6 @@ struct EdgeSpace {
   // two halves (slots 0-1 -> pair_col[0], slots 2-3 -> pair_col[1], 2 x int32 per row, -1 past
   // the row's end, padded to whole 128-row tiles)
   DevBuf pair_col[2];
-  // 3-slot slab (option bu_slab3 at finalize; the final-hop first pass with bu_fin_var bit 64):
-  // slot 2 of every row as one int32, bit 31 set when the row has a fourth entry (the packed
-  // words use at most 31 bits; -1 past the row's end), so slots 0-2 cost 12 B a row, not 16
-  DevBuf slab3;
   // quantised predicate packing (bottom-up hops): the words of pair_col and tcol_q carry the
   // source gidx in their low q_gbits bits and, above it, q_bits bits of the bucket of transposed
   // prop q_field's value: bucket(v) = (v - q_min) * 2^q_bits / q_range (monotone), so a
@@ -652,7 +648,12 @@ void lookup_gidx(Ctx& c, const int64_t* d_vids, int32_t* d_gidx, int64_t n);
 // the device counters d[0, n) (n <= 256) into pinned host h[0, n) once every launch before has
 // finished on the context's stream (a one-block publish kernel + a host spin, traverse.hip)
 // `before` (optional): an event recorded just ahead of the publish kernel
-void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h, hipEvent_t before = nullptr);
+// shards > 1: d is a sharded counter block (word i = sum of d[i + s * kShardStride], s < shards)
+void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h, hipEvent_t before = nullptr,
+                    int shards = 1);
+// sharded block sums (traverse.hip block_add_sums): shard s of counter word i at i + s * kShardStride
+constexpr size_t kShardStride = 256;
+constexpr int kSumShards = 8;
 // one host wait (counted in Timing::host_waits) until the device publishes `seq` in `word`
 void wait_host_word(Ctx& c, const unsigned long long* word, uint64_t seq);
 // a query's total_ms (ev[0] -> ev[1]) once asked for (go_run records ev[1] without waiting)

@@ -83,7 +83,6 @@ struct SpState {  // per-pair arrays, B entries each
   int32_t* met;             // 1: a meet this iteration; 2 + i: met in iteration i
   unsigned long long* deg;  // [2][B] frontier sum of (degree + 1)
   int32_t B;
-  int32_t vmajor;           // distance bytes vertex-major [v][pair] (else pair-major [pair][v])
   int32_t ilv;              // 1: the two sides' bytes of a (pair, vertex) adjacent (d1 = d0 + 1, index
                             // x 2): a claim reads its own and the other side's byte in one load
   // level filter (null: off): bit (v & lvmask) of level (side, l)'s lvw words is set when some
@@ -114,7 +113,7 @@ __device__ inline bool lv_maybe(const SpState& st, uint32_t side, int32_t l, uin
 // lines in L2 / the Infinity cache; pair-major keeps each pair's bytes contiguous.  Interleaved
 // (ilv), the index doubles and side 1's array starts one byte after side 0's.
 __device__ inline uint64_t didx(const SpState& st, uint32_t p, uint64_t v, int64_t n) {
-  return (st.vmajor ? v * uint64_t(st.B) + p : uint64_t(p) * uint64_t(n) + v) << st.ilv;
+  return (uint64_t(p) * uint64_t(n) + v) << st.ilv;  // pair-major (vertex-major lost: 3.84 vs 3.58 ms, r05)
 }
 
 struct SpBufs {
@@ -1274,13 +1273,11 @@ struct SpFilt {
   uint32_t* gf;     // blocked Bloom filter words (null: off)
   uint32_t gshift;  // 64 - log2(gf words)
   int32_t B;
-  int32_t k2;       // pair filters with two bits per vertex (option sp_pf_k = 2)
   int32_t diag;     // option sp_dv_diag (diagnostics): sweep bit 0 no tests, bit 1 filter tests
                     // without the byte reads (timing only, wrong results); bit 2 a walk error
                     // returns the partial result instead of failing the call
 };
 __device__ inline uint32_t pf_bit(uint32_t v) { return (v * 0x9E3779B1u) >> 20; }
-__device__ inline uint32_t pf_bit2(uint32_t v) { return ((v * 0x9E3779B1u) >> 8) & 4095u; }
 __device__ inline uint64_t gf_hash(uint32_t sl, uint32_t p, uint32_t v) {
   uint64_t h = (uint64_t(v) * 0xD6E8FEB86659FD93ull) ^ (uint64_t(p) * 0xA0761D6478BD642Full) ^
                (uint64_t(sl + 1) * 0xE7037ED1A0B428DBull);
@@ -1297,10 +1294,6 @@ __device__ inline void filt_mark(const SpFilt& f, uint32_t side, uint32_t l, uin
     uint32_t* row = f.pf + (size_t(sl) * uint32_t(f.B) + p) * 128;
     const uint32_t b = pf_bit(v);
     atomicOr(row + (b >> 5), 1u << (b & 31u));
-    if (f.k2) {
-      const uint32_t b2 = pf_bit2(v);
-      atomicOr(row + (b2 >> 5), 1u << (b2 & 31u));
-    }
   }
   if (f.gf) {
     const uint64_t h = gf_hash(sl, p, v);
@@ -1322,14 +1315,7 @@ __device__ inline bool pf_bit_set(uint2 row, uint32_t b) {
   const uint32_t hi = uint32_t(__builtin_amdgcn_ds_bpermute(src, int(row.y)));
   return ((((wd & 1u) ? hi : lo) >> (b & 31u)) & 1u) != 0u;
 }
-// (both cross-lane reads run on every active lane: a lane left out of a ds_bpermute reads as 0 to
-// the lanes that ask it, so the second read must not depend on the first's answer)
-__device__ inline bool pf_test(uint2 row, uint32_t v, bool k2) {
-  const bool a = pf_bit_set(row, pf_bit(v));
-  if (!k2) return a;  // wave-uniform
-  const bool b = pf_bit_set(row, pf_bit2(v));
-  return a && b;
-}
+__device__ inline bool pf_test(uint2 row, uint32_t v) { return pf_bit_set(row, pf_bit(v)); }  // wave-uniform call
 __device__ inline bool gf_test(const SpFilt& f, uint32_t side, int32_t l, uint32_t p, uint32_t v) {
   if (!f.gf || l < 1 || l >= kLv) return true;
   const uint64_t h = gf_hash(side * kLv + uint32_t(l), p, v);
@@ -1824,7 +1810,7 @@ __global__ __launch_bounds__(256) void k_dv_probe(SpDev d, SpState st, SpFilt f,
             uint32_t fm = 0;
 #pragma unroll
             for (int u = 0; u < U; u++) {
-              const bool pv = pf_on ? pf_test(prow, w[u], f.k2 != 0) : true;
+              const bool pv = pf_on ? pf_test(prow, w[u]) : true;
               if (stats) n_pf += (w[u] != 0xFFFFFFFFu && pv) ? 1u : 0u;
               fm |= (w[u] != 0xFFFFFFFFu && pv && gf_test(f, o, need, p, w[u])) ? 1u << u : 0u;
             }
@@ -1935,7 +1921,7 @@ __device__ inline void dv_flush_block(DvStage& s, unsigned long long* cnt, unsig
 template <int OCC>
 __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpFilt f, SpCsr g0, SpCsr g1,
                                                         uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo, int32_t it,
-                                                        int32_t lg_sub, int32_t cas) {
+                                                        int32_t lg_sub) {
   __shared__ uint64_t s_stage[4][2][kDvStage];
   // a producer overflowed: its tables are incomplete and the host re-runs the batch, so the block
   // expands nothing -- but the probe's claims still go to the arena below, which is the only
@@ -1994,11 +1980,11 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
           }
 #pragma unroll
           for (int u = 0; u < kProbeU; u++) {
-            // a claim: the CAS (option sp_dv_cas) or a plain byte store (the default: two chunks of one
+            // a claim: a plain byte store (two chunks of one
             // pair reaching the same vertex in this level may both list it; the byte holds l + 1 either
             // way, and a duplicate tuple only repeats work)
             const uint64_t wi = uint64_t(w[u]) << sh;
-            const bool cl = bt[u] == 0xFFu && (cas ? claim_byte(sdp, wi, l + 1) : (sdp[wi] = uint8_t(l + 1), true));
+            const bool cl = bt[u] == 0xFFu && (sdp[wi] = uint8_t(l + 1), true);
             bool meet = false;
             uint32_t dt = 0;
             if (cl) {
@@ -2337,7 +2323,7 @@ __global__ __launch_bounds__(256) void k_dv_sweep(SpDev d, SpState st, SpFilt f,
             uint32_t fm = 0;
 #pragma unroll
             for (int u = 0; u < U; u++) {
-              const bool pv = pf_on ? pf_test(prow, w[u], f.k2 != 0) : true;
+              const bool pv = pf_on ? pf_test(prow, w[u]) : true;
               fm |= (w[u] != 0xFFFFFFFFu && pv && gf_test(f, os, need, p, w[u])) ? 1u << u : 0u;
             }
             if (f.diag & 3) fm = (f.diag & 1) ? 0u : (__ballot(fm != 0) ? 0u : fm);
@@ -2420,7 +2406,7 @@ __global__ __launch_bounds__(256) void k_dv_walk_scan(SpDev d, SpState st, SpFil
           uint32_t fm = 0;
 #pragma unroll
           for (int u = 0; u < kProbeU; u++) {
-            const bool pv = pf_on ? pf_test(prow, w[u], f.k2 != 0) : true;
+            const bool pv = pf_on ? pf_test(prow, w[u]) : true;
             fm |= (w[u] != 0xFFFFFFFFu && pv && gf_test(f, 1, need, p, w[u])) ? 1u << u : 0u;
           }
 #pragma unroll
@@ -2757,7 +2743,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   // ---- device-driven batches (k_dv_*): fixed capacities sized once per context and batch size;
   // false = a list overflowed (the clean state is restored, the batch runs host-driven below)
   // (pair-major distance bytes only: the kernels address a pair's bytes from one row pointer)
-  const bool dev = c.opt("sp_dev", 1) != 0 && max_steps <= kMaxQ - 2 && lo == 0 && c.opt("sp_vmajor", 0) == 0 &&
+  const bool dev = c.opt("sp_dev", 1) != 0 && max_steps <= kMaxQ - 2 && lo == 0 &&
                    B <= kPairLds;
   auto dv_event = [&]() -> size_t {
     if (!c.hop_timing) return ~size_t(0);
@@ -2863,14 +2849,12 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     st.side = st.lvl + 2 * nb;
     st.pside = st.side + nb;
     st.met = st.pside + nb;
-    st.vmajor = int32_t(c.opt("sp_vmajor", 0));
     st.ilv = ilv;
     SpFilt f{};
     f.pf = W.dv_pf.as<uint32_t>();
     f.gf = W.dv_gf.as<uint32_t>();
     f.gshift = W.dv_gf.p ? uint32_t(64 - (W.dv_gf_log2 - 5)) : 0u;
     f.B = int32_t(nb);
-    f.k2 = c.opt("sp_pf_k", 1) >= 2 ? 1 : 0;
     f.diag = int32_t(c.opt("sp_dv_diag", 0));
     SpDev d{};
     d.cnt = W.dv_cnt.as<unsigned long long>();
@@ -2937,7 +2921,6 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     int32_t lg_sub = int32_t(std::min<int64_t>(std::max<int64_t>(c.opt("sp_dv_exp_sub", -1), -1), 6));
     if (lg_sub < 0) lg_sub = std::max<int32_t>(0, d.lg_chb - 8);
     lg_sub = std::min<int32_t>(lg_sub, d.lg_chb);
-    const int32_t cas = int32_t(c.opt("sp_dv_cas", 0));
     const int64_t pu = c.opt("sp_dv_probe_u", 4), su = c.opt("sp_dv_sweep_u", 4);  // entries per lane and step
     const int max_it = std::min<int>(max_steps, kMaxQ - 2);
     const int64_t htm = int64_t(c.ht_cap - 1);
@@ -2993,10 +2976,10 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       ++nl;
       if (occ >= 8)
         k_dv_expand<8><<<gsz((const void*)k_dv_expand<8>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it,
-                                                                               lg_sub, cas);
+                                                                               lg_sub);
       else
         k_dv_expand<1><<<gsz((const void*)k_dv_expand<1>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it,
-                                                                               lg_sub, cas);
+                                                                               lg_sub);
       evi[size_t(it)][2] = dv_event();
       seq[size_t(it)] = ++c.pub_seq;
       ++nl;
@@ -3157,7 +3140,6 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     st.side = st.lvl + 2 * nb;
     st.pside = st.side + nb;
     st.met = st.pside + nb;
-    st.vmajor = int32_t(c.opt("sp_vmajor", 0));
     st.ilv = ilv;
     if (c.opt("sp_lvbits", 1) != 0) {  // level filter: 2 * kLv maps, cleared per batch
       // bits per level: the power of two >= n, capped (option sp_lvbits_log2, default 23)

@@ -504,7 +504,6 @@ static void reset_transpose_derived(EdgeSpace& es) {
   es.q_field = -1;
   es.q_gbits = es.q_bits = 0;
   for (int h = 0; h < 2; h++) es.pair_col[h].release();
-  es.slab3.release();
   es.odeg.release();
   es.odeg8.release();
   es.max_odeg = -1;
@@ -1543,14 +1542,6 @@ __global__ void k_build_pair(const int64_t* trp, const T* src, int64_t n, T* lo,
   }
 }
 
-// 3-slot slab from the quad slab's upper half: slot 2, bit 31 flagging a fourth entry
-__global__ void k_build_slab3(const uint2* hi, int64_t n, uint32_t* out) {
-  for (int64_t d = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; d < n; d += int64_t(gridDim.x) * blockDim.x) {
-    const uint2 h = hi[d];
-    out[d] = h.x == 0xffffffffu ? h.x : (h.x | (h.y != 0xffffffffu ? 0x80000000u : 0u));
-  }
-}
-
 // rest records (EdgeSpace::brec): row d's start and clamped in-degree, then its first
 // kRecEntries entries of src, as one 64-byte line (four 16-byte stores)
 __global__ void k_build_rec(const int64_t* trp, const int32_t* src, int64_t n, uint4* rec) {
@@ -1753,7 +1744,6 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
   // the quad slab of the bottom-up first pass (k_bu_lean), packed with the quantised bucket of
   // the first INT-like transposed prop when the gidx leaves >= 3 spare bits below bit 31
   for (int h = 0; h < 2; h++) es.pair_col[h].release();
-  es.slab3.release();
   es.q_field = -1;
   es.q_gbits = es.q_bits = 0;
   es.tcol_q.release();
@@ -1800,10 +1790,6 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
       k_build_pair<int32_t><<<grid_for(n_own), 256, 0, c.stream>>>(t.row_ptr.as<int64_t>(), src_col, n_own,
                                                                    es.pair_col[0].as<int32_t>(),
                                                                    es.pair_col[1].as<int32_t>(), -1);
-    if (c.opt("bu_slab3", 0) != 0 && n_pad > 0) {
-      es.slab3.alloc(size_t(n_pad) * 4 + 16);
-      k_build_slab3<<<grid_for(n_pad), 256, 0, c.stream>>>(es.pair_col[1].as<uint2>(), n_pad, es.slab3.as<uint32_t>());
-    }
   }
   {
     // exact row bounds of the bottom-up hops: past the last row with an in-edge nothing can be

@@ -687,9 +687,14 @@ __device__ inline void block_store_partials(const unsigned long long* v, int k, 
   }
 }
 // the block's sums straight into out[0, k) with no-return atomics (option bu_atomic_sums: the
-// bottom-up passes then need no k_reduce_partials launch; out starts at zero)
+// bottom-up passes then need no k_reduce_partials launch; out starts at zero).
+// shards > 1: block b adds into shard b % shards, kShardStride words further per shard, and every
+// reader folds the shards (gate_open, k_publish): the adds of one address serialise at the memory
+// side (~10 ns each), so 512 blocks ending together added ~4 us to a kernel and 1024 ~10 us
+// (tools/atomic_tail, profiles/r12c_atomic_tail.jsonl); with 8 shards ~0.
 __device__ inline void block_add_sums(const unsigned long long* v, int k, unsigned long long* lds,
-                                      unsigned long long* out) {
+                                      unsigned long long* out, int shards = 1) {
+  if (shards > 1) out += size_t(blockIdx.x % unsigned(shards)) * kShardStride;
   const int w = threadIdx.x >> 6;
   const int nw = int(blockDim.x >> 6);
   for (int i = 0; i < k; i++) {
@@ -900,6 +905,7 @@ struct GateIn {
   unsigned long long thr = 0;
   const unsigned long long* all = nullptr;
   int world = 1;
+  int shards = 1;  // e / n are sharded block sums (block_add_sums): their shards are summed
 };
 __device__ inline bool gate_open(const GateIn& gi, unsigned long long* gate) {
   if (gi.e == nullptr && gi.all == nullptr) return gate == nullptr || *gate != 0ull;
@@ -908,8 +914,8 @@ __device__ inline bool gate_open(const GateIn& gi, unsigned long long* gate) {
     n = e = 0ull;
     for (int r = 0; r < gi.world; r++) n += gi.all[2 * r], e += gi.all[2 * r + 1];
   } else {
-    n = *gi.n;
-    e = *gi.e;
+    n = e = 0ull;
+    for (int s = 0; s < gi.shards; s++) n += gi.n[size_t(s) * kShardStride], e += gi.e[size_t(s) * kShardStride];
   }
   const bool open = (gi.pg == nullptr || *gi.pg != 0ull) && n > 0ull && e >= gi.thr;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1182,7 +1188,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_lean(const uint2* __restrict__ l
   // wave-uniform counters enter the block sums once, from lane 0
   if (lane != 0) nfound = npend = nwords = 0;
   unsigned long long acc64[8] = {nfound, odsum, nwords, npend, 0, 0, nglob, nhub};
-  if (atomic_sums) block_add_sums(acc64, 8, lds, partials);
+  if (atomic_sums) block_add_sums(acc64, 8, lds, partials, atomic_sums);
   else block_store_partials(acc64, 8, lds, partials);
 }
 
@@ -1208,17 +1214,15 @@ constexpr uint32_t kNoProbe = 0x0ffffff0u;
 // in L2): 158 -> 148 us at C3.  Measured without gain (r04f/r04g): the next tile's slab loads
 // issued behind the current tile's probes, an interleaved 16-byte slab (one load per row), two
 // tiles per wave; with no probes at all the slab alone streams at 4.7 TB/s in this loop.
-// VAR: bit 0 -- a probe instruction is issued only when some lane of the wave has an L2
-// candidate in that slot; bit 4 -- one 16-byte store of the tile's next / pending words; bit 5 --
-// rows a hub word already found send no L2 probe.  Measured without gain and removed (r06e-r06h):
-// contiguous tile ranges per wave, the same skip for the LDS reads, 16-byte lanes (rows 2l and
-// 2l + 1 per lane), the tile's L2 probes packed into the fewest lanes through an LDS scratch.
-// Bit 6 -- the 3-slot slab (EdgeSpace::slab3 as `hi`, 4 B a row: slot 2 with bit 31 flagging a
-// fourth entry): 12 B per row instead of 16; a row with a fourth entry and no passing hit in
-// slots 0-2 goes to the rest pass (which rescans the final hop's pending rows from entry 0).
-// Measured (r10e, C3): this pass 106.9 -> 90.5 us, the rest pass 43 -> 74 us, the query 0.413
-// -> 0.425 ms; kept as an option (bu_slab3 + bu_fin_var 113), not the default.
-template <int CLS, int NT, int VAR = 0>
+// Round 4 (r06h: 124.9 -> 105.8 us at C3): a probe instruction is issued only when some lane of
+// the wave has an L2 candidate in that slot; one 16-byte store of the tile's next / pending
+// words; rows a hub word already found send no L2 probe.  Measured without gain and removed
+// (r06e-r06h): contiguous tile ranges per wave, the same skip for the LDS reads, 16-byte lanes
+// (rows 2l and 2l + 1 per lane), the tile's L2 probes packed into the fewest lanes through an
+// LDS scratch.  Round 5, removed in round 6: the 3-slot slab (12 B a row, slot 2 flagging a fourth
+// entry in bit 31): this pass 106.9 -> 90.5 us but the rest pass 43 -> 74 us, the query 0.413 ->
+// 0.425 ms (r10e).
+template <int CLS, int NT>
 __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo, const uint2* __restrict__ hi,
                                                     int64_t ntiles, int64_t work_tiles,
                                                     const uint32_t* __restrict__ fbits,
@@ -1255,25 +1259,15 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
     const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
     return make_uint2(uint32_t(x), uint32_t(x >> 32));
   };
-  constexpr bool S3 = (VAR & 64) != 0;
-  constexpr int NS = S3 ? 3 : 4;  // slots per row
-  bool more[2] = {false, false};  // S3: the row has a fourth entry
+  constexpr int NS = 4;  // slots per row
   auto load = [&](int64_t t, uint32_t (&sw)[2][4]) {
     const int64_t r = t * 128 + lane;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const uint2 a = ld8(lo + r + 64 * h);
       sw[h][0] = a.x, sw[h][1] = a.y;
-      if (S3) {
-        const uint32_t* s3 = reinterpret_cast<const uint32_t*>(hi);
-        const uint32_t x = NT ? __builtin_nontemporal_load(s3 + r + 64 * h) : s3[r + 64 * h];
-        more[h] = x != 0xffffffffu && (x >> 31) != 0u;
-        sw[h][2] = more[h] ? x & 0x7fffffffu : x;
-        sw[h][3] = 0xffffffffu;
-      } else {
-        const uint2 b = ld8(hi + r + 64 * h);
-        sw[h][2] = b.x, sw[h][3] = b.y;
-      }
+      const uint2 b = ld8(hi + r + 64 * h);
+      sw[h][2] = b.x, sw[h][3] = b.y;
     }
   };
   const uint32_t rest_b = __builtin_amdgcn_readfirstlane(fb_rest);
@@ -1297,30 +1291,25 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
     for (int h = 0; h < 2; h++)
 #pragma unroll
       for (int k = 0; k < NS; k++) lw[h][k] = *(lds_u32p)(size_t(min(ob[h][k], cw4)));
-    // VAR bit 5: rows already found through a hub word send no L2 probe (most found rows have
-    // a hub in-neighbour in the frontier: their slots' L2 probes were wasted instructions)
+    // rows already found through a hub word send no L2 probe (most found rows have a hub
+    // in-neighbour in the frontier: their slots' L2 probes were wasted instructions)
     bool hubf[2] = {false, false};
-    if (VAR & 32) {
-#pragma unroll
-      for (int h = 0; h < 2; h++)
-#pragma unroll
-        for (int k = 0; k < NS; k++) {
-          const uint32_t w = sw[h][k];
-          const bool pass = CLS == 1 ? w >= plo : (w - plo <= pr) != pinv;
-          hubf[h] = hubf[h] || (__builtin_amdgcn_ubfe(lw[h][k], w, 1u) != 0u && pass);
-        }
-    }
 #pragma unroll
     for (int h = 0; h < 2; h++)
 #pragma unroll
       for (int k = 0; k < NS; k++) {
-        if (VAR & 1) {
-          gw[h][k] = 0u;
-          if (__ballot(ob[h][k] - cw4 < rest_b && !hubf[h]))
-            gw[h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, hubf[h] ? 0xfffffff0u : ob[h][k] - cw4, 0, 0);
-        } else {
-          gw[h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, ob[h][k] - cw4, 0, 0);
-        }
+        const uint32_t w = sw[h][k];
+        const bool pass = CLS == 1 ? w >= plo : (w - plo <= pr) != pinv;
+        hubf[h] = hubf[h] || (__builtin_amdgcn_ubfe(lw[h][k], w, 1u) != 0u && pass);
+      }
+    // a probe instruction only when some lane of the wave has an L2 candidate in that slot
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+      for (int k = 0; k < NS; k++) {
+        gw[h][k] = 0u;
+        if (__ballot(ob[h][k] - cw4 < rest_b && !hubf[h]))
+          gw[h][k] = __builtin_amdgcn_raw_buffer_load_b32(fb_rs, hubf[h] ? 0xfffffff0u : ob[h][k] - cw4, 0, 0);
       }
     __builtin_amdgcn_sched_barrier(0);
     bool f[2], pend[2];
@@ -1338,22 +1327,17 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
       f[h] = fh;
       // pending: no passing hit, and a hit (then in an undecided bucket) or a fifth entry
       // (slot 3 set)
-      pend[h] = !fh && (ah || (S3 ? more[h] : sw[h][3] != 0xffffffffu));
+      pend[h] = !fh && (ah || sw[h][3] != 0xffffffffu);
     }
     unsigned long long f0 = __ballot(f[0]), f1 = __ballot(f[1]);
     unsigned long long p0 = __ballot(pend[0]), p1 = __ballot(pend[1]);
-    if (VAR & 16) {
-      // one store instruction: lane 0 the two next-frontier words, lane 1 the two pending words
-      if (lane < 2) {
-        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-        u64x2 v;
-        v.x = lane ? p0 : f0;
-        v.y = lane ? p1 : f1;
-        *reinterpret_cast<u64x2*>((lane ? pbits : nbits) + 2 * t) = v;
-      }
-    } else if (lane < 2) {
-      nbits[2 * t + lane] = lane ? f1 : f0;
-      pbits[2 * t + lane] = lane ? p1 : p0;
+    // one store instruction: lane 0 the two next-frontier words, lane 1 the two pending words
+    if (lane < 2) {
+      typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+      u64x2 v;
+      v.x = lane ? p0 : f0;
+      v.y = lane ? p1 : f1;
+      *reinterpret_cast<u64x2*>((lane ? pbits : nbits) + 2 * t) = v;
     }
     nfound += uint64_t(__popcll(f0) + __popcll(f1));
     npend += uint64_t(__popcll(p0) + __popcll(p1));
@@ -1367,7 +1351,7 @@ __global__ __launch_bounds__(1024, 8) void k_bu_fin(const uint2* __restrict__ lo
     }
   if (lane != 0) nfound = npend = nwords = 0;
   unsigned long long acc64[8] = {nfound, 0, nwords, npend, 0, 0, 0, 0};
-  if (atomic_sums) block_add_sums(acc64, 8, lds, partials);
+  if (atomic_sums) block_add_sums(acc64, 8, lds, partials, atomic_sums);
   else block_store_partials(acc64, 8, lds, partials);
 }
 
@@ -1585,7 +1569,7 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
     }
   }
   unsigned long long acc64[6] = {acc[0], odsum, acc[2], acc[3], acc[4], acc[5]};
-  if (atomic_sums) block_add_sums(acc64, 6, lds, partials);
+  if (atomic_sums) block_add_sums(acc64, 6, lds, partials, atomic_sums);
   else block_store_partials(acc64, 6, lds, partials);
 }
 
@@ -1684,7 +1668,7 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
                                                  const uint8_t* row_ok, int require_deg, int32_t* out,
                                                  unsigned long long* n_out, unsigned long long* partials,
                                                  uint16_t* bits, const uint32_t* __restrict__ odeg,
-                                                 unsigned long long* sums = nullptr) {
+                                                 unsigned long long* sums = nullptr, int shards = 1) {
   // tile = 256 threads x 4 chunks of 16 bytes = 16384 vertices; one returning atomic per tile
   // (1024-thread tiles, a quarter of the atomics, measured slower: 40 -> 47 us at hop 1);
   // n_set (partials[0]), the kept out-degree sum (partials[1]) and the kept count (partials[2])
@@ -1795,7 +1779,7 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
     __syncthreads();
   }
   // sums (zeroed by the caller): the block sums added there, no k_reduce_partials launch
-  if (sums) block_add_sums(acc, 3, lds64, sums);
+  if (sums) block_add_sums(acc, 3, lds64, sums, shards);
   else block_store_partials(acc, 3, lds64, partials);
 }
 
@@ -1853,7 +1837,7 @@ __global__ __launch_bounds__(1024) void k_starts_small(const int64_t* __restrict
   __shared__ unsigned long long s_w[32];  // [0, 16): per-wave counts, [16, 32): per-wave degree sums
   __shared__ unsigned long long s_carry[2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid < 256) Kd[tid] = 0ull;
+  for (int i = tid; i < int(kShardStride) * kSumShards; i += blockDim.x) Kd[i] = 0ull;  // every shard
   for (int i = tid; i < ns; i += blockDim.x) {
     const int32_t x = ht_lookup(keys, vals, mask, vids[i], has_min, min_gidx);
     g[i] = x;
@@ -2203,8 +2187,30 @@ struct Counters {
 // of one per word.  A single wave, so the release's wait on the wave's outstanding stores covers
 // every copy.  (One thread copying every word waited on each load in turn: ~10 us more.)
 __global__ void k_publish(const unsigned long long* __restrict__ src, int n, unsigned long long* __restrict__ dst,
-                          unsigned long long* seq_slot, unsigned long long seq) {
-  for (int i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+                          unsigned long long* seq_slot, unsigned long long seq, int shards) {
+  // shards > 1: word i is the sum of its shards src[i + s * kShardStride] (block_add_sums).  All
+  // loads of a lane (<= 4 words x kSumShards shards; n <= 256) are issued before any add: one
+  // round trip (a per-word shard loop had made this launch 3.6 -> 8.0 us, r12d)
+  if (shards <= 1) {
+    for (int i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+  } else {
+    unsigned long long x[4][kSumShards];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+      for (int s = 0; s < kSumShards; s++) {
+        const int i = int(threadIdx.x) + 64 * j;
+        x[j][s] = i < n && s < shards ? src[size_t(s) * kShardStride + size_t(i)] : 0ull;
+      }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int i = int(threadIdx.x) + 64 * j;
+      unsigned long long v = 0;
+#pragma unroll
+      for (int s = 0; s < kSumShards; s++) v += x[j][s];
+      if (i < n) dst[i] = v;
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(seq_slot, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -2213,11 +2219,12 @@ __global__ void k_publish(const unsigned long long* __restrict__ src, int n, uns
 // one-thread-block kernel writes them and a sequence word to coherent host memory and the host
 // spins on the word (a memcpy + hipStreamSynchronize round trip cost ~19 us, tools/launch_gap);
 // past 2 s without it the stream is synchronised the ordinary way, which reports a fault
-void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h, hipEvent_t before) {
+void fetch_counters(Ctx& c, const unsigned long long* d, int n, unsigned long long* h, hipEvent_t before,
+                    int shards) {
   if (n > 256) throw Error(NBG_E_INVALID_ARG, "fetch_counters: at most 256 words");
   if (before) NBG_HIP(hipEventRecord(before, c.stream));
   const uint64_t seq = ++c.pub_seq;
-  k_publish<<<1, 64, 0, c.stream>>>(d, n, h, c.host_seq, seq);
+  k_publish<<<1, 64, 0, c.stream>>>(d, n, h, c.host_seq, seq, std::max(shards, 1));
   NBG_HIP(hipGetLastError());
   if (c.opt("wait_trace", 0)) fprintf(stderr, "[nbg wait] rank %d: counter fetch of %d words\n", c.rank, n);
   wait_host_word(c, c.host_seq, seq);
@@ -2267,7 +2274,9 @@ void ensure_workspaces(Ctx& c, int64_t nF_cap) {
   c.ws_front[0].ensure(size_t(nF_cap + 64) * 4);
   c.ws_front[1].ensure(size_t(nF_cap + 64) * 4);
   c.ws_off.ensure(size_t(nF_cap + 2) * 8);
-  c.ws_counters.ensure(256 * 8);  // [0, 64) hop counters, [64, 256) speculative hop blocks
+  // [0, 64) hop counters, [64, 256) speculative hop blocks; then shards 1 .. kSumShards - 1 of
+  // every word (block_add_sums), kShardStride words apart
+  c.ws_counters.ensure(kShardStride * kSumShards * 8);
   c.ws_partials.ensure(size_t(kAggBlocks) * kSlots * 8);
   c.ws_bits_send.ensure(size_t(mb / 8 + 64));
   c.ws_bits_recv.ensure(size_t(mb / 8 + 64));
@@ -2531,7 +2540,7 @@ static void lds_limit(const void* kern, size_t shm) {
 
 void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* row_ptr, const uint8_t* row_ok,
                     int require_deg, int32_t* out, uint16_t* bits, unsigned long long* Kd,
-                    const uint32_t* odeg = nullptr, bool sums_zero = false) {
+                    const uint32_t* odeg = nullptr, bool sums_zero = false, int shards = 1) {
   // counters: Kd[0] list length (atomic), Kd[12] vertices set, Kd[13] kept out-degree sum,
   // Kd[14] kept vertices (= the list length, also when out == nullptr writes no list).
   // sums_zero: Kd[12, 15) are already zero, so the blocks add into them (bu_atomic_sums)
@@ -2540,7 +2549,7 @@ void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* 
   int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, std::min<int64_t>(kAggBlocks, c.opt("compact_grid", 1024)))));
   const bool atomic = sums_zero && c.opt("bu_atomic_sums", 1) != 0;
   k_compact<<<grid, 256, 0, c.stream>>>(map, lo, n, row_ptr, row_ok, require_deg, out, Kd, partials, bits, odeg,
-                                        atomic ? Kd + 12 : nullptr);
+                                        atomic ? Kd + 12 : nullptr, atomic ? shards : 1);
   if (!atomic) k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, Kd + 12);
   NBG_HIP(hipGetLastError());
 }
@@ -2641,15 +2650,12 @@ QArgs make_qargs(const EdgeSpace& es, int pk, int fcol, const FastArgs& fp) {
   return q;
 }
 
-// DISTINCT _dst output: the vids of a bitmap's set rows (option bits_u: word pairs per lane
-// and step, 8 or 4; r05 sweep: 8 takes the C3 final hop 266 -> 258 us)
+// DISTINCT _dst output: the vids of a bitmap's set rows (8 word pairs per lane and step; r05
+// sweep: 8 took the C3 final hop 266 -> 258 us against 4, removed in round 6)
 static void launch_bits_vids(Ctx& c, const uint32_t* bits, int64_t rows, int64_t lo, void* out,
                              unsigned long long* n_out, const unsigned long long* gate) {
   const int grid = grid_cap((rows + 31) / 32, 1024, 4096);
-  if (c.opt("bits_u", 8) == 8)
-    k_bits_compact<1, 8><<<grid, 1024, 0, c.stream>>>(bits, rows, lo, c.vid_of.as<int64_t>(), out, n_out, gate);
-  else
-    k_bits_compact<1, 4><<<grid, 1024, 0, c.stream>>>(bits, rows, lo, c.vid_of.as<int64_t>(), out, n_out, gate);
+  k_bits_compact<1, 8><<<grid, 1024, 0, c.stream>>>(bits, rows, lo, c.vid_of.as<int64_t>(), out, n_out, gate);
 }
 
 // k_bu_fin's word ranges from a query's bucket decisions (q_test: buckets below ulo answer
@@ -2707,7 +2713,8 @@ FinArgs fin_args(const QArgs& q) {
 // without a memory access).
 size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits, const uint32_t* odeg, int pk,
                       const FastArgs& fp, int fcol, unsigned long long* out, bool hop_front,
-                      unsigned long long* gate = nullptr, GateIn gi = GateIn{}, bool out_zero = false) {
+                      unsigned long long* gate = nullptr, GateIn gi = GateIn{}, bool out_zero = false,
+                      int shards = 1) {
   const Csr& tr = es.tr;
   if (pk != PK_NONE && pk != PK_FAST) throw Error(NBG_E_DEVICE, "bottom-up hop with a VM predicate");
   if (!es.pair_col[0].p) throw Error(NBG_E_DEVICE, "bottom-up hop without the quad slab");
@@ -2728,8 +2735,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   // rows past the last one that can be found (final) or extend the next frontier (non-final)
   // get zero words without being read (exact bounds, snapshot build_transpose)
   const int64_t work = std::min(ntiles, fast ? es.bu_in_tiles : es.bu_both_tiles);
-  const int U = c.opt(fast ? "bu_lean_u_final" : "bu_lean_u", 1) == 1 ? 1 : 2;
-  const int64_t waves = std::max<int64_t>(1, (work + U - 1) / U);
+  const int64_t waves = std::max<int64_t>(1, work);
   // hub words in LDS (bu_lean_lds_kb KiB, 0 = off): 1024-thread blocks, two per CU
   const int64_t fb_words = (c.n_global + 31) / 32;
   // bu_hub_cap (tests): at most that many hub words, so small graphs exercise the L2 probes too
@@ -2751,7 +2757,9 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   // option bu_atomic_sums: both passes add their block sums into `out` (zeroed first unless the
   // caller's block is known zero) and no k_reduce_partials launch follows
   // (r06j: 0.4796 -> 0.4663 ms per C3 query, the two k_reduce_partials launches gone)
-  const int atomic_sums = int(c.opt("bu_atomic_sums", 1) != 0 && c.opt("bu_rest_dbg", 0) == 0);
+  // (sharded sums, shards > 1: only into a block the caller zeroed with its shards)
+  const int atomic_sums =
+      c.opt("bu_atomic_sums", 1) != 0 && c.opt("bu_rest_dbg", 0) == 0 ? (out_zero ? std::max(shards, 1) : 1) : 0;
   unsigned long long* partials = atomic_sums ? out : c.ws_partials.as<unsigned long long>();
   if (atomic_sums && !out_zero) NBG_HIP(hipMemsetAsync(out, 0, 8 * 8, c.stream));
   auto* nb = reinterpret_cast<unsigned long long*>(nbits);
@@ -2764,22 +2772,18 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     kern<<<grid, bs, shm, c.stream>>>(lo, hi, ntiles, work, fb, fb_bytes, nb, pbits, od, q, partials, cw,
                                       es.odeg8.as<uint8_t>(), gate, gi, atomic_sums);
   };
-  int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (U == 2 ? 1 : 0) + (cw > 0 ? 2 : 0);
-  if (sel == 2 && c.opt("bu_lean_nt", 1) != 0 && (fast || es.odeg8.p)) sel = 6;  // non-temporal, 1 B degrees
-  // default 3: the probe skip and hub-first L2 probes (r06j: 100.7 -> 91.6 us at C3 hop 2); 7 adds
-  // one store per tile
-  const int64_t lskip = c.opt("bu_lean_skip", 3);
-  if (sel == 6 && lskip != 0) sel = lskip == 3 ? 8 : lskip == 7 ? 9 : 7;  // + probe skip
+  // sel 0 / 2: no hub copy / hub copy; 4 / 5 the counting (diagnostic) instantiations; 8 the
+  // default: non-temporal slab, 1 B degrees, the probe skip and hub-first L2 probes (r06j: 100.7
+  // -> 91.6 us at C3 hop 2).  Removed in round 6, each measured without gain: two tiles per
+  // iteration (bu_lean_u 2), one store per tile in the non-final pass (bu_lean_skip 7), the probe
+  // skip without the hub-first probes (bu_lean_skip 1).
+  int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (cw > 0 ? 2 : 0);
+  if (sel == 2 && c.opt("bu_lean_nt", 1) != 0 && (fast || es.odeg8.p)) sel = 8;
 #define NBG_LEAN(PKV)                                \
   switch (sel) {                                     \
-    case 9: go(k_bu_lean<PKV, 1, 1, 0, 1, 7>); break; \
     case 8: go(k_bu_lean<PKV, 1, 1, 0, 1, 3>); break; \
-    case 7: go(k_bu_lean<PKV, 1, 1, 0, 1, 1>); break; \
-    case 6: go(k_bu_lean<PKV, 1, 1, 0, 1>); break;   \
     case 0: go(k_bu_lean<PKV, 1, 0, 0>); break;      \
-    case 1: go(k_bu_lean<PKV, 2, 0, 0>); break;      \
     case 2: go(k_bu_lean<PKV, 1, 1, 0>); break;      \
-    case 3: go(k_bu_lean<PKV, 2, 1, 0>); break;      \
     case 4: go(k_bu_lean<PKV, 1, 0, 1>); break;      \
     default: go(k_bu_lean<PKV, 1, 1, 1>); break;     \
   }
@@ -2793,32 +2797,18 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
     const size_t fshm = size_t((cw + 2) & ~1) * 4 + size_t(kSlots) * 16 * 8;
     const uint32_t rest = fb_bytes > uint32_t(cw) * 4u ? fb_bytes - uint32_t(cw) * 4u : 0u;
     const int nt = int(c.opt("bu_fin_nt", 1) != 0);
-    // default 49: the probe skip, one store per tile, hub-first L2 probes (r06h sweep:
-    // k_bu_fin 124.9 -> 108.1 us; the 16-byte-lane and blocked-tile variants measured no gain)
-    int var = cls1 && nt ? int(c.opt("bu_fin_var", 49) & (1 | 16 | 32 | 64)) : 0;
-    if (!es.slab3.p) var &= ~64;  // the 3-slot slab is built at finalize only with option bu_slab3
-    if (var & 64) var = 113;      // (the one 3-slot instantiation)
-    const uint2* fhi = (var & 64) ? reinterpret_cast<const uint2*>(es.slab3.p) : hi;
     auto gof = [&](auto kern) {
       if (fshm > 48 * 1024) lds_limit(reinterpret_cast<const void*>(kern), fshm);
-      kern<<<grid, bs, fshm, c.stream>>>(lo, fhi, ntiles, work, fb, nb, pbits, fa, partials, cw, rest, gate, gi,
+      kern<<<grid, bs, fshm, c.stream>>>(lo, hi, ntiles, work, fb, nb, pbits, fa, partials, cw, rest, gate, gi,
                                          atomic_sums);
     };
-    switch ((cls1 ? 1 : 0) | nt << 1 | var << 2) {
+    switch ((cls1 ? 1 : 0) | nt << 1) {
       case 0: gof(k_bu_fin<0, 0>); break;
       case 1: gof(k_bu_fin<1, 0>); break;
       case 2: gof(k_bu_fin<0, 1>); break;
-      case 3: gof(k_bu_fin<1, 1>); break;
-      case 3 | (1 << 2): gof(k_bu_fin<1, 1, 1>); break;
-      case 3 | (16 << 2): gof(k_bu_fin<1, 1, 16>); break;
-      case 3 | (17 << 2): gof(k_bu_fin<1, 1, 17>); break;
-      case 3 | (32 << 2): gof(k_bu_fin<1, 1, 32>); break;
-      case 3 | (33 << 2): gof(k_bu_fin<1, 1, 33>); break;
-      case 3 | (48 << 2): gof(k_bu_fin<1, 1, 48>); break;
-      case 3 | (113 << 2): gof(k_bu_fin<1, 1, 113>); break;
-      default: gof(k_bu_fin<1, 1, 49>); break;
+      default: gof(k_bu_fin<1, 1>); break;
     }
-    snprintf(fin_nm, sizeof fin_nm, "nbg::k_bu_fin<%d, %d, %d>", cls1 ? 1 : 0, nt, var);
+    snprintf(fin_nm, sizeof fin_nm, "nbg::k_bu_fin<%d, %d>", cls1 ? 1 : 0, nt);
   } else if (fast) {
     NBG_LEAN(PK_FAST)
   } else {
@@ -2897,13 +2887,12 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   if (fin)
     snprintf(nm, sizeof nm, "%s", fin_nm);
   else
-    snprintf(nm, sizeof nm, "nbg::k_bu_lean<%d, %d, %d, %d%s>", pk, probe_stats ? 1 : U, cw > 0 ? 1 : 0,
-             probe_stats ? 1 : 0,
-             sel == 9 ? ", 1, 7" : sel == 8 ? ", 1, 3" : sel == 7 ? ", 1, 1" : sel == 6 ? ", 1, 0" : ", 0, 0");
+    snprintf(nm, sizeof nm, "nbg::k_bu_lean<%d, 1, %d, %d%s>", pk, cw > 0 ? 1 : 0, probe_stats ? 1 : 0,
+             sel == 8 ? ", 1, 3" : ", 0, 0");
   c.bu_kernel_name = nm;
   // the non-final first pass reads one out-degree per row of its work tiles: 1 B (odeg8, the
   // non-temporal instantiations) or 4 B (odeg)
-  if (!fast) c.bu_od_bytes = uint64_t(work) * 128u * (sel >= 6 && sel <= 9 ? 1u : 4u);
+  if (!fast) c.bu_od_bytes = uint64_t(work) * 128u * (sel == 8 ? 1u : 4u);
   const int wn = fast ? (W == 1 || W == 2 || W == 4 ? W : 8) : 0;
   snprintf(nm, sizeof nm, "nbg::k_bu_rest_lean<%d, %d, %d, %d>", pk, wn, rcw > 0 ? 1 : 0, use_rec ? 1 : 0);
   c.bu_rest_rec = use_rec;
@@ -3100,6 +3089,17 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
                      c.opt("starts_small", 1) != 0;
   // counters summed over ranks on the device (dev_allsum) land at K.d[48, 52)
   const bool multi = c.sharded;
+  // one rank: the hop-1 compaction and the speculated hops add their block sums into kSumShards
+  // shards (option sum_shards; block_add_sums), folded by their readers -- the gates and the
+  // counter fetches below.  Shards are zero at the query start (k_starts_small / the memset);
+  // clean_shards zeroes them again before any later dense use of the same words.
+  const int ks = multi ? 1 : int(std::min<int64_t>(std::max<int64_t>(c.opt("sum_shards", kSumShards), 1), kSumShards));
+  bool shards_dirty = false;
+  auto clean_shards = [&]() {
+    if (!shards_dirty) return;
+    NBG_HIP(hipMemsetAsync(K.d + kShardStride, 0, kShardStride * size_t(ks - 1) * 8, c.stream));
+    shards_dirty = false;
+  };
   // the small-start path's one block reads the starts from coherent pinned host memory (the
   // stream's previous query finished before this one was enqueued): no copy between queries
   const int64_t* k_starts = d_starts;
@@ -3132,7 +3132,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     NBG_HIP(hipGetLastError());
     nF = ns;  // an upper bound: the entries past the list have degree 0
   } else {
-    NBG_HIP(hipMemsetAsync(K.d, 0, 256 * 8, c.stream));
+    NBG_HIP(hipMemsetAsync(K.d, 0, kShardStride * kSumShards * 8, c.stream));
   }
   if (ns && !fast1) {
     if (s.steps == 1 && !s.distinct) {
@@ -3367,8 +3367,12 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
     spec.clear();
     if (!spec_ok) return;
     // the blocks start at zero (query start); a second chain in one query reuses them
-    if (spec_blocks_used) NBG_HIP(hipMemsetAsync(SPd, 0, 16 * 12 * 8, c.stream));
+    if (spec_blocks_used) {
+      clean_shards();
+      NBG_HIP(hipMemsetAsync(SPd, 0, 16 * 12 * 8, c.stream));
+    }
     spec_blocks_used = true;
+    if (ks > 1) shards_dirty = true;
     const uint32_t* in = bitsA;
     uint32_t* outb = bitsB;
     const unsigned long long* pg = nullptr;
@@ -3380,6 +3384,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // the hop's first pass evaluates its gate (GateIn) and publishes it at blk[8]
       GateIn gi;
       gi.e = e, gi.n = n, gi.pg = pg, gi.thr = spec_thr;
+      gi.shards = ks;  // (several ranks: ks = 1)
       const int32_t hop = hop0 + int32_t(spec.size());
       // several ranks: the frontier bitmaps of every rank (the exchange runs whatever the gate
       // says: every rank enqueued it)
@@ -3396,12 +3401,12 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const size_t ia = timing_event(c);
       size_t ik;
       if (!fin) {
-        ik = launch_bu_lean(c, es, fb, outb, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, blk, true, blk + 8, gi, true);
+        ik = launch_bu_lean(c, es, fb, outb, es.odeg.as<uint32_t>(), PK_NONE, fp, -1, blk, true, blk + 8, gi, true, ks);
       } else {
         FastArgs tfp = fp0;
         if (fpk0.kind == PK_FAST) tfp.data = es.tr.props[size_t(fpk0.col)].data.p;
         ik = launch_bu_lean(c, es, fb, outb, nullptr, fpk0.kind, tfp, fpk0.kind == PK_FAST ? fpk0.col : -1, blk, true,
-                            blk + 8, gi, true);
+                            blk + 8, gi, true, ks);
         void* vout = vid_block(spec_vids, spec_hvids);
         launch_bits_vids(c, outb, es.tr.n_rows, lo, vout, blk + 9, blk + 8);
       }
@@ -3506,6 +3511,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   }
   for (int32_t step = 1; step < s.steps; step++) {
     c.timing.steps_run++;
+    clean_shards();  // (the speculated hops' sums were fetched: dense counters from here on)
     if (fast1 && step == 1) {
       // the first hop top-down from k_starts_small's list (nF = ns bounds it), compaction, then
       // one round trip for the start counts and the next frontier's together
@@ -3520,7 +3526,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       const bool lazy = bu_ok && c.opt("compact_list", 0) == 0;
       // (K.d[0, 256) are zero: k_starts_small cleared the counters)
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
-                     K.d, es.odeg.as<uint32_t>(), true);
+                     K.d, es.odeg.as<uint32_t>(), true, ks);
+      if (ks > 1) shards_dirty = true;
       // several ranks: the counts over ranks -- piggy: carried by the first speculated hop's
       // frontier exchange (its gate publishes them); else found, next out-degree sum and hop-1
       // entries summed into K.d[48, 51)
@@ -3533,7 +3540,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         dev_allsum(c, K.d, {12, 13, 41}, K.d + 48);
       }
       // (the device work ends here when the speculated final hop runs: ev[1] ahead of the fetch)
-      fetch_counters(c, K.d, spec_words(multi ? 52 : 42), K.h, spec_final() && tot_ev ? c.ev[1] : nullptr);
+      fetch_counters(c, K.d, spec_words(multi ? 52 : 42), K.h, spec_final() && tot_ev ? c.ev[1] : nullptr, ks);
       const int64_t nF1 = int64_t(K.h[40]), E1 = int64_t(K.h[41]);
       if (!s.distinct) hop1_scanned = int64_t(K.h[30]);
       c.timing.edges_scanned += uint64_t(hop1_scanned >= 0 ? hop1_scanned : E1);
@@ -3639,7 +3646,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         piggy_used = false;
         dev_allsum(c, K.d, {12, 13}, K.d + 48);
       }
-      fetch_counters(c, K.d, spec_words(multi ? 50 : 16), K.h, spec_final() && tot_ev ? c.ev[1] : nullptr);
+      fetch_counters(c, K.d, spec_words(multi ? 50 : 16), K.h, spec_final() && tot_ev ? c.ev[1] : nullptr, ks);
       nF = lazy ? 0 : int64_t(K.h[0]);
       list_n = lazy ? int64_t(K.h[14]) : -1;
       E = int64_t(K.h[13]);
@@ -3663,6 +3670,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   }
   // ---- final step ----
   c.timing.steps_run++;
+  if (!fin_done) clean_shards();
   if (multi_root) {
     env.in_root = root_buf[root_cur].as<int32_t>();
     env.in_root_tab = root_tab.as<int32_t>();
@@ -3711,7 +3719,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         const uint64_t kb = bu_first_bytes(fin_h, es.tr.n_rows, 0), hb = kb + bu_rest_bytes(fin_h, pw, c.bu_rest_rec);
         c.timing.expand_bytes += hb + uint64_t(es.tr.n_rows) / 8 + uint64_t(nrows) * 16;
         c.timing.hop(1, true, 0.0, fin_h, 0.0, kb);
-        c.timing.name_last_hop(fin_k0, fin_k1, c.opt("bits_u", 8) == 8 ? "nbg::k_bits_compact<1, 8>" : "nbg::k_bits_compact<1, 4>");
+        c.timing.name_last_hop(fin_k0, fin_k1, "nbg::k_bits_compact<1, 8>");
       } else {
         vout = nullptr;
       }
@@ -3740,7 +3748,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
         // + the DISTINCT _dst output (k_bits_compact<1>): next bits once, vid_of read + vid written
         c.timing.expand_bytes += hb + uint64_t(tr.n_rows) / 8 + uint64_t(nrows) * 16;
         c.timing.hop(1, true, 0.0, K.h + 8, 0.0, kb);
-        c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name, c.opt("bits_u", 8) == 8 ? "nbg::k_bits_compact<1, 8>" : "nbg::k_bits_compact<1, 4>");
+        c.timing.name_last_hop(c.bu_kernel_name, c.bu_rest_name, "nbg::k_bits_compact<1, 8>");
       } else {
         vids.alloc(size_t(c.n_global + 64) * 8);
         ensure_off();

@@ -593,20 +593,20 @@ def final_bu_kernels(sp):
 
 
 @pytest.mark.parametrize("fin", [0, 1])
-@pytest.mark.parametrize("u,lds,rest_lds,rsteps,unroll,cap", [(1, 64, 64, 4, 1, 36 * 1024), (2, 64, 0, 1, 2, 36 * 1024),
-                                                              (1, 0, 64, 2, 1, 36 * 1024), (2, 1, 1, 4, 2, 8)])
-def test_rmat_bottom_up_shapes(rmat12, u, lds, rest_lds, rsteps, unroll, cap, fin):
+@pytest.mark.parametrize("lds,rest_lds,rsteps,unroll,cap", [(64, 64, 4, 1, 36 * 1024), (64, 0, 1, 2, 36 * 1024),
+                                                          (0, 64, 2, 1, 36 * 1024), (1, 1, 4, 2, 8)])
+def test_rmat_bottom_up_shapes(rmat12, lds, rest_lds, rsteps, unroll, cap, fin):
     """the bottom-up kernels (k_bu_lean / k_bu_fin first pass + k_bu_rest_lean) for every tile / LDS hub /
     rest-chunk shape, non-final and final hops, thresholds that leave rows pending past the slab,
     against the oracle; the hop stats name the kernels that ran"""
     sp, st = rmat12
-    for k, v in {"bu_force": 1, "bu_lean_u": u, "bu_lean_u_final": u, "bu_lean_lds_kb": lds,
+    for k, v in {"bu_force": 1, "bu_lean_lds_kb": lds,
                  "bu_lean_lds_kb_final": lds, "bu_rest_lds_kb": rest_lds, "bu_rest_lds_kb_final": rest_lds,
                  "bu_rest_steps": rsteps, "bu_unroll": unroll, "bu_hub_cap": cap, "bu_fin": fin}.items():
         sp.set_option(k, v)
     # the final hop's first pass: k_bu_fin (the default) or k_bu_lean (bu_fin = 0; its
     # non-temporal instantiation carries a fifth argument)
-    first = "nbg::k_bu_fin<" if fin else f"nbg::k_bu_lean<1, {u}, {1 if lds else 0}, 0"
+    first = "nbg::k_bu_fin<" if fin else f"nbg::k_bu_lean<1, 1, {1 if lds else 0}, 0"
     starts = sorted(set(seeds_from(12, 48, seed=23)))
     pending = 0
     for k in (0, 499, 990):
@@ -630,7 +630,7 @@ def test_rmat_bottom_up_shapes(rmat12, u, lds, rest_lds, rsteps, unroll, cap, fi
     r_ = st.go(starts, 3, FOLLOW)
     assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0)))
     hops = [h for h in sp.last_timing()["hops"] if h["mode"] == "bottom-up"]
-    assert hops and hops[0]["kernels"][0].startswith(f"nbg::k_bu_lean<0, {u}, {1 if lds else 0}, 0")
+    assert hops and hops[0]["kernels"][0].startswith(f"nbg::k_bu_lean<0, 1, {1 if lds else 0}, 0")
 
 
 OPS = {">": lambda c, k: c > k, ">=": lambda c, k: c >= k, "<": lambda c, k: c < k, "<=": lambda c, k: c <= k,

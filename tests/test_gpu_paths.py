@@ -166,15 +166,14 @@ def test_list_overflow_recovery():
     sp.close()
 
 
-@pytest.mark.parametrize("probe,vmajor", [(0, 1), (1, 1), (1, 0), (0, 0)])
-def test_meet_probe_on_and_off_match_oracle(rmat, probe, vmajor):
+@pytest.mark.parametrize("probe", [0, 1])
+def test_meet_probe_on_and_off_match_oracle(rmat, probe):
     """the early-exit meet probe (pairs one edge short of meeting skip the expansion) and the
-    plain level-by-level expansion, over vertex-major and pair-major distance bytes, give the
-    oracle's hop counts and canonical paths"""
+    plain level-by-level expansion give the oracle's hop counts and canonical paths (the
+    vertex-major distance layout, sp_vmajor, lost and was removed in round 6)"""
     scale, sp, st = rmat
     sp.set_option("sp_probe", probe)
-    sp.set_option("sp_vmajor", vmajor)
-    sp.set_option("sp_dev", int(probe == 1 and vmajor == 0))
+    sp.set_option("sp_dev", int(probe == 1))
     try:
         s, t = synth.pairs(scale, 16, 1, 300, pick_seed=17)
         es, et_ = edge_case_pairs(scale)
@@ -185,14 +184,13 @@ def test_meet_probe_on_and_off_match_oracle(rmat, probe, vmajor):
     finally:
         sp.set_option("sp_dev", 1)
         sp.set_option("sp_probe", 1)
-        sp.set_option("sp_vmajor", 0)
 
 
-@pytest.mark.parametrize("dev,ilv,vmajor", [(1, 1, 0), (1, 0, 0), (0, 1, 0), (0, 0, 0), (0, 1, 1), (0, 0, 1)])
-def test_distance_layouts_match_oracle(rmat, dev, ilv, vmajor):
+@pytest.mark.parametrize("dev,ilv", [(1, 1), (1, 0), (0, 1), (0, 0)])
+def test_distance_layouts_match_oracle(rmat, dev, ilv):
     """the distance bytes interleaved by side (sp_ilv: one 2-byte load reads both sides of a vertex)
-    or in two separate halves, pair-major or vertex-major, device-driven or host-driven: the
-    oracle's paths; the layout switched between calls leaves the bytes clean (all unseen)"""
+    or in two separate halves, device-driven or host-driven: the oracle's paths; the layout
+    switched between calls leaves the bytes clean (all unseen)"""
     scale, sp, st = rmat
     s, t = synth.pairs(scale, 16, 1, 300, pick_seed=31)
     es, et_ = edge_case_pairs(scale)
@@ -201,16 +199,14 @@ def test_distance_layouts_match_oracle(rmat, dev, ilv, vmajor):
         for lay in (ilv, 1 - ilv, ilv):
             sp.set_option("sp_dev", dev)
             sp.set_option("sp_ilv", lay)
-            sp.set_option("sp_vmajor", vmajor)
             for max_steps in (2, 8):
                 got = sp.shortest_path(src, dst, FOLLOW, max_steps).rows()
                 assert got == oracle_paths(st, src, dst, FOLLOW, max_steps), (lay, max_steps)
-            if dev and not vmajor:
+            if dev:
                 assert sp.last_timing()["spec_hops"] >= 1  # the batches ran device-driven
     finally:
         sp.set_option("sp_dev", 1)
         sp.set_option("sp_ilv", 1)
-        sp.set_option("sp_vmajor", 0)
 
 
 @pytest.mark.parametrize("begin_x", [1, 0])

@@ -276,48 +276,23 @@ def test_configs2_rmat26_bench_query_digest():
         sp.close()
 
 
-@pytest.mark.parametrize("var,hub_cap", [(0, None), (1, None), (49, None), (49, 1024), (17, None), (33, 1024)])
-def test_bu_fin_variants_rmat20(rmat20, var, hub_cap):
-    """the k_bu_fin variants (bu_fin_var bits: probe-instruction skip, one store per tile, no L2
-    probe for rows a hub word found) and the non-final pass's (bu_lean_skip 1 / 3 / 7: probe skip,
-    hub-first, one store) against the committed digest, with the hub capped too"""
+@pytest.mark.parametrize("nt,cls,hub_cap", [(1, 1, None), (1, 1, 1024), (0, 1, None), (1, 0, 1024)])
+def test_bu_fin_instantiations_rmat20(rmat20, nt, cls, hub_cap):
+    """every k_bu_fin instantiation (non-temporal slab loads or not, the one-range "greater than"
+    compare or the general range test) against the committed digest, with the hub copy capped too
+    (the L2 probes then answer most rows).  Round 6 removed the variant knobs that lost
+    (bu_fin_var, bu_lean_skip, bu_slab3: DESIGN.md section 6)"""
     sp, g = rmat20
-    sp.set_option("bu_fin_var", var)
+    sp.set_option("bu_fin_nt", nt)
+    sp.set_option("bu_fin_cls", cls)
     if hub_cap:
         sp.set_option("bu_hub_cap", hub_cap)
     try:
-        for lskip in (1, 3, 7, 0):
-            sp.set_option("bu_lean_skip", lskip)
-            r = bench_query(sp, 20)
-            check_gold("go3_where499_distinct_s20", r.columns[0], r.edges_scanned)
-            hops = sp.last_timing()["hops"]
-            assert hops[-1]["kernels"][0] == f"nbg::k_bu_fin<1, 1, {var}>", hops[-1]["kernels"]
+        r = bench_query(sp, 20)
+        check_gold("go3_where499_distinct_s20", r.columns[0], r.edges_scanned)
+        hops = sp.last_timing()["hops"]
+        assert hops[-1]["kernels"][0] == f"nbg::k_bu_fin<{cls}, {nt}>", hops[-1]["kernels"]
     finally:
-        for k in ("bu_fin_var", "bu_hub_cap", "bu_lean_skip"):
+        for k in ("bu_fin_nt", "bu_fin_cls", "bu_hub_cap"):
             sp.unset_option(k)
-
-
-def test_bu_fin_three_slot_slab_rmat20():
-    """the 3-slot slab (bu_slab3 at finalize, bu_fin_var bit 64: slots 0-2 in 12 B a row, a
-    fourth entry flagged in bit 31 of slot 2) against the committed digest, with the hub copy on
-    and capped (the L2 probes then answer most rows); without the slab the option falls back"""
-    sp = rmat_space(20, bu_slab3=1)
-    try:
-        for hub_cap in (None, 1024):
-            if hub_cap:
-                sp.set_option("bu_hub_cap", hub_cap)
-            sp.set_option("bu_fin_var", 113)
-            r = bench_query(sp, 20)
-            check_gold("go3_where499_distinct_s20", r.columns[0], r.edges_scanned)
-            hops = sp.last_timing()["hops"]
-            assert hops[-1]["kernels"][0] == "nbg::k_bu_fin<1, 1, 113>", hops[-1]["kernels"]
-            # 3 slab words a row were read (the hop's counters feed the byte model)
-            sp.set_option("bu_fin_var", 49)
-            r4 = bench_query(sp, 20)
-            check_gold("go3_where499_distinct_s20", r4.columns[0], r4.edges_scanned)
-            h4 = sp.last_timing()["hops"][-1]
-            assert h4["kernels"][0] == "nbg::k_bu_fin<1, 1, 49>"
-            assert hops[-1]["c"][2] * 4 == h4["c"][2] * 3, (hops[-1]["c"][2], h4["c"][2])
-    finally:
-        sp.close()
 
