@@ -541,6 +541,11 @@ struct Ctx {
     int64_t dv_B = 0, dv_cap = 0, dv_cap_ch = 0, dv_cap_wch = 0, dv_gf_log2 = -1;
     bool dv_pf_on = false;
     bool dv_clean = false;  // filter words and counters all zero
+    // per direction (0 out, 1 in): min(degree, 65535) of every row of the CSR the last call used,
+    // rebuilt when that CSR changed (row_ptr block, rows or commit count differ)
+    DevBuf deg16[2];
+    const void* deg16_rp[2] = {nullptr, nullptr};
+    int64_t deg16_rows[2] = {-1, -1}, deg16_commits[2] = {-1, -1};
   } sp;
   // coherent pinned host block of the device-driven batches: publish slots, the pairs, results
   void* sp_host = nullptr;

@@ -67,11 +67,25 @@ struct SpCsr {  // one direction's adjacency over the owned rows
   const int64_t* row_ptr;
   const int32_t* col;     // global gidx of the other end
   const uint8_t* row_ok;  // rows whose keys sit outside hash(vid)'s part are invisible
+  // min(degree, 65535) per row, 0 where row_ok is 0 (null: off; 65535: read row_ptr): a claim's
+  // degree from a 2-byte entry of an array the Infinity Cache holds (66 MB at RMAT-26) instead of
+  // the 16-byte row_ptr pair of a 262 MB array (option sp_deg16)
+  const uint16_t* deg16;
 };
 
 __device__ inline int64_t sp_deg(const SpCsr& g, uint32_t r) {
+  if (g.deg16) {
+    const uint32_t d = g.deg16[r];
+    if (d != 0xFFFFu) return d;
+  }
   if (g.row_ok && !g.row_ok[r]) return 0;
   return g.row_ptr[r + 1] - g.row_ptr[r];
+}
+__global__ void k_deg16(const int64_t* row_ptr, const uint8_t* row_ok, int64_t n, uint16_t* out) {
+  for (int64_t r = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; r < n; r += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t d = row_ok && !row_ok[r] ? 0 : row_ptr[r + 1] - row_ptr[r];
+    out[r] = uint16_t(d < 0xFFFF ? d : 0xFFFF);
+  }
 }
 
 struct SpState {  // per-pair arrays, B entries each
@@ -1300,6 +1314,12 @@ __device__ inline void filt_mark(const SpFilt& f, uint32_t side, uint32_t l, uin
     atomicOr(f.gf + (h >> f.gshift), gf_mask(h));
   }
 }
+// the global filter's mark alone (k_dv_expand gathers a chunk's pair-filter bits in LDS instead)
+__device__ inline void gf_mark(const SpFilt& f, uint32_t side, uint32_t l, uint32_t p, uint32_t v) {
+  if (!f.gf || l < 1 || l >= uint32_t(kLv)) return;
+  const uint64_t h = gf_hash(side * kLv + l, p, v);
+  atomicOr(f.gf + (h >> f.gshift), gf_mask(h));
+}
 // the chunk's pair row of the pair filter (side, l) in registers: lane i holds words 2i, 2i + 1
 __device__ inline uint2 pf_load(const SpFilt& f, uint32_t side, int32_t l, uint32_t p, bool& on) {
   on = f.pf && l >= 1 && l < kLv;
@@ -1921,8 +1941,13 @@ __device__ inline void dv_flush_block(DvStage& s, unsigned long long* cnt, unsig
 template <int OCC>
 __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpFilt f, SpCsr g0, SpCsr g1,
                                                         uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo, int32_t it,
-                                                        int32_t lg_sub) {
+                                                        int32_t lg_sub, int32_t pf_agg) {
   __shared__ uint64_t s_stage[4][2][kDvStage];
+  // per wave, the pair-filter row its current chunk fills: every claim of a chunk is one
+  // (side, pair, level), so the chunk's bits are OR-ed here and leave as at most 128 word atomics
+  // over one contiguous 512-byte row (option sp_dv_pf_lds, default 1) instead of one scattered
+  // memory-side atomic per claim
+  __shared__ uint32_t s_pf[4][128];
   // a producer overflowed: its tables are incomplete and the host re-runs the batch, so the block
   // expands nothing -- but the probe's claims still go to the arena below, which is the only
   // record the host's abort resets distance bytes from (block-uniform)
@@ -1938,7 +1963,9 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
   uint64_t* const out1 = d.live[it & 1][1];
   DvStage sg0{s_stage[wid][0], 0u}, sg1{s_stage[wid][1], 0u};
   unsigned long long claims = 0, entries = 0;
-  if (!skip)
+  // sp_dv_diag (timing only, wrong results): bit 4 no chunk is expanded, bit 5 no probe claim
+  // is moved to the arena
+  if (!skip && !(f.diag & 16))
   chunk_groups(
       total << lg_sub,
       [&](int64_t vc, ChunkRec& r) {
@@ -1960,6 +1987,12 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
         const uint16_t* const bdp = reinterpret_cast<const uint16_t*>(d0 + ((uint64_t(p) * uint64_t(n)) << 1));
         entries += uint64_t(r.x1 - r.x0) * (lane == 0);
         unsigned long long dsum = 0;
+        const bool pf_lds = pf_agg && f.pf && l + 1 < uint32_t(kLv);  // wave-uniform
+        if (pf_lds) {
+          s_pf[wid][lane] = 0u;
+          s_pf[wid][lane + 64] = 0u;
+          __builtin_amdgcn_wave_barrier();
+        }
         for (int64_t x = step_start(r.x0); x < r.x1; x += 64 * kProbeU) {
           uint32_t w[kProbeU];
           col_step(g.col, x, r.x0, r.x1, lo, w);
@@ -1988,7 +2021,13 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
             bool meet = false;
             uint32_t dt = 0;
             if (cl) {
-              filt_mark(f, side, l + 1, p, w[u]);
+              if (pf_lds) {
+                const uint32_t b = pf_bit(w[u]);
+                atomicOr(&s_pf[wid][b >> 5], 1u << (b & 31u));
+                gf_mark(f, side, l + 1, p, w[u]);
+              } else {
+                filt_mark(f, side, l + 1, p, w[u]);
+              }
               dsum += (unsigned long long)sp_deg(g, w[u]) + 1;
               const uint32_t ob = sh ? obt[u] : uint32_t(odp[w[u]]);
               if (ob != 0xFFu) {
@@ -2007,6 +2046,13 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
             dput(d.meet, d.cap_meet, gcnt(d.cnt, D_MEET), d.cnt, meet, mk_tup(1, p, dt, w[u]));
           }
         }
+        if (pf_lds) {  // the chunk's row: nonzero words OR-ed into the pair filter
+          __builtin_amdgcn_wave_barrier();
+          uint32_t* const row = f.pf + (size_t(side * kLv + l + 1) * uint32_t(f.B) + p) * 128;
+          const uint32_t w0 = s_pf[wid][lane], w1 = s_pf[wid][lane + 64];
+          if (w0) atomicOr(row + lane, w0);
+          if (w1) atomicOr(row + lane + 64, w1);
+        }
         dsum = wsum(dsum);
         if (lane == 0 && dsum) {
           atomicAdd(st.deg + side * B + p, dsum);
@@ -2015,7 +2061,7 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
         }
       });
   // the probe's claims: meet tuples (the vertex at the backward depth) + arena entries
-  for (int64_t c0 = wave * 64; c0 < total; c0 += nwaves * 64) {
+  for (int64_t c0 = wave * 64; c0 < total && !(f.diag & 32); c0 += nwaves * 64) {
     const int64_t c = c0 + lane;
     const uint64_t v = c < total ? d.slot[c] : ~0ull;
     const bool hit = v != ~0ull;
@@ -2725,8 +2771,22 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   const int32_t ilv = c.opt("sp_ilv", 1) != 0 ? 1 : 0;
   uint8_t* d0 = c.sp_dist[0].as<uint8_t>();
   uint8_t* d1 = ilv ? d0 + 1 : d0 + c.sp_dist_bytes;
-  SpCsr gout{cout->row_ptr.as<int64_t>(), cout->col.as<int32_t>(), cout->row_ok.as<uint8_t>()};
-  SpCsr gin{cin->row_ptr.as<int64_t>(), cin->col.as<int32_t>(), cin->row_ok.as<uint8_t>()};
+  auto deg16 = [&](int k, const Csr* g) -> const uint16_t* {
+    if (c.opt("sp_deg16", 1) == 0 || g->n_rows <= 0) return nullptr;
+    if (W.deg16_rp[k] != g->row_ptr.p || W.deg16_rows[k] != g->n_rows || W.deg16_commits[k] != c.commits) {
+      PoolScope none(nullptr);  // kept across calls, outside the query pool
+      W.deg16[k].alloc(size_t(g->n_rows) * 2 + 64);
+      k_deg16<<<grid_n(g->n_rows), 256, 0, c.stream>>>(g->row_ptr.as<int64_t>(), g->row_ok.as<uint8_t>(), g->n_rows,
+                                                       W.deg16[k].as<uint16_t>());
+      NBG_HIP(hipGetLastError());
+      W.deg16_rp[k] = g->row_ptr.p;
+      W.deg16_rows[k] = g->n_rows;
+      W.deg16_commits[k] = c.commits;
+    }
+    return W.deg16[k].as<uint16_t>();
+  };
+  SpCsr gout{cout->row_ptr.as<int64_t>(), cout->col.as<int32_t>(), cout->row_ok.as<uint8_t>(), deg16(0, cout)};
+  SpCsr gin{cin->row_ptr.as<int64_t>(), cin->col.as<int32_t>(), cin->row_ok.as<uint8_t>(), deg16(1, cin)};
   const int64_t* vid_of = c.vid_of.as<int64_t>();
   unsigned long long* cnt = W.cnt.as<unsigned long long>();
   unsigned long long* hc = c.host_counters;  // pinned
@@ -2917,6 +2977,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       return probe_grid > 0 ? int(probe_grid) : grid_opt > 0 ? int(grid_opt) : std::min(resident_grid(k, 256), 5 * cu_count());
     };
     const int occ = int(c.opt("sp_dv_occ", 1));
+    const int32_t pf_agg = int32_t(c.opt("sp_dv_pf_lds", 1) != 0);
     // expansion waves per BFS chunk: option sp_dv_exp_sub (log2), default 256-entry sub-chunks
     int32_t lg_sub = int32_t(std::min<int64_t>(std::max<int64_t>(c.opt("sp_dv_exp_sub", -1), -1), 6));
     if (lg_sub < 0) lg_sub = std::max<int32_t>(0, d.lg_chb - 8);
@@ -2976,10 +3037,10 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       ++nl;
       if (occ >= 8)
         k_dv_expand<8><<<gsz((const void*)k_dv_expand<8>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it,
-                                                                               lg_sub);
+                                                                               lg_sub, pf_agg);
       else
         k_dv_expand<1><<<gsz((const void*)k_dv_expand<1>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it,
-                                                                               lg_sub);
+                                                                               lg_sub, pf_agg);
       evi[size_t(it)][2] = dv_event();
       seq[size_t(it)] = ++c.pub_seq;
       ++nl;

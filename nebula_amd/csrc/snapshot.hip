@@ -1887,9 +1887,11 @@ static void order_by_degree(Ctx& c, DevBuf& owned, int64_t n_owned) {
   int32_t min_idx = -1;
   NBG_HIP(hipMemcpyAsync(&min_idx, dmin.p, 4, hipMemcpyDeviceToHost, c.stream));
   NBG_HIP(hipStreamSynchronize(c.stream));
-  // one rank: in-degrees too (every in-edge of an owned vertex is in the local stage), for the
-  // degree classes of class_key
-  const bool classes = !c.sharded && c.opt("class_order", 1) != 0;
+  // in-degrees too, for the degree classes of class_key: one rank counts the dsts of its out-edge
+  // stage (every in-edge of an owned vertex is there); several ranks count the in-edge keys
+  // (dst, -type, rank, src) their parts hold -- the dst owner's, P5 -- so each rank's range is
+  // class-ordered too and its bottom-up hops stop at its own bu_both_tiles / bu_in_tiles
+  const bool classes = c.opt("class_order", 1) != 0;
   DevBuf ideg;
   if (classes) {
     ideg.alloc(size_t(n_owned) * 4);
@@ -1901,8 +1903,13 @@ static void order_by_degree(Ctx& c, DevBuf& owned, int64_t n_owned) {
     k_count_deg<<<grid_for(st.n), 256, 0, c.stream>>>(st.src.as<int64_t>(), st.n, keys.as<int64_t>(),
                                                      vals.as<int32_t>(), uint64_t(cap - 1), min_idx >= 0, min_idx,
                                                      deg.as<unsigned int>());
-    if (classes)
+    if (classes && !c.sharded)
       k_count_deg<<<grid_for(st.n), 256, 0, c.stream>>>(st.dst.as<int64_t>(), st.n, keys.as<int64_t>(),
+                                                       vals.as<int32_t>(), uint64_t(cap - 1), min_idx >= 0, min_idx,
+                                                       ideg.as<unsigned int>());
+    const Staging& si = kv.second.in_stage;
+    if (classes && c.sharded && si.n)
+      k_count_deg<<<grid_for(si.n), 256, 0, c.stream>>>(si.src.as<int64_t>(), si.n, keys.as<int64_t>(),
                                                        vals.as<int32_t>(), uint64_t(cap - 1), min_idx >= 0, min_idx,
                                                        ideg.as<unsigned int>());
   }

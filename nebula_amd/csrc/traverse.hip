@@ -1988,6 +1988,43 @@ __global__ void k_or_segments_to_map(const uint32_t* recv, int G, int64_t nw, ui
     for (; m; m &= m - 1) map_lo[w * 32 + (__ffs(m) - 1)] = 1;
   }
 }
+// several ranks, a top-down hop whose next frontier goes on as a bitmap (bottom-up hops): OR the
+// [G][nw] received mark words straight into the owned frontier bitmap, dropping vertices without
+// out-edges, with the compaction's counts -- sums[0] vertices set, [1] kept out-degree sum,
+// [2] kept vertices (k_compact's Kd[12, 15)) -- instead of writing the marks into the byte map
+// and compacting it again (k_or_segments_to_map + k_compact: 6 + 29 us at RMAT-26, r12h)
+__global__ __launch_bounds__(256) void k_or_segments_bits(const uint32_t* __restrict__ recv, int G, int64_t nw,
+                                                          const uint32_t* __restrict__ odeg, uint32_t* bits,
+                                                          unsigned long long* sums) {
+  __shared__ unsigned long long lds[kSlots * 16];
+  unsigned long long acc[3] = {0, 0, 0};
+  for (int64_t w = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; w < nw; w += int64_t(gridDim.x) * blockDim.x) {
+    uint32_t m = 0;
+    for (int p = 0; p < G; p++) m |= recv[size_t(p) * size_t(nw) + size_t(w)];
+    uint32_t keep = m;
+    if (m) {
+      // the word's 32 out-degrees as eight 16-byte loads issued together (odeg is padded to whole
+      // 128-row tiles), not one dependent load per set bit (24 us at RMAT-26 one rank, r12i)
+      uint32_t dg[32];
+      const uint4* p4 = reinterpret_cast<const uint4*>(odeg + w * 32);
+#pragma unroll
+      for (int a = 0; a < 8; a++) {
+        const uint4 v = p4[a];
+        dg[4 * a] = v.x, dg[4 * a + 1] = v.y, dg[4 * a + 2] = v.z, dg[4 * a + 3] = v.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 32; j++) {
+        const uint32_t d = (m >> j) & 1u ? dg[j] : 0u;
+        if ((m >> j) & 1u && d == 0) keep &= ~(1u << j);
+        acc[1] += d;
+      }
+    }
+    bits[w] = keep;
+    acc[0] += __popc(m);
+    acc[2] += __popc(keep);
+  }
+  block_add_sums(acc, 3, lds, sums);
+}
 // DISTINCT over rows with several ranks: rows are shuffled to rank hash(row) % G first
 __global__ void k_flag_dest(const uint32_t* dest, int64_t n, uint32_t p, uint8_t* flag) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
@@ -2369,7 +2406,8 @@ const uint32_t* global_bits_cnt(Ctx& c, const uint32_t* owned, const unsigned lo
 
 // top-down hops mark dsts of every rank in the global byte-map: ship each owner its slice as
 // a bitmap and OR the received slices back into the owned range of the map
-void exchange_marks(Ctx& c, uint8_t* map) {
+void exchange_marks(Ctx& c, uint8_t* map, uint32_t* owned_bits = nullptr, const uint32_t* odeg = nullptr,
+                    unsigned long long* sums = nullptr) {
   if (!c.sharded) return;
   CommTimer t(c);
   const size_t G = size_t(c.world);
@@ -2388,7 +2426,12 @@ void exchange_marks(Ctx& c, uint8_t* map) {
   }
   comm_alltoallv_bytes(c, sb, sbytes.data(), soff.data(), rbuf, rbytes.data(), roff.data());
   c.timing.comm_bytes += uint64_t(c.n_global - n_own) / 8;
-  k_or_segments_to_map<<<grid_cap(n_own / 32), 256, 0, c.stream>>>(rbuf, int(G), n_own / 32, map + lo);
+  if (owned_bits) {  // the next frontier as the owned bitmap + its counts (no byte map, no compaction)
+    const int grid = int(std::max<int64_t>(1, std::min<int64_t>((n_own / 32 + 255) / 256, 512)));
+    k_or_segments_bits<<<grid, 256, 0, c.stream>>>(rbuf, int(G), n_own / 32, odeg, owned_bits, sums);
+  } else {
+    k_or_segments_to_map<<<grid_cap(n_own / 32), 256, 0, c.stream>>>(rbuf, int(G), n_own / 32, map + lo);
+  }
   NBG_HIP(hipGetLastError());
 }
 
@@ -3520,14 +3563,19 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       a.off = c.ws_off.as<int64_t>();
       const int64_t e_bound = std::max<int64_t>(1, es.max_odeg >= 0 ? ns * es.max_odeg : csr.nnz);
       launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, std::min<int64_t>(e_bound, csr.nnz + 1), starts_tiles);
-      exchange_marks(c, map);  // several ranks: every owner receives the marks of its vertices
       cur ^= 1;
       F = c.ws_front[cur].as<int32_t>();
       const bool lazy = bu_ok && c.opt("compact_list", 0) == 0;
       // (K.d[0, 256) are zero: k_starts_small cleared the counters)
-      launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
-                     K.d, es.odeg.as<uint32_t>(), true, ks);
-      if (ks > 1) shards_dirty = true;
+      if (multi && lazy && es.odeg.p && c.opt("xchg_bits", 1) != 0) {
+        // several ranks: every owner ORs the marks it receives straight into its frontier bitmap
+        exchange_marks(c, map, bitsA, es.odeg.as<uint32_t>(), K.d + 12);
+      } else {
+        exchange_marks(c, map);  // several ranks: every owner receives the marks of its vertices
+        launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
+                       K.d, es.odeg.as<uint32_t>(), true, ks);
+        if (ks > 1) shards_dirty = true;
+      }
       // several ranks: the counts over ranks -- piggy: carried by the first speculated hop's
       // frontier exchange (its gate publishes them); else found, next out-degree sum and hop-1
       // entries summed into K.d[48, 51)
