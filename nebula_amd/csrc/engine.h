@@ -271,6 +271,27 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// Carves consecutive pieces (each rounded up to `align` bytes) out of one workspace block and
+// throws before a piece would pass the block's end: a hand-sized layout that drifted from its
+// allocation fails the call instead of overrunning a neighbour (round 5: the device-driven
+// batch's per-pair block was carved past its end at 8 in-process ranks)
+struct Carve {
+  char* q;
+  char* const end;
+  const char* what;
+  size_t align;
+  Carve(const DevBuf& b, const char* w, size_t a = 64)
+      : q(static_cast<char*>(b.p)), end(static_cast<char*>(b.p) + b.bytes), what(w), align(a) {}
+  template <typename T>
+  T* take(size_t bytes) {
+    char* r = q;
+    const size_t step = (bytes + align - 1) / align * align;
+    if (size_t(end - q) < step) throw Error(NBG_E_UNKNOWN, std::string(what) + ": workspace layout exceeds its block");
+    q += step;
+    return reinterpret_cast<T*>(r);
+  }
+};
+
 // RAII: route DevBuf allocations of the current thread through the context's pool
 struct PoolScope {
   std::shared_ptr<BufPool> prev;

@@ -110,6 +110,17 @@ struct SpState {  // per-pair arrays, B entries each
   int64_t lvw;
   uint32_t lvmask;
 };
+// the per-pair arrays of SpState carved from the W.state block (sized B * 48 + 64 bytes)
+static void sp_state_carve(const DevBuf& b, int64_t nb, SpState& st) {
+  Carve cv(b, "shortest path: per-pair state", 4);
+  st.deg = cv.take<unsigned long long>(size_t(nb) * 16);
+  st.state = cv.take<int32_t>(size_t(nb) * 4);
+  st.res = cv.take<int32_t>(size_t(nb) * 4);
+  st.lvl = cv.take<int32_t>(size_t(nb) * 8);
+  st.side = cv.take<int32_t>(size_t(nb) * 4);
+  st.pside = cv.take<int32_t>(size_t(nb) * 4);
+  st.met = cv.take<int32_t>(size_t(nb) * 4);
+}
 constexpr int kLv = 8;
 
 __device__ inline void lv_mark(const SpState& st, uint32_t side, uint32_t l, uint32_t v) {
@@ -2902,13 +2913,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     char* hb = static_cast<char*>(c.sp_host);
     SpState st{};
     st.B = int32_t(nb);
-    st.deg = W.state.as<unsigned long long>();
-    st.state = reinterpret_cast<int32_t*>(st.deg + 2 * nb);
-    st.res = st.state + nb;
-    st.lvl = st.res + nb;
-    st.side = st.lvl + 2 * nb;
-    st.pside = st.side + nb;
-    st.met = st.pside + nb;
+    sp_state_carve(W.state, nb, st);
     st.ilv = ilv;
     SpFilt f{};
     f.pf = W.dv_pf.as<uint32_t>();
@@ -2936,22 +2941,14 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     d.wchx = W.dv_wchx.as<int32_t>();
     d.cap_wch = W.dv_cap_wch;
     {
-      char* q = static_cast<char*>(W.dv_pair.p);
-      char* const q_end = q + W.dv_pair.bytes;
-      auto take = [&](size_t b) {
-        char* r = q;
-        q += (b + 63) & ~size_t(63);
-        if (q > q_end) throw Error(NBG_E_UNKNOWN, "shortest path: per-pair workspace layout exceeds its block");
-        return r;
-      };
-      d.gs = reinterpret_cast<int32_t*>(take(size_t(nb) * 8));
-      d.cur = reinterpret_cast<int32_t*>(take(size_t(nb) * 4));
-      d.best = reinterpret_cast<long long*>(take(size_t(nb) * 8));
-      d.wcb = reinterpret_cast<int64_t*>(take(size_t(nb) * 8));
-      d.doff = reinterpret_cast<int64_t*>(take(size_t(nb + 8) * 8));
-      d.pull = reinterpret_cast<unsigned long long*>(take(size_t(nb) * kMaxQ * 8));
-      d.push = d.pull + size_t(nb) * kMaxQ;  // adjacent: k_dv_begin clears both in one pass
-      (void)take(size_t(nb) * kMaxQ * 8);
+      Carve cv(W.dv_pair, "shortest path: per-pair workspace");
+      d.gs = cv.take<int32_t>(size_t(nb) * 8);
+      d.cur = cv.take<int32_t>(size_t(nb) * 4);
+      d.best = cv.take<long long>(size_t(nb) * 8);
+      d.wcb = cv.take<int64_t>(size_t(nb) * 8);
+      d.doff = cv.take<int64_t>(size_t(nb + 8) * 8);
+      d.pull = cv.take<unsigned long long>(size_t(nb) * kMaxQ * 8);
+      d.push = cv.take<unsigned long long>(size_t(nb) * kMaxQ * 8);  // adjacent: k_dv_begin clears both in one pass
     }
     d.path = W.dv_path.as<int64_t>();
     d.lg_chb = int32_t(std::min<int64_t>(std::max<int64_t>(c.opt("sp_dv_lg_ch", 10), 9), 14));
@@ -3194,13 +3191,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     }
     SpState st{};
     st.B = int32_t(nb);
-    st.deg = W.state.as<unsigned long long>();
-    st.state = reinterpret_cast<int32_t*>(st.deg + 2 * nb);
-    st.res = st.state + nb;
-    st.lvl = st.res + nb;
-    st.side = st.lvl + 2 * nb;
-    st.pside = st.side + nb;
-    st.met = st.pside + nb;
+    sp_state_carve(W.state, nb, st);
     st.ilv = ilv;
     if (c.opt("sp_lvbits", 1) != 0) {  // level filter: 2 * kLv maps, cleared per batch
       // bits per level: the power of two >= n, capped (option sp_lvbits_log2, default 23)
@@ -3620,13 +3611,12 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         const size_t wbytes = size_t(nb) * 4 + 64 + size_t(nb) * 8 + 64 + 2 * (size_t(nb + 1) * 8 + 64) +
                               size_t(max_tiles) * 4 + 64;
         wk.alloc(wbytes);
-        char* q = static_cast<char*>(wk.p);
-        auto take = [&](size_t b) { char* r = q; q += (b + 63) & ~size_t(63); return r; };
-        int32_t* dcur = reinterpret_cast<int32_t*>(take(size_t(nb) * 4));
-        long long* dbest = reinterpret_cast<long long*>(take(size_t(nb) * 8));
-        int64_t* wdeg = reinterpret_cast<int64_t*>(take(size_t(nb + 1) * 8));
-        int64_t* woff = reinterpret_cast<int64_t*>(take(size_t(nb + 1) * 8));
-        int32_t* wtr = reinterpret_cast<int32_t*>(take(size_t(max_tiles) * 4));
+        Carve cv(wk, "shortest path: walk workspace");
+        int32_t* dcur = cv.take<int32_t>(size_t(nb) * 4);
+        long long* dbest = cv.take<long long>(size_t(nb) * 8);
+        int64_t* wdeg = cv.take<int64_t>(size_t(nb + 1) * 8);
+        int64_t* woff = cv.take<int64_t>(size_t(nb + 1) * 8);
+        int32_t* wtr = cv.take<int32_t>(size_t(max_tiles) * 4);
         NBG_HIP(hipMemcpyAsync(dcur, dgs, size_t(nb) * 4, hipMemcpyDeviceToDevice, c.stream));
         size_t tb = 0;
         NBG_HIP(rocprim::exclusive_scan(nullptr, tb, wdeg, woff, int64_t(0), size_t(nb + 1), rocprim::plus<int64_t>(),
