@@ -88,7 +88,8 @@ def c3_group(scale, world, reps):
             ranks.append({"rank": r, "local_vertices": inf["local_vertices"],
                           "local_out_edges": inf["local_out_edges"], "rows": int(res[r].n_rows),
                           "device_ms": round(x["total_ms"], 4), "comm_ms": round(x["comm_ms"], 4),
-                          "comm_bytes": int(x["comm_bytes"]), "host_waits": x["host_waits"],
+                          "comm_bytes": int(x["comm_bytes"]), "comm_calls": x.get("comm_calls"),
+                          "host_waits": x["host_waits"],
                           "spec_hops": x["spec_hops"],
                           "hops": [{"mode": h["mode"], "final": h["final"], "ms": round(h["ms"], 4),
                                     "kernel_ms": round(h["kernel_ms"], 4), "bytes": h["bytes"],

@@ -4,33 +4,61 @@ work of C3 (LocalComm rank groups on one GPU) and C4 (rank 0's pair subset alone
 and the per-GPU time projected for W GPUs from them.
 
 Projection model (stated in the output):
-  C3 per GPU = the one-GPU query's kernel time x (rank's kernel bytes / one-GPU kernel bytes)
-               + host (one-GPU wall - kernel time)
-               + exchanges: per collective a latency L_coll, plus the rank's exchange bytes over
-                 its W - 1 xGMI links at B_link each (the peers' slices arrive in parallel)
+  C3 per GPU = K1 x (rank's kernel bytes / one-rank kernel bytes)
+               + host (one-rank wall - one-rank busy span)
+               + exchanges: N_coll collectives (counted by the engine, nbg_timing.comm_calls) x
+                 (L1 + dL), plus the rank's exchange bytes over its W - 1 xGMI links at B_link
+  where the one-rank numbers come from the SHARDED algorithm run through a real one-rank RCCL
+  communicator (bench.py --comm-single, tools/kt_timeline.sh ... --comm-single): K1 = its kernels
+  without the RCCL ones, L1 = one RCCL call on the engine stream (its kernel + the idle gap before
+  the next launch), measured; dL = the extra latency of a W-rank exchange over xGMI, ASSUMED
+  (a one-GPU lease cannot measure it).
   C4 per GPU = rank 0's measured batch time (no collective in the traversal)
 
-    python tools/sharded_summary.py gpurun_out/<tag>/sharded.jsonl <c3 one-GPU bench json> <out.md>
+    python tools/sharded_summary.py gpurun_out/<tag>/sharded.jsonl <comm-single bench json> \
+        <comm-single query timeline txt> <out.md> [round label]
 """
 import json
 import sys
 
-L_COLL_US = 20.0      # assumed RCCL latency per collective on 8 MI355X (not measurable on one GPU)
+DL_COLL_US = 5.0      # ASSUMED extra latency of a W-rank xGMI exchange over the one-rank call
 B_LINK_GBS = 153.0    # per xGMI link and direction (the task statement's figure)
-# the one-GPU C3 query's kernels (tools/query_timeline.py of the timed loop, profiles/r10a_c3_query_timeline.txt)
-ONE_GPU_KERNEL_US = 396.5
-ONE_GPU_KERNEL_MB = 0.0   # filled from the W = 1 hop records (bytes of the byte model)
+
+
+def timeline_stats(path):
+    """(busy us, RCCL kernel us, RCCL calls, us of RCCL kernel + the gap after it, span us)"""
+    rows = []
+    for line in open(path):
+        if line.startswith("#"):
+            continue
+        f = line.split()
+        if len(f) < 6:
+            continue
+        rows.append((float(f[0]), float(f[2]), float(f[4]), f[5]))
+    busy = sum(r[2] for r in rows)
+    rccl = [i for i, r in enumerate(rows) if "nccl" in r[3].lower()]
+    rk = sum(rows[i][2] for i in rccl)
+    per = sum(rows[i][2] + (rows[i + 1][1] if i + 1 < len(rows) else 0.0) for i in rccl)
+    span = rows[-1][0] + rows[-1][2] if rows else 0.0
+    return busy, rk, len(rccl), per, span
 
 
 def main():
     lines = [json.loads(l) for l in open(sys.argv[1]) if l.strip()]
-    bench = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
-    out = sys.argv[3]
+    bench = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
+    busy, rk_us, n_rccl, rccl_us, span = timeline_stats(sys.argv[3])
+    out = sys.argv[4]
+    label = sys.argv[5] if len(sys.argv) > 5 else "round 6"
     one_hops = bench["roofline"]["hops"]
     one_bytes = sum(h["kernel_bytes"] for h in one_hops if h.get("kernel_bytes"))
     one_wall = bench["ms_per_step"] * 1e3
-    host_us = max(0.0, one_wall - ONE_GPU_KERNEL_US)
-    md = ["# Multi-GPU cost evidence from one MI355X (round 5)", "",
+    k1_us = busy - rk_us                       # the sharded algorithm's kernels on one rank
+    l1_us = rccl_us / n_rccl if n_rccl else 0.0  # one RCCL call on the engine stream
+    # host: the synchronous call's entry and its one counter wait, beyond the kernels -- one
+    # rank's timed-loop wall minus its kernel span when that is positive (the span comes from a
+    # profiled run), else the ~15 us the one-GPU timeline shows (profiles/r10a_c3_query_timeline.txt)
+    host_us = one_wall - span if one_wall > span else 15.0
+    md = [f"# Multi-GPU cost evidence from one MI355X ({label})", "",
           "Measured on the one-GPU lease; the 8-GPU scaling curve itself is the driver's (SCALE_rNN).", "",
           "## C4: FIND SHORTEST PATH, 1024 pairs, RMAT-26 -- rank r's pair subset (pairs r, r + W, ...) alone", "",
           "Pairs are sharded i % W over replicated CSRs and the traversal exchanges nothing, so these are the",
@@ -66,21 +94,26 @@ def main():
             md.append(f"| {w} | {r['rank']} | {', '.join(f'{x:.1f}' for x in hb)} | {r['comm_bytes'] / 1e6:.1f} | "
                       f"{r['host_waits']} | {r['spec_hops']} |")
         comm_mb = max(r["comm_bytes"] for r in d["ranks"]) / 1e6
-        ncoll = 5  # hop-1 marks all-to-all, two frontier allgathers (counters piggybacked), two sums
-        k_us = ONE_GPU_KERNEL_US * mx_bytes / one_bytes if one_bytes else float("nan")
-        c_us = ncoll * L_COLL_US + comm_mb / (max(w - 1, 1) * B_LINK_GBS) * 1e3
-        proj.append((w, k_us, c_us, host_us, k_us + c_us + host_us))
+        ncoll = max((r.get("comm_calls") or 0) for r in d["ranks"]) or n_rccl
+        k_us = k1_us * mx_bytes / one_bytes if one_bytes else float("nan")
+        c_us = ncoll * (l1_us + DL_COLL_US) + comm_mb / (max(w - 1, 1) * B_LINK_GBS) * 1e3
+        proj.append((w, ncoll, k_us, c_us, host_us, k_us + c_us + host_us))
     md += ["", "## Projected per-GPU C3 query time at W GPUs", "",
-           f"kernels = {ONE_GPU_KERNEL_US:.0f} us (the one-GPU query's kernels) x the slowest rank's share of the bytes;",
-           f"exchanges = 5 collectives x {L_COLL_US:.0f} us (assumed RCCL latency) + its exchange bytes over W - 1 links",
-           f"at {B_LINK_GBS:.0f} GB/s; host = {host_us:.0f} us (one-GPU wall {one_wall:.0f} us - kernels).", "",
-           "| W | kernels us | exchanges us | host us | per query us | projected GTEPS (1.545 G edges / query) |",
-           "|---|---|---|---|---|---|"]
-    for w, k, c, h, t in proj:
-        md.append(f"| {w} | {k:.0f} | {c:.0f} | {h:.0f} | {t:.0f} | {1.545e9 / (t * 1e-6) / 1e9:,.0f} |")
-    md += ["", f"One GPU measured: {one_wall:.0f} us/query, {bench['value']:.0f} GTEPS.  The exchange latency, not",
-           "bytes, dominates past W = 4: a W-GPU query is bounded by its ~5 collectives' latency plus ~400 / W us",
-           "of kernels."]
+           "The one-rank numbers are the sharded algorithm run through a real one-rank RCCL communicator",
+           f"(`bench.py --comm-single`: {one_wall:.0f} us/query wall, digest {bench['parity'].get('status')};",
+           f"kernel timeline: {busy:.0f} us busy, of it {rk_us:.0f} us in {n_rccl} RCCL kernels).", "",
+           f"* kernels = {k1_us:.0f} us (the one-rank sharded query's kernels without RCCL's) x the slowest rank's share",
+           "  of the bytes;",
+           f"* exchanges = the rank's collectives (engine count) x ({l1_us:.1f} us measured one-rank RCCL call on the",
+           f"  engine stream: kernel + the gap before the next launch, + {DL_COLL_US:.0f} us ASSUMED for a W-rank xGMI",
+           f"  exchange) + its exchange bytes over W - 1 links at {B_LINK_GBS:.0f} GB/s;",
+           f"* host = {host_us:.0f} us (the call's entry and its counter wait beyond the kernels).", "",
+           "| W | collectives / query | kernels us | exchanges us | host us | per query us | projected GTEPS (1.545 G edges / query) |",
+           "|---|---|---|---|---|---|---|"]
+    for w, n, k, c, h, t in proj:
+        md.append(f"| {w} | {n} | {k:.0f} | {c:.0f} | {h:.0f} | {t:.0f} | {1.545e9 / (t * 1e-6) / 1e9:,.0f} |")
+    md += ["", f"One GPU, unsharded: see the round's bench line.  Past W = 4 the exchange latency, not the bytes,",
+           "bounds a query: its collectives' latency plus the kernels' 1 / W share."]
     open(out, "w").write("\n".join(md) + "\n")
     print("\n".join(md))
 
