@@ -2085,7 +2085,7 @@ __global__ __launch_bounds__(256, OCC) void k_dv_expand(SpDev d, SpState st, SpF
     dput(d.arena, d.cap_arena, gcnt(d.cnt, D_ARENA), d.cnt, hit, v);
     dput(d.meet, d.cap_meet, gcnt(d.cnt, D_MEET), d.cnt, hit, mt);
   }
-  if (skip) return;
+  if (skip || (f.diag & 64)) return;  // (diag bit 6: no final flush / sums, timing only)
   dv_flush_block(sg0, d.cnt, q + Q_LIVE0, out0, d.cap_live, d.arena, d.cap_arena);
   dv_flush_block(sg1, d.cnt, q + Q_LIVE1, out1, d.cap_live, d.arena, d.cap_arena);
   blk_add(q + Q_CLAIMS, claims);

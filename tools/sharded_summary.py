@@ -25,8 +25,14 @@ DL_COLL_US = 5.0      # ASSUMED extra latency of a W-rank xGMI exchange over the
 B_LINK_GBS = 153.0    # per xGMI link and direction (the task statement's figure)
 
 
+# kernels whose work does not shrink with W: the start frontier, hop 1 from 64 seeds (latency-
+# bound at any size), the byte map -> bitmap pass over the whole gidx space, the counter publish
+FIXED = ("k_starts_small", "k_expand<0, 0>", "k_map_to_bits", "k_publish")
+
+
 def timeline_stats(path):
-    """(busy us, RCCL kernel us, RCCL calls, us of RCCL kernel + the gap after it, span us)"""
+    """(busy us, RCCL kernel us, RCCL calls, us of RCCL kernel + the gap after it, span us,
+    us of the FIXED kernels)"""
     rows = []
     for line in open(path):
         if line.startswith("#"):
@@ -34,19 +40,20 @@ def timeline_stats(path):
         f = line.split()
         if len(f) < 6:
             continue
-        rows.append((float(f[0]), float(f[2]), float(f[4]), f[5]))
+        rows.append((float(f[0]), float(f[2]), float(f[4]), " ".join(f[5:])))
     busy = sum(r[2] for r in rows)
     rccl = [i for i, r in enumerate(rows) if "nccl" in r[3].lower()]
     rk = sum(rows[i][2] for i in rccl)
     per = sum(rows[i][2] + (rows[i + 1][1] if i + 1 < len(rows) else 0.0) for i in rccl)
     span = rows[-1][0] + rows[-1][2] if rows else 0.0
-    return busy, rk, len(rccl), per, span
+    fixed = sum(r[2] for r in rows if any(k in r[3] for k in FIXED))
+    return busy, rk, len(rccl), per, span, fixed
 
 
 def main():
     lines = [json.loads(l) for l in open(sys.argv[1]) if l.strip()]
     bench = json.loads([l for l in open(sys.argv[2]) if l.startswith("{")][-1])
-    busy, rk_us, n_rccl, rccl_us, span = timeline_stats(sys.argv[3])
+    busy, rk_us, n_rccl, rccl_us, span, fixed_us = timeline_stats(sys.argv[3])
     out = sys.argv[4]
     label = sys.argv[5] if len(sys.argv) > 5 else "round 6"
     one_hops = bench["roofline"]["hops"]
@@ -54,10 +61,9 @@ def main():
     one_wall = bench["ms_per_step"] * 1e3
     k1_us = busy - rk_us                       # the sharded algorithm's kernels on one rank
     l1_us = rccl_us / n_rccl if n_rccl else 0.0  # one RCCL call on the engine stream
-    # host: the synchronous call's entry and its one counter wait, beyond the kernels -- one
-    # rank's timed-loop wall minus its kernel span when that is positive (the span comes from a
-    # profiled run), else the ~15 us the one-GPU timeline shows (profiles/r10a_c3_query_timeline.txt)
-    host_us = one_wall - span if one_wall > span else 15.0
+    # host: the synchronous call's entry and its counter wait beyond the query's kernel span (the
+    # span's own idle gaps -- the ~4.7 us after each RCCL kernel -- are in the collective term)
+    host_us = max(0.0, one_wall - span)
     md = [f"# Multi-GPU cost evidence from one MI355X ({label})", "",
           "Measured on the one-GPU lease; the 8-GPU scaling curve itself is the driver's (SCALE_rNN).", "",
           "## C4: FIND SHORTEST PATH, 1024 pairs, RMAT-26 -- rank r's pair subset (pairs r, r + W, ...) alone", "",
@@ -95,15 +101,16 @@ def main():
                       f"{r['host_waits']} | {r['spec_hops']} |")
         comm_mb = max(r["comm_bytes"] for r in d["ranks"]) / 1e6
         ncoll = max((r.get("comm_calls") or 0) for r in d["ranks"]) or n_rccl
-        k_us = k1_us * mx_bytes / one_bytes if one_bytes else float("nan")
+        k_us = fixed_us + (k1_us - fixed_us) * mx_bytes / one_bytes if one_bytes else float("nan")
         c_us = ncoll * (l1_us + DL_COLL_US) + comm_mb / (max(w - 1, 1) * B_LINK_GBS) * 1e3
         proj.append((w, ncoll, k_us, c_us, host_us, k_us + c_us + host_us))
     md += ["", "## Projected per-GPU C3 query time at W GPUs", "",
            "The one-rank numbers are the sharded algorithm run through a real one-rank RCCL communicator",
            f"(`bench.py --comm-single`: {one_wall:.0f} us/query wall, digest {bench['parity'].get('status')};",
            f"kernel timeline: {busy:.0f} us busy, of it {rk_us:.0f} us in {n_rccl} RCCL kernels).", "",
-           f"* kernels = {k1_us:.0f} us (the one-rank sharded query's kernels without RCCL's) x the slowest rank's share",
-           "  of the bytes;",
+           f"* kernels = {fixed_us:.0f} us that do not shrink with W ({', '.join(FIXED)}) + the other",
+           f"  {k1_us - fixed_us:.0f} us of the one-rank sharded query's kernels (RCCL's excluded) x the slowest",
+           "  rank's share of the bytes;",
            f"* exchanges = the rank's collectives (engine count) x ({l1_us:.1f} us measured one-rank RCCL call on the",
            f"  engine stream: kernel + the gap before the next launch, + {DL_COLL_US:.0f} us ASSUMED for a W-rank xGMI",
            f"  exchange) + its exchange bytes over W - 1 links at {B_LINK_GBS:.0f} GB/s;",
