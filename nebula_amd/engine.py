@@ -68,6 +68,12 @@ def _view(ptr, n, ctype, dtype, holder):
     return np.frombuffer(ct, dtype=dtype)
 
 
+_EMPTY_I64 = np.zeros(0, dtype=np.int64)
+_ZERO1_I64 = np.zeros(1, dtype=np.int64)
+_EMPTY_I64.flags.writeable = False
+_ZERO1_I64.flags.writeable = False
+
+
 class RowSet:
     """Typed columnar result (copied to host unless ``on_device``).  With ``holder`` (nbg_go) the
     INT / VID / DOUBLE columns are views of the engine's pinned result blocks, not copies; the
@@ -80,6 +86,17 @@ class RowSet:
         self.on_device = bool(rows.on_device)
         self.columns = []
         self.device_ptrs = []
+        if self.on_device and not rows.row_vertex and not rows.n_vertices and not rows.n_failed \
+                and not rows.n_vertex_cols:
+            # a GO result left in HBM: column pointers only (the per-call cost of the bench loop)
+            self.device_ptrs = [rows.cols[c] for c in range(len(self.types))]
+            self.columns = [None] * len(self.types)
+            self.row_vertex = _EMPTY_I64
+            self.vertex_ids = _EMPTY_I64
+            self.vertex_row_offsets = _ZERO1_I64
+            self.failed = []
+            self.vertex_columns = []
+            return
         for c, t in enumerate(self.types):
             ptr = rows.cols[c]
             if self.on_device:
@@ -155,6 +172,7 @@ class GraphSpace:
         self.num_parts, self.rank, self.world_size = num_parts, rank, world_size
         self._options: set[str] = set()
         self._plan_views: dict = {}  # (WHERE bytes, YIELD bytes) -> their C views (go())
+        self._last_spec = None  # (argument key, GoSpec, start array) of the last go() call
         self.h = self.L.nbg_ctx_create(device, num_parts, rank, world_size)
         if not self.h:
             raise RuntimeError("nbg_ctx_create failed: no MI355X visible or bad arguments "
@@ -360,6 +378,16 @@ class GraphSpace:
         starts = np.ascontiguousarray(starts, dtype=np.int64)
         w = X.encode(where)
         ys = tuple(X.encode(y) for y in yields)
+        # a call repeating the previous one's arguments (the same start array object, plan and
+        # flags) re-uses its prepared spec: building it cost ~15 us of Python per call (numpy's
+        # ctypes pointer views), time the device sat idle between two queries.  The spec points at
+        # the array's data, so values changed in place are read as they are at the call.
+        ckey = (id(starts), len(starts), w, ys, steps, edge_type, bool(distinct), bool(keep_on_device))
+        if not inputs and self._last_spec is not None and self._last_spec[0] == ckey:
+            spec = self._last_spec[1]
+            rows = _lib.Rows()
+            self._check(self.L.nbg_go(self.h, C.byref(spec), C.byref(rows)))
+            return self._go_rows(rows, keep_on_device)
         # the C views of the encoded WHERE / YIELD bytes, built once per distinct plan (a GO
         # repeated with the same plan re-uses them; they live as long as the space)
         key = (w, ys)
@@ -381,8 +409,13 @@ class GraphSpace:
             spec.n_inputs = len(inputs)
             spec.input_names, spec.input_types = names, types
             spec.input_cols, spec.input_str_offsets = cols, offs
+        if not inputs:
+            self._last_spec = (ckey, spec, starts)  # (the array is held while the spec points at it)
         rows = _lib.Rows()
         self._check(self.L.nbg_go(self.h, C.byref(spec), C.byref(rows)))
+        return self._go_rows(rows, keep_on_device)
+
+    def _go_rows(self, rows, keep_on_device: bool) -> RowSet:
         if keep_on_device:
             try:
                 return RowSet(rows)
