@@ -326,8 +326,6 @@ def bench_paths(args, sp, info, build_s, rank, world, golden, dist=None):
         if rec["kind"] == "probe" and (h["c"][6] or h["c"][7]):
             # option sp_dv_diag bit 3: the meet probe's filter statistics
             rec.update(pair_filter_passes=h["c"][6], distance_bytes_read=h["c"][2], bytes_at_depth=h["c"][7])
-        elif h["c"][6] or h["c"][7]:  # option sp_sweep_stats: distinct scanned vertices, their degrees
-            rec.update(distinct_x=h["c"][6], distinct_entries=h["c"][7])
     # parity: the last result (host copy) against the committed digest
     hops, paths, srcs = r.hops, r.paths, r.src
     if dist is not None:

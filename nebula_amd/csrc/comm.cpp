@@ -323,7 +323,7 @@ void comm_init(Ctx& c, const uint8_t id_bytes[128]) {
   memcpy(&id, id_bytes, 128);
   NBG_HIP(hipSetDevice(c.device));
   auto* r = new RcclComm();
-  r->self_p2p = single || c.opt("comm_self_p2p", 0) != 0;
+  r->self_p2p = single;
   r->msg = size_t(std::max<int64_t>(1, c.opt("comm_chunk_mb", 1024))) << 20;
   pool_trim_all();  // RCCL's buffers come from the driver, which never trims the block caches
   ncclResult_t rc = ncclCommInitRank(&r->comm, c.world, id, c.rank);

@@ -2783,7 +2783,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   uint8_t* d0 = c.sp_dist[0].as<uint8_t>();
   uint8_t* d1 = ilv ? d0 + 1 : d0 + c.sp_dist_bytes;
   auto deg16 = [&](int k, const Csr* g) -> const uint16_t* {
-    if (c.opt("sp_deg16", 1) == 0 || g->n_rows <= 0) return nullptr;
+    if (g->n_rows <= 0) return nullptr;
     if (W.deg16_rp[k] != g->row_ptr.p || W.deg16_rows[k] != g->n_rows || W.deg16_commits[k] != c.commits) {
       PoolScope none(nullptr);  // kept across calls, outside the query pool
       W.deg16[k].alloc(size_t(g->n_rows) * 2 + 64);
@@ -2951,8 +2951,8 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       d.push = cv.take<unsigned long long>(size_t(nb) * kMaxQ * 8);  // adjacent: k_dv_begin clears both in one pass
     }
     d.path = W.dv_path.as<int64_t>();
-    d.lg_chb = int32_t(std::min<int64_t>(std::max<int64_t>(c.opt("sp_dv_lg_ch", 10), 9), 14));
-    d.lg_chs = int32_t(std::min<int64_t>(std::max<int64_t>(c.opt("sp_dv_lg_chs", 10), 9), 14));
+    d.lg_chb = 10;  // 1024-entry chunks
+    d.lg_chs = 10;
     int64_t* hp = reinterpret_cast<int64_t*>(hb + h_pairs);
     memcpy(hp, src + b0, size_t(nb) * 8);
     memcpy(hp + nb, dst + b0, size_t(nb) * 8);
@@ -2963,23 +2963,18 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     auto pub = [&](int it) { return reinterpret_cast<unsigned long long*>(hb + h_pub) + size_t(it) * kPubW; };
     unsigned long long* fin = reinterpret_cast<unsigned long long*>(hb + h_fin);
 
-    const int64_t sel_opt = c.opt("sp_dv_sel_grid", 0);  // select grids (default: resident)
-    auto gsel = [&](const void* k) { return sel_opt > 0 ? int(sel_opt) : resident_grid(k, kBlk); };
+    auto gsel = [&](const void* k) { return resident_grid(k, kBlk); };
     // scan grids: option sp_dv_grid, else each kernel's resident grid
     const int64_t grid_opt = c.opt("sp_dv_grid", 0);
     auto gsz = [&](const void* k) { return grid_opt > 0 ? int(grid_opt) : resident_grid(k, 256); };
     // the meet probe at 5 blocks per CU (its resident 8 ran the third iteration at 0.29 ms, 5: 0.22)
-    const int64_t probe_grid = c.opt("sp_dv_probe_grid", 0);
     auto gpr = [&](const void* k) {
-      return probe_grid > 0 ? int(probe_grid) : grid_opt > 0 ? int(grid_opt) : std::min(resident_grid(k, 256), 5 * cu_count());
+      return grid_opt > 0 ? int(grid_opt) : std::min(resident_grid(k, 256), 5 * cu_count());
     };
     const int occ = int(c.opt("sp_dv_occ", 1));
-    const int32_t pf_agg = int32_t(c.opt("sp_dv_pf_lds", 1) != 0);
-    // expansion waves per BFS chunk: option sp_dv_exp_sub (log2), default 256-entry sub-chunks
-    int32_t lg_sub = int32_t(std::min<int64_t>(std::max<int64_t>(c.opt("sp_dv_exp_sub", -1), -1), 6));
-    if (lg_sub < 0) lg_sub = std::max<int32_t>(0, d.lg_chb - 8);
-    lg_sub = std::min<int32_t>(lg_sub, d.lg_chb);
-    const int64_t pu = c.opt("sp_dv_probe_u", 4), su = c.opt("sp_dv_sweep_u", 4);  // entries per lane and step
+    const int32_t pf_agg = 1;
+    // expansion waves per BFS chunk: 256-entry sub-chunks
+    const int32_t lg_sub = std::max<int32_t>(0, d.lg_chb - 8);
     const int max_it = std::min<int>(max_steps, kMaxQ - 2);
     const int64_t htm = int64_t(c.ht_cap - 1);
     const int64_t* htk = c.ht_keys.as<int64_t>();
@@ -3023,12 +3018,8 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       evi[size_t(it)][0] = dv_event();
       if (probe) {
         ++nl;
-        if (pu >= 16)
-          k_dv_probe<16><<<gpr((const void*)k_dv_probe<16>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
-        else if (pu >= 8)
-          k_dv_probe<8><<<gpr((const void*)k_dv_probe<8>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
-        else
-          k_dv_probe<4><<<gpr((const void*)k_dv_probe<4>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
+        // 4 entries per lane and step (8 / 16 measured slower: 0.50 -> 0.70 ms, round 3)
+        k_dv_probe<4><<<gpr((const void*)k_dv_probe<4>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, it);
       }
       evi[size_t(it)][1] = dv_event();
       ++nl;
@@ -3056,21 +3047,16 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     const int64_t maxL = int64_t(pub(it)[D_MAXL]), maxF = int64_t(pub(it)[D_MAXF]);
     const int iters = it;
     ++nl;
-    k_dv_post<<<int(std::max<int64_t>(1, c.opt("sp_dv_post_grid", 512))), kBlk, 0, c.stream>>>(
+    k_dv_post<<<int(std::max<int64_t>(1, 512)), kBlk, 0, c.stream>>>(
         d, st, gout, gin, lo, htk, htv, uint64_t(htm), c.ht_has_min, c.ht_min_gidx);
     const int nsw = int(std::min<int64_t>(std::max<int64_t>(maxF - 1, 0), kMaxQ - 2));
-    const unsigned long long bias16 = (unsigned long long)std::max<int64_t>(0, c.opt("sp_push_bias", 16));
+    const unsigned long long bias16 = (unsigned long long)std::max<int64_t>(0, 16);
     for (int j = 1; j <= nsw; j++) {
       ++nl;
       k_dv_sweep_select<<<gsel((const void*)k_dv_sweep_select), kBlk, 0, c.stream>>>(d, st, gout, gin, j, bias16);
       evs[size_t(j)][0] = dv_event();
       ++nl;
-      if (su >= 16)
-        k_dv_sweep<16><<<gsz((const void*)k_dv_sweep<16>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
-      else if (su >= 8)
-        k_dv_sweep<8><<<gsz((const void*)k_dv_sweep<8>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
-      else
-        k_dv_sweep<4><<<gsz((const void*)k_dv_sweep<4>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
+      k_dv_sweep<4><<<gsz((const void*)k_dv_sweep<4>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
       evs[size_t(j)][1] = dv_event();
     }
     const int nwalk = int(std::min<int64_t>(maxL >= 2 ? maxL - 1 : 0, kMaxQ - 2));
@@ -3195,7 +3181,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     st.ilv = ilv;
     if (c.opt("sp_lvbits", 1) != 0) {  // level filter: 2 * kLv maps, cleared per batch
       // bits per level: the power of two >= n, capped (option sp_lvbits_log2, default 23)
-      const int cap = int(std::min<int64_t>(std::max<int64_t>(c.opt("sp_lvbits_log2", 23), 5), 31));
+      const int cap = int(std::min<int64_t>(std::max<int64_t>(23, 5), 31));
       int lg = 5;
       while (lg < cap && (int64_t(1) << lg) < n) lg++;
       const int64_t lvw = (int64_t(1) << lg) / 32;
@@ -3283,10 +3269,10 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       a.lo = lo;
       a.sweep = sweep_mode;
       const int64_t tiles = (E + kTileE - 1) / kTileE;
-      const int grid = int(std::max<int64_t>(1, std::min<int64_t>(tiles, c.opt("sp_grid", 256 * 8))));
+      const int grid = int(std::max<int64_t>(1, std::min<int64_t>(tiles, 256 * 8)));
       hipEventRecord(c.ev[2], c.stream);
       a.tile_row = nullptr;
-      if (c.opt("expand_tile_rows", 1) && nX < (int64_t(1) << 31)) {
+      if (nX < (int64_t(1) << 31)) {
         if (W.tile_rows.bytes < size_t(tiles + 2) * 4) {
           PoolScope none(nullptr);
           W.tile_rows.alloc(size_t(tiles + tiles / 4 + 64) * 4);
@@ -3308,7 +3294,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     };
     // per-launch record in the hop stats: mode 2 = BFS expansion, 3 = meet probe, 4 = sweep;
     // c[] = {X tuples, adjacency entries, claims, meets (total so far), iteration, active pairs}
-    unsigned long long diag[2] = {0, 0};  // option sp_sweep_stats: distinct X vertices, their degree sum
+    unsigned long long diag[2] = {0, 0};  // (c[6], c[7] of the sweep records: unused since round 6)
     auto sp_hop = [&](int32_t mode, double ms, int64_t nX, int64_t E, int64_t claims, int64_t it, int64_t act) {
       const unsigned long long c8[8] = {(unsigned long long)nX, (unsigned long long)E, (unsigned long long)claims,
                                         hc[C_MEET], (unsigned long long)it, (unsigned long long)act, diag[0], diag[1]};
@@ -3398,14 +3384,10 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
                                         size_t(nX + 1), rocprim::plus<int64_t>(), c.stream));
         hipEventRecord(c.ev[4], c.stream);
         const int pgrid =
-            int(std::max<int64_t>(1, std::min<int64_t>((max_chunks + 3) / 4, c.opt("sp_probe_grid", 4096))));
+            int(std::max<int64_t>(1, std::min<int64_t>((max_chunks + 3) / 4, 4096)));
         chx.alloc(size_t(max_chunks) * 4);
         k_chunk_x<<<grid_n(nX), 256, 0, c.stream>>>(choff.as<int64_t>(), nX, chx.as<int32_t>(), slot.as<uint64_t>());
-        if (c.opt("sp_probe_occ", 7) >= 8)
-          k_sp_probe<8><<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), chx.as<int32_t>(),
-                                                     gout, gin, d0, d1, n, lo, st, slot.as<uint64_t>(), cnt);
-        else
-          k_sp_probe<1><<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), chx.as<int32_t>(),
+        k_sp_probe<1><<<pgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), nX, choff.as<int64_t>(), chx.as<int32_t>(),
                                                      gout, gin, d0, d1, n, lo, st, slot.as<uint64_t>(), cnt);
         k_sp_gather_meets<<<grid_sel(max_chunks), kBlk, 0, c.stream>>>(slot.as<uint64_t>(), max_chunks, st, bf, cnt,
                                                                        choff.as<int64_t>() + nX);
@@ -3507,7 +3489,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
           k_sweep_push_cost<<<grid_n(n_arena), 256, 0, c.stream>>>(W.arena.as<uint64_t>(), n_arena, j, st, gout, pullc,
                                                                     pushc);
         k_sweep_choose<<<grid_n(nb, 1 << 20), 256, 0, c.stream>>>(
-            pullc, pushc, int32_t(nb), push_pair, (unsigned long long)std::max<int64_t>(0, c.opt("sp_push_bias", 16)));
+            pullc, pushc, int32_t(nb), push_pair, (unsigned long long)std::max<int64_t>(0, 16));
       }
       k_sp_select<<<grid_sel(n_sw), kBlk, 0, c.stream>>>(cur->as<uint64_t>(), n_sw, sweep_mode, st, gout, gin, W.X.as<uint64_t>(),
                                                        W.Xdeg.as<int64_t>(), W.cap_x, bf, cnt,
@@ -3520,19 +3502,6 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
       sync_counters();
       const int64_t nX = int64_t(hc[C_X]), E = int64_t(hc[C_XE]);
       if (nX == 0 || E == 0) break;
-      if (c.opt("sp_sweep_stats", 0) && nX <= (int64_t(1) << 26)) {
-        // diagnostics: how many distinct vertices the step's adjacency scans come from (pairs
-        // sharing a meet vertex scan its row once each)
-        std::vector<uint64_t> hx(static_cast<size_t>(nX));
-        std::vector<int64_t> hd(static_cast<size_t>(nX));
-        NBG_HIP(hipMemcpyAsync(hx.data(), W.X.p, size_t(nX) * 8, hipMemcpyDeviceToHost, c.stream));
-        NBG_HIP(hipMemcpyAsync(hd.data(), W.Xdeg.p, size_t(nX) * 8, hipMemcpyDeviceToHost, c.stream));
-        NBG_HIP(hipStreamSynchronize(c.stream));
-        std::unordered_map<uint64_t, int64_t> seen;
-        for (int64_t i = 0; i < nX; i++) seen[(hx[size_t(i)] >> 63) << 32 | uint32_t(hx[size_t(i)])] = hd[size_t(i)];
-        diag[0] = seen.size();
-        for (auto& kv : seen) diag[1] += uint64_t(kv.second);
-      }
       c.timing.edges_scanned += uint64_t(E);
       const int64_t want = std::min<int64_t>(E, soft) + 64;
       reserve(c, W.sweep[nxt], W.cap_sweep[nxt], want, 0);
@@ -3554,16 +3523,8 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         chx.alloc(size_t(max_ch) * 4);
         hipEventRecord(c.ev[2], c.stream);
         k_chunk_x<<<grid_n(nX), 256, 0, c.stream>>>(choff.as<int64_t>(), nX, chx.as<int32_t>());
-        const int sgrid = int(std::max<int64_t>(1, std::min<int64_t>((max_ch + 3) / 4, c.opt("sp_sweep_grid", 8192))));
-        const int64_t socc = c.opt("sp_sweep_occ", 5);
-        if (socc >= 8)
-          k_sp_sweep<8><<<sgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), choff.as<int64_t>(), chx.as<int32_t>(), nX,
-                                                      gout, gin, d0, d1, n, lo, st, bf, cnt);
-        else if (socc >= 6)
-          k_sp_sweep<6><<<sgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), choff.as<int64_t>(), chx.as<int32_t>(), nX,
-                                                      gout, gin, d0, d1, n, lo, st, bf, cnt);
-        else
-          k_sp_sweep<1><<<sgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), choff.as<int64_t>(), chx.as<int32_t>(), nX,
+        const int sgrid = int(std::max<int64_t>(1, std::min<int64_t>((max_ch + 3) / 4, 8192)));
+        k_sp_sweep<1><<<sgrid, 256, 0, c.stream>>>(W.X.as<uint64_t>(), choff.as<int64_t>(), chx.as<int32_t>(), nX,
                                                       gout, gin, d0, d1, n, lo, st, bf, cnt);
         NBG_HIP(hipGetLastError());
         hipEventRecord(c.ev[3], c.stream);
@@ -3622,7 +3583,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         NBG_HIP(rocprim::exclusive_scan(nullptr, tb, wdeg, woff, int64_t(0), size_t(nb + 1), rocprim::plus<int64_t>(),
                                         c.stream));
         c.ws_tmp.ensure(tb);
-        const int wgrid = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("sp_grid", 256 * 8), max_tiles)));
+        const int wgrid = int(std::max<int64_t>(1, std::min<int64_t>(256 * 8, max_tiles)));
         for (int32_t i = 0; i + 1 < maxL; i++) {
           k_sp_walk_front<<<grid_n(nb + 1, 1 << 20), 256, 0, c.stream>>>(st, i, dcur, gout, wdeg, dbest);
           NBG_HIP(rocprim::exclusive_scan(c.ws_tmp.p, tb, wdeg, woff, int64_t(0), size_t(nb + 1),

@@ -1078,7 +1078,7 @@ static void gather_props(Ctx& c, Staging& s, const std::vector<Field>& fields, c
       if (mn >= INT8_MIN && mx <= INT8_MAX) w = 1;
       else if (mn >= INT16_MIN && mx <= INT16_MAX) w = 2;
       else if (mn >= INT32_MIN && mx <= INT32_MAX) w = 4;
-      if (c.opt("narrow_props", 1) == 0 || !narrow) w = 8;
+      if (!narrow) w = 8;
       pc.width = w;
       pc.data.alloc(size_t(m) * size_t(w) + 16);
       int g = grid_for(m);
@@ -1747,7 +1747,7 @@ static void build_transpose(Ctx& c, EdgeSpace& es) {
   es.q_field = -1;
   es.q_gbits = es.q_bits = 0;
   es.tcol_q.release();
-  if (c.opt("bu_pack", 1) && R > 0) {
+  if (R > 0) {
     // 2^gb > n_global: an empty slot (-1) decodes to a gidx past every vertex, whose bitmap
     // probe is out of bounds (k_bu_lean relies on it)
     int gb = 1;
@@ -1891,7 +1891,7 @@ static void order_by_degree(Ctx& c, DevBuf& owned, int64_t n_owned) {
   // stage (every in-edge of an owned vertex is there); several ranks count the in-edge keys
   // (dst, -type, rank, src) their parts hold -- the dst owner's, P5 -- so each rank's range is
   // class-ordered too and its bottom-up hops stop at its own bu_both_tiles / bu_in_tiles
-  const bool classes = c.opt("class_order", 1) != 0;
+  const bool classes = true;
   DevBuf ideg;
   if (classes) {
     ideg.alloc(size_t(n_owned) * 4);
@@ -2369,7 +2369,7 @@ static bool commit_merge(Ctx& c) {
   if (c.opt("merge_commit", 1) == 0 || !c.brank.p) return false;
   bool tag_writes = false;
   for (auto& kv : c.tags) tag_writes |= kv.second.stage.n != kv.second.committed_n;
-  bool refuse = tag_writes && c.opt("merge_tags", 1) == 0;
+  bool refuse = false;
   DevBuf cnt;
   cnt.alloc(8);
   NBG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
@@ -2397,7 +2397,6 @@ static bool commit_merge(Ctx& c) {
     // rows for them, which the merge builds only where the batch has tuples: other batches
     // (and the off switch) take the full rebuild
     // (several ranks: the new vertices land in rows every CSR already has, the growth room)
-    if (c.opt("merge_new_vertices", 1) == 0) refuse = true;
     for (auto& kv : c.edges)
       for (int d = 0; d < 2 && !c.sharded; d++)
         if ((d ? kv.second.in_stage.n : kv.second.out_stage.n) == kv.second.ord[d].n) refuse = true;
@@ -2426,7 +2425,7 @@ static bool commit_merge(Ctx& c) {
   // rank (collective: the same union and decision everywhere), else the full rebuild
   NewVertexPlan plan;
   if (c.sharded && !flags[0] && flags[1] > 0 &&
-      (c.opt("merge_new_vertices", 1) == 0 || !plan_new_vertices_ranks(c, int64_t(unknown), plan)))
+      !plan_new_vertices_ranks(c, int64_t(unknown), plan))
     flags[0] = 1;
   if (flags[0]) return false;
   const bool any_tags = flags[2] > 0;
@@ -2654,7 +2653,7 @@ static void finalize_rmat_stream(Ctx& c, EdgeSpace& es) {
   uint32_t* order = idxB.as<uint32_t>();
   if (c.opt("degree_order", 1)) {
     // the staged build's key (k_class_key; this builder runs on one rank)
-    const bool classes = c.opt("class_order", 1) != 0;
+    const bool classes = true;
     DevBuf d1, d2;
     d1.alloc(size_t(n) * 8);
     d2.alloc(size_t(n) * 8);
@@ -2814,9 +2813,7 @@ static void finalize_rmat_stream(Ctx& c, EdgeSpace& es) {
       NBG_HIP(hipStreamSynchronize(c.stream));
       pc.minv = base ? hm[0] : 0;
       pc.maxv = base ? hm[1] : 0;
-      if (c.opt("narrow_props", 1) == 0) {
-        throw Error(NBG_E_UNSUPPORTED, "streamed RMAT with narrow_props = 0");
-      } else if (pc.minv >= INT8_MIN && pc.maxv <= INT8_MAX) {
+      if (pc.minv >= INT8_MIN && pc.maxv <= INT8_MAX) {
         pc.width = 1;
         pc.data.alloc(size_t(base) + 16);
         if (base) k_i16_to_i8<<<grid_for(base), 256, 0, c.stream>>>(w16.as<int16_t>(), pc.data.as<int8_t>(), base);
@@ -2971,7 +2968,7 @@ void snapshot_finalize(Ctx& c) {
     n_owned = ns ? unique_sorted<uint64_t>(c, s2.as<uint64_t>(), owned.as<uint64_t>(), int64_t(ns)) : 0;
     vA.release();
   }
-  if (c.opt("degree_order", 1)) order_by_degree(c, owned, n_owned);
+  order_by_degree(c, owned, n_owned);
   phase("degree order");
   // 3. counts -> base; allgather owned tables into vid_of (rank-major; within a rank by
   // descending out-degree, or by vid with degree_order=0)

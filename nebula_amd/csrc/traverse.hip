@@ -2615,11 +2615,11 @@ template <int MODE>
 void launch_expand(Ctx& c, ExpandArgs a, int pk, const FastArgs& fp, const Program* dprog, const EvalEnv& env,
                    int64_t E, bool tile_rows_ready = false) {
   int64_t ntiles = (E + kTile - 1) / kTile;
-  int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, int64_t(c.opt("expand_grid", 256 * 8)))));
+  int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, int64_t(256 * 8))));
   const size_t ia = timing_event(c);
   if (tile_rows_ready) {  // k_starts_small wrote the table
     a.tile_row = c.ws_tile_rows.as<int32_t>();
-  } else if (c.opt("expand_tile_rows", 1) && a.nF < (int64_t(1) << 31)) {
+  } else if (a.nF < (int64_t(1) << 31)) {
     c.ws_tile_rows.ensure(size_t(ntiles + 2) * 4);
     a.tile_row = c.ws_tile_rows.as<int32_t>();
     k_tile_rows<kTile><<<grid_cap(a.nF), 256, 0, c.stream>>>(a.off, a.nF, c.ws_tile_rows.as<int32_t>());
@@ -2789,10 +2789,10 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   const int bs = cw > 0 ? 1024 : 256;
   const int grid = int(std::max<int64_t>(
       1, std::min<int64_t>((waves + bs / 64 - 1) / (bs / 64),
-                           std::min<int64_t>(cw > 0 ? 512 : c.opt("bu_lean_grid", 2048), kAggBlocks / 2))));
+                           std::min<int64_t>(cw > 0 ? 512 : 2048, kAggBlocks / 2))));
   const size_t shm = size_t(cw + 1) * 4;  // + the zero word non-hub probes read
   uint32_t fb_bytes = uint32_t(fb_words * 4);
-  if (hop_front && !c.sharded && es.bu_both_tiles > 0 && c.opt("bu_fb_bound", 1) != 0)
+  if (hop_front && !c.sharded && es.bu_both_tiles > 0)
     fb_bytes = uint32_t(std::min<int64_t>(fb_bytes, (es.bu_both_tiles * 128 + 31) / 32 * 4));
   const int probe_stats = int(c.opt("bu_probe_stats", 0));  // partials [6] / [7]
   c.ws_pend.ensure(size_t(ntiles * 2 + 2) * 8);  // the pending bits, 2 words per tile
@@ -2821,7 +2821,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   // iteration (bu_lean_u 2), one store per tile in the non-final pass (bu_lean_skip 7), the probe
   // skip without the hub-first probes (bu_lean_skip 1).
   int sel = probe_stats ? 4 + (cw > 0 ? 1 : 0) : (cw > 0 ? 2 : 0);
-  if (sel == 2 && c.opt("bu_lean_nt", 1) != 0 && (fast || es.odeg8.p)) sel = 8;
+  if (sel == 2 && (fast || es.odeg8.p)) sel = 8;
 #define NBG_LEAN(PKV)                                \
   switch (sel) {                                     \
     case 8: go(k_bu_lean<PKV, 1, 1, 0, 1, 3>); break; \
@@ -2863,7 +2863,7 @@ size_t launch_bu_lean(Ctx& c, EdgeSpace& es, const uint32_t* fb, uint32_t* nbits
   const int64_t* trp = tr.row_ptr.as<int64_t>();
   const int32_t* tc = q.gbits ? es.tcol_q.as<int32_t>() : tr.col.as<int32_t>();
   const int ru = int(std::max<int64_t>(1, std::min<int64_t>(c.opt("bu_unroll", 1), kRestMax)));
-  const int grid2 = int(std::min<int64_t>(c.opt("bu_rest_grid", 512), kAggBlocks / 2));
+  const int grid2 = 512;
   const int W = fast ? int(fp.width) : 0;
   // the rest pass probes global memory only by default: its hub copy cost each block ~6 us of
   // LDS fill (r04h/r04k sweeps: 0.637 -> 0.625 ms per C3 query without it)
@@ -3161,7 +3161,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   int64_t hop1_scanned = -1;  // hop-1 rows with duplicate starts rescanned (k_starts_degree)
   int64_t Eg_known = -1;      // several ranks: the start frontier's out-degree sum over ranks
   // the hop-1 expansion's tile-row table is written by k_starts_small (sized for the degree bound)
-  const bool starts_tiles = fast1 && c.opt("expand_tile_rows", 1) != 0 && c.opt("starts_tile_rows", 1) != 0;
+  const bool starts_tiles = fast1;
   if (starts_tiles) {
     const int64_t eb = std::max<int64_t>(1, es.max_odeg >= 0 ? int64_t(ns) * es.max_odeg : csr.nnz);
     c.ws_tile_rows.ensure(size_t(std::min<int64_t>(eb, csr.nnz + 1) / kTile + 4) * 4);
@@ -3180,7 +3180,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   if (ns && !fast1) {
     if (s.steps == 1 && !s.distinct) {
       k_list_starts<<<grid_cap(ns), 256, 0, c.stream>>>(d_sg, ns, lo, hi, row_ptr, row_ok, F, K.d);
-    } else if (!c.sharded && es.odeg.p && c.opt("starts_bits", 1) != 0) {
+    } else if (!c.sharded && es.odeg.p) {
       // one rank: dedup the starts through the frontier bitmap itself (a few hundred atomics)
       // instead of marking the byte map and compacting the whole vertex space
       NBG_HIP(hipMemsetAsync(bits16, 0, c.ws_bits_send.bytes, c.stream));
@@ -3234,7 +3234,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   a.map = map;
   a.err = K.d + 4;
   a.storage = 0;
-  a.mark_check = int32_t(c.opt("mark_check", 0));
+  a.mark_check = 0;
   FastArgs fp{};
   EvalEnv env = make_env(c, es, csr, s.edge_type);
   DevBuf in_keys, in_rows, in_tab;
@@ -3567,7 +3567,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       F = c.ws_front[cur].as<int32_t>();
       const bool lazy = bu_ok && c.opt("compact_list", 0) == 0;
       // (K.d[0, 256) are zero: k_starts_small cleared the counters)
-      if (multi && lazy && es.odeg.p && c.opt("xchg_bits", 1) != 0) {
+      if (multi && lazy && es.odeg.p) {
         // several ranks: every owner ORs the marks it receives straight into its frontier bitmap
         exchange_marks(c, map, bitsA, es.odeg.as<uint32_t>(), K.d + 12);
       } else {
@@ -3837,8 +3837,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       a.F = F;
       a.nF = nF;
       a.off = c.ws_off.as<int64_t>();
-      const bool dst_only = yields.size() == 1 && yields[0].n == 1 && yields[0].ins[0].op == P_DST &&
-                            c.opt("fuse_dst", 1) != 0;
+      const bool dst_only = yields.size() == 1 && yields[0].n == 1 && yields[0].ins[0].op == P_DST;
       DevBuf fused;
       int64_t* rows_edge = nullptr;
       int32_t* rows_src = nullptr;
