@@ -366,9 +366,12 @@ struct EdgeSpace {
   Staging out_stage, in_stage;
   Csr out, in;
   // world > 1: replicas of every rank's out / in CSR over the whole gidx space (built on the
-  // first FIND SHORTEST PATH, which shards its pairs over the ranks)
+  // first FIND SHORTEST PATH, which shards its pairs over the ranks; the out replica alone and
+  // rep_odeg, its out-degrees with row_ok applied, on the first GO whose first hop every rank
+  // runs whole: ensure_rep_out)
   Csr rep_out, rep_in;
-  bool has_rep = false;
+  bool has_rep = false, has_rep_out = false;
+  DevBuf rep_odeg;  // u32 [n_global]
   // Transpose of the out CSR for bottom-up steps: row = owned dst, col = global src index,
   // props = copies of the INT-like out props in transpose order, t_eid = out-edge index.
   Csr tr;
@@ -540,6 +543,7 @@ struct Ctx {
   DevBuf ws_bits_send, ws_bits_recv;
   DevBuf ws_bits_glob;  // world > 1: allgathered frontier bitmap / per-owner mark bitmap
   DevBuf ws_bits_xchg;  // world > 1: received mark segments [world][owned/32]
+  DevBuf ws_bits_rep1;  // world > 1: the hop-1 frontier over the whole gidx space (go_rep1)
   DevBuf ws_piggy;      // world > 1: every rank's (n, e) counters per speculated hop
   DevBuf ws_starts;
   DevBuf ws_partials;  // per-block partial sums of the aggregated kernels
@@ -686,6 +690,8 @@ void wait_host_word(Ctx& c, const unsigned long long* word, uint64_t seq);
 void resolve_total(Ctx& c);
 // traverse.hip
 int32_t go_run(Ctx& c, const nbg_go_spec& spec, nbg_rows* out);
+// the out CSR replica and its out-degrees (collective: every rank calls it at the same point)
+void ensure_rep_out(Ctx& c, EdgeSpace& es);
 int32_t get_bound_run(Ctx& c, int32_t et, const int32_t* parts, const int64_t* vids, size_t n,
                       const uint8_t* filter, size_t flen, const nbg_prop_def* cols, size_t ncols,
                       nbg_rows* out, const int32_t* stats = nullptr);

@@ -2678,6 +2678,21 @@ static void replicate_csr(Ctx& c, const Csr& loc, Csr& rep) {
   NBG_HIP(hipStreamSynchronize(c.stream));
 }
 
+__global__ void k_rep_odeg(const int64_t* row_ptr, const uint8_t* row_ok, int64_t n, uint32_t* odeg) {
+  for (int64_t v = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; v < n; v += int64_t(gridDim.x) * blockDim.x)
+    odeg[v] = row_ok && !row_ok[v] ? 0u : uint32_t(row_ptr[v + 1] - row_ptr[v]);
+}
+
+void ensure_rep_out(Ctx& c, EdgeSpace& es) {
+  if (es.has_rep_out && es.rep_odeg.p) return;
+  if (!es.has_rep_out) replicate_csr(c, es.out, es.rep_out);
+  es.has_rep_out = true;
+  es.rep_odeg.alloc(size_t(std::max<int64_t>(c.n_global, 1)) * 4 + 64);
+  k_rep_odeg<<<grid_n(c.n_global), 256, 0, c.stream>>>(es.rep_out.row_ptr.as<int64_t>(), es.rep_out.row_ok.as<uint8_t>(),
+                                                      c.n_global, es.rep_odeg.as<uint32_t>());
+  NBG_HIP(hipGetLastError());
+}
+
 // the grid that fills the device exactly once with blocks of `kernel` (its occupancy x CUs): a
 // grid-stride scan over the chunks of a step then has no second, partial round of blocks
 // (measured: 1024 blocks of the sweep 0.42 ms, its resident 1280 0.38 ms, 2048 0.43 ms)
@@ -2722,7 +2737,8 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
   std::vector<int64_t> my_src, my_dst;
   if (c.sharded) {
     if (!es.has_rep) {
-      replicate_csr(c, es.out, es.rep_out);
+      if (!es.has_rep_out) replicate_csr(c, es.out, es.rep_out);
+      es.has_rep_out = true;
       replicate_csr(c, es.in, es.rep_in);
       es.has_rep = true;
     }

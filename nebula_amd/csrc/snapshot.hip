@@ -495,7 +495,8 @@ void snapshot_load_part(Ctx& c, int32_t part, const uint8_t* kb, const uint64_t*
 static void reset_transpose_derived(EdgeSpace& es) {
   es.rep_out = Csr();
   es.rep_in = Csr();
-  es.has_rep = false;
+  es.has_rep = es.has_rep_out = false;
+  es.rep_odeg.release();
   es.tr = Csr();
   es.t_eid.release();
   es.has_tr = es.has_t_eid = false;
@@ -2486,7 +2487,8 @@ static bool commit_merge(Ctx& c) {
       // replicated CSRs (FIND SHORTEST PATH on several ranks) are rebuilt on first use
       es.rep_out = Csr();
       es.rep_in = Csr();
-      es.has_rep = false;
+      es.has_rep = es.has_rep_out = false;
+      es.rep_odeg.release();
     }
     if (out_any && c.opt("bottom_up", 1)) build_transpose(c, es);  // collective on several ranks
     phase("transpose + slabs");

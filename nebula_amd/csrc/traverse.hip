@@ -1668,20 +1668,24 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
                                                  const uint8_t* row_ok, int require_deg, int32_t* out,
                                                  unsigned long long* n_out, unsigned long long* partials,
                                                  uint16_t* bits, const uint32_t* __restrict__ odeg,
-                                                 unsigned long long* sums = nullptr, int shards = 1) {
+                                                 unsigned long long* sums = nullptr, int shards = 1,
+                                                 int64_t own_lo = 0, int64_t own_hi = -1) {
   // tile = 256 threads x 4 chunks of 16 bytes = 16384 vertices; one returning atomic per tile
   // (1024-thread tiles, a quarter of the atomics, measured slower: 40 -> 47 us at hop 1);
   // n_set (partials[0]), the kept out-degree sum (partials[1]) and the kept count (partials[2])
   // go to per-block partials.  out == nullptr: bitmap and counts only, no list (the list is built
   // from the bitmap later if a top-down hop needs it: the per-tile list atomics were most of
-  // this kernel's time - 4096 tiles on one counter at RMAT-26)
+  // this kernel's time - 4096 tiles on one counter at RMAT-26).  own_lo < own_hi: the kept count
+  // and out-degree sum of the vertices in [own_lo, own_hi) too (slots 3, 4: a rank's share of a
+  // whole-space frontier, go_rep1; own_lo a multiple of 16)
   __shared__ uint32_t lds[16];
   __shared__ unsigned long long lds64[kSlots * 16];
   __shared__ unsigned long long s_base;
   const int64_t nchunks = (n + 15) / 16;
   const int64_t tile = int64_t(blockDim.x) * 4;
   const int64_t ntiles = (nchunks + tile - 1) / tile;
-  unsigned long long acc[3] = {0, 0, 0};
+  unsigned long long acc[5] = {0, 0, 0, 0, 0};
+  const int nsum = own_lo < own_hi ? 5 : 3;
   // bitmap-only compaction (out == nullptr, the bottom-up path): the next tile's chunk loads are
   // issued with this one's (its map words stay in registers for the next round), so a block waits
   // one map latency per round of tiles, not one per tile
@@ -1728,6 +1732,7 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
         for (int b = 0; b < 4; b++)
           if ((words[a] >> (8 * b)) & 0xff) setmask |= 1u << (a * 4 + b);
       uint32_t keepmask = setmask;
+      const unsigned long long deg0 = acc[1];
       if (require_deg && setmask && odeg) {
         // out-degrees (0 where row_ok == 0) of the chunk's 16 vertices: four 16-byte loads issued
         // together, instead of a dependent row_ptr pair per set vertex (hub tiles are dense)
@@ -1761,6 +1766,7 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
       if (bits && ch < nchunks) bits[ch] = uint16_t(keepmask);  // frontier bitmap for bottom-up
       if (setmask) reinterpret_cast<uint4*>(map + lo)[ch] = make_uint4(0, 0, 0, 0);
       acc[0] += __popc(setmask);
+      if (ch * 16 + lo >= own_lo && ch * 16 + lo < own_hi) acc[3] += __popc(keepmask), acc[4] += acc[1] - deg0;
       keep[q] = keepmask;
       cnt += __popc(keepmask);
     }
@@ -1779,8 +1785,8 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
     __syncthreads();
   }
   // sums (zeroed by the caller): the block sums added there, no k_reduce_partials launch
-  if (sums) block_add_sums(acc, 3, lds64, sums, shards);
-  else block_store_partials(acc, 3, lds64, partials);
+  if (sums) block_add_sums(acc, nsum, lds64, sums, shards);
+  else block_store_partials(acc, nsum, lds64, partials);
 }
 
 // starts (gidx) -> deduplicated frontier: bitmap bits (set once, by a returning atomicOr) and
@@ -2583,7 +2589,8 @@ static void lds_limit(const void* kern, size_t shm) {
 
 void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* row_ptr, const uint8_t* row_ok,
                     int require_deg, int32_t* out, uint16_t* bits, unsigned long long* Kd,
-                    const uint32_t* odeg = nullptr, bool sums_zero = false, int shards = 1) {
+                    const uint32_t* odeg = nullptr, bool sums_zero = false, int shards = 1, int64_t own_lo = 0,
+                    int64_t own_hi = -1) {
   // counters: Kd[0] list length (atomic), Kd[12] vertices set, Kd[13] kept out-degree sum,
   // Kd[14] kept vertices (= the list length, also when out == nullptr writes no list).
   // sums_zero: Kd[12, 15) are already zero, so the blocks add into them (bu_atomic_sums)
@@ -2592,7 +2599,7 @@ void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* 
   int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, std::min<int64_t>(kAggBlocks, c.opt("compact_grid", 1024)))));
   const bool atomic = sums_zero && c.opt("bu_atomic_sums", 1) != 0;
   k_compact<<<grid, 256, 0, c.stream>>>(map, lo, n, row_ptr, row_ok, require_deg, out, Kd, partials, bits, odeg,
-                                        atomic ? Kd + 12 : nullptr, atomic ? shards : 1);
+                                        atomic ? Kd + 12 : nullptr, atomic ? shards : 1, own_lo, own_hi);
   if (!atomic) k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, Kd + 12);
   NBG_HIP(hipGetLastError());
 }
@@ -3160,18 +3167,30 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   int64_t nset_global = ns;  // "starts_ non-empty" (GoExecutor.cpp:93-97)
   int64_t hop1_scanned = -1;  // hop-1 rows with duplicate starts rescanned (k_starts_degree)
   int64_t Eg_known = -1;      // several ranks: the start frontier's out-degree sum over ranks
+  // several ranks (option go_rep1): every rank runs the whole first hop -- every start, over a
+  // replica of the out CSR (ensure_rep_out, built on first use) -- into a frontier bitmap over the
+  // whole gidx space, so the hop needs no mark exchange and the second hop no frontier allgather:
+  // one collective a C3 query instead of three.  (The same branch on every rank: ns, the degree
+  // statistics and the options are the same everywhere.)
+  const bool rep1 = fast1 && multi && bu_ok && c.opt("compact_list", 0) == 0 && es.odeg.p && c.opt("go_rep1", 1) != 0;
+  const Csr& csr1 = rep1 ? es.rep_out : csr;  // the first hop's rows
+  if (rep1) {
+    ensure_rep_out(c, es);
+    c.ws_bits_rep1.ensure(size_t(map_bytes(c) / 8 + 64));
+  }
   // the hop-1 expansion's tile-row table is written by k_starts_small (sized for the degree bound)
   const bool starts_tiles = fast1;
+  const int64_t max_odeg1 = rep1 ? es.max_odeg_global : es.max_odeg;
   if (starts_tiles) {
-    const int64_t eb = std::max<int64_t>(1, es.max_odeg >= 0 ? int64_t(ns) * es.max_odeg : csr.nnz);
-    c.ws_tile_rows.ensure(size_t(std::min<int64_t>(eb, csr.nnz + 1) / kTile + 4) * 4);
+    const int64_t eb = std::max<int64_t>(1, max_odeg1 >= 0 ? int64_t(ns) * max_odeg1 : csr1.nnz);
+    c.ws_tile_rows.ensure(size_t(std::min<int64_t>(eb, csr1.nnz + 1) / kTile + 4) * 4);
   }
   if (fast1) {
-    k_starts_small<<<1, 1024, 0, c.stream>>>(k_starts, int32_t(ns), c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(),
-                                              uint64_t(c.ht_cap - 1), c.ht_has_min, c.ht_min_gidx, d_sg, lo, hi,
-                                              row_ptr, row_ok, reinterpret_cast<uint32_t*>(bits16), F,
-                                              c.ws_off.as<int64_t>(), K.d,
-                                              starts_tiles ? c.ws_tile_rows.as<int32_t>() : nullptr);
+    k_starts_small<<<1, 1024, 0, c.stream>>>(
+        k_starts, int32_t(ns), c.ht_keys.as<int64_t>(), c.ht_vals.as<int32_t>(), uint64_t(c.ht_cap - 1), c.ht_has_min,
+        c.ht_min_gidx, d_sg, rep1 ? 0 : lo, rep1 ? c.n_global : hi, csr1.row_ptr.as<int64_t>(),
+        csr1.row_ok.as<uint8_t>(), rep1 ? c.ws_bits_rep1.as<uint32_t>() : reinterpret_cast<uint32_t*>(bits16), F,
+        c.ws_off.as<int64_t>(), K.d, starts_tiles ? c.ws_tile_rows.as<int32_t>() : nullptr);
     NBG_HIP(hipGetLastError());
     nF = ns;  // an upper bound: the entries past the list have degree 0
   } else {
@@ -3405,8 +3424,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   // the first hop; every hop's frontier allgather carries the previous hop's (n, e) of every rank
   // to its gate (GateIn::all), one exchange per hop instead of an allgather and an all-reduce
   bool spec_blocks_used = false;
+  // fb_first (several ranks, go_rep1): the first hop reads this whole-space frontier and (e, n)
+  // summed over ranks already; the hops after it exchange as with cnt
   auto spec_enqueue = [&](int32_t first, const unsigned long long* e, const unsigned long long* n, int32_t hop0,
-                          const unsigned long long* cnt = nullptr) {
+                          const unsigned long long* cnt = nullptr, const uint32_t* fb_first = nullptr) {
     spec.clear();
     if (!spec_ok) return;
     // the blocks start at zero (query start); a second chain in one query reuses them
@@ -3432,7 +3453,9 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // several ranks: the frontier bitmaps of every rank (the exchange runs whatever the gate
       // says: every rank enqueued it)
       const uint32_t* fb;
-      if (cnt) {
+      if (fb_first && spec.empty()) {
+        fb = fb_first;
+      } else if (cnt) {
         unsigned long long* all = c.ws_piggy.as<unsigned long long>() + spec.size() * size_t(c.world) * 2;
         fb = global_bits_cnt(c, in, cnt, all);
         gi.e = gi.n = nullptr;
@@ -3461,7 +3484,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       e = blk + 1;
       n = blk + 0;
       last_blk = fin ? nullptr : blk;
-      if (cnt) {
+      if (cnt || fb_first) {
         cnt = blk;  // the next hop's exchange carries this hop's (n, e)
       } else if (multi && !fin) {
         dev_allsum(c, blk, {0, 1}, blk + 10);
@@ -3561,13 +3584,22 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       a.F = F;
       a.nF = nF;
       a.off = c.ws_off.as<int64_t>();
-      const int64_t e_bound = std::max<int64_t>(1, es.max_odeg >= 0 ? ns * es.max_odeg : csr.nnz);
-      launch_expand<EXP_MARK>(c, a, PK_NONE, fp, nullptr, env, std::min<int64_t>(e_bound, csr.nnz + 1), starts_tiles);
+      const int64_t e_bound = std::max<int64_t>(1, max_odeg1 >= 0 ? ns * max_odeg1 : csr1.nnz);
+      ExpandArgs a1 = a;
+      if (rep1) a1.row_ptr = csr1.row_ptr.as<int64_t>(), a1.col = csr1.col.as<int32_t>(), a1.lo = 0;
+      launch_expand<EXP_MARK>(c, a1, PK_NONE, fp, nullptr, env, std::min<int64_t>(e_bound, csr1.nnz + 1), starts_tiles);
       cur ^= 1;
       F = c.ws_front[cur].as<int32_t>();
       const bool lazy = bu_ok && c.opt("compact_list", 0) == 0;
       // (K.d[0, 256) are zero: k_starts_small cleared the counters)
-      if (multi && lazy && es.odeg.p) {
+      if (rep1) {
+        // the whole-space frontier and its counts (the same on every rank), plus this rank's share
+        // (K.d[15, 17)); its owned slice to bitsA for a host-chosen top-down hop 2
+        launch_compact(c, map, 0, c.n_global, csr1.row_ptr.as<int64_t>(), csr1.row_ok.as<uint8_t>(), 1, nullptr,
+                       c.ws_bits_rep1.as<uint16_t>(), K.d, es.rep_odeg.as<uint32_t>(), true, 1, lo, hi);
+        NBG_HIP(hipMemcpyAsync(bitsA, c.ws_bits_rep1.as<uint8_t>() + lo / 8, size_t(n_own + 7) / 8,
+                               hipMemcpyDeviceToDevice, c.stream));
+      } else if (multi && lazy && es.odeg.p) {
         // several ranks: every owner ORs the marks it receives straight into its frontier bitmap
         exchange_marks(c, map, bitsA, es.odeg.as<uint32_t>(), K.d + 12);
       } else {
@@ -3579,24 +3611,30 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // several ranks: the counts over ranks -- piggy: carried by the first speculated hop's
       // frontier exchange (its gate publishes them); else found, next out-degree sum and hop-1
       // entries summed into K.d[48, 51)
-      piggy_used = multi && spec_ok && c.opt("comm_piggy", 1) != 0;
+      piggy_used = multi && spec_ok && (rep1 || c.opt("comm_piggy", 1) != 0);
       if (multi && !piggy_used) dev_allsum(c, K.d, {12, 13, 41}, K.d + 48);
-      spec_enqueue(2, K.d + (multi ? 49 : 13), K.d + (multi ? 48 : 12), c.timing.n_hops + 1,
-                   piggy_used ? K.d + 12 : nullptr);  // (hop 1: below)
+      if (rep1)
+        spec_enqueue(2, K.d + 13, K.d + 12, c.timing.n_hops + 1, nullptr, c.ws_bits_rep1.as<uint32_t>());
+      else
+        spec_enqueue(2, K.d + (multi ? 49 : 13), K.d + (multi ? 48 : 12), c.timing.n_hops + 1,
+                     piggy_used ? K.d + 12 : nullptr);  // (hop 1: below)
       if (piggy_used && spec.empty()) {  // nothing speculated (steps == 2 without the final): sum here
         piggy_used = false;
-        dev_allsum(c, K.d, {12, 13, 41}, K.d + 48);
+        if (!rep1) dev_allsum(c, K.d, {12, 13, 41}, K.d + 48);
       }
       // (the device work ends here when the speculated final hop runs: ev[1] ahead of the fetch)
       fetch_counters(c, K.d, spec_words(multi ? 52 : 42), K.h, spec_final() && tot_ev ? c.ev[1] : nullptr, ks);
       const int64_t nF1 = int64_t(K.h[40]), E1 = int64_t(K.h[41]);
       if (!s.distinct) hop1_scanned = int64_t(K.h[30]);
-      c.timing.edges_scanned += uint64_t(hop1_scanned >= 0 ? hop1_scanned : E1);
+      // (go_rep1: every rank ran the whole hop; rank 0 counts it, so the ranks' sum is the hop's)
+      if (!rep1 || c.rank == 0) c.timing.edges_scanned += uint64_t(hop1_scanned >= 0 ? hop1_scanned : E1);
       if (E1 > 0) c.timing.expand_bytes += expand_bytes(nF1, E1, 0, EXP_MARK);
       const unsigned long long hs[8] = {(unsigned long long)nF1, (unsigned long long)E1, 0, 0, 0, 0, 0, 0};
       c.timing.hop(0, false, 0.0, hs);
       int64_t n1g = int64_t(K.h[12]), e1g = int64_t(K.h[13]), E1g = E1;
-      if (multi && piggy_used) {  // the first speculated hop's gate published hop 1's sums
+      if (rep1) {
+        // (whole-space counts: already the sums over ranks)
+      } else if (multi && piggy_used) {  // the first speculated hop's gate published hop 1's sums
         n1g = int64_t(K.h[64 + 10]);
         e1g = int64_t(K.h[64 + 11]);
         E1g = n1g;  // (no marks anywhere iff no start has out-edges: the empty result either way)
@@ -3607,8 +3645,8 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       }
       if (E1g == 0) return finish_empty();  // every start lacks out-edges
       nF = lazy ? 0 : int64_t(K.h[0]);
-      list_n = lazy ? int64_t(K.h[14]) : -1;
-      E = int64_t(K.h[13]);
+      list_n = lazy ? int64_t(K.h[rep1 ? 15 : 14]) : -1;
+      E = int64_t(K.h[rep1 ? 16 : 13]);
       E_known = E;
       nset_global = n1g;
       Eg = e1g;

@@ -68,6 +68,17 @@ def test_bench_query_rmat20_sharded(force):
                 t = g.each(lambda r, s: s.last_timing())
                 assert all(x["host_waits"] <= 2 and x["spec_hops"] >= 2 for x in t), \
                     [(x["host_waits"], x["spec_hops"]) for x in t]
+                # every rank ran the whole first hop over the out-CSR replica (go_rep1): the
+                # second hop's frontier allgather is the query's one collective
+                assert all(x["comm_calls"] == 1 for x in t), [x["comm_calls"] for x in t]
+                # the owner-computed first hop: marks all-to-all + two frontier allgathers
+                g.each(lambda r, s: s.set_option("go_rep1", 0))
+                res = g.go(synth.seeds(20, 16, 1, 64), 3, FOLLOW, where=W499, yields=[X.EdgeDst("follow")],
+                           distinct=True)
+                col = np.sort(np.concatenate([x.columns[0] for x in res]))
+                check_gold("go3_where499_distinct_s20", col, sum(x.edges_scanned for x in res))
+                t = g.each(lambda r, s: s.last_timing())
+                assert all(x["comm_calls"] == 3 for x in t), [x["comm_calls"] for x in t]
                 # the gates' counts summed by all-reduces instead of riding on the frontier
                 # exchanges (comm_piggy = 0): same rows
                 g.each(lambda r, s: s.set_option("comm_piggy", 0))

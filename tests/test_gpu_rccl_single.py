@@ -53,13 +53,16 @@ def rccl20():
     sp.close()
 
 
-@pytest.mark.parametrize("force,piggy", [(0, 1), (0, 0), (1, 1), (-1, 1)])
-def test_c3_query_rmat20_through_rccl(rccl20, force, piggy):
+@pytest.mark.parametrize("force,piggy,rep1", [(0, 1, 1), (0, 1, 0), (0, 0, 0), (1, 1, 1), (-1, 1, 1)])
+def test_c3_query_rmat20_through_rccl(rccl20, force, piggy, rep1):
     """configs[2]'s query at RMAT-20 through the one-rank RCCL communicator, every direction
-    mode, with the gate counters riding on the frontier allgathers or summed by all-reduces"""
+    mode; the first hop over the out-CSR replica (go_rep1, one collective a query) or computed by
+    the owners (marks all-to-all), with the gate counters riding on the frontier allgathers or
+    summed by all-reduces"""
     sp = rccl20
     sp.set_option("bu_force", force)
     sp.set_option("comm_piggy", piggy)
+    sp.set_option("go_rep1", rep1)
     try:
         for _ in range(2):  # the first query also gathers the snapshot's degree statistics
             r = sp.go(synth.seeds(20, 16, 1, 64), 3, FOLLOW, where=W499, yields=[X.EdgeDst("follow")],
@@ -69,11 +72,14 @@ def test_c3_query_rmat20_through_rccl(rccl20, force, piggy):
         assert t["comm_calls"] > 0, t
         if force == 0:
             assert t["host_waits"] <= 2 and t["spec_hops"] >= 2, (t["host_waits"], t["spec_hops"])
+            if piggy:
+                assert t["comm_calls"] == (1 if rep1 else 3), t["comm_calls"]
         print(f"force {force} piggy {piggy}: {t['comm_calls']} collectives, {t['comm_ms']:.3f} ms "
               f"({t['comm_ms'] / t['comm_calls'] * 1e3:.1f} us each), device {t['total_ms']:.3f} ms")
     finally:
         sp.unset_option("bu_force")
         sp.unset_option("comm_piggy")
+        sp.unset_option("go_rep1")
 
 
 def test_plain_rows_and_row_shuffle_rmat20(rccl20):
