@@ -1669,7 +1669,8 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
                                                  unsigned long long* n_out, unsigned long long* partials,
                                                  uint16_t* bits, const uint32_t* __restrict__ odeg,
                                                  unsigned long long* sums = nullptr, int shards = 1,
-                                                 int64_t own_lo = 0, int64_t own_hi = -1) {
+                                                 int64_t own_lo = 0, int64_t own_hi = -1,
+                                                 uint16_t* __restrict__ own_bits = nullptr, int64_t n_read = INT64_MAX) {
   // tile = 256 threads x 4 chunks of 16 bytes = 16384 vertices; one returning atomic per tile
   // (1024-thread tiles, a quarter of the atomics, measured slower: 40 -> 47 us at hop 1);
   // n_set (partials[0]), the kept out-degree sum (partials[1]) and the kept count (partials[2])
@@ -1677,11 +1678,15 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
   // from the bitmap later if a top-down hop needs it: the per-tile list atomics were most of
   // this kernel's time - 4096 tiles on one counter at RMAT-26).  own_lo < own_hi: the kept count
   // and out-degree sum of the vertices in [own_lo, own_hi) too (slots 3, 4: a rank's share of a
-  // whole-space frontier, go_rep1; own_lo a multiple of 16)
+  // whole-space frontier, go_rep1; own_lo a multiple of 16), and own_bits (if set) gets that
+  // range's bitmap.  n_read: past it the map is known to be zero (no dst of the hop's edge type
+  // lies there: the class-ordered numbering puts the vertices without in-edges last), so those
+  // chunks are not read and their bitmap words are written as zero
   __shared__ uint32_t lds[16];
   __shared__ unsigned long long lds64[kSlots * 16];
   __shared__ unsigned long long s_base;
   const int64_t nchunks = (n + 15) / 16;
+  const int64_t rchunks = min(nchunks, (n_read + 15) / 16);  // chunks whose map bytes are read
   const int64_t tile = int64_t(blockDim.x) * 4;
   const int64_t ntiles = (nchunks + tile - 1) / tile;
   unsigned long long acc[5] = {0, 0, 0, 0, 0};
@@ -1695,7 +1700,7 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int64_t ch = int64_t(blockIdx.x) * tile + q * int64_t(blockDim.x) + threadIdx.x;
-      wn[q] = int64_t(blockIdx.x) < ntiles && ch < nchunks ? reinterpret_cast<const uint4*>(map + lo)[ch]
+      wn[q] = int64_t(blockIdx.x) < ntiles && ch < rchunks ? reinterpret_cast<const uint4*>(map + lo)[ch]
                                                             : make_uint4(0, 0, 0, 0);
     }
   }
@@ -1711,13 +1716,13 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
       for (int q = 0; q < 4; q++) {
         wq[q] = wn[q];
         const int64_t ch = tn * tile + q * int64_t(blockDim.x) + threadIdx.x;
-        wn[q] = tn < ntiles && ch < nchunks ? reinterpret_cast<const uint4*>(map + lo)[ch] : make_uint4(0, 0, 0, 0);
+        wn[q] = tn < ntiles && ch < rchunks ? reinterpret_cast<const uint4*>(map + lo)[ch] : make_uint4(0, 0, 0, 0);
       }
     } else {
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int64_t ch = t * tile + q * int64_t(blockDim.x) + threadIdx.x;
-        wq[q] = ch < nchunks ? reinterpret_cast<const uint4*>(map + lo)[ch] : make_uint4(0, 0, 0, 0);
+        wq[q] = ch < rchunks ? reinterpret_cast<const uint4*>(map + lo)[ch] : make_uint4(0, 0, 0, 0);
       }
     }
 #pragma unroll
@@ -1766,7 +1771,10 @@ __global__ __launch_bounds__(256) void k_compact(uint8_t* map, int64_t lo, int64
       if (bits && ch < nchunks) bits[ch] = uint16_t(keepmask);  // frontier bitmap for bottom-up
       if (setmask) reinterpret_cast<uint4*>(map + lo)[ch] = make_uint4(0, 0, 0, 0);
       acc[0] += __popc(setmask);
-      if (ch * 16 + lo >= own_lo && ch * 16 + lo < own_hi) acc[3] += __popc(keepmask), acc[4] += acc[1] - deg0;
+      if (ch * 16 + lo >= own_lo && ch * 16 + lo < own_hi) {
+        acc[3] += __popc(keepmask), acc[4] += acc[1] - deg0;
+        if (own_bits) own_bits[ch - (own_lo - lo) / 16] = uint16_t(keepmask);
+      }
       keep[q] = keepmask;
       cnt += __popc(keepmask);
     }
@@ -2590,7 +2598,7 @@ static void lds_limit(const void* kern, size_t shm) {
 void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* row_ptr, const uint8_t* row_ok,
                     int require_deg, int32_t* out, uint16_t* bits, unsigned long long* Kd,
                     const uint32_t* odeg = nullptr, bool sums_zero = false, int shards = 1, int64_t own_lo = 0,
-                    int64_t own_hi = -1) {
+                    int64_t own_hi = -1, uint16_t* own_bits = nullptr, int64_t n_read = -1) {
   // counters: Kd[0] list length (atomic), Kd[12] vertices set, Kd[13] kept out-degree sum,
   // Kd[14] kept vertices (= the list length, also when out == nullptr writes no list).
   // sums_zero: Kd[12, 15) are already zero, so the blocks add into them (bu_atomic_sums)
@@ -2599,7 +2607,8 @@ void launch_compact(Ctx& c, uint8_t* map, int64_t lo, int64_t n, const int64_t* 
   int grid = int(std::max<int64_t>(1, std::min<int64_t>(ntiles, std::min<int64_t>(kAggBlocks, c.opt("compact_grid", 1024)))));
   const bool atomic = sums_zero && c.opt("bu_atomic_sums", 1) != 0;
   k_compact<<<grid, 256, 0, c.stream>>>(map, lo, n, row_ptr, row_ok, require_deg, out, Kd, partials, bits, odeg,
-                                        atomic ? Kd + 12 : nullptr, atomic ? shards : 1, own_lo, own_hi);
+                                        atomic ? Kd + 12 : nullptr, atomic ? shards : 1, own_lo, own_hi, own_bits,
+                                        n_read >= 0 ? n_read : n);
   if (!atomic) k_reduce_partials<<<1, 1024, 0, c.stream>>>(partials, grid, Kd + 12);
   NBG_HIP(hipGetLastError());
 }
@@ -3172,6 +3181,10 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
   // whole gidx space, so the hop needs no mark exchange and the second hop no frontier allgather:
   // one collective a C3 query instead of three.  (The same branch on every rank: ns, the degree
   // statistics and the options are the same everywhere.)
+  // the marks of a top-down hop over this edge type are its dsts: rows with an in-edge, the
+  // first bu_in_tiles tiles of the owned range (class-ordered numbering); the compactions read
+  // the byte map that far and write the bitmap past it as zero
+  const int64_t map_bound = es.has_tr && es.bu_in_tiles > 0 ? std::min<int64_t>(n_own, es.bu_in_tiles * 128) : n_own;
   const bool rep1 = fast1 && multi && bu_ok && c.opt("compact_list", 0) == 0 && es.odeg.p && c.opt("go_rep1", 1) != 0;
   const Csr& csr1 = rep1 ? es.rep_out : csr;  // the first hop's rows
   if (rep1) {
@@ -3594,18 +3607,19 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // (K.d[0, 256) are zero: k_starts_small cleared the counters)
       if (rep1) {
         // the whole-space frontier and its counts (the same on every rank), plus this rank's share
-        // (K.d[15, 17)); its owned slice to bitsA for a host-chosen top-down hop 2
+        // (K.d[15, 17)) and its owned slice in bitsA (for a host-chosen top-down hop 2).  (Block
+        // partials + a reduce launch instead of the block atomics measured the same: 0.4255 vs
+        // 0.4243 ms a one-rank RCCL query, profiles/r13b_*)
         launch_compact(c, map, 0, c.n_global, csr1.row_ptr.as<int64_t>(), csr1.row_ok.as<uint8_t>(), 1, nullptr,
-                       c.ws_bits_rep1.as<uint16_t>(), K.d, es.rep_odeg.as<uint32_t>(), true, 1, lo, hi);
-        NBG_HIP(hipMemcpyAsync(bitsA, c.ws_bits_rep1.as<uint8_t>() + lo / 8, size_t(n_own + 7) / 8,
-                               hipMemcpyDeviceToDevice, c.stream));
+                       c.ws_bits_rep1.as<uint16_t>(), K.d, es.rep_odeg.as<uint32_t>(), true, 1, lo, hi,
+                       reinterpret_cast<uint16_t*>(bitsA));
       } else if (multi && lazy && es.odeg.p) {
         // several ranks: every owner ORs the marks it receives straight into its frontier bitmap
         exchange_marks(c, map, bitsA, es.odeg.as<uint32_t>(), K.d + 12);
       } else {
         exchange_marks(c, map);  // several ranks: every owner receives the marks of its vertices
         launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
-                       K.d, es.odeg.as<uint32_t>(), true, ks);
+                       K.d, es.odeg.as<uint32_t>(), true, ks, 0, -1, nullptr, map_bound);
         if (ks > 1) shards_dirty = true;
       }
       // several ranks: the counts over ranks -- piggy: carried by the first speculated hop's
@@ -3722,7 +3736,7 @@ int32_t go_run(Ctx& c, const nbg_go_spec& s, nbg_rows* out) {
       // bitmap is slice-relative, ensure_list's input is the bottom-up's global-indexed one
       const bool lazy = bu_ok && !multi_root && c.opt("compact_list", 0) == 0;
       launch_compact(c, map, lo, n_own, row_ptr, row_ok, 1, lazy ? nullptr : F, reinterpret_cast<uint16_t*>(bitsA),
-                     K.d, es.odeg.as<uint32_t>());
+                     K.d, es.odeg.as<uint32_t>(), false, 1, 0, -1, nullptr, map_bound);
       piggy_used = multi && lazy && spec_ok && c.opt("comm_piggy", 1) != 0;
       if (multi && !piggy_used) dev_allsum(c, K.d, {12, 13}, K.d + 48);
       if (lazy)

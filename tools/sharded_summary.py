@@ -29,7 +29,8 @@ B_LINK_GBS = 153.0    # per xGMI link and direction (the task statement's figure
 # bound at any size; with go_rep1 every rank runs it whole), the byte map -> bitmap pass over the
 # whole gidx space (k_map_to_bits; go_rep1: the whole-space k_compact and the copy of the owned
 # slice), the counter publish
-FIXED = ("k_starts_small", "k_expand<0, 0>", "k_map_to_bits", "nbg::k_compact", "copyBuffer", "k_publish")
+FIXED = ("k_starts_small", "k_expand<0, 0>", "k_map_to_bits", "nbg::k_compact", "k_reduce_partials", "copyBuffer",
+         "k_publish")
 
 
 def timeline_stats(path):
