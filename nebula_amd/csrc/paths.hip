@@ -2329,8 +2329,8 @@ __global__ __launch_bounds__(kBlk) void k_dv_sweep_select(SpDev d, SpState st, S
 // once an out-neighbour has dt = L - l - 1 (the scan stops there).  Claims go to the arena and
 // the next sweep list, and the pull entries of the claimed vertices that the next step scans are
 // added to the pair's step j + 1 sum.
-template <int U>  // column entries per lane and step (4, 8, 16: a whole chunk in one step)
-__global__ __launch_bounds__(256) void k_dv_sweep(SpDev d, SpState st, SpFilt f, SpCsr gout, SpCsr gin,
+template <int U, int OCC = 1>  // column entries per lane and step; waves per SIMD the registers allow
+__global__ __launch_bounds__(256, OCC) void k_dv_sweep(SpDev d, SpState st, SpFilt f, SpCsr gout, SpCsr gin,
                                                        uint8_t* d0, uint8_t* d1, int64_t n, int64_t lo, int32_t j) {
   __shared__ uint64_t s_stage[4][kDvStage];
   if (dv_ovf_block(d.cnt)) return;  // a producer overflowed: its tables are incomplete (the host re-runs)
@@ -3029,6 +3029,7 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
     auto enqueue = [&](int it) {
       if (it > 1 || !sel1) {
         ++nl;
+        // (at 6 / 8 waves per SIMD, 104 / 176 B spilled: C4 1.133-1.154 -> 1.176-1.197 ms, c4occ3)
         k_dv_select<<<gsel((const void*)k_dv_select), kBlk, 0, c.stream>>>(d, st, gout, gin, it);
       }
       evi[size_t(it)][0] = dv_event();
@@ -3067,12 +3068,20 @@ int32_t shortest_path_run(Ctx& c, int32_t et, const int64_t* src_all, const int6
         d, st, gout, gin, lo, htk, htv, uint64_t(htm), c.ht_has_min, c.ht_min_gidx);
     const int nsw = int(std::min<int64_t>(std::max<int64_t>(maxF - 1, 0), kMaxQ - 2));
     const unsigned long long bias16 = (unsigned long long)std::max<int64_t>(0, 16);
+    // the sweep at 6 waves per SIMD (80 VGPRs, 12 B spilled): C4 1.164 -> 1.140 ms against the
+    // register-bound 5 (8: 64 VGPRs, 76 B spilled, 1.155; 8 entries per lane: 1.211; c4occ)
+    const int sw_occ = int(c.opt("sp_sweep_occ", 6));
     for (int j = 1; j <= nsw; j++) {
       ++nl;
       k_dv_sweep_select<<<gsel((const void*)k_dv_sweep_select), kBlk, 0, c.stream>>>(d, st, gout, gin, j, bias16);
       evs[size_t(j)][0] = dv_event();
       ++nl;
-      k_dv_sweep<4><<<gsz((const void*)k_dv_sweep<4>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
+      switch (sw_occ) {
+        case 6: k_dv_sweep<4, 6><<<gsz((const void*)k_dv_sweep<4, 6>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j); break;
+        case 8: k_dv_sweep<4, 8><<<gsz((const void*)k_dv_sweep<4, 8>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j); break;
+        case 2: k_dv_sweep<8, 1><<<gsz((const void*)k_dv_sweep<8, 1>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j); break;
+        default: k_dv_sweep<4><<<gsz((const void*)k_dv_sweep<4>), 256, 0, c.stream>>>(d, st, f, gout, gin, d0, d1, n, lo, j);
+      }
       evs[size_t(j)][1] = dv_event();
     }
     const int nwalk = int(std::min<int64_t>(maxL >= 2 ? maxL - 1 : 0, kMaxQ - 2));
