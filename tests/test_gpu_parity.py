@@ -661,7 +661,7 @@ def test_rmat_bottom_up_packed_predicate(rmat12, qpred, hub_cap, fin):
             g = sp.go(starts, 2, FOLLOW, where=w, yields=[X.EdgeDst("follow")], distinct=True)
             r_ = st.go(starts, 2, FOLLOW, where=w.encode(), yields=[X.EdgeDst("follow").encode()], distinct=True)
             assert np.array_equal(np.sort(g.columns[0]), np.sort(r_.int_col(0))), (k, op)
-            assert g.edges_scanned == r_.edges_scanned
+            assert g.edges_scanned == r_.edges_scanned, (k, op, [(h["mode"], h["c"][:6]) for h in sp.last_timing()["hops"]])
             ks = final_bu_kernels(sp)
             assert ks[0].startswith(first) and ks[1].startswith("nbg::k_bu_rest_lean<1, "), ks
 

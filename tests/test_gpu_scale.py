@@ -85,8 +85,11 @@ def test_where_thresholds_rmat20(rmat20, k):
         r = sp.go(starts, steps, FOLLOW, where=X.AliasProp("follow", "weight") > k,
                   yields=[X.EdgeDst("follow")], distinct=True)
         want, scanned = g.go(starts, steps, where_gt=k, distinct=True)
-        assert np.array_equal(np.sort(r.columns[0]), want)
-        assert r.edges_scanned == scanned
+        t = sp.last_timing()
+        diag = (steps, r.edges_scanned, scanned, t["host_waits"], t["spec_hops"],
+                [(h["mode"], h["c"][:6]) for h in t["hops"]])
+        assert np.array_equal(np.sort(r.columns[0]), want), diag
+        assert r.edges_scanned == scanned, diag
 
 
 OPS = {">": lambda c, k: c > k, ">=": lambda c, k: c >= k, "<": lambda c, k: c < k, "<=": lambda c, k: c <= k,
