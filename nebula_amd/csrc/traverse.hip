@@ -715,7 +715,7 @@ __device__ inline void block_add_sums(const unsigned long long* v, int k, unsign
 __global__ __launch_bounds__(1024) void k_reduce_partials(const unsigned long long* partials, int nblocks,
                                                           unsigned long long* out,
                                                           const unsigned long long* gate = nullptr) {
-  if (gate && *gate == 0ull) return;
+  if (gate && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull) return;
   __shared__ unsigned long long s[kSlots][16];
   unsigned long long a[kSlots];
 #pragma unroll
@@ -908,19 +908,24 @@ struct GateIn {
   int shards = 1;  // e / n are sharded block sums (block_add_sums): their shards are summed
 };
 __device__ inline bool gate_open(const GateIn& gi, unsigned long long* gate) {
-  if (gi.e == nullptr && gi.all == nullptr) return gate == nullptr || *gate != 0ull;
+  // (agent-scope loads of words other launches' atomics wrote, as in k_publish)
+  auto ld = [](const unsigned long long* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  if (gi.e == nullptr && gi.all == nullptr) return gate == nullptr || ld(gate) != 0ull;
   unsigned long long n, e;
   if (gi.all) {
     n = e = 0ull;
-    for (int r = 0; r < gi.world; r++) n += gi.all[2 * r], e += gi.all[2 * r + 1];
+    for (int r = 0; r < gi.world; r++) n += ld(gi.all + 2 * r), e += ld(gi.all + 2 * r + 1);
   } else {
     n = e = 0ull;
-    for (int s = 0; s < gi.shards; s++) n += gi.n[size_t(s) * kShardStride], e += gi.e[size_t(s) * kShardStride];
+    for (int s = 0; s < gi.shards; s++) n += ld(gi.n + size_t(s) * kShardStride), e += ld(gi.e + size_t(s) * kShardStride);
   }
-  const bool open = (gi.pg == nullptr || *gi.pg != 0ull) && n > 0ull && e >= gi.thr;
+  const bool open = (gi.pg == nullptr || ld(gi.pg) != 0ull) && n > 0ull && e >= gi.thr;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    *gate = open ? 1ull : 0ull;
-    if (gi.all) gate[2] = n, gate[3] = e;
+    __hip_atomic_store(gate, open ? 1ull : 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (gi.all) {
+      __hip_atomic_store(gate + 2, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gate + 3, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   return open;
 }
@@ -1393,7 +1398,7 @@ __global__ __launch_bounds__(1024, 4) void k_bu_rest_lean(const unsigned long lo
                                                           int steps, unsigned long long* dbg,
                                                           const unsigned long long* __restrict__ gate,
                                                           const uint4* __restrict__ rec, int atomic_sums) {
-  if (gate && *gate == 0ull) return;
+  if (gate && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull) return;
   const QArgs q = q_sgpr(q_arg);
   __shared__ unsigned long long lds[kSlots * 16];
   __shared__ unsigned long long s_found[16][64];
@@ -1584,7 +1589,7 @@ __global__ __launch_bounds__(1024) void k_bits_compact(const uint32_t* __restric
                                                        const int64_t* __restrict__ vid_of, void* out,
                                                        unsigned long long* n_out,
                                                        const unsigned long long* gate = nullptr) {
-  if (gate && *gate == 0ull) return;
+  if (gate && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0ull) return;
   // one word per thread: a 1024-thread block owns 1024 words (32 K vertices) per iteration, so
   // a 32.8 M-vertex bitmap is ~1000 blocks (4096-word tiles gave ~250: one block per CU, half
   // the resident waves this latency-bound gather needs); one counter atomic per tile
@@ -2238,13 +2243,16 @@ struct Counters {
 // the sequence with one system-scope release store: one system fence (an L2 write-back) instead
 // of one per word.  A single wave, so the release's wait on the wave's outstanding stores covers
 // every copy.  (One thread copying every word waited on each load in turn: ~10 us more.)
-__global__ void k_publish(const unsigned long long* __restrict__ src, int n, unsigned long long* __restrict__ dst,
+__global__ void k_publish(const unsigned long long* src, int n, unsigned long long* __restrict__ dst,
                           unsigned long long* seq_slot, unsigned long long seq, int shards) {
   // shards > 1: word i is the sum of its shards src[i + s * kShardStride] (block_add_sums).  All
   // loads of a lane (<= 4 words x kSumShards shards; n <= 256) are issued before any add: one
   // round trip (a per-word shard loop had made this launch 3.6 -> 8.0 us, r12d)
+  // (agent-scope loads: the words were added by other launches' atomics; a plain load may be
+  // served by a stale copy -- twice this round a count came back low)
+  auto ld = [&](size_t k) { return __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   if (shards <= 1) {
-    for (int i = threadIdx.x; i < n; i += 64) dst[i] = src[i];
+    for (int i = threadIdx.x; i < n; i += 64) dst[i] = ld(size_t(i));
   } else {
     unsigned long long x[4][kSumShards];
 #pragma unroll
@@ -2252,7 +2260,7 @@ __global__ void k_publish(const unsigned long long* __restrict__ src, int n, uns
 #pragma unroll
       for (int s = 0; s < kSumShards; s++) {
         const int i = int(threadIdx.x) + 64 * j;
-        x[j][s] = i < n && s < shards ? src[size_t(s) * kShardStride + size_t(i)] : 0ull;
+        x[j][s] = i < n && s < shards ? ld(size_t(s) * kShardStride + size_t(i)) : 0ull;
       }
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -2376,7 +2384,8 @@ void allsum(Ctx& c, int64_t* v, int n, unsigned long long* dscratch) {
 // device counters summed over ranks into dst (stream-ordered: a gate kernel reads the sums)
 // srcs: up to 8 counter indices of K.d; dst: n consecutive words
 __global__ void k_pick_counters(const unsigned long long* K, uint64_t idx, int n, unsigned long long* dst) {
-  if (threadIdx.x < unsigned(n)) dst[threadIdx.x] = K[(idx >> (8 * threadIdx.x)) & 0xffu];
+  if (threadIdx.x < unsigned(n))
+    dst[threadIdx.x] = __hip_atomic_load(K + ((idx >> (8 * threadIdx.x)) & 0xffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 void dev_allsum(Ctx& c, const unsigned long long* K, std::initializer_list<int> idx, unsigned long long* dst) {
   uint64_t packed = 0;
