@@ -2251,7 +2251,17 @@ __global__ void k_publish(const unsigned long long* src, int n, unsigned long lo
   // served by a stale copy -- twice this round a count came back low)
   auto ld = [&](size_t k) { return __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   if (shards <= 1) {
-    for (int i = threadIdx.x; i < n; i += 64) dst[i] = ld(size_t(i));
+    unsigned long long x[4];  // every load issued before the stores (n <= 256: 4 words a lane)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int i = int(threadIdx.x) + 64 * j;
+      x[j] = i < n ? ld(size_t(i)) : 0ull;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int i = int(threadIdx.x) + 64 * j;
+      if (i < n) dst[i] = x[j];
+    }
   } else {
     unsigned long long x[4][kSumShards];
 #pragma unroll
